@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""Headline benchmark: patient-trajectories/s of the INSITE hot path on MI355X.
+
+One "step" = one pass of the hot path over one synthetic batch (BASELINE.json configs[1], C2):
+    discovery  — fused savgol(5,3) + 4th-order FD + poly2 library + per-arm Gram   (gram kernel)
+               — [N>1: one RCCL all_reduce(SUM) of the 2 x (49 + 7) Gram/moment doubles]
+               — STLSQ(threshold 0.1, alpha 0.5) + unbias                          (stlsq kernel)
+    rollout    — RK4 counterfactual rollout of every patient over T steps          (rollout kernel)
+on N_per_gpu = 100,000 patients x T = 200 steps, fp64, inputs resident in HBM (generated on
+device before timing).  Weak scaling: every rank holds its own 100k-patient shard.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1: torchrun --nproc-per-node N bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(ROOT, "ode-discovery-for-longitudinal-heterogeneous-treatment-effects-inference_amd")
+sys.path.insert(0, PKG_DIR)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "patient-trajectories/sec (N×T RK4 steps) at 1/2/4/8 GPUs; RMSE vs CPU ref"
+HBM_PEAK_GBPS = 8000.0     # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--patients", type=int, default=100_000, help="patients per GPU (C2: 100k)")
+    ap.add_argument("--T", type=int, default=200)
+    ap.add_argument("--method", default="rk4", choices=["rk4", "euler5"])
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
+    ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
+                    help="per-launch HBM bytes from the rocprofv3 PMC passes (profiles/), if present")
+    return ap.parse_args()
+
+
+def rollout_bytes(N, T, U=2, w=8):
+    """Algorithmic HBM bytes of one rollout launch:
+    N*T*(S*w + 1) [state out + int8 arm in] + N*(S*w + U*w) [y0 + statics in]."""
+    return N * T * (w + 1) + N * (w + U * w)
+
+
+def gram_bytes(N, L, U=2, w=8):
+    """Algorithmic HBM bytes of one discovery (Gram) launch: N*L*w rows + N*(U*w + 1 + 4)."""
+    return N * L * w + N * (U * w + 1 + 4)
+
+
+def cpu_baseline(n_sample, T, method, seed):
+    """The oracle (numpy restatement) on a bounded sample of the same workload, 1 thread."""
+    sys.path.insert(0, ROOT)
+    from oracle import insite_ref as R
+    try:
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(limits=1)
+    except Exception:  # pragma: no cover
+        limiter = None
+    rng = np.random.default_rng(seed)
+    p = R.draw_params(n_sample, "EQ_4_C", rng)
+    sim = R.simulate_factual(p, T, rng, "EQ_4_C", 2.0)
+    x = sim["cancer_volume"]
+    u = np.stack([sim["observed_static_c_0"], sim["observed_static_c_1"]], axis=1)
+    arm = sim["treatment_application"][:, 0].astype(np.int64)
+    flip = rng.integers(0, T, size=(n_sample, 1))
+    arms = np.where(np.arange(T)[None, :] >= flip, 1 - arm[:, None], arm[:, None])
+    exps = R.poly_library(3, 2, True)
+    dt = R.MAX_TIME_HORIZON / T
+    t0 = time.perf_counter()
+    G, b = R.gram_moments_vectorized(x, u, arm, T - 2, dt, exps)
+    coef = np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)])
+    R.rollout(x[:, 0], u, arms, coef, exps, dt, method=method)
+    el = time.perf_counter() - t0
+    if limiter is not None:
+        limiter.unregister()
+    return {"value": n_sample / el, "unit": "patient-trajectories/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/insite_ref.py numpy fp64 (vectorised over patients, 1 BLAS thread): "
+                      f"{n_sample} EQ_4_C patients x {T} steps, discovery + STLSQ + {method} rollout, "
+                      f"{el:.2f} s; host cpus={os.cpu_count()}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from insite_amd import ops, cohort
+
+    N, T = args.patients, args.T
+    coh = cohort.synthetic_pkpd(N, T, seed=args.seed * 1000 + rank, device=dev, equation="EQ_4_C")
+    arm_cf = cohort.counterfactual_arms(coh.arm, T, seed=args.seed * 1000 + rank)
+    lib = coh.lib
+    F = lib.n_terms
+    y0 = coh.x[:, 0].contiguous()
+    GB = torch.empty(2 * F * F + 2 * F, dtype=torch.float64, device=dev)   # one all-reduce buffer
+    G = GB[: 2 * F * F].view(2, F, F)
+    b = GB[2 * F * F:].view(2, F)
+    coef = torch.empty((2, F), dtype=torch.float64, device=dev)
+    mask = torch.empty((2, F), dtype=torch.int8, device=dev)
+    iters = torch.empty((2,), dtype=torch.int32, device=dev)
+    y = torch.empty((N, T), dtype=torch.float64, device=dev)
+    ws = ops.Workspace()
+    stream = torch.cuda.current_stream(dev)
+    ev = []
+
+    def step(record=False):
+        ops.gram(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 2, "smoothed4", ws, out=(G, b))
+        if world > 1:
+            dist.all_reduce(GB, op=dist.ReduceOp.SUM)
+        ops.stlsq(G, b, 0.1, 0.5, 100, True, out=(coef, mask, iters))
+        if record:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        ops.rollout(y0, coh.u, arm_cf, coef, lib, coh.dt, method=args.method, T=T, out=y)
+        if record:
+            e1.record(stream)
+            ev.append((e0, e1))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(record=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ms_step = el / args.steps * 1e3
+    roll_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ev]))
+
+    # sanity on the measured result: discovered support is the EQ_4_C one, no NaN
+    sup = mask.cpu().numpy()
+    ok = bool(torch.isfinite(y).all().item())
+
+    out = None
+    if rank == 0:
+        rb = rollout_bytes(N, T)
+        achieved = rb / (roll_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                with open(args.traffic_json) as f:
+                    tj = json.load(f)
+                if tj.get("workload") == f"rollout_{args.method}_{N}x{T}":
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": METRIC,
+            "value": N * world / (ms_step * 1e-3),
+            "unit": "patient-trajectories/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: on-device EQ_4_C PK/PD cohort (reference distributions, Euler-5 truth + 0.01 noise)",
+            "config": {
+                "workload": f"C2: PK/PD {N // 1000}k patients/GPU x {T} steps fp64 - discovery (savgol+FD4+poly2 "
+                            f"library+Gram, RCCL all-reduce when N>1, STLSQ) + {args.method.upper()} counterfactual rollout",
+                "patients_per_gpu": N, "T": T, "rows_per_patient": T - 2, "library_terms": F,
+                "parallelism": f"patient-shard x{world}", "discovered_support": sup.tolist(), "finite": ok,
+            },
+            "roofline": {
+                "kernel": f"rollout_kernel ({args.method})",
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": rb,
+                "avg_launch_ms": roll_ms,
+            },
+        }
+    # north-star probe: 1M x 500 RK4 rollout alone (the >= 40 % roofline target), rank 0, N = 1
+    if rank == 0 and world == 1 and not args.no_north_star:
+        del y
+        torch.cuda.empty_cache()
+        Nn, Tn = 1_000_000, 500
+        g = torch.Generator(device=dev)
+        g.manual_seed(7)
+        y0n = torch.rand(Nn, generator=g, device=dev, dtype=torch.float64) * 49 + 1
+        un = torch.rand((Nn, 2), generator=g, device=dev, dtype=torch.float64) * 0.1 + 0.45
+        flip = torch.randint(0, Tn, (Nn, 1), generator=g, device=dev)
+        armn = (torch.arange(Tn, device=dev)[None, :] >= flip).to(torch.int8).contiguous()
+        yn = torch.empty((Nn, Tn), dtype=torch.float64, device=dev)
+        for _ in range(3):
+            ops.rollout(y0n, un, armn, coef, lib, 10.0 / Tn, method="rk4", out=yn)
+        evs = []
+        for _ in range(10):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            ops.rollout(y0n, un, armn, coef, lib, 10.0 / Tn, method="rk4", out=yn)
+            e1.record(stream)
+            evs.append((e0, e1))
+        torch.cuda.synchronize(dev)
+        ms = float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))
+        bn = rollout_bytes(Nn, Tn)
+        out["north_star_rollout"] = {"patients": Nn, "T": Tn, "method": "rk4", "avg_launch_ms": ms,
+                                     "algorithmic_bytes": bn, "achieved_GBps": bn / (ms * 1e-3) / 1e9,
+                                     "frac_of_8TBps": bn / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                                     "patient_trajectories_per_s": Nn / (ms * 1e-3)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_sample, T, args.method, args.seed)
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,145 @@
+/*
+ * insite_hip.h — C ABI of libinsite_hip.so, the MI355X (gfx950) implementation of the
+ * INSITE ODE-discovery hot path.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo root):
+ *   - pysindy  PolynomialLibrary(degree=2, interaction_only=True)
+ *       called at libs_m/ct/src/models/sindy.py:186-188          -> insite_poly_library
+ *   - pysindy  SINDy(STLSQ(threshold, alpha, max_iter=100),
+ *                    SmoothedFiniteDifference(savgol 5/3, order=4),
+ *                    PolynomialLibrary).fit(X_a, u=U_a, t=dt, multiple_trajectories=True)
+ *       called at libs_m/ct/src/models/sindy.py:190-192           -> insite_gram_f64
+ *                                                                   + insite_stlsq_f64
+ *   - STLSQ._reduce / LSQIntialMask (per-patient initial-mask refit)
+ *       libs_m/ct/src/data/pkpd/utils.py:183-327;
+ *       pkpd_simulation.py:791-800                               -> insite_stlsq_f64 (n_sys = N)
+ *   - jit(vmap(simulate_cancer_volume))(y0, treatments, dt, statics) with the Euler-5
+ *       odeint (libs_m/ct/src/models/sindy.py:413-431; pkpd/utils.py:68-94)
+ *                                                                -> insite_rollout_f64
+ *   - predict_with_reduced_coefs (per-patient coefficients)
+ *       libs_m/ct/src/models/sindy.py:767-778                     -> insite_rollout_f64
+ *                                                                   (coef_row_stride != 0)
+ *   - masked squared-error sums of get_normalised_masked_rmse /
+ *       get_normalised_n_step_rmses (time_varying_model.py:236-313) -> insite_masked_sse_f64
+ *
+ * The reference has no FFI (it is Python/JAX); these entry points are what a ctypes /
+ * cffi binding of the two call sites above binds to (INTEGRATION.md shows the stub).
+ *
+ * Conventions
+ *   - Every array argument is a DEVICE pointer to caller-owned memory unless documented
+ *     as host; row-major; leading dimensions in elements.  The library never allocates
+ *     device memory: callers size workspaces with the *_workspace_bytes queries.
+ *   - Every compute entry point is asynchronous on the caller's HIP stream (`stream` is a
+ *     hipStream_t passed as void*; NULL = the default stream) and uses the caller's current
+ *     device.  No entry point synchronises the device.
+ *   - Return value: 0 = success, negative = error (insite_strerror).  No exceptions cross
+ *     the ABI.  Entry points are reentrant; the library holds no mutable global state.
+ *   - Polynomial libraries are over the inputs [x, u_0, .., u_{U-1}] (one state x, U static
+ *     covariates) and are described by an exponent table exps[F][1+U] (int8, HOST memory)
+ *     in pysindy column order (insite_poly_library produces it).
+ */
+#ifndef INSITE_HIP_H_
+#define INSITE_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define INSITE_ABI_VERSION 1
+
+/* status codes */
+#define INSITE_OK 0
+#define INSITE_E_INVALID_ARG (-1)
+#define INSITE_E_UNSUPPORTED (-2)
+#define INSITE_E_WORKSPACE (-3)
+#define INSITE_E_HIP (-4)
+
+/* derivative estimators (pysindy differentiation methods used at sindy.py:190-203) */
+#define INSITE_FD_SMOOTHED4 0 /* SmoothedFiniteDifference(savgol 5/3, order=4); library on smoothed x */
+#define INSITE_FD_ORDER4 1    /* FiniteDifference(order=4) */
+#define INSITE_FD_ORDER1 2    /* FiniteDifference(order=1) */
+
+/* integrators (odeint, pkpd/utils.py:68-94) */
+#define INSITE_METHOD_EULER 0 /* `substeps` forward-Euler steps per interval; 5 = reference Euler-5 */
+#define INSITE_METHOD_RK4 1   /* `substeps` classical RK4 steps per interval */
+
+/* limits of this ABI version */
+#define INSITE_MAX_TERMS 9  /* F: one Gram/moment entry per wavefront lane (F(F+1)/2 + F <= 64) */
+#define INSITE_MAX_STATICS 3
+#define INSITE_MAX_ARMS 4
+#define INSITE_MAX_STATE_DEGREE 1 /* max exponent of x in a column (Theta affine in x) */
+
+int32_t insite_abi_version(void);
+const char* insite_strerror(int32_t code);
+
+/* pysindy PolynomialLibrary column order over (1 + n_statics) inputs: bias, linear, then
+ * products by degree in itertools.combinations(_with_replacement) order.
+ * exps_out: HOST int8 [max_terms][1 + n_statics]; *n_terms receives F. */
+int32_t insite_poly_library(int32_t n_statics, int32_t degree, int32_t interaction_only,
+                            int8_t* exps_out, int32_t max_terms, int32_t* n_terms);
+
+/* Fused discovery pass (smoothing + finite differences + library + Gram), replacing the
+ * row materialisation and Theta^T Theta of SINDy.fit.  For every patient p with
+ * L = rows[p] >= 5 observation rows x[p, 0..L-1] and training arm a = arm[p]:
+ *     G_out[a] += Theta_p^T Theta_p,   b_out[a] += Theta_p^T xdot_p
+ * where Theta_p[k, j] = column j evaluated at (xs[k], u[p, :]) and xs = x (or the savgol
+ * 5/3-smoothed x for INSITE_FD_SMOOTHED4).  Patients with L < 5 contribute nothing
+ * (pysindy raises; the caller validates).  Deterministic: fixed-order reductions.
+ *   x     [n_patients, ldx] f64   (ldx >= max rows; columns >= rows[p] are never used)
+ *   u     [n_patients, n_statics] f64
+ *   arm   [n_patients] int8 in [0, n_arms)
+ *   rows  [n_patients] int32
+ *   G_out [n_arms, F, F] f64 (overwritten), b_out [n_arms, F] f64 (overwritten)       */
+size_t insite_gram_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms);
+int32_t insite_gram_f64(const double* x, int64_t ldx, const double* u, const int8_t* arm,
+                        const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
+                        const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
+                        double* G_out, double* b_out, void* workspace, size_t workspace_bytes,
+                        void* stream);
+
+/* Batched sequentially-thresholded least squares on Gram systems (one system per thread):
+ * STLSQ._reduce semantics (all-ones initial support; ridge (G_SS + alpha I) c = b_S by
+ * Cholesky; zero |c| < threshold; stop when nothing was removed in the first pass or the
+ * support is unchanged; empty support -> 0) followed by the pysindy unbias (G_SS c = b_S)
+ * on ind = |c| > 1e-14 when `unbias` != 0.
+ *   G [n_sys, F, F], b [n_sys, F]; coef_out [n_sys, F] f64; mask_out [n_sys, F] int8 (may be
+ *   NULL); iters_out [n_sys] int32 (may be NULL; -1 flags a non-positive-definite solve). */
+int32_t insite_stlsq_f64(const double* G, const double* b, int64_t n_sys, int32_t n_terms,
+                         double threshold, double alpha, int32_t max_iter, int32_t unbias,
+                         double* coef_out, int8_t* mask_out, int32_t* iters_out, void* stream);
+
+/* Batched open-loop counterfactual rollout (one patient per lane, state in registers).
+ * For k = 0..T-1:  a = arm[r, k];  advance y over one interval dt with the RHS
+ *     f_a(y) = sum_j c[a, j] * Theta_j(y, u[r, :])   over terms with |c[a, j]| > drop_below
+ * and store y_out[r, k].  coef is [n_arms, F] (coef_row_stride = 0) or per row
+ * [n_rows, n_arms, F] (coef_row_stride = n_arms * F).
+ *   y0 [n_rows] f64, u [n_rows, n_statics] f64, arm [n_rows, ld_arm] int8,
+ *   y_out [n_rows, ld_y] f64.                                                          */
+int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm, int64_t ld_arm,
+                           const double* coef, int64_t coef_row_stride, const int8_t* exps,
+                           int32_t n_terms, int64_t n_rows, int32_t T, int32_t n_statics,
+                           int32_t n_arms, double dt, int32_t method, int32_t substeps,
+                           double drop_below, double* y_out, int64_t ld_y, void* stream);
+
+/* Masked squared-error sums for the RMSE metrics (time_varying_model.py:236-313):
+ *   err[r,k]  = (pred[r, k] * scale + shift - target[r, k])^2 * active[r, k]
+ *   per_step_out[k] = sum_r err[r, k]        per_step_cnt_out[k] = sum_r active[r, k]
+ *   last_out[0] = sum_r err[r, last_r], last_out[1] = count, where last_r is the final
+ *   active entry of row r (active[r,k]=1 and active[r,k+1]=0, or k = T-1).
+ * Deterministic fixed-order reduction.  pred [n_rows, ld_pred], target/active [n_rows, T].
+ * Outputs f64 device arrays (overwritten). */
+size_t insite_masked_sse_workspace_bytes(int64_t n_rows, int32_t T);
+int32_t insite_masked_sse_f64(const double* pred, int64_t ld_pred, double scale, double shift,
+                              const double* target, const double* active, int64_t n_rows,
+                              int32_t T, double* per_step_out, double* per_step_cnt_out,
+                              double* last_out, void* workspace, size_t workspace_bytes,
+                              void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* INSITE_HIP_H_ */

@@ -1,0 +1,94 @@
+"""On-device PK/PD cohort generation (input side of the hot path).
+
+Distributions follow ``get_standard_params`` / ``simulate_factual``
+(``libs_m/ct/src/data/pkpd/pkpd_simulation.py:96-203, 205-309``): c_a ~ N(0.5, 0.05),
+x0 ~ U(1, 50), C_a = c_a (EQ_4_A/B) or c_0 + 0.05 / c_1 + 0.15 (EQ_4_C/D; EQ_4_D adds one
+N(0, 0.25) shift per arm), treatment ~ Bernoulli(sigmoid(gamma/50 (x0 - 25))), volumes are the
+Euler-5 trajectory of dy/dt = -C_a y, plus 0.01 N(0,1) noise for B/C/D.  The trajectories are
+integrated by the same HIP rollout kernel the model uses (per-patient coefficient rows carrying
+the true -C_a on the ``x0`` column), so no host round trip is needed for multi-GPU shards.
+Random numbers come from torch's device generator (the reference's JAX threefry streams are not
+reproducible without jax).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import ops
+from .library import PolyLibrary, polynomial_library
+
+MAX_VALUE = 50.0
+MAX_TIME_HORIZON = 10.0
+OBSERVATION_NOISE = 0.01
+
+
+@dataclass
+class DeviceCohort:
+    x: torch.Tensor          # [N, ldx] f64 volume series (columns 0..T-1)
+    u: torch.Tensor          # [N, 2] f64 statics (c_0, c_1)
+    arm: torch.Tensor        # [N] int8 factual (training) arm
+    rows: torch.Tensor       # [N] int32 discovery rows per patient (seq_len - 1)
+    C: torch.Tensor          # [N, 2] f64 hidden rates
+    T: int
+    dt: float
+    lib: PolyLibrary
+
+
+def _gen(seed: int, device) -> torch.Generator:
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed))
+    return g
+
+
+def synthetic_pkpd(n_patients: int, T: int, seed: int, device, equation: str = "EQ_4_C",
+                   conf_coeff: float = 2.0, noise: bool | None = None) -> DeviceCohort:
+    dev = torch.device(device)
+    g = _gen(seed, dev)
+    N = int(n_patients)
+    f64 = torch.float64
+    c = torch.randn((N, 2), generator=g, device=dev, dtype=f64) * 0.05 + 0.5
+    C = c.clone()
+    if equation in ("EQ_4_C", "EQ_4_D"):
+        C[:, 0] += 0.05
+        C[:, 1] += 0.15
+        if equation == "EQ_4_D":
+            C += torch.randn((1, 2), generator=g, device=dev, dtype=f64) * 0.25
+    elif equation not in ("EQ_4_A", "EQ_4_B"):
+        raise NotImplementedError(equation)
+    x0 = torch.rand((N,), generator=g, device=dev, dtype=f64) * (MAX_VALUE - 1.0) + 1.0
+    prob = torch.sigmoid((conf_coeff / MAX_VALUE) * (x0 - MAX_VALUE / 2.0))
+    arm = (torch.rand((N,), generator=g, device=dev, dtype=f64) < prob).to(torch.int8)
+    lib = polynomial_library(2, 2, True)
+    dt = MAX_TIME_HORIZON / T
+    ldx = T + (T & 1)
+    x = torch.empty((N, ldx), device=dev, dtype=f64)
+    x[:, 0] = x0
+    if ldx > T:
+        x[:, T:] = 0.0
+    coef = torch.zeros((N, 2, lib.n_terms), device=dev, dtype=f64)
+    coef[:, :, 1] = -C                               # 'x0' column carries -C_a
+    arms = arm[:, None].expand(N, T - 1).contiguous()
+    if T > 1:
+        ops.rollout(x0, c.contiguous(), arms, coef, lib, dt, method="euler5", drop_below=0.0, T=T - 1,
+                    out=x[:, 1:T])
+    if noise if noise is not None else equation.split("_")[-1] in ("B", "C", "D"):
+        x[:, :T] += OBSERVATION_NOISE * torch.randn((N, T), generator=g, device=dev, dtype=f64)
+    rows = torch.full((N,), T - 2, device=dev, dtype=torch.int32)   # seq_len = T-1, offset 1
+    return DeviceCohort(x=x, u=c.contiguous(), arm=arm, rows=rows, C=C, T=T, dt=dt, lib=lib)
+
+
+def counterfactual_arms(arm: torch.Tensor, T: int, seed: int) -> torch.Tensor:
+    """Per-step arm sequences: the factual arm, flipped from a random step on (C2 workload)."""
+    dev = arm.device
+    g = _gen(seed + 7919, dev)
+    N = arm.numel()
+    flip = torch.randint(0, T, (N, 1), generator=g, device=dev)
+    steps = torch.arange(T, device=dev)[None, :]
+    lda = (T + 3) // 4 * 4
+    out = torch.empty((N, lda), dtype=torch.int8, device=dev)
+    out[:, :T] = torch.where(steps >= flip, 1 - arm[:, None], arm[:, None]).to(torch.int8)
+    if lda > T:
+        out[:, T:] = 0
+    return out

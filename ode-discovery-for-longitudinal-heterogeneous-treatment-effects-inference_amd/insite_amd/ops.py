@@ -1,0 +1,194 @@
+"""Torch-tensor front end of the C ABI (``include/insite_hip.h``).
+
+Every op takes device tensors (contiguous rows; leading dimension = ``stride(0)``), launches on
+torch's current HIP stream and returns without synchronising.  There is no CPU fallback: CPU
+tensors raise ``ValueError`` and a missing library raises ``InsiteLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .library import PolyLibrary
+
+METHODS = {"euler5": (_lib.METHOD_EULER, 5), "euler": (_lib.METHOD_EULER, 1), "rk4": (_lib.METHOD_RK4, 1)}
+FD_KINDS = {"smoothed4": _lib.FD_SMOOTHED4, "order4": _lib.FD_ORDER4}
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _dev(name, t, dtype, ndim=None):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ValueError(f"{name}: expected a device tensor (the INSITE HIP path has no CPU fallback)")
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: expected {dtype}, got {t.dtype}")
+    if ndim is not None and t.dim() != ndim:
+        raise ValueError(f"{name}: expected {ndim}-d tensor, got shape {tuple(t.shape)}")
+    if t.dim() >= 1 and t.stride(-1) != 1:
+        raise ValueError(f"{name}: innermost dimension must be contiguous")
+    if t.dim() == 2 and t.size(0) > 1 and t.stride(0) < t.size(1):
+        raise ValueError(f"{name}: overlapping rows")
+    return t
+
+
+class Workspace:
+    """Grow-only device scratch buffer (the library never allocates)."""
+
+    def __init__(self):
+        self._buf = {}
+
+    def get(self, nbytes: int, device) -> torch.Tensor:
+        key = torch.device(device).index
+        b = self._buf.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            self._buf[key] = b
+        return b
+
+
+_WS = Workspace()
+
+
+def gram(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor, dt: float,
+         lib: PolyLibrary, n_arms: int = 2, fd: str = "smoothed4", workspace: Workspace | None = None,
+         out: tuple | None = None):
+    """Per-arm Gram G[A,F,F] and moments b[A,F] of the discovery regression (insite_gram_f64)."""
+    L = _lib.load()
+    _dev("x", x, torch.float64, 2)
+    N = x.size(0)
+    _dev("arm", arm, torch.int8, 1)
+    _dev("rows", rows, torch.int32, 1)
+    if lib.n_statics:
+        _dev("u", u, torch.float64, 2)
+        if u.size(0) != N or u.size(1) != lib.n_statics or u.stride(0) != lib.n_statics:
+            raise ValueError("u must be a contiguous [N, n_statics] tensor")
+    if arm.numel() != N or rows.numel() != N:
+        raise ValueError("arm/rows must have one entry per patient")
+    F = lib.n_terms
+    if out is None:
+        G = torch.empty((n_arms, F, F), dtype=torch.float64, device=x.device)
+        b = torch.empty((n_arms, F), dtype=torch.float64, device=x.device)
+    else:
+        G, b = out
+    nbytes = L.insite_gram_workspace_bytes(N, n_arms, F)
+    ws = (workspace or _WS).get(nbytes, x.device)
+    tab = lib.ctypes_table()
+    st = L.insite_gram_f64(_p(x), x.stride(0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), _p(rows), N,
+                           lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p), F, FD_KINDS[fd], float(dt),
+                           _p(G), _p(b), _p(ws), ws.numel(), _stream(x.device))
+    _lib.check("insite_gram_f64", st)
+    return G, b
+
+
+def stlsq(G: torch.Tensor, b: torch.Tensor, threshold: float, alpha: float, max_iter: int = 100,
+          unbias: bool = True, out: tuple | None = None):
+    """Batched STLSQ on Gram systems (insite_stlsq_f64).  G [S,F,F], b [S,F]."""
+    L = _lib.load()
+    _dev("G", G, torch.float64)
+    _dev("b", b, torch.float64)
+    F = G.shape[-1]
+    S = G.numel() // (F * F)
+    if b.numel() != S * F or not G.is_contiguous() or not b.is_contiguous():
+        raise ValueError("G/b must be contiguous [S,F,F] / [S,F]")
+    if out is None:
+        coef = torch.empty((S, F), dtype=torch.float64, device=G.device)
+        mask = torch.empty((S, F), dtype=torch.int8, device=G.device)
+        iters = torch.empty((S,), dtype=torch.int32, device=G.device)
+    else:
+        coef, mask, iters = out
+    st = L.insite_stlsq_f64(_p(G), _p(b), S, F, float(threshold), float(alpha), int(max_iter), int(bool(unbias)),
+                            _p(coef), _p(mask), _p(iters), _stream(G.device))
+    _lib.check("insite_stlsq_f64", st)
+    return coef, mask, iters
+
+
+def rollout(y0: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, coef: torch.Tensor, lib: PolyLibrary,
+            dt: float, method: str = "euler5", substeps: int | None = None, drop_below: float = 1e-3,
+            T: int | None = None, out: torch.Tensor | None = None):
+    """Batched open-loop rollout (insite_rollout_f64).
+
+    y0 [N] f64, u [N,U] f64, arm [N, >=T] int8 (per-step arm), coef [A,F] (global model) or
+    [N,A,F] (per-patient).  Returns y [N,T] (state after each observation interval)."""
+    L = _lib.load()
+    _dev("y0", y0, torch.float64, 1)
+    _dev("arm", arm, torch.int8, 2)
+    N = y0.numel()
+    T = arm.size(1) if T is None else int(T)
+    if arm.size(0) != N:
+        raise ValueError("arm must have one row per patient")
+    if lib.n_statics:
+        _dev("u", u, torch.float64, 2)
+        if u.size(0) != N or u.size(1) != lib.n_statics or u.stride(0) != lib.n_statics:
+            raise ValueError("u must be a contiguous [N, n_statics] tensor")
+    _dev("coef", coef, torch.float64)
+    if not coef.is_contiguous():
+        raise ValueError("coef must be contiguous")
+    F = lib.n_terms
+    if coef.dim() == 2:
+        A = coef.size(0)
+        stride = 0
+    elif coef.dim() == 3:
+        if coef.size(0) != N:
+            raise ValueError("per-patient coef must be [N, A, F]")
+        A = coef.size(1)
+        stride = A * F
+    else:
+        raise ValueError("coef must be [A,F] or [N,A,F]")
+    if coef.size(-1) != F:
+        raise ValueError("coef last dim must equal the library size")
+    m, default_sub = METHODS[method]
+    sub = int(substeps or default_sub)
+    if out is None:
+        out = torch.empty((N, T), dtype=torch.float64, device=y0.device)
+    else:
+        _dev("out", out, torch.float64, 2)
+    tab = lib.ctypes_table()
+    st = L.insite_rollout_f64(_p(y0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), arm.stride(0),
+                              _p(coef), stride, tab.ctypes.data_as(ctypes.c_void_p), F, N, T, lib.n_statics, A,
+                              float(dt), m, sub, float(drop_below), _p(out), out.stride(0), _stream(y0.device))
+    _lib.check("insite_rollout_f64", st)
+    return out
+
+
+def masked_sse(pred: torch.Tensor, target: torch.Tensor, active: torch.Tensor, scale: float = 1.0,
+               shift: float = 0.0, workspace: Workspace | None = None):
+    """Masked squared-error sums (insite_masked_sse_f64).  Returns (per_step[T], count[T], last[2])."""
+    L = _lib.load()
+    _dev("pred", pred, torch.float64, 2)
+    _dev("target", target, torch.float64, 2)
+    _dev("active", active, torch.float64, 2)
+    N, T = target.shape
+    if not target.is_contiguous() or not active.is_contiguous() or active.shape != target.shape:
+        raise ValueError("target/active must be contiguous [N,T]")
+    if pred.size(0) != N or pred.size(1) < T:
+        raise ValueError("pred must be [N, >=T]")
+    per = torch.empty(T, dtype=torch.float64, device=pred.device)
+    cnt = torch.empty(T, dtype=torch.float64, device=pred.device)
+    last = torch.empty(2, dtype=torch.float64, device=pred.device)
+    nbytes = L.insite_masked_sse_workspace_bytes(N, T)
+    ws = (workspace or _WS).get(nbytes, pred.device)
+    st = L.insite_masked_sse_f64(_p(pred), pred.stride(0), float(scale), float(shift), _p(target), _p(active), N, T,
+                                 _p(per), _p(cnt), _p(last), _p(ws), ws.numel(), _stream(pred.device))
+    _lib.check("insite_masked_sse_f64", st)
+    return per, cnt, last
+
+
+def poly_library_native(n_statics: int, degree: int, interaction_only: bool) -> np.ndarray:
+    """The library exponent table as produced by the C ABI (host function, no GPU needed)."""
+    L = _lib.load()
+    n_in = 1 + n_statics
+    buf = np.zeros((256, n_in), dtype=np.int8)
+    n = ctypes.c_int32(0)
+    st = L.insite_poly_library(n_statics, degree, int(interaction_only), buf.ctypes.data_as(ctypes.c_void_p), 256,
+                               ctypes.byref(n))
+    _lib.check("insite_poly_library", st)
+    return buf[: n.value].copy()

@@ -1,0 +1,243 @@
+"""GPU parity: every kernel of libinsite_hip.so through the C ABI vs the CPU oracle.
+
+Tolerances (north star, BASELINE.json): identical discovered sparsity pattern, discovered
+coefficient L-inf < 1e-8, fp64 trajectory RMSE <= 1e-6.  Gram/moment sums are compared at
+relative 1e-10 (fp64 sums of up to ~1e7 terms in a different association order).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import insite_ref as R
+
+pytestmark = pytest.mark.gpu
+
+RMSE_TOL = 1e-6
+COEF_TOL = 1e-8
+
+
+def _t(a, dev, dtype=None):
+    return torch.tensor(np.ascontiguousarray(a), device=dev, dtype=dtype)
+
+
+def _lib(n_statics=2, degree=2, interaction_only=True):
+    from insite_amd.library import polynomial_library
+    return polynomial_library(n_statics, degree, interaction_only)
+
+
+def _cohort(eq="EQ_4_C", n=300, T=60, seed=0):
+    coll = R.make_collection(eq, {"train": n, "val": 4, "test": 4}, seq_length=T, seed=seed, with_tests=False)
+    tr = coll["train"]
+    return R.de_format(tr.data, tr.scaling_params)
+
+
+# ------------------------------------------------------------------------------------------ gram
+@pytest.mark.parametrize("eq,n,T", [("EQ_4_A", 300, 60), ("EQ_4_C", 257, 60), ("EQ_4_D", 1000, 200)])
+def test_gram_matches_oracle(dev, eq, n, T):
+    from insite_amd import ops
+    x, u, arm, rows = _cohort(eq, n, T)
+    lib = _lib()
+    dt = R.MAX_TIME_HORIZON / T
+    G_ref, b_ref = R.gram_moments(x, u, arm, rows, dt, lib.exps.astype(np.int64))
+    G, b = ops.gram(_t(x, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), dt, lib)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(G.cpu().numpy(), G_ref, rtol=1e-10, atol=1e-9)
+    np.testing.assert_allclose(b.cpu().numpy(), b_ref, rtol=1e-10, atol=1e-9)
+
+
+def test_gram_ragged_rows_odd_ld_and_order4(dev):
+    """Ragged trajectory lengths (incl. < 5 rows -> skipped), odd leading dim (8-byte staging
+    path), 4 arms, 1 static, unsmoothed 4th-order FD."""
+    from insite_amd import ops
+    rng = np.random.default_rng(3)
+    N, ld = 517, 71
+    x = rng.uniform(1, 50, size=(N, ld))
+    u = rng.normal(0.5, 0.05, size=(N, 1))
+    arm = rng.integers(0, 4, size=N)
+    rows = rng.integers(0, ld + 1, size=N)
+    rows[:5] = [0, 4, 5, 6, ld]
+    lib = _lib(1, 2, True)
+    exps = lib.exps.astype(np.int64)
+    for fd, smooth in (("order4", False), ("smoothed4", True)):
+        G_ref, b_ref = R.gram_moments(x, u, arm, rows, 0.1, exps, n_arms=4, fd=fd)
+        G, b = ops.gram(_t(x, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), 0.1, lib,
+                        n_arms=4, fd=fd)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(G.cpu().numpy(), G_ref, rtol=1e-10, atol=1e-8)
+        np.testing.assert_allclose(b.cpu().numpy(), b_ref, rtol=1e-10, atol=1e-8)
+
+
+def test_gram_deterministic(dev):
+    from insite_amd import ops
+    x, u, arm, rows = _cohort("EQ_4_B", 2000, 60)
+    lib = _lib()
+    args = (_t(x, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), 1 / 6, lib)
+    G1, b1 = ops.gram(*args)
+    G2, b2 = ops.gram(*args)
+    torch.cuda.synchronize()
+    assert torch.equal(G1, G2) and torch.equal(b1, b2)
+
+
+# ----------------------------------------------------------------------------------------- stlsq
+@pytest.mark.parametrize("eq", ["EQ_4_A", "EQ_4_B", "EQ_4_C", "EQ_4_D"])
+def test_discovery_matches_oracle(dev, eq):
+    """Full discovery (gram + STLSQ on the GPU) vs the pysindy-semantics oracle on Theta:
+    identical support, coefficient L-inf < 1e-8."""
+    from insite_amd import ops
+    x, u, arm, rows = _cohort(eq, 500, 60, seed=1)
+    lib = _lib()
+    dt = 1.0 / 6.0
+    G, b = ops.gram(_t(x, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), dt, lib)
+    coef, mask, iters = ops.stlsq(G, b, 0.1, 0.5, 100)
+    torch.cuda.synchronize()
+    X, U = R.de_lists(x, u, arm, rows)
+    for a in range(2):
+        c_ref, ind_ref, _, _ = R.sindy_fit(X[a], U[a], dt, 0.1, 0.5)
+        assert np.array_equal(mask.cpu().numpy()[a] != 0, ind_ref), (a, mask, ind_ref)
+        assert np.max(np.abs(coef.cpu().numpy()[a] - c_ref)) < COEF_TOL
+    assert (iters.cpu().numpy() > 0).all()
+
+
+def test_stlsq_batched_matches_oracle(dev):
+    """Many random well-posed systems (per-patient STLSQ shape), F = 7 and F = 4."""
+    from insite_amd import ops
+    rng = np.random.default_rng(11)
+    for F in (7, 4):
+        S = 300
+        Gs, bs = [], []
+        for _ in range(S):
+            Th = rng.normal(size=(60, F))
+            w = rng.normal(size=F) * (rng.random(F) < 0.5)
+            y = Th @ w + 0.01 * rng.normal(size=60)
+            Gs.append(Th.T @ Th)
+            bs.append(Th.T @ y)
+        G, b = np.stack(Gs), np.stack(bs)
+        coef, mask, iters = ops.stlsq(_t(G, dev), _t(b, dev), 0.2, 0.5, 100)
+        torch.cuda.synchronize()
+        for s in range(S):
+            c_ref, ind_ref, it_ref = R.stlsq_gram(G[s], b[s], 0.2, 0.5, 100)
+            assert np.array_equal(mask.cpu().numpy()[s] != 0, ind_ref)
+            np.testing.assert_allclose(coef.cpu().numpy()[s], c_ref, rtol=1e-9, atol=1e-12)
+            assert iters.cpu().numpy()[s] == it_ref
+
+
+def test_stlsq_empty_support(dev):
+    from insite_amd import ops
+    G = np.eye(3)[None] * 10.0
+    b = np.full((1, 3), 1e-3)
+    coef, mask, iters = ops.stlsq(_t(G, dev), _t(b, dev), 1.0, 0.0, 10)
+    torch.cuda.synchronize()
+    assert np.all(coef.cpu().numpy() == 0) and np.all(mask.cpu().numpy() == 0)
+
+
+# --------------------------------------------------------------------------------------- rollout
+def _random_rollout_case(rng, N, T, A=2, U=2, lda=None, per_patient=False):
+    lda = lda or T
+    lib = _lib(U, 2, True)
+    F = lib.n_terms
+    y0 = rng.uniform(1, 50, size=N)
+    u = rng.normal(0.5, 0.05, size=(N, U))
+    arm = rng.integers(0, A, size=(N, lda)).astype(np.int8)
+    base = np.zeros((A, F))
+    base[:, 1] = -0.1 * rng.random(A)                     # x0
+    base[:, F - 2] = -1.0 - 0.1 * rng.random(A)           # x0*u_last
+    base[:, 0] = 0.05 * rng.random(A)                     # bias
+    base[0, 2] = 5e-4                                     # below drop_below (1e-3): dropped
+    if per_patient:
+        coef = base[None] * (1.0 + 0.1 * rng.normal(size=(N, A, F)))
+    else:
+        coef = base
+    return lib, y0, u, arm, coef
+
+
+@pytest.mark.parametrize("method", ["euler5", "rk4", "euler"])
+@pytest.mark.parametrize("N,T,lda,per", [(1000, 60, 60, False), (777, 59, 59, False), (129, 201, 204, True),
+                                         (64, 1, 4, False), (65, 33, 35, True)])
+def test_rollout_matches_oracle(dev, method, N, T, lda, per):
+    from insite_amd import ops
+    rng = np.random.default_rng(N + T)
+    lib, y0, u, arm, coef = _random_rollout_case(rng, N, T, lda=lda, per_patient=per)
+    dt = R.MAX_TIME_HORIZON / max(T, 1)
+    y = ops.rollout(_t(y0, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(coef, dev), lib, dt, method=method, T=T)
+    torch.cuda.synchronize()
+    sub = 3 if method == "euler" else None
+    if method == "euler":
+        y = ops.rollout(_t(y0, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(coef, dev), lib, dt, method="euler",
+                        substeps=3, T=T)
+        torch.cuda.synchronize()
+    y_ref = R.rollout(y0, u, arm[:, :T], coef, lib.exps.astype(np.int64), dt, method=method, substeps=sub)
+    yg = y.cpu().numpy()
+    rmse = np.sqrt(np.mean((yg - y_ref) ** 2))
+    assert rmse <= RMSE_TOL
+    np.testing.assert_allclose(yg, y_ref, rtol=1e-11, atol=1e-12)
+
+
+def test_rollout_known_answer_y_equals_t(dev):
+    """Reference in-module test (pkpd/utils.py:757-778): dy/dt = 1, y0 = 0 on the 60-point grid
+    gives y(t) = t with MSE < 1e-16 (Euler-5 and RK4)."""
+    from insite_amd import ops
+    lib = _lib()
+    T = R.MAX_SEQUENCE_LENGTH
+    dt = R.STANDARD_DT
+    coef = np.zeros((2, lib.n_terms))
+    coef[:, 0] = 1.0
+    N = 3
+    for method in ("euler5", "rk4"):
+        y = ops.rollout(_t(np.zeros(N), dev), _t(np.full((N, 2), 0.5), dev), _t(np.zeros((N, T), np.int8), dev),
+                        _t(coef, dev), lib, dt, method=method)
+        torch.cuda.synchronize()
+        t = np.arange(1, T + 1) * dt
+        assert np.mean((y.cpu().numpy() - t[None]) ** 2) < 1e-16
+
+
+def test_rollout_deterministic_and_large_property(dev):
+    """Size-independent properties at a large size: bitwise repeatability, exact agreement of a
+    sampled row subset with the oracle, and the closed form of the linear ODE under RK4."""
+    from insite_amd import ops
+    rng = np.random.default_rng(5)
+    N, T = 200_003, 500
+    lib = _lib()
+    F = lib.n_terms
+    coef = np.zeros((2, F))
+    coef[0, 4] = -1.0   # x0*u0
+    coef[1, 5] = -1.0   # x0*u1
+    y0 = torch.rand(N, device=dev, dtype=torch.float64) * 49 + 1
+    u = torch.rand(N, 2, device=dev, dtype=torch.float64) * 0.2 + 0.4
+    flip = torch.randint(0, T, (N, 1), device=dev)
+    arm = (torch.arange(T, device=dev)[None, :] >= flip).to(torch.int8)
+    c = _t(coef, dev)
+    dt = R.MAX_TIME_HORIZON / T
+    y1 = ops.rollout(y0, u, arm, c, lib, dt, method="rk4")
+    y2 = ops.rollout(y0, u, arm, c, lib, dt, method="rk4")
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    idx = np.sort(rng.choice(N, 2000, replace=False))
+    y_ref = R.rollout(y0.cpu().numpy()[idx], u.cpu().numpy()[idx], arm.cpu().numpy()[idx], coef,
+                      lib.exps.astype(np.int64), dt, method="rk4")
+    np.testing.assert_allclose(y1.cpu().numpy()[idx], y_ref, rtol=1e-11, atol=1e-12)
+    # closed form: each RK4 interval multiplies y by the degree-4 Taylor polynomial of exp(-k dt)
+    a0 = arm[:, 0] == 0
+    k = torch.where(a0, u[:, 0], u[:, 1])
+    z = -k * dt
+    g = 1 + z + z ** 2 / 2 + z ** 3 / 6 + z ** 4 / 24
+    first = y0 * g
+    assert torch.allclose(y1[:, 0], first, rtol=1e-13)
+
+
+# --------------------------------------------------------------------------------------- metrics
+def test_masked_sse_matches_numpy(dev):
+    from insite_amd import ops
+    rng = np.random.default_rng(9)
+    N, T = 1234, 59
+    pred = rng.normal(size=(N, T + 3))
+    target = rng.normal(size=(N, T))
+    sl = rng.integers(1, T + 1, size=N)
+    active = (np.arange(T)[None, :] < sl[:, None]).astype(np.float64)
+    per, cnt, last = ops.masked_sse(_t(pred, dev), _t(target, dev), _t(active, dev), scale=2.0, shift=0.5)
+    torch.cuda.synchronize()
+    e = ((pred[:, :T] * 2.0 + 0.5 - target) ** 2) * active
+    np.testing.assert_allclose(per.cpu().numpy(), e.sum(0), rtol=1e-12)
+    np.testing.assert_allclose(cnt.cpu().numpy(), active.sum(0), rtol=0)
+    lw = active - np.concatenate([active[:, 1:], np.zeros((N, 1))], axis=1)
+    np.testing.assert_allclose(last.cpu().numpy(), [(((pred[:, :T] * 2 + 0.5 - target) ** 2) * lw).sum(), lw.sum()],
+                               rtol=1e-12)
