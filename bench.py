@@ -124,10 +124,13 @@ def main():
     ev = []
 
     def step(record=False):
-        ops.gram(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 2, "smoothed4", ws, out=(G, b))
-        if world > 1:
+        if world == 1:   # Gram kernel + fused reduction/STLSQ (2 launches)
+            ops.sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, 100, True, 2, "smoothed4", ws,
+                          out=(coef, mask, iters, G, b))
+        else:            # per-rank Gram, one RCCL all-reduce of G|b, replicated STLSQ
+            ops.gram(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 2, "smoothed4", ws, out=(G, b))
             dist.all_reduce(GB, op=dist.ReduceOp.SUM)
-        ops.stlsq(G, b, 0.1, 0.5, 100, True, out=(coef, mask, iters))
+            ops.stlsq(G, b, 0.1, 0.5, 100, True, out=(coef, mask, iters))
         if record:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)

@@ -66,6 +66,12 @@ extern "C" {
 #define INSITE_METHOD_EULER 0 /* `substeps` forward-Euler steps per interval; 5 = reference Euler-5 */
 #define INSITE_METHOD_RK4 1   /* `substeps` classical RK4 steps per interval */
 
+/* storage layouts of per-step matrices (arm, y): element (patient r, step k) at
+ *   PATIENT_MAJOR: a[r * ld + k]   (the reference's [N, T] arrays; ld >= T)
+ *   TIME_MAJOR:    a[k * ld + r]   (ld >= n_rows; every step of a wavefront is one contiguous run) */
+#define INSITE_LAYOUT_PATIENT_MAJOR 0
+#define INSITE_LAYOUT_TIME_MAJOR 1
+
 /* limits of this ABI version */
 #define INSITE_MAX_TERMS 9  /* F: one Gram/moment entry per wavefront lane (F(F+1)/2 + F <= 64) */
 #define INSITE_MAX_STATICS 3
@@ -100,6 +106,18 @@ int32_t insite_gram_f64(const double* x, int64_t ldx, const double* u, const int
                         double* G_out, double* b_out, void* workspace, size_t workspace_bytes,
                         void* stream);
 
+/* SINDy.fit replacement (reference sindy.py:190-192): insite_gram_f64 followed, in the same
+ * finalisation launch, by one STLSQ fit per arm (insite_stlsq_f64 semantics).
+ *   coef_out [n_arms, F] f64, mask_out [n_arms, F] int8 (may be NULL),
+ *   iters_out [n_arms] int32 (may be NULL; -1 flags a non-positive-definite solve).
+ *   G_out / b_out receive the Gram/moment sums as in insite_gram_f64.                     */
+int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, const double* u, const int8_t* arm,
+                             const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
+                             const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
+                             double threshold, double alpha, int32_t max_iter, int32_t unbias,
+                             double* G_out, double* b_out, double* coef_out, int8_t* mask_out,
+                             int32_t* iters_out, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Batched sequentially-thresholded least squares on Gram systems (one system per thread):
  * STLSQ._reduce semantics (all-ones initial support; ridge (G_SS + alpha I) c = b_S by
  * Cholesky; zero |c| < threshold; stop when nothing was removed in the first pass or the
@@ -115,14 +133,14 @@ int32_t insite_stlsq_f64(const double* G, const double* b, int64_t n_sys, int32_
  * For k = 0..T-1:  a = arm[r, k];  advance y over one interval dt with the RHS
  *     f_a(y) = sum_j c[a, j] * Theta_j(y, u[r, :])   over terms with |c[a, j]| > drop_below
  * and store y_out[r, k].  coef is [n_arms, F] (coef_row_stride = 0) or per row
- * [n_rows, n_arms, F] (coef_row_stride = n_arms * F).
- *   y0 [n_rows] f64, u [n_rows, n_statics] f64, arm [n_rows, ld_arm] int8,
- *   y_out [n_rows, ld_y] f64.                                                          */
+ * [n_rows, n_arms, F] (coef_row_stride = n_arms * F).  `layout` (INSITE_LAYOUT_*) applies to
+ * both arm and y_out.
+ *   y0 [n_rows] f64, u [n_rows, n_statics] f64, arm int8 and y_out f64 per `layout`.       */
 int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm, int64_t ld_arm,
                            const double* coef, int64_t coef_row_stride, const int8_t* exps,
                            int32_t n_terms, int64_t n_rows, int32_t T, int32_t n_statics,
                            int32_t n_arms, double dt, int32_t method, int32_t substeps,
-                           double drop_below, double* y_out, int64_t ld_y, void* stream);
+                           double drop_below, double* y_out, int64_t ld_y, int32_t layout, void* stream);
 
 /* Masked squared-error sums for the RMSE metrics (time_varying_model.py:236-313):
  *   err[r,k]  = (pred[r, k] * scale + shift - target[r, k])^2 * active[r, k]

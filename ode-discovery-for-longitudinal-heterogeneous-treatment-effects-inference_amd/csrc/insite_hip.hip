@@ -21,9 +21,11 @@
 //
 // All reductions are fixed-order (bitwise reproducible for a fixed problem size).
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 #include <cmath>
 #include <cstdint>
+#include <atomic>
 #include <cstring>
 
 #include "insite_hip.h"
@@ -47,6 +49,16 @@ struct LibDesc {
   int8_t eu[INSITE_MAX_TERMS][INSITE_MAX_STATICS];
   int8_t ei[kMaxEntries];
   int8_t ek[kMaxEntries];  // -1 => moment entry b[ei]
+  // MFMA Gram plan: C[16 x 16] += P^T Q over patients, P[p][a*F+i] = [arm_p == a] m_i(u_p),
+  // Q[p][c] = m_{qexp[c]}(u_p) * moment_{qmom[c]}(p); entry e of arm a = C[a*F + ei[e]][qcol[e]]
+  int32_t mfma;
+  int32_t nq;
+  int32_t n_atoms;                             // distinct u-monomials of the columns
+  int8_t atom_exp[16][INSITE_MAX_STATICS];     // exponents of atom a (each <= 2)
+  int8_t col_atom[INSITE_MAX_TERMS];           // atom of column j
+  int8_t qatom[16];                            // Q column c = atom[qatom] * moment[qmom]
+  int8_t qmom[16];  // 0: row count, 1: sum xs, 2: sum xs^2, 3: sum xdot, 4: sum xdot*xs
+  int8_t qcol[kMaxEntries];
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -119,229 +131,516 @@ __device__ __forceinline__ double monomial(const LibDesc& lib, int j, const doub
 // =============================================================================================
 // Discovery: fused smoothing + FD + library + Gram
 // =============================================================================================
-template <int KT, int VEC, int NARM, bool SMOOTH>
+// Streaming weights; 1/dt folded into the finite-difference weights.
+struct GramW {
+  double sg0, sg1, sg2;  // savgol interior: sg0*x[k] + sg1*(x[k-1]+x[k+1]) + sg2*(x[k-2]+x[k+2])
+  double fd1, fd2;       // FD4 interior:   fd1*(v[k+1]-v[k-1]) + fd2*(v[k+2]-v[k-2])
+  double inv_dt;
+};
+
+#ifndef INSITE_GT
+#define INSITE_GT 16
+#endif
+#ifndef INSITE_PF
+#define INSITE_PF 1
+#endif
+constexpr int kGT = INSITE_GT;     // time tile in steps: a multiple of the register ring length (8)
+constexpr int kGStride = kGT + 1;  // LDS row stride in doubles (odd -> lane-per-row reads conflict free)
+constexpr int kGPF = INSITE_PF;    // tiles in flight (register prefetch depth, 1 or 2)
+
+__device__ __forceinline__ double sg_int(const GramW& w, double a, double b, double c, double d, double e) {
+  return w.sg0 * c + w.sg1 * (b + d) + w.sg2 * (a + e);
+}
+__device__ __forceinline__ double fd_int(const GramW& w, double a, double b, double d, double e) {
+  return w.fd1 * (d - b) + w.fd2 * (e - a);
+}
+
+__device__ __forceinline__ void add_row(double xk, double dk, double& Sx, double& Sxx, double& Sd, double& Sdx) {
+  Sx += xk;
+  Sxx = fma(xk, xk, Sxx);
+  Sd += dk;
+  Sdx = fma(dk, xk, Sdx);
+}
+
+// Whole-trajectory moments for short smoothed trajectories (5 <= LL <= 7 rows), every stencil
+// position resolved at compile time.
+template <int LL>
+__device__ void small_trajectory(const double* __restrict__ xrow, const GramW& w, double& Sx, double& Sxx,
+                                 double& Sd, double& Sdx) {
+  double xv[LL], xs[LL];
+#pragma unroll
+  for (int j = 0; j < LL; ++j) xv[j] = xrow[j];
+#pragma unroll
+  for (int k = 0; k < LL; ++k) {
+    if (k == 0) xs[k] = sg_pos0(xv[0], xv[1], xv[2], xv[3], xv[4]);
+    else if (k == 1) xs[k] = sg_pos1(xv[0], xv[1], xv[2], xv[3], xv[4]);
+    else if (k == LL - 2) xs[k] = sg_pos3(xv[LL - 5], xv[LL - 4], xv[LL - 3], xv[LL - 2], xv[LL - 1]);
+    else if (k == LL - 1) xs[k] = sg_pos4(xv[LL - 5], xv[LL - 4], xv[LL - 3], xv[LL - 2], xv[LL - 1]);
+    else xs[k] = sg_int(w, xv[k - 2], xv[k - 1], xv[k], xv[k + 1], xv[k + 2]);
+  }
+#pragma unroll
+  for (int k = 0; k < LL; ++k) {
+    double d;
+    if (k == 0) d = fd_pos0(xs[0], xs[1], xs[2], xs[3], xs[4]) * w.inv_dt;
+    else if (k == 1) d = fd_pos1(xs[0], xs[1], xs[2], xs[3], xs[4]) * w.inv_dt;
+    else if (k == LL - 2) d = fd_pos3(xs[LL - 5], xs[LL - 4], xs[LL - 3], xs[LL - 2], xs[LL - 1]) * w.inv_dt;
+    else if (k == LL - 1) d = fd_pos4(xs[LL - 5], xs[LL - 4], xs[LL - 3], xs[LL - 2], xs[LL - 1]) * w.inv_dt;
+    else d = fd_int(w, xs[k - 2], xs[k - 1], xs[k + 1], xs[k + 2]);
+    add_row(xs[k], d, Sx, Sxx, Sd, Sdx);
+  }
+}
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// Telescoped derivative moments.  With the antisymmetric interior stencil
+// d_k = fd1 (v_{k+1} - v_{k-1}) + fd2 (v_{k+2} - v_{k-2}),  for rows k = a..b:
+//   sum d_k     = [fd1 (v_{b+1} + v_b) + fd2 (v_{b+2} + v_{b+1} + v_b + v_{b-1})]  - [same at a-1 .. a-2]
+//   sum d_k v_k = [fd1 v_b v_{b+1} + fd2 (v_{b-1} v_{b+1} + v_b v_{b+2})]             - [a-side mirror]
+// so the interior body needs no per-row derivative work at all.
+__device__ __forceinline__ void tele_hi(const GramW& w, double vm1, double v0, double v1, double v2, double& sd,
+                                        double& sdx) {  // v_{b-1}, v_b, v_{b+1}, v_{b+2}
+  sd = w.fd1 * (v1 + v0) + w.fd2 * ((v2 + v1) + (v0 + vm1));
+  sdx = w.fd1 * (v0 * v1) + w.fd2 * (vm1 * v1 + v0 * v2);
+}
+__device__ __forceinline__ void tele_lo(const GramW& w, double vm2, double vm1, double v0, double v1, double& sd,
+                                        double& sdx) {  // v_{a-2}, v_{a-1}, v_a, v_{a+1}
+  sd = w.fd1 * (v0 + vm1) + w.fd2 * ((v1 + v0) + (vm1 + vm2));
+  sdx = w.fd1 * (vm1 * v0) + w.fd2 * (vm2 * v0 + vm1 * v1);
+}
+
+// Lane = patient.  Work item = (64-patient tile, time segment [s*seg, (s+1)*seg)).  Rows are
+// staged [64 x kGT] through LDS (coalesced 16-B loads; the next tile in flight while the current
+// one is consumed); each lane streams its row through 8-deep register rings (compile-time ring
+// indices: no moves).  Per body row only xs (5 flops), sum xs and sum xs^2 are updated; the
+// derivative moments of the body are telescoped to its boundary samples.  A segment starts with
+// an 8-step (4 without smoothing) warm-up.  Edge rows: 4 head rows (segment 0) and 4 tail rows
+// (the segment holding step L-1) per patient, 2 + 2 without smoothing.  Moments are additive over
+// segments; each work item adds its A(u) M A(u)^T contribution, as a 16x16x64 f64 MFMA product
+// when the library fits (lib.mfma), else one Gram entry per lane.
+template <int VEC, int NARM, bool SMOOTH, bool MFMA>
 __global__ void __launch_bounds__(kBlock)
 gram_kernel(const double* __restrict__ x, int64_t ldx, const double* __restrict__ u,
-            const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N,
-            double inv_dt, LibDesc lib, double* __restrict__ partial) {
-  constexpr int kRowStride = KT + 1;  // odd (KT even): lane-per-row reads are bank-conflict free
-  __shared__ double smem[kWavesPerBlock * kWave * kRowStride];
+            const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, int seg, int n_seg,
+            GramW w, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ ticket) {
+  __shared__ double smem[kWavesPerBlock * kWave * kGStride];
   const int lane = threadIdx.x & (kWave - 1);
-  const int wid = threadIdx.x / kWave;
-  double* xt = smem + wid * (kWave * kRowStride);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform (SGPR)
+  double* xt = smem + wid * (kWave * kGStride);
+  constexpr int kMinMain = SMOOTH ? 8 : 5;  // shorter (5..7, smoothed) rows take small_trajectory
+  constexpr int kWarm = SMOOTH ? 8 : 4;     // warm-up steps of a segment's first tile
+  constexpr int kLag = SMOOTH ? 4 : 2;      // body row kd = t - kLag
+  constexpr int LPR = kGT / VEC;            // lanes per row segment
+  constexpr int RPI = kWave / LPR;          // rows per wave instruction
+  constexpr int NLD = kWave / RPI;          // load instructions per tile
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0u;  // consumed by discovery_finalize (next launch)
 
-  double acc[NARM];
+  // G-phase accumulators
+  dbl4 cacc = {0.0, 0.0, 0.0, 0.0};  // MFMA path: C[(lane>>4) + 4j][lane & 15]
+  double acc[NARM];                   // scalar path: entry `lane`, per arm
 #pragma unroll
   for (int a = 0; a < NARM; ++a) acc[a] = 0.0;
   const int my_i = lane < lib.nE ? lib.ei[lane] : 0;
   const int my_k = lane < lib.nE ? lib.ek[lane] : 0;
   const int my_exi = lib.ex[my_i];
   const int my_exk = my_k >= 0 ? lib.ex[my_k] : 0;
+  // MFMA operand roles of this lane: P row r = a*F + i (atom of column i, arm a), Q column r
+  const int pr_r = lane & 15;
+  const int pr_a = pr_r / lib.F, pr_i = pr_r - (pr_r / lib.F) * lib.F;
+  const bool pr_ok = MFMA && pr_r < NARM * lib.F;
+  const int pr_atom = pr_ok ? lib.col_atom[pr_i] : 0;
+  const bool q_ok = MFMA && pr_r < lib.nq;
+  const int q_atom = q_ok ? lib.qatom[pr_r] : 0;
+  const int q_mom = q_ok ? lib.qmom[pr_r] : 0;
+  const int cl = (lane % LPR) * VEC;
 
   const int64_t n_tiles = (N + kWave - 1) / kWave;
-  for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid; tile < n_tiles;
-       tile += (int64_t)gridDim.x * kWavesPerBlock) {
+  const int64_t n_items = n_tiles * n_seg;
+  for (int64_t item = (int64_t)blockIdx.x * kWavesPerBlock + wid; item < n_items;
+       item += (int64_t)gridDim.x * kWavesPerBlock) {
+    const int64_t tile = item / n_seg;
+    const int sidx = (int)(item - tile * n_seg);
     const int64_t p0 = tile * kWave;
     const int64_t p = p0 + lane;
     int L = 0;
-    if (p < N) {
-      L = rows[p];
-      if (L > ldx) L = (int)ldx;
-      if (L < 5) L = 0;  // too short for the 5-point stencils: contributes nothing
+    int arm_p = -1;
+    double uu[INSITE_MAX_STATICS] = {0.0, 0.0, 0.0};
+    {  // per-patient scalars, issued together and unconditionally (clamped index)
+      const int64_t pc = p < N ? p : N - 1;
+      const int Lr = rows[pc];
+      const int ar = arm[pc];
+#pragma unroll
+      for (int t = 0; t < INSITE_MAX_STATICS; ++t) {
+        const double q = u[pc * lib.U + (t < lib.U ? t : 0)];
+        uu[t] = (p < N && t < lib.U) ? q : 0.0;
+      }
+      if (p < N) {
+        L = Lr;
+        arm_p = ar;
+        if (L > ldx) L = (int)ldx;
+        if (L < 5) L = 0;  // too short for the 5-point stencils: contributes nothing
+      }
     }
-    const int Lmin = wave_min_i(L);
-    const int Lmax = wave_max_i(L);
-    const int steps = Lmax > 0 ? Lmax + 8 : 0;  // delay line: xs lags 4, d lags 8
+    const int Lm = L >= kMinMain ? L : 0;  // length on the streaming path
+    const int Lmax = wave_max_i(Lm);
+    const int s0 = sidx * seg;               // first step owned by this segment
+    const int s1 = min(s0 + seg, Lmax);      // one past the last step processed
+    const int e = min(Lm, s0 + seg);         // per-lane end of owned steps
+    const int Lmin = wave_min_i(e);
+    const int bstart = max(2 * kLag, s0);    // first body step of the segment
+    const bool has_body = e > bstart;        // at least one body row owned
+    double Sx = 0.0, Sxx = 0.0, Sd = 0.0, Sdx = 0.0;
 
-    double r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0, r5 = 0, r6 = 0, r7 = 0, r8 = 0;  // raw x[t-8..t]
-    double s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0, s7 = 0, s8 = 0;  // xs[t-12..t-4]
-    double Sx = 0, Sxx = 0, Sd = 0, Sdx = 0;
-
-    for (int t0 = 0; t0 < steps; t0 += KT) {
-      // ---- stage x[p0..p0+63][t0..t0+KT) into LDS: coalesced VEC*8-byte row segments ----
-      if (t0 < Lmax) {
-        constexpr int LPR = KT / VEC;      // lanes per row
-        constexpr int RPI = kWave / LPR;   // rows per wave instruction
-        const int cl = (lane % LPR) * VEC;
-        const int64_t col = t0 + cl;
-        double v[kWave / RPI][VEC];
+    if (s0 < Lmax) {
+      typedef double TileRegs[NLD][VEC];
+      TileRegs vA, vB;  // two tiles in flight (register prefetch, depth 2)
+      // Loads are issued unconditionally from a clamped (always valid) address and masked after
+      // the fact: exec-masked loads would make the compiler drain vmcnt(0) at every tile.
+      auto load_tile = [&](TileRegs& v, int t0) {
+        const int col = t0 + cl;
+        const bool col_ok = col < s1;
+        const int colc = col_ok ? col : 0;
 #pragma unroll
-        for (int it = 0; it < kWave / RPI; ++it) {
-          const int r = it * RPI + lane / LPR;
-          const int64_t pr = p0 + r;
-          if (pr < N && col < Lmax) {
-            if constexpr (VEC == 2) {
-              const double2 w = *reinterpret_cast<const double2*>(x + pr * ldx + col);
-              v[it][0] = w.x;
-              v[it][1] = w.y;
-            } else {
-              v[it][0] = x[pr * ldx + col];
-            }
+        for (int it = 0; it < NLD; ++it) {
+          const int64_t pr = p0 + it * RPI + lane / LPR;
+          const bool ok = col_ok && pr < N;
+          const double* src = x + (pr < N ? pr : N - 1) * ldx + colc;
+          if constexpr (VEC == 2) {
+            const double2 q = *reinterpret_cast<const double2*>(src);
+            v[it][0] = ok ? q.x : 0.0;
+            v[it][1] = ok ? q.y : 0.0;
           } else {
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) v[it][q] = 0.0;
+            const double q = *src;
+            v[it][0] = ok ? q : 0.0;
           }
         }
-        wave_lds_sync();  // previous tile's reads done
+      };
+      auto store_tile = [&](const TileRegs& v) {
+        wave_lds_sync();  // every lane finished reading the previous tile
 #pragma unroll
-        for (int it = 0; it < kWave / RPI; ++it) {
+        for (int it = 0; it < NLD; ++it) {
           const int r = it * RPI + lane / LPR;
 #pragma unroll
-          for (int q = 0; q < VEC; ++q) xt[r * kRowStride + cl + q] = v[it][q];
+          for (int q = 0; q < VEC; ++q) xt[r * kGStride + cl + q] = v[it][q];
         }
         wave_lds_sync();
-      }
+      };
 
+      double xr[8], sr[8];  // rings: xr[i & 7] = x[tb + i];  sr[k & 7] = xs[tb + k]
 #pragma unroll
-      for (int i = 0; i < KT; ++i) {
-        const int t = t0 + i;
-        if (t < steps) {
-          double xv = (t < L) ? xt[lane * kRowStride + i] : 0.0;
-          r0 = r1; r1 = r2; r2 = r3; r3 = r4; r4 = r5; r5 = r6; r6 = r7; r7 = r8; r8 = xv;
-          // xs[k], k = t - 4
-          const int k = t - 4;
-          double xs;
+      for (int j = 0; j < 8; ++j) xr[j] = sr[j] = 0.0;
+      double loSd = 0.0, loSdx = 0.0;  // telescoped a-side terms
+      // b-side / tail samples x[e-8 .. e-1] (x[e-5 .. e-1] unsmoothed), loaded during the last tile
+      const bool tail = Lm > 0 && e == Lm && Lm - 1 >= s0;  // this segment holds step L-1
+      const bool need_end = has_body || tail;
+      constexpr int NQ = SMOOTH ? 8 : 5;
+      double qe[NQ];
+      bool tail_issued = false;
+      auto issue_tail = [&]() {
+        if (tail_issued) return;
+        tail_issued = true;
+        const double* xe = x + (need_end ? p * ldx + (e - NQ) : 0);  // ldx >= L >= NQ: valid either way
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+          const double q = xe[j];
+          qe[j] = need_end ? q : 0.0;
+        }
+      };
+
+      // ---- first tile: steps [tb, tb+16): warm-up, a-side terms, head rows, body ----
+      const int tb = (sidx == 0) ? 0 : s0 - kWarm;
+      load_tile(vA, tb);
+      store_tile(vA);
+      if (tb + kGT < s1) load_tile(vA, tb + kGT);
+      if constexpr (kGPF == 2) {
+        if (tb + 2 * kGT < s1) load_tile(vB, tb + 2 * kGT);
+        else issue_tail();
+      } else {
+        if (tb + kGT >= s1) issue_tail();
+      }
+      {
+        const bool masked = tb + kGT > Lmin;
+#pragma unroll
+        for (int i = 0; i < kGT; ++i) {
+          xr[i & 7] = xt[lane * kGStride + i];
+          const int t = tb + i;
           if constexpr (SMOOTH) {
-            xs = sg_interior(r2, r3, r4, r5, r6);
-            if (k == 0) xs = sg_pos0(r4, r5, r6, r7, r8);
-            if (k == 1) xs = sg_pos1(r3, r4, r5, r6, r7);
-            if (k >= Lmin - 2) {
-              const double e3 = sg_pos3(r1, r2, r3, r4, r5);
-              const double e4 = sg_pos4(r0, r1, r2, r3, r4);
-              xs = (k == L - 2) ? e3 : xs;
-              xs = (k == L - 1) ? e4 : xs;
+            if (i >= 4) sr[(i - 2) & 7] = sg_int(w, xr[(i - 4) & 7], xr[(i - 3) & 7], xr[(i - 2) & 7], xr[(i - 1) & 7], xr[i & 7]);
+            if (i == 7) {
+              tele_lo(w, sr[2], sr[3], sr[4], sr[5], loSd, loSdx);  // xs[a-2..a+1], a = tb + 4
+              if (sidx == 0) {  // head rows kd = 0..3 from x[0..7], xs[2..5]
+                const double xs0 = sg_pos0(xr[0], xr[1], xr[2], xr[3], xr[4]);
+                const double xs1 = sg_pos1(xr[0], xr[1], xr[2], xr[3], xr[4]);
+                const double d0 = fd_pos0(xs0, xs1, sr[2], sr[3], sr[4]) * w.inv_dt;
+                const double d1 = fd_pos1(xs0, xs1, sr[2], sr[3], sr[4]) * w.inv_dt;
+                const double d2 = fd_int(w, xs0, xs1, sr[3], sr[4]);
+                const double d3 = fd_int(w, xs1, sr[2], sr[4], sr[5]);
+                const bool on = Lm > 0;
+                add_row(on ? xs0 : 0.0, on ? d0 : 0.0, Sx, Sxx, Sd, Sdx);
+                add_row(on ? xs1 : 0.0, on ? d1 : 0.0, Sx, Sxx, Sd, Sdx);
+                add_row(on ? sr[2] : 0.0, on ? d2 : 0.0, Sx, Sxx, Sd, Sdx);
+                add_row(on ? sr[3] : 0.0, on ? d3 : 0.0, Sx, Sxx, Sd, Sdx);
+              }
+            }
+            if (i >= 8) {  // body row kd = t - 4
+              double xk = sr[(i - 4) & 7];
+              if (masked) xk = (t < e) ? xk : 0.0;
+              Sx += xk;
+              Sxx = fma(xk, xk, Sxx);
             }
           } else {
-            xs = r4;
-          }
-          s0 = s1; s1 = s2; s2 = s3; s3 = s4; s4 = s5; s5 = s6; s6 = s7; s7 = s8; s8 = xs;
-          // d[kd], kd = t - 8 (derivative of xs)
-          const int kd = t - 8;
-          if (kd >= 0) {
-            double dv = fd_interior(s2, s3, s4, s5, s6);
-            if (kd == 0) dv = fd_pos0(s4, s5, s6, s7, s8);
-            if (kd == 1) dv = fd_pos1(s3, s4, s5, s6, s7);
-            if (kd >= Lmin - 2) {
-              const double e3 = fd_pos3(s1, s2, s3, s4, s5);
-              const double e4 = fd_pos4(s0, s1, s2, s3, s4);
-              dv = (kd == L - 2) ? e3 : dv;
-              dv = (kd == L - 1) ? e4 : dv;
+            if (i == 3) tele_lo(w, xr[0], xr[1], xr[2], xr[3], loSd, loSdx);  // x[a-2..a+1], a = tb + 2
+            if (i == 4 && sidx == 0) {  // head rows kd = 0, 1 from x[0..4]
+              const double d0 = fd_pos0(xr[0], xr[1], xr[2], xr[3], xr[4]) * w.inv_dt;
+              const double d1 = fd_pos1(xr[0], xr[1], xr[2], xr[3], xr[4]) * w.inv_dt;
+              const bool on = Lm > 0;
+              add_row(on ? xr[0] : 0.0, on ? d0 : 0.0, Sx, Sxx, Sd, Sdx);
+              add_row(on ? xr[1] : 0.0, on ? d1 : 0.0, Sx, Sxx, Sd, Sdx);
             }
-            dv *= inv_dt;
-            double xk = s4;
-            if (kd >= Lmin) {
-              const bool in = kd < L;
-              xk = in ? xk : 0.0;
-              dv = in ? dv : 0.0;
+            if (i >= 4) {  // body row kd = t - 2
+              double xk = xr[(i - 2) & 7];
+              if (masked) xk = (t < e) ? xk : 0.0;
+              Sx += xk;
+              Sxx = fma(xk, xk, Sxx);
+            }
+          }
+        }
+      }
+      // ---- remaining tiles of the segment (buffers alternate A, B; two tiles in flight) ----
+      auto consume = [&](int t0) {
+        if (t0 + kGT <= Lmin) {
+#pragma unroll
+          for (int i = 0; i < kGT; ++i) {
+            xr[i & 7] = xt[lane * kGStride + i];
+            double xk;
+            if constexpr (SMOOTH) {
+              sr[(i - 2) & 7] = sg_int(w, xr[(i - 4) & 7], xr[(i - 3) & 7], xr[(i - 2) & 7], xr[(i - 1) & 7], xr[i & 7]);
+              xk = sr[(i - 4) & 7];
+            } else {
+              xk = xr[(i - 2) & 7];
             }
             Sx += xk;
             Sxx = fma(xk, xk, Sxx);
-            Sd += dv;
-            Sdx = fma(dv, xk, Sdx);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < kGT; ++i) {
+            if (t0 + i < s1) {
+              xr[i & 7] = xt[lane * kGStride + i];
+              double xk;
+              if constexpr (SMOOTH) {
+                sr[(i - 2) & 7] = sg_int(w, xr[(i - 4) & 7], xr[(i - 3) & 7], xr[(i - 2) & 7], xr[(i - 1) & 7], xr[i & 7]);
+                xk = sr[(i - 4) & 7];
+              } else {
+                xk = xr[(i - 2) & 7];
+              }
+              xk = (t0 + i < e) ? xk : 0.0;
+              Sx += xk;
+              Sxx = fma(xk, xk, Sxx);
+            }
+          }
+        }
+      };
+      if constexpr (kGPF == 2) {
+        for (int t0 = tb + kGT; t0 < s1;) {
+          store_tile(vA);
+          if (t0 + 2 * kGT < s1) load_tile(vA, t0 + 2 * kGT);
+          else issue_tail();
+          consume(t0);
+          t0 += kGT;
+          if (t0 >= s1) break;
+          store_tile(vB);
+          if (t0 + 2 * kGT < s1) load_tile(vB, t0 + 2 * kGT);
+          else issue_tail();
+          consume(t0);
+          t0 += kGT;
+        }
+      } else {
+        for (int t0 = tb + kGT; t0 < s1; t0 += kGT) {
+          store_tile(vA);
+          if (t0 + kGT < s1) load_tile(vA, t0 + kGT);
+          else issue_tail();
+          consume(t0);
+        }
+      }
+      // ---- b-side telescoped terms and tail rows from the prefetched end samples ----
+      issue_tail();
+      if (need_end) {
+        if constexpr (SMOOTH) {
+          const double* q = qe;  // x[e-8 .. e-1]
+          const double a0 = sg_int(w, q[0], q[1], q[2], q[3], q[4]);  // xs[e-6]
+          const double a1 = sg_int(w, q[1], q[2], q[3], q[4], q[5]);  // xs[e-5]
+          const double a2 = sg_int(w, q[2], q[3], q[4], q[5], q[6]);  // xs[e-4]
+          const double a3 = sg_int(w, q[3], q[4], q[5], q[6], q[7]);  // xs[e-3]
+          if (has_body) {  // body rows a..b, b = e - 5
+            double hiSd, hiSdx;
+            tele_hi(w, a0, a1, a2, a3, hiSd, hiSdx);
+            Sd += hiSd - loSd;
+            Sdx += hiSdx - loSdx;
+          }
+          if (tail) {  // rows L-4 .. L-1
+            const double a4 = sg_pos3(q[3], q[4], q[5], q[6], q[7]);  // xs[L-2]
+            const double a5 = sg_pos4(q[3], q[4], q[5], q[6], q[7]);  // xs[L-1]
+            add_row(a2, fd_int(w, a0, a1, a3, a4), Sx, Sxx, Sd, Sdx);
+            add_row(a3, fd_int(w, a1, a2, a4, a5), Sx, Sxx, Sd, Sdx);
+            add_row(a4, fd_pos3(a1, a2, a3, a4, a5) * w.inv_dt, Sx, Sxx, Sd, Sdx);
+            add_row(a5, fd_pos4(a1, a2, a3, a4, a5) * w.inv_dt, Sx, Sxx, Sd, Sdx);
+          }
+        } else {
+          const double* q = qe;  // x[e-5 .. e-1]
+          if (has_body) {  // body rows a..b, b = e - 3: x[b-1..b+2] = x[e-4 .. e-1]
+            double hiSd, hiSdx;
+            tele_hi(w, q[1], q[2], q[3], q[4], hiSd, hiSdx);
+            Sd += hiSd - loSd;
+            Sdx += hiSdx - loSdx;
+          }
+          if (tail) {
+            add_row(q[3], fd_pos3(q[0], q[1], q[2], q[3], q[4]) * w.inv_dt, Sx, Sxx, Sd, Sdx);
+            add_row(q[4], fd_pos4(q[0], q[1], q[2], q[3], q[4]) * w.inv_dt, Sx, Sxx, Sd, Sdx);
           }
         }
       }
     }
-
-    // ---- per-patient Gram block A(u) M A(u)^T, one (entry) per lane, patients via LDS ----
-    double uu[INSITE_MAX_STATICS] = {0.0, 0.0, 0.0};
-    if (L > 0)
-      for (int i = 0; i < lib.U; ++i) uu[i] = u[p * lib.U + i];
-    wave_lds_sync();
-    double* ps = xt;  // reuse the x tile: 64 x kPsStride doubles
-    for (int j = 0; j < lib.F; ++j) ps[lane * kPsStride + j] = monomial(lib, j, uu);
-    ps[lane * kPsStride + 9] = (double)L;  // moment x^0
-    ps[lane * kPsStride + 10] = Sx;        // moment x^1
-    ps[lane * kPsStride + 11] = Sxx;       // moment x^2
-    ps[lane * kPsStride + 12] = Sd;        // moment xdot * x^0
-    ps[lane * kPsStride + 13] = Sdx;       // moment xdot * x^1
-    ps[lane * kPsStride + 14] = (L > 0) ? (double)arm[p] : -1.0;
-    wave_lds_sync();
-    if (lane < lib.nE) {
-      const int moff = my_k >= 0 ? 9 + my_exi + my_exk : 12 + my_exi;
-      for (int q = 0; q < kWave; ++q) {
-        const double* row = ps + q * kPsStride;
-        double w = row[my_i] * row[moff];
-        if (my_k >= 0) w *= row[my_k];
-        const int a = (int)row[14];
-#pragma unroll
-        for (int aa = 0; aa < NARM; ++aa) acc[aa] += (a == aa) ? w : 0.0;
+    if constexpr (SMOOTH) {
+      if (sidx == 0 && L > 0 && L < kMinMain) {
+        const double* xrow = x + p * ldx;
+        if (L == 5) small_trajectory<5>(xrow, w, Sx, Sxx, Sd, Sdx);
+        else if (L == 6) small_trajectory<6>(xrow, w, Sx, Sxx, Sd, Sdx);
+        else small_trajectory<7>(xrow, w, Sx, Sxx, Sd, Sdx);
       }
     }
-    wave_lds_sync();
-  }
+    if (s0 >= Lmax && !(SMOOTH && sidx == 0)) continue;  // nothing owned by this work item (uniform)
+#ifdef INSITE_ABLATE_NOGPHASE
+    acc[0] += Sx + Sxx + Sd + Sdx;
+    continue;
+#endif
 
-  // ---- block reduction (fixed order) -> partial[block][NARM][64] ----
-  __syncthreads();
-  double* red = smem;
+    // ---- per-patient Gram block A(u) M A(u)^T ----
+    const double M0 = (sidx == 0) ? (double)L : 0.0;  // row count, counted once per patient
+    const int my_arm = (L > 0) ? arm_p : -1;
+    double* ps = xt;  // reuse the x tile
+    if constexpr (MFMA) {
+      // producer row per patient: atoms (u-monomials) | 5 moments | arm; consumer lanes gather
+      // their P (arm-masked atom of column i) and Q (atom * moment) operands by per-lane index.
+      constexpr int kRS = 23;  // row stride (odd); 32 patients per half fit the x tile
+      for (int h = 0; h < 2; ++h) {
+        wave_lds_sync();
+        if ((lane >> 5) == h) {
+          double* row = ps + (lane & 31) * kRS;
+          for (int a = 0; a < lib.n_atoms; ++a) {  // uniform loop; exponents <= 2
+            double m = 1.0;
+            const int e0 = lib.atom_exp[a][0], e1 = lib.atom_exp[a][1], e2 = lib.atom_exp[a][2];
+            if (e0 >= 1) m *= uu[0];
+            if (e0 >= 2) m *= uu[0];
+            if (e1 >= 1) m *= uu[1];
+            if (e1 >= 2) m *= uu[1];
+            if (e2 >= 1) m *= uu[2];
+            if (e2 >= 2) m *= uu[2];
+            row[a] = m;
+          }
+          row[16] = M0;
+          row[17] = Sx;
+          row[18] = Sxx;
+          row[19] = Sd;
+          row[20] = Sdx;
+          row[21] = (double)my_arm;
+        }
+        wave_lds_sync();
 #pragma unroll
-  for (int a = 0; a < NARM; ++a) red[(wid * NARM + a) * kWave + lane] = acc[a];
-  __syncthreads();
-  if (wid == 0) {
+        for (int st = 0; st < 8; ++st) {  // K = 4 patients per MFMA, 8 steps per half
+          const double* row = ps + (4 * st + (lane >> 4)) * kRS;
+          const double av = (pr_ok && (int)row[21] == pr_a) ? row[pr_atom] : 0.0;
+          const double bv = q_ok ? row[q_atom] * row[16 + q_mom] : 0.0;
+          cacc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, cacc, 0, 0, 0);
+        }
+      }
+      wave_lds_sync();
+    } else {
+      wave_lds_sync();
+      for (int j = 0; j < lib.F; ++j) ps[lane * kPsStride + j] = monomial(lib, j, uu);
+      ps[lane * kPsStride + 9] = M0;    // moment x^0
+      ps[lane * kPsStride + 10] = Sx;   // moment x^1
+      ps[lane * kPsStride + 11] = Sxx;  // moment x^2
+      ps[lane * kPsStride + 12] = Sd;   // moment xdot * x^0
+      ps[lane * kPsStride + 13] = Sdx;  // moment xdot * x^1
+      ps[lane * kPsStride + 14] = (double)my_arm;
+      wave_lds_sync();
+      if (lane < lib.nE) {
+        const int moff = my_k >= 0 ? 9 + my_exi + my_exk : 12 + my_exi;
+        for (int q = 0; q < kWave; ++q) {
+          const double* row = ps + q * kPsStride;
+          double wq = row[my_i] * row[moff];
+          if (my_k >= 0) wq *= row[my_k];
+          const int a = (int)row[14];
 #pragma unroll
-    for (int a = 0; a < NARM; ++a) {
-      double s = red[(0 * NARM + a) * kWave + lane];
-#pragma unroll
-      for (int w = 1; w < kWavesPerBlock; ++w) s += red[(w * NARM + a) * kWave + lane];
-      partial[((int64_t)blockIdx.x * NARM + a) * kWave + lane] = s;
+          for (int aa = 0; aa < NARM; ++aa) acc[aa] += (a == aa) ? wq : 0.0;
+        }
+      }
+      wave_lds_sync();
     }
   }
-}
 
-__global__ void __launch_bounds__(kBlock)
-gram_finalize(const double* __restrict__ partial, int nblk, int narm_pad, int n_arms, LibDesc lib,
-              double* __restrict__ G, double* __restrict__ b) {
-  __shared__ double red[kBlock];
-  const int a = blockIdx.x / lib.nE;
-  const int e = blockIdx.x % lib.nE;
-  if (a >= n_arms) return;
-  double s = 0.0;
-  for (int g = threadIdx.x; g < nblk; g += kBlock) s += partial[((int64_t)g * narm_pad + a) * kWave + e];
-  red[threadIdx.x] = s;
+  // ---- block reduction (fixed order) -> partial[block][...] ----
   __syncthreads();
-  for (int off = kBlock / 2; off > 0; off >>= 1) {
-    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+  double* red = smem;
+  if constexpr (MFMA) {
+    // canonical C[row][col], row = (lane >> 4) + 4 j, col = lane & 15
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[wid * 256 + ((lane >> 4) + 4 * j) * 16 + (lane & 15)] = cacc[j];
     __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const int i = lib.ei[e], k = lib.ek[e];
-    if (k >= 0) {
-      G[((int64_t)a * lib.F + i) * lib.F + k] = red[0];
-      G[((int64_t)a * lib.F + k) * lib.F + i] = red[0];
-    } else {
-      b[(int64_t)a * lib.F + i] = red[0];
+    for (int q = threadIdx.x; q < 256; q += kBlock) {
+      double s = red[q];
+#pragma unroll
+      for (int ww = 1; ww < kWavesPerBlock; ++ww) s += red[ww * 256 + q];
+      partial[(int64_t)blockIdx.x * 256 + q] = s;
+    }
+  } else {
+#pragma unroll
+    for (int a = 0; a < NARM; ++a) red[(wid * NARM + a) * kWave + lane] = acc[a];
+    __syncthreads();
+    if (wid == 0) {
+#pragma unroll
+      for (int a = 0; a < NARM; ++a) {
+        double s = red[(0 * NARM + a) * kWave + lane];
+#pragma unroll
+        for (int ww = 1; ww < kWavesPerBlock; ++ww) s += red[(ww * NARM + a) * kWave + lane];
+        partial[((int64_t)blockIdx.x * NARM + a) * kWave + lane] = s;
+      }
     }
   }
 }
 
 // =============================================================================================
-// STLSQ on Gram systems (pkpd/utils.py:213-327 semantics), one system per thread
+// STLSQ on Gram systems (pkpd/utils.py:213-327 semantics)
 // =============================================================================================
 // Solve (G_SS + alpha I) c_S = b_S for the support mask `m` with the inactive rows/columns
 // replaced by identity rows: the Cholesky factor stays block diagonal, so the active block
-// performs exactly the operations of the reduced solve.  Returns false if not positive definite.
+// performs exactly the operations of the reduced solve (one reciprocal per pivot).  Only the lower
+// triangle of g is read.  Returns false if the active block is not positive definite.
 template <int F>
 __device__ bool masked_cholesky_solve(const double (&g)[F][F], const double (&rhs)[F], unsigned m,
                                       double alpha, double (&c)[F]) {
-  double l[F][F];
+  double l[F][F], rd[F];
   bool ok = true;
 #pragma unroll
   for (int i = 0; i < F; ++i) {
+    const bool ai = (m >> i) & 1u;
 #pragma unroll
     for (int j = 0; j <= i; ++j) {
-      const bool act = ((m >> i) & 1u) && ((m >> j) & 1u);
+      const bool act = ai && ((m >> j) & 1u);
       double a = act ? g[i][j] : 0.0;
-      if (i == j) a = ((m >> i) & 1u) ? a + alpha : 1.0;
+      if (i == j) a = ai ? a + alpha : 1.0;
 #pragma unroll
-      for (int q = 0; q < j; ++q) a -= l[i][q] * l[j][q];
+      for (int q = 0; q < j; ++q) a = fma(-l[i][q], l[j][q], a);
       if (i == j) {
         if (!(a > 0.0)) {
           ok = false;
           a = 1e-300;
         }
-        l[i][i] = sqrt(a);
+        const double r = sqrt(a);
+        l[i][i] = r;
+        rd[i] = 1.0 / r;
       } else {
-        l[i][j] = a / l[j][j];
+        l[i][j] = a * rd[j];
       }
     }
   }
@@ -350,41 +649,31 @@ __device__ bool masked_cholesky_solve(const double (&g)[F][F], const double (&rh
   for (int i = 0; i < F; ++i) {
     double s = ((m >> i) & 1u) ? rhs[i] : 0.0;
 #pragma unroll
-    for (int q = 0; q < i; ++q) s -= l[i][q] * z[q];
-    z[i] = s / l[i][i];
+    for (int q = 0; q < i; ++q) s = fma(-l[i][q], z[q], s);
+    z[i] = s * rd[i];
   }
 #pragma unroll
   for (int i = F - 1; i >= 0; --i) {
     double s = z[i];
 #pragma unroll
-    for (int q = i + 1; q < F; ++q) s -= l[q][i] * c[q];
-    c[i] = s / l[i][i];
+    for (int q = i + 1; q < F; ++q) s = fma(-l[q][i], c[q], s);
+    c[i] = ((m >> i) & 1u) ? s * rd[i] : 0.0;
   }
-#pragma unroll
-  for (int i = 0; i < F; ++i)
-    if (!((m >> i) & 1u)) c[i] = 0.0;
   return ok;
 }
 
+// One STLSQ fit: all-ones initial support (pysindy BaseOptimizer), ridge on the active set,
+// zero |c| < thr, stop when nothing was removed or the pattern repeats, then ind = |c| > 1e-14
+// and the unbias solve.  Returns the iteration count, -1 if a solve was not positive definite.
 template <int F>
-__global__ void __launch_bounds__(kBlock)
-stlsq_kernel(const double* __restrict__ G, const double* __restrict__ b, int64_t n_sys, double thr,
-             double alpha, int max_iter, int unbias, double* __restrict__ coef,
-             int8_t* __restrict__ mask, int32_t* __restrict__ iters) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n_sys) return;
-  double g[F][F], rhs[F], c[F];
-#pragma unroll
-  for (int i = 0; i < F; ++i) {
-    rhs[i] = b[s * F + i];
-    c[i] = 0.0;
-#pragma unroll
-    for (int j = 0; j < F; ++j) g[i][j] = G[(s * F + i) * F + j];
-  }
+__device__ int stlsq_solve(const double (&g)[F][F], const double (&rhs)[F], double thr, double alpha,
+                           int max_iter, int unbias, double (&c)[F], unsigned& sup) {
   const unsigned all = (1u << F) - 1u;
   unsigned ind = all, prev = all;
   bool ok = true;
   int it = 0;
+#pragma unroll
+  for (int i = 0; i < F; ++i) c[i] = 0.0;
   for (int k = 0; k < max_iter; ++k) {
     it = k + 1;
     if (ind == 0u) {
@@ -407,17 +696,112 @@ stlsq_kernel(const double* __restrict__ G, const double* __restrict__ b, int64_t
     if (ind == all || pattern == prev) break;
     prev = pattern;
   }
-  unsigned sup = 0u;
+  sup = 0u;
 #pragma unroll
   for (int i = 0; i < F; ++i)
     if (fabs(c[i]) > 1e-14) sup |= 1u << i;
   if (unbias && sup) ok &= masked_cholesky_solve<F>(g, rhs, sup, 0.0, c);
+  return ok ? it : -1;
+}
+
+template <int F>
+__global__ void __launch_bounds__(kBlock)
+stlsq_kernel(const double* __restrict__ G, const double* __restrict__ b, int64_t n_sys, double thr,
+             double alpha, int max_iter, int unbias, double* __restrict__ coef,
+             int8_t* __restrict__ mask, int32_t* __restrict__ iters) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_sys) return;
+  double g[F][F], rhs[F], c[F];
+#pragma unroll
+  for (int i = 0; i < F; ++i) {
+    rhs[i] = b[s * F + i];
+#pragma unroll
+    for (int j = 0; j <= i; ++j) g[i][j] = G[(s * F + i) * F + j];
+  }
+  unsigned sup = 0u;
+  const int it = stlsq_solve<F>(g, rhs, thr, alpha, max_iter, unbias, c, sup);
 #pragma unroll
   for (int i = 0; i < F; ++i) {
     coef[s * F + i] = c[i];
     if (mask) mask[s * F + i] = (int8_t)((sup >> i) & 1u);
   }
-  if (iters) iters[s] = ok ? it : -1;
+  if (iters) iters[s] = it;
+}
+
+struct StlsqParams {
+  double thr, alpha;
+  int32_t max_iter, unbias, enabled;
+};
+
+
+// Fixed-order reduction of the per-block Gram partials: one block per (arm, entry) — threads
+// strided over the partial blocks, then an LDS tree — G/b written out.  With F > 0 the block
+// that arrives last (agent-scope release/acquire around a ticket, MI355X_MICROARCH.md
+// "Workgroup dispatch ... visibility") runs one STLSQ fit per arm in the same launch
+// (SINDy.fit: reference sindy.py:190-192).  The ticket is zeroed by the preceding gram launch.
+template <int F>
+__global__ void __launch_bounds__(kBlock)
+discovery_finalize(const double* __restrict__ partial, int nblk, int narm_pad, int n_arms, LibDesc lib,
+                   double* __restrict__ G, double* __restrict__ b, StlsqParams sp,
+                   double* __restrict__ coef, int8_t* __restrict__ mask, int32_t* __restrict__ iters,
+                   unsigned* __restrict__ ticket) {
+  __shared__ double red[kBlock];
+  __shared__ int last;
+  const int a = blockIdx.x / lib.nE;
+  const int e = blockIdx.x % lib.nE;
+  double s = 0.0;
+  if (lib.mfma) {
+    const int off = (a * lib.F + lib.ei[e]) * 16 + lib.qcol[e];
+    for (int g = threadIdx.x; g < nblk; g += kBlock) s += partial[(int64_t)g * 256 + off];
+  } else {
+    for (int g = threadIdx.x; g < nblk; g += kBlock) s += partial[((int64_t)g * narm_pad + a) * kWave + e];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+#pragma unroll
+  for (int off = kBlock / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int i = lib.ei[e], k = lib.ek[e];
+    if (k >= 0) {
+      G[((int64_t)a * lib.F + i) * lib.F + k] = red[0];
+      G[((int64_t)a * lib.F + k) * lib.F + i] = red[0];
+    } else {
+      b[(int64_t)a * lib.F + i] = red[0];
+    }
+  }
+  if constexpr (F > 0) {
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = (t == gridDim.x - 1u);
+      if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (!last) return;
+    const int arm_i = threadIdx.x;
+    if (arm_i < n_arms) {
+      double g[F][F], rhs[F], c[F];
+#pragma unroll
+      for (int ii = 0; ii < F; ++ii) {
+        rhs[ii] = __hip_atomic_load(&b[arm_i * F + ii], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int jj = 0; jj <= ii; ++jj)
+          g[ii][jj] = __hip_atomic_load(&G[(arm_i * F + ii) * F + jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      unsigned sup = 0u;
+      const int it = stlsq_solve<F>(g, rhs, sp.thr, sp.alpha, sp.max_iter, sp.unbias, c, sup);
+#pragma unroll
+      for (int i = 0; i < F; ++i) {
+        coef[arm_i * F + i] = c[i];
+        if (mask) mask[arm_i * F + i] = (int8_t)((sup >> i) & 1u);
+      }
+      if (iters) iters[arm_i] = it;
+    }
+  }
 }
 
 // =============================================================================================
@@ -434,30 +818,80 @@ struct RolloutArgs {
   double dt, drop;
 };
 
-template <int METHOD, int NARM, bool PERROW, int AVEC, int KT>
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+constexpr unsigned kOOB = 0x80000000u;  // buffer offset beyond every descriptor: access dropped
+
+// Per-lane arm bytes of one 32-step tile, loaded straight from the lane's own row (32 contiguous
+// bytes; AV = bytes per load instruction) through a range-checked buffer descriptor.
+template <int AV, int KT>
+struct ArmTile {
+  static constexpr int NW = KT / 4;
+  unsigned w[NW];
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+    if constexpr (AV == 16) {
+#pragma unroll
+      for (int k = 0; k < NW / 4; ++k) {
+        const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * k, 0, 0);
+        w[4 * k] = a.x; w[4 * k + 1] = a.y; w[4 * k + 2] = a.z; w[4 * k + 3] = a.w;
+      }
+    } else if constexpr (AV == 4) {
+#pragma unroll
+      for (int k = 0; k < NW; ++k) w[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * k, 0, 0);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NW; ++k) {
+        unsigned v = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v |= (unsigned)__builtin_amdgcn_raw_buffer_load_b8(rs, off + 4 * k + q, 0, 0) << (8 * q);
+        w[k] = v;
+      }
+    }
+  }
+  __device__ __forceinline__ int at(int i) const { return (int)((w[i >> 2] >> (8 * (i & 3))) & 0xffu); }
+};
+
+// Lane = patient, ODE state in registers.  Per 32-step tile: the next tile's arm bytes are
+// requested before this tile's stores (vmcnt counts loads and stores in issue order, so a load
+// issued after the stores would wait for them), 32 steps are integrated, the [64 x 32] output
+// tile is staged in LDS and written as 256-byte row segments (16 B per lane when YV = 2) through a
+// range-checked buffer descriptor (rows past N and steps past T are dropped by the hardware).
+#ifndef INSITE_RT
+#define INSITE_RT 32
+#endif
+template <int METHOD, int NARM, bool PERROW, int AV, int YV>
 __global__ void __launch_bounds__(kBlock) rollout_kernel(RolloutArgs ra, LibDesc lib) {
-  static_assert(KT == 32, "write-out mapping assumes 32-step tiles");
-  constexpr int kYStride = KT + 1;           // doubles, odd -> conflict-free lane-per-row writes
-  constexpr int kAStrideW = (KT + 4) / 4;    // arm row stride in dwords (odd)
-  __shared__ double ysm[kWavesPerBlock * kWave * kYStride];
-  __shared__ uint32_t asm_[kWavesPerBlock * kWave * kAStrideW];
+  constexpr int KT = INSITE_RT;  // steps per output tile (multiple of 16)
+  constexpr int kYS = KT + 2;  // LDS row stride in doubles: rows 16-B aligned for 16-B reads
+  __shared__ double ysm[kWavesPerBlock * kWave * kYS];
   const int lane = threadIdx.x & (kWave - 1);
-  const int wid = threadIdx.x / kWave;
-  double* yt = ysm + wid * (kWave * kYStride);
-  uint32_t* at = asm_ + wid * (kWave * kAStrideW);
-  uint8_t* at8 = reinterpret_cast<uint8_t*>(at);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform (SGPR)
+  double* yt = ysm + wid * (kWave * kYS);
 
   const int64_t p0 = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * kWave;
   if (p0 >= ra.N) return;  // whole wave idle (no block-level sync below)
   const int64_t p = p0 + lane;
   const bool active = p < ra.N;
+  const int64_t pc = active ? p : ra.N - 1;
+  const int64_t nrows = ra.N - p0 < kWave ? ra.N - p0 : kWave;
+  const __amdgpu_buffer_rsrc_t ars =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(ra.arm + p0 * ra.lda), (short)0, (int)(nrows * ra.lda), 0x00020000);
+  const __amdgpu_buffer_rsrc_t yrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(ra.y + p0 * ra.ldy), (short)0, (int)(nrows * ra.ldy * 8), 0x00020000);
+  const unsigned arow = (unsigned)(lane * ra.lda);
+
+  ArmTile<AV, KT> cur, nxt;
+  cur.load(ars, arow);
 
   // ---- prologue: f_a(y) = alpha_a + beta_a * y for this patient's statics ----
-  double uu[INSITE_MAX_STATICS] = {0.0, 0.0, 0.0};
-  if (active)
-    for (int i = 0; i < lib.U; ++i) uu[i] = ra.u[p * lib.U + i];
+  double uu[INSITE_MAX_STATICS];
+#pragma unroll
+  for (int t = 0; t < INSITE_MAX_STATICS; ++t) {
+    const double q = ra.u[pc * lib.U + (t < lib.U ? t : 0)];
+    uu[t] = (active && t < lib.U) ? q : 0.0;
+  }
   double alpha[NARM], beta[NARM];
-  const double* cbase = ra.coef + (PERROW ? (active ? p : 0) * ra.coef_stride : 0);
+  const double* cbase = ra.coef + (PERROW ? pc * ra.coef_stride : 0);
 #pragma unroll
   for (int a = 0; a < NARM; ++a) {
     alpha[a] = 0.0;
@@ -472,79 +906,229 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(RolloutArgs ra, LibDesc
       }
     }
   }
-  double y = active ? ra.y0[p] : 0.0;
+  const double y0 = ra.y0[pc];
+  double y = active ? y0 : 0.0;
   const double h = ra.dt / (double)ra.substeps;
   const double h2 = 0.5 * h;
   const double h6 = h / 6.0;
 
+  auto step = [&](int a) {
+    double al = alpha[0], be = beta[0];
+#pragma unroll
+    for (int aa = 1; aa < NARM; ++aa) {
+      al = (a == aa) ? alpha[aa] : al;
+      be = (a == aa) ? beta[aa] : be;
+    }
+    if constexpr (METHOD == INSITE_METHOD_EULER) {
+      for (int s = 0; s < ra.substeps; ++s) {
+        const double f = fma(be, y, al);
+        y = fma(f, h, y);
+      }
+    } else {
+      for (int s = 0; s < ra.substeps; ++s) {
+        const double k1 = fma(be, y, al);
+        const double k2 = fma(be, fma(h2, k1, y), al);
+        const double k3 = fma(be, fma(h2, k2, y), al);
+        const double k4 = fma(be, fma(h, k3, y), al);
+        y = fma(h6, (k1 + 2.0 * k2) + (2.0 * k3 + k4), y);
+      }
+    }
+  };
+
   for (int t0 = 0; t0 < ra.T; t0 += KT) {
-    // ---- stage arm[p0..p0+63][t0..t0+KT) (int8) into LDS ----
-    {
-      constexpr int LPR = KT / AVEC;
+#ifndef INSITE_ABLATE_NOARM
+    if (t0 + KT < ra.T) nxt.load(ars, arow + (unsigned)(t0 + KT));
+#endif
+    if (t0 + KT <= ra.T) {
+#pragma unroll
+      for (int i = 0; i < KT; ++i) {
+        step(cur.at(i));
+        yt[lane * kYS + i] = y;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < KT; ++i) {
+        if (t0 + i < ra.T) {
+          step(cur.at(i));
+          yt[lane * kYS + i] = y;
+        }
+      }
+    }
+    wave_lds_sync();
+#ifdef INSITE_ABLATE_NOSTORE
+    if (yt[lane * kYS] == 12345.678) ra.y[p] = y;  // keep the tile live
+    continue;
+#endif
+    if constexpr (YV == 2) {  // 16 lanes x 16 B per row segment, 4 rows per instruction
+      constexpr int LPR = KT / 2;        // lanes per row segment (16 B each)
+      constexpr int RPI = kWave / LPR;   // rows per instruction
+#pragma unroll
+      for (int j = 0; j < kWave / RPI; ++j) {
+        const int r = RPI * j + lane / LPR;
+        const int c = (lane % LPR) * 2;
+        const double2 v = *reinterpret_cast<const double2*>(yt + r * kYS + c);
+        const unsigned off = (t0 + c < ra.T) ? (unsigned)((r * ra.ldy + t0 + c) * 8) : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, off, 0, 0);
+      }
+    } else {  // 32 lanes x 8 B per row segment, 2 rows per instruction
+      constexpr int LPR = KT;            // lanes per row segment (8 B each)
       constexpr int RPI = kWave / LPR;
-      const int cl = (lane % LPR) * AVEC;
-      const int64_t col = t0 + cl;
-      uint32_t v[kWave / RPI];
 #pragma unroll
-      for (int it = 0; it < kWave / RPI; ++it) {
-        const int64_t pr = p0 + it * RPI + lane / LPR;
-        v[it] = 0u;
-        if (pr < ra.N && col < ra.T) {
-          if constexpr (AVEC == 4) v[it] = *reinterpret_cast<const uint32_t*>(ra.arm + pr * ra.lda + col);
-          else v[it] = (uint8_t)ra.arm[pr * ra.lda + col];
-        }
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int it = 0; it < kWave / RPI; ++it) {
-        const int r = it * RPI + lane / LPR;
-        if constexpr (AVEC == 4) at[r * kAStrideW + cl / 4] = v[it];
-        else at8[r * kAStrideW * 4 + cl] = (uint8_t)v[it];
-      }
-      wave_lds_sync();
-    }
-    // ---- integrate KT observation intervals ----
-    uint32_t a4 = 0u;
-#pragma unroll
-    for (int i = 0; i < KT; ++i) {
-      if ((i & 3) == 0) a4 = at[lane * kAStrideW + i / 4];
-      if (t0 + i < ra.T) {
-        const int a = (int)((a4 >> (8 * (i & 3))) & 0xffu);
-        double al = alpha[0], be = beta[0];
-#pragma unroll
-        for (int aa = 1; aa < NARM; ++aa) {
-          al = (a == aa) ? alpha[aa] : al;
-          be = (a == aa) ? beta[aa] : be;
-        }
-        if constexpr (METHOD == INSITE_METHOD_EULER) {
-          for (int s = 0; s < ra.substeps; ++s) {
-            const double f = fma(be, y, al);
-            y = fma(f, h, y);
-          }
-        } else {
-          for (int s = 0; s < ra.substeps; ++s) {
-            const double k1 = fma(be, y, al);
-            const double k2 = fma(be, fma(h2, k1, y), al);
-            const double k3 = fma(be, fma(h2, k2, y), al);
-            const double k4 = fma(be, fma(h, k3, y), al);
-            y = fma(h6, (k1 + 2.0 * k2) + (2.0 * k3 + k4), y);
-          }
-        }
-        yt[lane * kYStride + i] = y;
+      for (int j = 0; j < kWave / RPI; ++j) {
+        const int r = RPI * j + lane / LPR;
+        const int c = lane % LPR;
+        const double v = yt[r * kYS + c];
+        const unsigned off = (t0 + c < ra.T) ? (unsigned)((r * ra.ldy + t0 + c) * 8) : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), yrs, off, 0, 0);
       }
     }
     wave_lds_sync();
-    // ---- write-out: two 256-byte row segments per wave instruction ----
 #pragma unroll
-    for (int j = 0; j < kWave / 2; ++j) {
-      const int r = 2 * j + (lane >> 5);
-      const int c = lane & 31;
-      const int64_t pr = p0 + r;
-      const int tc = t0 + c;
-      const double v = yt[r * kYStride + c];
-      if (pr < ra.N && tc < ra.T) ra.y[pr * ra.ldy + tc] = v;
+    for (int k = 0; k < KT / 4; ++k) cur.w[k] = nxt.w[k];
+  }
+}
+
+// Time-major rollout (layout INSITE_LAYOUT_TIME_MAJOR): arm[k * lda + r], y[k * ldy + r].  Lane =
+// PPL adjacent patients; per step the wave reads 64*PPL contiguous arm bytes and writes 512*PPL
+// contiguous bytes of y — fully coalesced, no LDS staging.  Steps run in groups of kTG; the arm
+// bytes of the next group are prefetched into a register ring while the current group integrates,
+// and every buffer access is unconditional: the per-group descriptors' num_records clip the
+// prefetch and the stores at step T (the tail group integrates a few dead steps whose stores the
+// hardware drops), and inactive lanes carry an out-of-range offset.  So vmcnt waits are exact
+// (never a drain of the outstanding stores).  With PPL = 2 every lane advances two independent
+// RK4/Euler chains, doubling the instruction-level parallelism.
+#ifndef INSITE_TG
+#define INSITE_TG 16
+#endif
+constexpr int kTG = INSITE_TG;  // steps per group = arm prefetch distance
+constexpr int64_t kTmMaxLd = ((int64_t)1 << 31) / (8 * kTG);  // group offsets stay below 2^31
+
+template <int METHOD, int NARM, bool PERROW, int PPL, bool AW4>
+__global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibDesc lib) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform (SGPR)
+  const int64_t p0 = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * (kWave * PPL);
+  if (p0 >= ra.N) return;
+  double y[PPL], alpha[PPL][NARM], beta[PPL][NARM];
+  bool act[PPL];
+#pragma unroll
+  for (int q = 0; q < PPL; ++q) {
+    const int64_t p = p0 + PPL * lane + q;
+    act[q] = p < ra.N;
+    const int64_t pc = act[q] ? p : ra.N - 1;
+    double uu[INSITE_MAX_STATICS];
+#pragma unroll
+    for (int t = 0; t < INSITE_MAX_STATICS; ++t) {
+      const double v = ra.u[pc * lib.U + (t < lib.U ? t : 0)];
+      uu[t] = (act[q] && t < lib.U) ? v : 0.0;
     }
-    wave_lds_sync();
+    const double* cbase = ra.coef + (PERROW ? pc * ra.coef_stride : 0);
+#pragma unroll
+    for (int a = 0; a < NARM; ++a) {
+      alpha[q][a] = 0.0;
+      beta[q][a] = 0.0;
+      if (a >= ra.A) continue;
+      for (int j = 0; j < lib.F; ++j) {
+        const double c = cbase[a * lib.F + j];
+        if (fabs(c) > ra.drop) {
+          const double t = c * monomial(lib, j, uu);
+          if (lib.ex[j] == 0) alpha[q][a] += t;
+          else beta[q][a] += t;
+        }
+      }
+    }
+    const double v0 = ra.y0[pc];
+    y[q] = act[q] ? v0 : 0.0;
+  }
+  const double h = ra.dt / (double)ra.substeps;
+  const double h2 = 0.5 * h;
+  const double h6 = h / 6.0;
+  const int nvalid = (int)(ra.N - p0 < kWave * PPL ? ra.N - p0 : kWave * PPL);
+  // Inactive lanes (only in the last wavefront) store through an offset the hardware drops
+  // (kOOB + group offsets stays >= 2^31 > num_records).
+  const unsigned yoff = act[0] ? (unsigned)(PPL * lane * 8) : kOOB;
+
+  // Descriptors cover rows [k0, min(k0 + kTG, T)) of a time-major matrix, based at column p0.
+  // AW4: each lane loads the aligned dword holding its PPL arm bytes (lanes sharing a dword read
+  // the same address) into a plain 32-bit ring, and extracts its bytes at the use.  Narrower ring
+  // elements get packed by the compiler, which then waits for every prefetched load at the loop
+  // latch.  Requires ld_arm % 4 == 0 and a 4-byte aligned base, so the last row's dword stays
+  // inside the allocation; otherwise (AW4 = false) plain byte loads are used.
+  using ArmT = std::conditional_t<AW4, uint32_t, std::conditional_t<PPL == 2, uint16_t, uint8_t>>;
+  const unsigned abyte = (unsigned)(PPL * lane);
+  const unsigned aoff = AW4 ? (abyte & ~3u) : abyte;
+  const unsigned ashift = AW4 ? 8u * (abyte & 3u) : 0u;
+  const int arec_tail = AW4 ? ((nvalid + 3) & ~3) : nvalid;  // arm bytes of the last row
+  auto arm_rsrc = [&](int k0) {
+    const int rows = ra.T - k0 < kTG ? ra.T - k0 : kTG;
+    const int bytes = rows > 0 ? (int)((int64_t)(rows - 1) * ra.lda + arec_tail) : 0;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(ra.arm + (int64_t)(rows > 0 ? k0 : 0) * ra.lda + p0), (short)0,
+                                             bytes, 0x00020000);
+  };
+  auto y_rsrc = [&](int k0) {
+    const int rows = ra.T - k0 < kTG ? ra.T - k0 : kTG;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(ra.y + (int64_t)k0 * ra.ldy + p0), (short)0,
+                                             (int)(((int64_t)(rows - 1) * ra.ldy + nvalid) * 8), 0x00020000);
+  };
+  auto load_arm = [&](__amdgpu_buffer_rsrc_t rs, int i) -> ArmT {  // step i of a group
+    const unsigned off = aoff + (unsigned)(i * ra.lda);
+    if constexpr (AW4) return __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+    else if constexpr (PPL == 2) return (ArmT)__builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0);
+    else return (ArmT)__builtin_amdgcn_raw_buffer_load_b8(rs, off, 0, 0);
+  };
+  auto step = [&](int q, int a) {
+    double al = alpha[q][0], be = beta[q][0];
+#pragma unroll
+    for (int aa = 1; aa < NARM; ++aa) {
+      al = (a == aa) ? alpha[q][aa] : al;
+      be = (a == aa) ? beta[q][aa] : be;
+    }
+    double yy = y[q];
+    if constexpr (METHOD == INSITE_METHOD_EULER) {
+      for (int s = 0; s < ra.substeps; ++s) {
+        const double f = fma(be, yy, al);
+        yy = fma(f, h, yy);
+      }
+    } else {
+      for (int s = 0; s < ra.substeps; ++s) {
+        const double k1 = fma(be, yy, al);
+        const double k2 = fma(be, fma(h2, k1, yy), al);
+        const double k3 = fma(be, fma(h2, k2, yy), al);
+        const double k4 = fma(be, fma(h, k3, yy), al);
+        yy = fma(h6, (k1 + 2.0 * k2) + (2.0 * k3 + k4), yy);
+      }
+    }
+    y[q] = yy;
+  };
+
+  ArmT ring[kTG];
+  {
+    const __amdgpu_buffer_rsrc_t rs = arm_rsrc(0);
+#pragma unroll
+    for (int i = 0; i < kTG; ++i) ring[i] = load_arm(rs, i);
+  }
+  for (int k0 = 0; k0 < ra.T; k0 += kTG) {
+    const __amdgpu_buffer_rsrc_t rsn = arm_rsrc(k0 + kTG);  // empty past T: loads return 0
+    const __amdgpu_buffer_rsrc_t ys = y_rsrc(k0);
+#pragma unroll
+    for (int i = 0; i < kTG; ++i) {
+      const unsigned a2 = (unsigned)ring[i] >> ashift;
+      // consume ring[i] before its refill is issued: otherwise the scheduler hoists the load, the
+      // slot needs two registers and the latch copy waits for the load
+      asm volatile("" ::"v"(a2) : "memory");
+      ring[i] = load_arm(rsn, i);
+#pragma unroll
+      for (int q = 0; q < PPL; ++q) step(q, (int)((a2 >> (8 * q)) & 0xffu));
+      const unsigned off = yoff + (unsigned)(i * ra.ldy * 8);
+      if constexpr (PPL == 2) {
+        // a pair with an inactive second patient only occurs at the very end of the cohort;
+        // both halves are clipped by num_records there (column >= nvalid lies beyond the row)
+        const double2 v = make_double2(y[0], y[1]);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ys, off, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y[0]), ys, off, 0, 0);
+      }
+    }
   }
 }
 
@@ -637,18 +1221,110 @@ int build_lib(const int8_t* exps, int32_t F, int32_t U, LibDesc* lib) {
     ++e;
   }
   lib->nE = e;
-  return e <= kMaxEntries ? INSITE_OK : INSITE_E_UNSUPPORTED;
+  if (e > kMaxEntries) return INSITE_E_UNSUPPORTED;
+  // atoms: distinct u-exponent tuples of the columns
+  bool fits = true;
+  lib->n_atoms = 0;
+  for (int j = 0; j < F; ++j) {
+    int found = -1;
+    for (int a = 0; a < lib->n_atoms; ++a) {
+      bool same = true;
+      for (int t = 0; t < INSITE_MAX_STATICS; ++t) same = same && lib->atom_exp[a][t] == (t < U ? lib->eu[j][t] : 0);
+      if (same) found = a;
+    }
+    if (found < 0) {
+      found = lib->n_atoms++;
+      for (int t = 0; t < INSITE_MAX_STATICS; ++t) {
+        const int8_t ee = t < U ? lib->eu[j][t] : 0;
+        lib->atom_exp[found][t] = ee;
+        if (ee > 2) fits = false;
+      }
+    }
+    lib->col_atom[j] = (int8_t)found;
+  }
+  // Q columns: (atom of the column index, moment) pairs, deduplicated; the atom of "1" for b
+  int one_atom = -1;
+  for (int a = 0; a < lib->n_atoms; ++a)
+    if (lib->atom_exp[a][0] == 0 && lib->atom_exp[a][1] == 0 && lib->atom_exp[a][2] == 0) one_atom = a;
+  if (one_atom < 0) {
+    if (lib->n_atoms < 16) {
+      one_atom = lib->n_atoms++;
+      for (int t = 0; t < INSITE_MAX_STATICS; ++t) lib->atom_exp[one_atom][t] = 0;
+    } else {
+      fits = false;
+    }
+  }
+  lib->nq = 0;
+  for (int q = 0; q < lib->nE && fits; ++q) {
+    const int i = lib->ei[q], k = lib->ek[q];
+    const int at = k >= 0 ? lib->col_atom[k] : one_atom;
+    const int mom = k >= 0 ? lib->ex[i] + lib->ex[k] : 3 + lib->ex[i];
+    int found = -1;
+    for (int c = 0; c < lib->nq; ++c)
+      if (lib->qmom[c] == mom && lib->qatom[c] == at) found = c;
+    if (found < 0) {
+      if (lib->nq >= 16) {
+        fits = false;
+        break;
+      }
+      found = lib->nq++;
+      lib->qmom[found] = (int8_t)mom;
+      lib->qatom[found] = (int8_t)at;
+    }
+    lib->qcol[q] = (int8_t)found;
+  }
+  lib->mfma = fits ? 1 : 0;  // refined by the caller with the arm count (NARM * F <= 16)
+  return INSITE_OK;
 }
 
 inline int narm_pad(int n_arms) { return n_arms <= 1 ? 1 : (n_arms <= 2 ? 2 : 4); }
 
-inline int gram_grid(int64_t N) {
-  const int64_t tiles = (N + kWave - 1) / kWave;
-  int64_t g = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-  if (g < 1) g = 1;
-  if (g > kGramMaxBlocks) g = kGramMaxBlocks;
-  return (int)g;
+struct GramPlan {
+  int grid, seg, n_seg;
+};
+
+// Resident wavefronts of a kernel instance on the current device (occupancy query, cached per
+// instance and device; a planning hint only — correctness never depends on residency).
+template <typename K>
+int resident_waves(K kernel) {
+  static std::atomic<int> cache[16];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  const int slot = dev < 16 ? dev : 15;
+  int v = cache[slot].load(std::memory_order_relaxed);
+  if (v > 0) return v;
+  int cus = 0, per_cu = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu <= 0) per_cu = 2;
+  v = cus * per_cu * kWavesPerBlock;
+  cache[slot].store(v, std::memory_order_relaxed);
+  return v;
 }
+
+// Work decomposition: 64-patient tiles x time segments.  Segments add parallelism for small
+// cohorts, but every work item pays a warm-up and a Gram contraction, and a second partial round
+// of items leaves the chip under-occupied, so the item count is sized to one resident round.
+inline GramPlan gram_plan(int64_t N, int64_t ldx, int resident) {
+  GramPlan pl;
+  const int64_t tiles = (N + kWave - 1) / kWave;
+  int64_t ns = tiles > 0 ? resident / tiles : 1;
+  const int64_t ns_max = ldx / 48 > 1 ? ldx / 48 : 1;
+  if (ns > ns_max) ns = ns_max;
+  if (ns < 1) ns = 1;
+  int64_t seg = (ldx + ns - 1) / ns;
+  seg = (seg + kGT - 1) / kGT * kGT;
+  pl.seg = (int)seg;
+  pl.n_seg = (int)((ldx + seg - 1) / seg);
+  int64_t g = (tiles * pl.n_seg + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int64_t gres = resident / kWavesPerBlock > 0 ? resident / kWavesPerBlock : 1;
+  if (g > gres) g = gres;
+  if (g > kGramMaxBlocks) g = kGramMaxBlocks;
+  if (g < 1) g = 1;
+  pl.grid = (int)g;
+  return pl;
+}
+
+constexpr size_t kGramWsHeader = 256;  // ticket word (+ padding)
 
 inline int sse_grid(int64_t n_rows) {
   int64_t g = (n_rows + 63) / 64;
@@ -659,39 +1335,153 @@ inline int sse_grid(int64_t n_rows) {
 
 inline int32_t launch_status() { return hipGetLastError() == hipSuccess ? INSITE_OK : INSITE_E_HIP; }
 
-template <int NARM>
-void launch_gram(bool vec2, bool smooth, dim3 grid, hipStream_t st, const double* x, int64_t ldx,
-                 const double* u, const int8_t* arm, const int32_t* rows, int64_t N, double inv_dt,
-                 const LibDesc& lib, double* part) {
-  constexpr int KT = 32;
+template <int VEC, int NARM, bool SMOOTH, bool MFMA>
+void launch_gram3(hipStream_t st, const double* x, int64_t ldx, const double* u, const int8_t* arm,
+                  const int32_t* rows, int64_t N, const GramW& w, const LibDesc& lib, double* part,
+                  unsigned* ticket, int* grid_out) {
+  auto kern = gram_kernel<VEC, NARM, SMOOTH, MFMA>;
+  const GramPlan pl = gram_plan(N, ldx, resident_waves(kern));
+  *grid_out = pl.grid;
+  kern<<<dim3(pl.grid), kBlock, 0, st>>>(x, ldx, u, arm, rows, N, pl.seg, pl.n_seg, w, lib, part, ticket);
+}
+
+template <int NARM, bool MFMA>
+void launch_gram2(bool vec2, bool smooth, hipStream_t st, const double* x, int64_t ldx, const double* u,
+                  const int8_t* arm, const int32_t* rows, int64_t N, const GramW& w, const LibDesc& lib,
+                  double* part, unsigned* ticket, int* grid_out) {
   if (vec2) {
-    if (smooth) gram_kernel<KT, 2, NARM, true><<<grid, kBlock, 0, st>>>(x, ldx, u, arm, rows, N, inv_dt, lib, part);
-    else gram_kernel<KT, 2, NARM, false><<<grid, kBlock, 0, st>>>(x, ldx, u, arm, rows, N, inv_dt, lib, part);
+    if (smooth) launch_gram3<2, NARM, true, MFMA>(st, x, ldx, u, arm, rows, N, w, lib, part, ticket, grid_out);
+    else launch_gram3<2, NARM, false, MFMA>(st, x, ldx, u, arm, rows, N, w, lib, part, ticket, grid_out);
   } else {
-    if (smooth) gram_kernel<KT, 1, NARM, true><<<grid, kBlock, 0, st>>>(x, ldx, u, arm, rows, N, inv_dt, lib, part);
-    else gram_kernel<KT, 1, NARM, false><<<grid, kBlock, 0, st>>>(x, ldx, u, arm, rows, N, inv_dt, lib, part);
+    if (smooth) launch_gram3<1, NARM, true, MFMA>(st, x, ldx, u, arm, rows, N, w, lib, part, ticket, grid_out);
+    else launch_gram3<1, NARM, false, MFMA>(st, x, ldx, u, arm, rows, N, w, lib, part, ticket, grid_out);
   }
 }
 
+template <int NARM>
+void launch_gram(bool vec2, bool smooth, hipStream_t st, const double* x, int64_t ldx, const double* u,
+                 const int8_t* arm, const int32_t* rows, int64_t N, const GramW& w, const LibDesc& lib,
+                 double* part, unsigned* ticket, int* grid_out) {
+  if (lib.mfma) launch_gram2<NARM, true>(vec2, smooth, st, x, ldx, u, arm, rows, N, w, lib, part, ticket, grid_out);
+  else launch_gram2<NARM, false>(vec2, smooth, st, x, ldx, u, arm, rows, N, w, lib, part, ticket, grid_out);
+}
+
+// gram kernel + fused finalize (+ STLSQ when sp.enabled)
+int32_t run_discovery(const double* x, int64_t ldx, const double* u, const int8_t* arm, const int32_t* rows,
+                      int64_t n_patients, int32_t n_statics, int32_t n_arms, const int8_t* exps, int32_t n_terms,
+                      int32_t fd_kind, double dt, double* G_out, double* b_out, void* workspace,
+                      size_t workspace_bytes, void* stream, const StlsqParams& sp, double* coef_out,
+                      int8_t* mask_out, int32_t* iters_out) {
+  if (n_patients < 0 || !G_out || !b_out || n_arms < 1 || n_arms > INSITE_MAX_ARMS || ldx < 1 || !(dt > 0.0))
+    return INSITE_E_INVALID_ARG;
+  if (n_patients > 0 && (!x || !arm || !rows || (n_statics > 0 && !u))) return INSITE_E_INVALID_ARG;
+  if (fd_kind != INSITE_FD_SMOOTHED4 && fd_kind != INSITE_FD_ORDER4) return INSITE_E_UNSUPPORTED;
+  LibDesc lib;
+  int32_t st = build_lib(exps, n_terms, n_statics, &lib);
+  if (st != INSITE_OK) return st;
+  if (workspace_bytes < insite_gram_workspace_bytes(n_patients, n_arms, n_terms) || !workspace)
+    return INSITE_E_WORKSPACE;
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  const int na = narm_pad(n_arms);
+  if (na * lib.F > 16) lib.mfma = 0;
+  unsigned* ticket = static_cast<unsigned*>(workspace);
+  double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + kGramWsHeader);
+  const bool vec2 = (ldx % 2 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15u) == 0);
+  const bool smooth = fd_kind == INSITE_FD_SMOOTHED4;
+  if (n_statics == 0) u = x;  // kernels load u unconditionally (values unused when U = 0)
+  GramW w;
+  w.sg0 = 17.0 / 35.0;
+  w.sg1 = 12.0 / 35.0;
+  w.sg2 = -3.0 / 35.0;
+  w.inv_dt = 1.0 / dt;
+  w.fd1 = (2.0 / 3.0) * w.inv_dt;
+  w.fd2 = (-1.0 / 12.0) * w.inv_dt;
+  int grid = 1;
+  if (na == 1) launch_gram<1>(vec2, smooth, hs, x, ldx, u, arm, rows, n_patients, w, lib, part, ticket, &grid);
+  else if (na == 2) launch_gram<2>(vec2, smooth, hs, x, ldx, u, arm, rows, n_patients, w, lib, part, ticket, &grid);
+  else launch_gram<4>(vec2, smooth, hs, x, ldx, u, arm, rows, n_patients, w, lib, part, ticket, &grid);
+  st = launch_status();
+  if (st != INSITE_OK) return st;
+  const dim3 fg(n_arms * lib.nE);
+  if (!sp.enabled) {
+    discovery_finalize<0><<<fg, kBlock, 0, hs>>>(part, grid, na, n_arms, lib, G_out, b_out, sp, nullptr, nullptr,
+                                                 nullptr, ticket);
+    return launch_status();
+  }
+  switch (n_terms) {
+#define INSITE_FIN_CASE(FF)                                                                          \
+  case FF:                                                                                           \
+    discovery_finalize<FF><<<fg, kBlock, 0, hs>>>(part, grid, na, n_arms, lib, G_out, b_out, sp, coef_out, \
+                                                  mask_out, iters_out, ticket);                      \
+    break;
+    INSITE_FIN_CASE(1)
+    INSITE_FIN_CASE(2)
+    INSITE_FIN_CASE(3)
+    INSITE_FIN_CASE(4)
+    INSITE_FIN_CASE(5)
+    INSITE_FIN_CASE(6)
+    INSITE_FIN_CASE(7)
+    INSITE_FIN_CASE(8)
+    INSITE_FIN_CASE(9)
+#undef INSITE_FIN_CASE
+    default:
+      return INSITE_E_UNSUPPORTED;
+  }
+  return launch_status();
+}
+
 template <int METHOD, int NARM, bool PERROW>
-void launch_rollout_a(bool avec4, dim3 grid, hipStream_t st, const RolloutArgs& ra, const LibDesc& lib) {
-  if (avec4) rollout_kernel<METHOD, NARM, PERROW, 4, 32><<<grid, kBlock, 0, st>>>(ra, lib);
-  else rollout_kernel<METHOD, NARM, PERROW, 1, 32><<<grid, kBlock, 0, st>>>(ra, lib);
+void launch_rollout_a(int av, bool yv2, dim3 grid, hipStream_t st, const RolloutArgs& ra, const LibDesc& lib) {
+  if (yv2) {
+    if (av == 16) rollout_kernel<METHOD, NARM, PERROW, 16, 2><<<grid, kBlock, 0, st>>>(ra, lib);
+    else if (av == 4) rollout_kernel<METHOD, NARM, PERROW, 4, 2><<<grid, kBlock, 0, st>>>(ra, lib);
+    else rollout_kernel<METHOD, NARM, PERROW, 1, 2><<<grid, kBlock, 0, st>>>(ra, lib);
+  } else {
+    if (av == 16) rollout_kernel<METHOD, NARM, PERROW, 16, 1><<<grid, kBlock, 0, st>>>(ra, lib);
+    else if (av == 4) rollout_kernel<METHOD, NARM, PERROW, 4, 1><<<grid, kBlock, 0, st>>>(ra, lib);
+    else rollout_kernel<METHOD, NARM, PERROW, 1, 1><<<grid, kBlock, 0, st>>>(ra, lib);
+  }
 }
 
 template <int METHOD, int NARM>
-void launch_rollout_p(bool perrow, bool avec4, dim3 grid, hipStream_t st, const RolloutArgs& ra,
+void launch_rollout_p(bool perrow, int av, bool yv2, dim3 grid, hipStream_t st, const RolloutArgs& ra,
                       const LibDesc& lib) {
-  if (perrow) launch_rollout_a<METHOD, NARM, true>(avec4, grid, st, ra, lib);
-  else launch_rollout_a<METHOD, NARM, false>(avec4, grid, st, ra, lib);
+  if (perrow) launch_rollout_a<METHOD, NARM, true>(av, yv2, grid, st, ra, lib);
+  else launch_rollout_a<METHOD, NARM, false>(av, yv2, grid, st, ra, lib);
+}
+
+template <int METHOD, int NARM, int PPL>
+void launch_rollout_tm_w(bool perrow, bool aw4, dim3 grid, hipStream_t st, const RolloutArgs& ra, const LibDesc& lib) {
+  if (perrow) {
+    if (aw4) rollout_tm_kernel<METHOD, NARM, true, PPL, true><<<grid, kBlock, 0, st>>>(ra, lib);
+    else rollout_tm_kernel<METHOD, NARM, true, PPL, false><<<grid, kBlock, 0, st>>>(ra, lib);
+  } else {
+    if (aw4) rollout_tm_kernel<METHOD, NARM, false, PPL, true><<<grid, kBlock, 0, st>>>(ra, lib);
+    else rollout_tm_kernel<METHOD, NARM, false, PPL, false><<<grid, kBlock, 0, st>>>(ra, lib);
+  }
+}
+
+template <int METHOD, int NARM>
+void launch_rollout_tm(bool perrow, int ppl, bool aw4, dim3 grid, hipStream_t st, const RolloutArgs& ra,
+                       const LibDesc& lib) {
+  if (ppl == 2) launch_rollout_tm_w<METHOD, NARM, 2>(perrow, aw4, grid, st, ra, lib);
+  else launch_rollout_tm_w<METHOD, NARM, 1>(perrow, aw4, grid, st, ra, lib);
 }
 
 template <int METHOD>
-void launch_rollout_m(int narm, bool perrow, bool avec4, dim3 grid, hipStream_t st,
+void launch_rollout_m(int narm, bool perrow, int av, bool yv2, dim3 grid, hipStream_t st,
                       const RolloutArgs& ra, const LibDesc& lib) {
-  if (narm == 1) launch_rollout_p<METHOD, 1>(perrow, avec4, grid, st, ra, lib);
-  else if (narm == 2) launch_rollout_p<METHOD, 2>(perrow, avec4, grid, st, ra, lib);
-  else launch_rollout_p<METHOD, 4>(perrow, avec4, grid, st, ra, lib);
+  if (narm == 1) launch_rollout_p<METHOD, 1>(perrow, av, yv2, grid, st, ra, lib);
+  else if (narm == 2) launch_rollout_p<METHOD, 2>(perrow, av, yv2, grid, st, ra, lib);
+  else launch_rollout_p<METHOD, 4>(perrow, av, yv2, grid, st, ra, lib);
+}
+
+template <int METHOD>
+void launch_rollout_tm_m(int narm, bool perrow, int ppl, bool aw4, dim3 grid, hipStream_t st, const RolloutArgs& ra,
+                         const LibDesc& lib) {
+  if (narm == 1) launch_rollout_tm<METHOD, 1>(perrow, ppl, aw4, grid, st, ra, lib);
+  else if (narm == 2) launch_rollout_tm<METHOD, 2>(perrow, ppl, aw4, grid, st, ra, lib);
+  else launch_rollout_tm<METHOD, 4>(perrow, ppl, aw4, grid, st, ra, lib);
 }
 
 }  // namespace
@@ -756,7 +1546,8 @@ int32_t insite_poly_library(int32_t n_statics, int32_t degree, int32_t interacti
 size_t insite_gram_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms) {
   (void)n_terms;
   if (n_patients < 0 || n_arms < 1 || n_arms > INSITE_MAX_ARMS) return 0;
-  return (size_t)gram_grid(n_patients) * (size_t)narm_pad(n_arms) * kWave * sizeof(double);
+  const size_t per_block = narm_pad(n_arms) * kWave > 256 ? (size_t)narm_pad(n_arms) * kWave : 256;
+  return kGramWsHeader + (size_t)kGramMaxBlocks * per_block * sizeof(double);
 }
 
 int32_t insite_gram_f64(const double* x, int64_t ldx, const double* u, const int8_t* arm,
@@ -764,30 +1555,21 @@ int32_t insite_gram_f64(const double* x, int64_t ldx, const double* u, const int
                         const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
                         double* G_out, double* b_out, void* workspace, size_t workspace_bytes,
                         void* stream) {
-  if (n_patients < 0 || !G_out || !b_out || n_arms < 1 || n_arms > INSITE_MAX_ARMS || ldx < 1 ||
-      !(dt > 0.0))
-    return INSITE_E_INVALID_ARG;
-  if (n_patients > 0 && (!x || !arm || !rows || (n_statics > 0 && !u))) return INSITE_E_INVALID_ARG;
-  if (fd_kind != INSITE_FD_SMOOTHED4 && fd_kind != INSITE_FD_ORDER4) return INSITE_E_UNSUPPORTED;
-  LibDesc lib;
-  int32_t st = build_lib(exps, n_terms, n_statics, &lib);
-  if (st != INSITE_OK) return st;
-  if (workspace_bytes < insite_gram_workspace_bytes(n_patients, n_arms, n_terms) || !workspace)
-    return INSITE_E_WORKSPACE;
-  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
-  const int grid = gram_grid(n_patients);
-  const int na = narm_pad(n_arms);
-  double* part = static_cast<double*>(workspace);
-  const bool vec2 = (ldx % 2 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15u) == 0);
-  const bool smooth = fd_kind == INSITE_FD_SMOOTHED4;
-  const double inv_dt = 1.0 / dt;
-  if (na == 1) launch_gram<1>(vec2, smooth, dim3(grid), hs, x, ldx, u, arm, rows, n_patients, inv_dt, lib, part);
-  else if (na == 2) launch_gram<2>(vec2, smooth, dim3(grid), hs, x, ldx, u, arm, rows, n_patients, inv_dt, lib, part);
-  else launch_gram<4>(vec2, smooth, dim3(grid), hs, x, ldx, u, arm, rows, n_patients, inv_dt, lib, part);
-  st = launch_status();
-  if (st != INSITE_OK) return st;
-  gram_finalize<<<dim3(n_arms * lib.nE), kBlock, 0, hs>>>(part, grid, na, n_arms, lib, G_out, b_out);
-  return launch_status();
+  StlsqParams sp{0.0, 0.0, 0, 0, 0};
+  return run_discovery(x, ldx, u, arm, rows, n_patients, n_statics, n_arms, exps, n_terms, fd_kind, dt, G_out,
+                       b_out, workspace, workspace_bytes, stream, sp, nullptr, nullptr, nullptr);
+}
+
+int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, const double* u, const int8_t* arm,
+                             const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
+                             const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
+                             double threshold, double alpha, int32_t max_iter, int32_t unbias,
+                             double* G_out, double* b_out, double* coef_out, int8_t* mask_out,
+                             int32_t* iters_out, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!coef_out || max_iter < 0 || !(threshold >= 0.0) || !(alpha >= 0.0)) return INSITE_E_INVALID_ARG;
+  StlsqParams sp{threshold, alpha, max_iter, unbias, 1};
+  return run_discovery(x, ldx, u, arm, rows, n_patients, n_statics, n_arms, exps, n_terms, fd_kind, dt, G_out,
+                       b_out, workspace, workspace_bytes, stream, sp, coef_out, mask_out, iters_out);
 }
 
 int32_t insite_stlsq_f64(const double* G, const double* b, int64_t n_sys, int32_t n_terms,
@@ -824,9 +1606,12 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
                            const double* coef, int64_t coef_row_stride, const int8_t* exps,
                            int32_t n_terms, int64_t n_rows, int32_t T, int32_t n_statics,
                            int32_t n_arms, double dt, int32_t method, int32_t substeps,
-                           double drop_below, double* y_out, int64_t ld_y, void* stream) {
+                           double drop_below, double* y_out, int64_t ld_y, int32_t layout, void* stream) {
+  const bool tm = layout == INSITE_LAYOUT_TIME_MAJOR;
+  if (layout != INSITE_LAYOUT_PATIENT_MAJOR && !tm) return INSITE_E_INVALID_ARG;
+  const int64_t minld = tm ? n_rows : (int64_t)T;
   if (n_rows < 0 || T < 0 || n_arms < 1 || n_arms > INSITE_MAX_ARMS || substeps < 1 ||
-      !(dt >= 0.0) || ld_arm < T || ld_y < T || coef_row_stride < 0)
+      !(dt >= 0.0) || ld_arm < minld || ld_y < minld || coef_row_stride < 0)
     return INSITE_E_INVALID_ARG;
   if (method != INSITE_METHOD_EULER && method != INSITE_METHOD_RK4) return INSITE_E_UNSUPPORTED;
   if (n_rows == 0 || T == 0) return INSITE_OK;
@@ -850,14 +1635,30 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
   ra.A = n_arms;
   ra.dt = dt;
   ra.drop = drop_below;
-  const bool avec4 = (ld_arm % 4 == 0) && ((reinterpret_cast<uintptr_t>(arm) & 3u) == 0);
-  const int64_t waves = (n_rows + kWave - 1) / kWave;
-  const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   const bool perrow = coef_row_stride != 0;
   const int na = narm_pad(n_arms);
-  if (method == INSITE_METHOD_EULER) launch_rollout_m<INSITE_METHOD_EULER>(na, perrow, avec4, grid, hs, ra, lib);
-  else launch_rollout_m<INSITE_METHOD_RK4>(na, perrow, avec4, grid, hs, ra, lib);
+  if (tm) {
+    if (ld_arm > kTmMaxLd || ld_y > kTmMaxLd) return INSITE_E_UNSUPPORTED;  // 32-bit offsets per step group
+    if (n_statics == 0) ra.u = y0;
+    const int ppl = (n_rows >= 256 * 1024 && n_rows % 2 == 0 && (ld_y % 2 == 0) && ((reinterpret_cast<uintptr_t>(y_out) & 15u) == 0) &&
+                     (ld_arm % 2 == 0) && ((reinterpret_cast<uintptr_t>(arm) & 1u) == 0)) ? 2 : 1;
+    const int64_t per_block = (int64_t)kBlock * ppl;
+    const dim3 grid((unsigned)((n_rows + per_block - 1) / per_block));
+    const bool aw4 = ld_arm % 4 == 0 && (reinterpret_cast<uintptr_t>(arm) & 3u) == 0;
+    if (method == INSITE_METHOD_EULER) launch_rollout_tm_m<INSITE_METHOD_EULER>(na, perrow, ppl, aw4, grid, hs, ra, lib);
+    else launch_rollout_tm_m<INSITE_METHOD_RK4>(na, perrow, ppl, aw4, grid, hs, ra, lib);
+    return launch_status();
+  }
+  if (ld_arm > (int64_t)0x1FFFFFF || ld_y > (int64_t)0x3FFFFF) return INSITE_E_UNSUPPORTED;  // 32-bit buffer offsets
+  const uintptr_t ab = reinterpret_cast<uintptr_t>(arm), yb = reinterpret_cast<uintptr_t>(y_out);
+  const int av = (ld_arm % 16 == 0 && (ab & 15u) == 0) ? 16 : ((ld_arm % 4 == 0 && (ab & 3u) == 0) ? 4 : 1);
+  const bool yv2 = (ld_y % 2 == 0) && (T % 2 == 0) && ((yb & 15u) == 0);
+  if (n_statics == 0) ra.u = y0;  // loaded unconditionally, unused when U = 0
+  const int64_t waves = (n_rows + kWave - 1) / kWave;
+  const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
+  if (method == INSITE_METHOD_EULER) launch_rollout_m<INSITE_METHOD_EULER>(na, perrow, av, yv2, grid, hs, ra, lib);
+  else launch_rollout_m<INSITE_METHOD_RK4>(na, perrow, av, yv2, grid, hs, ra, lib);
   return launch_status();
 }
 

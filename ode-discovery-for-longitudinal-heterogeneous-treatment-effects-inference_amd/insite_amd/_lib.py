@@ -16,6 +16,9 @@ import torch  # noqa: F401  (must precede the dlopen below: shared HIP runtime)
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(PKG_ROOT, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libinsite_hip.so")
+# profiling-only override (ablation builds under tools/); never set in product runs
+if os.environ.get("INSITE_LIB_OVERRIDE"):
+    LIB_PATH = os.environ["INSITE_LIB_OVERRIDE"]
 
 ABI_VERSION = 1
 
@@ -23,6 +26,7 @@ ABI_VERSION = 1
 INSITE_OK = 0
 FD_SMOOTHED4, FD_ORDER4, FD_ORDER1 = 0, 1, 2
 METHOD_EULER, METHOD_RK4 = 0, 1
+LAYOUT_PATIENT_MAJOR, LAYOUT_TIME_MAJOR = 0, 1
 MAX_TERMS, MAX_STATICS, MAX_ARMS, MAX_STATE_DEGREE = 9, 3, 4, 1
 
 EXPORTS = (
@@ -31,6 +35,7 @@ EXPORTS = (
     "insite_poly_library",
     "insite_gram_workspace_bytes",
     "insite_gram_f64",
+    "insite_sindy_fit_f64",
     "insite_stlsq_f64",
     "insite_rollout_f64",
     "insite_masked_sse_workspace_bytes",
@@ -60,9 +65,12 @@ _SIGNATURES = {
     "insite_gram_workspace_bytes": (_c_size, [_c_i64, _c_i32, _c_i32]),
     "insite_gram_f64": (_c_i32, [_vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp, _c_i32, _c_i32,
                                  _c_f64, _vp, _vp, _vp, _c_size, _vp]),
+    "insite_sindy_fit_f64": (_c_i32, [_vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp, _c_i32, _c_i32,
+                                      _c_f64, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _c_size,
+                                      _vp]),
     "insite_stlsq_f64": (_c_i32, [_vp, _vp, _c_i64, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _vp]),
     "insite_rollout_f64": (_c_i32, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _vp, _c_i32, _c_i64, _c_i32, _c_i32,
-                                    _c_i32, _c_f64, _c_i32, _c_i32, _c_f64, _vp, _c_i64, _vp]),
+                                    _c_i32, _c_f64, _c_i32, _c_i32, _c_f64, _vp, _c_i64, _c_i32, _vp]),
     "insite_masked_sse_workspace_bytes": (_c_size, [_c_i64, _c_i32]),
     "insite_masked_sse_f64": (_c_i32, [_vp, _c_i64, _c_f64, _c_f64, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _vp,
                                        _vp, _c_size, _vp]),

@@ -69,7 +69,9 @@ def synthetic_pkpd(n_patients: int, T: int, seed: int, device, equation: str = "
         x[:, T:] = 0.0
     coef = torch.zeros((N, 2, lib.n_terms), device=dev, dtype=f64)
     coef[:, :, 1] = -C                               # 'x0' column carries -C_a
-    arms = arm[:, None].expand(N, T - 1).contiguous()
+    lda = (T + 15) // 16 * 16
+    arms = torch.empty((N, lda), dtype=torch.int8, device=dev)
+    arms[:] = arm[:, None]
     if T > 1:
         ops.rollout(x0, c.contiguous(), arms, coef, lib, dt, method="euler5", drop_below=0.0, T=T - 1,
                     out=x[:, 1:T])
@@ -79,16 +81,26 @@ def synthetic_pkpd(n_patients: int, T: int, seed: int, device, equation: str = "
     return DeviceCohort(x=x, u=c.contiguous(), arm=arm, rows=rows, C=C, T=T, dt=dt, lib=lib)
 
 
-def counterfactual_arms(arm: torch.Tensor, T: int, seed: int) -> torch.Tensor:
-    """Per-step arm sequences: the factual arm, flipped from a random step on (C2 workload)."""
+def counterfactual_arms(arm: torch.Tensor, T: int, seed: int, layout: str = "patient") -> torch.Tensor:
+    """Per-step arm sequences: the factual arm, flipped from a random step on (C2 workload).
+
+    layout "patient": [N, round_up(T, 16)] (16-byte rows: the patient-major rollout reads 16 B per
+    lane); layout "time": [T, round_up(N, 4)] (time-major; 4-byte rows let the rollout load
+    dwords)."""
     dev = arm.device
     g = _gen(seed + 7919, dev)
     N = arm.numel()
     flip = torch.randint(0, T, (N, 1), generator=g, device=dev)
     steps = torch.arange(T, device=dev)[None, :]
-    lda = (T + 3) // 4 * 4
+    seq = torch.where(steps >= flip, 1 - arm[:, None], arm[:, None]).to(torch.int8)
+    if layout == "time":
+        ld = (N + 3) // 4 * 4
+        out = torch.zeros((T, ld), dtype=torch.int8, device=dev)
+        out[:, :N] = seq.t()
+        return out
+    lda = (T + 15) // 16 * 16
     out = torch.empty((N, lda), dtype=torch.int8, device=dev)
-    out[:, :T] = torch.where(steps >= flip, 1 - arm[:, None], arm[:, None]).to(torch.int8)
+    out[:, :T] = seq
     if lda > T:
         out[:, T:] = 0
     return out

@@ -16,6 +16,7 @@ from .library import PolyLibrary
 
 METHODS = {"euler5": (_lib.METHOD_EULER, 5), "euler": (_lib.METHOD_EULER, 1), "rk4": (_lib.METHOD_RK4, 1)}
 FD_KINDS = {"smoothed4": _lib.FD_SMOOTHED4, "order4": _lib.FD_ORDER4}
+LAYOUTS = {"patient": _lib.LAYOUT_PATIENT_MAJOR, "time": _lib.LAYOUT_TIME_MAJOR}
 
 
 def _p(t):
@@ -89,6 +90,46 @@ def gram(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor
     return G, b
 
 
+def sindy_fit(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor, dt: float,
+              lib: PolyLibrary, threshold: float, alpha: float, max_iter: int = 100, unbias: bool = True,
+              n_arms: int = 2, fd: str = "smoothed4", workspace: Workspace | None = None,
+              out: tuple | None = None):
+    """Discovery in two launches (insite_sindy_fit_f64): Gram kernel, then the fixed-order
+    reduction fused with one STLSQ fit per arm.  Replaces ``SINDy(...).fit`` per arm
+    (reference sindy.py:190-192).  Returns (coef[A,F], mask[A,F], iters[A], G[A,F,F], b[A,F])."""
+    L = _lib.load()
+    _dev("x", x, torch.float64, 2)
+    N = x.size(0)
+    _dev("arm", arm, torch.int8, 1)
+    _dev("rows", rows, torch.int32, 1)
+    if lib.n_statics:
+        _dev("u", u, torch.float64, 2)
+        if u.size(0) != N or u.size(1) != lib.n_statics or u.stride(0) != lib.n_statics:
+            raise ValueError("u must be a contiguous [N, n_statics] tensor")
+    if arm.numel() != N or rows.numel() != N:
+        raise ValueError("arm/rows must have one entry per patient")
+    F = lib.n_terms
+    dev = x.device
+    if out is None:
+        coef = torch.empty((n_arms, F), dtype=torch.float64, device=dev)
+        mask = torch.empty((n_arms, F), dtype=torch.int8, device=dev)
+        iters = torch.empty((n_arms,), dtype=torch.int32, device=dev)
+        G = torch.empty((n_arms, F, F), dtype=torch.float64, device=dev)
+        b = torch.empty((n_arms, F), dtype=torch.float64, device=dev)
+    else:
+        coef, mask, iters, G, b = out
+    nbytes = L.insite_gram_workspace_bytes(N, n_arms, F)
+    ws = (workspace or _WS).get(nbytes, dev)
+    tab = lib.ctypes_table()
+    st = L.insite_sindy_fit_f64(_p(x), x.stride(0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm),
+                                _p(rows), N, lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p), F,
+                                FD_KINDS[fd], float(dt), float(threshold), float(alpha), int(max_iter),
+                                int(bool(unbias)), _p(G), _p(b), _p(coef), _p(mask), _p(iters), _p(ws), ws.numel(),
+                                _stream(dev))
+    _lib.check("insite_sindy_fit_f64", st)
+    return coef, mask, iters, G, b
+
+
 def stlsq(G: torch.Tensor, b: torch.Tensor, threshold: float, alpha: float, max_iter: int = 100,
           unbias: bool = True, out: tuple | None = None):
     """Batched STLSQ on Gram systems (insite_stlsq_f64).  G [S,F,F], b [S,F]."""
@@ -113,18 +154,28 @@ def stlsq(G: torch.Tensor, b: torch.Tensor, threshold: float, alpha: float, max_
 
 def rollout(y0: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, coef: torch.Tensor, lib: PolyLibrary,
             dt: float, method: str = "euler5", substeps: int | None = None, drop_below: float = 1e-3,
-            T: int | None = None, out: torch.Tensor | None = None):
+            T: int | None = None, out: torch.Tensor | None = None, layout: str = "patient"):
     """Batched open-loop rollout (insite_rollout_f64).
 
-    y0 [N] f64, u [N,U] f64, arm [N, >=T] int8 (per-step arm), coef [A,F] (global model) or
-    [N,A,F] (per-patient).  Returns y [N,T] (state after each observation interval)."""
+    y0 [N] f64, u [N,U] f64, coef [A,F] (global model) or [N,A,F] (per-patient).
+    layout "patient": arm [N, >=T] int8, returns y [N,T] (the reference's [N, T] arrays).
+    layout "time":    arm [T, >=N] int8, returns y [T,N] (time-major: one contiguous run per step,
+    the fast layout on MI355X).  Row k holds the state after observation interval k."""
     L = _lib.load()
+    if layout not in LAYOUTS:
+        raise ValueError(f"layout must be one of {sorted(LAYOUTS)}")
+    tm = layout == "time"
     _dev("y0", y0, torch.float64, 1)
     _dev("arm", arm, torch.int8, 2)
     N = y0.numel()
-    T = arm.size(1) if T is None else int(T)
-    if arm.size(0) != N:
-        raise ValueError("arm must have one row per patient")
+    if tm:
+        T = arm.size(0) if T is None else int(T)
+        if arm.size(1) < N or arm.size(0) < T:
+            raise ValueError("time-major arm must be [>=T, >=N]")
+    else:
+        T = arm.size(1) if T is None else int(T)
+        if arm.size(0) != N or arm.size(1) < T:
+            raise ValueError("arm must be [N, >=T]")
     if lib.n_statics:
         _dev("u", u, torch.float64, 2)
         if u.size(0) != N or u.size(1) != lib.n_statics or u.stride(0) != lib.n_statics:
@@ -147,14 +198,18 @@ def rollout(y0: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, coef: torch.Te
         raise ValueError("coef last dim must equal the library size")
     m, default_sub = METHODS[method]
     sub = int(substeps or default_sub)
+    shape = (T, N) if tm else (N, T)
     if out is None:
-        out = torch.empty((N, T), dtype=torch.float64, device=y0.device)
+        out = torch.empty(shape, dtype=torch.float64, device=y0.device)
     else:
         _dev("out", out, torch.float64, 2)
+        if out.size(0) != shape[0] or out.size(1) < shape[1]:
+            raise ValueError(f"out must be {shape}")
     tab = lib.ctypes_table()
     st = L.insite_rollout_f64(_p(y0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), arm.stride(0),
                               _p(coef), stride, tab.ctypes.data_as(ctypes.c_void_p), F, N, T, lib.n_statics, A,
-                              float(dt), m, sub, float(drop_below), _p(out), out.stride(0), _stream(y0.device))
+                              float(dt), m, sub, float(drop_below), _p(out), out.stride(0), LAYOUTS[layout],
+                              _stream(y0.device))
     _lib.check("insite_rollout_f64", st)
     return out
 

@@ -67,6 +67,29 @@ def test_gram_ragged_rows_odd_ld_and_order4(dev):
         np.testing.assert_allclose(b.cpu().numpy(), b_ref, rtol=1e-10, atol=1e-8)
 
 
+@pytest.mark.parametrize("ld", [300, 301])
+def test_gram_ragged_multi_segment(dev, ld):
+    """Long ragged rows split over several time segments (small N -> segmented work items);
+    every row length from 0 to ld, both derivative kinds, both staging widths."""
+    from insite_amd import ops
+    rng = np.random.default_rng(ld)
+    N = 300
+    x = rng.uniform(1, 50, size=(N, ld))
+    u = rng.normal(0.5, 0.05, size=(N, 2))
+    arm = rng.integers(0, 2, size=N)
+    rows = rng.integers(0, ld + 1, size=N)
+    rows[:12] = [0, 4, 5, 6, 7, 8, 9, 63, 64, 65, ld - 1, ld]
+    lib = _lib(2, 2, True)
+    exps = lib.exps.astype(np.int64)
+    for fd in ("smoothed4", "order4"):
+        G_ref, b_ref = R.gram_moments(x, u, arm, rows, 0.05, exps, n_arms=2, fd=fd)
+        G, b = ops.gram(_t(x, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), 0.05, lib,
+                        n_arms=2, fd=fd)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(G.cpu().numpy(), G_ref, rtol=1e-10, atol=1e-8)
+        np.testing.assert_allclose(b.cpu().numpy(), b_ref, rtol=1e-10, atol=1e-8)
+
+
 def test_gram_deterministic(dev):
     from insite_amd import ops
     x, u, arm, rows = _cohort("EQ_4_B", 2000, 60)
@@ -150,26 +173,58 @@ def _random_rollout_case(rng, N, T, A=2, U=2, lda=None, per_patient=False):
     return lib, y0, u, arm, coef
 
 
+def _arm_layout(arm, T, layout, dev):
+    """Device arm matrix in the requested layout.  "time": [T, N + 3] (ragged leading dim ->
+    byte-load path); "time4": [T, round_up(N, 4)] (dword-load path of the time-major kernel)."""
+    if layout == "patient":
+        return _t(arm, dev, torch.int8)
+    N = arm.shape[0]
+    ld = N + 3 if layout == "time" else (N + 3) // 4 * 4
+    tm = np.zeros((T, ld), np.int8)
+    tm[:, :N] = arm[:, :T].T
+    return _t(tm, dev, torch.int8)
+
+
+def _as_patient_major(y, layout):
+    yg = y.cpu().numpy()
+    return yg if layout == "patient" else yg.T
+
+
+@pytest.mark.parametrize("layout", ["patient", "time", "time4"])
 @pytest.mark.parametrize("method", ["euler5", "rk4", "euler"])
 @pytest.mark.parametrize("N,T,lda,per", [(1000, 60, 60, False), (777, 59, 59, False), (129, 201, 204, True),
                                          (64, 1, 4, False), (65, 33, 35, True)])
-def test_rollout_matches_oracle(dev, method, N, T, lda, per):
+def test_rollout_matches_oracle(dev, method, N, T, lda, per, layout):
     from insite_amd import ops
     rng = np.random.default_rng(N + T)
     lib, y0, u, arm, coef = _random_rollout_case(rng, N, T, lda=lda, per_patient=per)
     dt = R.MAX_TIME_HORIZON / max(T, 1)
-    y = ops.rollout(_t(y0, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(coef, dev), lib, dt, method=method, T=T)
-    torch.cuda.synchronize()
     sub = 3 if method == "euler" else None
-    if method == "euler":
-        y = ops.rollout(_t(y0, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(coef, dev), lib, dt, method="euler",
-                        substeps=3, T=T)
-        torch.cuda.synchronize()
+    y = ops.rollout(_t(y0, dev), _t(u, dev), _arm_layout(arm, T, layout, dev), _t(coef, dev), lib, dt,
+                    method=method, substeps=sub, T=T, layout="patient" if layout == "patient" else "time")
+    torch.cuda.synchronize()
     y_ref = R.rollout(y0, u, arm[:, :T], coef, lib.exps.astype(np.int64), dt, method=method, substeps=sub)
-    yg = y.cpu().numpy()
+    yg = _as_patient_major(y, layout)
     rmse = np.sqrt(np.mean((yg - y_ref) ** 2))
     assert rmse <= RMSE_TOL
     np.testing.assert_allclose(yg, y_ref, rtol=1e-11, atol=1e-12)
+
+
+def test_rollout_time_major_out_padding_untouched(dev):
+    """Time-major output with ld_y > N: the padding columns and the rows beyond T stay untouched
+    (the last wavefront's inactive lanes must not store)."""
+    from insite_amd import ops
+    rng = np.random.default_rng(11)
+    N, T = 300, 17
+    lib, y0, u, arm, coef = _random_rollout_case(rng, N, T)
+    out = torch.full((T + 2, N + 5), 7.0, dtype=torch.float64, device=dev)
+    ops.rollout(_t(y0, dev), _t(u, dev), _arm_layout(arm, T, "time4", dev), _t(coef, dev), lib, 0.1,
+                method="rk4", T=T, out=out[:T], layout="time")
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    assert np.all(o[:, N:] == 7.0) and np.all(o[T:] == 7.0)
+    y_ref = R.rollout(y0, u, arm, coef, lib.exps.astype(np.int64), 0.1, method="rk4")
+    np.testing.assert_allclose(o[:T, :N].T, y_ref, rtol=1e-11, atol=1e-12)
 
 
 def test_rollout_known_answer_y_equals_t(dev):
@@ -190,12 +245,14 @@ def test_rollout_known_answer_y_equals_t(dev):
         assert np.mean((y.cpu().numpy() - t[None]) ** 2) < 1e-16
 
 
-def test_rollout_deterministic_and_large_property(dev):
+@pytest.mark.parametrize("layout", ["patient", "time", "time4"])
+def test_rollout_deterministic_and_large_property(dev, layout):
     """Size-independent properties at a large size: bitwise repeatability, exact agreement of a
-    sampled row subset with the oracle, and the closed form of the linear ODE under RK4."""
+    sampled row subset with the oracle, and the closed form of the linear ODE under RK4.
+    N > 256k exercises the two-patients-per-lane time-major kernel."""
     from insite_amd import ops
     rng = np.random.default_rng(5)
-    N, T = 200_003, 500
+    N, T = 200_003 if layout == "patient" else 300_002, 500
     lib = _lib()
     F = lib.n_terms
     coef = np.zeros((2, F))
@@ -205,13 +262,23 @@ def test_rollout_deterministic_and_large_property(dev):
     u = torch.rand(N, 2, device=dev, dtype=torch.float64) * 0.2 + 0.4
     flip = torch.randint(0, T, (N, 1), device=dev)
     arm = (torch.arange(T, device=dev)[None, :] >= flip).to(torch.int8)
+    if layout == "patient":
+        arm_in = arm
+    else:
+        ld = N + 1 if layout == "time" else (N + 3) // 4 * 4
+        arm_in = torch.zeros((T, ld), dtype=torch.int8, device=dev)
+        arm_in[:, :N] = arm.t()
+    lay = "patient" if layout == "patient" else "time"
     c = _t(coef, dev)
     dt = R.MAX_TIME_HORIZON / T
-    y1 = ops.rollout(y0, u, arm, c, lib, dt, method="rk4")
-    y2 = ops.rollout(y0, u, arm, c, lib, dt, method="rk4")
+    y1 = ops.rollout(y0, u, arm_in, c, lib, dt, method="rk4", layout=lay)
+    y2 = ops.rollout(y0, u, arm_in, c, lib, dt, method="rk4", layout=lay)
     torch.cuda.synchronize()
     assert torch.equal(y1, y2)
+    if lay == "time":
+        y1 = y1.t()
     idx = np.sort(rng.choice(N, 2000, replace=False))
+    idx[-1] = N - 1
     y_ref = R.rollout(y0.cpu().numpy()[idx], u.cpu().numpy()[idx], arm.cpu().numpy()[idx], coef,
                       lib.exps.astype(np.int64), dt, method="rk4")
     np.testing.assert_allclose(y1.cpu().numpy()[idx], y_ref, rtol=1e-11, atol=1e-12)
@@ -241,3 +308,24 @@ def test_masked_sse_matches_numpy(dev):
     lw = active - np.concatenate([active[:, 1:], np.zeros((N, 1))], axis=1)
     np.testing.assert_allclose(last.cpu().numpy(), [(((pred[:, :T] * 2 + 0.5 - target) ** 2) * lw).sum(), lw.sum()],
                                rtol=1e-12)
+
+
+@pytest.mark.parametrize("eq,T", [("EQ_4_A", 60), ("EQ_4_C", 60), ("EQ_4_D", 200)])
+def test_sindy_fit_fused_matches_oracle(dev, eq, T):
+    """insite_sindy_fit_f64 (Gram + fused STLSQ) == gram + stlsq == oracle (support, L-inf < 1e-8)."""
+    from insite_amd import ops
+    x, u, arm, rows = _cohort(eq, 700, T, seed=2)
+    lib = _lib()
+    dt = R.MAX_TIME_HORIZON / T
+    args = (_t(x, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), dt, lib)
+    coef, mask, iters, G, b = ops.sindy_fit(*args, 0.1, 0.5)
+    G2, b2 = ops.gram(*args)
+    coef2, mask2, _ = ops.stlsq(G2, b2, 0.1, 0.5)
+    torch.cuda.synchronize()
+    assert torch.equal(G, G2) and torch.equal(b, b2)
+    assert torch.equal(coef, coef2) and torch.equal(mask, mask2)
+    X, U = R.de_lists(x, u, arm, rows)
+    for a in range(2):
+        c_ref, ind_ref, _, _ = R.sindy_fit(X[a], U[a], dt, 0.1, 0.5)
+        assert np.array_equal(mask.cpu().numpy()[a] != 0, ind_ref)
+        assert np.max(np.abs(coef.cpu().numpy()[a] - c_ref)) < COEF_TOL

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Profiling-only ablation / tuning builds of libinsite_hip.so (never used by product code paths).
+set -e
+R="$(cd "$(dirname "$0")/.." && pwd)"
+P="$R/ode-discovery-for-longitudinal-heterogeneous-treatment-effects-inference_amd"
+rm -rf "$P/lib/ablate"; mkdir -p "$P/lib/ablate"
+build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC "$@" -I "$R/include" -o "$P/lib/ablate/libinsite_hip_$NAME.so" "$P/csrc/insite_hip.hip"; }
+for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
+  case $v in
+    NOSTORE) NAME=$v build -DINSITE_ABLATE_NOSTORE ;;
+    NOARM) NAME=$v build -DINSITE_ABLATE_NOARM ;;
+    RT16) NAME=$v build -DINSITE_RT=16 ;;
+    RT64) NAME=$v build -DINSITE_RT=64 ;;
+    NOGPHASE) NAME=$v build -DINSITE_ABLATE_NOGPHASE ;;
+    GT32) NAME=$v build -DINSITE_GT=32 ;;
+  esac
+done

@@ -12,7 +12,7 @@ rc=$?
 echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 cd /tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o bench --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o bench --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-north-star > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
 rc=$?
 echo "rocprof rc=$rc"
 exit $rc
