@@ -41,6 +41,10 @@ def parse():
     ap.add_argument("--T", type=int, default=200)
     ap.add_argument("--method", default="rk4", choices=["rk4", "euler5"])
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--layout", default="time", choices=["time", "patient"],
+                    help="HBM layout of the per-step arrays (DESIGN.md): time-major is the fast path")
+    ap.add_argument("--arm-format", default="bits", choices=["bits", "int8"],
+                    help="per-step arms of the time-major rollout: 1-bit mask (A <= 2) or int8")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
@@ -49,14 +53,16 @@ def parse():
     return ap.parse_args()
 
 
-def rollout_bytes(N, T, U=2, w=8):
+def rollout_bytes(N, T, U=2, w=8, arm_bits=8):
     """Algorithmic HBM bytes of one rollout launch:
-    N*T*(S*w + 1) [state out + int8 arm in] + N*(S*w + U*w) [y0 + statics in]."""
-    return N * T * (w + 1) + N * (w + U * w)
+    N*T*(S*w + arm_bits/8) [state out + per-step arm in: int8 = 8 bits, packed = 1 bit]
+    + N*(S*w + U*w) [y0 + statics in]."""
+    return N * T * w + (N * T * arm_bits + 7) // 8 + N * (w + U * w)
 
 
 def gram_bytes(N, L, U=2, w=8):
-    """Algorithmic HBM bytes of one discovery (Gram) launch: N*L*w rows + N*(U*w + 1 + 4)."""
+    """Algorithmic HBM bytes of one discovery pass: the L = T observations of every patient
+    (x[p, 0..L-1] feed the L-1 rows' smoothing stencils) + statics, arm byte and row count."""
     return N * L * w + N * (U * w + 1 + 4)
 
 
@@ -105,40 +111,39 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from insite_amd import ops, cohort
+    from insite_amd import dist as idist
 
     N, T = args.patients, args.T
-    coh = cohort.synthetic_pkpd(N, T, seed=args.seed * 1000 + rank, device=dev, equation="EQ_4_C")
-    arm_cf = cohort.counterfactual_arms(coh.arm, T, seed=args.seed * 1000 + rank)
+    coh = cohort.synthetic_pkpd(N, T, seed=args.seed * 1000 + rank, device=dev, equation="EQ_4_C",
+                                layout=args.layout)
+    # time-major arm sequences / trajectories: one contiguous run per step ("HBM layout")
+    roll_layout = "time_bits" if (args.layout == "time" and args.arm_format == "bits") else args.layout
+    arm_cf = cohort.counterfactual_arms(coh.arm, T, seed=args.seed * 1000 + rank, layout=roll_layout)
     lib = coh.lib
     F = lib.n_terms
-    y0 = coh.x[:, 0].contiguous()
-    GB = torch.empty(2 * F * F + 2 * F, dtype=torch.float64, device=dev)   # one all-reduce buffer
-    G = GB[: 2 * F * F].view(2, F, F)
-    b = GB[2 * F * F:].view(2, F)
+    y0 = coh.y0
+    buf = idist.MomentBuffer(2, F, dev)          # G|b in one buffer: one all-reduce when N > 1
     coef = torch.empty((2, F), dtype=torch.float64, device=dev)
     mask = torch.empty((2, F), dtype=torch.int8, device=dev)
     iters = torch.empty((2,), dtype=torch.int32, device=dev)
-    y = torch.empty((N, T), dtype=torch.float64, device=dev)
+    y = torch.empty((T, N) if args.layout == "time" else (N, T), dtype=torch.float64, device=dev)
     ws = ops.Workspace()
     stream = torch.cuda.current_stream(dev)
-    ev = []
+    ev_roll, ev_disc = [], []
 
     def step(record=False):
-        if world == 1:   # Gram kernel + fused reduction/STLSQ (2 launches)
-            ops.sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, 100, True, 2, "smoothed4", ws,
-                          out=(coef, mask, iters, G, b))
-        else:            # per-rank Gram, one RCCL all-reduce of G|b, replicated STLSQ
-            ops.gram(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 2, "smoothed4", ws, out=(G, b))
-            dist.all_reduce(GB, op=dist.ReduceOp.SUM)
-            ops.stlsq(G, b, 0.1, 0.5, 100, True, out=(coef, mask, iters))
         if record:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        ops.rollout(y0, coh.u, arm_cf, coef, lib, coh.dt, method=args.method, T=T, out=y)
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record(stream)
+        idist.discover_sharded(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, buf, workspace=ws,
+                               out=(coef, mask, iters), layout=args.layout)
         if record:
-            e1.record(stream)
-            ev.append((e0, e1))
+            e[1].record(stream)
+        ops.rollout(y0, coh.u, arm_cf, coef, lib, coh.dt, method=args.method, T=T, out=y, layout=roll_layout)
+        if record:
+            e[2].record(stream)
+            ev_disc.append((e[0], e[1]))
+            ev_roll.append((e[1], e[2]))
 
     for _ in range(args.warmup):
         step()
@@ -152,13 +157,10 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
+    el = idist.max_over_ranks(time.perf_counter() - t0, dev)
     ms_step = el / args.steps * 1e3
-    roll_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ev]))
+    roll_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ev_roll]))
+    disc_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ev_disc]))
 
     # sanity on the measured result: discovered support is the EQ_4_C one, no NaN
     sup = mask.cpu().numpy()
@@ -166,7 +168,8 @@ def main():
 
     out = None
     if rank == 0:
-        rb = rollout_bytes(N, T)
+        arm_bits = 1 if roll_layout == "time_bits" else 8
+        rb = rollout_bytes(N, T, arm_bits=arm_bits)
         achieved = rb / (roll_ms * 1e-3) / 1e9
         traffic = None
         if os.path.exists(args.traffic_json):
@@ -206,6 +209,17 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": rb,
                 "avg_launch_ms": roll_ms,
+                "layout": {"time_bits": "time-major x[T,N], 1-bit arm mask [T,N/32], y[T,N]",
+                           "time": "time-major x[T,N], int8 arm[T,N], y[T,N]",
+                           "patient": "patient-major x[N,T], int8 arm[N,T], y[N,T]"}[roll_layout],
+            },
+            "discovery": {
+                "kernels": "gram_kernel + discovery_finalize (fused STLSQ)" if world == 1
+                           else "gram_kernel + RCCL all_reduce + stlsq_kernel",
+                "avg_ms": disc_ms,
+                "algorithmic_bytes": gram_bytes(N, T),
+                "achieved_GBps": gram_bytes(N, T) / (disc_ms * 1e-3) / 1e9,
+                "frac": gram_bytes(N, T) / (disc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
             },
         }
     # north-star probe: 1M x 500 RK4 rollout alone (the >= 40 % roofline target), rank 0, N = 1
@@ -218,22 +232,26 @@ def main():
         y0n = torch.rand(Nn, generator=g, device=dev, dtype=torch.float64) * 49 + 1
         un = torch.rand((Nn, 2), generator=g, device=dev, dtype=torch.float64) * 0.1 + 0.45
         flip = torch.randint(0, Tn, (Nn, 1), generator=g, device=dev)
-        armn = (torch.arange(Tn, device=dev)[None, :] >= flip).to(torch.int8).contiguous()
-        yn = torch.empty((Nn, Tn), dtype=torch.float64, device=dev)
+        armn = torch.zeros((Tn, Nn), dtype=torch.int8, device=dev)
+        armn[:] = (torch.arange(Tn, device=dev)[:, None] >= flip[:, 0][None, :]).to(torch.int8)
+        nlay = "time_bits" if args.arm_format == "bits" else "time"
+        if nlay == "time_bits":
+            armn = ops.pack_arm_bits(armn, Nn)
+        yn = torch.empty((Tn, Nn), dtype=torch.float64, device=dev)
         for _ in range(3):
-            ops.rollout(y0n, un, armn, coef, lib, 10.0 / Tn, method="rk4", out=yn)
+            ops.rollout(y0n, un, armn, coef, lib, 10.0 / Tn, method="rk4", out=yn, layout=nlay)
         evs = []
         for _ in range(10):
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            ops.rollout(y0n, un, armn, coef, lib, 10.0 / Tn, method="rk4", out=yn)
+            ops.rollout(y0n, un, armn, coef, lib, 10.0 / Tn, method="rk4", out=yn, layout=nlay)
             e1.record(stream)
             evs.append((e0, e1))
         torch.cuda.synchronize(dev)
         ms = float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))
-        bn = rollout_bytes(Nn, Tn)
-        out["north_star_rollout"] = {"patients": Nn, "T": Tn, "method": "rk4", "avg_launch_ms": ms,
+        bn = rollout_bytes(Nn, Tn, arm_bits=1 if nlay == "time_bits" else 8)
+        out["north_star_rollout"] = {"patients": Nn, "T": Tn, "method": "rk4", "layout": nlay, "avg_launch_ms": ms,
                                      "algorithmic_bytes": bn, "achieved_GBps": bn / (ms * 1e-3) / 1e9,
                                      "frac_of_8TBps": bn / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                                      "patient_trajectories_per_s": Nn / (ms * 1e-3)}

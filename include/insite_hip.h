@@ -68,9 +68,13 @@ extern "C" {
 
 /* storage layouts of per-step matrices (arm, y): element (patient r, step k) at
  *   PATIENT_MAJOR: a[r * ld + k]   (the reference's [N, T] arrays; ld >= T)
- *   TIME_MAJOR:    a[k * ld + r]   (ld >= n_rows; every step of a wavefront is one contiguous run) */
+ *   TIME_MAJOR:    a[k * ld + r]   (ld >= n_rows; every step of a wavefront is one contiguous run)
+ *   TIME_MAJOR_BITS (rollout only, n_arms <= 2): y as TIME_MAJOR; the arms are a bitmask,
+ *                  arm of (r, k) = bit (r & 31) of ((const uint32_t*)arm)[k * ld_arm + (r >> 5)],
+ *                  ld_arm in 32-bit words >= ceil(n_rows / 32), arm 4-byte aligned            */
 #define INSITE_LAYOUT_PATIENT_MAJOR 0
 #define INSITE_LAYOUT_TIME_MAJOR 1
+#define INSITE_LAYOUT_TIME_MAJOR_BITS 2
 
 /* limits of this ABI version */
 #define INSITE_MAX_TERMS 9  /* F: one Gram/moment entry per wavefront lane (F(F+1)/2 + F <= 64) */
@@ -89,20 +93,22 @@ int32_t insite_poly_library(int32_t n_statics, int32_t degree, int32_t interacti
 
 /* Fused discovery pass (smoothing + finite differences + library + Gram), replacing the
  * row materialisation and Theta^T Theta of SINDy.fit.  For every patient p with
- * L = rows[p] >= 5 observation rows x[p, 0..L-1] and training arm a = arm[p]:
+ * L = min(rows[p], n_steps) >= 5 observation rows x[p, 0..L-1] and training arm a = arm[p]:
  *     G_out[a] += Theta_p^T Theta_p,   b_out[a] += Theta_p^T xdot_p
  * where Theta_p[k, j] = column j evaluated at (xs[k], u[p, :]) and xs = x (or the savgol
  * 5/3-smoothed x for INSITE_FD_SMOOTHED4).  Patients with L < 5 contribute nothing
  * (pysindy raises; the caller validates).  Deterministic: fixed-order reductions.
- *   x     [n_patients, ldx] f64   (ldx >= max rows; columns >= rows[p] are never used)
+ *   x     f64, `layout` (INSITE_LAYOUT_*) with n_steps stored steps:
+ *           PATIENT_MAJOR x[p * ldx + k], ldx >= n_steps  (the reference's [N, T] array)
+ *           TIME_MAJOR    x[k * ldx + p], ldx >= n_patients (coalesced streaming)
  *   u     [n_patients, n_statics] f64
  *   arm   [n_patients] int8 in [0, n_arms)
  *   rows  [n_patients] int32
  *   G_out [n_arms, F, F] f64 (overwritten), b_out [n_arms, F] f64 (overwritten)       */
 size_t insite_gram_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms);
-int32_t insite_gram_f64(const double* x, int64_t ldx, const double* u, const int8_t* arm,
-                        const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
-                        const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
+int32_t insite_gram_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,
+                        const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics,
+                        int32_t n_arms, const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
                         double* G_out, double* b_out, void* workspace, size_t workspace_bytes,
                         void* stream);
 
@@ -111,9 +117,9 @@ int32_t insite_gram_f64(const double* x, int64_t ldx, const double* u, const int
  *   coef_out [n_arms, F] f64, mask_out [n_arms, F] int8 (may be NULL),
  *   iters_out [n_arms] int32 (may be NULL; -1 flags a non-positive-definite solve).
  *   G_out / b_out receive the Gram/moment sums as in insite_gram_f64.                     */
-int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, const double* u, const int8_t* arm,
-                             const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
-                             const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
+int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,
+                             const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics,
+                             int32_t n_arms, const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
                              double threshold, double alpha, int32_t max_iter, int32_t unbias,
                              double* G_out, double* b_out, double* coef_out, int8_t* mask_out,
                              int32_t* iters_out, void* workspace, size_t workspace_bytes, void* stream);

@@ -165,11 +165,11 @@ __device__ __forceinline__ void add_row(double xk, double dk, double& Sx, double
 // Whole-trajectory moments for short smoothed trajectories (5 <= LL <= 7 rows), every stencil
 // position resolved at compile time.
 template <int LL>
-__device__ void small_trajectory(const double* __restrict__ xrow, const GramW& w, double& Sx, double& Sxx,
-                                 double& Sd, double& Sdx) {
+__device__ void small_trajectory(const double* __restrict__ xrow, int64_t step, const GramW& w, double& Sx,
+                                 double& Sxx, double& Sd, double& Sdx) {
   double xv[LL], xs[LL];
 #pragma unroll
-  for (int j = 0; j < LL; ++j) xv[j] = xrow[j];
+  for (int j = 0; j < LL; ++j) xv[j] = xrow[j * step];
 #pragma unroll
   for (int k = 0; k < LL; ++k) {
     if (k == 0) xs[k] = sg_pos0(xv[0], xv[1], xv[2], xv[3], xv[4]);
@@ -217,9 +217,11 @@ __device__ __forceinline__ void tele_lo(const GramW& w, double vm2, double vm1, 
 // (the segment holding step L-1) per patient, 2 + 2 without smoothing.  Moments are additive over
 // segments; each work item adds its A(u) M A(u)^T contribution, as a 16x16x64 f64 MFMA product
 // when the library fits (lib.mfma), else one Gram entry per lane.
-template <int VEC, int NARM, bool SMOOTH, bool MFMA>
+// TM (time-major x[k * ldx + p]): a lane loads its own patient's kGT samples of a tile directly
+// (each wave instruction reads 64 consecutive doubles of one step); no LDS staging or wave sync.
+template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM>
 __global__ void __launch_bounds__(kBlock)
-gram_kernel(const double* __restrict__ x, int64_t ldx, const double* __restrict__ u,
+gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
             const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, int seg, int n_seg,
             GramW w, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ ticket) {
   __shared__ double smem[kWavesPerBlock * kWave * kGStride];
@@ -232,6 +234,7 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, const double* __restrict_
   constexpr int LPR = kGT / VEC;            // lanes per row segment
   constexpr int RPI = kWave / LPR;          // rows per wave instruction
   constexpr int NLD = kWave / RPI;          // load instructions per tile
+  static_assert(!TM || (VEC == 1 && NLD == kGT), "time-major tiles hold the lane's own kGT samples");
   if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0u;  // consumed by discovery_finalize (next launch)
 
   // G-phase accumulators
@@ -276,7 +279,7 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, const double* __restrict_
       if (p < N) {
         L = Lr;
         arm_p = ar;
-        if (L > ldx) L = (int)ldx;
+        if (L > n_steps) L = n_steps;  // stored steps (host: n_steps <= ldx when patient-major)
         if (L < 5) L = 0;  // too short for the 5-point stencils: contributes nothing
       }
     }
@@ -296,6 +299,16 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, const double* __restrict_
       // Loads are issued unconditionally from a clamped (always valid) address and masked after
       // the fact: exec-masked loads would make the compiler drain vmcnt(0) at every tile.
       auto load_tile = [&](TileRegs& v, int t0) {
+        if constexpr (TM) {
+          const int64_t pc = p < N ? p : N - 1;
+#pragma unroll
+          for (int i = 0; i < kGT; ++i) {
+            const bool ok = t0 + i < s1 && p < N;
+            const double q = x[(int64_t)(ok ? t0 + i : 0) * ldx + pc];
+            v[i][0] = ok ? q : 0.0;
+          }
+          return;
+        }
         const int col = t0 + cl;
         const bool col_ok = col < s1;
         const int colc = col_ok ? col : 0;
@@ -315,6 +328,7 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, const double* __restrict_
         }
       };
       auto store_tile = [&](const TileRegs& v) {
+        if constexpr (TM) return;
         wave_lds_sync();  // every lane finished reading the previous tile
 #pragma unroll
         for (int it = 0; it < NLD; ++it) {
@@ -338,30 +352,44 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, const double* __restrict_
       auto issue_tail = [&]() {
         if (tail_issued) return;
         tail_issued = true;
-        const double* xe = x + (need_end ? p * ldx + (e - NQ) : 0);  // ldx >= L >= NQ: valid either way
+        // valid either way: e >= NQ when need_end, and the patient-major ldx >= L >= NQ
+        const int64_t pc = p < N ? p : N - 1;
+        const double* xe = TM ? x + (need_end ? (int64_t)(e - NQ) * ldx + pc : pc)
+                              : x + (need_end ? p * ldx + (e - NQ) : 0);
+        const int64_t st = TM ? (need_end ? ldx : 0) : 1;
 #pragma unroll
         for (int j = 0; j < NQ; ++j) {
-          const double q = xe[j];
+          const double q = xe[j * st];
           qe[j] = need_end ? q : 0.0;
         }
       };
 
       // ---- first tile: steps [tb, tb+16): warm-up, a-side terms, head rows, body ----
       const int tb = (sidx == 0) ? 0 : s0 - kWarm;
+      // sample i of the tile being consumed: LDS (patient-major) or the lane's own registers
+      auto sample = [&](const TileRegs& v, int i) -> double {
+        if constexpr (TM) return v[i][0];
+        else return xt[lane * kGStride + i];
+      };
       load_tile(vA, tb);
       store_tile(vA);
-      if (tb + kGT < s1) load_tile(vA, tb + kGT);
-      if constexpr (kGPF == 2) {
-        if (tb + 2 * kGT < s1) load_tile(vB, tb + 2 * kGT);
+      if constexpr (TM) {
+        if (tb + kGT < s1) load_tile(vB, tb + kGT);
         else issue_tail();
       } else {
-        if (tb + kGT >= s1) issue_tail();
+        if (tb + kGT < s1) load_tile(vA, tb + kGT);
+        if constexpr (kGPF == 2) {
+          if (tb + 2 * kGT < s1) load_tile(vB, tb + 2 * kGT);
+          else issue_tail();
+        } else {
+          if (tb + kGT >= s1) issue_tail();
+        }
       }
       {
         const bool masked = tb + kGT > Lmin;
 #pragma unroll
         for (int i = 0; i < kGT; ++i) {
-          xr[i & 7] = xt[lane * kGStride + i];
+          xr[i & 7] = sample(vA, i);
           const int t = tb + i;
           if constexpr (SMOOTH) {
             if (i >= 4) sr[(i - 2) & 7] = sg_int(w, xr[(i - 4) & 7], xr[(i - 3) & 7], xr[(i - 2) & 7], xr[(i - 1) & 7], xr[i & 7]);
@@ -406,11 +434,11 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, const double* __restrict_
         }
       }
       // ---- remaining tiles of the segment (buffers alternate A, B; two tiles in flight) ----
-      auto consume = [&](int t0) {
+      auto consume = [&](int t0, const TileRegs& v) {
         if (t0 + kGT <= Lmin) {
 #pragma unroll
           for (int i = 0; i < kGT; ++i) {
-            xr[i & 7] = xt[lane * kGStride + i];
+            xr[i & 7] = sample(v, i);
             double xk;
             if constexpr (SMOOTH) {
               sr[(i - 2) & 7] = sg_int(w, xr[(i - 4) & 7], xr[(i - 3) & 7], xr[(i - 2) & 7], xr[(i - 1) & 7], xr[i & 7]);
@@ -425,7 +453,7 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, const double* __restrict_
 #pragma unroll
           for (int i = 0; i < kGT; ++i) {
             if (t0 + i < s1) {
-              xr[i & 7] = xt[lane * kGStride + i];
+              xr[i & 7] = sample(v, i);
               double xk;
               if constexpr (SMOOTH) {
                 sr[(i - 2) & 7] = sg_int(w, xr[(i - 4) & 7], xr[(i - 3) & 7], xr[(i - 2) & 7], xr[(i - 1) & 7], xr[i & 7]);
@@ -440,18 +468,34 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, const double* __restrict_
           }
         }
       };
-      if constexpr (kGPF == 2) {
+      if constexpr (TM) {
+        // vA is free after the first tile; vB holds tile tb + kGT.  Refill each buffer right
+        // after it is consumed (one tile in flight during a consume).
+        if (tb + 2 * kGT < s1) load_tile(vA, tb + 2 * kGT);
+        else issue_tail();
+        for (int t0 = tb + kGT; t0 < s1;) {
+          consume(t0, vB);
+          if (t0 + 2 * kGT < s1) load_tile(vB, t0 + 2 * kGT);
+          else issue_tail();
+          t0 += kGT;
+          if (t0 >= s1) break;
+          consume(t0, vA);
+          if (t0 + 2 * kGT < s1) load_tile(vA, t0 + 2 * kGT);
+          else issue_tail();
+          t0 += kGT;
+        }
+      } else if constexpr (kGPF == 2) {
         for (int t0 = tb + kGT; t0 < s1;) {
           store_tile(vA);
           if (t0 + 2 * kGT < s1) load_tile(vA, t0 + 2 * kGT);
           else issue_tail();
-          consume(t0);
+          consume(t0, vA);
           t0 += kGT;
           if (t0 >= s1) break;
           store_tile(vB);
           if (t0 + 2 * kGT < s1) load_tile(vB, t0 + 2 * kGT);
           else issue_tail();
-          consume(t0);
+          consume(t0, vB);
           t0 += kGT;
         }
       } else {
@@ -459,7 +503,7 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, const double* __restrict_
           store_tile(vA);
           if (t0 + kGT < s1) load_tile(vA, t0 + kGT);
           else issue_tail();
-          consume(t0);
+          consume(t0, vA);
         }
       }
       // ---- b-side telescoped terms and tail rows from the prefetched end samples ----
@@ -502,10 +546,11 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, const double* __restrict_
     }
     if constexpr (SMOOTH) {
       if (sidx == 0 && L > 0 && L < kMinMain) {
-        const double* xrow = x + p * ldx;
-        if (L == 5) small_trajectory<5>(xrow, w, Sx, Sxx, Sd, Sdx);
-        else if (L == 6) small_trajectory<6>(xrow, w, Sx, Sxx, Sd, Sdx);
-        else small_trajectory<7>(xrow, w, Sx, Sxx, Sd, Sdx);
+        const double* xrow = TM ? x + p : x + p * ldx;
+        const int64_t st = TM ? ldx : 1;
+        if (L == 5) small_trajectory<5>(xrow, st, w, Sx, Sxx, Sd, Sdx);
+        else if (L == 6) small_trajectory<6>(xrow, st, w, Sx, Sxx, Sd, Sdx);
+        else small_trajectory<7>(xrow, st, w, Sx, Sxx, Sd, Sdx);
       }
     }
     if (s0 >= Lmax && !(SMOOTH && sidx == 0)) continue;  // nothing owned by this work item (uniform)
@@ -1001,10 +1046,19 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(RolloutArgs ra, LibDesc
 #define INSITE_TG 16
 #endif
 constexpr int kTG = INSITE_TG;  // steps per group = arm prefetch distance
+#ifndef INSITE_STORE_AUX
+#define INSITE_STORE_AUX 0
+#endif
+constexpr int kStoreAux = INSITE_STORE_AUX;  // cache-policy bits of the trajectory stores (tuning)
 constexpr int64_t kTmMaxLd = ((int64_t)1 << 31) / (8 * kTG);  // group offsets stay below 2^31
 
-template <int METHOD, int NARM, bool PERROW, int PPL, bool AW4>
+// AFMT: kArmByte (one int8 per lane), kArmDword (the aligned dword holding the lane's PPL int8
+// arms), kArmBits (time-major bitmask, n_arms <= 2: bit r & 31 of word r >> 5 of the step row).
+constexpr int kArmByte = 0, kArmDword = 1, kArmBits = 2;
+
+template <int METHOD, int NARM, bool PERROW, int PPL, int AFMT>
 __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibDesc lib) {
+  constexpr bool AW4 = AFMT != kArmByte;  // 32-bit ring elements
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform (SGPR)
   const int64_t p0 = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * (kWave * PPL);
@@ -1054,15 +1108,23 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
   // elements get packed by the compiler, which then waits for every prefetched load at the loop
   // latch.  Requires ld_arm % 4 == 0 and a 4-byte aligned base, so the last row's dword stays
   // inside the allocation; otherwise (AW4 = false) plain byte loads are used.
-  using ArmT = std::conditional_t<AW4, uint32_t, std::conditional_t<PPL == 2, uint16_t, uint8_t>>;
-  const unsigned abyte = (unsigned)(PPL * lane);
-  const unsigned aoff = AW4 ? (abyte & ~3u) : abyte;
-  const unsigned ashift = AW4 ? 8u * (abyte & 3u) : 0u;
-  const int arec_tail = AW4 ? ((nvalid + 3) & ~3) : nvalid;  // arm bytes of the last row
+  static_assert(AW4 || PPL == 1, "several patients per lane need dword arm loads");
+  using ArmT = std::conditional_t<AW4, uint32_t, uint8_t>;
+  const unsigned abyte = (unsigned)(PPL * lane);  // the lane's first patient, relative to p0
+  // byte offset of the lane's arm word within a step row (relative to the wave's base) and the
+  // shift that brings its first patient's arm to bit 0
+  const unsigned aoff = AFMT == kArmBits ? (abyte >> 5) * 4u : (AW4 ? (abyte & ~3u) : abyte);
+  const unsigned ashift = AFMT == kArmBits ? (abyte & 31u) : (AW4 ? 8u * (abyte & 3u) : 0u);
+  constexpr unsigned kArmStride = AFMT == kArmBits ? 1u : 8u;  // bit distance between lane patients
+  constexpr unsigned kArmMask = AFMT == kArmBits ? 1u : 0xffu;
+  // row stride and wave base in bytes (bit rows: lda counts 32-bit words; p0 is a multiple of 64)
+  const int64_t arow = AFMT == kArmBits ? ra.lda * 4 : ra.lda;
+  const int64_t abase = AFMT == kArmBits ? (p0 >> 5) * 4 : p0;
+  const int arec_tail = AFMT == kArmBits ? ((nvalid + 31) >> 5) * 4 : (AW4 ? ((nvalid + 3) & ~3) : nvalid);
   auto arm_rsrc = [&](int k0) {
     const int rows = ra.T - k0 < kTG ? ra.T - k0 : kTG;
-    const int bytes = rows > 0 ? (int)((int64_t)(rows - 1) * ra.lda + arec_tail) : 0;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(ra.arm + (int64_t)(rows > 0 ? k0 : 0) * ra.lda + p0), (short)0,
+    const int bytes = rows > 0 ? (int)((int64_t)(rows - 1) * arow + arec_tail) : 0;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(ra.arm + (int64_t)(rows > 0 ? k0 : 0) * arow + abase), (short)0,
                                              bytes, 0x00020000);
   };
   auto y_rsrc = [&](int k0) {
@@ -1071,9 +1133,11 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
                                              (int)(((int64_t)(rows - 1) * ra.ldy + nvalid) * 8), 0x00020000);
   };
   auto load_arm = [&](__amdgpu_buffer_rsrc_t rs, int i) -> ArmT {  // step i of a group
-    const unsigned off = aoff + (unsigned)(i * ra.lda);
+#ifdef INSITE_ABLATE_NOARM
+    return (ArmT)(i & 1);
+#endif
+    const unsigned off = aoff + (unsigned)(i * arow);
     if constexpr (AW4) return __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
-    else if constexpr (PPL == 2) return (ArmT)__builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0);
     else return (ArmT)__builtin_amdgcn_raw_buffer_load_b8(rs, off, 0, 0);
   };
   auto step = [&](int q, int a) {
@@ -1117,17 +1181,29 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
       // slot needs two registers and the latch copy waits for the load
       asm volatile("" ::"v"(a2) : "memory");
       ring[i] = load_arm(rsn, i);
+#ifndef INSITE_ABLATE_NOCOMPUTE
 #pragma unroll
-      for (int q = 0; q < PPL; ++q) step(q, (int)((a2 >> (8 * q)) & 0xffu));
+      for (int q = 0; q < PPL; ++q) step(q, (int)((a2 >> (kArmStride * q)) & kArmMask));
+#else
+#pragma unroll
+      for (int q = 0; q < PPL; ++q) y[q] += (double)((a2 >> (kArmStride * q)) & kArmMask);
+#endif
       const unsigned off = yoff + (unsigned)(i * ra.ldy * 8);
-      if constexpr (PPL == 2) {
-        // a pair with an inactive second patient only occurs at the very end of the cohort;
-        // both halves are clipped by num_records there (column >= nvalid lies beyond the row)
-        const double2 v = make_double2(y[0], y[1]);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ys, off, 0, 0);
+#ifndef INSITE_ABLATE_NOSTORE
+      if constexpr (PPL >= 2) {
+        // groups of PPL patients are whole (the launcher requires N % PPL == 0); the last row's
+        // columns >= nvalid are clipped by num_records
+#pragma unroll
+        for (int q2 = 0; q2 < PPL / 2; ++q2) {
+          const double2 v = make_double2(y[2 * q2], y[2 * q2 + 1]);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ys, off + 16u * q2, 0, kStoreAux);
+        }
       } else {
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y[0]), ys, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y[0]), ys, off, 0, kStoreAux);
       }
+#else
+      if (y[0] == 12345.678) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y[0]), ys, off, 0, 0);
+#endif
     }
   }
 }
@@ -1304,17 +1380,18 @@ int resident_waves(K kernel) {
 // Work decomposition: 64-patient tiles x time segments.  Segments add parallelism for small
 // cohorts, but every work item pays a warm-up and a Gram contraction, and a second partial round
 // of items leaves the chip under-occupied, so the item count is sized to one resident round.
-inline GramPlan gram_plan(int64_t N, int64_t ldx, int resident) {
+inline GramPlan gram_plan(int64_t N, int64_t n_steps, int resident) {
   GramPlan pl;
   const int64_t tiles = (N + kWave - 1) / kWave;
+  const int64_t T = n_steps > 0 ? n_steps : 1;
   int64_t ns = tiles > 0 ? resident / tiles : 1;
-  const int64_t ns_max = ldx / 48 > 1 ? ldx / 48 : 1;
+  const int64_t ns_max = T / 48 > 1 ? T / 48 : 1;
   if (ns > ns_max) ns = ns_max;
   if (ns < 1) ns = 1;
-  int64_t seg = (ldx + ns - 1) / ns;
+  int64_t seg = (T + ns - 1) / ns;
   seg = (seg + kGT - 1) / kGT * kGT;
   pl.seg = (int)seg;
-  pl.n_seg = (int)((ldx + seg - 1) / seg);
+  pl.n_seg = (int)((T + seg - 1) / seg);
   int64_t g = (tiles * pl.n_seg + kWavesPerBlock - 1) / kWavesPerBlock;
   const int64_t gres = resident / kWavesPerBlock > 0 ? resident / kWavesPerBlock : 1;
   if (g > gres) g = gres;
@@ -1335,44 +1412,54 @@ inline int sse_grid(int64_t n_rows) {
 
 inline int32_t launch_status() { return hipGetLastError() == hipSuccess ? INSITE_OK : INSITE_E_HIP; }
 
-template <int VEC, int NARM, bool SMOOTH, bool MFMA>
-void launch_gram3(hipStream_t st, const double* x, int64_t ldx, const double* u, const int8_t* arm,
-                  const int32_t* rows, int64_t N, const GramW& w, const LibDesc& lib, double* part,
-                  unsigned* ticket, int* grid_out) {
-  auto kern = gram_kernel<VEC, NARM, SMOOTH, MFMA>;
-  const GramPlan pl = gram_plan(N, ldx, resident_waves(kern));
-  *grid_out = pl.grid;
-  kern<<<dim3(pl.grid), kBlock, 0, st>>>(x, ldx, u, arm, rows, N, pl.seg, pl.n_seg, w, lib, part, ticket);
+struct GramLaunch {
+  const double* x;
+  int64_t ldx;
+  int n_steps;
+  const double* u;
+  const int8_t* arm;
+  const int32_t* rows;
+  int64_t N;
+  GramW w;
+  LibDesc lib;
+  double* part;
+  unsigned* ticket;
+};
+
+template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM>
+int launch_gram4(hipStream_t st, const GramLaunch& g) {
+  auto kern = gram_kernel<VEC, NARM, SMOOTH, MFMA, TM>;
+  const GramPlan pl = gram_plan(g.N, g.n_steps, resident_waves(kern));
+  kern<<<dim3(pl.grid), kBlock, 0, st>>>(g.x, g.ldx, g.n_steps, g.u, g.arm, g.rows, g.N, pl.seg, pl.n_seg, g.w,
+                                          g.lib, g.part, g.ticket);
+  return pl.grid;
 }
 
-template <int NARM, bool MFMA>
-void launch_gram2(bool vec2, bool smooth, hipStream_t st, const double* x, int64_t ldx, const double* u,
-                  const int8_t* arm, const int32_t* rows, int64_t N, const GramW& w, const LibDesc& lib,
-                  double* part, unsigned* ticket, int* grid_out) {
-  if (vec2) {
-    if (smooth) launch_gram3<2, NARM, true, MFMA>(st, x, ldx, u, arm, rows, N, w, lib, part, ticket, grid_out);
-    else launch_gram3<2, NARM, false, MFMA>(st, x, ldx, u, arm, rows, N, w, lib, part, ticket, grid_out);
-  } else {
-    if (smooth) launch_gram3<1, NARM, true, MFMA>(st, x, ldx, u, arm, rows, N, w, lib, part, ticket, grid_out);
-    else launch_gram3<1, NARM, false, MFMA>(st, x, ldx, u, arm, rows, N, w, lib, part, ticket, grid_out);
-  }
+template <int NARM, bool SMOOTH, bool MFMA>
+int launch_gram3(int mode, hipStream_t st, const GramLaunch& g) {  // mode: 0 PM/8-B, 1 PM/16-B, 2 TM
+  if (mode == 2) return launch_gram4<1, NARM, SMOOTH, MFMA, true>(st, g);
+  if (mode == 1) return launch_gram4<2, NARM, SMOOTH, MFMA, false>(st, g);
+  return launch_gram4<1, NARM, SMOOTH, MFMA, false>(st, g);
 }
 
 template <int NARM>
-void launch_gram(bool vec2, bool smooth, hipStream_t st, const double* x, int64_t ldx, const double* u,
-                 const int8_t* arm, const int32_t* rows, int64_t N, const GramW& w, const LibDesc& lib,
-                 double* part, unsigned* ticket, int* grid_out) {
-  if (lib.mfma) launch_gram2<NARM, true>(vec2, smooth, st, x, ldx, u, arm, rows, N, w, lib, part, ticket, grid_out);
-  else launch_gram2<NARM, false>(vec2, smooth, st, x, ldx, u, arm, rows, N, w, lib, part, ticket, grid_out);
+int launch_gram(int mode, bool smooth, hipStream_t st, const GramLaunch& g) {
+  if (g.lib.mfma) {
+    return smooth ? launch_gram3<NARM, true, true>(mode, st, g) : launch_gram3<NARM, false, true>(mode, st, g);
+  }
+  return smooth ? launch_gram3<NARM, true, false>(mode, st, g) : launch_gram3<NARM, false, false>(mode, st, g);
 }
 
 // gram kernel + fused finalize (+ STLSQ when sp.enabled)
-int32_t run_discovery(const double* x, int64_t ldx, const double* u, const int8_t* arm, const int32_t* rows,
-                      int64_t n_patients, int32_t n_statics, int32_t n_arms, const int8_t* exps, int32_t n_terms,
-                      int32_t fd_kind, double dt, double* G_out, double* b_out, void* workspace,
-                      size_t workspace_bytes, void* stream, const StlsqParams& sp, double* coef_out,
-                      int8_t* mask_out, int32_t* iters_out) {
-  if (n_patients < 0 || !G_out || !b_out || n_arms < 1 || n_arms > INSITE_MAX_ARMS || ldx < 1 || !(dt > 0.0))
+int32_t run_discovery(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,
+                      const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
+                      const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt, double* G_out, double* b_out,
+                      void* workspace, size_t workspace_bytes, void* stream, const StlsqParams& sp,
+                      double* coef_out, int8_t* mask_out, int32_t* iters_out) {
+  const bool tm = layout == INSITE_LAYOUT_TIME_MAJOR;
+  if (layout != INSITE_LAYOUT_PATIENT_MAJOR && !tm) return INSITE_E_INVALID_ARG;
+  if (n_patients < 0 || !G_out || !b_out || n_arms < 1 || n_arms > INSITE_MAX_ARMS || ldx < 1 || !(dt > 0.0) ||
+      n_steps < 0 || (tm ? ldx < n_patients : ldx < n_steps))
     return INSITE_E_INVALID_ARG;
   if (n_patients > 0 && (!x || !arm || !rows || (n_statics > 0 && !u))) return INSITE_E_INVALID_ARG;
   if (fd_kind != INSITE_FD_SMOOTHED4 && fd_kind != INSITE_FD_ORDER4) return INSITE_E_UNSUPPORTED;
@@ -1387,6 +1474,7 @@ int32_t run_discovery(const double* x, int64_t ldx, const double* u, const int8_
   unsigned* ticket = static_cast<unsigned*>(workspace);
   double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + kGramWsHeader);
   const bool vec2 = (ldx % 2 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15u) == 0);
+  const int mode = tm ? 2 : (vec2 ? 1 : 0);
   const bool smooth = fd_kind == INSITE_FD_SMOOTHED4;
   if (n_statics == 0) u = x;  // kernels load u unconditionally (values unused when U = 0)
   GramW w;
@@ -1396,10 +1484,11 @@ int32_t run_discovery(const double* x, int64_t ldx, const double* u, const int8_
   w.inv_dt = 1.0 / dt;
   w.fd1 = (2.0 / 3.0) * w.inv_dt;
   w.fd2 = (-1.0 / 12.0) * w.inv_dt;
+  const GramLaunch g{x, ldx, n_steps, u, arm, rows, n_patients, w, lib, part, ticket};
   int grid = 1;
-  if (na == 1) launch_gram<1>(vec2, smooth, hs, x, ldx, u, arm, rows, n_patients, w, lib, part, ticket, &grid);
-  else if (na == 2) launch_gram<2>(vec2, smooth, hs, x, ldx, u, arm, rows, n_patients, w, lib, part, ticket, &grid);
-  else launch_gram<4>(vec2, smooth, hs, x, ldx, u, arm, rows, n_patients, w, lib, part, ticket, &grid);
+  if (na == 1) grid = launch_gram<1>(mode, smooth, hs, g);
+  else if (na == 2) grid = launch_gram<2>(mode, smooth, hs, g);
+  else grid = launch_gram<4>(mode, smooth, hs, g);
   st = launch_status();
   if (st != INSITE_OK) return st;
   const dim3 fg(n_arms * lib.nE);
@@ -1451,21 +1540,26 @@ void launch_rollout_p(bool perrow, int av, bool yv2, dim3 grid, hipStream_t st, 
 }
 
 template <int METHOD, int NARM, int PPL>
-void launch_rollout_tm_w(bool perrow, bool aw4, dim3 grid, hipStream_t st, const RolloutArgs& ra, const LibDesc& lib) {
-  if (perrow) {
-    if (aw4) rollout_tm_kernel<METHOD, NARM, true, PPL, true><<<grid, kBlock, 0, st>>>(ra, lib);
-    else rollout_tm_kernel<METHOD, NARM, true, PPL, false><<<grid, kBlock, 0, st>>>(ra, lib);
+void launch_rollout_tm_w(bool perrow, int afmt, dim3 grid, hipStream_t st, const RolloutArgs& ra, const LibDesc& lib) {
+  // PPL > 1 is only chosen with dword-aligned arm rows (the lane's PPL int8 arms share one dword)
+  if (afmt == kArmBits) {
+    if (perrow) rollout_tm_kernel<METHOD, NARM, true, PPL, kArmBits><<<grid, kBlock, 0, st>>>(ra, lib);
+    else rollout_tm_kernel<METHOD, NARM, false, PPL, kArmBits><<<grid, kBlock, 0, st>>>(ra, lib);
+  } else if (PPL > 1 || afmt == kArmDword) {
+    if (perrow) rollout_tm_kernel<METHOD, NARM, true, PPL, kArmDword><<<grid, kBlock, 0, st>>>(ra, lib);
+    else rollout_tm_kernel<METHOD, NARM, false, PPL, kArmDword><<<grid, kBlock, 0, st>>>(ra, lib);
   } else {
-    if (aw4) rollout_tm_kernel<METHOD, NARM, false, PPL, true><<<grid, kBlock, 0, st>>>(ra, lib);
-    else rollout_tm_kernel<METHOD, NARM, false, PPL, false><<<grid, kBlock, 0, st>>>(ra, lib);
+    if (perrow) rollout_tm_kernel<METHOD, NARM, true, 1, kArmByte><<<grid, kBlock, 0, st>>>(ra, lib);
+    else rollout_tm_kernel<METHOD, NARM, false, 1, kArmByte><<<grid, kBlock, 0, st>>>(ra, lib);
   }
 }
 
 template <int METHOD, int NARM>
-void launch_rollout_tm(bool perrow, int ppl, bool aw4, dim3 grid, hipStream_t st, const RolloutArgs& ra,
+void launch_rollout_tm(bool perrow, int ppl, int afmt, dim3 grid, hipStream_t st, const RolloutArgs& ra,
                        const LibDesc& lib) {
-  if (ppl == 2) launch_rollout_tm_w<METHOD, NARM, 2>(perrow, aw4, grid, st, ra, lib);
-  else launch_rollout_tm_w<METHOD, NARM, 1>(perrow, aw4, grid, st, ra, lib);
+  if (ppl == 4) launch_rollout_tm_w<METHOD, NARM, 4>(perrow, afmt, grid, st, ra, lib);
+  else if (ppl == 2) launch_rollout_tm_w<METHOD, NARM, 2>(perrow, afmt, grid, st, ra, lib);
+  else launch_rollout_tm_w<METHOD, NARM, 1>(perrow, afmt, grid, st, ra, lib);
 }
 
 template <int METHOD>
@@ -1477,11 +1571,11 @@ void launch_rollout_m(int narm, bool perrow, int av, bool yv2, dim3 grid, hipStr
 }
 
 template <int METHOD>
-void launch_rollout_tm_m(int narm, bool perrow, int ppl, bool aw4, dim3 grid, hipStream_t st, const RolloutArgs& ra,
+void launch_rollout_tm_m(int narm, bool perrow, int ppl, int afmt, dim3 grid, hipStream_t st, const RolloutArgs& ra,
                          const LibDesc& lib) {
-  if (narm == 1) launch_rollout_tm<METHOD, 1>(perrow, ppl, aw4, grid, st, ra, lib);
-  else if (narm == 2) launch_rollout_tm<METHOD, 2>(perrow, ppl, aw4, grid, st, ra, lib);
-  else launch_rollout_tm<METHOD, 4>(perrow, ppl, aw4, grid, st, ra, lib);
+  if (narm == 1) launch_rollout_tm<METHOD, 1>(perrow, ppl, afmt, grid, st, ra, lib);
+  else if (narm == 2) launch_rollout_tm<METHOD, 2>(perrow, ppl, afmt, grid, st, ra, lib);
+  else launch_rollout_tm<METHOD, 4>(perrow, ppl, afmt, grid, st, ra, lib);
 }
 
 }  // namespace
@@ -1550,26 +1644,26 @@ size_t insite_gram_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n
   return kGramWsHeader + (size_t)kGramMaxBlocks * per_block * sizeof(double);
 }
 
-int32_t insite_gram_f64(const double* x, int64_t ldx, const double* u, const int8_t* arm,
-                        const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
-                        const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
+int32_t insite_gram_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,
+                        const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics,
+                        int32_t n_arms, const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
                         double* G_out, double* b_out, void* workspace, size_t workspace_bytes,
                         void* stream) {
   StlsqParams sp{0.0, 0.0, 0, 0, 0};
-  return run_discovery(x, ldx, u, arm, rows, n_patients, n_statics, n_arms, exps, n_terms, fd_kind, dt, G_out,
-                       b_out, workspace, workspace_bytes, stream, sp, nullptr, nullptr, nullptr);
+  return run_discovery(x, ldx, layout, n_steps, u, arm, rows, n_patients, n_statics, n_arms, exps, n_terms, fd_kind,
+                       dt, G_out, b_out, workspace, workspace_bytes, stream, sp, nullptr, nullptr, nullptr);
 }
 
-int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, const double* u, const int8_t* arm,
-                             const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
-                             const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
+int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,
+                             const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics,
+                             int32_t n_arms, const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
                              double threshold, double alpha, int32_t max_iter, int32_t unbias,
                              double* G_out, double* b_out, double* coef_out, int8_t* mask_out,
                              int32_t* iters_out, void* workspace, size_t workspace_bytes, void* stream) {
   if (!coef_out || max_iter < 0 || !(threshold >= 0.0) || !(alpha >= 0.0)) return INSITE_E_INVALID_ARG;
   StlsqParams sp{threshold, alpha, max_iter, unbias, 1};
-  return run_discovery(x, ldx, u, arm, rows, n_patients, n_statics, n_arms, exps, n_terms, fd_kind, dt, G_out,
-                       b_out, workspace, workspace_bytes, stream, sp, coef_out, mask_out, iters_out);
+  return run_discovery(x, ldx, layout, n_steps, u, arm, rows, n_patients, n_statics, n_arms, exps, n_terms, fd_kind,
+                       dt, G_out, b_out, workspace, workspace_bytes, stream, sp, coef_out, mask_out, iters_out);
 }
 
 int32_t insite_stlsq_f64(const double* G, const double* b, int64_t n_sys, int32_t n_terms,
@@ -1607,11 +1701,13 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
                            int32_t n_terms, int64_t n_rows, int32_t T, int32_t n_statics,
                            int32_t n_arms, double dt, int32_t method, int32_t substeps,
                            double drop_below, double* y_out, int64_t ld_y, int32_t layout, void* stream) {
-  const bool tm = layout == INSITE_LAYOUT_TIME_MAJOR;
+  const bool bits = layout == INSITE_LAYOUT_TIME_MAJOR_BITS;
+  const bool tm = layout == INSITE_LAYOUT_TIME_MAJOR || bits;
   if (layout != INSITE_LAYOUT_PATIENT_MAJOR && !tm) return INSITE_E_INVALID_ARG;
   const int64_t minld = tm ? n_rows : (int64_t)T;
+  const int64_t minld_arm = bits ? (n_rows + 31) / 32 : minld;
   if (n_rows < 0 || T < 0 || n_arms < 1 || n_arms > INSITE_MAX_ARMS || substeps < 1 ||
-      !(dt >= 0.0) || ld_arm < minld || ld_y < minld || coef_row_stride < 0)
+      !(dt >= 0.0) || ld_arm < minld_arm || ld_y < minld || coef_row_stride < 0 || (bits && n_arms > 2))
     return INSITE_E_INVALID_ARG;
   if (method != INSITE_METHOD_EULER && method != INSITE_METHOD_RK4) return INSITE_E_UNSUPPORTED;
   if (n_rows == 0 || T == 0) return INSITE_OK;
@@ -1639,15 +1735,23 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
   const bool perrow = coef_row_stride != 0;
   const int na = narm_pad(n_arms);
   if (tm) {
-    if (ld_arm > kTmMaxLd || ld_y > kTmMaxLd) return INSITE_E_UNSUPPORTED;  // 32-bit offsets per step group
+    if ((bits ? ld_arm * 4 : ld_arm) > kTmMaxLd || ld_y > kTmMaxLd) return INSITE_E_UNSUPPORTED;  // 32-bit offsets per step group
     if (n_statics == 0) ra.u = y0;
-    const int ppl = (n_rows >= 256 * 1024 && n_rows % 2 == 0 && (ld_y % 2 == 0) && ((reinterpret_cast<uintptr_t>(y_out) & 15u) == 0) &&
-                     (ld_arm % 2 == 0) && ((reinterpret_cast<uintptr_t>(arm) & 1u) == 0)) ? 2 : 1;
+    if (bits && (reinterpret_cast<uintptr_t>(arm) & 3u) != 0) return INSITE_E_INVALID_ARG;
+    const bool aw4 = bits || (ld_arm % 4 == 0 && (reinterpret_cast<uintptr_t>(arm) & 3u) == 0);
+    const bool y16 = ld_y % 2 == 0 && (reinterpret_cast<uintptr_t>(y_out) & 15u) == 0;
+    const int afmt = bits ? kArmBits : (aw4 ? kArmDword : kArmByte);
+    int ppl = 1;  // patients per lane: more independent chains per lane for big cohorts
+#ifdef INSITE_FORCE_PPL
+    ppl = INSITE_FORCE_PPL;
+#else
+    if (n_rows >= 256 * 1024) ppl = 2;
+#endif
+    if (ppl >= 2 && !(y16 && aw4 && n_rows % ppl == 0)) ppl = 1;
     const int64_t per_block = (int64_t)kBlock * ppl;
     const dim3 grid((unsigned)((n_rows + per_block - 1) / per_block));
-    const bool aw4 = ld_arm % 4 == 0 && (reinterpret_cast<uintptr_t>(arm) & 3u) == 0;
-    if (method == INSITE_METHOD_EULER) launch_rollout_tm_m<INSITE_METHOD_EULER>(na, perrow, ppl, aw4, grid, hs, ra, lib);
-    else launch_rollout_tm_m<INSITE_METHOD_RK4>(na, perrow, ppl, aw4, grid, hs, ra, lib);
+    if (method == INSITE_METHOD_EULER) launch_rollout_tm_m<INSITE_METHOD_EULER>(na, perrow, ppl, afmt, grid, hs, ra, lib);
+    else launch_rollout_tm_m<INSITE_METHOD_RK4>(na, perrow, ppl, afmt, grid, hs, ra, lib);
     return launch_status();
   }
   if (ld_arm > (int64_t)0x1FFFFFF || ld_y > (int64_t)0x3FFFFF) return INSITE_E_UNSUPPORTED;  // 32-bit buffer offsets

@@ -26,7 +26,7 @@ ABI_VERSION = 1
 INSITE_OK = 0
 FD_SMOOTHED4, FD_ORDER4, FD_ORDER1 = 0, 1, 2
 METHOD_EULER, METHOD_RK4 = 0, 1
-LAYOUT_PATIENT_MAJOR, LAYOUT_TIME_MAJOR = 0, 1
+LAYOUT_PATIENT_MAJOR, LAYOUT_TIME_MAJOR, LAYOUT_TIME_MAJOR_BITS = 0, 1, 2
 MAX_TERMS, MAX_STATICS, MAX_ARMS, MAX_STATE_DEGREE = 9, 3, 4, 1
 
 EXPORTS = (
@@ -63,9 +63,10 @@ _SIGNATURES = {
     "insite_strerror": (ctypes.c_char_p, [_c_i32]),
     "insite_poly_library": (_c_i32, [_c_i32, _c_i32, _c_i32, _vp, _c_i32, ctypes.POINTER(_c_i32)]),
     "insite_gram_workspace_bytes": (_c_size, [_c_i64, _c_i32, _c_i32]),
-    "insite_gram_f64": (_c_i32, [_vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp, _c_i32, _c_i32,
-                                 _c_f64, _vp, _vp, _vp, _c_size, _vp]),
-    "insite_sindy_fit_f64": (_c_i32, [_vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp, _c_i32, _c_i32,
+    "insite_gram_f64": (_c_i32, [_vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp, _c_i32,
+                                 _c_i32, _c_f64, _vp, _vp, _vp, _c_size, _vp]),
+    "insite_sindy_fit_f64": (_c_i32, [_vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp,
+                                      _c_i32, _c_i32,
                                       _c_f64, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _c_size,
                                       _vp]),
     "insite_stlsq_f64": (_c_i32, [_vp, _vp, _c_i64, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _vp]),

@@ -26,7 +26,7 @@ OBSERVATION_NOISE = 0.01
 
 @dataclass
 class DeviceCohort:
-    x: torch.Tensor          # [N, ldx] f64 volume series (columns 0..T-1)
+    x: torch.Tensor          # volume series: [N, ldx] (layout "patient") or [T, ldx >= N] ("time")
     u: torch.Tensor          # [N, 2] f64 statics (c_0, c_1)
     arm: torch.Tensor        # [N] int8 factual (training) arm
     rows: torch.Tensor       # [N] int32 discovery rows per patient (seq_len - 1)
@@ -34,6 +34,11 @@ class DeviceCohort:
     T: int
     dt: float
     lib: PolyLibrary
+    layout: str = "patient"
+
+    @property
+    def y0(self) -> torch.Tensor:
+        return (self.x[0, : self.arm.numel()] if self.layout == "time" else self.x[:, 0]).contiguous()
 
 
 def _gen(seed: int, device) -> torch.Generator:
@@ -43,7 +48,9 @@ def _gen(seed: int, device) -> torch.Generator:
 
 
 def synthetic_pkpd(n_patients: int, T: int, seed: int, device, equation: str = "EQ_4_C",
-                   conf_coeff: float = 2.0, noise: bool | None = None) -> DeviceCohort:
+                   conf_coeff: float = 2.0, noise: bool | None = None, layout: str = "patient") -> DeviceCohort:
+    """Cohort of ``n_patients`` factual trajectories of T observations.  layout "patient": x is
+    [N, T + (T & 1)]; layout "time": x is [T, round_up(N, 2)] (one contiguous run per step)."""
     dev = torch.device(device)
     g = _gen(seed, dev)
     N = int(n_patients)
@@ -62,23 +69,39 @@ def synthetic_pkpd(n_patients: int, T: int, seed: int, device, equation: str = "
     arm = (torch.rand((N,), generator=g, device=dev, dtype=f64) < prob).to(torch.int8)
     lib = polynomial_library(2, 2, True)
     dt = MAX_TIME_HORIZON / T
-    ldx = T + (T & 1)
-    x = torch.empty((N, ldx), device=dev, dtype=f64)
-    x[:, 0] = x0
-    if ldx > T:
-        x[:, T:] = 0.0
     coef = torch.zeros((N, 2, lib.n_terms), device=dev, dtype=f64)
     coef[:, :, 1] = -C                               # 'x0' column carries -C_a
-    lda = (T + 15) // 16 * 16
-    arms = torch.empty((N, lda), dtype=torch.int8, device=dev)
-    arms[:] = arm[:, None]
-    if T > 1:
-        ops.rollout(x0, c.contiguous(), arms, coef, lib, dt, method="euler5", drop_below=0.0, T=T - 1,
-                    out=x[:, 1:T])
-    if noise if noise is not None else equation.split("_")[-1] in ("B", "C", "D"):
-        x[:, :T] += OBSERVATION_NOISE * torch.randn((N, T), generator=g, device=dev, dtype=f64)
+    if layout == "time":
+        ld = N + (N & 1)
+        x = torch.zeros((T, ld), device=dev, dtype=f64)
+        x[0, :N] = x0
+        lda = (N + 3) // 4 * 4
+        arms = torch.empty((max(T - 1, 1), lda), dtype=torch.int8, device=dev)
+        arms[:, :N] = arm[None, :]
+        arms[:, N:] = 0
+        if T > 1:
+            ops.rollout(x0, c.contiguous(), arms, coef, lib, dt, method="euler5", drop_below=0.0, T=T - 1,
+                        out=x[1:T], layout="time")
+        if noise if noise is not None else equation.split("_")[-1] in ("B", "C", "D"):
+            x[:, :N] += OBSERVATION_NOISE * torch.randn((T, N), generator=g, device=dev, dtype=f64)
+    elif layout == "patient":
+        ldx = T + (T & 1)
+        x = torch.empty((N, ldx), device=dev, dtype=f64)
+        x[:, 0] = x0
+        if ldx > T:
+            x[:, T:] = 0.0
+        lda = (T + 15) // 16 * 16
+        arms = torch.empty((N, lda), dtype=torch.int8, device=dev)
+        arms[:] = arm[:, None]
+        if T > 1:
+            ops.rollout(x0, c.contiguous(), arms, coef, lib, dt, method="euler5", drop_below=0.0, T=T - 1,
+                        out=x[:, 1:T])
+        if noise if noise is not None else equation.split("_")[-1] in ("B", "C", "D"):
+            x[:, :T] += OBSERVATION_NOISE * torch.randn((N, T), generator=g, device=dev, dtype=f64)
+    else:
+        raise ValueError(f"layout {layout!r}")
     rows = torch.full((N,), T - 2, device=dev, dtype=torch.int32)   # seq_len = T-1, offset 1
-    return DeviceCohort(x=x, u=c.contiguous(), arm=arm, rows=rows, C=C, T=T, dt=dt, lib=lib)
+    return DeviceCohort(x=x, u=c.contiguous(), arm=arm, rows=rows, C=C, T=T, dt=dt, lib=lib, layout=layout)
 
 
 def counterfactual_arms(arm: torch.Tensor, T: int, seed: int, layout: str = "patient") -> torch.Tensor:
@@ -86,17 +109,20 @@ def counterfactual_arms(arm: torch.Tensor, T: int, seed: int, layout: str = "pat
 
     layout "patient": [N, round_up(T, 16)] (16-byte rows: the patient-major rollout reads 16 B per
     lane); layout "time": [T, round_up(N, 4)] (time-major; 4-byte rows let the rollout load
-    dwords)."""
+    dwords); layout "time_bits": int32 [T, ceil(N/32)] bitmask (ops.pack_arm_bits)."""
     dev = arm.device
     g = _gen(seed + 7919, dev)
     N = arm.numel()
     flip = torch.randint(0, T, (N, 1), generator=g, device=dev)
     steps = torch.arange(T, device=dev)[None, :]
     seq = torch.where(steps >= flip, 1 - arm[:, None], arm[:, None]).to(torch.int8)
-    if layout == "time":
+    if layout in ("time", "time_bits"):
         ld = (N + 3) // 4 * 4
         out = torch.zeros((T, ld), dtype=torch.int8, device=dev)
         out[:, :N] = seq.t()
+        if layout == "time_bits":
+            from .ops import pack_arm_bits
+            return pack_arm_bits(out, N)
         return out
     lda = (T + 15) // 16 * 16
     out = torch.empty((N, lda), dtype=torch.int8, device=dev)

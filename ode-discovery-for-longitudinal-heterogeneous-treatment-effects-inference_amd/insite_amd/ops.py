@@ -17,6 +17,23 @@ from .library import PolyLibrary
 METHODS = {"euler5": (_lib.METHOD_EULER, 5), "euler": (_lib.METHOD_EULER, 1), "rk4": (_lib.METHOD_RK4, 1)}
 FD_KINDS = {"smoothed4": _lib.FD_SMOOTHED4, "order4": _lib.FD_ORDER4}
 LAYOUTS = {"patient": _lib.LAYOUT_PATIENT_MAJOR, "time": _lib.LAYOUT_TIME_MAJOR}
+ROLLOUT_LAYOUTS = dict(LAYOUTS, time_bits=_lib.LAYOUT_TIME_MAJOR_BITS)
+
+
+def pack_arm_bits(arm: torch.Tensor, n: int | None = None) -> torch.Tensor:
+    """Time-major int8 arms [T, >=N] (values 0/1) -> the INSITE_LAYOUT_TIME_MAJOR_BITS bitmask
+    int32 [T, ceil(N/32)]: bit (r & 31) of word r >> 5 is the arm of patient r.  Device-agnostic
+    torch ops (data preparation, not on the hot path)."""
+    T = arm.size(0)
+    N = arm.size(1) if n is None else int(n)
+    W = (N + 31) // 32
+    a = torch.zeros((T, W * 32), dtype=torch.int64, device=arm.device)
+    a[:, :N] = arm[:, :N].to(torch.int64)
+    if bool((a > 1).any()):
+        raise ValueError("bit-packed arms need n_arms <= 2 (arm values 0/1)")
+    w = (a.view(T, W, 32) << torch.arange(32, device=arm.device, dtype=torch.int64)).sum(-1)
+    w = torch.where(w >= 2 ** 31, w - 2 ** 32, w)
+    return w.to(torch.int32).contiguous()
 
 
 def _p(t):
@@ -59,21 +76,36 @@ class Workspace:
 _WS = Workspace()
 
 
-def gram(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor, dt: float,
-         lib: PolyLibrary, n_arms: int = 2, fd: str = "smoothed4", workspace: Workspace | None = None,
-         out: tuple | None = None):
-    """Per-arm Gram G[A,F,F] and moments b[A,F] of the discovery regression (insite_gram_f64)."""
-    L = _lib.load()
+def _discovery_inputs(x, u, arm, rows, lib, layout):
+    """Validate the discovery inputs; returns (N, n_steps, layout code)."""
+    if layout not in LAYOUTS:
+        raise ValueError(f"layout must be one of {sorted(LAYOUTS)}")
     _dev("x", x, torch.float64, 2)
-    N = x.size(0)
     _dev("arm", arm, torch.int8, 1)
     _dev("rows", rows, torch.int32, 1)
+    if layout == "time":
+        N, n_steps = arm.numel(), x.size(0)
+        if x.size(1) < N:
+            raise ValueError("time-major x must be [n_steps, >= N]")
+    else:
+        N, n_steps = x.size(0), x.size(1)
     if lib.n_statics:
         _dev("u", u, torch.float64, 2)
         if u.size(0) != N or u.size(1) != lib.n_statics or u.stride(0) != lib.n_statics:
             raise ValueError("u must be a contiguous [N, n_statics] tensor")
     if arm.numel() != N or rows.numel() != N:
         raise ValueError("arm/rows must have one entry per patient")
+    return N, n_steps, LAYOUTS[layout]
+
+
+def gram(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor, dt: float,
+         lib: PolyLibrary, n_arms: int = 2, fd: str = "smoothed4", workspace: Workspace | None = None,
+         out: tuple | None = None, layout: str = "patient"):
+    """Per-arm Gram G[A,F,F] and moments b[A,F] of the discovery regression (insite_gram_f64).
+
+    layout "patient": x [N, T] (the reference's array); "time": x [T, >=N] (coalesced)."""
+    L = _lib.load()
+    N, n_steps, lay = _discovery_inputs(x, u, arm, rows, lib, layout)
     F = lib.n_terms
     if out is None:
         G = torch.empty((n_arms, F, F), dtype=torch.float64, device=x.device)
@@ -83,9 +115,9 @@ def gram(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor
     nbytes = L.insite_gram_workspace_bytes(N, n_arms, F)
     ws = (workspace or _WS).get(nbytes, x.device)
     tab = lib.ctypes_table()
-    st = L.insite_gram_f64(_p(x), x.stride(0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), _p(rows), N,
-                           lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p), F, FD_KINDS[fd], float(dt),
-                           _p(G), _p(b), _p(ws), ws.numel(), _stream(x.device))
+    st = L.insite_gram_f64(_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else ctypes.c_void_p(0),
+                           _p(arm), _p(rows), N, lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p), F,
+                           FD_KINDS[fd], float(dt), _p(G), _p(b), _p(ws), ws.numel(), _stream(x.device))
     _lib.check("insite_gram_f64", st)
     return G, b
 
@@ -93,21 +125,12 @@ def gram(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor
 def sindy_fit(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor, dt: float,
               lib: PolyLibrary, threshold: float, alpha: float, max_iter: int = 100, unbias: bool = True,
               n_arms: int = 2, fd: str = "smoothed4", workspace: Workspace | None = None,
-              out: tuple | None = None):
+              out: tuple | None = None, layout: str = "patient"):
     """Discovery in two launches (insite_sindy_fit_f64): Gram kernel, then the fixed-order
     reduction fused with one STLSQ fit per arm.  Replaces ``SINDy(...).fit`` per arm
     (reference sindy.py:190-192).  Returns (coef[A,F], mask[A,F], iters[A], G[A,F,F], b[A,F])."""
     L = _lib.load()
-    _dev("x", x, torch.float64, 2)
-    N = x.size(0)
-    _dev("arm", arm, torch.int8, 1)
-    _dev("rows", rows, torch.int32, 1)
-    if lib.n_statics:
-        _dev("u", u, torch.float64, 2)
-        if u.size(0) != N or u.size(1) != lib.n_statics or u.stride(0) != lib.n_statics:
-            raise ValueError("u must be a contiguous [N, n_statics] tensor")
-    if arm.numel() != N or rows.numel() != N:
-        raise ValueError("arm/rows must have one entry per patient")
+    N, n_steps, lay = _discovery_inputs(x, u, arm, rows, lib, layout)
     F = lib.n_terms
     dev = x.device
     if out is None:
@@ -121,8 +144,8 @@ def sindy_fit(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.T
     nbytes = L.insite_gram_workspace_bytes(N, n_arms, F)
     ws = (workspace or _WS).get(nbytes, dev)
     tab = lib.ctypes_table()
-    st = L.insite_sindy_fit_f64(_p(x), x.stride(0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm),
-                                _p(rows), N, lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p), F,
+    st = L.insite_sindy_fit_f64(_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else ctypes.c_void_p(0),
+                                _p(arm), _p(rows), N, lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p), F,
                                 FD_KINDS[fd], float(dt), float(threshold), float(alpha), int(max_iter),
                                 int(bool(unbias)), _p(G), _p(b), _p(coef), _p(mask), _p(iters), _p(ws), ws.numel(),
                                 _stream(dev))
@@ -158,21 +181,29 @@ def rollout(y0: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, coef: torch.Te
     """Batched open-loop rollout (insite_rollout_f64).
 
     y0 [N] f64, u [N,U] f64, coef [A,F] (global model) or [N,A,F] (per-patient).
-    layout "patient": arm [N, >=T] int8, returns y [N,T] (the reference's [N, T] arrays).
-    layout "time":    arm [T, >=N] int8, returns y [T,N] (time-major: one contiguous run per step,
-    the fast layout on MI355X).  Row k holds the state after observation interval k."""
+    layout "patient":   arm int8 [N, >=T], returns y [N,T] (the reference's [N, T] arrays).
+    layout "time":      arm int8 [T, >=N], returns y [T,N] (one contiguous run per step).
+    layout "time_bits": arm int32 [T, >=ceil(N/32)] bitmask (pack_arm_bits; A <= 2), y [T,N] —
+                        the fast layout on MI355X.  Row k of y is the state after
+                        observation interval k."""
     L = _lib.load()
-    if layout not in LAYOUTS:
-        raise ValueError(f"layout must be one of {sorted(LAYOUTS)}")
-    tm = layout == "time"
+    if layout not in ROLLOUT_LAYOUTS:
+        raise ValueError(f"layout must be one of {sorted(ROLLOUT_LAYOUTS)}")
+    tm = layout != "patient"
     _dev("y0", y0, torch.float64, 1)
-    _dev("arm", arm, torch.int8, 2)
     N = y0.numel()
-    if tm:
+    if layout == "time_bits":
+        _dev("arm", arm, torch.int32, 2)
+        T = arm.size(0) if T is None else int(T)
+        if arm.size(1) < (N + 31) // 32 or arm.size(0) < T:
+            raise ValueError("bit-packed arm must be [>=T, >=ceil(N/32)] int32")
+    elif tm:
+        _dev("arm", arm, torch.int8, 2)
         T = arm.size(0) if T is None else int(T)
         if arm.size(1) < N or arm.size(0) < T:
             raise ValueError("time-major arm must be [>=T, >=N]")
     else:
+        _dev("arm", arm, torch.int8, 2)
         T = arm.size(1) if T is None else int(T)
         if arm.size(0) != N or arm.size(1) < T:
             raise ValueError("arm must be [N, >=T]")
@@ -208,7 +239,7 @@ def rollout(y0: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, coef: torch.Te
     tab = lib.ctypes_table()
     st = L.insite_rollout_f64(_p(y0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), arm.stride(0),
                               _p(coef), stride, tab.ctypes.data_as(ctypes.c_void_p), F, N, T, lib.n_statics, A,
-                              float(dt), m, sub, float(drop_below), _p(out), out.stride(0), LAYOUTS[layout],
+                              float(dt), m, sub, float(drop_below), _p(out), out.stride(0), ROLLOUT_LAYOUTS[layout],
                               _stream(y0.device))
     _lib.check("insite_rollout_f64", st)
     return out

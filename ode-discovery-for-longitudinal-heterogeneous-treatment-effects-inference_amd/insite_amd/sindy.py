@@ -1,0 +1,282 @@
+"""The ``+backbone=sindy`` plugin on MI355X: drop-in for the reference ``SINDY`` model
+(``libs_m/ct/src/models/sindy.py:57-431, 717-760``; metrics inherited from
+``libs_m/ct/src/models/time_varying_model.py:236-313``).
+
+Same constructor (``SINDY(args, dataset_collection)``), methods (``fit``, ``get_predictions``,
+``get_autoregressive_predictions``, ``get_normalised_masked_rmse``,
+``get_normalised_n_step_rmses``), attributes (``global_equation_string``, ``joint_coefs``,
+``feature_library_names``, ``insite``, ``hparams``) and error behaviour (Python exceptions;
+``AssertionError`` on NaN predictions).  The two inner call sites of the reference run on the GPU
+through the C ABI (include/insite_hip.h):
+
+* ``SINDy(...).fit(X_a, u=U_a, t=dt, multiple_trajectories=True)`` per arm (sindy.py:190-192)
+  -> ``insite_sindy_fit_f64``: smoothing + 4th-order FD + library + per-arm Gram in one streaming
+  kernel, then the reduction fused with STLSQ + unbias for every arm.
+* ``jit(vmap(simulate_cancer_volume))`` (sindy.py:413-431) -> ``insite_rollout_f64`` (Euler-5).
+
+The DE-format extraction (A1, pkpd/utils.py:523-606), the tau-step slice (A9) and the masked
+squared-error sums of the metrics (A10) also run on the device; only scalars and the returned
+prediction arrays cross back to the host.  Out of scope in this build (raise
+``NotImplementedError``): the INSITE per-patient refinement (``insite: true``),
+weak SINDy, the joint model, the degree-4 ablation library and the cancer_sim / EQ_5 datasets.
+"""
+from __future__ import annotations
+
+import logging
+
+import numpy as np
+import torch
+
+from . import ops
+from .library import polynomial_library
+
+logger = logging.getLogger(__name__)
+
+MAX_SEQUENCE_LENGTH = 60
+MAX_TIME_HORIZON = 10.0
+STANDARD_DT = MAX_TIME_HORIZON / MAX_SEQUENCE_LENGTH   # pkpd/utils.py:53; SINDY.dt (sindy.py:89)
+RHS_COEF_EPS = 1e-3                                    # pkpd/utils.py:388
+
+
+def _get(cfg, path, default=None):
+    """Read ``a.b.c`` from a nested dict / attribute config (DictConfig-like)."""
+    cur = cfg
+    for key in path.split("."):
+        if cur is None:
+            return default
+        if isinstance(cur, dict):
+            cur = cur.get(key, None)
+        else:
+            cur = getattr(cur, key, None)
+    return default if cur is None else cur
+
+
+def equation_terms(coefs, names, quantize=False, round_to=3) -> str:
+    """Term string of ``convert_sindy_model_to_sympyjax_model_core`` (pkpd/utils.py:378-397):
+    ``+{c}*term`` for every |c| > 1e-3, with numpy's shortest round-trip float formatting."""
+    s = ""
+    for j, c in enumerate(np.asarray(coefs, dtype=np.float64)):
+        if np.abs(c) > RHS_COEF_EPS:
+            if quantize:
+                c = np.round(c, round_to)
+            s += f"+{c}*" + names[j].replace(" ", "*")
+    return s
+
+
+def equation_string(joint_coefs, names, quantize=False, round_to=3) -> str:
+    """``global_equation_string`` (sindy.py:276): 'Treatment 0: x_dot = ... | Treatment 1: ...'."""
+    return " | ".join(f"Treatment {a}: x_dot = {equation_terms(c, names, quantize, round_to)}"
+                      for a, c in enumerate(np.asarray(joint_coefs)))
+
+
+def rhs_coefficients(joint_coefs, quantize=False, round_to=3) -> np.ndarray:
+    """Coefficient table the sympy RHS evaluates: terms with |c| <= 1e-3 dropped, optionally
+    rounded (the rounded value is what ``sympify`` of the string parses back)."""
+    c = np.asarray(joint_coefs, dtype=np.float64).copy()
+    keep = np.abs(c) > RHS_COEF_EPS
+    if quantize:
+        c = np.round(c, round_to)
+    return np.where(keep, c, 0.0)
+
+
+class SINDY:
+    """MI355X drop-in for ``src.models.sindy.SINDY`` (EQ_4 PK/PD datasets, non-joint model)."""
+
+    model_type = "sindy_regressor"
+    tuning_criterion = "rmse"
+
+    def __init__(self, args, dataset_collection=None, autoregressive=None, has_vitals=None, device=None, **kwargs):
+        self.hparams = args
+        self.dataset_collection = dataset_collection
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device()
+                                                                                    if torch.cuda.is_available() else 0)
+        m = lambda k, d=None: _get(args, f"model.{k}", d)   # noqa: E731
+        self.lag_features = m("lag_features", 1)
+        self.dim_outcome = int(m("dim_outcomes", 1))
+        self.dim_treatments = int(m("dim_treatments", 2))
+        self.dim_static_features = int(m("dim_static_features", 2))
+        self.dim_vitals = int(m("dim_vitals", 0))
+        self.smoother_kws = {"window_length": 5, "polyorder": 3}
+        self.dt = float(m("dt", STANDARD_DT))   # reference hard-codes STANDARD_DT
+        self.insite_val_error_threshold = m("insite_val_error_threshold")
+        self.global_equation_string = ""
+        self.sindy_threshold = float(m("sindy_threshold"))
+        self.sindy_alpha = float(m("sindy_alpha"))
+        self.smooth_input_data = bool(m("smooth_input_data", False))
+        self.sindy_quantize = bool(m("sindy_quantize", False))
+        self.sindy_quantize_global_model_round_to = int(m("sindy_quantize_global_model_round_to", 2))
+        self.lam = m("lam")
+        self.joint_model = bool(m("joint_model", False))
+        self.insite = bool(m("insite", False))
+        self.wsindy = bool(m("wsindy", False))
+        self.use_smoothed_finite_difference = bool(m("use_smoothed_finite_difference", False))
+        self.dataset_name = str(m("dataset_name", ""))
+        self.ablation_more_complex_basis_functions = bool(m("ablation_more_complex_basis_functions", False))
+        self.insight_recover_parametric_dist = bool(m("insight_recover_parametric_dist", False))
+        self.treatment_mode = _get(args, "dataset.treatment_mode", "multiclass")
+        self.projection_horizon = int(_get(args, "dataset.projection_horizon", 5))
+        self.unscale_rmse = bool(_get(args, "exp.unscale_rmse", True))
+        self.percentage_rmse = bool(_get(args, "exp.percentage_rmse", True))
+        self.integrator = str(m("integrator", "euler5"))   # reference: Euler-5 (pkpd/utils.py:68-94)
+        self.library = polynomial_library(self.dim_static_features, 2, True)
+        self.feature_library_names = self.library.get_feature_names()
+        self.feature_names = ["x0"] + [f"u{i}" for i in range(self.dim_static_features)]
+        self.joint_coefs = None
+        self.n_iter = None
+        self._coef_dev = None
+        self._check_supported()
+
+    # ------------------------------------------------------------------ configuration checks
+    def _check_supported(self):
+        if "EQ_4" not in self.dataset_name.upper():
+            raise NotImplementedError(f"dataset {self.dataset_name!r}: this build covers the PK/PD EQ_4 family "
+                                      "(cancer_sim / EQ_5 are SURVEY.md §8 F4)")
+        if self.insite:
+            raise NotImplementedError("INSITE per-patient refinement (insite: true) is SURVEY.md §8 F2, not in "
+                                      "this build; use +backbone=sindy")
+        if self.wsindy:
+            raise NotImplementedError("weak SINDy (wsindy: true) is not on the MI355X path")
+        if self.joint_model:
+            raise NotImplementedError("joint_model: true (treatment as a library input) is not on the MI355X path")
+        if self.ablation_more_complex_basis_functions:
+            raise NotImplementedError("the degree-4 ablation library has state exponents > 1 "
+                                      "(outside INSITE_MAX_STATE_DEGREE)")
+        if self.integrator not in ops.METHODS:
+            raise ValueError(f"integrator must be one of {sorted(ops.METHODS)}")
+
+    def prepare_data(self) -> None:
+        c = self.dataset_collection
+        if c is not None and not getattr(c, "processed_data_multi", True):
+            c.process_data_multi()
+
+    # ------------------------------------------------------------------ A1: DE format on device
+    def _unscaled_inputs(self, dataset):
+        sp = dataset.scaling_params
+        d = dataset.data
+        dev = self.device
+        std, mean = float(sp["output_stds"]), float(sp["output_means"])
+        prev = torch.as_tensor(np.ascontiguousarray(d["prev_outputs"][..., 0]), device=dev) * std + mean
+        lo, hi = self.dim_outcome, self.dim_outcome + self.dim_static_features
+        stat = (torch.as_tensor(np.ascontiguousarray(d["static_features"]), device=dev)
+                * torch.as_tensor(np.asarray(sp["inputs_stds"][lo:hi], dtype=np.float64), device=dev)
+                + torch.as_tensor(np.asarray(sp["input_means"][lo:hi], dtype=np.float64), device=dev))
+        return prev, stat.contiguous(), std, mean
+
+    def de_format(self, dataset, sequence_lengths_offset=1):
+        """Device arrays of ``process_dataset_into_de_format`` (pkpd/utils.py:523-606): the
+        reconstructed volume series x[N,T] (prev_outputs[:,0] ++ unscaled_outputs), statics u[N,U],
+        the arm of each patient (current_treatments[:,0] == [1,0] -> 0, else 1; utils.py:425) and
+        the discovery rows seq_len - offset (utils.py:426).  ``smooth_input_data`` smooths a copy
+        the reference never reads back (utils.py:568-571), so it has no effect there or here."""
+        d = dataset.data
+        prev, stat, _, _ = self._unscaled_inputs(dataset)
+        uo = torch.as_tensor(np.ascontiguousarray(d["unscaled_outputs"][..., 0]), device=self.device)
+        x = torch.cat([prev[:, :1], uo], dim=1).contiguous()
+        ct = torch.as_tensor(np.ascontiguousarray(d["current_treatments"][:, 0, :]), device=self.device)
+        arm = torch.where((ct[:, 0] == 1) & (ct[:, 1] == 0), 0, 1).to(torch.int8)
+        rows = (torch.as_tensor(np.asarray(d["sequence_lengths"]), device=self.device).to(torch.int64)
+                - sequence_lengths_offset).to(torch.int32)
+        return x, stat, arm, rows
+
+    # ------------------------------------------------------------------ discovery
+    def fit(self, train_f, val_f=None):
+        """Global discovery per arm (sindy.py:145-336): one Gram pass + STLSQ on the GPU."""
+        self.prepare_data()
+        x, u, arm, rows = self.de_format(train_f)
+        if int(rows.min().item()) < 5:
+            raise ValueError("a training trajectory has fewer than 5 rows: the savgol(5, 3) smoother "
+                             "and the 5-point derivative need at least 5 samples")
+        coef, mask, iters, _, _ = ops.sindy_fit(x, u, arm, rows, self.dt, self.library, self.sindy_threshold,
+                                                self.sindy_alpha, max_iter=100, unbias=True,
+                                                n_arms=self.dim_treatments, fd="smoothed4")
+        iters_h = iters.cpu().numpy()
+        if np.any(iters_h < 0):
+            raise np.linalg.LinAlgError("STLSQ ridge system is not positive definite")
+        self.joint_coefs = coef.cpu().numpy()
+        self.coef_mask = mask.cpu().numpy().astype(bool)
+        self.n_iter = iters_h
+        rhs = rhs_coefficients(self.joint_coefs, self.sindy_quantize, self.sindy_quantize_global_model_round_to)
+        self._coef_dev = torch.as_tensor(rhs, device=self.device)
+        self.global_equation_string = equation_string(self.joint_coefs, self.feature_library_names,
+                                                      self.sindy_quantize, self.sindy_quantize_global_model_round_to)
+        logger.info("[Model]: %s", self.global_equation_string)
+        return self
+
+    # ------------------------------------------------------------------ rollout (A8)
+    def _predict_device(self, dataset):
+        """Standardised open-loop predictions [N, T-1] on the device (sindy.py:371-431)."""
+        if self._coef_dev is None:
+            raise RuntimeError("fit() first")
+        d = dataset.data
+        prev, stat, std, mean = self._unscaled_inputs(dataset)
+        T = d["prev_outputs"].shape[1]
+        arm = torch.as_tensor(np.argmax(d["current_treatments"], axis=-1).astype(np.int8), device=self.device)
+        y = ops.rollout(prev[:, 0].contiguous(), stat, arm, self._coef_dev, self.library, self.dt,
+                        method=self.integrator, drop_below=0.0, T=T)
+        return (y - mean) / std
+
+    def get_predictions(self, dataset) -> np.ndarray:
+        logger.info("Predictions for %s.", getattr(dataset, "subset_name", "?"))
+        p = self._predict_device(dataset).cpu().numpy()[..., None]
+        assert not np.any(np.isnan(p)), "Predictions contains NaN"
+        return p
+
+    def _slice_device(self, pred, dataset, offset=1):
+        """tau-step window per row from max(offset, seq_len - tau) (sindy.py:729-733), with
+        jax.lax.dynamic_slice's clamp to [0, T - tau]."""
+        tau = self.projection_horizon
+        T = pred.shape[1]
+        sl = torch.as_tensor(np.asarray(dataset.data["sequence_lengths"]).astype(np.int64), device=pred.device)
+        lo = torch.clamp(torch.clamp(sl - tau, min=offset), 0, T - tau)
+        idx = lo[:, None] + torch.arange(tau, device=pred.device)[None, :]
+        return torch.gather(pred, 1, idx)
+
+    def get_autoregressive_predictions(self, dataset) -> np.ndarray:
+        logger.info("Autoregressive Prediction for %s.", getattr(dataset, "subset_name", "?"))
+        return self._slice_device(self._predict_device(dataset), dataset).cpu().numpy()[..., None]
+
+    # ------------------------------------------------------------------ metrics (A10)
+    def _sse(self, pred_scaled, target, active, std, mean):
+        """Masked squared-error sums on the device; the prediction is un-scaled in the kernel
+        (pred * std + mean, as time_varying_model.py:249) when ``unscale_rmse``."""
+        tgt = torch.as_tensor(np.ascontiguousarray(target), device=pred_scaled.device)
+        act = torch.as_tensor(np.ascontiguousarray(active), device=pred_scaled.device)
+        if self.unscale_rmse:
+            return ops.masked_sse(pred_scaled.contiguous(), tgt, act, scale=std, shift=mean)
+        return ops.masked_sse(pred_scaled.contiguous(), tgt, act)
+
+    def get_normalised_masked_rmse(self, dataset, one_step_counterfactual=False):
+        logger.info("RMSE calculation for %s.", getattr(dataset, "subset_name", "?"))
+        sp = dataset.scaling_params
+        std, mean = float(sp["output_stds"]), float(sp["output_means"])
+        pred = self._predict_device(dataset)
+        if torch.isnan(pred).any():
+            raise AssertionError("Predictions contains NaN")
+        key = "unscaled_outputs" if self.unscale_rmse else "outputs"
+        per, cnt, last = self._sse(pred, dataset.data[key][..., 0], dataset.data["active_entries"][..., 0], std, mean)
+        per, cnt, last = per.cpu().numpy(), cnt.cpu().numpy(), last.cpu().numpy()
+        norm = dataset.norm_const
+        scale = 100.0 if self.percentage_rmse else 1.0
+        with np.errstate(invalid="ignore", divide="ignore"):
+            orig = np.sqrt((per / cnt).mean()) / norm * scale
+            allv = np.sqrt(per.sum() / cnt.sum()) / norm * scale
+            if not one_step_counterfactual:
+                return orig, allv
+            lastv = np.sqrt(last[0] / last[1]) / norm * scale
+        return orig, allv, lastv
+
+    def get_normalised_n_step_rmses(self, dataset, datasets_mc=None):
+        logger.info("RMSE calculation for %s.", getattr(dataset, "subset_name", "?"))
+        seq = dataset.data_processed_seq
+        assert seq is not None, "dataset has no data_processed_seq (process_data_multi first)"
+        sp = dataset.scaling_params
+        std, mean = float(sp["output_stds"]), float(sp["output_means"])
+        pred = self._slice_device(self._predict_device(dataset if datasets_mc is None else datasets_mc), dataset)
+        key = "unscaled_outputs" if self.unscale_rmse else "outputs"
+        not_nan = ~np.isnan(seq["outputs"][..., 0]).any(axis=1)          # time_varying_model.py:302-303
+        idx = torch.as_tensor(np.nonzero(not_nan)[0], device=pred.device)
+        per, cnt, _ = self._sse(pred.index_select(0, idx), seq[key][not_nan][..., 0],
+                                seq["active_entries"][not_nan][..., 0], std, mean)
+        per, cnt = per.cpu().numpy(), cnt.cpu().numpy()
+        r = np.sqrt(per / cnt) / dataset.norm_const
+        return r * (100.0 if self.percentage_rmse else 1.0)

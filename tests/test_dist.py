@@ -1,0 +1,100 @@
+"""Multi-process (gloo, world_size 2, CPU) tests of the sharded discovery path.
+
+The GPU path (insite_amd.dist.discover_sharded) is: per-rank Gram over a contiguous patient
+shard -> ONE all-reduce(SUM) of the packed G|b buffer -> replicated STLSQ.  Here each rank builds
+its shard's partial moments with the oracle (the Gram kernel's CPU restatement), and the product
+host logic (shard_bounds, MomentBuffer packing, reduce_moments, max_over_ranks) runs unchanged
+over gloo.  The reduced system must equal the single-process full-cohort one, and the STLSQ on
+it must give the same model on every rank.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "ode-discovery-for-longitudinal-heterogeneous-treatment-effects-inference_amd")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from oracle import insite_ref as R
+    from insite_amd import dist as idist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        g = np.load(os.path.join(ROOT, "tests", "golden", "discovery_eq_4_c.npz"))
+        x, u, arm, rows = g["x"], g["u"], g["arm"], g["rows"]
+        lo, hi = idist.shard_bounds(x.shape[0], rank, world)
+        exps = R.poly_library(3, 2, True)
+        buf = idist.MomentBuffer(2, exps.shape[0], "cpu")
+        G, b = R.gram_moments(x[lo:hi], u[lo:hi], arm[lo:hi], rows[lo:hi], float(g["dt"]), exps)
+        buf.G.copy_(torch.from_numpy(G))
+        buf.b.copy_(torch.from_numpy(b))
+        idist.reduce_moments(buf)
+        coefs = [R.stlsq_gram(buf.G[a].numpy(), buf.b[a].numpy(), 0.1, 0.5)[0] for a in range(2)]
+        t = idist.max_over_ranks(0.5 + rank)
+        q.put((rank, lo, hi, buf.flat.numpy().copy(), np.stack(coefs), t))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_shard_bounds_partition():
+    from insite_amd.dist import shard_bounds
+    for n in (0, 1, 7, 100, 100_003):
+        for w in (1, 2, 3, 8):
+            spans = [shard_bounds(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+            sizes = [h - l_ for l_, h in spans]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard_bounds(10, 2, 2)
+
+
+def test_moment_buffer_views():
+    from insite_amd.dist import MomentBuffer
+    m = MomentBuffer(2, 7, "cpu")
+    assert m.flat.numel() == 2 * 49 + 14
+    m.G[1, 2, 3] = 5.0
+    m.b[0, 6] = 7.0
+    assert m.flat[49 + 2 * 7 + 3] == 5.0 and m.flat[98 + 6] == 7.0
+
+
+def test_sharded_discovery_gloo_world2():
+    from oracle import insite_ref as R
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda r: r[0])
+    g = np.load(os.path.join(ROOT, "tests", "golden", "discovery_eq_4_c.npz"))
+    # shards tile the cohort
+    assert res[0][1] == 0 and res[0][2] == res[1][1] and res[1][2] == g["x"].shape[0]
+    full = np.concatenate([g["G"].reshape(-1), g["b"].reshape(-1)])
+    for r in res:
+        np.testing.assert_allclose(r[3], full, rtol=1e-12, atol=1e-9)   # all-reduced == full cohort
+        assert r[5] == 1.5                                              # max over ranks
+    np.testing.assert_array_equal(res[0][4], res[1][4])                 # replicated STLSQ identical
+    assert np.max(np.abs(res[0][4] - g["coef"])) < 1e-8
+    assert np.array_equal(res[0][4] != 0, g["mask"].astype(bool))

@@ -32,20 +32,37 @@ def _cohort(eq="EQ_4_C", n=300, T=60, seed=0):
 
 
 # ------------------------------------------------------------------------------------------ gram
+LAYOUTS = ["patient", "time"]
+
+
+def _x_layout(x, layout, dev, pad=5):
+    """Device series in the requested layout (time-major: [steps, N + pad], padding = NaN so a
+    stray read of a padding column would poison the sums)."""
+    if layout == "patient":
+        return _t(x, dev)
+    N, S = x.shape
+    tm = np.full((S, N + pad), np.nan)
+    tm[:, :N] = x.T
+    return _t(tm, dev)
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("eq,n,T", [("EQ_4_A", 300, 60), ("EQ_4_C", 257, 60), ("EQ_4_D", 1000, 200)])
-def test_gram_matches_oracle(dev, eq, n, T):
+def test_gram_matches_oracle(dev, eq, n, T, layout):
     from insite_amd import ops
     x, u, arm, rows = _cohort(eq, n, T)
     lib = _lib()
     dt = R.MAX_TIME_HORIZON / T
     G_ref, b_ref = R.gram_moments(x, u, arm, rows, dt, lib.exps.astype(np.int64))
-    G, b = ops.gram(_t(x, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), dt, lib)
+    G, b = ops.gram(_x_layout(x, layout, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), dt,
+                    lib, layout=layout)
     torch.cuda.synchronize()
     np.testing.assert_allclose(G.cpu().numpy(), G_ref, rtol=1e-10, atol=1e-9)
     np.testing.assert_allclose(b.cpu().numpy(), b_ref, rtol=1e-10, atol=1e-9)
 
 
-def test_gram_ragged_rows_odd_ld_and_order4(dev):
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_gram_ragged_rows_odd_ld_and_order4(dev, layout):
     """Ragged trajectory lengths (incl. < 5 rows -> skipped), odd leading dim (8-byte staging
     path), 4 arms, 1 static, unsmoothed 4th-order FD."""
     from insite_amd import ops
@@ -60,15 +77,16 @@ def test_gram_ragged_rows_odd_ld_and_order4(dev):
     exps = lib.exps.astype(np.int64)
     for fd, smooth in (("order4", False), ("smoothed4", True)):
         G_ref, b_ref = R.gram_moments(x, u, arm, rows, 0.1, exps, n_arms=4, fd=fd)
-        G, b = ops.gram(_t(x, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), 0.1, lib,
-                        n_arms=4, fd=fd)
+        G, b = ops.gram(_x_layout(x, layout, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32),
+                        0.1, lib, n_arms=4, fd=fd, layout=layout)
         torch.cuda.synchronize()
         np.testing.assert_allclose(G.cpu().numpy(), G_ref, rtol=1e-10, atol=1e-8)
         np.testing.assert_allclose(b.cpu().numpy(), b_ref, rtol=1e-10, atol=1e-8)
 
 
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("ld", [300, 301])
-def test_gram_ragged_multi_segment(dev, ld):
+def test_gram_ragged_multi_segment(dev, ld, layout):
     """Long ragged rows split over several time segments (small N -> segmented work items);
     every row length from 0 to ld, both derivative kinds, both staging widths."""
     from insite_amd import ops
@@ -83,8 +101,8 @@ def test_gram_ragged_multi_segment(dev, ld):
     exps = lib.exps.astype(np.int64)
     for fd in ("smoothed4", "order4"):
         G_ref, b_ref = R.gram_moments(x, u, arm, rows, 0.05, exps, n_arms=2, fd=fd)
-        G, b = ops.gram(_t(x, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), 0.05, lib,
-                        n_arms=2, fd=fd)
+        G, b = ops.gram(_x_layout(x, layout, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32),
+                        0.05, lib, n_arms=2, fd=fd, layout=layout)
         torch.cuda.synchronize()
         np.testing.assert_allclose(G.cpu().numpy(), G_ref, rtol=1e-10, atol=1e-8)
         np.testing.assert_allclose(b.cpu().numpy(), b_ref, rtol=1e-10, atol=1e-8)
@@ -94,23 +112,40 @@ def test_gram_deterministic(dev):
     from insite_amd import ops
     x, u, arm, rows = _cohort("EQ_4_B", 2000, 60)
     lib = _lib()
-    args = (_t(x, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), 1 / 6, lib)
-    G1, b1 = ops.gram(*args)
-    G2, b2 = ops.gram(*args)
+    for layout in LAYOUTS:
+        args = (_x_layout(x, layout, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), 1 / 6, lib)
+        G1, b1 = ops.gram(*args, layout=layout)
+        G2, b2 = ops.gram(*args, layout=layout)
+        torch.cuda.synchronize()
+        assert torch.equal(G1, G2) and torch.equal(b1, b2)
+
+
+def test_gram_layouts_agree_at_scale(dev):
+    """Size-independent property at C2 scale: the time-major and patient-major kernels see the
+    same cohort and must agree to fp64 summation-order noise; the Gram is symmetric."""
+    from insite_amd import cohort, ops
+    coh = cohort.synthetic_pkpd(100_000, 200, seed=3, device=dev, equation="EQ_4_C")
+    xt = coh.x[:, :200].t().contiguous()
+    G1, b1 = ops.gram(coh.x, coh.u, coh.arm, coh.rows, coh.dt, coh.lib)
+    G2, b2 = ops.gram(xt, coh.u, coh.arm, coh.rows, coh.dt, coh.lib, layout="time")
     torch.cuda.synchronize()
-    assert torch.equal(G1, G2) and torch.equal(b1, b2)
+    torch.testing.assert_close(G2, G1, rtol=1e-11, atol=0)
+    torch.testing.assert_close(b2, b1, rtol=1e-10, atol=1e-6)
+    torch.testing.assert_close(G1, G1.transpose(1, 2), rtol=0, atol=0)
 
 
 # ----------------------------------------------------------------------------------------- stlsq
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("eq", ["EQ_4_A", "EQ_4_B", "EQ_4_C", "EQ_4_D"])
-def test_discovery_matches_oracle(dev, eq):
+def test_discovery_matches_oracle(dev, eq, layout):
     """Full discovery (gram + STLSQ on the GPU) vs the pysindy-semantics oracle on Theta:
     identical support, coefficient L-inf < 1e-8."""
     from insite_amd import ops
     x, u, arm, rows = _cohort(eq, 500, 60, seed=1)
     lib = _lib()
     dt = 1.0 / 6.0
-    G, b = ops.gram(_t(x, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), dt, lib)
+    G, b = ops.gram(_x_layout(x, layout, dev), _t(u, dev), _t(arm, dev, torch.int8), _t(rows, dev, torch.int32), dt,
+                    lib, layout=layout)
     coef, mask, iters = ops.stlsq(G, b, 0.1, 0.5, 100)
     torch.cuda.synchronize()
     X, U = R.de_lists(x, u, arm, rows)
@@ -182,7 +217,14 @@ def _arm_layout(arm, T, layout, dev):
     ld = N + 3 if layout == "time" else (N + 3) // 4 * 4
     tm = np.zeros((T, ld), np.int8)
     tm[:, :N] = arm[:, :T].T
+    if layout == "bits":
+        from insite_amd import ops
+        return ops.pack_arm_bits(_t(tm, dev, torch.int8), N)
     return _t(tm, dev, torch.int8)
+
+
+def _kernel_layout(layout):
+    return {"patient": "patient", "time": "time", "time4": "time", "bits": "time_bits"}[layout]
 
 
 def _as_patient_major(y, layout):
@@ -190,7 +232,7 @@ def _as_patient_major(y, layout):
     return yg if layout == "patient" else yg.T
 
 
-@pytest.mark.parametrize("layout", ["patient", "time", "time4"])
+@pytest.mark.parametrize("layout", ["patient", "time", "time4", "bits"])
 @pytest.mark.parametrize("method", ["euler5", "rk4", "euler"])
 @pytest.mark.parametrize("N,T,lda,per", [(1000, 60, 60, False), (777, 59, 59, False), (129, 201, 204, True),
                                          (64, 1, 4, False), (65, 33, 35, True)])
@@ -201,7 +243,7 @@ def test_rollout_matches_oracle(dev, method, N, T, lda, per, layout):
     dt = R.MAX_TIME_HORIZON / max(T, 1)
     sub = 3 if method == "euler" else None
     y = ops.rollout(_t(y0, dev), _t(u, dev), _arm_layout(arm, T, layout, dev), _t(coef, dev), lib, dt,
-                    method=method, substeps=sub, T=T, layout="patient" if layout == "patient" else "time")
+                    method=method, substeps=sub, T=T, layout=_kernel_layout(layout))
     torch.cuda.synchronize()
     y_ref = R.rollout(y0, u, arm[:, :T], coef, lib.exps.astype(np.int64), dt, method=method, substeps=sub)
     yg = _as_patient_major(y, layout)
@@ -210,7 +252,8 @@ def test_rollout_matches_oracle(dev, method, N, T, lda, per, layout):
     np.testing.assert_allclose(yg, y_ref, rtol=1e-11, atol=1e-12)
 
 
-def test_rollout_time_major_out_padding_untouched(dev):
+@pytest.mark.parametrize("layout", ["time4", "bits"])
+def test_rollout_time_major_out_padding_untouched(dev, layout):
     """Time-major output with ld_y > N: the padding columns and the rows beyond T stay untouched
     (the last wavefront's inactive lanes must not store)."""
     from insite_amd import ops
@@ -218,8 +261,8 @@ def test_rollout_time_major_out_padding_untouched(dev):
     N, T = 300, 17
     lib, y0, u, arm, coef = _random_rollout_case(rng, N, T)
     out = torch.full((T + 2, N + 5), 7.0, dtype=torch.float64, device=dev)
-    ops.rollout(_t(y0, dev), _t(u, dev), _arm_layout(arm, T, "time4", dev), _t(coef, dev), lib, 0.1,
-                method="rk4", T=T, out=out[:T], layout="time")
+    ops.rollout(_t(y0, dev), _t(u, dev), _arm_layout(arm, T, layout, dev), _t(coef, dev), lib, 0.1,
+                method="rk4", T=T, out=out[:T], layout=_kernel_layout(layout))
     torch.cuda.synchronize()
     o = out.cpu().numpy()
     assert np.all(o[:, N:] == 7.0) and np.all(o[T:] == 7.0)
@@ -245,7 +288,7 @@ def test_rollout_known_answer_y_equals_t(dev):
         assert np.mean((y.cpu().numpy() - t[None]) ** 2) < 1e-16
 
 
-@pytest.mark.parametrize("layout", ["patient", "time", "time4"])
+@pytest.mark.parametrize("layout", ["patient", "time", "time4", "bits"])
 def test_rollout_deterministic_and_large_property(dev, layout):
     """Size-independent properties at a large size: bitwise repeatability, exact agreement of a
     sampled row subset with the oracle, and the closed form of the linear ODE under RK4.
@@ -268,14 +311,16 @@ def test_rollout_deterministic_and_large_property(dev, layout):
         ld = N + 1 if layout == "time" else (N + 3) // 4 * 4
         arm_in = torch.zeros((T, ld), dtype=torch.int8, device=dev)
         arm_in[:, :N] = arm.t()
-    lay = "patient" if layout == "patient" else "time"
+        if layout == "bits":
+            arm_in = ops.pack_arm_bits(arm_in, N)
+    lay = _kernel_layout(layout)
     c = _t(coef, dev)
     dt = R.MAX_TIME_HORIZON / T
     y1 = ops.rollout(y0, u, arm_in, c, lib, dt, method="rk4", layout=lay)
     y2 = ops.rollout(y0, u, arm_in, c, lib, dt, method="rk4", layout=lay)
     torch.cuda.synchronize()
     assert torch.equal(y1, y2)
-    if lay == "time":
+    if lay != "patient":
         y1 = y1.t()
     idx = np.sort(rng.choice(N, 2000, replace=False))
     idx[-1] = N - 1
@@ -329,3 +374,76 @@ def test_sindy_fit_fused_matches_oracle(dev, eq, T):
         c_ref, ind_ref, _, _ = R.sindy_fit(X[a], U[a], dt, 0.1, 0.5)
         assert np.array_equal(mask.cpu().numpy()[a] != 0, ind_ref)
         assert np.max(np.abs(coef.cpu().numpy()[a] - c_ref)) < COEF_TOL
+
+
+# ------------------------------------------------------------------------- golden fixtures
+def _golden(name):
+    import os
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", name))
+
+
+@pytest.mark.parametrize("eq", ["EQ_4_A", "EQ_4_C"])
+def test_golden_discovery(dev, eq):
+    """Fused discovery (Gram + STLSQ) on the committed fixture cohort: identical support,
+    coefficient L-inf < 1e-8, Gram/moments at rtol 1e-10, same equation string."""
+    from insite_amd import ops
+    from insite_amd.sindy import equation_string
+    g = _golden(f"discovery_{eq.lower()}.npz")
+    lib = _lib()
+    coef, mask, iters, G, b = ops.sindy_fit(_t(g["x"], dev), _t(g["u"], dev), _t(g["arm"], dev, torch.int8),
+                                            _t(g["rows"], dev, torch.int32), float(g["dt"]), lib,
+                                            float(g["threshold"]), float(g["alpha"]))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(G.cpu().numpy(), g["G"], rtol=1e-10, atol=1e-9)
+    np.testing.assert_allclose(b.cpu().numpy(), g["b"], rtol=1e-10, atol=1e-9)
+    np.testing.assert_array_equal(mask.cpu().numpy(), g["mask"])
+    assert np.max(np.abs(coef.cpu().numpy() - g["coef"])) < COEF_TOL
+    np.testing.assert_array_equal(iters.cpu().numpy(), g["iters"])
+    # same terms in the same order; the printed values differ only in the last ulps (L-inf above)
+    terms = lambda s: [[t.split("*", 1)[1] for t in a.split("= ", 1)[1].split("+")[1:]]  # noqa: E731
+                       for a in s.split(" | ")]
+    assert terms(equation_string(coef.cpu().numpy(), lib.get_feature_names())) == terms(str(g["equation"]))
+
+
+@pytest.mark.parametrize("layout", ["patient", "time4", "bits"])
+def test_golden_rollout(dev, layout):
+    from insite_amd import ops
+    g = _golden("rollout.npz")
+    lib = _lib()
+    dt = float(g["dt"])
+    T = g["arm"].shape[1]
+    lay = _kernel_layout(layout)
+    for key, method, sub, coef in [("euler5", "euler5", None, g["coef"]), ("rk4", "rk4", None, g["coef"]),
+                                   ("euler3", "euler", 3, g["coef"]),
+                                   ("euler5_per_patient", "euler5", None, g["coef_per_patient"])]:
+        y = ops.rollout(_t(g["y0"], dev), _t(g["u"], dev), _arm_layout(g["arm"], T, layout, dev), _t(coef, dev),
+                        lib, dt, method=method, substeps=sub, layout=lay, T=T)
+        torch.cuda.synchronize()
+        yg = _as_patient_major(y, layout)
+        assert np.sqrt(np.mean((yg - g[key]) ** 2)) <= RMSE_TOL
+        np.testing.assert_allclose(yg, g[key], rtol=1e-11, atol=1e-12)
+
+
+def test_golden_metrics(dev):
+    from insite_amd import ops
+    g = _golden("metrics.npz")
+    pred, target, active = g["pred"][..., 0], g["target"][..., 0], g["active"][..., 0]
+    per, cnt, last = ops.masked_sse(_t(pred, dev), _t(target, dev), _t(active, dev))
+    torch.cuda.synchronize()
+    per, cnt, last = per.cpu().numpy(), cnt.cpu().numpy(), last.cpu().numpy()
+    rmse_all = np.sqrt(per.sum() / cnt.sum()) / 50 * 100
+    rmse_orig = np.sqrt(np.mean(per / cnt)) / 50 * 100
+    rmse_last = np.sqrt(last[0] / last[1]) / 50 * 100
+    assert abs(rmse_all - float(g["rmse_all"])) < 1e-12
+    assert abs(rmse_orig - float(g["rmse_orig"])) < 1e-12
+    assert abs(rmse_last - float(g["rmse_last"])) < 1e-12
+
+
+def test_cohort_layouts_identical_trajectories(dev):
+    """The on-device generator writes the same noise-free Euler-5 trajectories in both layouts."""
+    from insite_amd import cohort
+    a = cohort.synthetic_pkpd(1001, 33, seed=4, device=dev, equation="EQ_4_C", noise=False)
+    b = cohort.synthetic_pkpd(1001, 33, seed=4, device=dev, equation="EQ_4_C", noise=False, layout="time")
+    torch.cuda.synchronize()
+    assert torch.equal(a.x[:, :33], b.x[:, :1001].t())
+    assert torch.equal(a.y0, b.y0)

@@ -1,0 +1,161 @@
+"""CPU tests of the plugin's host logic: config composition, SINDY construction and validation,
+equation strings, the PK/PD collection layout, DE-format extraction and the tau-step slice.
+No kernels run here (the device ops are covered by tests/test_gpu_*.py)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import insite_ref as R
+
+
+def _args(**model):
+    from insite_amd import config as C
+    ov = ["+backbone=sindy", "+dataset=pkpd_sim", "dataset.equation_str=EQ_4_C", "model.dataset_name=EQ_4_C",
+          "model.sindy_threshold=0.1", "model.sindy_alpha=0.5", "model.lam=10.0"]
+    ov += [f"model.{k}={v}" for k, v in model.items()]
+    return C.compose(ov)
+
+
+def test_compose_groups_and_overrides():
+    a = _args()
+    assert a["model"]["name"] == "SINDY" and a["model"]["sindy_threshold"] == 0.1
+    assert a["dataset"]["equation_str"] == "EQ_4_C" and a["dataset"]["projection_horizon"] == 5
+    assert a["exp"]["unscale_rmse"] is True and a["dataset"]["seed"] == 0
+    from insite_amd import config as C
+    b = C.compose(["+backbone=insite", "exp.seed=3", "+dataset=pkpd_sim"])
+    assert b["model"]["insite"] is True and b["dataset"]["seed"] == 3
+    with pytest.raises(FileNotFoundError):
+        C.compose(["+backbone=crn"])
+
+
+def test_run_overrides_pick_thresholds_by_dataset():
+    from insite_amd import config as C
+    drv = C.driver_config()
+    ov = C.run_overrides(drv, "EQ_4_D", "sindy", 2, 2)
+    a = C.compose(ov)
+    assert a["model"]["sindy_threshold"] == 0.1 and a["model"]["lam"] == 10.0
+    assert a["dataset"]["num_patients"] == {"train": 1000, "val": 100, "test": 100}
+    assert a["exp"]["seed"] == 2 and a["dataset"]["coeff"] == 2
+    with pytest.raises(NotImplementedError):
+        C.run_overrides(drv, "cancer_sim", "sindy", 0, 2)
+
+
+def test_sindy_reads_config_and_rejects_unsupported_modes():
+    from insite_amd.sindy import SINDY
+    m = SINDY(_args(), device="cpu")
+    assert (m.sindy_threshold, m.sindy_alpha, m.dt) == (0.1, 0.5, 10.0 / 60)
+    assert m.feature_library_names == ["1", "x0", "u0", "u1", "x0 u0", "x0 u1", "u0 u1"]
+    assert m.model_type == "sindy_regressor" and m.insite is False
+    for flag in ("insite", "wsindy", "joint_model", "ablation_more_complex_basis_functions"):
+        with pytest.raises(NotImplementedError):
+            SINDY(_args(**{flag: True}), device="cpu")
+    a = _args()
+    a["model"]["dataset_name"] = "cancer_sim"
+    with pytest.raises(NotImplementedError):
+        SINDY(a, device="cpu")
+    with pytest.raises(ValueError):
+        SINDY(_args(integrator="rk45"), device="cpu")
+    with pytest.raises(RuntimeError):          # predictions before fit()
+        SINDY(_args(), device="cpu")._predict_device(None)
+
+
+def test_equation_string_matches_oracle_and_quantize():
+    from insite_amd.sindy import equation_string, rhs_coefficients
+    g = np.load("tests/golden/discovery_eq_4_c.npz")
+    names = ["1", "x0", "u0", "u1", "x0 u0", "x0 u1", "u0 u1"]
+    assert equation_string(g["coef"], names) == str(g["equation"]) == R.global_equation_string(g["coef"], names)
+    c = np.array([[0.0, 0.0005, 0.0, 0.0, -1.23456, 0.0, 0.0]])
+    assert equation_string(c, names, quantize=True, round_to=2) == "Treatment 0: x_dot = +-1.23*x0*u0"
+    np.testing.assert_array_equal(rhs_coefficients(c, True, 2), [[0, 0, 0, 0, -1.23, 0, 0]])
+    np.testing.assert_array_equal(rhs_coefficients(c), [[0, 0, 0, 0, -1.23456, 0, 0]])
+
+
+def test_de_format_on_host_torch_matches_oracle():
+    from insite_amd.sindy import SINDY
+    coll = R.make_collection("EQ_4_C", {"train": 50, "val": 2, "test": 2}, seq_length=60, seed=1, with_tests=False)
+    tr = coll["train"]
+    m = SINDY(_args(), device="cpu")
+    x, u, arm, rows = m.de_format(tr)
+    xr, ur, ar, rr = R.de_format(tr.data, tr.scaling_params)
+    np.testing.assert_array_equal(x.numpy(), xr)
+    np.testing.assert_array_equal(u.numpy(), ur)
+    np.testing.assert_array_equal(arm.numpy(), ar)
+    np.testing.assert_array_equal(rows.numpy(), rr)
+
+
+def test_tau_slice_matches_oracle():
+    from insite_amd.sindy import SINDY
+    m = SINDY(_args(), device="cpu")
+    pred = torch.arange(6 * 12, dtype=torch.float64).reshape(6, 12)
+
+    class D:
+        data = {"sequence_lengths": np.array([12.0, 3.0, 6.0, 1.0, 9.0, 5.0])}
+    got = m._slice_device(pred, D()).numpy()
+    ref = R.autoregressive_slice(pred.numpy()[..., None], D.data["sequence_lengths"], 5)[..., 0]
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_pkpd_collection_layout_matches_reference_format():
+    from insite_amd import pkpd
+    c = pkpd.dataset_collection("EQ_4_C", {"train": 40, "val": 5, "test": 4}, seed=0, device="cpu")
+    o = R.make_collection("EQ_4_C", {"train": 40, "val": 5, "test": 4}, seq_length=60, seed=0)
+    for mine, ref in ((c.train_f, o["train"]), (c.val_f, o["val"]), (c.test_cf_one_step, o["test_cf_one_step"]),
+                      (c.test_cf_treatment_seq, o["test_cf_treatment_seq"])):
+        for k, v in ref.data.items():
+            if k.startswith("hidden_"):
+                continue
+            assert mine.data[k].shape == v.shape, k
+            assert mine.data[k].dtype == v.dtype, k
+        assert set(mine.scaling_params) == set(ref.scaling_params)
+    for k, v in o["test_cf_treatment_seq"].data_processed_seq.items():
+        assert c.test_cf_treatment_seq.data_processed_seq[k].shape == v.shape
+    # every subset uses the train scaling
+    assert c.test_cf_one_step.scaling_params["output_means"] == c.train_f.scaling_params["output_means"]
+
+
+def test_pkpd_counterfactual_structure():
+    """One-step rows come in pairs that share the history and differ in the last step only
+    (treatment flipped at step i); tau-step rows follow one-hot / inverted one-hot plans."""
+    from insite_amd import pkpd
+    T, tau = 12, 3
+    c = pkpd.SyntheticPkpdDatasetCollection(2.0, {"train": 6, "val": 2, "test": 3}, "EQ_4_A", seed=4,
+                                            max_seq_length=T, projection_horizon=tau, device="cpu")
+    one = {k: v.numpy() for k, v in c.test_cf_one_step.sim.items()}
+    V, trt, sl = one["cancer_volume"], one["treatment_application"], one["sequence_lengths"]
+    for p in range(3):
+        for i in range(T - 1):
+            r0, r1 = p * 2 * (T - 1) + 2 * i, p * 2 * (T - 1) + 2 * i + 1
+            assert sl[r0] == sl[r1] == i + 1
+            np.testing.assert_array_equal(V[r0, : i + 1], V[r1, : i + 1])
+            assert trt[r0, i] == 1 - trt[r1, i]
+            assert np.all(V[r0, i + 2:] == 0) and np.all(V[r1, i + 2:] == 0)
+    seq = {k: v.numpy() for k, v in c.test_cf_treatment_seq.sim.items()}
+    trt, sl = seq["treatment_application"], seq["sequence_lengths"]
+    plans = np.concatenate([np.eye(tau), 1 - np.eye(tau)])
+    for i in range(T - 1):
+        for p in range(2 * tau):
+            r = i * 2 * tau + p
+            assert sl[r] == i + 1 + tau
+            np.testing.assert_array_equal(trt[r, i + 1: i + 1 + tau], plans[p])
+
+
+def test_pkpd_noise_free_trajectory_is_euler5_decay():
+    from insite_amd import pkpd
+    c = pkpd.SyntheticPkpdDatasetCollection(2.0, {"train": 20, "val": 2, "test": 2}, "EQ_4_A", seed=5,
+                                            max_seq_length=30, device="cpu")
+    s = {k: v.numpy() for k, v in c.train_f.sim.items()}
+    V, a = s["cancer_volume"], s["treatment_application"][:, 0]
+    dt = 10.0 / 30
+    # EQ_4_A: C_a = c_a (observed statics), no noise
+    C = np.where(a == 0, s["observed_static_c_0"], s["observed_static_c_1"])
+    ratio = V[:, 1:] / V[:, :-1]
+    np.testing.assert_allclose(ratio, np.broadcast_to(((1 - C * dt / 5) ** 5)[:, None], ratio.shape), rtol=1e-12)
+
+
+def test_pkpd_is_deterministic_per_seed():
+    from insite_amd import pkpd
+    a = pkpd.dataset_collection("EQ_4_D", {"train": 10, "val": 2, "test": 2}, seed=9, device="cpu")
+    b = pkpd.dataset_collection("EQ_4_D", {"train": 10, "val": 2, "test": 2}, seed=9, device="cpu")
+    np.testing.assert_array_equal(a.train_f.data["outputs"], b.train_f.data["outputs"])
+    c = pkpd.dataset_collection("EQ_4_D", {"train": 10, "val": 2, "test": 2}, seed=10, device="cpu")
+    assert not np.array_equal(a.train_f.data["outputs"], c.train_f.data["outputs"])

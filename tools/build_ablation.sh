@@ -13,5 +13,13 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     RT64) NAME=$v build -DINSITE_RT=64 ;;
     NOGPHASE) NAME=$v build -DINSITE_ABLATE_NOGPHASE ;;
     GT32) NAME=$v build -DINSITE_GT=32 ;;
+    TG8) NAME=$v build -DINSITE_TG=8 ;;
+    TG32) NAME=$v build -DINSITE_TG=32 ;;
+    TG64) NAME=$v build -DINSITE_TG=64 ;;
+    NOCOMPUTE) NAME=$v build -DINSITE_ABLATE_NOCOMPUTE ;;
+    NT) NAME=$v build -DINSITE_STORE_AUX=2 ;;
+    PPL1) NAME=$v build -DINSITE_FORCE_PPL=1 ;;
+    PPL2) NAME=$v build -DINSITE_FORCE_PPL=2 ;;
+    PPL4) NAME=$v build -DINSITE_FORCE_PPL=4 ;;
   esac
 done

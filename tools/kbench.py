@@ -14,10 +14,11 @@ ap.add_argument("--patients", type=int, default=100_000)
 ap.add_argument("--T", type=int, default=200)
 ap.add_argument("--iters", type=int, default=50)
 ap.add_argument("--method", default="rk4")
-ap.add_argument("--layout", default="patient", choices=["patient", "time"])
+ap.add_argument("--layout", default="patient", choices=["patient", "time", "time_bits"])
 a = ap.parse_args()
 dev = torch.device("cuda:0")
-coh = cohort.synthetic_pkpd(a.patients, a.T, seed=1, device=dev, equation="EQ_4_C")
+xlay = "time" if a.layout == "time_bits" else a.layout
+coh = cohort.synthetic_pkpd(a.patients, a.T, seed=1, device=dev, equation="EQ_4_C", layout=xlay)
 lib = coh.lib
 ws = ops.Workspace()
 coef = torch.zeros((2, lib.n_terms), dtype=torch.float64, device=dev)
@@ -29,11 +30,12 @@ G = G @ G.transpose(1, 2) + torch.eye(7, dtype=torch.float64, device=dev) * 7
 bb = torch.randn(a.patients, 7, dtype=torch.float64, device=dev)
 def run():
     if a.op == "gram":
-        ops.gram(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 2, "smoothed4", ws)
+        ops.gram(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 2, "smoothed4", ws, layout=xlay)
     elif a.op == "sindy_fit":
-        ops.sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, 100, True, 2, "smoothed4", ws)
+        ops.sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, 100, True, 2, "smoothed4", ws,
+                      layout=xlay)
     elif a.op == "rollout":
-        ops.rollout(coh.x[:, 0].contiguous(), coh.u, arm_cf, coef, lib, coh.dt, method=a.method, T=a.T, out=y,
+        ops.rollout(coh.y0, coh.u, arm_cf, coef, lib, coh.dt, method=a.method, T=a.T, out=y,
                     layout=a.layout)
     else:
         ops.stlsq(G, bb, 0.1, 0.5)
