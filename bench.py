@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--arm-format", default="bits", choices=["bits", "int8"],
                     help="per-step arms of the time-major rollout: 1-bit mask (A <= 2) or int8")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
+                    help="run discovery and rollout of consecutive steps strictly in sequence on one stream")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
@@ -123,37 +125,70 @@ def main():
     F = lib.n_terms
     y0 = coh.y0
     buf = idist.MomentBuffer(2, F, dev)          # G|b in one buffer: one all-reduce when N > 1
-    coef = torch.empty((2, F), dtype=torch.float64, device=dev)
+    # coefficients double-buffered: discovery of step i+1 may run while the rollout of step i reads
+    coefs = [torch.empty((2, F), dtype=torch.float64, device=dev) for _ in range(2)]
     mask = torch.empty((2, F), dtype=torch.int8, device=dev)
     iters = torch.empty((2,), dtype=torch.int32, device=dev)
     y = torch.empty((T, N) if args.layout == "time" else (N, T), dtype=torch.float64, device=dev)
     ws = ops.Workspace()
-    stream = torch.cuda.current_stream(dev)
+    s_disc = torch.cuda.current_stream(dev)
+    s_roll = torch.cuda.Stream(dev) if args.pipeline else s_disc
     ev_roll, ev_disc = [], []
 
-    def step(record=False):
-        if record:
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-            e[0].record(stream)
-        idist.discover_sharded(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, buf, workspace=ws,
-                               out=(coef, mask, iters), layout=args.layout)
-        if record:
-            e[1].record(stream)
-        ops.rollout(y0, coh.u, arm_cf, coef, lib, coh.dt, method=args.method, T=T, out=y, layout=roll_layout)
-        if record:
-            e[2].record(stream)
-            ev_disc.append((e[0], e[1]))
-            ev_roll.append((e[1], e[2]))
+    # one step = discovery (Gram -> [all-reduce] -> STLSQ) on s_disc, then the rollout on s_roll
+    # once that step's coefficients exist.  With --pipeline (default) the two phases of consecutive
+    # steps overlap: the discovery of step i+1 runs while the rollout of step i streams (both are
+    # HBM-bound; the overlap hides the STLSQ tail and the launch gaps, not bandwidth).  Launches go
+    # through prepared plans (arguments validated and packed once), events are preallocated.
+    with torch.cuda.stream(s_disc):
+        if world == 1:   # Gram kernel + fused reduction/STLSQ (2 launches)
+            disc_plans = [ops.plan_sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, 100, True, 2,
+                                             "smoothed4", ws, out=(c, mask, iters, buf.G, buf.b), layout=args.layout)
+                          for c in coefs]
+        else:            # per-rank Gram -> one all-reduce of G|b -> replicated STLSQ
+            gram_plan = ops.plan_gram(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 2, "smoothed4", ws,
+                                      out=(buf.G, buf.b), layout=args.layout)
+            stlsq_plans = [ops.plan_stlsq(buf.G, buf.b, 0.1, 0.5, 100, True, out=(c, mask, iters)) for c in coefs]
+    roll_plans = [ops.plan_rollout(y0, coh.u, arm_cf, c, lib, coh.dt, method=args.method, T=T, out=y,
+                                   layout=roll_layout) for c in coefs]
+    n_ev = (args.warmup * 2 + args.steps + 2) * 4
+    ev_pool = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
 
-    for _ in range(args.warmup):
-        step()
+    def step(i, record=False):
+        e = ev_pool[4 * (i % (n_ev // 4)): 4 * (i % (n_ev // 4)) + 4]
+        if record:
+            e[0].record(s_disc)
+        if done[i % 2] is not None:
+            s_disc.wait_event(done[i % 2])          # rollout i-2 finished reading this coef buffer
+        if world == 1:
+            disc_plans[i % 2](s_disc)
+        else:
+            gram_plan(s_disc)
+            with torch.cuda.stream(s_disc):
+                idist.reduce_moments(buf)           # the only collective
+            stlsq_plans[i % 2](s_disc)
+        e[1].record(s_disc)
+        s_roll.wait_event(e[1])
+        if record:
+            e[2].record(s_roll)
+        roll_plans[i % 2](s_roll)
+        e[3].record(s_roll)
+        done[i % 2] = e[3]
+        if record:
+            ev_disc.append((e[0], e[1]))
+            ev_roll.append((e[2], e[3]))
+
+    done = [None, None]
+    for i in range(args.warmup):
+        step(i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(record=True)
+    for i in range(args.steps):
+        step(i + 2 * args.warmup, record=True)
+    host_ms = (time.perf_counter() - t0) / args.steps * 1e3   # submit time per step (no sync)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -161,6 +196,7 @@ def main():
     ms_step = el / args.steps * 1e3
     roll_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ev_roll]))
     disc_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ev_disc]))
+    coef = coefs[(args.steps - 1 + 2 * args.warmup) % 2]
 
     # sanity on the measured result: discovered support is the EQ_4_C one, no NaN
     sup = mask.cpu().numpy()
@@ -199,6 +235,7 @@ def main():
                 "patients_per_gpu": N, "T": T, "rows_per_patient": T - 2, "library_terms": F,
                 "parallelism": f"patient-shard x{world}", "discovered_support": sup.tolist(), "finite": ok,
             },
+            "host_submit_ms_per_step": host_ms,
             "roofline": {
                 "kernel": f"rollout_kernel ({args.method})",
                 "bound": "hbm",
@@ -216,6 +253,8 @@ def main():
             "discovery": {
                 "kernels": "gram_kernel + discovery_finalize (fused STLSQ)" if world == 1
                            else "gram_kernel + RCCL all_reduce + stlsq_kernel",
+                "streams": "discovery and rollout on two streams, consecutive steps overlapped" if args.pipeline
+                           else "one stream, strictly sequential",
                 "avg_ms": disc_ms,
                 "algorithmic_bytes": gram_bytes(N, T),
                 "achieved_GBps": gram_bytes(N, T) / (disc_ms * 1e-3) / 1e9,

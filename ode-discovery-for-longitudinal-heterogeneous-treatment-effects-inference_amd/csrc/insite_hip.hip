@@ -110,15 +110,18 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
+// Butterfly reductions over a full wave; every lane holds the result, returned through
+// readfirstlane so the compiler treats it as wave-uniform (SGPR: scalar branches, uniform
+// buffer descriptors without waterfall loops).
 __device__ __forceinline__ int wave_min_i(int v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, kWave));
-  return v;
+  return __builtin_amdgcn_readfirstlane(v);
 }
 __device__ __forceinline__ int wave_max_i(int v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, kWave));
-  return v;
+  return __builtin_amdgcn_readfirstlane(v);
 }
 
 __device__ __forceinline__ double monomial(const LibDesc& lib, int j, const double* u) {
@@ -191,6 +194,7 @@ __device__ void small_trajectory(const double* __restrict__ xrow, int64_t step, 
 }
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
+constexpr unsigned kOOB = 0x80000000u;  // buffer offset beyond every descriptor: access dropped
 
 // Telescoped derivative moments.  With the antisymmetric interior stencil
 // d_k = fd1 (v_{k+1} - v_{k-1}) + fd2 (v_{k+2} - v_{k-2}),  for rows k = a..b:
@@ -220,7 +224,7 @@ __device__ __forceinline__ void tele_lo(const GramW& w, double vm2, double vm1, 
 // TM (time-major x[k * ldx + p]): a lane loads its own patient's kGT samples of a tile directly
 // (each wave instruction reads 64 consecutive doubles of one step); no LDS staging or wave sync.
 template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))  // <= 256 VGPR+AGPR
 gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
             const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, int seg, int n_seg,
             GramW w, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ ticket) {
@@ -284,6 +288,9 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
       }
     }
     const int Lm = L >= kMinMain ? L : 0;  // length on the streaming path
+    // time-major tile loads: patients of this tile inside the cohort, and the lane's byte offset
+    const int tm_valid = (int)(N - p0 < kWave ? N - p0 : kWave);
+    const unsigned tm_off = p < N ? (unsigned)lane * 8u : kOOB;
     const int Lmax = wave_max_i(Lm);
     const int s0 = sidx * seg;               // first step owned by this segment
     const int s1 = min(s0 + seg, Lmax);      // one past the last step processed
@@ -300,13 +307,16 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
       // the fact: exec-masked loads would make the compiler drain vmcnt(0) at every tile.
       auto load_tile = [&](TileRegs& v, int t0) {
         if constexpr (TM) {
-          const int64_t pc = p < N ? p : N - 1;
+          // wave-uniform descriptor over steps [t0, min(t0 + kGT, s1)) based at column p0: steps
+          // past s1 and lanes past N (out-of-range offset) read as 0
+          const int nrow = s1 - t0 < kGT ? s1 - t0 : kGT;
+          const int bytes = nrow > 0 ? (int)(((int64_t)(nrow - 1) * ldx + tm_valid) * 8) : 0;
+          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+              (void*)(x + (int64_t)(nrow > 0 ? t0 : 0) * ldx + p0), (short)0, bytes, 0x00020000);
 #pragma unroll
-          for (int i = 0; i < kGT; ++i) {
-            const bool ok = t0 + i < s1 && p < N;
-            const double q = x[(int64_t)(ok ? t0 + i : 0) * ldx + pc];
-            v[i][0] = ok ? q : 0.0;
-          }
+          for (int i = 0; i < kGT; ++i)
+            v[i][0] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                     rs, tm_off + (unsigned)(i * ldx * 8), 0, 0));
           return;
         }
         const int col = t0 + cl;
@@ -865,7 +875,6 @@ struct RolloutArgs {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-constexpr unsigned kOOB = 0x80000000u;  // buffer offset beyond every descriptor: access dropped
 
 // Per-lane arm bytes of one 32-step tile, loaded straight from the lane's own row (32 contiguous
 // bytes; AV = bytes per load instruction) through a range-checked buffer descriptor.
@@ -1473,6 +1482,7 @@ int32_t run_discovery(const double* x, int64_t ldx, int32_t layout, int32_t n_st
   if (na * lib.F > 16) lib.mfma = 0;
   unsigned* ticket = static_cast<unsigned*>(workspace);
   double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + kGramWsHeader);
+  if (tm && ldx > ((int64_t)1 << 31) / (8 * kGT)) return INSITE_E_UNSUPPORTED;  // 32-bit tile offsets
   const bool vec2 = (ldx % 2 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15u) == 0);
   const int mode = tm ? 2 : (vec2 ? 1 : 0);
   const bool smooth = fd_kind == INSITE_FD_SMOOTHED4;

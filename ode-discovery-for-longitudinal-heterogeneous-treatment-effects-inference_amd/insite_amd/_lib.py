@@ -81,6 +81,8 @@ _SIGNATURES = {
 def load(path: str | None = None):
     """Load (once) and return the ctypes handle; raises InsiteLibraryError if unavailable."""
     global _lib
+    if path is None and _lib is not None:   # lock-free fast path once loaded
+        return _lib
     with _lock:
         if _lib is not None and path is None:
             return _lib

@@ -46,7 +46,13 @@ class PolyLibrary:
         return names
 
     def ctypes_table(self) -> np.ndarray:
-        return np.ascontiguousarray(self.exps, dtype=np.int8)
+        """Contiguous int8 copy handed to the C ABI (built once per library object)."""
+        t = self.__dict__.get("_table")
+        if t is None:
+            t = np.ascontiguousarray(self.exps, dtype=np.int8)
+            t.setflags(write=False)
+            object.__setattr__(self, "_table", t)
+        return t
 
 
 def polynomial_library(n_statics: int, degree: int = 2, interaction_only: bool = True,

@@ -76,6 +76,33 @@ class Workspace:
 _WS = Workspace()
 
 
+class Plan:
+    """A prepared launch: arguments validated and packed once (tensors referenced by the plan stay
+    alive); each call enqueues the kernel(s) on the current stream of the plan's device (or the
+    given stream) with nothing but the C call left on the host path.  ``out`` holds the outputs."""
+
+    def __init__(self, fn_name: str, args: tuple, device, out):
+        self.fn_name = fn_name
+        self._fn = getattr(_lib.load(), fn_name)
+        self._args = args
+        self.device = torch.device(device)
+        self.out = out
+
+    def __call__(self, stream: torch.cuda.Stream | None = None):
+        h = (stream if stream is not None else torch.cuda.current_stream(self.device)).cuda_stream
+        st = self._fn(*self._args, ctypes.c_void_p(h))
+        if st:
+            _lib.check(self.fn_name, st)
+        return self.out
+
+
+def _run(prep):
+    name, args, dev, out = prep
+    st = getattr(_lib.load(), name)(*args, _stream(dev))
+    _lib.check(name, st)
+    return out
+
+
 def _discovery_inputs(x, u, arm, rows, lib, layout):
     """Validate the discovery inputs; returns (N, n_steps, layout code)."""
     if layout not in LAYOUTS:
@@ -98,28 +125,42 @@ def _discovery_inputs(x, u, arm, rows, lib, layout):
     return N, n_steps, LAYOUTS[layout]
 
 
+def _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout, stlsq_args=None):
+    L = _lib.load()
+    N, n_steps, lay = _discovery_inputs(x, u, arm, rows, lib, layout)
+    F = lib.n_terms
+    dev = x.device
+    nbytes = L.insite_gram_workspace_bytes(N, n_arms, F)
+    ws = (workspace or _WS).get(nbytes, dev)
+    tab = lib.ctypes_table()
+    head = (_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), _p(rows), N,
+            lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p), F, FD_KINDS[fd], float(dt))
+    if stlsq_args is None:
+        if out is None:
+            out = (torch.empty((n_arms, F, F), dtype=torch.float64, device=dev),
+                   torch.empty((n_arms, F), dtype=torch.float64, device=dev))
+        G, b = out
+        return "insite_gram_f64", head + (_p(G), _p(b), _p(ws), ws.numel()), dev, out
+    threshold, alpha, max_iter, unbias = stlsq_args
+    if out is None:
+        out = (torch.empty((n_arms, F), dtype=torch.float64, device=dev),
+               torch.empty((n_arms, F), dtype=torch.int8, device=dev),
+               torch.empty((n_arms,), dtype=torch.int32, device=dev),
+               torch.empty((n_arms, F, F), dtype=torch.float64, device=dev),
+               torch.empty((n_arms, F), dtype=torch.float64, device=dev))
+    coef, mask, iters, G, b = out
+    args = head + (float(threshold), float(alpha), int(max_iter), int(bool(unbias)), _p(G), _p(b), _p(coef),
+                   _p(mask), _p(iters), _p(ws), ws.numel())
+    return "insite_sindy_fit_f64", args, dev, out
+
+
 def gram(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor, dt: float,
          lib: PolyLibrary, n_arms: int = 2, fd: str = "smoothed4", workspace: Workspace | None = None,
          out: tuple | None = None, layout: str = "patient"):
     """Per-arm Gram G[A,F,F] and moments b[A,F] of the discovery regression (insite_gram_f64).
 
     layout "patient": x [N, T] (the reference's array); "time": x [T, >=N] (coalesced)."""
-    L = _lib.load()
-    N, n_steps, lay = _discovery_inputs(x, u, arm, rows, lib, layout)
-    F = lib.n_terms
-    if out is None:
-        G = torch.empty((n_arms, F, F), dtype=torch.float64, device=x.device)
-        b = torch.empty((n_arms, F), dtype=torch.float64, device=x.device)
-    else:
-        G, b = out
-    nbytes = L.insite_gram_workspace_bytes(N, n_arms, F)
-    ws = (workspace or _WS).get(nbytes, x.device)
-    tab = lib.ctypes_table()
-    st = L.insite_gram_f64(_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else ctypes.c_void_p(0),
-                           _p(arm), _p(rows), N, lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p), F,
-                           FD_KINDS[fd], float(dt), _p(G), _p(b), _p(ws), ws.numel(), _stream(x.device))
-    _lib.check("insite_gram_f64", st)
-    return G, b
+    return _run(_prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout))
 
 
 def sindy_fit(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor, dt: float,
@@ -129,34 +170,26 @@ def sindy_fit(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.T
     """Discovery in two launches (insite_sindy_fit_f64): Gram kernel, then the fixed-order
     reduction fused with one STLSQ fit per arm.  Replaces ``SINDy(...).fit`` per arm
     (reference sindy.py:190-192).  Returns (coef[A,F], mask[A,F], iters[A], G[A,F,F], b[A,F])."""
-    L = _lib.load()
-    N, n_steps, lay = _discovery_inputs(x, u, arm, rows, lib, layout)
-    F = lib.n_terms
-    dev = x.device
-    if out is None:
-        coef = torch.empty((n_arms, F), dtype=torch.float64, device=dev)
-        mask = torch.empty((n_arms, F), dtype=torch.int8, device=dev)
-        iters = torch.empty((n_arms,), dtype=torch.int32, device=dev)
-        G = torch.empty((n_arms, F, F), dtype=torch.float64, device=dev)
-        b = torch.empty((n_arms, F), dtype=torch.float64, device=dev)
-    else:
-        coef, mask, iters, G, b = out
-    nbytes = L.insite_gram_workspace_bytes(N, n_arms, F)
-    ws = (workspace or _WS).get(nbytes, dev)
-    tab = lib.ctypes_table()
-    st = L.insite_sindy_fit_f64(_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else ctypes.c_void_p(0),
-                                _p(arm), _p(rows), N, lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p), F,
-                                FD_KINDS[fd], float(dt), float(threshold), float(alpha), int(max_iter),
-                                int(bool(unbias)), _p(G), _p(b), _p(coef), _p(mask), _p(iters), _p(ws), ws.numel(),
-                                _stream(dev))
-    _lib.check("insite_sindy_fit_f64", st)
-    return coef, mask, iters, G, b
+    return _run(_prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout,
+                           (threshold, alpha, max_iter, unbias)))
 
 
-def stlsq(G: torch.Tensor, b: torch.Tensor, threshold: float, alpha: float, max_iter: int = 100,
-          unbias: bool = True, out: tuple | None = None):
-    """Batched STLSQ on Gram systems (insite_stlsq_f64).  G [S,F,F], b [S,F]."""
-    L = _lib.load()
+def plan_gram(x, u, arm, rows, dt, lib, n_arms=2, fd="smoothed4", workspace=None, out=None,
+              layout="patient") -> Plan:
+    """``gram`` as a prepared launch (``Plan``); ``plan.out`` = (G, b)."""
+    name, args, dev, out = _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout)
+    return Plan(name, args, dev, out)
+
+
+def plan_sindy_fit(x, u, arm, rows, dt, lib, threshold, alpha, max_iter=100, unbias=True, n_arms=2,
+                   fd="smoothed4", workspace=None, out=None, layout="patient") -> Plan:
+    """``sindy_fit`` as a prepared launch; ``plan.out`` = (coef, mask, iters, G, b)."""
+    name, args, dev, out = _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout,
+                                      (threshold, alpha, max_iter, unbias))
+    return Plan(name, args, dev, out)
+
+
+def _prep_stlsq(G, b, threshold, alpha, max_iter, unbias, out):
     _dev("G", G, torch.float64)
     _dev("b", b, torch.float64)
     F = G.shape[-1]
@@ -164,29 +197,27 @@ def stlsq(G: torch.Tensor, b: torch.Tensor, threshold: float, alpha: float, max_
     if b.numel() != S * F or not G.is_contiguous() or not b.is_contiguous():
         raise ValueError("G/b must be contiguous [S,F,F] / [S,F]")
     if out is None:
-        coef = torch.empty((S, F), dtype=torch.float64, device=G.device)
-        mask = torch.empty((S, F), dtype=torch.int8, device=G.device)
-        iters = torch.empty((S,), dtype=torch.int32, device=G.device)
-    else:
-        coef, mask, iters = out
-    st = L.insite_stlsq_f64(_p(G), _p(b), S, F, float(threshold), float(alpha), int(max_iter), int(bool(unbias)),
-                            _p(coef), _p(mask), _p(iters), _stream(G.device))
-    _lib.check("insite_stlsq_f64", st)
-    return coef, mask, iters
+        out = (torch.empty((S, F), dtype=torch.float64, device=G.device),
+               torch.empty((S, F), dtype=torch.int8, device=G.device),
+               torch.empty((S,), dtype=torch.int32, device=G.device))
+    coef, mask, iters = out
+    args = (_p(G), _p(b), S, F, float(threshold), float(alpha), int(max_iter), int(bool(unbias)), _p(coef), _p(mask),
+            _p(iters))
+    return "insite_stlsq_f64", args, G.device, out
 
 
-def rollout(y0: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, coef: torch.Tensor, lib: PolyLibrary,
-            dt: float, method: str = "euler5", substeps: int | None = None, drop_below: float = 1e-3,
-            T: int | None = None, out: torch.Tensor | None = None, layout: str = "patient"):
-    """Batched open-loop rollout (insite_rollout_f64).
+def stlsq(G: torch.Tensor, b: torch.Tensor, threshold: float, alpha: float, max_iter: int = 100,
+          unbias: bool = True, out: tuple | None = None):
+    """Batched STLSQ on Gram systems (insite_stlsq_f64).  G [S,F,F], b [S,F]."""
+    return _run(_prep_stlsq(G, b, threshold, alpha, max_iter, unbias, out))
 
-    y0 [N] f64, u [N,U] f64, coef [A,F] (global model) or [N,A,F] (per-patient).
-    layout "patient":   arm int8 [N, >=T], returns y [N,T] (the reference's [N, T] arrays).
-    layout "time":      arm int8 [T, >=N], returns y [T,N] (one contiguous run per step).
-    layout "time_bits": arm int32 [T, >=ceil(N/32)] bitmask (pack_arm_bits; A <= 2), y [T,N] —
-                        the fast layout on MI355X (DESIGN.md).  Row k of y is the state after
-                        observation interval k."""
-    L = _lib.load()
+
+def plan_stlsq(G, b, threshold, alpha, max_iter=100, unbias=True, out=None) -> Plan:
+    name, args, dev, out = _prep_stlsq(G, b, threshold, alpha, max_iter, unbias, out)
+    return Plan(name, args, dev, out)
+
+
+def _prep_rollout(y0, u, arm, coef, lib, dt, method, substeps, drop_below, T, out, layout):
     if layout not in ROLLOUT_LAYOUTS:
         raise ValueError(f"layout must be one of {sorted(ROLLOUT_LAYOUTS)}")
     tm = layout != "patient"
@@ -237,12 +268,31 @@ def rollout(y0: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, coef: torch.Te
         if out.size(0) != shape[0] or out.size(1) < shape[1]:
             raise ValueError(f"out must be {shape}")
     tab = lib.ctypes_table()
-    st = L.insite_rollout_f64(_p(y0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), arm.stride(0),
-                              _p(coef), stride, tab.ctypes.data_as(ctypes.c_void_p), F, N, T, lib.n_statics, A,
-                              float(dt), m, sub, float(drop_below), _p(out), out.stride(0), ROLLOUT_LAYOUTS[layout],
-                              _stream(y0.device))
-    _lib.check("insite_rollout_f64", st)
-    return out
+    args = (_p(y0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), arm.stride(0), _p(coef), stride,
+            tab.ctypes.data_as(ctypes.c_void_p), F, N, T, lib.n_statics, A, float(dt), m, sub, float(drop_below),
+            _p(out), out.stride(0), ROLLOUT_LAYOUTS[layout])
+    return "insite_rollout_f64", args, y0.device, out
+
+
+def rollout(y0: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, coef: torch.Tensor, lib: PolyLibrary,
+            dt: float, method: str = "euler5", substeps: int | None = None, drop_below: float = 1e-3,
+            T: int | None = None, out: torch.Tensor | None = None, layout: str = "patient"):
+    """Batched open-loop rollout (insite_rollout_f64).
+
+    y0 [N] f64, u [N,U] f64, coef [A,F] (global model) or [N,A,F] (per-patient).
+    layout "patient":   arm int8 [N, >=T], returns y [N,T] (the reference's [N, T] arrays).
+    layout "time":      arm int8 [T, >=N], returns y [T,N] (one contiguous run per step).
+    layout "time_bits": arm int32 [T, >=ceil(N/32)] bitmask (pack_arm_bits; A <= 2), y [T,N] —
+                        the fast layout on MI355X (DESIGN.md).  Row k of y is the state after
+                        observation interval k."""
+    return _run(_prep_rollout(y0, u, arm, coef, lib, dt, method, substeps, drop_below, T, out, layout))
+
+
+def plan_rollout(y0, u, arm, coef, lib, dt, method="euler5", substeps=None, drop_below=1e-3, T=None, out=None,
+                 layout="patient") -> Plan:
+    """``rollout`` as a prepared launch; ``plan.out`` = y."""
+    name, args, dev, out = _prep_rollout(y0, u, arm, coef, lib, dt, method, substeps, drop_below, T, out, layout)
+    return Plan(name, args, dev, out)
 
 
 def masked_sse(pred: torch.Tensor, target: torch.Tensor, active: torch.Tensor, scale: float = 1.0,
