@@ -12,7 +12,8 @@
  *                                                                   + insite_stlsq_f64
  *   - STLSQ._reduce / LSQIntialMask (per-patient initial-mask refit)
  *       libs_m/ct/src/data/pkpd/utils.py:183-327;
- *       pkpd_simulation.py:791-800                               -> insite_stlsq_f64 (n_sys = N)
+ *       pkpd_simulation.py:791-800                  -> insite_sindy_fit_per_patient_f64,
+ *                                                      insite_stlsq_f64 (n_sys = N)
  *   - jit(vmap(simulate_cancer_volume))(y0, treatments, dt, statics) with the Euler-5
  *       odeint (libs_m/ct/src/models/sindy.py:413-431; pkpd/utils.py:68-94)
  *                                                                -> insite_rollout_f64
@@ -123,6 +124,26 @@ int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, int32_t layout, int32
                              double threshold, double alpha, int32_t max_iter, int32_t unbias,
                              double* G_out, double* b_out, double* coef_out, int8_t* mask_out,
                              int32_t* iters_out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Per-patient refit (reference LSQIntialMask, pkpd/utils.py:183-327,
+ * as used by determine_individualized_equation_coefs, pkpd_simulation.py:791-800): for every patient
+ * with >= 5 rows, STLSQ on its own rows (same derivative estimator and library as
+ * insite_gram_f64) starting from the support of global_coef[arm[p]] (|c| > 1e-14); unbias = the
+ * minimum-norm least-squares solution on the final support (lstsq semantics; with constant statics a
+ * patient's Theta has rank <= 2); if sum |c| > 10 the last ridge iterate is kept (the reference's
+ * unbias=False refit).  Other arms keep the global rows; patients with < 5 rows keep the global
+ * model (iters 0).  Inputs as insite_gram_f64, plus
+ *   global_coef [n_arms, F] f64 (device); coef_out [n_patients, n_arms, F] f64 (feeds
+ *   insite_rollout_f64 with coef_row_stride = n_arms * F); mask_out [n_patients, F] int8 (may be
+ *   NULL); iters_out [n_patients] int32 (may be NULL).                                          */
+size_t insite_per_patient_workspace_bytes(int64_t n_patients);
+int32_t insite_sindy_fit_per_patient_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps,
+                                         const double* u, const int8_t* arm, const int32_t* rows,
+                                         int64_t n_patients, int32_t n_statics, int32_t n_arms, const int8_t* exps,
+                                         int32_t n_terms, int32_t fd_kind, double dt, const double* global_coef,
+                                         double threshold, double alpha, int32_t max_iter, int32_t unbias,
+                                         double* coef_out, int8_t* mask_out, int32_t* iters_out, void* workspace,
+                                         size_t workspace_bytes, void* stream);
 
 /* Batched sequentially-thresholded least squares on Gram systems (one system per thread):
  * STLSQ._reduce semantics (all-ones initial support; ridge (G_SS + alpha I) c = b_S by

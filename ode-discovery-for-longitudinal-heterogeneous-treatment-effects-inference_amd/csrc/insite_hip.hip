@@ -223,7 +223,10 @@ __device__ __forceinline__ void tele_lo(const GramW& w, double vm2, double vm1, 
 // when the library fits (lib.mfma), else one Gram entry per lane.
 // TM (time-major x[k * ldx + p]): a lane loads its own patient's kGT samples of a tile directly
 // (each wave instruction reads 64 consecutive doubles of one step); no LDS staging or wave sync.
-template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM>
+// MOM: per-patient moments mode (one time segment per patient): instead of the Gram contraction
+// every lane writes its patient's moments {L, sum xs, sum xs^2, sum xdot, sum xdot xs} to
+// partial[p * 5 ..] (insite_sindy_fit_per_patient_f64).
+template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))  // <= 256 VGPR+AGPR
 gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
             const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, int seg, int n_seg,
@@ -564,6 +567,17 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
       }
     }
     if (s0 >= Lmax && !(SMOOTH && sidx == 0)) continue;  // nothing owned by this work item (uniform)
+    if constexpr (MOM) {
+      if (p < N) {
+        double* mrow = partial + p * 5;
+        mrow[0] = (double)L;
+        mrow[1] = Sx;
+        mrow[2] = Sxx;
+        mrow[3] = Sd;
+        mrow[4] = Sdx;
+      }
+      continue;
+    }
 #ifdef INSITE_ABLATE_NOGPHASE
     acc[0] += Sx + Sxx + Sd + Sdx;
     continue;
@@ -635,6 +649,7 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
   }
 
   // ---- block reduction (fixed order) -> partial[block][...] ----
+  if constexpr (MOM) return;
   __syncthreads();
   double* red = smem;
   if constexpr (MFMA) {
@@ -722,9 +737,13 @@ __device__ bool masked_cholesky_solve(const double (&g)[F][F], const double (&rh
 // and the unbias solve.  Returns the iteration count, -1 if a solve was not positive definite.
 template <int F>
 __device__ int stlsq_solve(const double (&g)[F][F], const double (&rhs)[F], double thr, double alpha,
-                           int max_iter, int unbias, double (&c)[F], unsigned& sup) {
+                           int max_iter, int unbias, double (&c)[F], unsigned& sup,
+                           unsigned init = (1u << F) - 1u) {
+  // init: initial support (all ones = pysindy BaseOptimizer; a global model's support =
+  // LSQIntialMask, pkpd/utils.py:250-253).  The stop rule compares the support size with the
+  // initial one (:308) and the pattern with the previous iterate (history_[0] = full lstsq guess).
   const unsigned all = (1u << F) - 1u;
-  unsigned ind = all, prev = all;
+  unsigned ind = init, prev = all;
   bool ok = true;
   int it = 0;
 #pragma unroll
@@ -748,7 +767,7 @@ __device__ int stlsq_solve(const double (&g)[F][F], const double (&rhs)[F], doub
 #pragma unroll
     for (int i = 0; i < F; ++i)
       if (c[i] != 0.0) pattern |= 1u << i;
-    if (ind == all || pattern == prev) break;
+    if (ind == init || pattern == prev) break;
     prev = pattern;
   }
   sup = 0u;
@@ -857,6 +876,127 @@ discovery_finalize(const double* __restrict__ partial, int nblk, int narm_pad, i
       if (iters) iters[arm_i] = it;
     }
   }
+}
+
+// Per-patient refit (LSQIntialMask per patient, pkpd_simulation.py:791-800):
+// thread = patient.  Its Gram G_p = A(u) M A(u)^T and moments b_p come from the five moments the
+// MOM pass wrote; STLSQ starts from the support of the global model of the patient's arm.  The
+// unbias is the minimum-norm least-squares solution (what lstsq returns): with one patient the
+// statics are constant, so Theta_p = [m_j(u) x^{e_j}] has rank <= 2 and the fitted RHS is
+// alpha + beta x; (alpha, beta) solve the 1x1 / 2x2 moment system of the support's exponent
+// groups and c_j = m_j * alpha / sum m_k^2 (e_j = 0), m_j * beta / sum m_k^2 (e_j = 1).  If
+// sum |c| > 10 the reference refits without unbias (:795-798): the last ridge iterate is kept.
+// Other arms keep the global coefficients; patients with < 5 rows keep the global model.
+template <int F>
+__global__ void __launch_bounds__(kBlock)
+patient_fit_kernel(const double* __restrict__ mom, const double* __restrict__ u, const int8_t* __restrict__ arm,
+                   const int32_t* __restrict__ rows, int64_t N, int n_steps, int n_arms, LibDesc lib,
+                   const double* __restrict__ gcoef, StlsqParams sp, double* __restrict__ coef,
+                   int8_t* __restrict__ mask, int32_t* __restrict__ iters) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= N) return;
+  const int a = arm[p];
+  int L = rows[p];
+  if (L > n_steps) L = n_steps;
+  for (int aa = 0; aa < n_arms; ++aa)
+#pragma unroll
+    for (int j = 0; j < F; ++j) coef[(p * n_arms + aa) * F + j] = gcoef[aa * F + j];
+  if (a < 0 || a >= n_arms) {
+    if (iters) iters[p] = -2;
+    return;
+  }
+  unsigned init = 0u;
+#pragma unroll
+  for (int j = 0; j < F; ++j)
+    if (fabs(gcoef[a * F + j]) > 1e-14) init |= 1u << j;
+  if (L < 5) {
+    if (mask) {
+#pragma unroll
+      for (int j = 0; j < F; ++j) mask[p * F + j] = (int8_t)((init >> j) & 1u);
+    }
+    if (iters) iters[p] = 0;
+    return;
+  }
+  double uu[INSITE_MAX_STATICS];
+#pragma unroll
+  for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < lib.U ? u[p * lib.U + t] : 0.0;
+  const double M[3] = {mom[p * 5 + 0], mom[p * 5 + 1], mom[p * 5 + 2]};
+  const double Sd = mom[p * 5 + 3], Sdx = mom[p * 5 + 4];
+  double m[F], g[F][F], rhs[F], c[F];
+  int e[F];
+#pragma unroll
+  for (int j = 0; j < F; ++j) {
+    m[j] = monomial(lib, j, uu);
+    e[j] = lib.ex[j];
+  }
+#pragma unroll
+  for (int i = 0; i < F; ++i) {
+    rhs[i] = m[i] * (e[i] ? Sdx : Sd);
+#pragma unroll
+    for (int j = 0; j <= i; ++j) g[i][j] = m[i] * m[j] * M[e[i] + e[j]];
+  }
+  unsigned sup = 0u;
+  int it = stlsq_solve<F>(g, rhs, sp.thr, sp.alpha, sp.max_iter, 0, c, sup, init);
+  if (sp.unbias && sup) {
+    double n0 = 0.0, n1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < F; ++j)
+      if ((sup >> j) & 1u) {
+        if (e[j]) n1 += m[j] * m[j];
+        else n0 += m[j] * m[j];
+      }
+    const bool h0 = n0 > 0.0, h1 = n1 > 0.0;
+    double al = 0.0, be = 0.0, cu[F];
+    bool rank1 = false;
+    if (h0 && h1) {
+      const double det = M[0] * M[2] - M[1] * M[1];
+      if (det > 1e-13 * M[0] * M[2]) {
+        al = (Sd * M[2] - M[1] * Sdx) / det;
+        be = (M[0] * Sdx - M[1] * Sd) / det;
+      } else {
+        rank1 = true;  // x constant: every support column ~ m_j x0^{e_j}
+      }
+    } else if (h0) {
+      al = Sd / M[0];
+    } else if (h1 && M[2] > 0.0) {
+      be = Sdx / M[2];
+    }
+    double s1 = 0.0;
+    if (rank1) {
+      const double x0 = M[1] / M[0];
+      double vv = 0.0;
+#pragma unroll
+      for (int j = 0; j < F; ++j)
+        if ((sup >> j) & 1u) vv += (m[j] * (e[j] ? x0 : 1.0)) * (m[j] * (e[j] ? x0 : 1.0));
+      const double tq = vv > 0.0 ? Sd / (M[0] * vv) : 0.0;
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        cu[j] = ((sup >> j) & 1u) ? m[j] * (e[j] ? x0 : 1.0) * tq : 0.0;
+        s1 += fabs(cu[j]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        cu[j] = ((sup >> j) & 1u) ? (e[j] ? (h1 ? m[j] * be / n1 : 0.0) : (h0 ? m[j] * al / n0 : 0.0)) : 0.0;
+        s1 += fabs(cu[j]);
+      }
+    }
+    if (s1 <= 10.0) {
+#pragma unroll
+      for (int j = 0; j < F; ++j) c[j] = cu[j];
+    }
+  }
+  unsigned fin = 0u;
+#pragma unroll
+  for (int j = 0; j < F; ++j) {
+    coef[(p * n_arms + a) * F + j] = c[j];
+    if (fabs(c[j]) > 1e-14) fin |= 1u << j;
+  }
+  if (mask) {
+#pragma unroll
+    for (int j = 0; j < F; ++j) mask[p * F + j] = (int8_t)((fin >> j) & 1u);
+  }
+  if (iters) iters[p] = it;
 }
 
 // =============================================================================================
@@ -1435,10 +1575,20 @@ struct GramLaunch {
   unsigned* ticket;
 };
 
-template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM>
+template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM = false>
 int launch_gram4(hipStream_t st, const GramLaunch& g) {
-  auto kern = gram_kernel<VEC, NARM, SMOOTH, MFMA, TM>;
-  const GramPlan pl = gram_plan(g.N, g.n_steps, resident_waves(kern));
+  auto kern = gram_kernel<VEC, NARM, SMOOTH, MFMA, TM, MOM>;
+  GramPlan pl = gram_plan(g.N, g.n_steps, resident_waves(kern));
+  if constexpr (MOM) {  // one segment per patient: the lane holds the patient's complete moments
+    const int64_t tiles = (g.N + kWave - 1) / kWave;
+    const int64_t gres = resident_waves(kern) / kWavesPerBlock;
+    int64_t gb = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (gb > gres && gres > 0) gb = gres;
+    pl.grid = (int)(gb < 1 ? 1 : gb);
+    pl.n_seg = 1;
+    pl.seg = (int)((g.n_steps + kGT - 1) / kGT * kGT);
+    if (pl.seg < kGT) pl.seg = kGT;
+  }
   kern<<<dim3(pl.grid), kBlock, 0, st>>>(g.x, g.ldx, g.n_steps, g.u, g.arm, g.rows, g.N, pl.seg, pl.n_seg, g.w,
                                           g.lib, g.part, g.ticket);
   return pl.grid;
@@ -1457,6 +1607,24 @@ int launch_gram(int mode, bool smooth, hipStream_t st, const GramLaunch& g) {
     return smooth ? launch_gram3<NARM, true, true>(mode, st, g) : launch_gram3<NARM, false, true>(mode, st, g);
   }
   return smooth ? launch_gram3<NARM, true, false>(mode, st, g) : launch_gram3<NARM, false, false>(mode, st, g);
+}
+
+inline GramW make_gram_w(double dt) {
+  GramW w;
+  w.sg0 = 17.0 / 35.0;  // savgol(5,3) interior taps [-3, 12, 17, 12, -3] / 35
+  w.sg1 = 12.0 / 35.0;
+  w.sg2 = -3.0 / 35.0;
+  w.inv_dt = 1.0 / dt;
+  w.fd1 = (2.0 / 3.0) * w.inv_dt;  // 5-point first derivative [1, -8, 0, 8, -1] / 12 dt
+  w.fd2 = (-1.0 / 12.0) * w.inv_dt;
+  return w;
+}
+
+template <bool SMOOTH>
+int launch_moments(int mode, hipStream_t st, const GramLaunch& g) {
+  if (mode == 2) return launch_gram4<1, 1, SMOOTH, false, true, true>(st, g);
+  if (mode == 1) return launch_gram4<2, 1, SMOOTH, false, false, true>(st, g);
+  return launch_gram4<1, 1, SMOOTH, false, false, true>(st, g);
 }
 
 // gram kernel + fused finalize (+ STLSQ when sp.enabled)
@@ -1487,14 +1655,7 @@ int32_t run_discovery(const double* x, int64_t ldx, int32_t layout, int32_t n_st
   const int mode = tm ? 2 : (vec2 ? 1 : 0);
   const bool smooth = fd_kind == INSITE_FD_SMOOTHED4;
   if (n_statics == 0) u = x;  // kernels load u unconditionally (values unused when U = 0)
-  GramW w;
-  w.sg0 = 17.0 / 35.0;
-  w.sg1 = 12.0 / 35.0;
-  w.sg2 = -3.0 / 35.0;
-  w.inv_dt = 1.0 / dt;
-  w.fd1 = (2.0 / 3.0) * w.inv_dt;
-  w.fd2 = (-1.0 / 12.0) * w.inv_dt;
-  const GramLaunch g{x, ldx, n_steps, u, arm, rows, n_patients, w, lib, part, ticket};
+  const GramLaunch g{x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, part, ticket};
   int grid = 1;
   if (na == 1) grid = launch_gram<1>(mode, smooth, hs, g);
   else if (na == 2) grid = launch_gram<2>(mode, smooth, hs, g);
@@ -1674,6 +1835,67 @@ int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, int32_t layout, int32
   StlsqParams sp{threshold, alpha, max_iter, unbias, 1};
   return run_discovery(x, ldx, layout, n_steps, u, arm, rows, n_patients, n_statics, n_arms, exps, n_terms, fd_kind,
                        dt, G_out, b_out, workspace, workspace_bytes, stream, sp, coef_out, mask_out, iters_out);
+}
+
+size_t insite_per_patient_workspace_bytes(int64_t n_patients) {
+  if (n_patients < 0) return 0;
+  return kGramWsHeader + (size_t)n_patients * 5 * sizeof(double);
+}
+
+int32_t insite_sindy_fit_per_patient_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps,
+                                         const double* u, const int8_t* arm, const int32_t* rows,
+                                         int64_t n_patients, int32_t n_statics, int32_t n_arms, const int8_t* exps,
+                                         int32_t n_terms, int32_t fd_kind, double dt, const double* global_coef,
+                                         double threshold, double alpha, int32_t max_iter, int32_t unbias,
+                                         double* coef_out, int8_t* mask_out, int32_t* iters_out, void* workspace,
+                                         size_t workspace_bytes, void* stream) {
+  const bool tm = layout == INSITE_LAYOUT_TIME_MAJOR;
+  if (layout != INSITE_LAYOUT_PATIENT_MAJOR && !tm) return INSITE_E_INVALID_ARG;
+  if (n_patients < 0 || n_arms < 1 || n_arms > INSITE_MAX_ARMS || ldx < 1 || !(dt > 0.0) || n_steps < 0 ||
+      (tm ? ldx < n_patients : ldx < n_steps) || max_iter < 0 || !(threshold >= 0.0) || !(alpha >= 0.0))
+    return INSITE_E_INVALID_ARG;
+  if (n_patients == 0) return INSITE_OK;
+  if (!x || !arm || !rows || !global_coef || !coef_out || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
+  if (fd_kind != INSITE_FD_SMOOTHED4 && fd_kind != INSITE_FD_ORDER4) return INSITE_E_UNSUPPORTED;
+  if (tm && ldx > ((int64_t)1 << 31) / (8 * kGT)) return INSITE_E_UNSUPPORTED;
+  LibDesc lib;
+  int32_t st = build_lib(exps, n_terms, n_statics, &lib);
+  if (st != INSITE_OK) return st;
+  if (!workspace || workspace_bytes < insite_per_patient_workspace_bytes(n_patients)) return INSITE_E_WORKSPACE;
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  unsigned* ticket = static_cast<unsigned*>(workspace);
+  double* mom = reinterpret_cast<double*>(static_cast<char*>(workspace) + kGramWsHeader);
+  const bool vec2 = (ldx % 2 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15u) == 0);
+  const int mode = tm ? 2 : (vec2 ? 1 : 0);
+  if (n_statics == 0) u = x;
+  lib.mfma = 0;
+  const GramLaunch g{x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, mom, ticket};
+  if (fd_kind == INSITE_FD_SMOOTHED4) launch_moments<true>(mode, hs, g);
+  else launch_moments<false>(mode, hs, g);
+  st = launch_status();
+  if (st != INSITE_OK) return st;
+  const StlsqParams sp{threshold, alpha, max_iter, unbias, 1};
+  const dim3 grid((unsigned)((n_patients + kBlock - 1) / kBlock));
+  switch (n_terms) {
+#define INSITE_PP_CASE(FF)                                                                                      \
+  case FF:                                                                                                     \
+    patient_fit_kernel<FF><<<grid, kBlock, 0, hs>>>(mom, u, arm, rows, n_patients, n_steps, n_arms, lib,        \
+                                                    global_coef, sp, coef_out, mask_out, iters_out);           \
+    break;
+    INSITE_PP_CASE(1)
+    INSITE_PP_CASE(2)
+    INSITE_PP_CASE(3)
+    INSITE_PP_CASE(4)
+    INSITE_PP_CASE(5)
+    INSITE_PP_CASE(6)
+    INSITE_PP_CASE(7)
+    INSITE_PP_CASE(8)
+    INSITE_PP_CASE(9)
+#undef INSITE_PP_CASE
+    default:
+      return INSITE_E_UNSUPPORTED;
+  }
+  return launch_status();
 }
 
 int32_t insite_stlsq_f64(const double* G, const double* b, int64_t n_sys, int32_t n_terms,

@@ -36,6 +36,8 @@ EXPORTS = (
     "insite_gram_workspace_bytes",
     "insite_gram_f64",
     "insite_sindy_fit_f64",
+    "insite_per_patient_workspace_bytes",
+    "insite_sindy_fit_per_patient_f64",
     "insite_stlsq_f64",
     "insite_rollout_f64",
     "insite_masked_sse_workspace_bytes",
@@ -69,6 +71,10 @@ _SIGNATURES = {
                                       _c_i32, _c_i32,
                                       _c_f64, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _c_size,
                                       _vp]),
+    "insite_per_patient_workspace_bytes": (_c_size, [_c_i64]),
+    "insite_sindy_fit_per_patient_f64": (_c_i32, [_vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32,
+                                                  _vp, _c_i32, _c_i32, _c_f64, _vp, _c_f64, _c_f64, _c_i32, _c_i32,
+                                                  _vp, _vp, _vp, _vp, _c_size, _vp]),
     "insite_stlsq_f64": (_c_i32, [_vp, _vp, _c_i64, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _vp]),
     "insite_rollout_f64": (_c_i32, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _vp, _c_i32, _c_i64, _c_i32, _c_i32,
                                     _c_i32, _c_f64, _c_i32, _c_i32, _c_f64, _vp, _c_i64, _c_i32, _vp]),

@@ -189,6 +189,34 @@ def plan_sindy_fit(x, u, arm, rows, dt, lib, threshold, alpha, max_iter=100, unb
     return Plan(name, args, dev, out)
 
 
+def sindy_fit_per_patient(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor, dt: float,
+                          lib: PolyLibrary, global_coef: torch.Tensor, threshold: float, alpha: float,
+                          max_iter: int = 100, unbias: bool = True, fd: str = "smoothed4",
+                          workspace: Workspace | None = None, out: tuple | None = None, layout: str = "patient"):
+    """Per-patient refit from the global model's support (insite_sindy_fit_per_patient_f64;
+    reference LSQIntialMask per patient, pkpd_simulation.py:791-800).  Returns
+    (coef[N, A, F] — the patient's own arm refit, other arms global —, mask[N, F], iters[N])."""
+    L = _lib.load()
+    N, n_steps, lay = _discovery_inputs(x, u, arm, rows, lib, layout)
+    _dev("global_coef", global_coef, torch.float64, 2)
+    A, F = global_coef.shape
+    if F != lib.n_terms or not global_coef.is_contiguous():
+        raise ValueError("global_coef must be a contiguous [n_arms, F] tensor")
+    dev = x.device
+    if out is None:
+        out = (torch.empty((N, A, F), dtype=torch.float64, device=dev),
+               torch.empty((N, F), dtype=torch.int8, device=dev),
+               torch.empty((N,), dtype=torch.int32, device=dev))
+    coef, mask, iters = out
+    ws = (workspace or _WS).get(L.insite_per_patient_workspace_bytes(N), dev)
+    tab = lib.ctypes_table()
+    args = (_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), _p(rows), N,
+            lib.n_statics, A, tab.ctypes.data_as(ctypes.c_void_p), F, FD_KINDS[fd], float(dt), _p(global_coef),
+            float(threshold), float(alpha), int(max_iter), int(bool(unbias)), _p(coef), _p(mask), _p(iters), _p(ws),
+            ws.numel())
+    return _run(("insite_sindy_fit_per_patient_f64", args, dev, out))
+
+
 def _prep_stlsq(G, b, threshold, alpha, max_iter, unbias, out):
     _dev("G", G, torch.float64)
     _dev("b", b, torch.float64)

@@ -555,6 +555,71 @@ def stlsq(Theta, y, threshold, alpha, max_iter=100, unbias=True):
     return coef, ind, it
 
 
+def stlsq_initial_mask(Theta, y, threshold, alpha, init_coef, max_iter=100, unbias=True):
+    """``LSQIntialMask`` (pkpd/utils.py:183-327) as used per patient by
+    ``determine_individualized_equation_coefs`` (pkpd_simulation.py:791-800): the initial support is
+    |global coef| > 1e-14 (:250-253), the stop rule compares the support size with the INITIAL one
+    (:308) and the pattern with the previous history entry (:234-241; history_[0] is the full lstsq
+    guess, all non-zero); then the unbias refit — unless sum|c| > 10, where the reference refits with
+    unbias=False (:795-798), i.e. keeps the last thresholded ridge iterate.  Returns (coef, ind, it)."""
+    F = Theta.shape[1]
+    init = np.abs(np.asarray(init_coef, dtype=np.float64)) > SUPPORT_EPS
+    ind = init.copy()
+    n_sel0 = int(init.sum())
+    prev_pattern = np.ones(F, dtype=bool)
+    coef = np.zeros(F)
+    it = 0
+    for k in range(max_iter):
+        it = k + 1
+        if not ind.any():
+            coef = np.zeros(F)
+            break
+        c_act = ridge_cholesky(Theta[:, ind], y, alpha)
+        c = np.zeros(F)
+        c[ind] = c_act
+        big = np.abs(c) >= threshold
+        c[~big] = 0.0
+        coef = c
+        ind = big
+        pattern = coef != 0
+        if int(ind.sum()) == n_sel0 or np.array_equal(pattern, prev_pattern):
+            break
+        prev_pattern = pattern
+    ridge = coef
+    sup = np.abs(coef) > SUPPORT_EPS
+    if unbias and sup.any():
+        out = np.zeros(F)
+        out[sup] = np.linalg.lstsq(Theta[:, sup], y, rcond=None)[0]
+        if np.abs(out).sum() > 10.0:
+            out = ridge
+        coef = out
+    return coef, np.abs(coef) > SUPPORT_EPS, it
+
+
+def per_patient_fit(x, u, arm, rows, dt, exps, global_coef, threshold, alpha, max_iter=100, fd="smoothed4"):
+    """Per-patient refit: every patient with >= 5 rows refits its own
+    arm's equation on its own rows with the initial support of the global model
+    (``stlsq_initial_mask``); the other arms keep the global coefficients.  Patients with < 5 rows
+    keep the global model (pysindy would raise).  Returns coef[N, A, F], mask[N, F], iters[N]."""
+    N = x.shape[0]
+    A, F = global_coef.shape
+    coef = np.repeat(np.asarray(global_coef, dtype=np.float64)[None], N, axis=0)
+    mask = np.zeros((N, F), dtype=np.int8)
+    iters = np.zeros(N, dtype=np.int32)
+    for i in range(N):
+        a = int(arm[i])
+        L = int(rows[i])
+        if L < 5:
+            mask[i] = np.abs(global_coef[a]) > SUPPORT_EPS
+            continue
+        Z, Y = build_regression([x[i, :L].reshape(-1, 1)], [np.repeat(u[i][None, :], L, 0)], dt, fd)
+        c, ind, it = stlsq_initial_mask(eval_library(exps, Z), Y, threshold, alpha, global_coef[a], max_iter)
+        coef[i, a] = c
+        mask[i] = ind
+        iters[i] = it
+    return coef, mask, iters
+
+
 def stlsq_gram(G, b, threshold, alpha, max_iter=100, unbias=True):
     """The same algorithm expressed on the Gram G = Theta^T Theta and moment b = Theta^T y
     (the form the GPU path uses; unbias via the normal equations)."""

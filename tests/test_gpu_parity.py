@@ -447,3 +447,83 @@ def test_cohort_layouts_identical_trajectories(dev):
     torch.cuda.synchronize()
     assert torch.equal(a.x[:, :33], b.x[:, :1001].t())
     assert torch.equal(a.y0, b.y0)
+
+
+# ----------------------------------------------------------------------- per-patient refit (A5)
+@pytest.mark.parametrize("layout", LAYOUTS)
+@pytest.mark.parametrize("eq", ["EQ_4_A", "EQ_4_C"])
+def test_per_patient_fit_matches_oracle(dev, eq, layout):
+    """LSQIntialMask per patient from the global support: identical supports and iteration counts,
+    coefficients L-inf < 1e-8 (the unbias is lstsq's minimum-norm solution of a rank <= 2 system)."""
+    from insite_amd import ops
+    g = _golden(f"discovery_{eq.lower()}.npz")
+    lib = _lib()
+    exps = lib.exps.astype(np.int64)
+    dt = float(g["dt"])
+    c_ref, m_ref, it_ref = R.per_patient_fit(g["x"], g["u"], g["arm"], g["rows"], dt, exps, g["coef"], 0.1, 0.5)
+    coef, mask, iters = ops.sindy_fit_per_patient(_x_layout(g["x"], layout, dev), _t(g["u"], dev),
+                                                  _t(g["arm"], dev, torch.int8), _t(g["rows"], dev, torch.int32), dt,
+                                                  lib, _t(g["coef"], dev), 0.1, 0.5, layout=layout)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mask.cpu().numpy(), m_ref)
+    np.testing.assert_array_equal(iters.cpu().numpy(), it_ref)
+    assert np.max(np.abs(coef.cpu().numpy() - c_ref)) < COEF_TOL
+
+
+def test_per_patient_fit_ragged_short_and_large_coefficients(dev):
+    """Rows < 5 keep the global model; a fast-growing patient (|beta| > 10) keeps the ridge
+    iterate (the reference's unbias=False refit); the rest refit from the global support."""
+    from insite_amd import ops
+    rng = np.random.default_rng(21)
+    N, T = 40, 50
+    dt = 0.02
+    t = np.arange(T) * dt
+    u = rng.normal(0.5, 0.05, (N, 2))
+    arm = rng.integers(0, 2, N)
+    # a fast-growing patient (|beta| > 10) with a well-posed collinear ridge system: the near-null
+    # eigenvalue of G + alpha I is alpha plus rounding noise ~eps * lambda_max, so lambda_max must stay
+    # far below alpha / eps (at x ~ 1e7 any two fp64 evaluations, the reference's included, disagree
+    # at the percent level)
+    # (amplitude 1e-3 for that patient: beta is scale-free, the Gram's magnitude is not)
+    rate = np.where(np.arange(N) == 3, 12.0, -rng.uniform(0.3, 1.0, N))
+    amp = np.where(np.arange(N) == 3, 1e-3, rng.uniform(1, 5, N))
+    x = amp[:, None] * (np.exp(rate[:, None] * t[None, :]) + 1e-3 * rng.normal(size=(N, T)))
+    rows = rng.integers(3, T + 1, N)
+    rows[3] = T
+    lib = _lib()
+    gcoef = np.zeros((2, lib.n_terms))
+    gcoef[:, 1] = -0.5        # support {x0} for both arms
+    gcoef[1, 4] = 0.2         # arm 1: {x0, x0 u0}
+    c_ref, m_ref, it_ref = R.per_patient_fit(x, u, arm, rows, dt, lib.exps.astype(np.int64), gcoef, 0.1, 0.5)
+    assert np.abs(c_ref[3, arm[3]]).sum() > 10      # the large-coefficient branch is exercised
+    coef, mask, iters = ops.sindy_fit_per_patient(_t(x, dev), _t(u, dev), _t(arm, dev, torch.int8),
+                                                  _t(rows, dev, torch.int32), dt, lib, _t(gcoef, dev), 0.1, 0.5)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mask.cpu().numpy(), m_ref)
+    np.testing.assert_array_equal(iters.cpu().numpy(), it_ref)
+    np.testing.assert_allclose(coef.cpu().numpy(), c_ref, rtol=1e-9, atol=1e-9)
+    short = rows < 5
+    assert short.any()
+    np.testing.assert_array_equal(coef.cpu().numpy()[short], np.repeat(gcoef[None], short.sum(), 0))
+
+
+def test_per_patient_rollout_end_to_end(dev):
+    """Global fit -> per-patient refit -> per-patient rollout (config C4 chain) vs the oracle."""
+    from insite_amd import ops
+    g = _golden("discovery_eq_4_c.npz")
+    lib = _lib()
+    exps = lib.exps.astype(np.int64)
+    dt = float(g["dt"])
+    xd, ud = _t(g["x"], dev), _t(g["u"], dev)
+    armd, rowsd = _t(g["arm"], dev, torch.int8), _t(g["rows"], dev, torch.int32)
+    coef, _, _, _, _ = ops.sindy_fit(xd, ud, armd, rowsd, dt, lib, 0.1, 0.5)
+    pc, _, _ = ops.sindy_fit_per_patient(xd, ud, armd, rowsd, dt, lib, coef, 0.1, 0.5)
+    T = 40
+    rng = np.random.default_rng(2)
+    arms = rng.integers(0, 2, (g["x"].shape[0], T)).astype(np.int8)
+    y = ops.rollout(xd[:, 0].contiguous(), ud, _t(arms, dev, torch.int8), pc, lib, dt, method="euler5", T=T)
+    torch.cuda.synchronize()
+    c_ref, _, _ = R.per_patient_fit(g["x"], g["u"], g["arm"], g["rows"], dt, exps, coef.cpu().numpy(), 0.1, 0.5)
+    y_ref = R.rollout(g["x"][:, 0], g["u"], arms, c_ref, exps, dt, "euler5")
+    yg = y.cpu().numpy()
+    assert np.sqrt(np.mean((yg - y_ref) ** 2)) <= RMSE_TOL
