@@ -46,8 +46,9 @@ def parse():
     ap.add_argument("--arm-format", default="bits", choices=["bits", "int8"],
                     help="per-step arms of the time-major rollout: 1-bit mask (A <= 2) or int8")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
-                    help="run discovery and rollout of consecutive steps strictly in sequence on one stream")
+    ap.add_argument("--mode", default="seq", choices=["graph", "seq", "pipeline"],
+                    help="graph: one step captured in a HIP graph and replayed; seq: eager launches on one "
+                         "stream; pipeline: discovery of step i+1 overlaps the rollout of step i (two streams)")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
@@ -131,15 +132,19 @@ def main():
     iters = torch.empty((2,), dtype=torch.int32, device=dev)
     y = torch.empty((T, N) if args.layout == "time" else (N, T), dtype=torch.float64, device=dev)
     ws = ops.Workspace()
+    mode = args.mode if (world == 1 or args.mode != "graph") else "seq"   # RCCL stays outside graphs
     s_disc = torch.cuda.current_stream(dev)
-    s_roll = torch.cuda.Stream(dev) if args.pipeline else s_disc
-    ev_roll, ev_disc = [], []
+    s_roll = torch.cuda.Stream(dev) if mode == "pipeline" else s_disc
 
-    # one step = discovery (Gram -> [all-reduce] -> STLSQ) on s_disc, then the rollout on s_roll
-    # once that step's coefficients exist.  With --pipeline (default) the two phases of consecutive
-    # steps overlap: the discovery of step i+1 runs while the rollout of step i streams (both are
-    # HBM-bound; the overlap hides the STLSQ tail and the launch gaps, not bandwidth).  Launches go
-    # through prepared plans (arguments validated and packed once), events are preallocated.
+    # one step = discovery (Gram -> [all-reduce] -> STLSQ) then the rollout with that step's
+    # coefficients.  Launches go through prepared plans (arguments validated and packed once).
+    #   graph    : the step's launches captured once in a HIP graph, replayed K times (no host
+    #              launch gaps between the kernels; N = 1 only — the all-reduce stays eager)
+    #   seq      : the same launches issued eagerly on one stream
+    #   pipeline : discovery of step i+1 on one stream overlaps the rollout of step i on another
+    #              (double-buffered coefficients, event waits)
+    # The timed region holds no timing events: per-kernel durations come from the separate
+    # roofline pass below (and rocprofv3), not from markers that stall the queue.
     with torch.cuda.stream(s_disc):
         if world == 1:   # Gram kernel + fused reduction/STLSQ (2 launches)
             disc_plans = [ops.plan_sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, 100, True, 2,
@@ -151,52 +156,77 @@ def main():
             stlsq_plans = [ops.plan_stlsq(buf.G, buf.b, 0.1, 0.5, 100, True, out=(c, mask, iters)) for c in coefs]
     roll_plans = [ops.plan_rollout(y0, coh.u, arm_cf, c, lib, coh.dt, method=args.method, T=T, out=y,
                                    layout=roll_layout) for c in coefs]
-    n_ev = (args.warmup * 2 + args.steps + 2) * 4
-    ev_pool = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
+    done = [None, None]
+    sync_ev = [torch.cuda.Event() for _ in range(4)]   # cross-stream ordering only (no timing)
 
-    def step(i, record=False):
-        e = ev_pool[4 * (i % (n_ev // 4)): 4 * (i % (n_ev // 4)) + 4]
-        if record:
-            e[0].record(s_disc)
+    def discover(i, stream):
+        if world == 1:
+            disc_plans[i % 2](stream)
+        else:
+            gram_plan(stream)
+            with torch.cuda.stream(stream):
+                idist.reduce_moments(buf)           # the only collective
+            stlsq_plans[i % 2](stream)
+
+    def step(i):
+        if mode != "pipeline":                      # current stream: the capture stream under graph capture
+            st = torch.cuda.current_stream(dev)
+            discover(i, st)
+            roll_plans[i % 2](st)
+            return
         if done[i % 2] is not None:
             s_disc.wait_event(done[i % 2])          # rollout i-2 finished reading this coef buffer
-        if world == 1:
-            disc_plans[i % 2](s_disc)
-        else:
-            gram_plan(s_disc)
-            with torch.cuda.stream(s_disc):
-                idist.reduce_moments(buf)           # the only collective
-            stlsq_plans[i % 2](s_disc)
-        e[1].record(s_disc)
-        s_roll.wait_event(e[1])
-        if record:
-            e[2].record(s_roll)
+        discover(i, s_disc)
+        e_disc, e_roll = sync_ev[2 * (i % 2)], sync_ev[2 * (i % 2) + 1]
+        e_disc.record(s_disc)
+        s_roll.wait_event(e_disc)
         roll_plans[i % 2](s_roll)
-        e[3].record(s_roll)
-        done[i % 2] = e[3]
-        if record:
-            ev_disc.append((e[0], e[1]))
-            ev_roll.append((e[2], e[3]))
+        e_roll.record(s_roll)
+        done[i % 2] = e_roll
 
-    done = [None, None]
+    graph = None
+    if mode == "graph":
+        for i in range(2):                          # warm the plans outside capture
+            step(i)
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step(0)
+        run = lambda i: graph.replay()  # noqa: E731
+    else:
+        run = step
     for i in range(args.warmup):
-        step(i)
+        run(i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i + 2 * args.warmup, record=True)
+        run(i)
     host_ms = (time.perf_counter() - t0) / args.steps * 1e3   # submit time per step (no sync)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     el = idist.max_over_ranks(time.perf_counter() - t0, dev)
     ms_step = el / args.steps * 1e3
-    roll_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ev_roll]))
-    disc_ms = float(np.mean([a.elapsed_time(b_) for a, b_ in ev_disc]))
-    coef = coefs[(args.steps - 1 + 2 * args.warmup) % 2]
+    coef = coefs[0] if mode == "graph" else coefs[(args.steps - 1) % 2]
+
+    # roofline pass (outside the timed region): each phase's kernels launched back to back on one
+    # stream between two HIP events; avg = elapsed / launches.  Same kernels, same inputs.
+    def timed(fn, n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st = torch.cuda.current_stream(dev)
+        e0.record(st)
+        for _ in range(n):
+            fn(st)
+        e1.record(st)
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / n
+
+    n_roof = max(args.steps, 10)
+    roll_ms = timed(roll_plans[0], n_roof)
+    disc_ms = timed(lambda st: discover(0, st), n_roof)
 
     # sanity on the measured result: discovered support is the EQ_4_C one, no NaN
     sup = mask.cpu().numpy()
@@ -233,11 +263,11 @@ def main():
                 "workload": f"C2: PK/PD {N // 1000}k patients/GPU x {T} steps fp64 - discovery (savgol+FD4+poly2 "
                             f"library+Gram, RCCL all-reduce when N>1, STLSQ) + {args.method.upper()} counterfactual rollout",
                 "patients_per_gpu": N, "T": T, "rows_per_patient": T - 2, "library_terms": F,
-                "parallelism": f"patient-shard x{world}", "discovered_support": sup.tolist(), "finite": ok,
+                "parallelism": f"patient-shard x{world}", "mode": mode, "discovered_support": sup.tolist(), "finite": ok,
             },
             "host_submit_ms_per_step": host_ms,
             "roofline": {
-                "kernel": f"rollout_kernel ({args.method})",
+                "kernel": f"rollout_tm_kernel ({args.method})" if args.layout == "time" else f"rollout_kernel ({args.method})",
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBPS,
@@ -253,8 +283,10 @@ def main():
             "discovery": {
                 "kernels": "gram_kernel + discovery_finalize (fused STLSQ)" if world == 1
                            else "gram_kernel + RCCL all_reduce + stlsq_kernel",
-                "streams": "discovery and rollout on two streams, consecutive steps overlapped" if args.pipeline
-                           else "one stream, strictly sequential",
+                "timed_region": {"graph": "one step (gram, finalize+STLSQ, rollout) captured in a HIP graph, replayed",
+                                 "seq": "eager launches, one stream, strictly sequential",
+                                 "pipeline": "discovery and rollout on two streams, consecutive steps overlapped"}[mode],
+                "avg_ms_source": "roofline pass: back-to-back launches between two HIP events",
                 "avg_ms": disc_ms,
                 "algorithmic_bytes": gram_bytes(N, T),
                 "achieved_GBps": gram_bytes(N, T) / (disc_ms * 1e-3) / 1e9,
@@ -283,9 +315,9 @@ def main():
         for _ in range(10):
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
+            e0.record(torch.cuda.current_stream(dev))
             ops.rollout(y0n, un, armn, coef, lib, 10.0 / Tn, method="rk4", out=yn, layout=nlay)
-            e1.record(stream)
+            e1.record(torch.cuda.current_stream(dev))
             evs.append((e0, e1))
         torch.cuda.synchronize(dev)
         ms = float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))

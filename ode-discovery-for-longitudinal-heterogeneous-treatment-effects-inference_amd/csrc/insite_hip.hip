@@ -39,6 +39,30 @@ constexpr int kMaxEntries = 64;       // Gram + moment entries, one per lane
 constexpr int kGramMaxBlocks = 1024;  // fixed cap -> deterministic reduction order
 constexpr int kPsStride = 17;         // per-patient LDS scratch row (odd -> conflict-free)
 
+// Profiling-only phase timestamps (built with -DINSITE_TIMING by tools/build_ablation.sh): lane 0
+// of each wave stores s_memtime at phase boundaries into g_tstamp[wave][slot].
+#ifdef INSITE_TIMING
+constexpr int kTsWaves = 1 << 16, kTsSlots = 10;  // slots 8/9: s_memrealtime at entry / exit
+__device__ unsigned long long g_tstamp[kTsWaves * kTsSlots];
+#define INSITE_TSTAMP(wave, slot)                                                                   \
+  do {                                                                                              \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                     \
+    if ((threadIdx.x & 63) == 0 && (wave) < kTsWaves) g_tstamp[(int64_t)(wave) * kTsSlots + (slot)] = t_; \
+  } while (0)
+#define INSITE_TREAL(wave, slot)                                                                    \
+  do {                                                                                              \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                 \
+    if ((threadIdx.x & 63) == 0 && (wave) < kTsWaves) g_tstamp[(int64_t)(wave) * kTsSlots + (slot)] = t_; \
+  } while (0)
+#else
+#define INSITE_TSTAMP(wave, slot) \
+  do {                            \
+  } while (0)
+#define INSITE_TREAL(wave, slot) \
+  do {                           \
+  } while (0)
+#endif
+
 // Polynomial library over [x, u_0..u_{U-1}] (one state, U statics), pysindy column order.
 struct LibDesc {
   int32_t F;   // columns
@@ -124,6 +148,19 @@ __device__ __forceinline__ int wave_max_i(int v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
+// 32x32 bit transpose across each half-wave: lane j holds row j (bit i = column i); afterwards
+// lane i holds column i (bit j = row j).  Five butterfly stages (ds_swizzle/bpermute).
+__device__ __forceinline__ unsigned bit_transpose32(unsigned x, int lane) {
+  const unsigned m[5] = {0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int sh = 16 >> k;
+    const unsigned y = (unsigned)__shfl_xor((int)x, sh, kWave);
+    x = (lane & sh) ? ((x & ~m[k]) | ((y >> sh) & m[k])) : ((x & m[k]) | ((y << sh) & ~m[k]));
+  }
+  return x;
+}
+
 __device__ __forceinline__ double monomial(const LibDesc& lib, int j, const double* u) {
   double m = 1.0;
   for (int i = 0; i < lib.U; ++i)
@@ -150,6 +187,13 @@ struct GramW {
 constexpr int kGT = INSITE_GT;     // time tile in steps: a multiple of the register ring length (8)
 constexpr int kGStride = kGT + 1;  // LDS row stride in doubles (odd -> lane-per-row reads conflict free)
 constexpr int kGPF = INSITE_PF;    // tiles in flight (register prefetch depth, 1 or 2)
+#ifndef INSITE_TM_DEPTH
+#define INSITE_TM_DEPTH 2
+#endif
+// Time-major register ring: tiles of kGT steps, kTmDepth - 1 in flight while one is consumed.  A
+// wave's step loads are 512-B rows; with ~1.5 waves per SIMD at C2 sizes the bytes in flight per
+// wave set the achieved bandwidth (Little's law), so the ring is deep.
+constexpr int kTmDepth = INSITE_TM_DEPTH;
 
 __device__ __forceinline__ double sg_int(const GramW& w, double a, double b, double c, double d, double e) {
   return w.sg0 * c + w.sg1 * (b + d) + w.sg2 * (a + e);
@@ -243,6 +287,8 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
   constexpr int NLD = kWave / RPI;          // load instructions per tile
   static_assert(!TM || (VEC == 1 && NLD == kGT), "time-major tiles hold the lane's own kGT samples");
   if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0u;  // consumed by discovery_finalize (next launch)
+  INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 0);
+  INSITE_TREAL(blockIdx.x * kWavesPerBlock + wid, 8);
 
   // G-phase accumulators
   dbl4 cacc = {0.0, 0.0, 0.0, 0.0};  // MFMA path: C[(lane>>4) + 4j][lane & 15]
@@ -271,6 +317,33 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
     const int sidx = (int)(item - tile * n_seg);
     const int64_t p0 = tile * kWave;
     const int64_t p = p0 + lane;
+    // time-major: the first kTmDepth tiles are requested before the per-patient scalars (their
+    // range is clipped at the stored steps, not at this wave's longest row, which is not known yet)
+    const int s0 = sidx * seg;  // first step owned by this segment
+    const int tb = (sidx == 0) ? 0 : s0 - kWarm;
+    const int tm_valid = (int)(N - p0 < kWave ? N - p0 : kWave);
+    const unsigned tm_off = p < N ? (unsigned)lane * 8u : kOOB;
+    typedef double TmTile[kGT];
+    TmTile vr[TM ? kTmDepth : 1];
+    // wave-uniform descriptor over steps [t0, min(t0 + kGT, lim)) based at column p0: steps past
+    // lim and lanes past N (out-of-range offset) read as 0
+    auto tm_load = [&](TmTile& v, int t0, int lim) {
+      const int nrow = lim - t0 < kGT ? lim - t0 : kGT;
+      const int bytes = nrow > 0 ? (int)(((int64_t)(nrow - 1) * ldx + tm_valid) * 8) : 0;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(x + (int64_t)(nrow > 0 ? t0 : 0) * ldx + p0), (short)0, bytes, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < kGT; ++i)
+        v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, tm_off + (unsigned)(i * ldx * 8), 0, 0));
+    };
+#ifndef INSITE_GRAM_LATE_ISSUE
+    if constexpr (TM) {
+      const int s1p = min(s0 + seg, n_steps);
+#pragma unroll
+      for (int d = 0; d < kTmDepth; ++d)
+        if (tb + d * kGT < s1p) tm_load(vr[d], tb + d * kGT, s1p);
+    }
+#endif
     int L = 0;
     int arm_p = -1;
     double uu[INSITE_MAX_STATICS] = {0.0, 0.0, 0.0};
@@ -291,12 +364,9 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
       }
     }
     const int Lm = L >= kMinMain ? L : 0;  // length on the streaming path
-    // time-major tile loads: patients of this tile inside the cohort, and the lane's byte offset
-    const int tm_valid = (int)(N - p0 < kWave ? N - p0 : kWave);
-    const unsigned tm_off = p < N ? (unsigned)lane * 8u : kOOB;
     const int Lmax = wave_max_i(Lm);
-    const int s0 = sidx * seg;               // first step owned by this segment
     const int s1 = min(s0 + seg, Lmax);      // one past the last step processed
+    INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 1);
     const int e = min(Lm, s0 + seg);         // per-lane end of owned steps
     const int Lmin = wave_min_i(e);
     const int bstart = max(2 * kLag, s0);    // first body step of the segment
@@ -309,19 +379,6 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
       // Loads are issued unconditionally from a clamped (always valid) address and masked after
       // the fact: exec-masked loads would make the compiler drain vmcnt(0) at every tile.
       auto load_tile = [&](TileRegs& v, int t0) {
-        if constexpr (TM) {
-          // wave-uniform descriptor over steps [t0, min(t0 + kGT, s1)) based at column p0: steps
-          // past s1 and lanes past N (out-of-range offset) read as 0
-          const int nrow = s1 - t0 < kGT ? s1 - t0 : kGT;
-          const int bytes = nrow > 0 ? (int)(((int64_t)(nrow - 1) * ldx + tm_valid) * 8) : 0;
-          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-              (void*)(x + (int64_t)(nrow > 0 ? t0 : 0) * ldx + p0), (short)0, bytes, 0x00020000);
-#pragma unroll
-          for (int i = 0; i < kGT; ++i)
-            v[i][0] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
-                                                     rs, tm_off + (unsigned)(i * ldx * 8), 0, 0));
-          return;
-        }
         const int col = t0 + cl;
         const bool col_ok = col < s1;
         const int colc = col_ok ? col : 0;
@@ -378,18 +435,21 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
       };
 
       // ---- first tile: steps [tb, tb+16): warm-up, a-side terms, head rows, body ----
-      const int tb = (sidx == 0) ? 0 : s0 - kWarm;
       // sample i of the tile being consumed: LDS (patient-major) or the lane's own registers
-      auto sample = [&](const TileRegs& v, int i) -> double {
-        if constexpr (TM) return v[i][0];
+      auto sample = [&](const auto& v, int i) -> double {
+        if constexpr (TM) return v[i];
         else return xt[lane * kGStride + i];
       };
-      load_tile(vA, tb);
-      store_tile(vA);
       if constexpr (TM) {
-        if (tb + kGT < s1) load_tile(vB, tb + kGT);
-        else issue_tail();
+#ifdef INSITE_GRAM_LATE_ISSUE
+#pragma unroll
+        for (int d = 0; d < kTmDepth; ++d)
+          if (tb + d * kGT < s1) tm_load(vr[d], tb + d * kGT, s1);
+#endif
+        if (!(tb + kTmDepth * kGT < s1)) issue_tail();  // every remaining tile already in flight
       } else {
+        load_tile(vA, tb);
+        store_tile(vA);
         if (tb + kGT < s1) load_tile(vA, tb + kGT);
         if constexpr (kGPF == 2) {
           if (tb + 2 * kGT < s1) load_tile(vB, tb + 2 * kGT);
@@ -402,7 +462,8 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
         const bool masked = tb + kGT > Lmin;
 #pragma unroll
         for (int i = 0; i < kGT; ++i) {
-          xr[i & 7] = sample(vA, i);
+          if constexpr (TM) xr[i & 7] = sample(vr[0], i);
+          else xr[i & 7] = sample(vA, i);
           const int t = tb + i;
           if constexpr (SMOOTH) {
             if (i >= 4) sr[(i - 2) & 7] = sg_int(w, xr[(i - 4) & 7], xr[(i - 3) & 7], xr[(i - 2) & 7], xr[(i - 1) & 7], xr[i & 7]);
@@ -446,8 +507,9 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
           }
         }
       }
+      INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 2);
       // ---- remaining tiles of the segment (buffers alternate A, B; two tiles in flight) ----
-      auto consume = [&](int t0, const TileRegs& v) {
+      auto consume = [&](int t0, const auto& v) {
         if (t0 + kGT <= Lmin) {
 #pragma unroll
           for (int i = 0; i < kGT; ++i) {
@@ -482,20 +544,20 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
         }
       };
       if constexpr (TM) {
-        // vA is free after the first tile; vB holds tile tb + kGT.  Refill each buffer right
-        // after it is consumed (one tile in flight during a consume).
-        if (tb + 2 * kGT < s1) load_tile(vA, tb + 2 * kGT);
+        // ring slot d holds tile tb + d * kGT (mod kTmDepth); each slot is refilled with the tile
+        // kTmDepth ahead right after it is consumed (compile-time slot indices: no moves)
+        if (tb + kTmDepth * kGT < s1) tm_load(vr[0], tb + kTmDepth * kGT, s1);
         else issue_tail();
         for (int t0 = tb + kGT; t0 < s1;) {
-          consume(t0, vB);
-          if (t0 + 2 * kGT < s1) load_tile(vB, t0 + 2 * kGT);
-          else issue_tail();
-          t0 += kGT;
-          if (t0 >= s1) break;
-          consume(t0, vA);
-          if (t0 + 2 * kGT < s1) load_tile(vA, t0 + 2 * kGT);
-          else issue_tail();
-          t0 += kGT;
+#pragma unroll
+          for (int d = 1; d <= kTmDepth; ++d) {
+            if (t0 < s1) {  // uniform
+              consume(t0, vr[d % kTmDepth]);
+              if (t0 + kTmDepth * kGT < s1) tm_load(vr[d % kTmDepth], t0 + kTmDepth * kGT, s1);
+              else issue_tail();
+              t0 += kGT;
+            }
+          }
         }
       } else if constexpr (kGPF == 2) {
         for (int t0 = tb + kGT; t0 < s1;) {
@@ -519,6 +581,7 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
           consume(t0, vA);
         }
       }
+      INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 3);
       // ---- b-side telescoped terms and tail rows from the prefetched end samples ----
       issue_tail();
       if (need_end) {
@@ -583,6 +646,7 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
     continue;
 #endif
 
+    INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 4);
     // ---- per-patient Gram block A(u) M A(u)^T ----
     const double M0 = (sidx == 0) ? (double)L : 0.0;  // row count, counted once per patient
     const int my_arm = (L > 0) ? arm_p : -1;
@@ -648,6 +712,7 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
     }
   }
 
+  INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 5);
   // ---- block reduction (fixed order) -> partial[block][...] ----
   if constexpr (MOM) return;
   __syncthreads();
@@ -677,6 +742,8 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
       }
     }
   }
+  INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 6);
+  INSITE_TREAL(blockIdx.x * kWavesPerBlock + wid, 9);
 }
 
 // =============================================================================================
@@ -706,9 +773,13 @@ __device__ bool masked_cholesky_solve(const double (&g)[F][F], const double (&rh
           ok = false;
           a = 1e-300;
         }
-        const double r = sqrt(a);
-        l[i][i] = r;
-        rd[i] = 1.0 / r;
+        // 1/sqrt(a) from v_rsq_f64 + two Newton steps (no IEEE sqrt/div sequences on the
+        // factorisation's critical path); l_ii = a / sqrt(a)
+        double r = __builtin_amdgcn_rsq(a);
+        r = r * fma(-0.5 * a * r, r, 1.5);
+        r = r * fma(-0.5 * a * r, r, 1.5);
+        l[i][i] = a * r;
+        rd[i] = r;
       } else {
         l[i][j] = a * rd[j];
       }
@@ -823,6 +894,8 @@ discovery_finalize(const double* __restrict__ partial, int nblk, int narm_pad, i
   __shared__ int last;
   const int a = blockIdx.x / lib.nE;
   const int e = blockIdx.x % lib.nE;
+  INSITE_TSTAMP(49152 + blockIdx.x, 0);
+  INSITE_TREAL(49152 + blockIdx.x, 8);
   double s = 0.0;
   if (lib.mfma) {
     const int off = (a * lib.F + lib.ei[e]) * 16 + lib.qcol[e];
@@ -837,6 +910,7 @@ discovery_finalize(const double* __restrict__ partial, int nblk, int narm_pad, i
     if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
     __syncthreads();
   }
+  INSITE_TSTAMP(49152 + blockIdx.x, 1);
   if (threadIdx.x == 0) {
     const int i = lib.ei[e], k = lib.ek[e];
     if (k >= 0) {
@@ -855,6 +929,8 @@ discovery_finalize(const double* __restrict__ partial, int nblk, int narm_pad, i
       if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
+    INSITE_TSTAMP(49152 + blockIdx.x, 2);
+    INSITE_TREAL(49152 + blockIdx.x, 9);
     if (!last) return;
     const int arm_i = threadIdx.x;
     if (arm_i < n_arms) {
@@ -875,6 +951,8 @@ discovery_finalize(const double* __restrict__ partial, int nblk, int narm_pad, i
       }
       if (iters) iters[arm_i] = it;
     }
+    INSITE_TSTAMP(49152 + blockIdx.x, 3);
+    INSITE_TREAL(49152 + blockIdx.x, 9);
   }
 }
 
@@ -1002,6 +1080,15 @@ patient_fit_kernel(const double* __restrict__ mom, const double* __restrict__ u,
 // =============================================================================================
 // Batched rollout: lane = patient
 // =============================================================================================
+#ifndef INSITE_STORE_AUX
+#define INSITE_STORE_AUX 2
+#endif
+// Cache policy of the trajectory stores: non-temporal (aux bit 1).  Trajectories are written once
+// and read by a later consumer; kept out of the Infinity Cache they do not leave ~160 MB of dirty
+// lines that the next discovery pass would have to write back while it streams its own input
+// (C2 step: 87.5 -> 76 us measured, tools/build_ablation.sh NT).
+constexpr int kStoreAux = INSITE_STORE_AUX;
+
 struct RolloutArgs {
   const double* y0;
   const double* u;
@@ -1015,6 +1102,36 @@ struct RolloutArgs {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// Interval propagator.  Every library of this ABI is affine in the state (INSITE_MAX_STATE_DEGREE
+// 1), so per arm the RHS is f(y) = al + be * y with al, be fixed per patient, and one observation
+// interval of either integrator is an affine map y <- A y + B whose coefficients are loop
+// invariants (the stage arithmetic of the reference scan, hoisted out of the time loop):
+//   Euler, S substeps of h = dt/S (odeint, pkpd/utils.py:68-94): y <- (1 + h be) y + h al, S times;
+//   RK4, S steps: k1..k4 of the linear RHS give y <- R(z) y + h al P(z), z = h be,
+//     R = 1 + z + z^2/2 + z^3/6 + z^4/24,  P = 1 + z/2 + z^2/6 + z^3/24, composed S times.
+// The time loop is then one dependent FMA per step instead of ~10 (the RK4 chain's latency, not
+// HBM, bounded small cohorts: DESIGN.md §5).  Results agree with the stage-by-stage evaluation to
+// fp64 rounding (tests: rtol 1e-11 against the oracle's explicit stages).
+__device__ __forceinline__ void interval_propagator(int method, int substeps, double h, double al, double be,
+                                                    double& A, double& B) {
+  double a1, b1;
+  if (method == INSITE_METHOD_EULER) {
+    a1 = fma(h, be, 1.0);
+    b1 = h * al;
+  } else {
+    const double z = h * be;
+    const double P = fma(z, fma(z, fma(z, 1.0 / 24.0, 1.0 / 6.0), 0.5), 1.0);  // 1 + z/2 + z^2/6 + z^3/24
+    a1 = fma(z, P, 1.0);                                                        // R = 1 + z P
+    b1 = h * al * P;
+  }
+  A = 1.0;
+  B = 0.0;
+  for (int s = 0; s < substeps; ++s) {
+    B = fma(a1, B, b1);
+    A *= a1;
+  }
+}
 
 // Per-lane arm bytes of one 32-step tile, loaded straight from the lane's own row (32 contiguous
 // bytes; AV = bytes per load instruction) through a range-checked buffer descriptor.
@@ -1106,6 +1223,20 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(RolloutArgs ra, LibDesc
   const double h2 = 0.5 * h;
   const double h6 = h / 6.0;
 
+#ifndef INSITE_ROLLOUT_STAGEWISE
+  double PA[NARM], PB[NARM];
+#pragma unroll
+  for (int a = 0; a < NARM; ++a) interval_propagator(METHOD, ra.substeps, h, alpha[a], beta[a], PA[a], PB[a]);
+  auto step = [&](int a) {
+    double A = PA[0], B = PB[0];
+#pragma unroll
+    for (int aa = 1; aa < NARM; ++aa) {
+      A = (a == aa) ? PA[aa] : A;
+      B = (a == aa) ? PB[aa] : B;
+    }
+    y = fma(A, y, B);
+  };
+#else
   auto step = [&](int a) {
     double al = alpha[0], be = beta[0];
 #pragma unroll
@@ -1128,6 +1259,7 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(RolloutArgs ra, LibDesc
       }
     }
   };
+#endif
 
   for (int t0 = 0; t0 < ra.T; t0 += KT) {
 #ifndef INSITE_ABLATE_NOARM
@@ -1162,7 +1294,7 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(RolloutArgs ra, LibDesc
         const int c = (lane % LPR) * 2;
         const double2 v = *reinterpret_cast<const double2*>(yt + r * kYS + c);
         const unsigned off = (t0 + c < ra.T) ? (unsigned)((r * ra.ldy + t0 + c) * 8) : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, off, 0, kStoreAux);
       }
     } else {  // 32 lanes x 8 B per row segment, 2 rows per instruction
       constexpr int LPR = KT;            // lanes per row segment (8 B each)
@@ -1173,7 +1305,7 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(RolloutArgs ra, LibDesc
         const int c = lane % LPR;
         const double v = yt[r * kYS + c];
         const unsigned off = (t0 + c < ra.T) ? (unsigned)((r * ra.ldy + t0 + c) * 8) : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), yrs, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), yrs, off, 0, kStoreAux);
       }
     }
     wave_lds_sync();
@@ -1195,10 +1327,6 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(RolloutArgs ra, LibDesc
 #define INSITE_TG 16
 #endif
 constexpr int kTG = INSITE_TG;  // steps per group = arm prefetch distance
-#ifndef INSITE_STORE_AUX
-#define INSITE_STORE_AUX 0
-#endif
-constexpr int kStoreAux = INSITE_STORE_AUX;  // cache-policy bits of the trajectory stores (tuning)
 constexpr int64_t kTmMaxLd = ((int64_t)1 << 31) / (8 * kTG);  // group offsets stay below 2^31
 
 // AFMT: kArmByte (one int8 per lane), kArmDword (the aligned dword holding the lane's PPL int8
@@ -1212,6 +1340,8 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform (SGPR)
   const int64_t p0 = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * (kWave * PPL);
   if (p0 >= ra.N) return;
+  INSITE_TSTAMP(32768 + blockIdx.x * kWavesPerBlock + wid, 0);
+  INSITE_TREAL(32768 + blockIdx.x * kWavesPerBlock + wid, 8);
   double y[PPL], alpha[PPL][NARM], beta[PPL][NARM];
   bool act[PPL];
 #pragma unroll
@@ -1276,10 +1406,11 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
     return __builtin_amdgcn_make_buffer_rsrc((void*)(ra.arm + (int64_t)(rows > 0 ? k0 : 0) * arow + abase), (short)0,
                                              bytes, 0x00020000);
   };
-  auto y_rsrc = [&](int k0) {
+  auto y_rsrc = [&](int k0) {  // rows [k0, min(k0 + kTG, T)); empty (all stores dropped) past T
     const int rows = ra.T - k0 < kTG ? ra.T - k0 : kTG;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(ra.y + (int64_t)k0 * ra.ldy + p0), (short)0,
-                                             (int)(((int64_t)(rows - 1) * ra.ldy + nvalid) * 8), 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(ra.y + (int64_t)(rows > 0 ? k0 : 0) * ra.ldy + p0), (short)0,
+                                             rows > 0 ? (int)(((int64_t)(rows - 1) * ra.ldy + nvalid) * 8) : 0,
+                                             0x00020000);
   };
   auto load_arm = [&](__amdgpu_buffer_rsrc_t rs, int i) -> ArmT {  // step i of a group
 #ifdef INSITE_ABLATE_NOARM
@@ -1289,6 +1420,22 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
     if constexpr (AW4) return __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
     else return (ArmT)__builtin_amdgcn_raw_buffer_load_b8(rs, off, 0, 0);
   };
+#ifndef INSITE_ROLLOUT_STAGEWISE
+  double PA[PPL][NARM], PB[PPL][NARM];
+#pragma unroll
+  for (int q = 0; q < PPL; ++q)
+#pragma unroll
+    for (int a = 0; a < NARM; ++a) interval_propagator(METHOD, ra.substeps, h, alpha[q][a], beta[q][a], PA[q][a], PB[q][a]);
+  auto step = [&](int q, int a) {
+    double A = PA[q][0], B = PB[q][0];
+#pragma unroll
+    for (int aa = 1; aa < NARM; ++aa) {
+      A = (a == aa) ? PA[q][aa] : A;
+      B = (a == aa) ? PB[q][aa] : B;
+    }
+    y[q] = fma(A, y[q], B);
+  };
+#else
   auto step = [&](int q, int a) {
     double al = alpha[q][0], be = beta[q][0];
 #pragma unroll
@@ -1313,7 +1460,60 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
     }
     y[q] = yy;
   };
+#endif
 
+  INSITE_TSTAMP(32768 + blockIdx.x * kWavesPerBlock + wid, 1);
+  if constexpr (AFMT == kArmBits && PPL == 1) {
+    // Arm bits 32 steps at a time: lane l loads word (k0 + (l & 31), p0/32 + (l >> 5)) of the
+    // [T, N/32] mask (one 256-B request per wave), and a 32x32 bit transpose per half-wave leaves
+    // the lane's own 32 steps in one register.  Groups are requested kAG groups (128 steps) ahead
+    // into compile-time ring slots, so the time loop never waits on arm data; per step it is one
+    // select + one FMA + one 512-B store per wave.
+    constexpr int kAG = 4;
+    constexpr int kGS = 32;  // steps per arm group
+    const unsigned goff = (unsigned)((lane & 31) * arow + (lane >> 5) * 4);
+    auto grp_load = [&](int k0) -> unsigned {
+      const int rows = ra.T - k0 < kGS ? ra.T - k0 : kGS;
+      const int bytes = rows > 0 ? (int)((int64_t)(rows - 1) * arow + arec_tail) : 0;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(ra.arm + (int64_t)(rows > 0 ? k0 : 0) * arow + abase), (short)0, bytes, 0x00020000);
+      return __builtin_amdgcn_raw_buffer_load_b32(rs, goff, 0, 0);
+    };
+    unsigned aring[kAG];
+#pragma unroll
+    for (int d = 0; d < kAG; ++d) aring[d] = grp_load(d * kGS);
+    for (int k0 = 0; k0 < ra.T;) {
+#pragma unroll
+      for (int d = 0; d < kAG; ++d) {
+        if (k0 < ra.T) {  // uniform
+          const unsigned wb = bit_transpose32(aring[d], lane);
+          aring[d] = grp_load(k0 + kAG * kGS);  // empty past T: returns 0
+#pragma unroll
+          for (int hh = 0; hh < kGS / kTG; ++hh) {
+            const __amdgpu_buffer_rsrc_t ys = y_rsrc(k0 + hh * kTG);
+#pragma unroll
+            for (int i = 0; i < kTG; ++i) {
+#ifndef INSITE_ABLATE_NOCOMPUTE
+              step(0, (int)((wb >> (hh * kTG + i)) & 1u));
+#else
+              y[0] += (double)((wb >> (hh * kTG + i)) & 1u);
+#endif
+#ifndef INSITE_ABLATE_NOSTORE
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y[0]), ys,
+                                                    yoff + (unsigned)(i * ra.ldy * 8), 0, kStoreAux);
+#else
+              if (y[0] == 12345.678) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y[0]), ys, yoff, 0, 0);
+#endif
+            }
+          }
+          k0 += kGS;
+        }
+      }
+    }
+    INSITE_TSTAMP(32768 + blockIdx.x * kWavesPerBlock + wid, 2);
+    INSITE_TREAL(32768 + blockIdx.x * kWavesPerBlock + wid, 9);
+    return;
+  }
   ArmT ring[kTG];
   {
     const __amdgpu_buffer_rsrc_t rs = arm_rsrc(0);
@@ -1534,6 +1734,9 @@ inline GramPlan gram_plan(int64_t N, int64_t n_steps, int resident) {
   const int64_t tiles = (N + kWave - 1) / kWave;
   const int64_t T = n_steps > 0 ? n_steps : 1;
   int64_t ns = tiles > 0 ? resident / tiles : 1;
+#ifdef INSITE_GRAM_NS_MIN
+  if (ns < INSITE_GRAM_NS_MIN) ns = INSITE_GRAM_NS_MIN;
+#endif
   const int64_t ns_max = T / 48 > 1 ? T / 48 : 1;
   if (ns > ns_max) ns = ns_max;
   if (ns < 1) ns = 1;
@@ -1758,6 +1961,19 @@ extern "C" {
 
 int32_t insite_abi_version(void) { return INSITE_ABI_VERSION; }
 
+#ifdef INSITE_TIMING
+// profiling builds only: copy / clear the phase timestamps (host buffer of kTsWaves * kTsSlots u64)
+int32_t insite_debug_tstamps(unsigned long long* host, int32_t clear) {
+  if (clear) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_tstamp)) != hipSuccess) return INSITE_E_HIP;
+    return hipMemset(p, 0, sizeof(unsigned long long) * kTsWaves * kTsSlots) == hipSuccess ? INSITE_OK : INSITE_E_HIP;
+  }
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tstamp), sizeof(unsigned long long) * kTsWaves * kTsSlots) == hipSuccess
+             ? INSITE_OK : INSITE_E_HIP;
+}
+#endif
+
 const char* insite_strerror(int32_t code) {
   switch (code) {
     case INSITE_OK: return "ok";
@@ -1977,7 +2193,9 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
 #ifdef INSITE_FORCE_PPL
     ppl = INSITE_FORCE_PPL;
 #else
-    if (n_rows >= 256 * 1024) ppl = 2;
+    // bit-packed arms take the transposed-word path (one patient per lane: with the interval
+    // propagator the time loop is store-bound, more chains per lane buy nothing)
+    if (n_rows >= 256 * 1024 && !bits) ppl = 2;
 #endif
     if (ppl >= 2 && !(y16 && aw4 && n_rows % ppl == 0)) ppl = 1;
     const int64_t per_block = (int64_t)kBlock * ppl;

@@ -4,22 +4,31 @@ set -e
 R="$(cd "$(dirname "$0")/.." && pwd)"
 P="$R/ode-discovery-for-longitudinal-heterogeneous-treatment-effects-inference_amd"
 rm -rf "$P/lib/ablate"; mkdir -p "$P/lib/ablate"
-build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC "$@" -I "$R/include" -o "$P/lib/ablate/libinsite_hip_$NAME.so" "$P/csrc/insite_hip.hip"; }
+build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC "$@" -I "$R/include" -o "$P/lib/ablate/libinsite_hip_$NAME.so" "$P/csrc/insite_hip.hip" & }
 for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
   case $v in
     NOSTORE) NAME=$v build -DINSITE_ABLATE_NOSTORE ;;
     NOARM) NAME=$v build -DINSITE_ABLATE_NOARM ;;
+    TIMING) NAME=$v build -DINSITE_TIMING ;;
+    LATE) NAME=$v build -DINSITE_GRAM_LATE_ISSUE ;;
+    NOMEM) NAME=$v build -DINSITE_ABLATE_NOARM -DINSITE_ABLATE_NOSTORE ;;
     RT16) NAME=$v build -DINSITE_RT=16 ;;
     RT64) NAME=$v build -DINSITE_RT=64 ;;
     NOGPHASE) NAME=$v build -DINSITE_ABLATE_NOGPHASE ;;
     GT32) NAME=$v build -DINSITE_GT=32 ;;
+    NS2) NAME=$v build -DINSITE_GRAM_NS_MIN=2 ;;
+    NS4) NAME=$v build -DINSITE_GRAM_NS_MIN=4 ;;
+    GT32NS2) NAME=$v build -DINSITE_GT=32 -DINSITE_GRAM_NS_MIN=2 ;;
     TG8) NAME=$v build -DINSITE_TG=8 ;;
     TG32) NAME=$v build -DINSITE_TG=32 ;;
     TG64) NAME=$v build -DINSITE_TG=64 ;;
     NOCOMPUTE) NAME=$v build -DINSITE_ABLATE_NOCOMPUTE ;;
     NT) NAME=$v build -DINSITE_STORE_AUX=2 ;;
+    SC1) NAME=$v build -DINSITE_STORE_AUX=1 ;;
+    NT3) NAME=$v build -DINSITE_STORE_AUX=3 ;;
     PPL1) NAME=$v build -DINSITE_FORCE_PPL=1 ;;
     PPL2) NAME=$v build -DINSITE_FORCE_PPL=2 ;;
     PPL4) NAME=$v build -DINSITE_FORCE_PPL=4 ;;
   esac
 done
+wait

@@ -9,12 +9,17 @@ import torch
 from insite_amd import ops, cohort
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--op", default="gram", choices=["gram", "sindy_fit", "rollout", "stlsq"])
+ap.add_argument("--op", default="gram", choices=["gram", "sindy_fit", "rollout", "stlsq", "step"])
 ap.add_argument("--patients", type=int, default=100_000)
 ap.add_argument("--T", type=int, default=200)
 ap.add_argument("--iters", type=int, default=50)
 ap.add_argument("--method", default="rk4")
 ap.add_argument("--layout", default="patient", choices=["patient", "time", "time_bits"])
+ap.add_argument("--cold", action="store_true",
+                help="evict L2/Infinity Cache before every call and time each call alone")
+ap.add_argument("--flush", default="read", choices=["read", "write"],
+                help="cold eviction by reading 512 MB (clean cache) or writing it (dirty lines left behind)")
+ap.add_argument("--timing", action="store_true", help="phase timestamps (needs an INSITE_TIMING build)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 xlay = "time" if a.layout == "time_bits" else a.layout
@@ -28,6 +33,10 @@ y = torch.empty((a.patients, a.T) if a.layout == "patient" else (a.T, a.patients
 G = torch.randn(a.patients, 7, 7, dtype=torch.float64, device=dev)
 G = G @ G.transpose(1, 2) + torch.eye(7, dtype=torch.float64, device=dev) * 7
 bb = torch.randn(a.patients, 7, dtype=torch.float64, device=dev)
+step_out = (torch.empty((2, lib.n_terms), dtype=torch.float64, device=dev),
+            torch.empty((2, lib.n_terms), dtype=torch.int8, device=dev), torch.empty(2, dtype=torch.int32, device=dev),
+            torch.empty((2, lib.n_terms, lib.n_terms), dtype=torch.float64, device=dev),
+            torch.empty((2, lib.n_terms), dtype=torch.float64, device=dev))
 def run():
     if a.op == "gram":
         ops.gram(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 2, "smoothed4", ws, layout=xlay)
@@ -37,15 +46,65 @@ def run():
     elif a.op == "rollout":
         ops.rollout(coh.y0, coh.u, arm_cf, coef, lib, coh.dt, method=a.method, T=a.T, out=y,
                     layout=a.layout)
+    elif a.op == "step":   # one bench step: discovery (gram + finalize/STLSQ) then the rollout
+        ops.sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, 100, True, 2, "smoothed4", ws,
+                      layout=xlay, out=step_out)
+        ops.rollout(coh.y0, coh.u, arm_cf, step_out[0], lib, coh.dt, method=a.method, T=a.T, out=y, layout=a.layout)
     else:
         ops.stlsq(G, bb, 0.1, 0.5)
 for _ in range(5): run()
 torch.cuda.synchronize()
 st = torch.cuda.current_stream()
-e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
-e0.record(st)
-for _ in range(a.iters): run()
-e1.record(st); torch.cuda.synchronize()
-ms = e0.elapsed_time(e1) / a.iters
+if a.cold:
+    flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    evs = []
+    for i in range(a.iters):
+        if a.flush == "write":
+            flush.fill_(i & 0xff)
+        else:
+            fsum = flush.view(torch.float32).sum()
+        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(st); run(); e1.record(st)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    ms = float(np.mean([x.elapsed_time(y_) for x, y_ in evs]))
+else:
+    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(a.iters): run()
+    e1.record(st); torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.iters
+if a.timing:
+    import ctypes
+    from insite_amd import _lib
+    fn = _lib.load().insite_debug_tstamps
+    buf = np.zeros((1 << 16) * 10, dtype=np.uint64)
+    fn(ctypes.c_void_p(buf.ctypes.data), 1)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    fn(ctypes.c_void_p(buf.ctypes.data), 0)
+    ts_all = buf.reshape(-1, 10).astype(np.int64)
+    rbase = None
+    for part, ts in (("gram", ts_all[:32768]), ("rollout", ts_all[32768:49152]), ("finalize", ts_all[49152:])):
+        t = ts[ts[:, 0] > 0]
+        if not len(t):
+            continue
+        out = {"kernel": part, "waves": len(t)}
+        for j in range(1, 8):
+            ok = t[:, j] > 0
+            if ok.any():
+                out[f"slot{j}_cyc"] = round(float((t[ok, j] - t[ok, 0]).mean()))
+        r0, r1 = t[:, 8], t[:, 9]
+        okr = (r0 > 0) & (r1 > 0)
+        r0, r1 = r0[okr], r1[okr]
+        if rbase is None:
+            rbase = r0.min()
+        q = lambda v: [round(float(np.percentile(v, x)) / 100, 2) for x in (0, 10, 50, 90, 100)]
+        out["start_us_pcts"] = q(r0 - rbase)
+        out["end_us_pcts"] = q(r1 - rbase)
+        out["dur_us_pcts"] = q(r1 - r0)
+        print(json.dumps(out))
 print(json.dumps({"op": a.op, "patients": a.patients, "T": a.T, "ms_per_call": ms,
-                  "layout": a.layout, "lib": os.environ.get("INSITE_LIB_OVERRIDE", "default")}))
+                  "layout": a.layout, "cold": (a.flush if a.cold else False), "lib": os.environ.get("INSITE_LIB_OVERRIDE", "default")}))
