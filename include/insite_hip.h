@@ -183,6 +183,50 @@ int32_t insite_masked_sse_f64(const double* pred, int64_t ld_pred, double scale,
                               double* last_out, void* workspace, size_t workspace_bytes,
                               void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Multi-state path (configuration C3 of BASELINE.json: S = 5 coupled states + one binary per-step
+ * treatment input, fp32 storage, fp64 Gram).  Build-defined extension of the same discovery
+ * semantics to S states (no reference counterpart; oracle/multistate_ref.py is the restatement):
+ * the library is pysindy PolynomialLibrary(degree 2) over the inputs (x_1..x_S, a) — states first,
+ * then the input —, the derivative estimator savgol(5,3) + FD4 per state (SmoothedFiniteDifference,
+ * reference sindy.py:190), one STLSQ per target state on the shared Gram.
+ * Layouts (time-major structure of arrays):
+ *   states   x[(k * S + s) * ldx + p]  f32, ldx >= N          (step k, state s, patient p)
+ *   input    TIME_MAJOR_BITS bitmask [T, ld_bits] u32, bit p & 31 of word k * ld_bits + p / 32
+ *   y0       y0[s * ld_y0 + p] f32;   trajectories y[(k * S + s) * ld_y + p] f32
+ * This ABI version instantiates S = 5.
+ * --------------------------------------------------------------------------------------------- */
+
+/* Gram of the multi-state regression, replacing the per-target SINDy.fit rows / X^T X:
+ *   G_out [F, F] = sum_p Theta_p^T Theta_p,  B_out [F, S] = sum_p Theta_p^T xdot_p  (f64)
+ * over patients with >= 5 rows (rows may be NULL: every patient has n_steps rows).  inp_bits may be
+ * NULL (library over the states only).  exps: HOST int8 [F][S + (inp_bits != NULL)], the pysindy
+ * degree-2 library over those inputs (interaction_only, or full degree 2 without an input);
+ * other tables return INSITE_E_UNSUPPORTED.  fd_kind: INSITE_FD_SMOOTHED4. */
+size_t insite_gram_ms_workspace_bytes(int64_t n_patients);
+int32_t insite_gram_ms_f32(const float* x, int64_t ldx, int32_t n_steps, int32_t n_states, const uint32_t* inp_bits,
+                           int64_t ld_bits, const int32_t* rows, int64_t n_patients, const int8_t* exps,
+                           int32_t n_terms, int32_t fd_kind, double dt, double* G_out, double* B_out, void* workspace,
+                           size_t workspace_bytes, void* stream);
+
+/* One STLSQ (insite_stlsq_f64 semantics) per target on a shared Gram, F <= 32 (one wavefront per
+ * target, lane-per-row Cholesky):  G [F, F], B [F, n_targets] (column t = target t);
+ * coef_out [n_targets, F], mask_out [n_targets, F] (may be NULL), iters_out [n_targets] (may be NULL,
+ * -1 flags a non-positive-definite solve). */
+int32_t insite_stlsq_wave_f64(const double* G, const double* B, int32_t n_terms, int32_t n_targets, double threshold,
+                              double alpha, int32_t max_iter, int32_t unbias, double* coef_out, int8_t* mask_out,
+                              int32_t* iters_out, void* stream);
+
+/* Multi-state open-loop rollout (odeint/RK4 of pkpd/utils.py:68-94 with an S-dimensional state):
+ * for k = 0..T-1 the input a = bit (p, k) of inp_bits (0 when NULL) is held over interval k and
+ * y advances by `substeps` Euler / RK4 steps of f(y, a) = coef Theta(y, a), coef [S, F] f64 with
+ * |c| <= drop_below dropped (utils.py:388); y_out row k = the state after interval k.
+ * Arithmetic in fp32 (the C3 configuration's dtype).  exps as insite_gram_ms_f32 (interaction_only). */
+int32_t insite_rollout_ms_f32(const float* y0, int64_t ld_y0, const uint32_t* inp_bits, int64_t ld_bits,
+                              const double* coef, const int8_t* exps, int32_t n_terms, int32_t n_states,
+                              int64_t n_rows, int32_t T, double dt, int32_t method, int32_t substeps,
+                              double drop_below, float* y_out, int64_t ld_y, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

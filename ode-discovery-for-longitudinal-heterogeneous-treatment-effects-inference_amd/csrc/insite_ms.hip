@@ -1,0 +1,662 @@
+// insite_ms.hip — multi-state (S > 1) path of the INSITE hot path on MI355X (gfx950): configuration C3
+// of BASELINE.json (5-state coupled ODE + binary per-step treatment, fp32 storage, fp64 Gram).
+//
+// Kernels:
+//   gram_ms_kernel     fused savgol(5,3) smoothing + FD4 derivatives of S states + degree-2 polynomial
+//                      library over (x_1..x_S, a) + the Gram Y^T Z, Y = Theta, Z = [Theta | xdot], on
+//                      v_mfma_f64_16x16x4f64.  Lane = patient; every step the wave stages its 64 library
+//                      rows [Theta | xdot] (<= 32 doubles each) in LDS and issues 16 x 3 MFMAs (tiles
+//                      Y0^T Z0, Y0^T Z1, Y1^T Z1 of the 32 x 32 padded product; the Y1^T Z0 tile is the
+//                      transpose of part of Y0^T Z1).  Interior rows stream through compile-time register
+//                      rings; the 4 + 4 edge rows per patient use the one-sided stencils from directly
+//                      loaded end windows.  Replaces pysindy SmoothedFiniteDifference + PolynomialLibrary
+//                      + X^T X (reference sindy.py:186-192) generalised to S states.
+//   ms_finalize        fixed-order reduction of the per-block tile partials -> G [F, F], B [F, S].
+//   stlsq_wave_kernel  one wavefront per target state: STLSQ (pkpd/utils.py:213-327 semantics) with a
+//                      lane-per-row masked Cholesky in LDS (F <= 32, beyond the register-resident
+//                      one-thread solver of insite_hip.hip).
+//   rollout_ms_kernel  lane = patient, S-dimensional state in fp32 registers, RK4 / Euler of the dense
+//                      degree-2 RHS, per-step treatment bits (32 steps per register via the half-wave bit
+//                      transpose), non-temporal stores of [T][S][N] fp32 trajectories.
+#include <cmath>
+#include <cstring>
+
+#include "insite_common.h"
+
+namespace {
+
+constexpr int kMsMaxF = 32;       // library columns: Y has two 16-row MFMA tiles
+constexpr int kMsMaxS = 8;        // states
+constexpr int kMsRowStride = 33;  // LDS stride (doubles) of a staged [Theta | xdot | 0] row
+constexpr int kMsMaxBlocks = 512;
+constexpr int kMsTiles = 3;       // Y0^T Z0, Y0^T Z1, Y1^T Z1
+
+// Number of degree-<=2 polynomial columns over n inputs (bias, linear, pairwise) in pysindy order.
+__host__ __device__ constexpr int ms_cols(int n, bool inter) { return 1 + n + (inter ? n * (n - 1) / 2 : n * (n + 1) / 2); }
+
+// Library columns over z = [1, x_1..x_S, a_1..a_NIN]: column index j -> (z index i, z index k),
+// pysindy order (bias; linear; products by combinations(_with_replacement)).  Compile-time.
+template <int NZ, bool INTER>  // NZ = S + NIN inputs
+struct PolyCols {
+  static constexpr int F = ms_cols(NZ, INTER);
+  int ci[F], ck[F];
+  constexpr PolyCols() : ci(), ck() {
+    int j = 0;
+    ci[j] = 0; ck[j] = 0; ++j;                    // 1
+    for (int i = 0; i < NZ; ++i) { ci[j] = 1 + i; ck[j] = 0; ++j; }
+    for (int i = 0; i < NZ; ++i)
+      for (int k = INTER ? i + 1 : i; k < NZ; ++k) { ci[j] = 1 + i; ck[j] = 1 + k; ++j; }
+  }
+};
+
+// Library row Theta[F] from z[NZ + 1] (z[0] = 1).
+template <int NZ, bool INTER>
+__device__ __forceinline__ void poly_row(const double (&z)[NZ + 1], double (&th)[PolyCols<NZ, INTER>::F]) {
+  constexpr PolyCols<NZ, INTER> pc;
+#pragma unroll
+  for (int j = 0; j < PolyCols<NZ, INTER>::F; ++j) th[j] = pc.ck[j] == 0 ? z[pc.ci[j]] : z[pc.ci[j]] * z[pc.ck[j]];
+}
+
+// Fetch bit (lane & 31) of word row k of a TIME_MAJOR_BITS mask for patient p (edge rows only).
+__device__ __forceinline__ double input_bit(const uint32_t* __restrict__ abits, int64_t lda, int k, int64_t p) {
+  if (!abits) return 0.0;
+  return (double)((abits[(int64_t)k * lda + (p >> 5)] >> (p & 31)) & 1u);
+}
+
+// Stage this lane's library row into LDS and run the 16 x 3 MFMAs over the wave's 64 rows.
+// Row layout: [Theta_0..Theta_{F-1}, xdot_0..xdot_{S-1}, 0 ...] (32 doubles).  A[m][k] = Y_m of row
+// 4g + k (m = lane & 15, k = lane >> 4); B[k][n] = Z_n of the same row; C[(lane>>4) + 4j][lane & 15].
+template <int S, int F>
+__device__ __forceinline__ void ms_emit(double* __restrict__ wrow, const double* __restrict__ wbase, bool valid,
+                                        const double (&th)[F], const double (&xd)[S], dbl4& c00, dbl4& c01,
+                                        dbl4& c11, int lane) {
+  static_assert(F + S <= kMsMaxF, "Theta + xdot must fit two 16-column tiles");
+  wave_lds_sync();  // every lane finished reading the previous rows
+#pragma unroll
+  for (int j = 0; j < kMsMaxF; ++j) {
+    double v = 0.0;
+    if (j < F) v = th[j];
+    else if (j < F + S) v = xd[j - F];
+    wrow[j] = valid ? v : 0.0;
+  }
+  wave_lds_sync();
+  const int m = lane & 15, k = lane >> 4;
+  const bool y1ok = 16 + m < F;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const double* src = wbase + (4 * g + k) * kMsRowStride;
+    const double y0 = src[m];
+    const double z1 = src[16 + m];
+    const double y1 = y1ok ? z1 : 0.0;
+    c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(y0, y0, c00, 0, 0, 0);
+    c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(y0, z1, c01, 0, 0, 0);
+    c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(y1, z1, c11, 0, 0, 0);
+  }
+}
+
+// Smoothed values and derivatives of one short trajectory (5 <= LL <= 7 rows), every position
+// resolved at compile time (scipy savgol mode='interp' edges, pysindy one-sided FD4 edges).
+template <int LL>
+__device__ __forceinline__ void ms_small(const double (&xv)[8], const GramW& w, double (&xs)[8], double (&xd)[8]) {
+#pragma unroll
+  for (int k = 0; k < LL; ++k) {
+    if (k == 0) xs[k] = sg_pos0(xv[0], xv[1], xv[2], xv[3], xv[4]);
+    else if (k == 1) xs[k] = sg_pos1(xv[0], xv[1], xv[2], xv[3], xv[4]);
+    else if (k == LL - 2) xs[k] = sg_pos3(xv[LL - 5], xv[LL - 4], xv[LL - 3], xv[LL - 2], xv[LL - 1]);
+    else if (k == LL - 1) xs[k] = sg_pos4(xv[LL - 5], xv[LL - 4], xv[LL - 3], xv[LL - 2], xv[LL - 1]);
+    else xs[k] = sg_int(w, xv[k - 2], xv[k - 1], xv[k], xv[k + 1], xv[k + 2]);
+  }
+#pragma unroll
+  for (int k = 0; k < LL; ++k) {
+    if (k == 0) xd[k] = fd_pos0(xs[0], xs[1], xs[2], xs[3], xs[4]) * w.inv_dt;
+    else if (k == 1) xd[k] = fd_pos1(xs[0], xs[1], xs[2], xs[3], xs[4]) * w.inv_dt;
+    else if (k == LL - 2) xd[k] = fd_pos3(xs[LL - 5], xs[LL - 4], xs[LL - 3], xs[LL - 2], xs[LL - 1]) * w.inv_dt;
+    else if (k == LL - 1) xd[k] = fd_pos4(xs[LL - 5], xs[LL - 4], xs[LL - 3], xs[LL - 2], xs[LL - 1]) * w.inv_dt;
+    else xd[k] = fd_int(w, xs[k - 2], xs[k - 1], xs[k + 1], xs[k + 2]);
+  }
+  for (int k = LL; k < 8; ++k) xs[k] = xd[k] = 0.0;
+}
+
+// Lane = patient, work item = 64-patient tile (grid-stride).  Time-major SoA fp32 states
+// x[(k * S + s) * ldx + p]; treatment bits abits[k * lda + p / 32] (TIME_MAJOR_BITS; NULL = no input
+// column); rows[p] observation rows (>= 5 to contribute; NULL = n_steps).
+//   interior rows r = 4 .. L-5: streamed, raw ring xr[8][S] (fp32, loads 4 steps ahead into the slot
+//     just consumed), smoothed ring sr[8][S] (fp64); row r leaves at step t = r + 4
+//   edge rows 0..3 and L-4..L-1 (all rows when L < 8): one-sided stencils from end windows
+template <int S, int NIN, bool INTER>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
+gram_ms_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint32_t* __restrict__ abits,
+               int64_t lda, const int32_t* __restrict__ rows, int64_t N, GramW w, double* __restrict__ partial) {
+  constexpr int NZ = S + NIN;
+  constexpr int F = PolyCols<NZ, INTER>::F;
+  __shared__ double stage[kWavesPerBlock * kWave * kMsRowStride];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  double* wbase = stage + wid * kWave * kMsRowStride;
+  double* wrow = wbase + lane * kMsRowStride;
+  dbl4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00, c11 = c00;
+  const int64_t n_tiles = (N + kWave - 1) / kWave;
+  const int64_t sstride = ldx;              // between states of one step
+  const int64_t kstride = (int64_t)S * ldx; // between steps
+
+  for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid; tile < n_tiles;
+       tile += (int64_t)gridDim.x * kWavesPerBlock) {
+    const int64_t p0 = tile * kWave;
+    const int64_t p = p0 + lane;
+    const bool in = p < N;
+    const int64_t pc = in ? p : N - 1;
+    int L = rows ? rows[pc] : n_steps;
+    if (L > n_steps) L = n_steps;
+    if (!in || L < 5) L = 0;
+    const int Lmax = wave_max_i(L);
+    const float* xp = x + pc;
+    auto ld = [&](int k, int s) -> double { return (double)xp[(int64_t)k * kstride + s * sstride]; };
+
+    // ---------------- interior rows (L >= 9): r = 4 .. L-5 at steps t = 8 .. L-1 ----------------
+    if (Lmax >= 9) {
+      float xr[8][S];
+      double sr[8][S];
+      // treatment word of rows [32 g, 32 g + 32): one load per lane, transposed across the half-wave
+      auto word = [&](int g) -> unsigned {
+        if (!abits) return 0u;
+        const int k = 32 * g + (lane & 31);
+        const int kk = k < n_steps ? k : n_steps - 1;
+        const int64_t col = (p0 >> 5) + (lane >> 5);
+        const uint32_t v = col * 32 < N ? abits[(int64_t)kk * lda + col] : 0u;  // words past N: not read
+        return bit_transpose32(v, lane);
+      };
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int s = 0; s < S; ++s) xr[t][s] = xp[(int64_t)t * kstride + s * sstride];
+      unsigned wcur = word(0);
+      // steps are processed in blocks of 8 (compile-time ring slots); loads run 4 steps ahead
+      for (int t0 = 0; t0 < Lmax; t0 += 8) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int t = t0 + i;
+          if (t < Lmax) {  // uniform
+            if (t >= 4) {
+#pragma unroll
+              for (int s = 0; s < S; ++s)
+                sr[(i + 6) & 7][s] = sg_int(w, xr[(i + 4) & 7][s], xr[(i + 5) & 7][s], xr[(i + 6) & 7][s],
+                                            xr[(i + 7) & 7][s], xr[i & 7][s]);  // xs[t - 2]
+            }
+            if (t >= 8) {  // row r = t - 4
+              const int r = t - 4;
+              if ((r & 31) == 0) wcur = word(r >> 5);
+              double z[NZ + 1], xd[S];
+              z[0] = 1.0;
+#pragma unroll
+              for (int s = 0; s < S; ++s) {
+                z[1 + s] = sr[(i + 4) & 7][s];
+                xd[s] = fd_int(w, sr[(i + 2) & 7][s], sr[(i + 3) & 7][s], sr[(i + 5) & 7][s], sr[(i + 6) & 7][s]);
+              }
+#pragma unroll
+              for (int q = 0; q < NIN; ++q) z[1 + S + q] = (double)((wcur >> (r & 31)) & 1u);
+              double th[F];
+              poly_row<NZ, INTER>(z, th);
+              ms_emit<S, F>(wrow, wbase, t <= L - 1, th, xd, c00, c01, c11, lane);
+            }
+            // x[t + 4] is loaded straight into the slot x[t - 4] occupied (read above): the wait
+            // for it falls 4 steps later, at its first use
+            const int tn = t + 4 < n_steps ? t + 4 : n_steps - 1;
+#pragma unroll
+            for (int s = 0; s < S; ++s) xr[(i + 4) & 7][s] = xp[(int64_t)tn * kstride + s * sstride];
+          }
+        }
+      }
+    }
+
+    // ---------------- edge rows: 0..3 and L-4..L-1 (all rows when 5 <= L < 8) ----------------
+    if (Lmax >= 5) {
+      // head window x[0..7] (clamped to the stored steps; values past L are never used)
+#pragma unroll
+      for (int part = 0; part < 2; ++part) {
+        double xs[4][S], xdd[4][S];  // the 4 rows this part emits
+        int base = 0;  // first step of the window
+        if (part == 1) base = L >= 8 ? L - 8 : 0;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          double xv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int k = base + j < n_steps ? base + j : n_steps - 1;
+            xv[j] = ld(k, s);
+          }
+          double a8[8], d8[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) a8[j] = d8[j] = 0.0;
+          if (L >= 8) {
+            if (part == 0) {
+              a8[0] = sg_pos0(xv[0], xv[1], xv[2], xv[3], xv[4]);
+              a8[1] = sg_pos1(xv[0], xv[1], xv[2], xv[3], xv[4]);
+#pragma unroll
+              for (int k = 2; k < 6; ++k) a8[k] = sg_int(w, xv[k - 2], xv[k - 1], xv[k], xv[k + 1], xv[k + 2]);
+              a8[6] = a8[7] = 0.0;
+              d8[0] = fd_pos0(a8[0], a8[1], a8[2], a8[3], a8[4]) * w.inv_dt;
+              d8[1] = fd_pos1(a8[0], a8[1], a8[2], a8[3], a8[4]) * w.inv_dt;
+              d8[2] = fd_int(w, a8[0], a8[1], a8[3], a8[4]);
+              d8[3] = fd_int(w, a8[1], a8[2], a8[4], a8[5]);
+            } else {  // window index j <-> step L - 8 + j; rows L-4..L-1 = j 4..7
+#pragma unroll
+              for (int k = 2; k < 6; ++k) a8[k] = sg_int(w, xv[k - 2], xv[k - 1], xv[k], xv[k + 1], xv[k + 2]);
+              a8[6] = sg_pos3(xv[3], xv[4], xv[5], xv[6], xv[7]);
+              a8[7] = sg_pos4(xv[3], xv[4], xv[5], xv[6], xv[7]);
+              a8[0] = a8[1] = 0.0;
+              d8[4] = fd_int(w, a8[2], a8[3], a8[5], a8[6]);
+              d8[5] = fd_int(w, a8[3], a8[4], a8[6], a8[7]);
+              d8[6] = fd_pos3(a8[3], a8[4], a8[5], a8[6], a8[7]) * w.inv_dt;
+              d8[7] = fd_pos4(a8[3], a8[4], a8[5], a8[6], a8[7]) * w.inv_dt;
+            }
+          } else if (L == 7) {
+            ms_small<7>(xv, w, a8, d8);
+          } else if (L == 6) {
+            ms_small<6>(xv, w, a8, d8);
+          } else {
+            ms_small<5>(xv, w, a8, d8);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            xs[q][s] = a8[4 * part + q];
+            xdd[q][s] = d8[4 * part + q];
+          }
+        }
+        // slots: part 0 -> window rows 0..3; part 1 -> window rows 4..7 (L >= 8) or rows 4..L-1
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = 4 * part + q;  // window row
+          const bool valid = (L >= 8) || (j < L);
+          const int step = base + j;
+          double z[NZ + 1], xd[S];
+          z[0] = 1.0;
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            z[1 + s] = xs[q][s];
+            xd[s] = xdd[q][s];
+          }
+#pragma unroll
+          for (int qq = 0; qq < NIN; ++qq) z[1 + S + qq] = (L > 0 && step < n_steps) ? input_bit(abits, lda, step, pc) : 0.0;
+          double th[F];
+          poly_row<NZ, INTER>(z, th);
+          ms_emit<S, F>(wrow, wbase, L > 0 && valid, th, xd, c00, c01, c11, lane);
+        }
+      }
+    }
+  }
+
+  // ---- block reduction (fixed order) -> partial[block][tile][256], canonical [row][col] ----
+  __syncthreads();
+  double* red = stage;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = ((lane >> 4) + 4 * j) * 16 + (lane & 15);
+    red[(wid * kMsTiles + 0) * 256 + e] = c00[j];
+    red[(wid * kMsTiles + 1) * 256 + e] = c01[j];
+    red[(wid * kMsTiles + 2) * 256 + e] = c11[j];
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < kMsTiles * 256; q += kBlock) {
+    double s = red[q];
+#pragma unroll
+    for (int ww = 1; ww < kWavesPerBlock; ++ww) s += red[ww * kMsTiles * 256 + q];
+    partial[(int64_t)blockIdx.x * kMsTiles * 256 + q] = s;
+  }
+}
+
+// Fixed-order reduction of the tile partials and scatter into G [F, F] (symmetric) and B [F, S].
+__global__ void __launch_bounds__(kWave) ms_finalize(const double* __restrict__ partial, int nblk, int F, int S,
+                                                     double* __restrict__ G, double* __restrict__ B) {
+  const int q = blockIdx.x * kWave + threadIdx.x;  // tile entry, < 3 * 256
+  if (q >= kMsTiles * 256) return;
+  double v = 0.0;
+  for (int g = 0; g < nblk; ++g) v += partial[(int64_t)g * kMsTiles * 256 + q];
+  const int t = q / 256, e = q % 256, r = e / 16, c = e % 16;
+  const int row = t == 2 ? 16 + r : r;        // Y row
+  const int col = t == 0 ? c : 16 + c;        // Z column
+  if (row >= F) return;
+  if (col < F) {
+    G[(int64_t)row * F + col] = v;
+    if (t == 1) G[(int64_t)col * F + row] = v;  // the skipped Y1^T Z0 tile, by symmetry
+  } else if (col < F + S) {
+    B[(int64_t)row * S + (col - F)] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wave-cooperative STLSQ for F <= 32 (one wavefront per target state)
+// ---------------------------------------------------------------------------------------------
+// Masked ridge solve (G_SS + alpha I) c_S = b_S with inactive rows/columns replaced by identity rows
+// (the operations of the reduced solve on the active block, as masked_cholesky_solve in
+// insite_hip.hip).  Lane i owns row i of M (LDS, row-major with stride kMsMaxF + 1); right-looking
+// Cholesky, then forward/backward substitution.  Returns false if not positive definite.
+__device__ bool wave_chol_solve(const double* __restrict__ G, const double* __restrict__ b, int bstride, int F,
+                                unsigned m, double alpha, double* M, double* v, double* c, int lane) {
+  constexpr int LD = kMsMaxF + 1;
+  const bool row_on = lane < F;
+  const bool ai = row_on && ((m >> lane) & 1u);
+  if (row_on) {
+    for (int j = 0; j < F; ++j) {
+      const bool act = ai && ((m >> j) & 1u);
+      double a = act ? G[(int64_t)lane * F + j] : 0.0;
+      if (j == lane) a = ai ? a + alpha : 1.0;
+      M[lane * LD + j] = a;
+    }
+    v[lane] = ai ? b[(int64_t)lane * bstride] : 0.0;
+  }
+  wave_lds_sync();
+  bool ok = true;
+  for (int j = 0; j < F; ++j) {
+    double d = M[j * LD + j];
+    if (!(d > 0.0)) {
+      ok = false;
+      d = 1e-300;
+    }
+    const double rd = 1.0 / sqrt(d);
+    wave_lds_sync();
+    if (lane > j && lane < F) M[lane * LD + j] *= rd;  // L[i][j]
+    if (lane == j) M[j * LD + j] = d * rd;                // L[j][j] = sqrt(d)
+    wave_lds_sync();
+    if (lane > j && lane < F) {
+      const double lij = M[lane * LD + j];
+      for (int k = j + 1; k <= lane; ++k) M[lane * LD + k] = fma(-lij, M[k * LD + j], M[lane * LD + k]);
+    }
+    wave_lds_sync();
+  }
+  // forward: L z = v
+  for (int j = 0; j < F; ++j) {
+    const double zj = v[j] / M[j * LD + j];
+    wave_lds_sync();
+    if (lane == j) v[j] = zj;
+    if (lane > j && lane < F) v[lane] = fma(-M[lane * LD + j], zj, v[lane]);
+    wave_lds_sync();
+  }
+  // backward: L^T c = z
+  for (int j = F - 1; j >= 0; --j) {
+    const double cj = v[j] / M[j * LD + j];
+    wave_lds_sync();
+    if (lane == j) c[j] = ((m >> j) & 1u) ? cj : 0.0;
+    if (lane < j) v[lane] = fma(-M[j * LD + lane], cj, v[lane]);
+    wave_lds_sync();
+  }
+  return ok;
+}
+
+__global__ void __launch_bounds__(kWave)
+stlsq_wave_kernel(const double* __restrict__ G, const double* __restrict__ B, int F, int n_sys, StlsqParams sp,
+                  double* __restrict__ coef, int8_t* __restrict__ mask, int32_t* __restrict__ iters) {
+  __shared__ double M[kMsMaxF * (kMsMaxF + 1)];
+  __shared__ double v[kMsMaxF], c[kMsMaxF];
+  const int s = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (s >= n_sys) return;
+  const double* b = B + s;  // column s of B [F, n_sys]
+  const unsigned all = F >= 32 ? 0xffffffffu : ((1u << F) - 1u);
+  unsigned ind = all, prev = all;
+  bool ok = true;
+  int it = 0;
+  if (lane < kMsMaxF) c[lane] = 0.0;
+  wave_lds_sync();
+  for (int k = 0; k < sp.max_iter; ++k) {
+    it = k + 1;
+    if (ind == 0u) {
+      if (lane < kMsMaxF) c[lane] = 0.0;
+      wave_lds_sync();
+      break;
+    }
+    ok &= wave_chol_solve(G, b, n_sys, F, ind, sp.alpha, M, v, c, lane);
+    wave_lds_sync();
+    const bool big_l = lane < F && fabs(c[lane]) >= sp.thr;
+    if (lane < F && !big_l) c[lane] = 0.0;
+    wave_lds_sync();
+    const unsigned big = (unsigned)__builtin_amdgcn_readfirstlane((int)(uint32_t)__ballot(big_l));
+    const unsigned pattern = (unsigned)__builtin_amdgcn_readfirstlane((int)(uint32_t)__ballot(lane < F && c[lane] != 0.0));
+    ind = big;
+    if (ind == all || pattern == prev) break;
+    prev = pattern;
+  }
+  const unsigned sup = (unsigned)__builtin_amdgcn_readfirstlane((int)(uint32_t)__ballot(lane < F && fabs(c[lane]) > 1e-14));
+  if (sp.unbias && sup) ok &= wave_chol_solve(G, b, n_sys, F, sup, 0.0, M, v, c, lane);
+  wave_lds_sync();
+  if (lane < F) {
+    coef[(int64_t)s * F + lane] = c[lane];
+    if (mask) mask[(int64_t)s * F + lane] = (int8_t)((sup >> lane) & 1u);
+  }
+  if (lane == 0 && iters) iters[s] = ok ? it : -1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Multi-state rollout
+// ---------------------------------------------------------------------------------------------
+struct MsRollArgs {
+  const float* y0;     // [S][ld0]
+  const uint32_t* a;   // TIME_MAJOR_BITS [T][lda] (NULL: input column 0 throughout)
+  const double* coef;  // [S][F]
+  float* y;            // [T][S][ldy]
+  int64_t ld0, lda, ldy, N;
+  int32_t T, method, substeps;
+  double dt, drop;
+};
+
+// f(y, a)[S] = C Theta(y, a) (dense over the library; coefficients |c| <= drop zeroed at setup).
+template <int S, int NIN, bool INTER>
+__device__ __forceinline__ void ms_rhs(const float (&y)[S], float a, const float (&cf)[S][PolyCols<S + NIN, INTER>::F],
+                                       float (&f)[S]) {
+  constexpr int NZ = S + NIN;
+  constexpr PolyCols<NZ, INTER> pc;
+  float z[NZ + 1];
+  z[0] = 1.0f;
+#pragma unroll
+  for (int s = 0; s < S; ++s) z[1 + s] = y[s];
+#pragma unroll
+  for (int q = 0; q < NIN; ++q) z[1 + S + q] = a;
+#pragma unroll
+  for (int s = 0; s < S; ++s) f[s] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < PolyCols<NZ, INTER>::F; ++j) {
+    const float th = pc.ck[j] == 0 ? z[pc.ci[j]] : z[pc.ci[j]] * z[pc.ck[j]];
+#pragma unroll
+    for (int s = 0; s < S; ++s) f[s] = fmaf(cf[s][j], th, f[s]);
+  }
+}
+
+template <int S, int NIN, bool INTER>
+__global__ void __launch_bounds__(kBlock) rollout_ms_kernel(MsRollArgs ra) {
+  constexpr int F = PolyCols<S + NIN, INTER>::F;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t p0 = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * kWave;
+  if (p0 >= ra.N) return;
+  const int64_t p = p0 + lane;
+  const bool act = p < ra.N;
+  const int64_t pc = act ? p : ra.N - 1;
+  float cf[S][F];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      const double c = ra.coef[s * F + j];
+      cf[s][j] = fabs(c) > ra.drop ? (float)c : 0.0f;
+    }
+  float y[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) y[s] = ra.y0[s * ra.ld0 + pc];
+  const float h = (float)(ra.dt / ra.substeps);
+  const float h2 = 0.5f * h, h6 = h / 6.0f;
+  const int nvalid = (int)(ra.N - p0 < kWave ? ra.N - p0 : kWave);
+  const unsigned yoff = act ? (unsigned)(lane * 4) : kOOB;
+  const int64_t lda = ra.lda;
+  auto word = [&](int g) -> unsigned {  // treatment bits of steps [32 g, 32 g + 32) for this lane
+    if (!ra.a) return 0u;
+    const int k = 32 * g + (lane & 31);
+    const int kk = k < ra.T ? k : ra.T - 1;
+    const int64_t col = (p0 >> 5) + (lane >> 5);
+    const uint32_t v = col * 32 < ra.N ? ra.a[(int64_t)kk * lda + col] : 0u;  // words past N: not read
+    return bit_transpose32(v, lane);
+  };
+  unsigned wnext = word(0);
+  for (int k0 = 0; k0 < ra.T; k0 += 32) {
+    const unsigned wcur = wnext;
+    if (k0 + 32 < ra.T) wnext = word((k0 >> 5) + 1);  // one group ahead
+    const int kend = ra.T - k0 < 32 ? ra.T - k0 : 32;
+    for (int i = 0; i < kend; ++i) {
+      const float a = (float)((wcur >> i) & 1u);
+      for (int sub = 0; sub < ra.substeps; ++sub) {
+        if (ra.method == INSITE_METHOD_EULER) {
+          float f[S];
+          ms_rhs<S, NIN, INTER>(y, a, cf, f);
+#pragma unroll
+          for (int s = 0; s < S; ++s) y[s] = fmaf(h, f[s], y[s]);
+        } else {
+          float k1[S], k2[S], k3[S], k4[S], t[S];
+          ms_rhs<S, NIN, INTER>(y, a, cf, k1);
+#pragma unroll
+          for (int s = 0; s < S; ++s) t[s] = fmaf(h2, k1[s], y[s]);
+          ms_rhs<S, NIN, INTER>(t, a, cf, k2);
+#pragma unroll
+          for (int s = 0; s < S; ++s) t[s] = fmaf(h2, k2[s], y[s]);
+          ms_rhs<S, NIN, INTER>(t, a, cf, k3);
+#pragma unroll
+          for (int s = 0; s < S; ++s) t[s] = fmaf(h, k3[s], y[s]);
+          ms_rhs<S, NIN, INTER>(t, a, cf, k4);
+#pragma unroll
+          for (int s = 0; s < S; ++s) y[s] = fmaf(h6, (k1[s] + 2.0f * k2[s]) + (2.0f * k3[s] + k4[s]), y[s]);
+        }
+      }
+      const int k = k0 + i;
+      // step row k: S contiguous runs of N floats; this wave's 64 columns through a range-checked
+      // descriptor (lanes past N carry an out-of-range offset)
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(ra.y + (int64_t)k * S * ra.ldy + p0), (short)0, (int)(((int64_t)(S - 1) * ra.ldy + nvalid) * 4),
+          0x00020000);
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y[s]), rs, yoff + (unsigned)(s * ra.ldy * 4),
+                                              0, kStoreAux);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host helpers
+// ---------------------------------------------------------------------------------------------
+// The exponent table must be the pysindy PolynomialLibrary(degree 2, interaction_only) over S + NIN
+// inputs (states first, then inputs); returns the matching interaction flag or -1.
+int ms_library_kind(const int8_t* exps, int F, int S, int NIN) {
+  const int n = S + NIN;
+  for (int inter = 1; inter >= 0; --inter) {
+    if (F != ms_cols(n, inter)) continue;
+    bool ok = true;
+    int j = 0;
+    auto row_is = [&](int i, int k) {  // column with inputs i, k (-1 = none)
+      for (int q = 0; q < n; ++q) {
+        int e = (q == i) + (q == k);
+        if (exps[j * n + q] != e) return false;
+      }
+      return true;
+    };
+    ok &= row_is(-1, -1);
+    ++j;
+    for (int i = 0; ok && i < n; ++i, ++j) ok &= row_is(i, -1);
+    for (int i = 0; ok && i < n; ++i)
+      for (int k = inter ? i + 1 : i; ok && k < n; ++k, ++j) ok &= row_is(i, k);
+    if (ok) return inter;
+  }
+  return -1;
+}
+
+inline int ms_grid(int64_t N) {
+  int64_t tiles = (N + kWave - 1) / kWave;
+  int64_t g = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (g > kMsMaxBlocks) g = kMsMaxBlocks;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t insite_gram_ms_workspace_bytes(int64_t n_patients) {
+  return (size_t)ms_grid(n_patients) * kMsTiles * 256 * sizeof(double);
+}
+
+int32_t insite_gram_ms_f32(const float* x, int64_t ldx, int32_t n_steps, int32_t n_states, const uint32_t* inp_bits,
+                           int64_t ld_bits, const int32_t* rows, int64_t n_patients, const int8_t* exps,
+                           int32_t n_terms, int32_t fd_kind, double dt, double* G_out, double* B_out, void* workspace,
+                           size_t workspace_bytes, void* stream) {
+  if (n_states != 5) return INSITE_E_UNSUPPORTED;  // instantiated for the C3 system
+  if (n_patients < 0 || n_steps < 0 || ldx < n_patients || !(dt > 0.0) || !G_out || !B_out || !exps)
+    return INSITE_E_INVALID_ARG;
+  if (fd_kind != INSITE_FD_SMOOTHED4) return INSITE_E_UNSUPPORTED;
+  const int nin = inp_bits ? 1 : 0;
+  if (inp_bits && ld_bits < (n_patients + 31) / 32) return INSITE_E_INVALID_ARG;
+  const int inter = ms_library_kind(exps, n_terms, n_states, nin);
+  if (inter < 0) return INSITE_E_UNSUPPORTED;
+  if (n_terms + n_states > kMsMaxF) return INSITE_E_UNSUPPORTED;
+  if (!workspace || workspace_bytes < insite_gram_ms_workspace_bytes(n_patients)) return INSITE_E_WORKSPACE;
+  if (n_patients > 0 && !x) return INSITE_E_INVALID_ARG;
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  double* part = static_cast<double*>(workspace);
+  const int grid = ms_grid(n_patients);
+  GramW w;
+  w.sg0 = 17.0 / 35.0;
+  w.sg1 = 12.0 / 35.0;
+  w.sg2 = -3.0 / 35.0;
+  w.inv_dt = 1.0 / dt;
+  w.fd1 = (2.0 / 3.0) * w.inv_dt;
+  w.fd2 = (-1.0 / 12.0) * w.inv_dt;
+  if (n_patients == 0 || n_steps < 5) {
+    if (hipMemsetAsync(part, 0, (size_t)grid * kMsTiles * 256 * sizeof(double), hs) != hipSuccess) return INSITE_E_HIP;
+  } else if (nin == 1 && inter == 1) {
+    gram_ms_kernel<5, 1, true><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, inp_bits, ld_bits, rows, n_patients, w, part);
+  } else if (nin == 1) {
+    return INSITE_E_UNSUPPORTED;  // 5 states + input, full degree 2: F + S > 32
+  } else if (inter == 1) {
+    gram_ms_kernel<5, 0, true><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, nullptr, 0, rows, n_patients, w, part);
+  } else {
+    gram_ms_kernel<5, 0, false><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, nullptr, 0, rows, n_patients, w, part);
+  }
+  int32_t st = launch_status();
+  if (st != INSITE_OK) return st;
+  ms_finalize<<<(kMsTiles * 256 + kWave - 1) / kWave, kWave, 0, hs>>>(part, grid, n_terms, n_states, G_out, B_out);
+  return launch_status();
+}
+
+int32_t insite_stlsq_wave_f64(const double* G, const double* B, int32_t n_terms, int32_t n_targets, double threshold,
+                              double alpha, int32_t max_iter, int32_t unbias, double* coef_out, int8_t* mask_out,
+                              int32_t* iters_out, void* stream) {
+  if (n_terms < 1 || n_terms > kMsMaxF || n_targets < 0 || !G || !B || !coef_out || max_iter < 1)
+    return INSITE_E_INVALID_ARG;
+  if (n_targets == 0) return INSITE_OK;
+  StlsqParams sp{threshold, alpha, max_iter, unbias, 1};
+  stlsq_wave_kernel<<<n_targets, kWave, 0, reinterpret_cast<hipStream_t>(stream)>>>(G, B, n_terms, n_targets, sp,
+                                                                                     coef_out, mask_out, iters_out);
+  return launch_status();
+}
+
+int32_t insite_rollout_ms_f32(const float* y0, int64_t ld_y0, const uint32_t* inp_bits, int64_t ld_bits,
+                              const double* coef, const int8_t* exps, int32_t n_terms, int32_t n_states,
+                              int64_t n_rows, int32_t T, double dt, int32_t method, int32_t substeps,
+                              double drop_below, float* y_out, int64_t ld_y, void* stream) {
+  if (n_states != 5) return INSITE_E_UNSUPPORTED;
+  if (n_rows < 0 || T < 0 || substeps < 1 || !(dt >= 0.0) || ld_y0 < n_rows || ld_y < n_rows || !exps)
+    return INSITE_E_INVALID_ARG;
+  if (inp_bits && ld_bits < (n_rows + 31) / 32) return INSITE_E_INVALID_ARG;
+  if (method != INSITE_METHOD_EULER && method != INSITE_METHOD_RK4) return INSITE_E_UNSUPPORTED;
+  const int nin = inp_bits ? 1 : 0;
+  const int inter = ms_library_kind(exps, n_terms, n_states, nin);
+  if (inter != 1) return INSITE_E_UNSUPPORTED;
+  if (n_rows == 0 || T == 0) return INSITE_OK;
+  if (!y0 || !coef || !y_out) return INSITE_E_INVALID_ARG;
+  if ((int64_t)n_states * ld_y * 4 >= ((int64_t)1 << 31)) return INSITE_E_UNSUPPORTED;  // 32-bit step offsets
+  MsRollArgs ra{y0, inp_bits, coef, y_out, ld_y0, ld_bits, ld_y, n_rows, T, method, substeps, dt, drop_below};
+  const int64_t waves = (n_rows + kWave - 1) / kWave;
+  const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  if (nin == 1) rollout_ms_kernel<5, 1, true><<<grid, kBlock, 0, hs>>>(ra);
+  else rollout_ms_kernel<5, 0, true><<<grid, kBlock, 0, hs>>>(ra);
+  return launch_status();
+}
+
+}  // extern "C"

@@ -42,6 +42,10 @@ EXPORTS = (
     "insite_rollout_f64",
     "insite_masked_sse_workspace_bytes",
     "insite_masked_sse_f64",
+    "insite_gram_ms_workspace_bytes",
+    "insite_gram_ms_f32",
+    "insite_stlsq_wave_f64",
+    "insite_rollout_ms_f32",
 )
 
 
@@ -81,6 +85,13 @@ _SIGNATURES = {
     "insite_masked_sse_workspace_bytes": (_c_size, [_c_i64, _c_i32]),
     "insite_masked_sse_f64": (_c_i32, [_vp, _c_i64, _c_f64, _c_f64, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _vp,
                                        _vp, _c_size, _vp]),
+    "insite_gram_ms_workspace_bytes": (_c_size, [_c_i64]),
+    "insite_gram_ms_f32": (_c_i32, [_vp, _c_i64, _c_i32, _c_i32, _vp, _c_i64, _vp, _c_i64, _vp, _c_i32, _c_i32,
+                                    _c_f64, _vp, _vp, _vp, _c_size, _vp]),
+    "insite_stlsq_wave_f64": (_c_i32, [_vp, _vp, _c_i32, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp,
+                                       _vp]),
+    "insite_rollout_ms_f32": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _vp, _vp, _c_i32, _c_i32, _c_i64, _c_i32, _c_f64,
+                                       _c_i32, _c_i32, _c_f64, _vp, _c_i64, _vp]),
 }
 
 
