@@ -51,6 +51,9 @@ def parse():
                          "stream; pipeline: discovery of step i+1 overlaps the rollout of step i (two streams)")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5"],
+                    help="c2: BASELINE configs[1], the headline line (default); c3: configs[2], the 5-state fp32 "
+                         "system (parity-test configuration, measured separately)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                     help="per-launch HBM bytes from the rocprofv3 PMC passes (profiles/), if present")
     return ap.parse_args()
@@ -101,8 +104,158 @@ def cpu_baseline(n_sample, T, method, seed):
                       f"{el:.2f} s; host cpus={os.cpu_count()}"}
 
 
+def c3_main(args):
+    """Configuration C3 (BASELINE.json configs[2]): 5-state coupled ODE + binary per-step treatment,
+    1M patients x 500 steps, fp32 storage, fp64 Gram on MFMA.  One step = discovery (gram_ms on f64
+    MFMA + fixed-order finalize + one wave-STLSQ per state) + RK4 counterfactual rollout of every
+    patient under a fresh treatment sequence.  Single GPU (patients would shard like C2)."""
+    from insite_amd import multistate as MS
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    N = args.patients if args.patients != 100_000 else 1_000_000
+    T = args.T if args.T != 200 else 500
+    coh = MS.synthetic_c3(N, T, seed=args.seed, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed + 17)
+    a_cf = MS.markov_treatment_bits(N, T, g, dev)
+    lib = coh.lib
+    F, S = lib.n_terms, lib.n_states
+    G = torch.empty((F, F), dtype=torch.float64, device=dev)
+    B = torch.empty((F, S), dtype=torch.float64, device=dev)
+    coef = torch.empty((S, F), dtype=torch.float64, device=dev)
+    mask = torch.empty((S, F), dtype=torch.int8, device=dev)
+    iters = torch.empty((S,), dtype=torch.int32, device=dev)
+    y = torch.empty((T, S, N), dtype=torch.float32, device=dev)
+
+    def disc():
+        MS.gram_ms(coh.x, coh.a, lib, coh.dt, out=(G, B))
+        MS.stlsq_wave(G, B, MS.THRESHOLD_C3, MS.ALPHA_C3, out=(coef, mask, iters))
+
+    def roll():
+        MS.rollout_ms(coh.y0, a_cf, coef, lib, coh.dt, T, method="rk4", out=y)
+
+    for _ in range(args.warmup):
+        disc()
+        roll()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        disc()
+        roll()
+    torch.cuda.synchronize(dev)
+    ms_step = (time.perf_counter() - t0) / args.steps * 1e3
+
+    def timed(fn, n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            fn()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / n
+
+    n_roof = max(args.steps, 5)
+    gram_ms_t = timed(lambda: MS.gram_ms(coh.x, coh.a, lib, coh.dt, out=(G, B)), n_roof)
+    roll_ms_t = timed(roll, n_roof)
+    truth = MS.c3_truth_coef(lib, device=dev)
+    rows = N * T
+    gflop = 2.0 * (F * (F + 1) / 2 + F * S) * rows          # algorithmic: G upper triangle + B per row
+    mfma_flop = 3 * 16 * 16 * 4 * 2 * rows / 4               # issued: 3 f64 16x16x4 tiles per 4 rows
+    roll_bytes = T * N * S * 4 + N * S * 4 + T * ((N + 31) // 32) * 4
+    gram_bytes = T * N * S * 4 + T * ((N + 31) // 32) * 4
+    out = {
+        "metric": METRIC, "value": N / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32 (storage, rollout) / f64 (Gram, STLSQ)",
+        "data": "synthetic: on-device C3 cohort (planted 5-state system, Markov treatment, RK4-10 truth)",
+        "config": {"workload": f"C3: 5-state + binary treatment, {N // 1000}k patients x {T} steps: discovery "
+                               f"(S-state Gram on f64 MFMA + STLSQ per state) + RK4 counterfactual rollout",
+                   "patients": N, "T": T, "states": S, "library_terms": F,
+                   "support_equals_truth": bool(torch.equal(mask != 0, truth != 0))},
+        "roofline": {"kernel": "gram_ms_kernel", "bound": "mfma", "achieved": gflop / (gram_ms_t * 1e-3) / 1e12,
+                     "peak": 78.6, "unit": "TFLOP/s", "frac": gflop / (gram_ms_t * 1e-3) / 1e12 / 78.6,
+                     "traffic": None, "avg_launch_ms": gram_ms_t,
+                     "issued_mfma_TFLOPs": mfma_flop / (gram_ms_t * 1e-3) / 1e12,
+                     "hbm_GBps": gram_bytes / (gram_ms_t * 1e-3) / 1e9},
+        "rollout": {"kernel": "rollout_ms_kernel (rk4, fp32)", "bound": "hbm", "avg_launch_ms": roll_ms_t,
+                    "algorithmic_bytes": roll_bytes, "achieved_GBps": roll_bytes / (roll_ms_t * 1e-3) / 1e9,
+                    "frac": roll_bytes / (roll_ms_t * 1e-3) / 1e9 / HBM_PEAK_GBPS},
+    }
+    print(json.dumps(out))
+
+
+def c5_main(args):
+    """Configuration C5 (BASELINE.json configs[4]): PK/PD EQ_4_C model rolled out with the adaptive
+    RK45 controller (scipy solve_ivp semantics, rtol = atol = 1.4e-8) on per-patient irregular grids
+    (20..60 observations on [0, 10]), 1M patients; arms switch per interval.  One step = one rollout
+    of every patient.  Lane-level step-size control: waves run until their slowest lane finishes."""
+    from insite_amd import ops, cohort
+    from insite_amd.library import polynomial_library
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    N = args.patients if args.patients != 100_000 else 1_000_000
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed + 5)
+    t_obs, n_obs = cohort.irregular_grid(N, seed=args.seed + 4, device=dev)
+    Tm = t_obs.size(0)
+    t_dev = torch.nan_to_num(t_obs, nan=0.0)
+    u = torch.randn((N, 2), generator=g, device=dev, dtype=torch.float64) * 0.05 + 0.5
+    y0 = torch.rand((N,), generator=g, device=dev, dtype=torch.float64) * 49 + 1
+    arm = (torch.rand((Tm, N), generator=g, device=dev) < 0.5).to(torch.int8)
+    bits = ops.pack_arm_bits(arm, N)
+    lib = polynomial_library(2, 2, True)
+    coef = torch.zeros((2, lib.n_terms), dtype=torch.float64, device=dev)
+    coef[0, 4], coef[1, 1], coef[1, 5] = -1.1108, -0.1454, -1.0235   # the EQ_4_C model (log :182)
+    y = torch.empty((Tm, N), dtype=torch.float64, device=dev)
+    steps = torch.empty((N,), dtype=torch.int32, device=dev)
+
+    def run():
+        ops.rollout_rk45(y0, u, bits, t_dev, n_obs, coef, lib, out=y, steps=steps)
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize(dev)
+    ms_step = (time.perf_counter() - t0) / args.steps * 1e3
+    st = steps.to(torch.float64)
+    per_wave = st[: N // 64 * 64].view(-1, 64)
+    intervals = (n_obs - 1).to(torch.float64)
+    out = {
+        "metric": METRIC, "value": N / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: irregular grids T_p ~ U{20..60} on [0,10], EQ_4_C statics, random per-interval arms",
+        "config": {"workload": f"C5: adaptive RK45 (rtol=atol=1.4e-8) on irregular grids, {N // 1000}k patients",
+                   "patients": N, "max_obs": Tm, "mean_intervals": float(intervals.mean())},
+        "rk45": {"mean_attempts_per_patient": float(st.mean()),
+                 "mean_attempts_per_interval": float(st.sum() / intervals.sum()),
+                 "wave_divergence": float((per_wave.max(dim=1).values.mean() / per_wave.mean()).item()),
+                 "rhs_evals_per_s": float(st.sum() * 6 / (ms_step * 1e-3))},
+    }
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        from oracle import rk45_ref as K
+        n_s = min(args.cpu_sample, 2000)
+        tc, nc = t_obs[:, :n_s].T.cpu().numpy(), n_obs[:n_s].cpu().numpy()
+        t1 = time.perf_counter()
+        K.rollout_rk45(y0[:n_s].cpu().numpy(), u[:n_s].cpu().numpy(), arm[:, :n_s].T.cpu().numpy(), tc, nc,
+                       coef.cpu().numpy(), lib.exps.astype(np.int64))
+        el = time.perf_counter() - t1
+        out["cpu_baseline"] = {"value": n_s / el, "unit": "patient-trajectories/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/rk45_ref.py (scalar restatement of scipy RK45) on {n_s} patients, "
+                                         f"{el:.2f} s"}
+    print(json.dumps(out))
+
+
 def main():
     args = parse()
+    if args.config == "c3":
+        return c3_main(args)
+    if args.config == "c5":
+        return c5_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -169,6 +169,22 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
                            int32_t n_arms, double dt, int32_t method, int32_t substeps,
                            double drop_below, double* y_out, int64_t ld_y, int32_t layout, void* stream);
 
+/* Adaptive RK45 rollout on irregular observation grids (configuration C5): for patient r and
+ * interval k < n_obs[r] - 1, y advances from t_obs[k, r] to t_obs[k + 1, r] under the arm of bit
+ * (r, k) of arm_bits (TIME_MAJOR_BITS [T_max, ld_arm], n_arms <= 2) by scipy's
+ * solve_ivp(method='RK45', rtol, atol) controller (Dormand-Prince 5(4), select_initial_step per
+ * interval; the reference odeint's tolerances are rtol = atol = 1.4e-8, pkpd/utils.py:87).  This
+ * replaces the fixed-grid odeint scan (sindy.py:413-424) when the observation times are irregular.
+ *   t_obs [T_max, ld_t] f64 time-major (ld_t >= n_rows), n_obs [n_rows] int32 in [1, T_max]
+ *   coef  [n_arms, F] or per row [n_rows, n_arms, F] (coef_row_stride = n_arms * F)
+ *   y_out [T_max, ld_y] f64: row k = state at t_obs[k + 1] (rows >= n_obs[r] - 1 untouched)
+ *   steps_out [n_rows] int32 step attempts (accepted + rejected) per row, may be NULL        */
+int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_t* arm_bits, int64_t ld_arm,
+                                const double* t_obs, int64_t ld_t, const int32_t* n_obs, const double* coef,
+                                int64_t coef_row_stride, const int8_t* exps, int32_t n_terms, int64_t n_rows,
+                                int32_t T_max, int32_t n_statics, int32_t n_arms, double rtol, double atol,
+                                double drop_below, double* y_out, int64_t ld_y, int32_t* steps_out, void* stream);
+
 /* Masked squared-error sums for the RMSE metrics (time_varying_model.py:236-313):
  *   err[r,k]  = (pred[r, k] * scale + shift - target[r, k])^2 * active[r, k]
  *   per_step_out[k] = sum_r err[r, k]        per_step_cnt_out[k] = sum_r active[r, k]

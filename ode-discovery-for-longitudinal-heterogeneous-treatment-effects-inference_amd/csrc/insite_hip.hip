@@ -1450,6 +1450,149 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
 }
 
 // =============================================================================================
+// Adaptive RK45 rollout on irregular observation grids (configuration C5)
+// =============================================================================================
+// scipy.integrate.solve_ivp(method='RK45') restated per observation interval (oracle/rk45_ref.py; scipy
+// 1.15.3 _ivp/rk.py RungeKutta._step_impl + common.select_initial_step), the treatment held over the
+// interval as the reference's odeint scan does (sindy.py:413-424).  Lane = patient: every lane runs its
+// own step-size controller, so lanes of a wavefront take different numbers of steps per interval (the
+// divergence C5 stresses: the wave runs until its slowest lane finishes the interval, finished lanes
+// masked).  The RHS is state-affine, f_a(y) = alpha_a + beta_a y (per-patient rates from the library).
+struct Rk45Args {
+  const double* y0;
+  const double* u;
+  const uint32_t* arm;  // TIME_MAJOR_BITS [T_max, lda]: arm of interval k
+  const double* t;      // [T_max, ldt] observation times (time-major)
+  const int32_t* nobs;  // [N] observations per patient (intervals = nobs - 1)
+  const double* coef;
+  double* y;            // [T_max, ldy]: row k = state at t[k + 1]
+  int32_t* steps;       // [N] RK45 step attempts (may be NULL)
+  int64_t lda, ldt, ldy, coef_stride, N;
+  int32_t Tmax, A;
+  double rtol, atol, drop;
+};
+
+template <int NARM, bool PERROW>
+__global__ void __launch_bounds__(kBlock) rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
+  constexpr double a21 = 1.0 / 5.0;
+  constexpr double a31 = 3.0 / 40.0, a32 = 9.0 / 40.0;
+  constexpr double a41 = 44.0 / 45.0, a42 = -56.0 / 15.0, a43 = 32.0 / 9.0;
+  constexpr double a51 = 19372.0 / 6561.0, a52 = -25360.0 / 2187.0, a53 = 64448.0 / 6561.0, a54 = -212.0 / 729.0;
+  constexpr double a61 = 9017.0 / 3168.0, a62 = -355.0 / 33.0, a63 = 46732.0 / 5247.0, a64 = 49.0 / 176.0,
+                   a65 = -5103.0 / 18656.0;
+  constexpr double b1 = 35.0 / 384.0, b3 = 500.0 / 1113.0, b4 = 125.0 / 192.0, b5 = -2187.0 / 6784.0, b6 = 11.0 / 84.0;
+  constexpr double e1 = -71.0 / 57600.0, e3 = 71.0 / 16695.0, e4 = -71.0 / 1920.0, e5 = 17253.0 / 339200.0,
+                   e6 = -22.0 / 525.0, e7 = 1.0 / 40.0;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t p0 = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * kWave;
+  if (p0 >= ra.N) return;
+  const int64_t p = p0 + lane;
+  const bool act = p < ra.N;
+  const int64_t pc = act ? p : ra.N - 1;
+  double uu[INSITE_MAX_STATICS];
+#pragma unroll
+  for (int t = 0; t < INSITE_MAX_STATICS; ++t) {
+    const double v = ra.u[pc * lib.U + (t < lib.U ? t : 0)];
+    uu[t] = (act && t < lib.U) ? v : 0.0;
+  }
+  double alpha[NARM], beta[NARM];
+  const double* cbase = ra.coef + (PERROW ? pc * ra.coef_stride : 0);
+#pragma unroll
+  for (int a = 0; a < NARM; ++a) {
+    alpha[a] = 0.0;
+    beta[a] = 0.0;
+    if (a >= ra.A) continue;
+    for (int j = 0; j < lib.F; ++j) {
+      const double c = cbase[a * lib.F + j];
+      if (fabs(c) > ra.drop) {
+        const double t = c * monomial(lib, j, uu);
+        if (lib.ex[j] == 0) alpha[a] += t;
+        else beta[a] += t;
+      }
+    }
+  }
+  int n = act ? ra.nobs[pc] : 0;
+  if (n > ra.Tmax) n = ra.Tmax;
+  const int nmax = wave_max_i(n);
+  double y = act ? ra.y0[pc] : 0.0;
+  int attempts = 0;
+  unsigned w = 0u;
+  const double rtol = ra.rtol, atol = ra.atol;
+  for (int k = 0; k + 1 < nmax; ++k) {
+    if ((k & 31) == 0) {  // arm bits of intervals [k, k + 32): one word per lane, half-wave transpose
+      const int kk = k + (lane & 31) < ra.Tmax ? k + (lane & 31) : ra.Tmax - 1;
+      const int64_t col = (p0 >> 5) + (lane >> 5);
+      const uint32_t v = col * 32 < ra.N ? ra.arm[(int64_t)kk * ra.lda + col] : 0u;
+      w = bit_transpose32(v, lane);
+    }
+    const bool on = k + 1 < n;
+    const int a = (int)((w >> (k & 31)) & 1u);
+    double al = alpha[0], be = beta[0];
+#pragma unroll
+    for (int aa = 1; aa < NARM; ++aa) {
+      al = (a == aa) ? alpha[aa] : al;
+      be = (a == aa) ? beta[aa] : be;
+    }
+    double t = on ? ra.t[(int64_t)k * ra.ldt + pc] : 0.0;
+    const double t1 = on ? ra.t[(int64_t)(k + 1) * ra.ldt + pc] : 0.0;
+    if (on && t < t1) {
+      // ---- select_initial_step (order 4, n = 1) ----
+      double f = fma(be, y, al);
+      const double interval = t1 - t;
+      double h_abs;
+      {
+        const double scale = atol + fabs(y) * rtol;
+        const double d0 = fabs(y / scale), d1 = fabs(f / scale);
+        double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+        h0 = fmin(h0, interval);
+        const double f1 = fma(be, y + h0 * f, al);
+        const double d2 = fabs((f1 - f) / scale) / h0;
+        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
+        h_abs = fmin(fmin(100.0 * h0, h1), interval);
+      }
+      // ---- accepted steps until t reaches t1 ----
+      while (t < t1) {
+        const double min_step = 10.0 * fabs(nextafter(t, INFINITY) - t);
+        if (h_abs < min_step) h_abs = min_step;
+        bool rejected = false;
+        for (;;) {
+          double t_new = t + h_abs;
+          if (t_new > t1) t_new = t1;
+          const double h = t_new - t;
+          h_abs = fabs(h);
+          const double k1 = f;
+          const double k2 = fma(be, y + (k1 * a21) * h, al);
+          const double k3 = fma(be, y + (k1 * a31 + k2 * a32) * h, al);
+          const double k4 = fma(be, y + ((k1 * a41 + k2 * a42) + k3 * a43) * h, al);
+          const double k5 = fma(be, y + (((k1 * a51 + k2 * a52) + k3 * a53) + k4 * a54) * h, al);
+          const double k6 = fma(be, y + ((((k1 * a61 + k2 * a62) + k3 * a63) + k4 * a64) + k5 * a65) * h, al);
+          const double y_new = y + h * ((((k1 * b1 + k3 * b3) + k4 * b4) + k5 * b5) + k6 * b6);
+          const double f_new = fma(be, y_new, al);
+          const double scale = atol + fmax(fabs(y), fabs(y_new)) * rtol;
+          const double e = ((((k1 * e1 + k3 * e3) + k4 * e4) + k5 * e5) + k6 * e6) + f_new * e7;
+          const double err = fabs(e * h / scale);
+          ++attempts;
+          if (err < 1.0) {
+            double factor = err == 0.0 ? 10.0 : fmin(10.0, 0.9 * pow(err, -0.2));
+            if (rejected) factor = fmin(1.0, factor);
+            h_abs *= factor;
+            t = t_new;
+            y = y_new;
+            f = f_new;
+            break;
+          }
+          h_abs *= fmax(0.2, 0.9 * pow(err, -0.2));
+          rejected = true;
+        }
+      }
+    }
+    if (on) __builtin_nontemporal_store(y, ra.y + (int64_t)k * ra.ldy + p);
+  }
+  if (act && ra.steps) ra.steps[p] = attempts;
+}
+
+// =============================================================================================
 // Masked squared-error sums (metrics)
 // =============================================================================================
 __global__ void __launch_bounds__(kBlock)
@@ -2104,6 +2247,36 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
   if (method == INSITE_METHOD_EULER) launch_rollout_m<INSITE_METHOD_EULER>(na, perrow, av, yv2, grid, hs, ra, lib);
   else launch_rollout_m<INSITE_METHOD_RK4>(na, perrow, av, yv2, grid, hs, ra, lib);
+  return launch_status();
+}
+
+int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_t* arm_bits, int64_t ld_arm,
+                                const double* t_obs, int64_t ld_t, const int32_t* n_obs, const double* coef,
+                                int64_t coef_row_stride, const int8_t* exps, int32_t n_terms, int64_t n_rows,
+                                int32_t T_max, int32_t n_statics, int32_t n_arms, double rtol, double atol,
+                                double drop_below, double* y_out, int64_t ld_y, int32_t* steps_out, void* stream) {
+  if (n_rows < 0 || T_max < 1 || n_arms < 1 || n_arms > 2 || !(rtol > 0.0) || !(atol > 0.0) ||
+      ld_t < n_rows || ld_y < n_rows || ld_arm < (n_rows + 31) / 32 || coef_row_stride < 0)
+    return INSITE_E_INVALID_ARG;
+  if (n_rows == 0) return INSITE_OK;
+  if (!y0 || !arm_bits || !t_obs || !n_obs || !coef || !y_out || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
+  LibDesc lib;
+  int32_t st = build_lib(exps, n_terms, n_statics, &lib);
+  if (st != INSITE_OK) return st;
+  if (coef_row_stride != 0 && coef_row_stride < (int64_t)n_arms * n_terms) return INSITE_E_INVALID_ARG;
+  Rk45Args ra{y0, n_statics > 0 ? u : y0, arm_bits, t_obs, n_obs, coef, y_out, steps_out, ld_arm, ld_t, ld_y,
+              coef_row_stride, n_rows, T_max, n_arms, rtol, atol, drop_below};
+  const int64_t waves = (n_rows + kWave - 1) / kWave;
+  const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  const bool perrow = coef_row_stride != 0;
+  if (n_arms == 1) {
+    if (perrow) rollout_rk45_kernel<1, true><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else rollout_rk45_kernel<1, false><<<grid, kBlock, 0, hs>>>(ra, lib);
+  } else {
+    if (perrow) rollout_rk45_kernel<2, true><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else rollout_rk45_kernel<2, false><<<grid, kBlock, 0, hs>>>(ra, lib);
+  }
   return launch_status();
 }
 

@@ -130,3 +130,22 @@ def counterfactual_arms(arm: torch.Tensor, T: int, seed: int, layout: str = "pat
     if lda > T:
         out[:, T:] = 0
     return out
+
+
+def irregular_grid(n_patients: int, seed: int, device, t_max: float = MAX_TIME_HORIZON, n_min: int = 20,
+                   n_max: int = 60):
+    """C5 observation grids on device (oracle/rk45_ref.irregular_grid distribution): T_p ~ U{n_min..n_max},
+    t_0 = 0 and T_p - 1 sorted U(0, t_max) times.  Returns (t_obs [n_max, N] f64 time-major — rows past
+    a patient's grid are NaN —, n_obs [N] int32)."""
+    dev = torch.device(device)
+    g = _gen(seed, dev)
+    N = int(n_patients)
+    n_obs = torch.randint(n_min, n_max + 1, (N,), generator=g, device=dev, dtype=torch.int32)
+    r = torch.rand((n_max - 1, N), generator=g, device=dev, dtype=torch.float64) * t_max
+    k = torch.arange(n_max - 1, device=dev)[:, None]
+    r = torch.where(k < (n_obs[None, :] - 1), r, torch.full_like(r, float("inf")))
+    r, _ = torch.sort(r, dim=0)
+    t = torch.empty((n_max, N), dtype=torch.float64, device=dev)
+    t[0] = 0.0
+    t[1:] = torch.where(torch.isinf(r), torch.full_like(r, float("nan")), r)
+    return t.contiguous(), n_obs

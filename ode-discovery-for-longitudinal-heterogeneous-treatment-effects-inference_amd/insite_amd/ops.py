@@ -51,7 +51,7 @@ def _dev(name, t, dtype, ndim=None):
         raise ValueError(f"{name}: expected {dtype}, got {t.dtype}")
     if ndim is not None and t.dim() != ndim:
         raise ValueError(f"{name}: expected {ndim}-d tensor, got shape {tuple(t.shape)}")
-    if t.dim() >= 1 and t.stride(-1) != 1:
+    if t.dim() >= 1 and t.size(-1) > 1 and t.stride(-1) != 1:   # a size-1 dimension may carry any stride
         raise ValueError(f"{name}: innermost dimension must be contiguous")
     if t.dim() == 2 and t.size(0) > 1 and t.stride(0) < t.size(1):
         raise ValueError(f"{name}: overlapping rows")
@@ -321,6 +321,54 @@ def plan_rollout(y0, u, arm, coef, lib, dt, method="euler5", substeps=None, drop
     """``rollout`` as a prepared launch; ``plan.out`` = y."""
     name, args, dev, out = _prep_rollout(y0, u, arm, coef, lib, dt, method, substeps, drop_below, T, out, layout)
     return Plan(name, args, dev, out)
+
+
+def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_obs: torch.Tensor,
+                 n_obs: torch.Tensor, coef: torch.Tensor, lib: PolyLibrary, rtol: float = 1.4e-8, atol: float = 1.4e-8,
+                 drop_below: float = 1e-3, out: torch.Tensor | None = None, steps: torch.Tensor | None = None):
+    """Adaptive RK45 rollout on per-patient irregular observation grids (insite_rollout_rk45_f64;
+    configuration C5).  y0 [N] f64, u [N,U] f64, arm_bits [T_max, >=ceil(N/32)] int32 (arm of each
+    interval, pack_arm_bits), t_obs [T_max, >=N] f64 time-major, n_obs [N] int32, coef [A,F] or
+    [N,A,F].  Returns (y [T_max, N] — row k = state at t_obs[k + 1] —, step attempts [N] int32)."""
+    _dev("y0", y0, torch.float64, 1)
+    N = y0.numel()
+    _dev("t_obs", t_obs, torch.float64, 2)
+    Tm = t_obs.size(0)
+    if t_obs.size(1) < N:
+        raise ValueError("t_obs must be [T_max, >=N]")
+    _dev("arm_bits", arm_bits, torch.int32, 2)
+    if arm_bits.size(0) < Tm or arm_bits.size(1) < (N + 31) // 32:
+        raise ValueError("arm_bits must be [>=T_max, >=ceil(N/32)] int32")
+    _dev("n_obs", n_obs, torch.int32, 1)
+    if n_obs.numel() != N:
+        raise ValueError("n_obs must have one entry per patient")
+    if lib.n_statics:
+        _dev("u", u, torch.float64, 2)
+        if u.size(0) != N or u.size(1) != lib.n_statics or u.stride(0) != lib.n_statics:
+            raise ValueError("u must be a contiguous [N, n_statics] tensor")
+    _dev("coef", coef, torch.float64)
+    F = lib.n_terms
+    if coef.dim() == 2:
+        A, stride = coef.size(0), 0
+    elif coef.dim() == 3 and coef.size(0) == N:
+        A, stride = coef.size(1), coef.size(1) * F
+    else:
+        raise ValueError("coef must be [A,F] or [N,A,F]")
+    if coef.size(-1) != F or not coef.is_contiguous():
+        raise ValueError("coef must be contiguous with the library's F columns")
+    if out is None:
+        out = torch.full((Tm, N), float("nan"), dtype=torch.float64, device=y0.device)
+    else:
+        _dev("out", out, torch.float64, 2)
+        if out.size(0) < Tm or out.size(1) < N:
+            raise ValueError("out must be [T_max, >=N]")
+    if steps is None:
+        steps = torch.empty((N,), dtype=torch.int32, device=y0.device)
+    tab = lib.ctypes_table()
+    args = (_p(y0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm_bits), arm_bits.stride(0), _p(t_obs),
+            t_obs.stride(0), _p(n_obs), _p(coef), stride, tab.ctypes.data_as(ctypes.c_void_p), F, N, Tm,
+            lib.n_statics, A, float(rtol), float(atol), float(drop_below), _p(out), out.stride(0), _p(steps))
+    return _run(("insite_rollout_rk45_f64", args, y0.device, (out, steps)))
 
 
 def masked_sse(pred: torch.Tensor, target: torch.Tensor, active: torch.Tensor, scale: float = 1.0,

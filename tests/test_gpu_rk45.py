@@ -1,0 +1,94 @@
+"""GPU parity of the adaptive RK45 rollout on irregular grids (configuration C5) vs oracle/rk45_ref.py
+(itself pinned to scipy's solve_ivp in test_rk45_oracle.py).  Tolerance: the same step-size controller
+in the same fp64 arithmetic — relative 1e-9 per sample (ulp-level differences can flip an accept/reject
+decision near err = 1, which moves the result by at most the RK45 tolerance) and fp64 RMSE <= 1e-6."""
+import numpy as np
+import pytest
+import torch
+from scipy.integrate import solve_ivp
+
+from oracle import insite_ref as R
+from oracle import rk45_ref as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(N, seed, per_patient=False):
+    rng = np.random.default_rng(seed)
+    ex = R.poly_library(3, 2, True)
+    t, n = K.irregular_grid(N, rng)
+    u = rng.normal(0.5, 0.05, (N, 2))
+    arm = (rng.random((N, 60)) < 0.5).astype(np.int8)
+    y0 = rng.uniform(1, 50, N)
+    coef = np.zeros((2, 7))
+    coef[0, 4] = -1.11
+    coef[1, 1] = -0.146
+    coef[1, 5] = -1.02
+    if per_patient:
+        coef = np.repeat(coef[None], N, axis=0) * rng.uniform(0.8, 1.2, (N, 1, 1))
+    return ex, t, n, u, arm, y0, coef
+
+
+def _run(dev, ex, t, n, u, arm, y0, coef):
+    from insite_amd import ops
+    from insite_amd.library import polynomial_library
+    lib = polynomial_library(2, 2, True)
+    assert np.array_equal(lib.exps.astype(np.int64), ex)
+    N = y0.size
+    tt = torch.tensor(np.ascontiguousarray(np.nan_to_num(t, nan=0.0).T), device=dev)
+    bits = ops.pack_arm_bits(torch.tensor(np.ascontiguousarray(arm.T), device=dev), N)
+    y, steps = ops.rollout_rk45(torch.tensor(y0, device=dev), torch.tensor(u, device=dev), bits, tt,
+                                torch.tensor(n, device=dev), torch.tensor(np.ascontiguousarray(coef), device=dev), lib)
+    torch.cuda.synchronize()
+    return y.cpu().numpy().T, steps.cpu().numpy()
+
+
+@pytest.mark.parametrize("N,seed", [(1, 0), (63, 1), (200, 2), (257, 3)])
+def test_rk45_rollout_matches_oracle(dev, N, seed):
+    ex, t, n, u, arm, y0, coef = _setup(N, seed)
+    y, steps = _run(dev, ex, t, n, u, arm, y0, coef)
+    ref, ref_steps = K.rollout_rk45(y0, u, arm, t, n, coef, ex)
+    valid = ~np.isnan(ref)
+    assert np.array_equal(np.isnan(y), ~valid)            # rows past each grid untouched (NaN)
+    rel = np.abs(y[valid] - ref[valid]) / np.abs(ref[valid])
+    assert rel.max() < 1e-9, rel.max()
+    assert np.sqrt(np.mean((y[valid] - ref[valid]) ** 2)) <= 1e-6
+    assert np.mean(steps == ref_steps) >= 0.99
+
+
+def test_rk45_rollout_per_patient_coefficients(dev):
+    ex, t, n, u, arm, y0, coef = _setup(150, 9, per_patient=True)
+    y, _ = _run(dev, ex, t, n, u, arm, y0, coef)
+    ref, _ = K.rollout_rk45(y0, u, arm, t, n, coef[0], ex) if False else (None, None)
+    # per-patient oracle: each patient with its own [A, F] rows
+    for p in range(0, 150, 7):
+        rp, _ = K.rollout_rk45(y0[p:p + 1], u[p:p + 1], arm[p:p + 1], t[p:p + 1], n[p:p + 1], coef[p], ex)
+        m = ~np.isnan(rp[0])
+        assert np.allclose(y[p, m], rp[0, m], rtol=1e-9, atol=0)
+
+
+def test_rk45_rollout_against_solve_ivp(dev):
+    """End-to-end against scipy itself on a few patients (the sub-oracle)."""
+    ex, t, n, u, arm, y0, coef = _setup(8, 5)
+    y, _ = _run(dev, ex, t, n, u, arm, y0, coef)
+    for p in range(8):
+        al, be = K.patient_rates(u[p], coef, ex)
+        v = y0[p]
+        for k in range(n[p] - 1):
+            a = arm[p, k]
+            if t[p, k + 1] > t[p, k]:
+                s = solve_ivp(lambda tt, w: al[a] + be[a] * w, (t[p, k], t[p, k + 1]), [v], method="RK45",
+                              rtol=K.RTOL, atol=K.ATOL)
+                v = s.y[0, -1]
+            assert abs(y[p, k] - v) <= 1e-9 * abs(v)
+
+
+def test_device_irregular_grid(dev):
+    from insite_amd import cohort
+    t, n = cohort.irregular_grid(10_000, seed=4, device=dev)
+    tc, nc = t.cpu().numpy(), n.cpu().numpy()
+    assert nc.min() >= 20 and nc.max() <= 60
+    for p in range(0, 10_000, 97):
+        g = tc[: nc[p], p]
+        assert g[0] == 0.0 and np.all(np.diff(g) >= 0) and g[-1] <= 10.0
+        assert np.isnan(tc[nc[p]:, p]).all()
