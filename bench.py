@@ -51,7 +51,7 @@ def parse():
                          "stream; pipeline: discovery of step i+1 overlaps the rollout of step i (two streams)")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5", "insite"],
                     help="c2: BASELINE configs[1], the headline line (default); c3: configs[2], the 5-state fp32 "
                          "system (parity-test configuration, measured separately)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
@@ -250,8 +250,75 @@ def c5_main(args):
     print(json.dumps(out))
 
 
+def insite_main(args):
+    """INSITE per-patient refinement (reference sindy.py:433-715): every row of a
+    counterfactual evaluation set refines the global EQ_4_C model by BFGS on its observed prefix
+    (tau = 5) and rolls its model out with Euler-5.  Rows: PK/PD trajectories of T = 60 observations,
+    sequence lengths U{1..59}, per-step arms (factual arm, flipped at a random step).  One step = one
+    refinement of every row (1M rows; the reference's tau-step test set has 59,000)."""
+    from insite_amd import ops, cohort
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    N = args.patients if args.patients != 100_000 else 1_000_000
+    T = 60
+    coh = cohort.synthetic_pkpd(N, T, seed=args.seed + 9, device=dev, equation="EQ_4_C")
+    V = coh.x[:, :T].contiguous()
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed + 10)
+    flip = torch.randint(1, T, (N, 1), generator=g, device=dev)
+    arm = torch.where(torch.arange(T, device=dev)[None, :] >= flip, 1 - coh.arm[:, None].to(torch.int64),
+                      coh.arm[:, None].to(torch.int64)).to(torch.int8).contiguous()
+    sl = torch.randint(1, T, (N,), generator=g, device=dev, dtype=torch.int32)
+    c0 = np.zeros((2, coh.lib.n_terms))
+    c0[0, 4], c0[1, 1], c0[1, 5] = -1.1107592869834308, -0.14540553723951796, -1.0234639833519243  # log :182
+    dt = 10.0 / T
+
+    def run():
+        return ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5)
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        preds, coef, status, iters = run()
+    torch.cuda.synchronize(dev)
+    ms_step = (time.perf_counter() - t0) / args.steps * 1e3
+    st = status.cpu().numpy()
+    it = iters.cpu().numpy()
+    out = {
+        "metric": METRIC, "value": N / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: on-device EQ_4_C cohort, T=60, seq_len U{1..59}, arm flip at a random step",
+        "config": {"workload": f"INSITE refinement (BFGS per row, tau=5, lam=10) + Euler-5 rollout, "
+                               f"{N // 1000}k rows", "rows": N, "T": T},
+        "insite": {"refined_rows": int((st >= 0).sum()), "converged": int((st == 0).sum()),
+                   "zoom_failed_fallback": int((st == 3).sum()), "mean_bfgs_iterations": float(it[st >= 0].mean()),
+                   "reference_wall_time_s": "88.96 s per INSITE EQ_4_A run incl. 59,000 + 11,800 refinements "
+                                            "(results/2_main_table/final_with_insite.txt:2346; SURVEY.md §6)"},
+    }
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        from oracle import insite_ref as R
+        from oracle import insite_refine_ref as Q
+        n_s = 300
+        Vh, ah, uh, sh = V[:n_s].cpu().numpy(), arm[:n_s].cpu().numpy(), coh.u[:n_s].cpu().numpy(), sl[:n_s].cpu().numpy()
+        ex = R.poly_library(3, 2, True)
+        t1 = time.perf_counter()
+        for i in range(n_s):
+            Q.refine_patient(Vh[i], ah[i], uh[i], int(sh[i]), c0, ex, dt, 10.0, 5)
+        el = time.perf_counter() - t1
+        out["cpu_baseline"] = {"value": n_s / el, "unit": "patient-trajectories/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/insite_refine_ref.py (jax BFGS restated, numpy) on {n_s} rows, "
+                                         f"{el:.2f} s"}
+    print(json.dumps(out))
+
+
 def main():
     args = parse()
+    if args.config == "insite":
+        return insite_main(args)
     if args.config == "c3":
         return c3_main(args)
     if args.config == "c5":

@@ -185,6 +185,27 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
                                 int32_t T_max, int32_t n_statics, int32_t n_arms, double rtol, double atol,
                                 double drop_below, double* y_out, int64_t ld_y, int32_t* steps_out, void* stream);
 
+/* INSITE per-patient refinement (reference SINDY._get_fine_tuned_predictions /
+ * f_to_min_func / predict_with_reduced_coefs, sindy.py:433-715, 767-794): for every row r with
+ * seq_len[r] > tau, the active global coefficients (|coef0| > 1e-3) are refined by BFGS
+ * (jax.scipy.optimize.minimize(method='BFGS') semantics) on
+ *   f(c) = mse(c) / (2.5 mse(coef0)) + lam * mean((coef0 - c)^2),
+ *   mse  = mean_{k < min(seq_len - tau, T - 1)} (V[k + 1] - pred_k)^2, pred = the Euler scan
+ *          (`substeps` sub-steps per dt; 5 = odeint) from V[0] under the row's per-step arms;
+ * BFGS status 3 (zoom failed) keeps coef0 (sindy.py:628-631).  Every row then gets the Euler scan
+ * of its (refined or global) model over all T steps.
+ *   V        [T, ld_v] f64 unscaled observations, time-major (ld_v >= n_rows)
+ *   arm_bits TIME_MAJOR_BITS [T, ld_arm] per-step arm (n_arms <= 2)
+ *   coef0    HOST [n_arms, F] f64: the global model (at most 8 active coefficients)
+ *   preds    [T, ld_p] f64 (row k = state after step k); coef_out [n_rows, n_arms, F] (may be NULL);
+ *   status_out [n_rows] int32 (-1 = not refined: seq_len <= tau; else the BFGS status: 0 converged,
+ *   1 maxiter, 3 zoom failed, 5 line-search maxiter), iters_out [n_rows] int32 (may be NULL). */
+int32_t insite_refine_f64(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, int64_t ld_arm,
+                          const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics, const int8_t* exps,
+                          int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam, int32_t tau,
+                          int32_t substeps, double* preds, int64_t ld_p, double* coef_out, int32_t* status_out,
+                          int32_t* iters_out, void* stream);
+
 /* Masked squared-error sums for the RMSE metrics (time_varying_model.py:236-313):
  *   err[r,k]  = (pred[r, k] * scale + shift - target[r, k])^2 * active[r, k]
  *   per_step_out[k] = sum_r err[r, k]        per_step_cnt_out[k] = sum_r active[r, k]

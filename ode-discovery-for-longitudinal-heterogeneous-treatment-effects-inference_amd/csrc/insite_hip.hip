@@ -1593,6 +1593,375 @@ __global__ void __launch_bounds__(kBlock) rollout_rk45_kernel(Rk45Args ra, LibDe
 }
 
 // =============================================================================================
+// INSITE per-patient refinement
+// =============================================================================================
+// Reference: SINDY._get_fine_tuned_predictions / f_to_min_func / predict_with_reduced_coefs
+// (sindy.py:433-715, 767-794); restatement oracle/insite_refine_ref.py.  Lane = patient.  Objective
+//   f(c) = mse(c * mask) / (2.5 mse(c0)) + lam * mean((c0 - c)^2),  mask = |c0| > 1e-3,
+//   mse  = mean over k < min(sl - tau, T - 1) of (V[k+1] - pred_k)^2, pred = Euler-5 scan from V[0],
+// minimised by jax.scipy.optimize.minimize(method='BFGS') restated (oracle docstring): BFGS with the
+// inverse-Hessian update, strong-Wolfe line search, cubic/quadratic/bisection zoom.  The objective
+// depends on c only through (alpha_a, beta_a) of the state-affine RHS, so one forward pass with four
+// tangents d y / d(alpha_0, beta_0, alpha_1, beta_1) gives f and the exact gradient (what jax's
+// autodiff computes).  Only the m active coefficients move (the search runs in that subspace; oracle
+// docstring); every lane runs its own optimiser — lanes finishing early idle until the wave's last.
+constexpr int kRefineMaxActive = 8;
+struct RefineArgs {
+  const double* V;      // [T, ldv] unscaled observations (time-major)
+  const uint32_t* arm;  // TIME_MAJOR_BITS [T, lda] per-step arm
+  const double* u;      // [N, U]
+  const int32_t* sl;    // [N] sequence lengths
+  double* preds;        // [T, ldp]
+  double* coef_out;     // [N, A, F] or NULL
+  int32_t* status;      // [N] or NULL (-1 skipped, else the BFGS status)
+  int32_t* iters;       // [N] or NULL
+  int64_t ldv, lda, ldp, N;
+  int32_t T, tau, sub, A, m, n_total;
+  double dt, lam;
+  int32_t t_flat[kRefineMaxActive], t_arm[kRefineMaxActive], t_ex[kRefineMaxActive], t_col[kRefineMaxActive];
+  double c0[INSITE_MAX_ARMS * INSITE_MAX_TERMS];  // the global model [A, F]
+};
+
+template <int M>
+struct RefineLane {
+  const RefineArgs& ra;
+  const LibDesc& lib;
+  int64_t p;
+  int K;
+  double norm;
+  double mono[M];
+  double c0a[M];
+  __device__ int armbit(int k) const {
+    return (int)((ra.arm[(int64_t)k * ra.lda + (p >> 5)] >> (p & 31)) & 1u);
+  }
+  // f and gradient at c (active coordinates)
+  __device__ double fg(const double (&c)[M], double (&g)[M]) const {
+    double al0 = 0.0, al1 = 0.0, be0 = 0.0, be1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      if (i >= ra.m) break;
+      const double t = c[i] * mono[i];
+      if (ra.t_ex[i] == 0) {
+        if (ra.t_arm[i] == 0) al0 += t; else al1 += t;
+      } else {
+        if (ra.t_arm[i] == 0) be0 += t; else be1 += t;
+      }
+    }
+    const double h = ra.dt / (double)ra.sub;
+    double y = ra.V[p];
+    double da0 = 0.0, da1 = 0.0, db0 = 0.0, db1 = 0.0;
+    double L = 0.0, gA0 = 0.0, gA1 = 0.0, gB0 = 0.0, gB1 = 0.0;
+    for (int k = 0; k < K; ++k) {
+      const int a = armbit(k);
+      const double al = a ? al1 : al0, be = a ? be1 : be0;
+      const double hb = h * be;
+      for (int s = 0; s < ra.sub; ++s) {
+        da0 = da0 + hb * da0;
+        da1 = da1 + hb * da1;
+        db0 = db0 + hb * db0;
+        db1 = db1 + hb * db1;
+        if (a) {
+          da1 += h;
+          db1 += h * y;
+        } else {
+          da0 += h;
+          db0 += h * y;
+        }
+        y = y + h * (al + be * y);
+      }
+      const double r = ra.V[(int64_t)(k + 1) * ra.ldv + p] - y;
+      L += r * r;
+      gA0 += -2.0 * r * da0;
+      gA1 += -2.0 * r * da1;
+      gB0 += -2.0 * r * db0;
+      gB1 += -2.0 * r * db1;
+    }
+    const double iK = 1.0 / (double)K;
+    L *= iK;
+    double pen = 0.0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      if (i >= ra.m) {
+        g[i] = 0.0;
+        continue;
+      }
+      const double d = c0a[i] - c[i];
+      pen += d * d;
+      const double gd = ra.t_ex[i] == 0 ? (ra.t_arm[i] ? gA1 : gA0) : (ra.t_arm[i] ? gB1 : gB0);
+      g[i] = gd * iK * mono[i] / norm + 2.0 * ra.lam * (c[i] - c0a[i]) / (double)ra.n_total;
+    }
+    return L / norm + ra.lam * pen / (double)ra.n_total;
+  }
+  __device__ double dot(const double (&a)[M], const double (&b)[M]) const {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) s += a[i] * b[i];
+    return s;
+  }
+  // phi(t) = f(x + t pk), dphi = g . pk
+  __device__ double phi(const double (&x)[M], const double (&pk)[M], double t, double& dphi, double (&g)[M]) const {
+    double xt[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) xt[i] = x[i] + t * pk[i];
+    const double f = fg(xt, g);
+    dphi = dot(g, pk);
+    return f;
+  }
+};
+
+__device__ __forceinline__ double cubicmin(double a, double fa, double fpa, double b, double fb, double c, double fc) {
+  const double C = fpa, db = b - a, dc = c - a;
+  const double denom = (db * dc) * (db * dc) * (db - dc);
+  const double A = (dc * dc * (fb - fa - C * db) + (-db * db) * (fc - fa - C * dc)) / denom;
+  const double B = ((-dc * dc * dc) * (fb - fa - C * db) + (db * db * db) * (fc - fa - C * dc)) / denom;
+  const double radical = B * B - 3.0 * A * C;
+  return a + (-B + sqrt(radical)) / (3.0 * A);
+}
+__device__ __forceinline__ double quadmin(double a, double fa, double fpa, double b, double fb) {
+  const double db = b - a;
+  const double B = (fb - fa - fpa * db) / (db * db);
+  return a - fpa / (2.0 * B);
+}
+
+template <int M>
+__global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, LibDesc lib) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= ra.N) return;
+  double uu[INSITE_MAX_STATICS];
+#pragma unroll
+  for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < lib.U ? ra.u[p * lib.U + t] : 0.0;
+  RefineLane<M> ln{ra, lib, p, 0, 1.0, {}, {}};
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    ln.mono[i] = i < ra.m ? monomial(lib, ra.t_col[i], uu) : 0.0;
+    ln.c0a[i] = i < ra.m ? ra.c0[ra.t_flat[i]] : 0.0;
+  }
+  double x[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
+  const int sl = ra.sl[p];
+  int status = -1, nit = 0;
+  if (sl > ra.tau && ra.T >= 2) {
+    ln.K = min(sl - ra.tau, ra.T - 1);
+    double g[M];
+    const double start = ln.fg(x, g);  // norm 1, penalty 0 at c0
+    ln.norm = start * 2.5;
+    // ---------------- BFGS (jax minimize_bfgs, norm = inf, gtol 1e-5) ----------------
+    double H[M][M];
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+      for (int j = 0; j < M; ++j) H[i][j] = i == j ? 1.0 : 0.0;
+    double f = ln.fg(x, g);
+    double gmax = 0.0, g2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      gmax = fmax(gmax, fabs(g[i]));
+      g2 += g[i] * g[i];
+    }
+    bool converged = gmax < 1e-5, failed = false;
+    double old_old = f + sqrt(g2) / 2.0;
+    int ls_status = 0;
+    const int maxiter = 200 * ra.n_total;
+    int k = 0;
+    while (!converged && !failed && k < maxiter) {
+      double pk[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < M; ++j) s += H[i][j] * g[j];
+        pk[i] = -s;
+      }
+      // ---- line search (jax line_search, c1 1e-4, c2 0.9, maxiter 10) ----
+      const double phi0 = f, dphi0 = ln.dot(g, pk);
+      const double cand = 1.01 * 2.0 * (phi0 - old_old) / dphi0;
+      const double start_a = cand > 1.0 ? 1.0 : cand;
+      bool ls_done = false, ls_failed = false;
+      int li = 1;
+      double a_i1 = 0.0, phi_i1 = phi0, dphi_i1 = dphi0;
+      double a_star = 0.0, phi_star = phi0;
+      double g_star[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) g_star[i] = g[i];
+      auto wolfe_one = [&](double a_, double ph) { return ph > phi0 + 1e-4 * a_ * dphi0; };
+      auto wolfe_two = [&](double dph) { return fabs(dph) <= -0.9 * dphi0; };
+      // zoom between (lo, hi); returns failure, fills the star point on success
+      auto zoom = [&](double a_lo, double phi_lo, double dphi_lo, double a_hi, double phi_hi, double dphi_hi,
+                      bool& z_failed) {
+        bool done = false;
+        z_failed = false;
+        int j = 0;
+        double a_rec = (a_lo + a_hi) / 2.0, phi_rec = (phi_lo + phi_hi) / 2.0;
+        double za = 1.0, zphi = phi_lo;
+        double zg[M];
+#pragma unroll
+        for (int i = 0; i < M; ++i) zg[i] = g[i];
+        while (!done && !z_failed) {
+          const double dalpha = a_hi - a_lo;
+          const double lo = fmin(a_hi, a_lo), hi = fmax(a_hi, a_lo);
+          const double cchk = 0.2 * dalpha, qchk = 0.1 * dalpha;
+          z_failed = z_failed || (dalpha <= 1e-10);
+          const double a_cub = cubicmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi, a_rec, phi_rec);
+          const bool use_cubic = (j > 0) && (a_cub > lo + cchk) && (a_cub < hi - cchk);
+          const double a_quad = quadmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi);
+          const bool use_quad = !use_cubic && (a_quad > lo + qchk) && (a_quad < hi - qchk);
+          double a_j = a_rec;
+          if (use_cubic) a_j = a_cub;
+          if (use_quad) a_j = a_quad;
+          if (!use_cubic && !use_quad) a_j = (a_lo + a_hi) / 2.0;
+          double dphi_j, g_j[M];
+          const double phi_j = ln.phi(x, pk, a_j, dphi_j, g_j);
+          const bool hi_to_j = wolfe_one(a_j, phi_j) || (phi_j >= phi_lo);
+          const bool star_to_j = wolfe_two(dphi_j) && !hi_to_j;
+          const bool hi_to_lo = (dphi_j * (a_hi - a_lo) >= 0.0) && !hi_to_j && !star_to_j;
+          const bool lo_to_j = !hi_to_j && !star_to_j;
+          if (hi_to_j) {
+            a_rec = a_hi;
+            phi_rec = phi_hi;
+            a_hi = a_j;
+            phi_hi = phi_j;
+            dphi_hi = dphi_j;
+          }
+          done = done || star_to_j;
+          if (star_to_j) {
+            za = a_j;
+            zphi = phi_j;
+#pragma unroll
+            for (int i = 0; i < M; ++i) zg[i] = g_j[i];
+          }
+          if (hi_to_lo) {
+            a_rec = a_hi;
+            phi_rec = phi_hi;
+            a_hi = a_lo;
+            phi_hi = phi_lo;
+            dphi_hi = dphi_lo;
+          }
+          if (lo_to_j) {
+            a_rec = a_lo;
+            phi_rec = phi_lo;
+            a_lo = a_j;
+            phi_lo = phi_j;
+            dphi_lo = dphi_j;
+          }
+          ++j;
+          z_failed = ((z_failed ? 1 : 0) | j) >= 30;  // jax: `failed | j >= 30` (no parentheses)
+        }
+        a_star = za;
+        phi_star = zphi;
+#pragma unroll
+        for (int i = 0; i < M; ++i) g_star[i] = zg[i];
+      };
+      while (!ls_done && li <= 10 && !ls_failed) {
+        const double a_i = li == 1 ? start_a : a_i1 * 2.0;
+        double dphi_i, g_i[M];
+        const double phi_i = ln.phi(x, pk, a_i, dphi_i, g_i);
+        const bool s_z1 = wolfe_one(a_i, phi_i) || ((phi_i >= phi_i1) && (li > 1));
+        const bool s_i = wolfe_two(dphi_i) && !s_z1;
+        const bool s_z2 = (dphi_i >= 0.0) && !s_z1 && !s_i;
+        if (s_z1) {
+          bool zf;
+          zoom(a_i1, phi_i1, dphi_i1, a_i, phi_i, dphi_i, zf);
+          ls_failed = ls_failed || zf;
+        }
+        if (s_i) {
+          a_star = a_i;
+          phi_star = phi_i;
+#pragma unroll
+          for (int i = 0; i < M; ++i) g_star[i] = g_i[i];
+        }
+        if (s_z2) {
+          bool zf;
+          zoom(a_i, phi_i, dphi_i, a_i1, phi_i1, dphi_i1, zf);
+          ls_failed = ls_failed || zf;
+        }
+        ls_done = s_z1 || ls_done || s_i || s_z2;
+        ++li;
+        a_i1 = a_i;
+        phi_i1 = phi_i;
+        dphi_i1 = dphi_i;
+      }
+      ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
+      failed = ls_failed || !ls_done;
+      // ---- BFGS update ----
+      double sk[M], yk[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        sk[i] = a_star * pk[i];
+        yk[i] = g_star[i] - g[i];
+      }
+      const double rho = 1.0 / ln.dot(yk, sk);
+      if (isfinite(rho)) {
+        double W[M][M], WH[M][M];
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+#pragma unroll
+          for (int j = 0; j < M; ++j) W[i][j] = (i == j ? 1.0 : 0.0) - rho * (sk[i] * yk[j]);
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+#pragma unroll
+          for (int j = 0; j < M; ++j) {
+            double s = 0.0;
+#pragma unroll
+            for (int q = 0; q < M; ++q) s += W[i][q] * H[q][j];
+            WH[i][j] = s;
+          }
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+#pragma unroll
+          for (int j = 0; j < M; ++j) {
+            double s = 0.0;
+#pragma unroll
+            for (int q = 0; q < M; ++q) s += WH[i][q] * W[j][q];
+            H[i][j] = s + rho * (sk[i] * sk[j]);
+          }
+      }
+      double gm = 0.0;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        x[i] = x[i] + sk[i];
+        g[i] = g_star[i];
+        gm = fmax(gm, fabs(g[i]));
+      }
+      converged = gm < 1e-5;
+      old_old = f;
+      f = phi_star;
+      ++k;
+    }
+    nit = k;
+    status = converged ? 0 : (k == maxiter ? 1 : (failed ? 2 + ls_status : -1));
+    if (status == 3) {  // zoom failed: the reference keeps the global coefficients (sindy.py:628-631)
+#pragma unroll
+      for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
+    }
+  }
+  // ---------------- final Euler scan with the (refined) model, every coefficient (sindy.py:668) ----------------
+  double cf[INSITE_MAX_ARMS * INSITE_MAX_TERMS];
+  for (int q = 0; q < ra.A * lib.F; ++q) cf[q] = ra.c0[q];
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+    if (i < ra.m) cf[ra.t_flat[i]] = x[i];
+  double al[2] = {0.0, 0.0}, be[2] = {0.0, 0.0};
+  for (int a = 0; a < ra.A && a < 2; ++a)
+    for (int j = 0; j < lib.F; ++j) {
+      const double t = cf[a * lib.F + j] * monomial(lib, j, uu);
+      if (lib.ex[j] == 0) al[a] += t;
+      else be[a] += t;
+    }
+  const double h = ra.dt / (double)ra.sub;
+  double y = ra.V[p];
+  for (int k = 0; k < ra.T; ++k) {
+    const int a = ln.armbit(k);
+    for (int s = 0; s < ra.sub; ++s) y = y + h * (al[a] + be[a] * y);
+    ra.preds[(int64_t)k * ra.ldp + p] = y;
+  }
+  if (ra.coef_out)
+    for (int q = 0; q < ra.A * lib.F; ++q) ra.coef_out[p * ra.A * lib.F + q] = cf[q];
+  if (ra.status) ra.status[p] = status;
+  if (ra.iters) ra.iters[p] = nit;
+}
+
+// =============================================================================================
 // Masked squared-error sums (metrics)
 // =============================================================================================
 __global__ void __launch_bounds__(kBlock)
@@ -2277,6 +2646,61 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
     if (perrow) rollout_rk45_kernel<2, true><<<grid, kBlock, 0, hs>>>(ra, lib);
     else rollout_rk45_kernel<2, false><<<grid, kBlock, 0, hs>>>(ra, lib);
   }
+  return launch_status();
+}
+
+int32_t insite_refine_f64(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, int64_t ld_arm,
+                          const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics, const int8_t* exps,
+                          int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam, int32_t tau,
+                          int32_t substeps, double* preds, int64_t ld_p, double* coef_out, int32_t* status_out,
+                          int32_t* iters_out, void* stream) {
+  if (n_rows < 0 || T < 1 || n_arms < 1 || n_arms > 2 || substeps < 1 || !(dt > 0.0) || !(lam >= 0.0) || tau < 0 ||
+      ld_v < n_rows || ld_p < n_rows || ld_arm < (n_rows + 31) / 32 || !coef0)
+    return INSITE_E_INVALID_ARG;
+  LibDesc lib;
+  int32_t st = build_lib(exps, n_terms, n_statics, &lib);
+  if (st != INSITE_OK) return st;
+  if (n_rows == 0) return INSITE_OK;
+  if (!V || !arm_bits || !seq_len || !preds || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
+  RefineArgs ra{};
+  ra.V = V;
+  ra.arm = arm_bits;
+  ra.u = n_statics > 0 ? u : V;
+  ra.sl = seq_len;
+  ra.preds = preds;
+  ra.coef_out = coef_out;
+  ra.status = status_out;
+  ra.iters = iters_out;
+  ra.ldv = ld_v;
+  ra.lda = ld_arm;
+  ra.ldp = ld_p;
+  ra.N = n_rows;
+  ra.T = T;
+  ra.tau = tau;
+  ra.sub = substeps;
+  ra.A = n_arms;
+  ra.n_total = n_arms * n_terms;
+  ra.dt = dt;
+  ra.lam = lam;
+  int m = 0;
+  for (int a = 0; a < n_arms; ++a)
+    for (int j = 0; j < n_terms; ++j) {
+      const double c = coef0[a * n_terms + j];
+      ra.c0[a * n_terms + j] = c;
+      if (fabs(c) > 1e-3) {  // coef_sparse_mask (sindy.py:587)
+        if (m >= kRefineMaxActive) return INSITE_E_UNSUPPORTED;
+        ra.t_flat[m] = a * n_terms + j;
+        ra.t_arm[m] = a;
+        ra.t_ex[m] = lib.ex[j];
+        ra.t_col[m] = j;
+        ++m;
+      }
+    }
+  ra.m = m;
+  const dim3 grid((unsigned)((n_rows + kBlock - 1) / kBlock));
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  if (m <= 4) insite_refine_kernel<4><<<grid, kBlock, 0, hs>>>(ra, lib);
+  else insite_refine_kernel<8><<<grid, kBlock, 0, hs>>>(ra, lib);
   return launch_status();
 }
 

@@ -371,6 +371,42 @@ def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_ob
     return _run(("insite_rollout_rk45_f64", args, y0.device, (out, steps)))
 
 
+def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: torch.Tensor, coef0: np.ndarray,
+                  lib: PolyLibrary, dt: float, lam: float, tau: int, substeps: int = 5):
+    """INSITE per-patient refinement (insite_refine_f64; reference sindy.py:433-715).  V [N, T] f64
+    unscaled observations and arm [N, T] int8 per-step arms in the reference's patient-major layout
+    (transposed to the kernel's time-major layout here), u [N, U], seq_len [N], coef0 the HOST global
+    model [A, F].  Returns (preds [N, T], coef [N, A, F], status [N], iterations [N])."""
+    _dev("V", V, torch.float64, 2)
+    _dev("arm", arm, torch.int8, 2)
+    N, T = V.shape
+    if arm.shape != (N, T):
+        raise ValueError("arm must be [N, T]")
+    if lib.n_statics:
+        _dev("u", u, torch.float64, 2)
+        if u.size(0) != N or u.size(1) != lib.n_statics or u.stride(0) != lib.n_statics:
+            raise ValueError("u must be a contiguous [N, n_statics] tensor")
+    _dev("seq_len", seq_len, torch.int32, 1)
+    c0 = np.ascontiguousarray(coef0, dtype=np.float64)
+    if c0.ndim != 2 or c0.shape[1] != lib.n_terms:
+        raise ValueError("coef0 must be a host [A, F] array")
+    A = c0.shape[0]
+    Vt = V.t().contiguous()
+    bits = pack_arm_bits(arm.t().contiguous(), N)
+    dev = V.device
+    preds = torch.empty((T, N), dtype=torch.float64, device=dev)
+    coef = torch.empty((N, A, lib.n_terms), dtype=torch.float64, device=dev)
+    status = torch.empty((N,), dtype=torch.int32, device=dev)
+    iters = torch.empty((N,), dtype=torch.int32, device=dev)
+    tab = lib.ctypes_table()
+    args = (_p(Vt), Vt.stride(0), T, _p(bits), bits.stride(0), _p(u) if lib.n_statics else ctypes.c_void_p(0),
+            _p(seq_len), N, lib.n_statics, tab.ctypes.data_as(ctypes.c_void_p), lib.n_terms,
+            c0.ctypes.data_as(ctypes.c_void_p), A, float(dt), float(lam), int(tau), int(substeps), _p(preds),
+            preds.stride(0), _p(coef), _p(status), _p(iters))
+    _run(("insite_refine_f64", args, dev, None))
+    return preds.t(), coef, status, iters
+
+
 def masked_sse(pred: torch.Tensor, target: torch.Tensor, active: torch.Tensor, scale: float = 1.0,
                shift: float = 0.0, workspace: Workspace | None = None):
     """Masked squared-error sums (insite_masked_sse_f64).  Returns (per_step[T], count[T], last[2])."""

@@ -13,12 +13,14 @@ through the C ABI (include/insite_hip.h):
   -> ``insite_sindy_fit_f64``: smoothing + 4th-order FD + library + per-arm Gram in one streaming
   kernel, then the reduction fused with STLSQ + unbias for every arm.
 * ``jit(vmap(simulate_cancer_volume))`` (sindy.py:413-431) -> ``insite_rollout_f64`` (Euler-5).
+* ``insite: true`` — ``pmap(vmap(simulate_cancer_volume_with_fine_tuning))`` (sindy.py:433-715): the
+  per-patient BFGS refinement -> ``insite_refine_f64`` (one lane per patient).
 
 The DE-format extraction (A1, pkpd/utils.py:523-606), the tau-step slice (A9) and the masked
 squared-error sums of the metrics (A10) also run on the device; only scalars and the returned
 prediction arrays cross back to the host.  Out of scope in this build (raise
-``NotImplementedError``): the INSITE per-patient refinement (``insite: true``),
-weak SINDy, the joint model, the degree-4 ablation library and the cancer_sim / EQ_5 datasets.
+``NotImplementedError``): weak SINDy, the joint model, the degree-4 ablation library and the
+cancer_sim / EQ_5 datasets.
 """
 from __future__ import annotations
 
@@ -36,6 +38,25 @@ MAX_SEQUENCE_LENGTH = 60
 MAX_TIME_HORIZON = 10.0
 STANDARD_DT = MAX_TIME_HORIZON / MAX_SEQUENCE_LENGTH   # pkpd/utils.py:53; SINDY.dt (sindy.py:89)
 RHS_COEF_EPS = 1e-3                                    # pkpd/utils.py:388
+
+
+# scipy.signal.savgol_filter(window_length=5, polyorder=3, mode='interp') weights: interior taps and the
+# polynomial-fit edge rows (the same table as the HIP kernels' sg_pos*/sg_interior)
+_SG53 = np.array([[69, 4, -6, 4, -1], [4, 54, 24, -16, 4], [-3, 12, 17, 12, -3], [4, -16, 24, 54, 4],
+                  [-1, 4, -6, 4, 69]], dtype=np.float64) / np.array([70, 70, 35, 70, 70], dtype=np.float64)[:, None]
+
+
+def savgol_5_3_rows(V: torch.Tensor) -> torch.Tensor:
+    """savgol(5, 3, mode='interp') along the time axis of [N, T] device rows (T >= 5)."""
+    W = torch.as_tensor(_SG53, device=V.device, dtype=V.dtype)
+    T = V.size(1)
+    out = torch.empty_like(V)
+    c = W[2]
+    out[:, 2:T - 2] = (c[0] * V[:, 0:T - 4] + c[1] * V[:, 1:T - 3] + c[2] * V[:, 2:T - 2] + c[3] * V[:, 3:T - 1]
+                       + c[4] * V[:, 4:T])
+    out[:, :2] = V[:, :5] @ W[:2].t()
+    out[:, T - 2:] = V[:, T - 5:] @ W[3:].t()
+    return out
 
 
 def _get(cfg, path, default=None):
@@ -131,9 +152,6 @@ class SINDY:
         if "EQ_4" not in self.dataset_name.upper():
             raise NotImplementedError(f"dataset {self.dataset_name!r}: this build covers the PK/PD EQ_4 family "
                                       "(cancer_sim / EQ_5 are SURVEY.md §8 F4)")
-        if self.insite:
-            raise NotImplementedError("INSITE per-patient refinement (insite: true) is SURVEY.md §8 F2, not in "
-                                      "this build; use +backbone=sindy")
         if self.wsindy:
             raise NotImplementedError("weak SINDy (wsindy: true) is not on the MI355X path")
         if self.joint_model:
@@ -203,8 +221,12 @@ class SINDY:
         return self
 
     # ------------------------------------------------------------------ rollout (A8)
-    def _predict_device(self, dataset):
-        """Standardised open-loop predictions [N, T-1] on the device (sindy.py:371-431)."""
+    def _predict_device(self, dataset, tau=1):
+        """Standardised open-loop predictions [N, T-1] on the device (sindy.py:371-431); with
+        ``insite`` the per-patient refined predictions (get_predictions passes the reference's default
+        projection_horizon=1, the autoregressive path the dataset's tau; sindy.py:362-369, 736-738)."""
+        if self.insite:
+            return self._refined_device(dataset, tau)
         if self._coef_dev is None:
             raise RuntimeError("fit() first")
         d = dataset.data
@@ -214,6 +236,25 @@ class SINDY:
         y = ops.rollout(prev[:, 0].contiguous(), stat, arm, self._coef_dev, self.library, self.dt,
                         method=self.integrator, drop_below=0.0, T=T)
         return (y - mean) / std
+
+    def _refined_device(self, dataset, tau):
+        """INSITE predictions (sindy.py:433-715): every row with sequence_length > tau refines the active
+        global coefficients by BFGS on its own observed prefix (insite_refine_f64, one lane per row),
+        then rolls its refined model out with the reference's Euler-5 odeint.  Standardised [N, T]."""
+        if self.joint_coefs is None:
+            raise RuntimeError("fit() first")
+        if self.lam is None:
+            raise ValueError("model.lam must be set for insite: true (reference config: 10.0 for EQ_4)")
+        d = dataset.data
+        prev, stat, std, mean = self._unscaled_inputs(dataset)
+        if self.smooth_input_data:      # applied here in the reference (sindy.py:557-560), unlike the DE format
+            prev = savgol_5_3_rows(prev)
+        arm = torch.as_tensor(np.argmax(d["current_treatments"], axis=-1).astype(np.int8), device=self.device)
+        sl = torch.as_tensor(np.asarray(d["sequence_lengths"]).astype(np.int32), device=self.device)
+        preds, coef, status, iters = ops.insite_refine(prev.contiguous(), arm.contiguous(), stat, sl, self.joint_coefs,
+                                                       self.library, self.dt, float(self.lam), int(tau), substeps=5)
+        self.insite_status, self.insite_iters, self.insite_coefs = status, iters, coef
+        return ((preds - mean) / std).contiguous()
 
     def get_predictions(self, dataset) -> np.ndarray:
         logger.info("Predictions for %s.", getattr(dataset, "subset_name", "?"))
@@ -233,7 +274,8 @@ class SINDY:
 
     def get_autoregressive_predictions(self, dataset) -> np.ndarray:
         logger.info("Autoregressive Prediction for %s.", getattr(dataset, "subset_name", "?"))
-        return self._slice_device(self._predict_device(dataset), dataset).cpu().numpy()[..., None]
+        pred = self._predict_device(dataset, tau=self.projection_horizon)
+        return self._slice_device(pred, dataset).cpu().numpy()[..., None]
 
     # ------------------------------------------------------------------ metrics (A10)
     def _sse(self, pred_scaled, target, active, std, mean):
@@ -271,7 +313,8 @@ class SINDY:
         assert seq is not None, "dataset has no data_processed_seq (process_data_multi first)"
         sp = dataset.scaling_params
         std, mean = float(sp["output_stds"]), float(sp["output_means"])
-        pred = self._slice_device(self._predict_device(dataset if datasets_mc is None else datasets_mc), dataset)
+        pred = self._slice_device(self._predict_device(dataset if datasets_mc is None else datasets_mc,
+                                                       tau=self.projection_horizon), dataset)
         key = "unscaled_outputs" if self.unscale_rmse else "outputs"
         not_nan = ~np.isnan(seq["outputs"][..., 0]).any(axis=1)          # time_varying_model.py:302-303
         idx = torch.as_tensor(np.nonzero(not_nan)[0], device=pred.device)

@@ -1,0 +1,308 @@
+"""CPU restatement of the INSITE per-patient refinement — TEST INFRASTRUCTURE ONLY
+(imported by tests/ and bench.py's cpu_baseline leg, never by the product package).
+
+Reference: ``SINDY._get_fine_tuned_predictions`` / ``f_to_min_func`` / ``predict_with_reduced_coefs``
+(libs_m/ct/src/models/sindy.py:433-715, 767-794).  Per patient with sequence_length > tau:
+
+  mask    = |c0| > 1e-3                                  (coef_sparse_mask, :587)
+  preds   = Euler-5 scan of sum_j c_aj Theta_j(y, u) from V[0] under the patient's per-step arms
+  mse(c)  = sum_{k < sl - tau} (V[k+1] - preds[k])^2 / #      (create_mask, pkpd/utils.py:367-370; :781-792)
+  f(c)    = mse(c * mask) / (2.5 mse(c0)) + lam * mean((c0 - c)^2)       (norm_const = start_res * 2.5, :614)
+  c*      = jax.scipy.optimize.minimize(f, c0, method='BFGS', tol=1e-12)  (:627); status 3 -> keep c0 (:628-631)
+  output  = preds(c*) over the whole row                                  (:668)
+
+The minimiser is a third-party algorithm: jax (unpinned; a transitive dependency of sympy2jax,
+setup/requirements.txt) ``jax/_src/scipy/optimize/{minimize,bfgs,line_search}.py``, restated here:
+``minimize`` passes no tolerance to ``minimize_bfgs`` (gtol = 1e-5 on the inf-norm of the gradient,
+maxiter = 200 * size(x0), line_search maxiter = 10), BFGS with H0 = I and the inverse update
+H <- (I - rho s y^T) H (I - rho y s^T) + rho s s^T (kept when rho is not finite); strong-Wolfe line search
+(c1 = 1e-4, c2 = 0.9, first trial min(1, 1.01 * 2 (f_k - f_{k-1}) / phi'(0)), then doubling) with the
+cubic / quadratic / bisection zoom (delta1 = 0.2, delta2 = 0.1, dalpha threshold 1e-10, and jax's
+``failed | j >= 30`` written without parentheses, i.e. (failed | j) >= 30).  Status: 0 converged, 1
+maxiter, 2 + line-search status (1 zoom failed, 3 line-search maxiter).  Without jax this restatement
+is **parity unpinned** against the reference; tests pin the objective/gradient (finite differences), the
+minimiser (scipy.optimize.minimize BFGS reaches the same optimum) and the GPU kernel (same algorithm).
+
+Only the masked-in coefficients move: inactive ones have zero data gradient and start at c0, so the
+penalty gradient is zero and BFGS (H0 = I) keeps its inverse Hessian block-diagonal — the search runs
+in the m-dimensional active subspace with identical arithmetic (the mean is still over all A*F).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import insite_ref as R
+
+C1, C2 = 1e-4, 0.9
+GTOL = 1e-5
+LS_MAXITER = 10
+MASK_EPS = 1e-3
+
+
+def active_terms(c0, exps):
+    """Active coefficients (|c0| > 1e-3): list of (flat index, arm, state exponent, column)."""
+    A, F = c0.shape
+    out = []
+    for a in range(A):
+        for j in range(F):
+            if abs(c0[a, j]) > MASK_EPS:
+                out.append((a * F + j, a, int(exps[j, 0]), j))
+    return out
+
+
+def monomials(u, exps):
+    m = np.ones(exps.shape[0])
+    for j, e in enumerate(exps):
+        for i in range(1, e.shape[0]):
+            for _ in range(int(e[i])):
+                m[j] *= u[i - 1]
+    return m
+
+
+class PatientProblem:
+    """f(c_active) and its gradient for one patient: V [T'] unscaled observations, arms [T'] per step,
+    K = min(sl - tau, T' - 1) loss terms."""
+
+    def __init__(self, V, arms, u, c0, exps, K, dt, lam, substeps=R.STEPS_FOR_DT):
+        self.V = np.asarray(V, dtype=np.float64)
+        self.arms = np.asarray(arms, dtype=np.int64)
+        self.terms = active_terms(c0, exps)
+        self.mono = monomials(u, exps)
+        self.c0 = np.array([c0.flat[t[0]] for t in self.terms])
+        self.n_total = c0.size
+        self.K = int(K)
+        self.h = dt / substeps
+        self.sub = substeps
+        self.lam = lam
+        self.norm = 1.0
+        self.A = c0.shape[0]
+
+    def rates(self, c):
+        al = np.zeros(self.A)
+        be = np.zeros(self.A)
+        for ci, (_, a, ex, j) in zip(c, self.terms):
+            if ex == 0:
+                al[a] += ci * self.mono[j]
+            else:
+                be[a] += ci * self.mono[j]
+        return al, be
+
+    def mse_and_grad(self, c):
+        """Euler-5 rollout with forward sensitivities d y / d(alpha_a, beta_a)."""
+        al, be = self.rates(c)
+        A = self.A
+        y = self.V[0]
+        dya = np.zeros(A)
+        dyb = np.zeros(A)
+        L = 0.0
+        gA = np.zeros(A)
+        gB = np.zeros(A)
+        h = self.h
+        for k in range(self.K):
+            a = self.arms[k]
+            for _ in range(self.sub):
+                b = be[a]
+                ndya = dya + h * b * dya
+                ndyb = dyb + h * b * dyb
+                ndya[a] += h
+                ndyb[a] += h * y
+                y = y + h * (al[a] + b * y)
+                dya, dyb = ndya, ndyb
+            r = self.V[k + 1] - y
+            L += r * r
+            gA += -2.0 * r * dya
+            gB += -2.0 * r * dyb
+        return L / self.K, gA / self.K, gB / self.K
+
+    def value_and_grad(self, c):
+        L, gA, gB = self.mse_and_grad(c)
+        f = L / self.norm + self.lam * np.sum((self.c0 - c) ** 2) / self.n_total
+        g = np.empty_like(c)
+        for i, (_, a, ex, j) in enumerate(self.terms):
+            g[i] = (gA[a] if ex == 0 else gB[a]) * self.mono[j] / self.norm
+        g += 2.0 * self.lam * (c - self.c0) / self.n_total
+        return f, g
+
+
+# ------------------------------------------------------------------------------------------------
+# jax.scipy.optimize BFGS + line search (restated)
+# ------------------------------------------------------------------------------------------------
+def _cubicmin(a, fa, fpa, b, fb, c, fc):
+    C = fpa
+    db = b - a
+    dc = c - a
+    denom = (db * dc) ** 2 * (db - dc)
+    d1 = np.array([[dc ** 2, -db ** 2], [-dc ** 3, db ** 3]])
+    d2 = np.array([fb - fa - C * db, fc - fa - C * dc])
+    with np.errstate(all="ignore"):
+        A, B = (d1 @ d2) / denom
+        radical = B * B - 3.0 * A * C
+        return a + (-B + np.sqrt(radical)) / (3.0 * A)
+
+
+def _quadmin(a, fa, fpa, b, fb):
+    D = fa
+    C = fpa
+    db = b - 1.0 * a
+    with np.errstate(all="ignore"):
+        B = (fb - D - C * db) / (db ** 2)
+        return a - C / (2.0 * B)
+
+
+def _zoom(phi_fn, wolfe_one, wolfe_two, a_lo, phi_lo, dphi_lo, a_hi, phi_hi, dphi_hi, g_0):
+    st = dict(done=False, failed=False, j=0, a_lo=a_lo, phi_lo=phi_lo, dphi_lo=dphi_lo, a_hi=a_hi, phi_hi=phi_hi,
+              dphi_hi=dphi_hi, a_rec=(a_lo + a_hi) / 2.0, phi_rec=(phi_lo + phi_hi) / 2.0, a_star=1.0,
+              phi_star=phi_lo, dphi_star=dphi_lo, g_star=g_0, nfev=0)
+    delta1, delta2 = 0.2, 0.1
+    while (not st["done"]) and (not st["failed"]):
+        dalpha = st["a_hi"] - st["a_lo"]
+        a = min(st["a_hi"], st["a_lo"])
+        b = max(st["a_hi"], st["a_lo"])
+        cchk = delta1 * dalpha
+        qchk = delta2 * dalpha
+        st["failed"] = st["failed"] or (dalpha <= 1e-10)
+        a_cub = _cubicmin(st["a_lo"], st["phi_lo"], st["dphi_lo"], st["a_hi"], st["phi_hi"], st["a_rec"], st["phi_rec"])
+        use_cubic = (st["j"] > 0) and (a_cub > a + cchk) and (a_cub < b - cchk)
+        a_quad = _quadmin(st["a_lo"], st["phi_lo"], st["dphi_lo"], st["a_hi"], st["phi_hi"])
+        use_quad = (not use_cubic) and (a_quad > a + qchk) and (a_quad < b - qchk)
+        use_bis = (not use_cubic) and (not use_quad)
+        a_j = st["a_rec"]
+        if use_cubic:
+            a_j = a_cub
+        if use_quad:
+            a_j = a_quad
+        if use_bis:
+            a_j = (st["a_lo"] + st["a_hi"]) / 2.0
+        phi_j, dphi_j, g_j = phi_fn(a_j)
+        st["nfev"] += 1
+        hi_to_j = wolfe_one(a_j, phi_j) or (phi_j >= st["phi_lo"])
+        star_to_j = wolfe_two(dphi_j) and (not hi_to_j)
+        hi_to_lo = (dphi_j * (st["a_hi"] - st["a_lo"]) >= 0.0) and (not hi_to_j) and (not star_to_j)
+        lo_to_j = (not hi_to_j) and (not star_to_j)
+        if hi_to_j:
+            st.update(a_hi=a_j, phi_hi=phi_j, dphi_hi=dphi_j, a_rec=st["a_hi"], phi_rec=st["phi_hi"])
+        st["done"] = star_to_j or st["done"]
+        if star_to_j:
+            st.update(a_star=a_j, phi_star=phi_j, dphi_star=dphi_j, g_star=g_j)
+        if hi_to_lo:
+            st.update(a_hi=st["a_lo"], phi_hi=st["phi_lo"], dphi_hi=st["dphi_lo"], a_rec=st["a_hi"],
+                      phi_rec=st["phi_hi"])
+        if lo_to_j:
+            st.update(a_lo=a_j, phi_lo=phi_j, dphi_lo=dphi_j, a_rec=st["a_lo"], phi_rec=st["phi_lo"])
+        st["j"] += 1
+        st["failed"] = (int(st["failed"]) | st["j"]) >= 30    # jax: failed | j >= 30 (no parentheses)
+    return st
+
+
+def line_search(fg, xk, pk, old_fval, old_old_fval, gfk, maxiter=LS_MAXITER):
+    def phi_fn(t):
+        f, g = fg(xk + t * pk)
+        return f, float(g @ pk), g
+
+    phi_0 = old_fval
+    dphi_0 = float(gfk @ pk)
+    cand = 1.01 * 2 * (phi_0 - old_old_fval) / dphi_0
+    start = 1.0 if cand > 1 else cand
+
+    def wolfe_one(a_i, phi_i):
+        return phi_i > phi_0 + C1 * a_i * dphi_0
+
+    def wolfe_two(dphi_i):
+        return abs(dphi_i) <= -C2 * dphi_0
+
+    st = dict(done=False, failed=False, i=1, a_i1=0.0, phi_i1=phi_0, dphi_i1=dphi_0, nfev=0, a_star=0.0,
+              phi_star=phi_0, dphi_star=dphi_0, g_star=gfk)
+    while (not st["done"]) and (st["i"] <= maxiter) and (not st["failed"]):
+        a_i = start if st["i"] == 1 else st["a_i1"] * 2.0
+        phi_i, dphi_i, g_i = phi_fn(a_i)
+        st["nfev"] += 1
+        s_z1 = wolfe_one(a_i, phi_i) or ((phi_i >= st["phi_i1"]) and (st["i"] > 1))
+        s_i = wolfe_two(dphi_i) and (not s_z1)
+        s_z2 = (dphi_i >= 0.0) and (not s_z1) and (not s_i)
+        if s_z1:
+            z = _zoom(phi_fn, wolfe_one, wolfe_two, st["a_i1"], st["phi_i1"], st["dphi_i1"], a_i, phi_i, dphi_i, gfk)
+            st["nfev"] += z["nfev"]
+            st["failed"] = st["failed"] or z["failed"]
+            st.update(a_star=z["a_star"], phi_star=z["phi_star"], dphi_star=z["dphi_star"], g_star=z["g_star"])
+        if s_i:
+            st.update(a_star=a_i, phi_star=phi_i, dphi_star=dphi_i, g_star=g_i)
+        if s_z2:
+            z = _zoom(phi_fn, wolfe_one, wolfe_two, a_i, phi_i, dphi_i, st["a_i1"], st["phi_i1"], st["dphi_i1"], gfk)
+            st["nfev"] += z["nfev"]
+            st["failed"] = st["failed"] or z["failed"]
+            st.update(a_star=z["a_star"], phi_star=z["phi_star"], dphi_star=z["dphi_star"], g_star=z["g_star"])
+        st["done"] = s_z1 or st["done"] or s_i or s_z2
+        st.update(i=st["i"] + 1, a_i1=a_i, phi_i1=phi_i, dphi_i1=dphi_i)
+    status = 1 if st["failed"] else (3 if st["i"] > maxiter else 0)
+    return dict(failed=st["failed"] or not st["done"], a_k=st["a_star"], f_k=st["phi_star"], g_k=st["g_star"],
+                status=status, nfev=st["nfev"])
+
+
+def minimize_bfgs(fg, x0, maxiter, gtol=GTOL):
+    """jax minimize_bfgs (norm = inf): returns (x, f, status, iterations, function evaluations)."""
+    d = x0.size
+    H = np.eye(d)
+    f, g = fg(x0)
+    x = x0.copy()
+    converged = np.max(np.abs(g)) < gtol if d else True
+    failed = False
+    k = 0
+    nfev = 1
+    old_old = f + np.linalg.norm(g) / 2
+    ls_status = 0
+    while (not converged) and (not failed) and k < maxiter:
+        p = -(H @ g)
+        ls = line_search(fg, x, p, f, old_old, g)
+        nfev += ls["nfev"]
+        failed = ls["failed"]
+        ls_status = ls["status"]
+        s = ls["a_k"] * p
+        x_new = x + s
+        f_new, g_new = ls["f_k"], ls["g_k"]
+        y = g_new - g
+        with np.errstate(all="ignore"):
+            rho = np.float64(1.0) / np.float64(y @ s)
+        if np.isfinite(rho):
+            w = np.eye(d) - rho * np.outer(s, y)
+            H = w @ H @ w.T + rho * np.outer(s, s)
+        converged = np.max(np.abs(g_new)) < gtol
+        old_old = f
+        x, f, g = x_new, f_new, g_new
+        k += 1
+    status = 0 if converged else (1 if k == maxiter else (2 + ls_status if failed else -1))
+    return x, f, status, k, nfev
+
+
+def euler5_rollout(V0, arms, u, coef, exps, dt, T):
+    """predict_with_reduced_coefs (sindy.py:767-778): Euler-5 scan with every coefficient (no RHS drop)."""
+    mono = monomials(u, exps)
+    y = float(V0)
+    out = np.empty(T)
+    h = dt / R.STEPS_FOR_DT
+    for k in range(T):
+        a = int(arms[k])
+        al = sum(coef[a, j] * mono[j] for j in range(exps.shape[0]) if exps[j, 0] == 0)
+        be = sum(coef[a, j] * mono[j] for j in range(exps.shape[0]) if exps[j, 0] == 1)
+        for _ in range(R.STEPS_FOR_DT):
+            y = y + h * (al + be * y)
+        out[k] = y
+    return out
+
+
+def refine_patient(V, arms, u, sl, c0, exps, dt, lam, tau):
+    """One patient of ``simulate_cancer_volume_with_fine_tuning`` (sindy.py:570-668).  Returns
+    (preds [T'], refined coefficients [A, F], status, iterations); status -1 = skipped (sl <= tau)."""
+    T = V.shape[0]
+    c0 = np.asarray(c0, dtype=np.float64)
+    if sl <= tau:
+        return euler5_rollout(V[0], arms, u, c0, exps, dt, T), c0.copy(), -1, 0
+    K = min(int(sl) - tau, T - 1)
+    pb = PatientProblem(V, arms, u, c0, exps, K, dt, lam)
+    start, _ = pb.value_and_grad(pb.c0)          # norm_const = 1, penalty 0 at c0
+    pb.norm = start * 2.5
+    x, f, status, k, _ = minimize_bfgs(pb.value_and_grad, pb.c0.copy(), maxiter=200 * c0.size)
+    c = c0.copy()
+    if status != 3:
+        for xi, (flat, _, _, _) in zip(x, pb.terms):
+            c.flat[flat] = xi
+    return euler5_rollout(V[0], arms, u, c, exps, dt, T), c, status, k

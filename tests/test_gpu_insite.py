@@ -1,0 +1,101 @@
+"""GPU parity of the INSITE per-patient refinement (insite_refine_f64) against the
+restatement oracle/insite_refine_ref.py (jax BFGS semantics; parity against jax itself is unpinned —
+jax is absent — see that module).  Same algorithm in fp64 on both sides: statuses identical, refined
+coefficients to 1e-7 relative (an ulp-level difference can move a line-search trial point; both stop at
+the same gtol), predictions RMSE <= 1e-6 (north-star trajectory tolerance)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import insite_ref as R
+from oracle import insite_refine_ref as Q
+
+pytestmark = pytest.mark.gpu
+EX = R.poly_library(3, 2, True)
+
+
+@pytest.fixture(scope="module")
+def model():
+    coll = R.make_collection("EQ_4_C", {"train": 200, "val": 10, "test": 30}, seq_length=60, seed=2)
+    tr = coll["train"]
+    x, u, arm, rows = R.de_format(tr.data, tr.scaling_params)
+    G, b = R.gram_moments(x, u, arm, rows, R.STANDARD_DT, EX)
+    c0 = np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)])
+    return coll, x, u, arm, c0
+
+
+def _run(dev, V, arms, u, sl, c0, tau, lam=10.0):
+    from insite_amd import ops
+    from insite_amd.library import polynomial_library
+    lib = polynomial_library(2, 2, True)
+    preds, coef, status, iters = ops.insite_refine(torch.tensor(V, device=dev), torch.tensor(arms, device=dev),
+                                                   torch.tensor(u, device=dev), torch.tensor(sl, device=dev), c0, lib,
+                                                   R.STANDARD_DT, lam, tau)
+    torch.cuda.synchronize()
+    return preds.cpu().numpy(), coef.cpu().numpy(), status.cpu().numpy(), iters.cpu().numpy()
+
+
+@pytest.mark.parametrize("tau", [1, 5])
+def test_refine_matches_oracle(dev, model, tau):
+    coll, x, u, arm, c0 = model
+    rng = np.random.default_rng(tau)
+    N, T = 150, x.shape[1]
+    V = x[:N].copy()
+    arms = np.repeat(arm[:N, None], T, axis=1).astype(np.int8)
+    flip = rng.integers(10, T, N)
+    for i in range(0, N, 3):                      # per-step treatment switches in a third of the rows
+        arms[i, flip[i]:] = 1 - arms[i, flip[i]:]
+    sl = rng.integers(1, T + 1, N).astype(np.int32)
+    sl[:4] = [1, tau, tau + 1, T]
+    preds, coef, status, iters = _run(dev, V, arms, u[:N], sl, c0, tau)
+    for p in range(N):
+        rp, rc, rs, ri = Q.refine_patient(V[p], arms[p], u[p], sl[p], c0, EX, R.STANDARD_DT, 10.0, tau)
+        assert status[p] == rs, (p, status[p], rs)
+        assert np.abs(coef[p] - rc).max() <= 1e-7 * max(1.0, np.abs(rc).max()), p
+        assert np.sqrt(np.mean((preds[p] - rp) ** 2)) <= 1e-6
+    assert (status[sl <= tau] == -1).all() and (iters[sl > tau] > 0).all()
+
+
+def test_refined_model_fits_better_than_global(dev, model):
+    coll, x, u, arm, c0 = model
+    N, T = 100, x.shape[1]
+    arms = np.repeat(arm[:N, None], T, axis=1).astype(np.int8)
+    sl = np.full(N, T, dtype=np.int32)
+    preds, coef, status, _ = _run(dev, x[:N], arms, u[:N], sl, c0, 5)
+    K = T - 5
+    base = np.stack([Q.euler5_rollout(x[p, 0], arms[p], u[p], c0, EX, R.STANDARD_DT, T) for p in range(N)])
+    e_ref = np.mean((x[:N, 1:K + 1] - preds[:, :K]) ** 2, axis=1)
+    e_glob = np.mean((x[:N, 1:K + 1] - base[:, :K]) ** 2, axis=1)
+    assert (e_ref <= e_glob * (1 + 1e-12)).all()
+    assert (status == 0).mean() > 0.9
+
+
+def test_plugin_insite_end_to_end(dev, model):
+    """+backbone=insite: fit, refined one-step predictions (tau = 1, the reference's get_predictions
+    default) and tau-step autoregressive predictions, against the oracle per row."""
+    from insite_amd import config as C
+    from insite_amd.sindy import SINDY
+    coll, x, u, arm, c0 = model
+    args = C.compose(["+backbone=insite", "+dataset=pkpd_sim", "dataset.equation_str=EQ_4_C",
+                      "model.dataset_name=EQ_4_C", "model.sindy_threshold=0.1", "model.sindy_alpha=0.5",
+                      "model.lam=10.0"])
+    m = SINDY(args, device=dev)
+    m.fit(coll["train"])
+    assert m.insite and np.abs(m.joint_coefs - c0).max() < 1e-8
+    m.joint_coefs = c0.copy()
+    ds = coll["test_cf_one_step"]
+    p = m.get_predictions(ds)
+    assert p.shape == ds.data["outputs"].shape and not np.isnan(p).any()
+    prev, stat = R.unscale_inputs(ds.data, ds.scaling_params)
+    arms = np.argmax(ds.data["current_treatments"], axis=-1)
+    sp = ds.scaling_params
+    got = p[..., 0] * sp["output_stds"] + sp["output_means"]
+    for i in range(0, prev.shape[0], 97):
+        rp, *_ = Q.refine_patient(prev[i], arms[i], stat[i], int(ds.data["sequence_lengths"][i]), c0, EX,
+                                  R.STANDARD_DT, 10.0, 1)
+        assert np.sqrt(np.mean((got[i] - rp) ** 2)) <= 1e-6
+    orig, allv, last = m.get_normalised_masked_rmse(ds, one_step_counterfactual=True)
+    assert np.isfinite([orig, allv, last]).all()
+    seq = coll["test_cf_treatment_seq"]
+    ar = m.get_autoregressive_predictions(seq)
+    assert ar.shape == (seq.data["outputs"].shape[0], m.projection_horizon, 1) and np.isfinite(ar).all()

@@ -46,9 +46,13 @@ def test_sindy_reads_config_and_rejects_unsupported_modes():
     assert (m.sindy_threshold, m.sindy_alpha, m.dt) == (0.1, 0.5, 10.0 / 60)
     assert m.feature_library_names == ["1", "x0", "u0", "u1", "x0 u0", "x0 u1", "u0 u1"]
     assert m.model_type == "sindy_regressor" and m.insite is False
-    for flag in ("insite", "wsindy", "joint_model", "ablation_more_complex_basis_functions"):
+    for flag in ("wsindy", "joint_model", "ablation_more_complex_basis_functions"):
         with pytest.raises(NotImplementedError):
             SINDY(_args(**{flag: True}), device="cpu")
+    ins = SINDY(_args(insite=True), device="cpu")   # the INSITE refinement (F2) is on the GPU path
+    assert ins.insite is True
+    with pytest.raises(RuntimeError):               # refined predictions before fit()
+        ins._predict_device(None)
     a = _args()
     a["model"]["dataset_name"] = "cancer_sim"
     with pytest.raises(NotImplementedError):
@@ -159,3 +163,13 @@ def test_pkpd_is_deterministic_per_seed():
     np.testing.assert_array_equal(a.train_f.data["outputs"], b.train_f.data["outputs"])
     c = pkpd.dataset_collection("EQ_4_D", {"train": 10, "val": 2, "test": 2}, seed=10, device="cpu")
     assert not np.array_equal(a.train_f.data["outputs"], c.train_f.data["outputs"])
+
+
+def test_savgol_rows_matches_scipy():
+    """smooth_input_data (INSITE path, sindy.py:557-560): scipy savgol_filter(5, 3, mode='interp')."""
+    import torch
+    from scipy.signal import savgol_filter
+    from insite_amd.sindy import savgol_5_3_rows
+    V = np.random.default_rng(0).normal(size=(7, 23))
+    got = savgol_5_3_rows(torch.tensor(V)).numpy()
+    assert np.allclose(got, savgol_filter(V, 5, 3, axis=1), rtol=1e-12, atol=1e-12)
