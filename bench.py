@@ -46,9 +46,9 @@ def parse():
     ap.add_argument("--arm-format", default="bits", choices=["bits", "int8"],
                     help="per-step arms of the time-major rollout: 1-bit mask (A <= 2) or int8")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", default="seq", choices=["graph", "seq", "pipeline"],
-                    help="graph: one step captured in a HIP graph and replayed; seq: eager launches on one "
-                         "stream; pipeline: discovery of step i+1 overlaps the rollout of step i (two streams)")
+    ap.add_argument("--mode", default="pipeline", choices=["graph", "seq", "pipeline"],
+                    help="pipeline: gram | [all-reduce +] STLSQ | rollout on three streams, consecutive steps "
+                         "overlapped (default); seq: eager launches on one stream; graph: the seq step in a HIP graph")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5", "insite"],
@@ -345,64 +345,77 @@ def main():
     lib = coh.lib
     F = lib.n_terms
     y0 = coh.y0
-    buf = idist.MomentBuffer(2, F, dev)          # G|b in one buffer: one all-reduce when N > 1
-    # coefficients double-buffered: discovery of step i+1 may run while the rollout of step i reads
+    # double-buffered per-step state: discovery of step i+1 may run while step i's STLSQ / rollout read
+    bufs = [idist.MomentBuffer(2, F, dev) for _ in range(2)]      # G|b in one buffer: one all-reduce
     coefs = [torch.empty((2, F), dtype=torch.float64, device=dev) for _ in range(2)]
-    mask = torch.empty((2, F), dtype=torch.int8, device=dev)
-    iters = torch.empty((2,), dtype=torch.int32, device=dev)
+    masks = [torch.empty((2, F), dtype=torch.int8, device=dev) for _ in range(2)]
+    iters = [torch.empty((2,), dtype=torch.int32, device=dev) for _ in range(2)]
+    mask = masks[0]
     y = torch.empty((T, N) if args.layout == "time" else (N, T), dtype=torch.float64, device=dev)
-    ws = ops.Workspace()
+    wss = [ops.Workspace(), ops.Workspace()]
     mode = args.mode if (world == 1 or args.mode != "graph") else "seq"   # RCCL stays outside graphs
-    s_disc = torch.cuda.current_stream(dev)
-    s_roll = torch.cuda.Stream(dev) if mode == "pipeline" else s_disc
+    s_g = torch.cuda.current_stream(dev)
+    s_c = torch.cuda.Stream(dev) if mode == "pipeline" else s_g
+    s_r = torch.cuda.Stream(dev) if mode == "pipeline" else s_g
 
-    # one step = discovery (Gram -> [all-reduce] -> STLSQ) then the rollout with that step's
-    # coefficients.  Launches go through prepared plans (arguments validated and packed once).
-    #   graph    : the step's launches captured once in a HIP graph, replayed K times (no host
-    #              launch gaps between the kernels; N = 1 only — the all-reduce stays eager)
-    #   seq      : the same launches issued eagerly on one stream
-    #   pipeline : discovery of step i+1 on one stream overlaps the rollout of step i on another
-    #              (double-buffered coefficients, event waits)
+    # one step = discovery (Gram -> [RCCL all-reduce when N > 1] -> STLSQ) then the rollout with that
+    # step's coefficients.  Launches go through prepared plans (arguments validated and packed once).
+    #   pipeline : three streams — gram + partial reduction | [all-reduce +] STLSQ | rollout — with
+    #              double-buffered G|b, workspaces and coefficients, ordered by events: the gram of
+    #              step i+1 streams while step i's STLSQ tail, all-reduce and rollout run, so the
+    #              small-grid tail kernels and the collective's latency leave the critical path
+    #   seq      : gram + fused reduction/STLSQ (N = 1) then the rollout, eagerly on one stream
+    #   graph    : the seq step captured once in a HIP graph and replayed (N = 1)
     # The timed region holds no timing events: per-kernel durations come from the separate
-    # roofline pass below (and rocprofv3), not from markers that stall the queue.
-    with torch.cuda.stream(s_disc):
-        if world == 1:   # Gram kernel + fused reduction/STLSQ (2 launches)
-            disc_plans = [ops.plan_sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, 100, True, 2,
-                                             "smoothed4", ws, out=(c, mask, iters, buf.G, buf.b), layout=args.layout)
-                          for c in coefs]
-        else:            # per-rank Gram -> one all-reduce of G|b -> replicated STLSQ
-            gram_plan = ops.plan_gram(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 2, "smoothed4", ws,
-                                      out=(buf.G, buf.b), layout=args.layout)
-            stlsq_plans = [ops.plan_stlsq(buf.G, buf.b, 0.1, 0.5, 100, True, out=(c, mask, iters)) for c in coefs]
-    roll_plans = [ops.plan_rollout(y0, coh.u, arm_cf, c, lib, coh.dt, method=args.method, T=T, out=y,
-                                   layout=roll_layout) for c in coefs]
-    done = [None, None]
-    sync_ev = [torch.cuda.Event() for _ in range(4)]   # cross-stream ordering only (no timing)
+    # roofline pass below (isolated launches) and rocprofv3.
+    with torch.cuda.stream(s_g):
+        fused = [ops.plan_sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, 100, True, 2,
+                                    "smoothed4", wss[j], out=(coefs[j], masks[j], iters[j], bufs[j].G, bufs[j].b),
+                                    layout=args.layout) for j in range(2)]
+        gram_plans = [ops.plan_gram(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 2, "smoothed4", wss[j],
+                                    out=(bufs[j].G, bufs[j].b), layout=args.layout) for j in range(2)]
+        stlsq_plans = [ops.plan_stlsq(bufs[j].G, bufs[j].b, 0.1, 0.5, 100, True, out=(coefs[j], masks[j], iters[j]))
+                       for j in range(2)]
+    roll_plans = [ops.plan_rollout(y0, coh.u, arm_cf, coefs[j], lib, coh.dt, method=args.method, T=T, out=y,
+                                   layout=roll_layout) for j in range(2)]
+    ev = {k: torch.cuda.Event() for k in [(n, j) for n in "gcr" for j in range(2)]}  # ordering only
+    last_c, last_r = [None, None], [None, None]
 
-    def discover(i, stream):
+    def discover(i, st):
+        """Discovery of step i on stream st (used by seq / graph and the roofline pass)."""
+        j = i % 2
         if world == 1:
-            disc_plans[i % 2](stream)
+            fused[j](st)
         else:
-            gram_plan(stream)
-            with torch.cuda.stream(stream):
-                idist.reduce_moments(buf)           # the only collective
-            stlsq_plans[i % 2](stream)
+            gram_plans[j](st)
+            with torch.cuda.stream(st):
+                idist.reduce_moments(bufs[j])       # the only collective
+            stlsq_plans[j](st)
 
     def step(i):
+        j = i % 2
         if mode != "pipeline":                      # current stream: the capture stream under graph capture
             st = torch.cuda.current_stream(dev)
             discover(i, st)
-            roll_plans[i % 2](st)
+            roll_plans[j](st)
             return
-        if done[i % 2] is not None:
-            s_disc.wait_event(done[i % 2])          # rollout i-2 finished reading this coef buffer
-        discover(i, s_disc)
-        e_disc, e_roll = sync_ev[2 * (i % 2)], sync_ev[2 * (i % 2) + 1]
-        e_disc.record(s_disc)
-        s_roll.wait_event(e_disc)
-        roll_plans[i % 2](s_roll)
-        e_roll.record(s_roll)
-        done[i % 2] = e_roll
+        if last_c[j] is not None:
+            s_g.wait_event(last_c[j])               # step i-2's STLSQ has read G|b[j]
+        gram_plans[j](s_g)
+        ev["g", j].record(s_g)
+        s_c.wait_event(ev["g", j])
+        if world > 1:
+            with torch.cuda.stream(s_c):
+                idist.reduce_moments(bufs[j])       # the only collective
+        if last_r[j] is not None:
+            s_c.wait_event(last_r[j])               # step i-2's rollout has read coefs[j]
+        stlsq_plans[j](s_c)
+        ev["c", j].record(s_c)
+        last_c[j] = ev["c", j]
+        s_r.wait_event(ev["c", j])
+        roll_plans[j](s_r)
+        ev["r", j].record(s_r)
+        last_r[j] = ev["r", j]
 
     graph = None
     if mode == "graph":
@@ -431,6 +444,7 @@ def main():
     el = idist.max_over_ranks(time.perf_counter() - t0, dev)
     ms_step = el / args.steps * 1e3
     coef = coefs[0] if mode == "graph" else coefs[(args.steps - 1) % 2]
+    mask = masks[0] if mode == "graph" else masks[(args.steps - 1) % 2]
 
     # roofline pass (outside the timed region): each phase's kernels launched back to back on one
     # stream between two HIP events; avg = elapsed / launches.  Same kernels, same inputs.
@@ -505,7 +519,8 @@ def main():
                            else "gram_kernel + RCCL all_reduce + stlsq_kernel",
                 "timed_region": {"graph": "one step (gram, finalize+STLSQ, rollout) captured in a HIP graph, replayed",
                                  "seq": "eager launches, one stream, strictly sequential",
-                                 "pipeline": "discovery and rollout on two streams, consecutive steps overlapped"}[mode],
+                                 "pipeline": "gram+reduce | [all-reduce+] STLSQ | rollout on three streams, "
+                                             "double-buffered, consecutive steps overlapped"}[mode],
                 "avg_ms_source": "roofline pass: back-to-back launches between two HIP events",
                 "avg_ms": disc_ms,
                 "algorithmic_bytes": gram_bytes(N, T),
