@@ -59,6 +59,39 @@ def parse():
     return ap.parse_args()
 
 
+class HipEvents:
+    """hipEventRecord / hipStreamWaitEvent on raw handles (the HIP runtime torch already loaded)."""
+
+    def __init__(self):
+        import ctypes
+        self._c = ctypes
+        self._hip = ctypes.CDLL("libamdhip64.so.7")
+        self._hip.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+        self._hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self._hip.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+        self._hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        self._events = []
+
+    def create(self):
+        e = self._c.c_void_p()
+        if self._hip.hipEventCreateWithFlags(self._c.byref(e), 0x2) != 0:   # hipEventDisableTiming
+            raise RuntimeError("hipEventCreateWithFlags failed")
+        self._events.append(e)
+        return e
+
+    def record(self, e, stream):
+        if self._hip.hipEventRecord(e, self._c.c_void_p(stream)) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def wait(self, stream, e):
+        if self._hip.hipStreamWaitEvent(self._c.c_void_p(stream), e, 0) != 0:
+            raise RuntimeError("hipStreamWaitEvent failed")
+
+    def __del__(self):
+        for e in getattr(self, "_events", []):
+            self._hip.hipEventDestroy(e)
+
+
 def rollout_bytes(N, T, U=2, w=8, arm_bits=8):
     """Algorithmic HBM bytes of one rollout launch:
     N*T*(S*w + arm_bits/8) [state out + per-step arm in: int8 = 8 bits, packed = 1 bit]
@@ -378,8 +411,15 @@ def main():
                        for j in range(2)]
     roll_plans = [ops.plan_rollout(y0, coh.u, arm_cf, coefs[j], lib, coh.dt, method=args.method, T=T, out=y,
                                    layout=roll_layout) for j in range(2)]
-    ev = {k: torch.cuda.Event() for k in [(n, j) for n in "gcr" for j in range(2)]}  # ordering only
+    # cross-stream ordering through the HIP runtime directly (torch's Event wrappers cost ~3-5 us of host
+    # time each; at N > 1 the host also issues the all-reduce, and must stay ahead of a ~70 us step)
+    hip = HipEvents()
+    ev = {k: hip.create() for k in [(n, j) for n in "gcr" for j in range(2)]}
+    hs = {"g": s_g.cuda_stream, "c": s_c.cuda_stream, "r": s_r.cuda_stream}
     last_c, last_r = [None, None], [None, None]
+    g_fast = [p.bind(s_g) for p in gram_plans]
+    c_fast = [p.bind(s_c) for p in stlsq_plans]
+    r_fast = [p.bind(s_r) for p in roll_plans]
 
     def discover(i, st):
         """Discovery of step i on stream st (used by seq / graph and the roofline pass)."""
@@ -400,21 +440,21 @@ def main():
             roll_plans[j](st)
             return
         if last_c[j] is not None:
-            s_g.wait_event(last_c[j])               # step i-2's STLSQ has read G|b[j]
-        gram_plans[j](s_g)
-        ev["g", j].record(s_g)
-        s_c.wait_event(ev["g", j])
+            hip.wait(hs["g"], last_c[j])            # step i-2's STLSQ has read G|b[j]
+        g_fast[j]()
+        hip.record(ev["g", j], hs["g"])
+        hip.wait(hs["c"], ev["g", j])
         if world > 1:
             with torch.cuda.stream(s_c):
                 idist.reduce_moments(bufs[j])       # the only collective
         if last_r[j] is not None:
-            s_c.wait_event(last_r[j])               # step i-2's rollout has read coefs[j]
-        stlsq_plans[j](s_c)
-        ev["c", j].record(s_c)
+            hip.wait(hs["c"], last_r[j])            # step i-2's rollout has read coefs[j]
+        c_fast[j]()
+        hip.record(ev["c", j], hs["c"])
         last_c[j] = ev["c", j]
-        s_r.wait_event(ev["c", j])
-        roll_plans[j](s_r)
-        ev["r", j].record(s_r)
+        hip.wait(hs["r"], ev["c", j])
+        r_fast[j]()
+        hip.record(ev["r", j], hs["r"])
         last_r[j] = ev["r", j]
 
     graph = None

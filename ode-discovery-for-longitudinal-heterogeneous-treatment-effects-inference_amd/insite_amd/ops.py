@@ -95,6 +95,16 @@ class Plan:
             _lib.check(self.fn_name, st)
         return self.out
 
+    def bind(self, stream: torch.cuda.Stream):
+        """A zero-argument launcher with the stream handle packed too (hot loops: one C call)."""
+        fn, args, name = self._fn, self._args + (ctypes.c_void_p(stream.cuda_stream),), self.fn_name
+
+        def launch():
+            st = fn(*args)
+            if st:
+                _lib.check(name, st)
+        return launch
+
 
 def _run(prep):
     name, args, dev, out = prep
