@@ -61,7 +61,8 @@ extern "C" {
 /* derivative estimators (pysindy differentiation methods used at sindy.py:190-203) */
 #define INSITE_FD_SMOOTHED4 0 /* SmoothedFiniteDifference(savgol 5/3, order=4); library on smoothed x */
 #define INSITE_FD_ORDER4 1    /* FiniteDifference(order=4) */
-#define INSITE_FD_ORDER1 2    /* FiniteDifference(order=1) */
+#define INSITE_FD_ORDER1 2    /* FiniteDifference(order=1): forward, backward at the last sample */
+#define INSITE_FD_SMOOTHED1 3 /* SmoothedFiniteDifference(savgol window 2, polyorder 1) + order 1 */
 
 /* integrators (odeint, pkpd/utils.py:68-94) */
 #define INSITE_METHOD_EULER 0 /* `substeps` forward-Euler steps per interval; 5 = reference Euler-5 */
@@ -124,6 +125,37 @@ int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, int32_t layout, int32
                              double threshold, double alpha, int32_t max_iter, int32_t unbias,
                              double* G_out, double* b_out, double* coef_out, int8_t* mask_out,
                              int32_t* iters_out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Treatment-segment discovery for the cancer_sim / EQ_5 datasets, replacing
+ * process_sindy_training_data's segment split (libs_m/ct/src/data/pkpd/utils.py:433-462, 607-637)
+ * and the four per-arm SINDy(FiniteDifference(order=1)).fit calls (libs_m/ct/src/models/sindy.py:
+ * 193-216).  For patient p with L = min(seq_len[p], n_steps - 1) the samples x(p, 0..L) are cut at
+ * every k in 1..L-1 where arm(p, k) != arm(p, k-1) into treatment-constant segments that share their
+ * boundary sample (each >= 2 samples); every segment s of arm a adds
+ *     G_out[a] += Theta_s^T Theta_s,   b_out[a] += Theta_s^T xdot_s
+ * with xdot from pysindy FiniteDifference(order=1) on the segment (forward differences, backward at
+ * its last sample; INSITE_FD_ORDER1) or SmoothedFiniteDifference(savgol window 2, polyorder 1)
+ * (INSITE_FD_SMOOTHED1: the library then sees the smoothed samples).  G_out[a][0][0] (bias column)
+ * is arm a's sample count; an arm with none has G = b = 0 (pysindy raises; the caller checks).
+ *   x        f64 element (p, k) at x[p * ldx + k] (PATIENT_MAJOR, ldx >= n_steps) or x[k * ldx + p]
+ *            (TIME_MAJOR, ldx >= n_patients), k < n_steps
+ *   arm      int8 in [0, n_arms), element (p, k), k < n_steps - 1, same layout, leading dim ld_arm
+ *   seq_len  [n_patients] int32;  u [n_patients, n_statics] f64 (statics, constant over time)
+ *   G_out [n_arms, F, F], b_out [n_arms, F] f64 (overwritten); deterministic (fixed-order sums).
+ * insite_sindy_fit_segments_f64 adds one STLSQ fit per arm in the finalisation launch
+ * (insite_sindy_fit_f64 semantics for coef_out / mask_out / iters_out). */
+size_t insite_gram_segments_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms);
+int32_t insite_gram_segments_f64(const double* x, int64_t ldx, const int8_t* arm, int64_t ld_arm, int32_t layout,
+                                 int32_t n_steps, const int32_t* seq_len, const double* u, int64_t n_patients,
+                                 int32_t n_statics, int32_t n_arms, const int8_t* exps, int32_t n_terms,
+                                 int32_t fd_kind, double dt, double* G_out, double* b_out, void* workspace,
+                                 size_t workspace_bytes, void* stream);
+int32_t insite_sindy_fit_segments_f64(const double* x, int64_t ldx, const int8_t* arm, int64_t ld_arm, int32_t layout,
+                                      int32_t n_steps, const int32_t* seq_len, const double* u, int64_t n_patients,
+                                      int32_t n_statics, int32_t n_arms, const int8_t* exps, int32_t n_terms,
+                                      int32_t fd_kind, double dt, double threshold, double alpha, int32_t max_iter,
+                                      int32_t unbias, double* G_out, double* b_out, double* coef_out, int8_t* mask_out,
+                                      int32_t* iters_out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Per-patient refit (reference LSQIntialMask, pkpd/utils.py:183-327,
  * as used by determine_individualized_equation_coefs, pkpd_simulation.py:791-800): for every patient

@@ -858,6 +858,165 @@ discovery_finalize(const double* __restrict__ partial, int nblk, int narm_pad, i
   }
 }
 
+// =============================================================================================
+// Treatment-segment discovery (cancer_sim / EQ_5)
+// =============================================================================================
+// Reference: process_sindy_training_data (pkpd/utils.py:433-462, 607-637) cuts a patient's samples
+// x[0..L] at every change of the per-step treatment into segments that share their boundary sample
+// (the last one ends at x[L]); the four per-arm SINDy fits (sindy.py:193-216) differentiate each
+// segment with FiniteDifference(order=1) — forward difference, backward at the segment's last
+// sample — or SmoothedFiniteDifference(savgol window 2, polyorder 1).  Streaming form, lane =
+// patient, one pass over the samples j < L of each lane:
+//   sample j (own segment, arm a_j): library input xo_j, derivative d_j = (xs_{j+1} - xo_j) / dt;
+//   if sample j+1 ends that segment (j+1 = L or a_{j+1} != a_j) it is added to the same arm as its
+//   last sample: input x_{j+1}, derivative d_j (the backward difference at a segment end equals the
+//   forward difference of the sample before it).
+// So per step the lane adds (n, sx, sxx, n d, d sx), n = 1 + end, to arm a_j: one select per arm.
+// Smoothed: inside a segment xs_i = (x_i + x_{i+1}) / 2 except at its first and last sample (raw).
+// Per 64-patient tile the per-(patient, arm) moments are contracted to Gram entries (one entry per
+// lane, patients staged through LDS in two halves); block partials in the gram_kernel scalar layout
+// feed discovery_finalize.
+constexpr int kSegKC = 8;       // steps per register chunk (loads issued ahead of the arithmetic)
+constexpr int kSegMono = INSITE_MAX_TERMS;
+constexpr int kSegRS = kSegMono + 5 * INSITE_MAX_ARMS;  // LDS row: F monomials | NARM x 5 moments (29, odd)
+
+template <int NARM, bool SMOOTH1>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))  // <= 128 VGPRs
+gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const int8_t* __restrict__ arm, int64_t asp,
+                int64_t ask, const int32_t* __restrict__ seq_len, int n_steps, const double* __restrict__ u, int64_t N,
+                double inv_dt, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ ticket) {
+  __shared__ double smem[kWavesPerBlock * 32 * kSegRS];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  double* ps = smem + wid * (32 * kSegRS);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0u;  // consumed by discovery_finalize (next launch)
+  double acc[NARM];
+#pragma unroll
+  for (int a = 0; a < NARM; ++a) acc[a] = 0.0;
+  const bool ent = lane < lib.nE;
+  const int my_i = ent ? lib.ei[lane] : 0;
+  const int my_k = ent ? lib.ek[lane] : -1;
+  const int moff = kSegMono + (my_k >= 0 ? lib.ex[my_i] + lib.ex[my_k] : 3 + lib.ex[my_i]);
+
+  const int64_t n_tiles = (N + kWave - 1) / kWave;
+  for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid; tile < n_tiles;
+       tile += (int64_t)gridDim.x * kWavesPerBlock) {
+    const int64_t p = tile * kWave + lane;
+    const bool valid = p < N;
+    int L = valid ? seq_len[p] : 0;
+    if (L > n_steps - 1) L = n_steps - 1;
+    if (L < 0) L = 0;
+    const int Lw = wave_max_i(L);
+    double mo[NARM][5];
+#pragma unroll
+    for (int a = 0; a < NARM; ++a)
+#pragma unroll
+      for (int j = 0; j < 5; ++j) mo[a][j] = 0.0;
+    const double* xp = x + (valid ? p * xsp : 0);
+    const int8_t* ap = arm + (valid ? p * asp : 0);
+    // samples k <= L and arms k < L of this lane; everything else reads as (0, -1)
+    // loads are issued unconditionally from a clamped (always valid) index and masked afterwards:
+    // exec-masked loads would make the compiler drain vmcnt at every chunk
+    auto ldx = [&](int k) {
+      const double v = xp[(int64_t)(k < L ? k : L) * xsk];
+      return k <= L ? v : 0.0;
+    };
+    auto lda = [&](int k) {
+      const int v = ap[(int64_t)(k < L ? k : (L > 0 ? L - 1 : 0)) * ask];
+      return k < L ? v : -1;
+    };
+    if (Lw > 0) {
+      double xj = ldx(0);
+      int aj = lda(0);
+      int aprev = -1;  // arm of sample j-1 (SMOOTH1: segment-start test)
+      for (int k0 = 0; k0 < Lw; k0 += kSegKC) {
+        constexpr int NX = kSegKC + (SMOOTH1 ? 1 : 0);
+        double xn[NX];
+        int an[kSegKC];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) xn[j] = ldx(k0 + 1 + j);
+#pragma unroll
+        for (int j = 0; j < kSegKC; ++j) an[j] = lda(k0 + 1 + j);
+#pragma unroll
+        for (int j = 0; j < kSegKC; ++j) {
+          const double x1 = xn[j];
+          const int a1 = an[j];
+          const bool endf = a1 != aj;  // sample j+1 closes j's segment (also at j+1 = L)
+          double xo, xs1;
+          if constexpr (SMOOTH1) {
+            const double x2 = xn[j + 1];
+            xo = (aj != aprev) ? xj : 0.5 * (xj + x1);
+            xs1 = endf ? x1 : 0.5 * (x1 + x2);
+          } else {
+            xo = xj;
+            xs1 = x1;
+          }
+          const double d = (xs1 - xo) * inv_dt;
+          const double xc = endf ? x1 : 0.0;
+          const double n = endf ? 2.0 : 1.0;
+          const double sx = xo + xc;
+          const double sxx = fma(xo, xo, xc * xc);
+          const double sd = d * n;
+          const double sdx = d * sx;
+#pragma unroll
+          for (int a = 0; a < NARM; ++a) {
+            const double w = (aj == a) ? 1.0 : 0.0;  // aj = -1 past the lane's own samples
+            mo[a][0] = fma(w, n, mo[a][0]);
+            mo[a][1] = fma(w, sx, mo[a][1]);
+            mo[a][2] = fma(w, sxx, mo[a][2]);
+            mo[a][3] = fma(w, sd, mo[a][3]);
+            mo[a][4] = fma(w, sdx, mo[a][4]);
+          }
+          aprev = aj;
+          aj = a1;
+          xj = x1;
+        }
+      }
+    }
+    // ---- per-(patient, arm) Gram blocks A(u) M_a A(u)^T, one entry per lane ----
+    double uu[INSITE_MAX_STATICS];
+#pragma unroll
+    for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = (valid && t < lib.U) ? u[p * lib.U + t] : 0.0;
+    for (int h = 0; h < 2; ++h) {
+      wave_lds_sync();
+      if ((lane >> 5) == h) {
+        double* row = ps + (lane & 31) * kSegRS;
+        for (int j = 0; j < lib.F; ++j) row[j] = valid ? monomial(lib, j, uu) : 0.0;
+#pragma unroll
+        for (int a = 0; a < NARM; ++a)
+#pragma unroll
+          for (int j = 0; j < 5; ++j) row[kSegMono + 5 * a + j] = mo[a][j];
+      }
+      wave_lds_sync();
+      if (ent) {
+#pragma unroll 2
+        for (int q = 0; q < 32; ++q) {
+          const double* row = ps + q * kSegRS;
+          const double wq = row[my_i] * (my_k >= 0 ? row[my_k] : 1.0);
+#pragma unroll
+          for (int a = 0; a < NARM; ++a) acc[a] = fma(wq, row[moff + 5 * a], acc[a]);
+        }
+      }
+    }
+    wave_lds_sync();
+  }
+  // ---- block reduction (fixed order) -> partial[block][arm][entry] (gram_kernel scalar layout) ----
+  __syncthreads();
+  double* red = smem;
+#pragma unroll
+  for (int a = 0; a < NARM; ++a) red[(wid * NARM + a) * kWave + lane] = acc[a];
+  __syncthreads();
+  if (wid == 0) {
+#pragma unroll
+    for (int a = 0; a < NARM; ++a) {
+      double s = red[(0 * NARM + a) * kWave + lane];
+#pragma unroll
+      for (int ww = 1; ww < kWavesPerBlock; ++ww) s += red[(ww * NARM + a) * kWave + lane];
+      partial[((int64_t)blockIdx.x * NARM + a) * kWave + lane] = s;
+    }
+  }
+}
+
 // Per-patient refit (LSQIntialMask per patient, pkpd_simulation.py:791-800):
 // thread = patient.  Its Gram G_p = A(u) M A(u)^T and moments b_p come from the five moments the
 // MOM pass wrote; STLSQ starts from the support of the global model of the patient's arm.  The
@@ -2296,6 +2455,100 @@ int32_t run_discovery(const double* x, int64_t ldx, int32_t layout, int32_t n_st
   return launch_status();
 }
 
+template <int NARM, bool SMOOTH1>
+int launch_gram_seg(hipStream_t st, const double* x, int64_t xsp, int64_t xsk, const int8_t* arm, int64_t asp,
+                    int64_t ask, const int32_t* seq_len, int n_steps, const double* u, int64_t N, double inv_dt,
+                    const LibDesc& lib, double* part, unsigned* ticket) {
+  auto kern = gram_seg_kernel<NARM, SMOOTH1>;
+  const int64_t tiles = (N + kWave - 1) / kWave;
+  int64_t g = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int64_t gres = resident_waves(kern) / kWavesPerBlock;
+  if (gres > 0 && g > gres) g = gres;
+  if (g > kGramMaxBlocks) g = kGramMaxBlocks;
+  if (g < 1) g = 1;
+  kern<<<dim3((unsigned)g), kBlock, 0, st>>>(x, xsp, xsk, arm, asp, ask, seq_len, n_steps, u, N, inv_dt, lib, part,
+                                             ticket);
+  return (int)g;
+}
+
+// segment-split Gram (+ fused finalize / STLSQ when sp.enabled): insite_gram_segments_f64 /
+// insite_sindy_fit_segments_f64
+int32_t run_segment_discovery(const double* x, int64_t ldx, const int8_t* arm, int64_t ld_arm, int32_t layout,
+                              int32_t n_steps, const int32_t* seq_len, const double* u, int64_t n_patients,
+                              int32_t n_statics, int32_t n_arms, const int8_t* exps, int32_t n_terms, int32_t fd_kind,
+                              double dt, double* G_out, double* b_out, void* workspace, size_t workspace_bytes,
+                              void* stream, const StlsqParams& sp, double* coef_out, int8_t* mask_out,
+                              int32_t* iters_out) {
+  const bool tm = layout == INSITE_LAYOUT_TIME_MAJOR;
+  if (layout != INSITE_LAYOUT_PATIENT_MAJOR && !tm) return INSITE_E_INVALID_ARG;
+  if (n_patients < 0 || !G_out || !b_out || n_arms < 1 || n_arms > INSITE_MAX_ARMS || !(dt > 0.0) || n_steps < 1 ||
+      ldx < 1 || ld_arm < 1)
+    return INSITE_E_INVALID_ARG;
+  if (tm ? (ldx < n_patients || ld_arm < n_patients) : (ldx < n_steps || ld_arm < n_steps - 1))
+    return INSITE_E_INVALID_ARG;
+  if (n_patients > 0 && (!x || !arm || !seq_len || (n_statics > 0 && !u))) return INSITE_E_INVALID_ARG;
+  if (fd_kind != INSITE_FD_ORDER1 && fd_kind != INSITE_FD_SMOOTHED1) return INSITE_E_UNSUPPORTED;
+  LibDesc lib;
+  int32_t st = build_lib(exps, n_terms, n_statics, &lib);
+  if (st != INSITE_OK) return st;
+  if (!workspace || workspace_bytes < insite_gram_workspace_bytes(n_patients, n_arms, n_terms))
+    return INSITE_E_WORKSPACE;
+  lib.mfma = 0;
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  const int na = narm_pad(n_arms);
+  unsigned* ticket = static_cast<unsigned*>(workspace);
+  double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + kGramWsHeader);
+  if (n_statics == 0) u = x;
+  if (n_patients == 0) {  // G = b = 0 (and the fit of an all-zero system) through the same finalize
+    x = G_out;
+    arm = reinterpret_cast<const int8_t*>(G_out);
+    seq_len = reinterpret_cast<const int32_t*>(G_out);
+    u = G_out;
+  }
+  const int64_t xsp = tm ? 1 : ldx, xsk = tm ? ldx : 1;
+  const int64_t asp = tm ? 1 : ld_arm, ask = tm ? ld_arm : 1;
+  const double inv_dt = 1.0 / dt;
+  const bool sm = fd_kind == INSITE_FD_SMOOTHED1;
+  int grid;
+#define INSITE_SEG_LAUNCH(NA)                                                                                    \
+  grid = sm ? launch_gram_seg<NA, true>(hs, x, xsp, xsk, arm, asp, ask, seq_len, n_steps, u, n_patients, inv_dt, \
+                                        lib, part, ticket)                                                       \
+            : launch_gram_seg<NA, false>(hs, x, xsp, xsk, arm, asp, ask, seq_len, n_steps, u, n_patients, inv_dt, \
+                                         lib, part, ticket)
+  if (na == 1) INSITE_SEG_LAUNCH(1);
+  else if (na == 2) INSITE_SEG_LAUNCH(2);
+  else INSITE_SEG_LAUNCH(4);
+#undef INSITE_SEG_LAUNCH
+  st = launch_status();
+  if (st != INSITE_OK) return st;
+  const dim3 fg(n_arms * lib.nE);
+  if (!sp.enabled) {
+    discovery_finalize<0><<<fg, kBlock, 0, hs>>>(part, grid, na, n_arms, lib, G_out, b_out, sp, nullptr, nullptr,
+                                                 nullptr, ticket);
+    return launch_status();
+  }
+  switch (n_terms) {
+#define INSITE_FIN_CASE(FF)                                                                                    \
+  case FF:                                                                                                     \
+    discovery_finalize<FF><<<fg, kBlock, 0, hs>>>(part, grid, na, n_arms, lib, G_out, b_out, sp, coef_out,     \
+                                                  mask_out, iters_out, ticket);                                \
+    break;
+    INSITE_FIN_CASE(1)
+    INSITE_FIN_CASE(2)
+    INSITE_FIN_CASE(3)
+    INSITE_FIN_CASE(4)
+    INSITE_FIN_CASE(5)
+    INSITE_FIN_CASE(6)
+    INSITE_FIN_CASE(7)
+    INSITE_FIN_CASE(8)
+    INSITE_FIN_CASE(9)
+#undef INSITE_FIN_CASE
+    default:
+      return INSITE_E_UNSUPPORTED;
+  }
+  return launch_status();
+}
+
 template <int METHOD, int NARM, bool PERROW>
 void launch_rollout_a(int av, bool yv2, dim3 grid, hipStream_t st, const RolloutArgs& ra, const LibDesc& lib) {
   if (yv2) {
@@ -2454,6 +2707,34 @@ int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, int32_t layout, int32
   StlsqParams sp{threshold, alpha, max_iter, unbias, 1};
   return run_discovery(x, ldx, layout, n_steps, u, arm, rows, n_patients, n_statics, n_arms, exps, n_terms, fd_kind,
                        dt, G_out, b_out, workspace, workspace_bytes, stream, sp, coef_out, mask_out, iters_out);
+}
+
+size_t insite_gram_segments_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms) {
+  return insite_gram_workspace_bytes(n_patients, n_arms, n_terms);
+}
+
+int32_t insite_gram_segments_f64(const double* x, int64_t ldx, const int8_t* arm, int64_t ld_arm, int32_t layout,
+                                 int32_t n_steps, const int32_t* seq_len, const double* u, int64_t n_patients,
+                                 int32_t n_statics, int32_t n_arms, const int8_t* exps, int32_t n_terms,
+                                 int32_t fd_kind, double dt, double* G_out, double* b_out, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
+  StlsqParams sp{0.0, 0.0, 0, 0, 0};
+  return run_segment_discovery(x, ldx, arm, ld_arm, layout, n_steps, seq_len, u, n_patients, n_statics, n_arms, exps,
+                               n_terms, fd_kind, dt, G_out, b_out, workspace, workspace_bytes, stream, sp, nullptr,
+                               nullptr, nullptr);
+}
+
+int32_t insite_sindy_fit_segments_f64(const double* x, int64_t ldx, const int8_t* arm, int64_t ld_arm, int32_t layout,
+                                      int32_t n_steps, const int32_t* seq_len, const double* u, int64_t n_patients,
+                                      int32_t n_statics, int32_t n_arms, const int8_t* exps, int32_t n_terms,
+                                      int32_t fd_kind, double dt, double threshold, double alpha, int32_t max_iter,
+                                      int32_t unbias, double* G_out, double* b_out, double* coef_out, int8_t* mask_out,
+                                      int32_t* iters_out, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!coef_out || max_iter < 0 || !(threshold >= 0.0) || !(alpha >= 0.0)) return INSITE_E_INVALID_ARG;
+  StlsqParams sp{threshold, alpha, max_iter, unbias, 1};
+  return run_segment_discovery(x, ldx, arm, ld_arm, layout, n_steps, seq_len, u, n_patients, n_statics, n_arms, exps,
+                               n_terms, fd_kind, dt, G_out, b_out, workspace, workspace_bytes, stream, sp, coef_out,
+                               mask_out, iters_out);
 }
 
 size_t insite_per_patient_workspace_bytes(int64_t n_patients) {

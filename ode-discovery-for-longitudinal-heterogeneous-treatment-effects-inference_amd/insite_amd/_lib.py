@@ -24,7 +24,7 @@ ABI_VERSION = 1
 
 # status codes / enums (insite_hip.h)
 INSITE_OK = 0
-FD_SMOOTHED4, FD_ORDER4, FD_ORDER1 = 0, 1, 2
+FD_SMOOTHED4, FD_ORDER4, FD_ORDER1, FD_SMOOTHED1 = 0, 1, 2, 3
 METHOD_EULER, METHOD_RK4 = 0, 1
 LAYOUT_PATIENT_MAJOR, LAYOUT_TIME_MAJOR, LAYOUT_TIME_MAJOR_BITS = 0, 1, 2
 MAX_TERMS, MAX_STATICS, MAX_ARMS, MAX_STATE_DEGREE = 9, 3, 4, 1
@@ -36,6 +36,9 @@ EXPORTS = (
     "insite_gram_workspace_bytes",
     "insite_gram_f64",
     "insite_sindy_fit_f64",
+    "insite_gram_segments_workspace_bytes",
+    "insite_gram_segments_f64",
+    "insite_sindy_fit_segments_f64",
     "insite_per_patient_workspace_bytes",
     "insite_sindy_fit_per_patient_f64",
     "insite_stlsq_f64",
@@ -77,6 +80,12 @@ _SIGNATURES = {
                                       _c_i32, _c_i32,
                                       _c_f64, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _c_size,
                                       _vp]),
+    "insite_gram_segments_workspace_bytes": (_c_size, [_c_i64, _c_i32, _c_i32]),
+    "insite_gram_segments_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i64, _c_i32, _c_i32,
+                                          _vp, _c_i32, _c_i32, _c_f64, _vp, _vp, _vp, _c_size, _vp]),
+    "insite_sindy_fit_segments_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i64, _c_i32,
+                                               _c_i32, _vp, _c_i32, _c_i32, _c_f64, _c_f64, _c_f64, _c_i32, _c_i32,
+                                               _vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
     "insite_per_patient_workspace_bytes": (_c_size, [_c_i64]),
     "insite_sindy_fit_per_patient_f64": (_c_i32, [_vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32,
                                                   _vp, _c_i32, _c_i32, _c_f64, _vp, _c_f64, _c_f64, _c_i32, _c_i32,

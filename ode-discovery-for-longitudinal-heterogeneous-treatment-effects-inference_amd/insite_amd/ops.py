@@ -227,6 +227,92 @@ def sindy_fit_per_patient(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, r
     return _run(("insite_sindy_fit_per_patient_f64", args, dev, out))
 
 
+SEGMENT_FD_KINDS = {"order1": _lib.FD_ORDER1, "smoothed1": _lib.FD_SMOOTHED1}
+
+
+def _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layout, stlsq_args=None):
+    """Validate the F4 (treatment-segment) discovery inputs and pack the C arguments."""
+    if layout not in LAYOUTS:
+        raise ValueError(f"layout must be one of {sorted(LAYOUTS)}")
+    if fd not in SEGMENT_FD_KINDS:
+        raise ValueError(f"fd must be one of {sorted(SEGMENT_FD_KINDS)}")
+    _dev("x", x, torch.float64, 2)
+    _dev("arm", arm, torch.int8, 2)
+    _dev("seq_len", seq_len, torch.int32, 1)
+    if not 1 <= n_arms <= _lib.MAX_ARMS:
+        raise ValueError(f"n_arms must be in [1, {_lib.MAX_ARMS}]")
+    N = seq_len.numel()
+    if layout == "time":
+        n_steps = x.size(0)
+        if x.size(1) < N or arm.size(1) < N or arm.size(0) < n_steps - 1:
+            raise ValueError("time-major x must be [n_steps, >=N] and arm [>=n_steps-1, >=N]")
+    else:
+        n_steps = x.size(1)
+        if x.size(0) != N or arm.size(0) != N or arm.size(1) < n_steps - 1:
+            raise ValueError("patient-major x must be [N, n_steps] and arm [N, >=n_steps-1]")
+    if n_steps < 1:
+        raise ValueError("need at least one stored sample")
+    if lib.n_statics:
+        _dev("u", u, torch.float64, 2)
+        if u.size(0) != N or u.size(1) != lib.n_statics or u.stride(0) != lib.n_statics:
+            raise ValueError("u must be a contiguous [N, n_statics] tensor")
+    L = _lib.load()
+    F = lib.n_terms
+    dev = x.device
+    ws = (workspace or _WS).get(L.insite_gram_segments_workspace_bytes(N, n_arms, F), dev)
+    tab = lib.ctypes_table()
+    head = (_p(x), x.stride(0), _p(arm), arm.stride(0), LAYOUTS[layout], n_steps, _p(seq_len),
+            _p(u) if lib.n_statics else ctypes.c_void_p(0), N, lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p),
+            F, SEGMENT_FD_KINDS[fd], float(dt))
+    if stlsq_args is None:
+        if out is None:
+            out = (torch.empty((n_arms, F, F), dtype=torch.float64, device=dev),
+                   torch.empty((n_arms, F), dtype=torch.float64, device=dev))
+        G, b = out
+        return "insite_gram_segments_f64", head + (_p(G), _p(b), _p(ws), ws.numel()), dev, out
+    threshold, alpha, max_iter, unbias = stlsq_args
+    if out is None:
+        out = (torch.empty((n_arms, F), dtype=torch.float64, device=dev),
+               torch.empty((n_arms, F), dtype=torch.int8, device=dev),
+               torch.empty((n_arms,), dtype=torch.int32, device=dev),
+               torch.empty((n_arms, F, F), dtype=torch.float64, device=dev),
+               torch.empty((n_arms, F), dtype=torch.float64, device=dev))
+    coef, mask, iters, G, b = out
+    args = head + (float(threshold), float(alpha), int(max_iter), int(bool(unbias)), _p(G), _p(b), _p(coef), _p(mask),
+                   _p(iters), _p(ws), ws.numel())
+    return "insite_sindy_fit_segments_f64", args, dev, out
+
+
+def gram_segments(x: torch.Tensor, arm: torch.Tensor, seq_len: torch.Tensor, u: torch.Tensor, dt: float,
+                  lib: PolyLibrary, n_arms: int = 4, fd: str = "order1", workspace: Workspace | None = None,
+                  out: tuple | None = None, layout: str = "patient"):
+    """Per-arm Gram of the treatment-segment regression (insite_gram_segments_f64; reference
+    process_sindy_training_data, pkpd/utils.py:433-462).  layout "patient": x [N, T], arm [N, >=T-1]
+    (the reference's arrays, arm = argmax of the one-hot); "time": x [T, >=N], arm [>=T-1, >=N].
+    Returns (G[A,F,F], b[A,F]); G[a,0,0] is arm a's sample count."""
+    return _run(_prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layout))
+
+
+def sindy_fit_segments(x: torch.Tensor, arm: torch.Tensor, seq_len: torch.Tensor, u: torch.Tensor, dt: float,
+                       lib: PolyLibrary, threshold: float, alpha: float, max_iter: int = 100, unbias: bool = True,
+                       n_arms: int = 4, fd: str = "order1", workspace: Workspace | None = None,
+                       out: tuple | None = None, layout: str = "patient"):
+    """cancer_sim / EQ_5 discovery in two launches (insite_sindy_fit_segments_f64): the segment-split
+    Gram kernel, then the fixed-order reduction fused with one STLSQ per arm — replaces the four
+    ``SINDy(FiniteDifference(order=1)).fit`` calls (reference sindy.py:193-216).
+    Returns (coef[A,F], mask[A,F], iters[A], G[A,F,F], b[A,F])."""
+    return _run(_prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layout,
+                               (threshold, alpha, max_iter, unbias)))
+
+
+def plan_sindy_fit_segments(x, arm, seq_len, u, dt, lib, threshold, alpha, max_iter=100, unbias=True, n_arms=4,
+                            fd="order1", workspace=None, out=None, layout="patient") -> Plan:
+    """``sindy_fit_segments`` as a prepared launch; ``plan.out`` = (coef, mask, iters, G, b)."""
+    name, args, dev, out = _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layout,
+                                          (threshold, alpha, max_iter, unbias))
+    return Plan(name, args, dev, out)
+
+
 def _prep_stlsq(G, b, threshold, alpha, max_iter, unbias, out):
     _dev("G", G, torch.float64)
     _dev("b", b, torch.float64)

@@ -20,7 +20,8 @@ The DE-format extraction (A1, pkpd/utils.py:523-606), the tau-step slice (A9) an
 squared-error sums of the metrics (A10) also run on the device; only scalars and the returned
 prediction arrays cross back to the host.  Out of scope in this build (raise
 ``NotImplementedError``): weak SINDy, the joint model, the degree-4 ablation library and the
-cancer_sim / EQ_5 datasets.
+``insite: true`` on the 4-arm datasets.  The cancer_sim / EQ_5 datasets run the
+treatment-segment discovery (``insite_sindy_fit_segments_f64``) and the 4-arm rollout.
 """
 from __future__ import annotations
 
@@ -132,6 +133,9 @@ class SINDY:
         self.wsindy = bool(m("wsindy", False))
         self.use_smoothed_finite_difference = bool(m("use_smoothed_finite_difference", False))
         self.dataset_name = str(m("dataset_name", ""))
+        # cancer_sim / EQ_5: treatment-segment split, FiniteDifference(order=1), one fit per arm of
+        # the 4-valued treatment (sindy.py:160-183, 193-216, 289-312)
+        self.segment_mode = "EQ_5" in self.dataset_name.upper() or "CANCER_SIM" in self.dataset_name.upper()
         self.ablation_more_complex_basis_functions = bool(m("ablation_more_complex_basis_functions", False))
         self.insight_recover_parametric_dist = bool(m("insight_recover_parametric_dist", False))
         self.treatment_mode = _get(args, "dataset.treatment_mode", "multiclass")
@@ -149,9 +153,12 @@ class SINDY:
 
     # ------------------------------------------------------------------ configuration checks
     def _check_supported(self):
-        if "EQ_4" not in self.dataset_name.upper():
-            raise NotImplementedError(f"dataset {self.dataset_name!r}: this build covers the PK/PD EQ_4 family "
-                                      "(cancer_sim / EQ_5 are SURVEY.md §8 F4)")
+        if not (self.segment_mode or "EQ_4" in self.dataset_name.upper()):
+            raise NotImplementedError(f"dataset {self.dataset_name!r}: this build covers the PK/PD EQ_4 family and "
+                                      "the treatment-segment datasets (cancer_sim, EQ_5_*)")
+        if self.segment_mode and self.insite:
+            raise NotImplementedError("insite: true on the 4-arm cancer_sim / EQ_5 datasets (the refinement kernel "
+                                      "takes bit-packed arms, n_arms <= 2)")
         if self.wsindy:
             raise NotImplementedError("weak SINDy (wsindy: true) is not on the MI355X path")
         if self.joint_model:
@@ -196,10 +203,39 @@ class SINDY:
                 - sequence_lengths_offset).to(torch.int32)
         return x, stat, arm, rows
 
+    def de_format_segments(self, dataset):
+        """Device arrays of the cancer_sim / EQ_5 branch of ``process_dataset_into_de_format``
+        (pkpd/utils.py:607-637, sequence_lengths_offset = 0): the reconstructed series x[N, T], statics
+        u[N, U], the per-step arm argmax(current_treatments) [N, T-1] (utils.py:624) and seq_len[N].
+        The treatment-constant segments themselves are cut inside the Gram kernel."""
+        d = dataset.data
+        prev, stat, _, _ = self._unscaled_inputs(dataset)
+        uo = torch.as_tensor(np.ascontiguousarray(d["unscaled_outputs"][..., 0]), device=self.device)
+        x = torch.cat([prev[:, :1], uo], dim=1).contiguous()
+        arm = torch.as_tensor(np.argmax(d["current_treatments"], axis=-1).astype(np.int8), device=self.device)
+        sl = torch.as_tensor(np.asarray(d["sequence_lengths"]).astype(np.int32), device=self.device)
+        return x, stat, arm.contiguous(), sl
+
+    def _fit_segments(self, train_f):
+        """cancer_sim / EQ_5 discovery (sindy.py:160-216): segment split + FD order 1 (or the
+        savgol(2, 1)-smoothed variant) + library + per-arm Gram in one kernel, STLSQ per arm fused into
+        the reduction launch (insite_sindy_fit_segments_f64)."""
+        x, u, arm, sl = self.de_format_segments(train_f)
+        fd = "smoothed1" if self.use_smoothed_finite_difference else "order1"
+        return ops.sindy_fit_segments(x, arm, sl, u, self.dt, self.library, self.sindy_threshold, self.sindy_alpha,
+                                      max_iter=100, unbias=True, n_arms=self.dim_treatments, fd=fd)
+
     # ------------------------------------------------------------------ discovery
     def fit(self, train_f, val_f=None):
         """Global discovery per arm (sindy.py:145-336): one Gram pass + STLSQ on the GPU."""
         self.prepare_data()
+        if self.segment_mode:
+            coef, mask, iters, G, _ = self._fit_segments(train_f)
+            empty = np.nonzero(G[:, 0, 0].cpu().numpy() == 0)[0]
+            if empty.size:
+                raise ValueError(f"treatment arm(s) {empty.tolist()} have no training segments "
+                                 "(pysindy cannot fit an empty trajectory list)")
+            return self._finish_fit(coef, mask, iters)
         x, u, arm, rows = self.de_format(train_f)
         if int(rows.min().item()) < 5:
             raise ValueError("a training trajectory has fewer than 5 rows: the savgol(5, 3) smoother "
@@ -207,6 +243,9 @@ class SINDY:
         coef, mask, iters, _, _ = ops.sindy_fit(x, u, arm, rows, self.dt, self.library, self.sindy_threshold,
                                                 self.sindy_alpha, max_iter=100, unbias=True,
                                                 n_arms=self.dim_treatments, fd="smoothed4")
+        return self._finish_fit(coef, mask, iters)
+
+    def _finish_fit(self, coef, mask, iters):
         iters_h = iters.cpu().numpy()
         if np.any(iters_h < 0):
             raise np.linalg.LinAlgError("STLSQ ridge system is not positive definite")

@@ -33,7 +33,7 @@ def _header_functions():
 def test_header_declares_the_abi():
     fns = _header_functions()
     assert "insite_rollout_f64" in fns and "insite_sindy_fit_f64" in fns
-    assert len(fns) == 18
+    assert len(fns) == 21
 
 
 def test_library_exports_every_header_symbol(L):
@@ -72,8 +72,8 @@ def test_header_constants_match_bindings():
         return int(re.search(rf"#define {name} \(?(-?\d+)\)?", src).group(1))
 
     assert const("INSITE_OK") == _lib.INSITE_OK
-    assert (const("INSITE_FD_SMOOTHED4"), const("INSITE_FD_ORDER4"), const("INSITE_FD_ORDER1")) == \
-        (_lib.FD_SMOOTHED4, _lib.FD_ORDER4, _lib.FD_ORDER1)
+    assert (const("INSITE_FD_SMOOTHED4"), const("INSITE_FD_ORDER4"), const("INSITE_FD_ORDER1"),
+            const("INSITE_FD_SMOOTHED1")) == (_lib.FD_SMOOTHED4, _lib.FD_ORDER4, _lib.FD_ORDER1, _lib.FD_SMOOTHED1)
     assert (const("INSITE_METHOD_EULER"), const("INSITE_METHOD_RK4")) == (_lib.METHOD_EULER, _lib.METHOD_RK4)
     assert (const("INSITE_LAYOUT_PATIENT_MAJOR"), const("INSITE_LAYOUT_TIME_MAJOR"),
             const("INSITE_LAYOUT_TIME_MAJOR_BITS")) == \
@@ -159,6 +159,19 @@ def test_invalid_arguments_rejected_without_device(L):
     e2[1, 0] = 2
     assert L.insite_gram_f64(x, 60, 0, 60, x, x, x, 10, 2, 2, e2.ctypes.data_as(ctypes.c_void_p), 7, 0, 0.1, g, bb,
                              nul, 0, nul) == -2
+    # treatment-segment discovery (F4): FD kinds of the cancer_sim / EQ_5 path only; arm leading dim;
+    # short workspace; the fit validates its STLSQ arguments first
+    o1, s1 = _lib.FD_ORDER1, _lib.FD_SMOOTHED1
+    seg = L.insite_gram_segments_f64
+    assert seg(x, 60, x, 59, 0, 60, x, x, 10, 2, 4, ep, 7, 0, 0.1, g, bb, nul, 0, nul) == -2        # smoothed4
+    assert seg(x, 60, x, 58, 0, 60, x, x, 10, 2, 4, ep, 7, o1, 0.1, g, bb, nul, 0, nul) == -1       # ld_arm < T-1
+    assert seg(x, 60, x, 59, 3, 60, x, x, 10, 2, 4, ep, 7, o1, 0.1, g, bb, nul, 0, nul) == -1       # layout
+    assert seg(x, 9, x, 10, 1, 60, x, x, 10, 2, 4, ep, 7, o1, 0.1, g, bb, nul, 0, nul) == -1        # TM ldx < N
+    assert seg(x, 60, x, 59, 0, 60, x, x, 10, 2, 5, ep, 7, s1, 0.1, g, bb, nul, 0, nul) == -1       # 5 arms
+    assert seg(x, 60, x, 59, 0, 60, x, x, 10, 2, 4, ep, 7, s1, 0.1, g, bb, nul, 0, nul) == -3       # workspace
+    assert L.insite_sindy_fit_segments_f64(x, 60, x, 59, 0, 60, x, x, 10, 2, 4, ep, 7, o1, 0.1, -1.0, 0.5, 100, 1,
+                                           g, bb, g, nul, nul, nul, 0, nul) == -1
+    assert L.insite_gram_segments_workspace_bytes(1000, 4, 7) == L.insite_gram_workspace_bytes(1000, 4, 7) > 0
 
 
 def test_ops_refuse_host_tensors(L):

@@ -53,8 +53,15 @@ def test_sindy_reads_config_and_rejects_unsupported_modes():
     assert ins.insite is True
     with pytest.raises(RuntimeError):               # refined predictions before fit()
         ins._predict_device(None)
-    a = _args()
+    a = _args(dim_treatments=4, dim_static_features=1)
     a["model"]["dataset_name"] = "cancer_sim"
+    seg = SINDY(a, device="cpu")                 # F4: the treatment-segment path
+    assert seg.segment_mode and seg.feature_library_names == ["1", "x0", "u0", "x0 u0"]
+    a["model"]["insite"] = True
+    with pytest.raises(NotImplementedError):     # INSITE refinement takes <= 2 arms
+        SINDY(a, device="cpu")
+    a = _args()
+    a["model"]["dataset_name"] = "mimic3"
     with pytest.raises(NotImplementedError):
         SINDY(a, device="cpu")
     with pytest.raises(ValueError):
