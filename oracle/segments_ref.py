@@ -250,7 +250,7 @@ def synthetic_cohort(n, T, rng, switch_p=0.1, noise=0.0, dt=0.1, coef=TRUE_COEF_
     arms[:, 0] = rng.integers(0, A, size=n)
     for k in range(1, T):
         sw = rng.random(n) < switch_p
-        other = (arms[:, k - 1] + rng.integers(1, A, size=n)) % A
+        other = (arms[:, k - 1] + rng.integers(1, A, size=n)) % A if A > 1 else arms[:, k - 1]
         arms[:, k] = np.where(sw, other, arms[:, k - 1])
     x = np.empty((n, T + 1))
     x[:, 0] = y
