@@ -51,7 +51,7 @@ def parse():
                          "overlapped (default); seq: eager launches on one stream; graph: the seq step in a HIP graph")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5", "insite"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5", "insite", "f4"],
                     help="c2: BASELINE configs[1], the headline line (default); c3: configs[2], the 5-state fp32 "
                          "system (parity-test configuration, measured separately)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
@@ -348,8 +348,109 @@ def insite_main(args):
     print(json.dumps(out))
 
 
+# planted per-arm model of the F4 cohort over [1, x0, u0, x0 u0]: no treatment / chemo / radio / both
+F4_COEF = [[0.0, 0.20, 0.0, 0.0], [0.0, 0.0, 0.0, -0.60], [0.0, -0.30, 0.0, 0.0], [0.0, -0.25, 0.0, -0.90]]
+
+
+def f4_main(args):
+    """Treatment-segment path of the cancer_sim / EQ_5 datasets (reference
+    pkpd/utils.py:433-462, 607-637, sindy.py:193-216, 289-312): 1M patients x 60 steps, 4 arms, one
+    static.  One step = discovery (segment split + FD order 1 + library + per-arm Gram in one kernel,
+    fixed-order reduction fused with the four STLSQ fits) + Euler-5 (the reference odeint) 4-arm
+    counterfactual rollout under fresh per-step arms."""
+    from insite_amd import ops, cohort
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    N = args.patients if args.patients != 100_000 else 1_000_000
+    T = args.T if args.T != 200 else 60
+    coh = cohort.synthetic_segments(N, T, seed=args.seed + 31, device=dev, coef=F4_COEF, dt=0.1)
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed + 32)
+    arm_cf = cohort.markov_arms(N, T, 4, 0.1, g, dev)
+    lib, F = coh.lib, coh.lib.n_terms
+    out = (torch.empty((4, F), dtype=torch.float64, device=dev), torch.empty((4, F), dtype=torch.int8, device=dev),
+           torch.empty((4,), dtype=torch.int32, device=dev), torch.empty((4, F, F), dtype=torch.float64, device=dev),
+           torch.empty((4, F), dtype=torch.float64, device=dev))
+    y = torch.empty((T, N), dtype=torch.float64, device=dev)
+    y0 = coh.x[0].contiguous()
+    ws = ops.Workspace()
+    fit = ops.plan_sindy_fit_segments(coh.x, coh.arm, coh.seq_len, coh.u, coh.dt, lib, 0.001, 0.5, workspace=ws,
+                                      out=out, layout="time")
+    roll = ops.plan_rollout(y0, coh.u, arm_cf, out[0], lib, coh.dt, method="euler5", T=T, out=y, layout="time")
+    gram = ops.plan_gram_segments(coh.x, coh.arm, coh.seq_len, coh.u, coh.dt, lib, 4, "order1", ws,
+                                  out=(out[3], out[4]), layout="time")
+
+    def step(st):
+        fit(st)
+        roll(st)
+
+    st = torch.cuda.current_stream(dev)
+    for _ in range(args.warmup):
+        step(st)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(st)
+    torch.cuda.synchronize(dev)
+    ms_step = (time.perf_counter() - t0) / args.steps * 1e3
+
+    def timed(fn, n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(n):
+            fn(st)
+        e1.record(st)
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / n
+
+    n_roof = max(args.steps, 10)
+    gram_ms = timed(gram, n_roof)
+    roll_ms = timed(roll, n_roof)
+    gb = N * (T + 1) * 8 + N * T + N * (8 * lib.n_statics + 4)          # x samples + arms + (u, seq_len)
+    rb = rollout_bytes(N, T, U=lib.n_statics)
+    achieved = gb / (gram_ms * 1e-3) / 1e9
+    res = {
+        "metric": METRIC, "value": N / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: on-device 4-arm cohort (planted per-arm model, Markov arms p=0.1, Euler-5 truth + 0.01 noise)",
+        "config": {"workload": f"F4: cancer_sim/EQ_5 path, {N // 1000}k patients x {T} steps, 4 arms: segment-split "
+                               f"FD1 discovery + STLSQ (threshold 0.001) + Euler-5 4-arm counterfactual rollout",
+                   "patients": N, "T": T, "arms": 4, "library_terms": F,
+                   "discovered_support": (out[1].cpu().numpy() != 0).astype(int).tolist()},
+        "roofline": {"kernel": "gram_seg_kernel (order1, 4 arms) + discovery_finalize<0>", "bound": "hbm",
+                     "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
+                     "traffic": None, "algorithmic_bytes_per_launch": gb, "avg_launch_ms": gram_ms},
+        "rollout": {"kernel": "rollout_tm_kernel (euler5, 4 arms, int8 arms)", "avg_launch_ms": roll_ms,
+                    "algorithmic_bytes": rb, "achieved_GBps": rb / (roll_ms * 1e-3) / 1e9,
+                    "frac": rb / (roll_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS},
+    }
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        from oracle import insite_ref as R
+        from oracle import segments_ref as S
+        n_s = min(10 * args.cpu_sample, N)         # ~10 s of one host core at the default sizes
+        xs = coh.x[:, :n_s].T.contiguous().cpu().numpy()
+        us = coh.u[:n_s].cpu().numpy()
+        a_f = coh.arm[:, :n_s].T.cpu().numpy().astype(np.int64)
+        a_c = arm_cf[:, :n_s].T.cpu().numpy().astype(np.int64)
+        sl = np.full(n_s, T, dtype=np.int64)
+        ex = lib.exps.astype(np.int64)
+        t1 = time.perf_counter()
+        G, b = S.gram_segments_vectorized(xs, us, a_f, sl, coh.dt, ex)
+        c = np.stack([R.stlsq_gram(G[k], b[k], 0.001, 0.5)[0] for k in range(4)])
+        R.rollout(xs[:, 0], us, a_c, c, ex, coh.dt, method="euler5")
+        el = time.perf_counter() - t1
+        res["cpu_baseline"] = {"value": n_s / el, "unit": "patient-trajectories/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/segments_ref.py + insite_ref.rollout (numpy, vectorised over patients) "
+                                         f"on {n_s} patients x {T} steps, {el:.2f} s"}
+    print(json.dumps(res))
+
+
 def main():
     args = parse()
+    if args.config == "f4":
+        return f4_main(args)
     if args.config == "insite":
         return insite_main(args)
     if args.config == "c3":

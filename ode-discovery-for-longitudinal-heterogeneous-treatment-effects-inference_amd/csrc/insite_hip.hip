@@ -912,31 +912,55 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
     for (int a = 0; a < NARM; ++a)
 #pragma unroll
       for (int j = 0; j < 5; ++j) mo[a][j] = 0.0;
-    const double* xp = x + (valid ? p * xsp : 0);
-    const int8_t* ap = arm + (valid ? p * asp : 0);
-    // samples k <= L and arms k < L of this lane; everything else reads as (0, -1)
-    // loads are issued unconditionally from a clamped (always valid) index and masked afterwards:
-    // exec-masked loads would make the compiler drain vmcnt at every chunk
-    auto ldx = [&](int k) {
-      const double v = xp[(int64_t)(k < L ? k : L) * xsk];
-      return k <= L ? v : 0.0;
+    // Per chunk the wave reads samples k0+1 .. k0+KC (+1) and arms k0+1 .. k0+KC through buffer
+    // descriptors based at the wave's first patient (wave-uniform base, 32-bit per-lane offsets), every
+    // load issued unconditionally: lanes past N read through an offset the hardware drops, steps past
+    // the stored range read 0, and samples past the lane's own L are masked after the load (exec-masked
+    // loads would serialise: one vmcnt(0) per load).
+    const int64_t p0 = tile * kWave;
+    const int nvalid = (int)(N - p0 < kWave ? N - p0 : kWave);
+    const unsigned xvo = valid ? (unsigned)((int64_t)lane * xsp * 8) : kOOB;
+    const unsigned avo = valid ? (unsigned)((int64_t)lane * asp) : kOOB;
+    auto x_rsrc = [&](int kb) {  // samples kb .. kb + KC of the wave's patients
+      int rows = n_steps - kb;
+      if (rows > kSegKC + 1) rows = kSegKC + 1;
+      const int bytes = rows > 0 ? (int)(((int64_t)(nvalid - 1) * xsp + (int64_t)(rows - 1) * xsk + 1) * 8) : 0;
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(x + p0 * xsp + (int64_t)(rows > 0 ? kb : 0) * xsk), (short)0,
+                                               bytes, 0x00020000);
     };
-    auto lda = [&](int k) {
-      const int v = ap[(int64_t)(k < L ? k : (L > 0 ? L - 1 : 0)) * ask];
-      return k < L ? v : -1;
+    auto a_rsrc = [&](int kb) {  // arms kb .. kb + KC - 1 (stored steps < n_steps - 1)
+      int rows = n_steps - 1 - kb;
+      if (rows > kSegKC) rows = kSegKC;
+      const int bytes = rows > 0 ? (int)((int64_t)(nvalid - 1) * asp + (int64_t)(rows - 1) * ask + 1) : 0;
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(arm + p0 * asp + (int64_t)(rows > 0 ? kb : 0) * ask), (short)0,
+                                               bytes, 0x00020000);
     };
+    const unsigned xstep = (unsigned)(xsk * 8), astep = (unsigned)ask;
     if (Lw > 0) {
-      double xj = ldx(0);
-      int aj = lda(0);
+      double xj;
+      int aj;
+      {
+        const __amdgpu_buffer_rsrc_t rx = x_rsrc(0), ra = a_rsrc(0);
+        xj = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, xvo, 0, 0));
+        const int a0 = (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(ra, avo, 0, 0);
+        aj = 0 < L ? a0 : -1;
+      }
       int aprev = -1;  // arm of sample j-1 (SMOOTH1: segment-start test)
       for (int k0 = 0; k0 < Lw; k0 += kSegKC) {
         constexpr int NX = kSegKC + (SMOOTH1 ? 1 : 0);
         double xn[NX];
         int an[kSegKC];
+        const __amdgpu_buffer_rsrc_t rx = x_rsrc(k0 + 1), ra = a_rsrc(k0 + 1);
 #pragma unroll
-        for (int j = 0; j < NX; ++j) xn[j] = ldx(k0 + 1 + j);
+        for (int j = 0; j < NX; ++j) {
+          const double v = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, xvo + j * xstep, 0, 0));
+          xn[j] = (k0 + 1 + j <= L) ? v : 0.0;
+        }
 #pragma unroll
-        for (int j = 0; j < kSegKC; ++j) an[j] = lda(k0 + 1 + j);
+        for (int j = 0; j < kSegKC; ++j) {
+          const int v = (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(ra, avo + j * astep, 0, 0);
+          an[j] = (k0 + 1 + j < L) ? v : -1;
+        }
 #pragma unroll
         for (int j = 0; j < kSegKC; ++j) {
           const double x1 = xn[j];
@@ -2488,6 +2512,9 @@ int32_t run_segment_discovery(const double* x, int64_t ldx, const int8_t* arm, i
     return INSITE_E_INVALID_ARG;
   if (n_patients > 0 && (!x || !arm || !seq_len || (n_statics > 0 && !u))) return INSITE_E_INVALID_ARG;
   if (fd_kind != INSITE_FD_ORDER1 && fd_kind != INSITE_FD_SMOOTHED1) return INSITE_E_UNSUPPORTED;
+  // 32-bit buffer offsets: a chunk of kSegKC + 2 steps (time-major) or a wave's 64 rows (patient-major)
+  const int64_t span = tm ? (int64_t)(kSegKC + 2) : (int64_t)kWave;
+  if (ldx > ((int64_t)1 << 31) / (8 * span) || ld_arm > ((int64_t)1 << 31) / span) return INSITE_E_UNSUPPORTED;
   LibDesc lib;
   int32_t st = build_lib(exps, n_terms, n_statics, &lib);
   if (st != INSITE_OK) return st;

@@ -149,3 +149,54 @@ def irregular_grid(n_patients: int, seed: int, device, t_max: float = MAX_TIME_H
     t[0] = 0.0
     t[1:] = torch.where(torch.isinf(r), torch.full_like(r, float("nan")), r)
     return t.contiguous(), n_obs
+
+
+@dataclass
+class SegmentCohort:
+    x: torch.Tensor          # [T + 1, N] f64 time-major samples (x[0] = y0)
+    u: torch.Tensor          # [N, U] f64 statics
+    arm: torch.Tensor        # [T, round_up(N, 4)] int8 time-major per-step arm (4 arms)
+    seq_len: torch.Tensor    # [N] int32
+    T: int
+    dt: float
+    lib: PolyLibrary
+
+
+def markov_arms(n_patients: int, T: int, n_arms: int, switch_p: float, g: torch.Generator, device) -> torch.Tensor:
+    """Per-step treatment sequences [T, round_up(N, 4)] int8 (time-major): a uniformly drawn first arm,
+    then with probability ``switch_p`` per step a switch to a uniformly drawn other arm."""
+    N = int(n_patients)
+    ld = (N + 3) // 4 * 4
+    out = torch.zeros((T, ld), dtype=torch.int8, device=device)
+    a = torch.randint(0, n_arms, (N,), generator=g, device=device)
+    for k in range(T):
+        if k:
+            sw = torch.rand((N,), generator=g, device=device) < switch_p
+            other = (a + torch.randint(1, max(n_arms, 2), (N,), generator=g, device=device)) % n_arms
+            a = torch.where(sw, other, a)
+        out[k, :N] = a.to(torch.int8)
+    return out
+
+
+def synthetic_segments(n_patients: int, T: int, seed: int, device, coef, n_statics: int = 1, switch_p: float = 0.1,
+                       noise: float = OBSERVATION_NOISE, dt: float = 0.1) -> SegmentCohort:
+    """A 4-arm cohort with the layout of the cancer_sim / EQ_5 datasets (the reference
+    simulators themselves, data/cancer_sim and data/continuous/continuous.py, are not on the path): the
+    planted per-arm model ``coef`` [A, F] over the degree-2 interaction library of [x0, statics] is
+    integrated with the Euler-5 rollout kernel under Markov per-step arms, plus observation noise."""
+    dev = torch.device(device)
+    g = _gen(seed, dev)
+    N = int(n_patients)
+    f64 = torch.float64
+    lib = polynomial_library(n_statics, 2, True)
+    c = torch.as_tensor(coef, dtype=f64, device=dev).contiguous()
+    u = (torch.randn((N, n_statics), generator=g, device=dev, dtype=f64) * 0.05 + 0.5).contiguous()
+    y0 = torch.rand((N,), generator=g, device=dev, dtype=f64) * 4.0 + 1.0
+    arms = markov_arms(N, T, c.size(0), switch_p, g, dev)
+    x = torch.empty((T + 1, N), dtype=f64, device=dev)
+    x[0] = y0
+    ops.rollout(y0, u, arms, c, lib, dt, method="euler5", drop_below=0.0, T=T, out=x[1:], layout="time")
+    if noise:
+        x += noise * torch.randn((T + 1, N), generator=g, device=dev, dtype=f64)
+    sl = torch.full((N,), T, dtype=torch.int32, device=dev)
+    return SegmentCohort(x=x, u=u, arm=arms, seq_len=sl, T=T, dt=dt, lib=lib)

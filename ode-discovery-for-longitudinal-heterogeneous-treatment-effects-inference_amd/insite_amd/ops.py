@@ -305,6 +305,13 @@ def sindy_fit_segments(x: torch.Tensor, arm: torch.Tensor, seq_len: torch.Tensor
                                (threshold, alpha, max_iter, unbias)))
 
 
+def plan_gram_segments(x, arm, seq_len, u, dt, lib, n_arms=4, fd="order1", workspace=None, out=None,
+                       layout="patient") -> Plan:
+    """``gram_segments`` as a prepared launch; ``plan.out`` = (G, b)."""
+    name, args, dev, out = _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layout)
+    return Plan(name, args, dev, out)
+
+
 def plan_sindy_fit_segments(x, arm, seq_len, u, dt, lib, threshold, alpha, max_iter=100, unbias=True, n_arms=4,
                             fd="order1", workspace=None, out=None, layout="patient") -> Plan:
     """``sindy_fit_segments`` as a prepared launch; ``plan.out`` = (coef, mask, iters, G, b)."""
