@@ -876,12 +876,23 @@ discovery_finalize(const double* __restrict__ partial, int nblk, int narm_pad, i
 // Per 64-patient tile the per-(patient, arm) moments are contracted to Gram entries (one entry per
 // lane, patients staged through LDS in two halves); block partials in the gram_kernel scalar layout
 // feed discovery_finalize.
-constexpr int kSegKC = 8;       // steps per register chunk (loads issued ahead of the arithmetic)
+#ifndef INSITE_SEG_KC
+#define INSITE_SEG_KC 4
+#endif
+#ifndef INSITE_SEG_PF
+#define INSITE_SEG_PF 1
+#endif
+constexpr int kSegMaxBlocks = 8192;  // partials: kSegMaxBlocks x NARM x 64 doubles (16 MB)
+constexpr int kSegKC = INSITE_SEG_KC;  // steps per register chunk (loads issued ahead of the arithmetic)
+constexpr bool kSegPF = INSITE_SEG_PF != 0;  // double-buffered chunks (next chunk in flight)
 constexpr int kSegMono = INSITE_MAX_TERMS;
 constexpr int kSegRS = kSegMono + 5 * INSITE_MAX_ARMS;  // LDS row: F monomials | NARM x 5 moments (29, odd)
 
+#ifndef INSITE_SEG_WPE
+#define INSITE_SEG_WPE 4  // waves per SIMD the register budget is sized for (4: <= 128 VGPRs)
+#endif
 template <int NARM, bool SMOOTH1>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))  // <= 128 VGPRs
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_SEG_WPE)))
 gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const int8_t* __restrict__ arm, int64_t asp,
                 int64_t ask, const int32_t* __restrict__ seq_len, int n_steps, const double* __restrict__ u, int64_t N,
                 double inv_dt, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ ticket) {
@@ -893,9 +904,14 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
   double acc[NARM];
 #pragma unroll
   for (int a = 0; a < NARM; ++a) acc[a] = 0.0;
-  const bool ent = lane < lib.nE;
-  const int my_i = ent ? lib.ei[lane] : 0;
-  const int my_k = ent ? lib.ek[lane] : -1;
+  // contraction roles: lane = entry e + nE * g; the ng = 64 / nE lane groups split each half-tile's
+  // 32 patients (group g takes q = g, g + ng, ...), so small libraries keep every lane busy
+  const int ng = lib.nE <= kWave ? kWave / lib.nE : 1;
+  const int my_g = lane / lib.nE;
+  const int my_e = lane - my_g * lib.nE;
+  const bool ent = my_g < ng;
+  const int my_i = ent ? lib.ei[my_e] : 0;
+  const int my_k = ent ? lib.ek[my_e] : -1;
   const int moff = kSegMono + (my_k >= 0 ? lib.ex[my_i] + lib.ex[my_k] : 3 + lib.ex[my_i]);
 
   const int64_t n_tiles = (N + kWave - 1) / kWave;
@@ -946,29 +962,27 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
         aj = 0 < L ? a0 : -1;
       }
       int aprev = -1;  // arm of sample j-1 (SMOOTH1: segment-start test)
-      for (int k0 = 0; k0 < Lw; k0 += kSegKC) {
-        constexpr int NX = kSegKC + (SMOOTH1 ? 1 : 0);
-        double xn[NX];
-        int an[kSegKC];
+      constexpr int NX = kSegKC + (SMOOTH1 ? 1 : 0);
+      // raw chunk registers; the masks (k <= L, k < L) are applied at the use, so a prefetched chunk
+      // is not waited for when it is issued
+      auto load = [&](double (&xr)[NX], int (&ar)[kSegKC], int k0) {
         const __amdgpu_buffer_rsrc_t rx = x_rsrc(k0 + 1), ra = a_rsrc(k0 + 1);
 #pragma unroll
-        for (int j = 0; j < NX; ++j) {
-          const double v = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, xvo + j * xstep, 0, 0));
-          xn[j] = (k0 + 1 + j <= L) ? v : 0.0;
-        }
+        for (int j = 0; j < NX; ++j)
+          xr[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, xvo + j * xstep, 0, 0));
+#pragma unroll
+        for (int j = 0; j < kSegKC; ++j)
+          ar[j] = (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(ra, avo + j * astep, 0, 0);
+      };
+      auto process = [&](const double (&xr)[NX], const int (&ar)[kSegKC], int k0) {
 #pragma unroll
         for (int j = 0; j < kSegKC; ++j) {
-          const int v = (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(ra, avo + j * astep, 0, 0);
-          an[j] = (k0 + 1 + j < L) ? v : -1;
-        }
-#pragma unroll
-        for (int j = 0; j < kSegKC; ++j) {
-          const double x1 = xn[j];
-          const int a1 = an[j];
+          const double x1 = (k0 + 1 + j <= L) ? xr[j] : 0.0;
+          const int a1 = (k0 + 1 + j < L) ? ar[j] : -1;
           const bool endf = a1 != aj;  // sample j+1 closes j's segment (also at j+1 = L)
           double xo, xs1;
           if constexpr (SMOOTH1) {
-            const double x2 = xn[j + 1];
+            const double x2 = (k0 + 2 + j <= L) ? xr[j + 1] : 0.0;
             xo = (aj != aprev) ? xj : 0.5 * (xj + x1);
             xs1 = endf ? x1 : 0.5 * (x1 + x2);
           } else {
@@ -995,6 +1009,26 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
           aj = a1;
           xj = x1;
         }
+      };
+      double xA[NX], xB[NX];
+      int aA[kSegKC], aB[kSegKC];
+      if constexpr (kSegPF) {
+        // two chunks in flight: chunk c + 1 is requested before chunk c is consumed (buffers alternate)
+        load(xA, aA, 0);
+        for (int k0 = 0; k0 < Lw;) {
+          if (k0 + kSegKC < Lw) load(xB, aB, k0 + kSegKC);
+          process(xA, aA, k0);
+          k0 += kSegKC;
+          if (k0 >= Lw) break;
+          if (k0 + kSegKC < Lw) load(xA, aA, k0 + kSegKC);
+          process(xB, aB, k0);
+          k0 += kSegKC;
+        }
+      } else {
+        for (int k0 = 0; k0 < Lw; k0 += kSegKC) {
+          load(xA, aA, k0);
+          process(xA, aA, k0);
+        }
       }
     }
     // ---- per-(patient, arm) Gram blocks A(u) M_a A(u)^T, one entry per lane ----
@@ -1014,7 +1048,7 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
       wave_lds_sync();
       if (ent) {
 #pragma unroll 2
-        for (int q = 0; q < 32; ++q) {
+        for (int q = my_g; q < 32; q += ng) {
           const double* row = ps + q * kSegRS;
           const double wq = row[my_i] * (my_k >= 0 ? row[my_k] : 1.0);
 #pragma unroll
@@ -1030,12 +1064,12 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
 #pragma unroll
   for (int a = 0; a < NARM; ++a) red[(wid * NARM + a) * kWave + lane] = acc[a];
   __syncthreads();
-  if (wid == 0) {
+  if (wid == 0 && lane < lib.nE) {  // entry `lane`: fixed-order sum over waves and lane groups
 #pragma unroll
     for (int a = 0; a < NARM; ++a) {
-      double s = red[(0 * NARM + a) * kWave + lane];
-#pragma unroll
-      for (int ww = 1; ww < kWavesPerBlock; ++ww) s += red[(ww * NARM + a) * kWave + lane];
+      double s = 0.0;
+      for (int ww = 0; ww < kWavesPerBlock; ++ww)
+        for (int g = 0; g < ng; ++g) s += red[(ww * NARM + a) * kWave + g * lib.nE + lane];
       partial[((int64_t)blockIdx.x * NARM + a) * kWave + lane] = s;
     }
   }
@@ -2479,17 +2513,20 @@ int32_t run_discovery(const double* x, int64_t ldx, int32_t layout, int32_t n_st
   return launch_status();
 }
 
+inline int64_t seg_grid(int64_t N) {
+  int64_t g = ((N + kWave - 1) / kWave + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (g > kSegMaxBlocks) g = kSegMaxBlocks;
+  return g < 1 ? 1 : g;
+}
+
 template <int NARM, bool SMOOTH1>
 int launch_gram_seg(hipStream_t st, const double* x, int64_t xsp, int64_t xsk, const int8_t* arm, int64_t asp,
                     int64_t ask, const int32_t* seq_len, int n_steps, const double* u, int64_t N, double inv_dt,
                     const LibDesc& lib, double* part, unsigned* ticket) {
   auto kern = gram_seg_kernel<NARM, SMOOTH1>;
-  const int64_t tiles = (N + kWave - 1) / kWave;
-  int64_t g = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-  const int64_t gres = resident_waves(kern) / kWavesPerBlock;
-  if (gres > 0 && g > gres) g = gres;
-  if (g > kGramMaxBlocks) g = kGramMaxBlocks;
-  if (g < 1) g = 1;
+  // one 64-patient tile per wave up to kSegMaxBlocks blocks: the dispatcher hands freed slots to the
+  // next block, which balances the tail better than a resident grid striding over 5-6 tiles per wave
+  const int64_t g = seg_grid(N);
   kern<<<dim3((unsigned)g), kBlock, 0, st>>>(x, xsp, xsk, arm, asp, ask, seq_len, n_steps, u, N, inv_dt, lib, part,
                                              ticket);
   return (int)g;
@@ -2518,7 +2555,7 @@ int32_t run_segment_discovery(const double* x, int64_t ldx, const int8_t* arm, i
   LibDesc lib;
   int32_t st = build_lib(exps, n_terms, n_statics, &lib);
   if (st != INSITE_OK) return st;
-  if (!workspace || workspace_bytes < insite_gram_workspace_bytes(n_patients, n_arms, n_terms))
+  if (!workspace || workspace_bytes < insite_gram_segments_workspace_bytes(n_patients, n_arms, n_terms))
     return INSITE_E_WORKSPACE;
   lib.mfma = 0;
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
@@ -2737,7 +2774,9 @@ int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, int32_t layout, int32
 }
 
 size_t insite_gram_segments_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms) {
-  return insite_gram_workspace_bytes(n_patients, n_arms, n_terms);
+  (void)n_terms;
+  if (n_patients < 0 || n_arms < 1 || n_arms > INSITE_MAX_ARMS) return 0;
+  return kGramWsHeader + (size_t)seg_grid(n_patients) * narm_pad(n_arms) * kWave * sizeof(double);
 }
 
 int32_t insite_gram_segments_f64(const double* x, int64_t ldx, const int8_t* arm, int64_t ld_arm, int32_t layout,

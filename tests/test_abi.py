@@ -171,7 +171,7 @@ def test_invalid_arguments_rejected_without_device(L):
     assert seg(x, 60, x, 59, 0, 60, x, x, 10, 2, 4, ep, 7, s1, 0.1, g, bb, nul, 0, nul) == -3       # workspace
     assert L.insite_sindy_fit_segments_f64(x, 60, x, 59, 0, 60, x, x, 10, 2, 4, ep, 7, o1, 0.1, -1.0, 0.5, 100, 1,
                                            g, bb, g, nul, nul, nul, 0, nul) == -1
-    assert L.insite_gram_segments_workspace_bytes(1000, 4, 7) == L.insite_gram_workspace_bytes(1000, 4, 7) > 0
+    assert 0 < L.insite_gram_segments_workspace_bytes(1000, 4, 7) <= L.insite_gram_segments_workspace_bytes(10**7, 4, 7)
 
 
 def test_ops_refuse_host_tensors(L):

@@ -8,6 +8,11 @@ build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC
 for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
   case $v in
     NOSTORE) NAME=$v build -DINSITE_ABLATE_NOSTORE ;;
+    SEGKC8) NAME=$v build -DINSITE_SEG_KC=8 -DINSITE_SEG_WPE=3 ;;
+    SEGKC4) NAME=$v build -DINSITE_SEG_KC=4 -DINSITE_SEG_WPE=4 ;;
+    SEGKC16) NAME=$v build -DINSITE_SEG_KC=16 -DINSITE_SEG_WPE=2 ;;
+    SEGNOPF) NAME=$v build -DINSITE_SEG_PF=0 -DINSITE_SEG_WPE=4 ;;
+    SEGKC16NOPF) NAME=$v build -DINSITE_SEG_KC=16 -DINSITE_SEG_PF=0 -DINSITE_SEG_WPE=3 ;;
     NOARM) NAME=$v build -DINSITE_ABLATE_NOARM ;;
     TIMING) NAME=$v build -DINSITE_TIMING ;;
     LATE) NAME=$v build -DINSITE_GRAM_LATE_ISSUE ;;

@@ -9,7 +9,7 @@ import torch
 from insite_amd import ops, cohort
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--op", default="gram", choices=["gram", "sindy_fit", "rollout", "stlsq", "step"])
+ap.add_argument("--op", default="gram", choices=["gram", "sindy_fit", "rollout", "stlsq", "step", "gram_seg"])
 ap.add_argument("--patients", type=int, default=100_000)
 ap.add_argument("--T", type=int, default=200)
 ap.add_argument("--iters", type=int, default=50)
@@ -37,8 +37,13 @@ step_out = (torch.empty((2, lib.n_terms), dtype=torch.float64, device=dev),
             torch.empty((2, lib.n_terms), dtype=torch.int8, device=dev), torch.empty(2, dtype=torch.int32, device=dev),
             torch.empty((2, lib.n_terms, lib.n_terms), dtype=torch.float64, device=dev),
             torch.empty((2, lib.n_terms), dtype=torch.float64, device=dev))
+if a.op == "gram_seg":   # F4: 4-arm treatment-segment Gram, time-major (bench.py --config f4 cohort)
+    seg = cohort.synthetic_segments(a.patients, a.T, seed=31, device=dev,
+                                    coef=[[0, .2, 0, 0], [0, 0, 0, -.6], [0, -.3, 0, 0], [0, -.25, 0, -.9]])
 def run():
-    if a.op == "gram":
+    if a.op == "gram_seg":
+        ops.gram_segments(seg.x, seg.arm, seg.seq_len, seg.u, seg.dt, seg.lib, 4, "order1", ws, layout="time")
+    elif a.op == "gram":
         ops.gram(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 2, "smoothed4", ws, layout=xlay)
     elif a.op == "sindy_fit":
         ops.sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, 100, True, 2, "smoothed4", ws,
