@@ -462,10 +462,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    # rehearsal knobs for a one-GPU box (never set by the driver): every rank on cuda:0 over gloo, which
+    # exercises the multi-rank step (shards, the all-reduce on the STLSQ stream, max-over-ranks timing)
+    if os.environ.get("INSITE_REHEARSE_ONE_GPU"):
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("INSITE_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from insite_amd import ops, cohort
     from insite_amd import dist as idist
