@@ -34,7 +34,8 @@
  *     hipStream_t passed as void*; NULL = the default stream) and uses the caller's current
  *     device.  No entry point synchronises the device.
  *   - Return value: 0 = success, negative = error (insite_strerror).  No exceptions cross
- *     the ABI.  Entry points are reentrant; the library holds no mutable global state.
+ *     the ABI.  Entry points are reentrant; the library holds no mutable global state apart from
+ *     the mutex-guarded hipRTC kernel cache of insite_rollout_ms_sparse_f32.
  *   - Polynomial libraries are over the inputs [x, u_0, .., u_{U-1}] (one state x, U static
  *     covariates) and are described by an exponent table exps[F][1+U] (int8, HOST memory)
  *     in pysindy column order (insite_poly_library produces it).
@@ -295,6 +296,20 @@ int32_t insite_rollout_ms_f32(const float* y0, int64_t ld_y0, const uint32_t* in
                               const double* coef, const int8_t* exps, int32_t n_terms, int32_t n_states,
                               int64_t n_rows, int32_t T, double dt, int32_t method, int32_t substeps,
                               double drop_below, float* y_out, int64_t ld_y, void* stream);
+
+/* Support-specialised variant of insite_rollout_ms_f32 (a sparse discovered model keeps
+ * the S-state rollout off the VALU roof).  support: HOST int8 [S][F], nonzero = the term is in the model
+ * (e.g. the STLSQ mask).  On first use per (support, method, input count, device) the kernel is generated
+ * and compiled with hipRTC (cached for the process; the first call pays ~1-2 s), and evaluates only the
+ * supported terms, in the library's column order — the same fp32 sums as the dense kernel, whose dropped
+ * terms add fmaf(0, th, f) = f.  Coefficient values are read from `coef` (device) at every launch; if
+ * any coefficient outside the support is above drop_below, the launch runs the dense RHS instead (a
+ * stale support costs speed, not correctness).  Other arguments and results as insite_rollout_ms_f32;
+ * INSITE_E_HIP if hipRTC or the module load fails. */
+int32_t insite_rollout_ms_sparse_f32(const float* y0, int64_t ld_y0, const uint32_t* inp_bits, int64_t ld_bits,
+                                     const double* coef, const int8_t* support, const int8_t* exps, int32_t n_terms,
+                                     int32_t n_states, int64_t n_rows, int32_t T, double dt, int32_t method,
+                                     int32_t substeps, double drop_below, float* y_out, int64_t ld_y, void* stream);
 
 #ifdef __cplusplus
 }

@@ -18,8 +18,14 @@
 //   rollout_ms_kernel  lane = patient, S-dimensional state in fp32 registers, RK4 / Euler of the dense
 //                      degree-2 RHS, per-step treatment bits (32 steps per register via the half-wave bit
 //                      transpose), non-temporal stores of [T][S][N] fp32 trajectories.
+#include <hip/hiprtc.h>
+
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
 
 #include "insite_common.h"
 
@@ -573,6 +579,239 @@ inline int ms_grid(int64_t N) {
   return (int)g;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Support-specialised S-state rollout, generated at run time (hipRTC).  A discovered model is sparse
+// (C3: 11 of the 110 state x column coefficients), and the dense RHS keeps the rollout VALU-bound
+// (SURVEY.md §7.3-4).  The generated kernel evaluates exactly the supported terms, column by column in
+// library order: with the dropped terms contributing fmaf(0, th, f) = f, the sums are the dense ones.
+// The coefficient VALUES stay device data (read once per wave into scalar registers); only the support
+// pattern is compiled in.  If any coefficient outside the pattern is above the drop threshold the
+// launch takes the embedded dense RHS instead, so a stale pattern can cost speed, never correctness.
+// ---------------------------------------------------------------------------------------------
+const char* kMsSparseTemplate = R"HIPSRC(
+#define S @S@
+#define NIN @NIN@
+#define F @F@
+#define METHOD @METHOD@
+static __device__ __forceinline__ unsigned bit_transpose32(unsigned x, int lane) {
+  const unsigned m[5] = {0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int sh = 16 >> k;
+    const unsigned y = (unsigned)__shfl_xor((int)x, sh, 64);
+    x = (lane & sh) ? ((x & ~m[k]) | ((y >> sh) & m[k])) : ((x & m[k]) | ((y << sh) & ~m[k]));
+  }
+  return x;
+}
+__constant__ int kCI[F] = {@CI@};
+__constant__ int kCK[F] = {@CK@};
+static __device__ __forceinline__ void rhs_dense(const float (&v)[S], float a, const float (&cf)[S][F], float (&f)[S]) {
+  float z[S + NIN + 1];
+  z[0] = 1.0f;
+#pragma unroll
+  for (int s = 0; s < S; ++s) z[1 + s] = v[s];
+#pragma unroll
+  for (int q = 0; q < NIN; ++q) z[1 + S + q] = a;
+#pragma unroll
+  for (int s = 0; s < S; ++s) f[s] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < F; ++j) {
+    const float th = kCK[j] == 0 ? z[kCI[j]] : z[kCI[j]] * z[kCK[j]];
+#pragma unroll
+    for (int s = 0; s < S; ++s) f[s] = fmaf(cf[s][j], th, f[s]);
+  }
+}
+static __device__ __forceinline__ float coef_at(const double* c, int i, double drop) {
+  const double v = c[i];
+  return fabs(v) > drop ? (float)v : 0.0f;
+}
+extern "C" __global__ void __launch_bounds__(256) ms_rollout_sparse(
+    const float* __restrict__ y0, long long ld0, const unsigned* __restrict__ abits, long long lda,
+    const double* __restrict__ coef, float* __restrict__ yout, long long ldy, long long N, int T, int substeps,
+    double dt, double drop) {
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long long p0 = ((long long)blockIdx.x * 4 + wid) * 64;
+  if (p0 >= N) return;
+  const long long p = p0 + lane;
+  const bool act = p < N;
+  const long long pc = act ? p : N - 1;
+  // pattern check: every coefficient outside the compiled support must be dropped
+  const unsigned long long sup[2] = {@SUPLO@ull, @SUPHI@ull};
+  bool viol = false;
+  for (int t = lane; t < S * F; t += 64) {
+    const bool in = (sup[t >> 6] >> (t & 63)) & 1ull;
+    viol = viol || (!in && fabs(coef[t]) > drop);
+  }
+  const bool dense = __ballot(viol) != 0ull;
+  float y[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) y[s] = y0[s * ld0 + pc];
+  const float h = (float)(dt / substeps);
+  const float h2 = 0.5f * h, h6 = h / 6.0f;
+  const int nvalid = (int)(N - p0 < 64 ? N - p0 : 64);
+  const unsigned yoff = act ? (unsigned)(lane * 4) : 0x80000000u;
+  auto word = [&](int g) -> unsigned {
+    if (!abits) return 0u;
+    const int k = 32 * g + (lane & 31);
+    const int kk = k < T ? k : T - 1;
+    const long long col = (p0 >> 5) + (lane >> 5);
+    const unsigned v = col * 32 < N ? abits[(long long)kk * lda + col] : 0u;
+    return bit_transpose32(v, lane);
+  };
+  auto run = [&](auto&& rhs) {
+    unsigned wnext = word(0);
+    for (int k0 = 0; k0 < T; k0 += 32) {
+      const unsigned wcur = wnext;
+      if (k0 + 32 < T) wnext = word((k0 >> 5) + 1);
+      const int kend = T - k0 < 32 ? T - k0 : 32;
+      for (int i = 0; i < kend; ++i) {
+        const float a = (float)((wcur >> i) & 1u);
+        for (int sub = 0; sub < substeps; ++sub) {
+          if (METHOD == 0) {
+            float f[S];
+            rhs(y, a, f);
+#pragma unroll
+            for (int s = 0; s < S; ++s) y[s] = fmaf(h, f[s], y[s]);
+          } else {
+            float k1[S], k2[S], k3[S], k4[S], t[S];
+            rhs(y, a, k1);
+#pragma unroll
+            for (int s = 0; s < S; ++s) t[s] = fmaf(h2, k1[s], y[s]);
+            rhs(t, a, k2);
+#pragma unroll
+            for (int s = 0; s < S; ++s) t[s] = fmaf(h2, k2[s], y[s]);
+            rhs(t, a, k3);
+#pragma unroll
+            for (int s = 0; s < S; ++s) t[s] = fmaf(h, k3[s], y[s]);
+            rhs(t, a, k4);
+#pragma unroll
+            for (int s = 0; s < S; ++s) y[s] = fmaf(h6, (k1[s] + 2.0f * k2[s]) + (2.0f * k3[s] + k4[s]), y[s]);
+          }
+        }
+        const int k = k0 + i;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(yout + (long long)k * S * ldy + p0), (short)0, (int)(((long long)(S - 1) * ldy + nvalid) * 4),
+            0x00020000);
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, y[s]), rs, yoff + (unsigned)(s * ldy * 4),
+                                                0, @AUX@);
+      }
+    }
+  };
+  if (dense) {
+    float cf[S][F];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int j = 0; j < F; ++j) cf[s][j] = coef_at(coef, s * F + j, drop);
+    run([&](const float (&v)[S], float a, float (&f)[S]) { rhs_dense(v, a, cf, f); });
+  } else {
+@COEFS@
+    run([&](const float (&v)[S], float a, float (&f)[S]) {
+      float z[S + NIN + 1];
+      z[0] = 1.0f;
+#pragma unroll
+      for (int s = 0; s < S; ++s) z[1 + s] = v[s];
+#pragma unroll
+      for (int q = 0; q < NIN; ++q) z[1 + S + q] = a;
+#pragma unroll
+      for (int s = 0; s < S; ++s) f[s] = 0.0f;
+@BODY@
+    });
+  }
+}
+)HIPSRC";
+
+std::string ms_replace(std::string src, const std::string& key, const std::string& val) {
+  for (size_t pos; (pos = src.find(key)) != std::string::npos;) src.replace(pos, key.size(), val);
+  return src;
+}
+
+// Kernel source for one (S, NIN, method, support) — interaction-only degree-2 library.
+template <int S, int NIN>
+std::string ms_sparse_source(int method, const int8_t* support) {
+  constexpr PolyCols<S + NIN, true> pc;
+  constexpr int F = PolyCols<S + NIN, true>::F;
+  std::string ci, ck, coefs, body;
+  unsigned long long sup[2] = {0ull, 0ull};
+  for (int j = 0; j < F; ++j) {
+    ci += std::to_string(pc.ci[j]) + (j + 1 < F ? "," : "");
+    ck += std::to_string(pc.ck[j]) + (j + 1 < F ? "," : "");
+  }
+  for (int j = 0; j < F; ++j) {  // column order = the dense kernel's summation order
+    bool any = false;
+    std::string col;
+    for (int st = 0; st < S; ++st) {
+      const int t = st * F + j;
+      if (!support[t]) continue;
+      sup[t >> 6] |= 1ull << (t & 63);
+      coefs += "    const float c" + std::to_string(t) + " = coef_at(coef, " + std::to_string(t) + ", drop);\n";
+      col += "        f[" + std::to_string(st) + "] = fmaf(c" + std::to_string(t) + ", th, f[" + std::to_string(st) + "]);\n";
+      any = true;
+    }
+    if (!any) continue;
+    const std::string th = pc.ck[j] == 0 ? "z[" + std::to_string(pc.ci[j]) + "]"
+                                         : "z[" + std::to_string(pc.ci[j]) + "] * z[" + std::to_string(pc.ck[j]) + "]";
+    body += "      {\n        const float th = " + th + ";\n" + col + "      }\n";
+  }
+  std::string src = kMsSparseTemplate;
+  src = ms_replace(src, "@S@", std::to_string(S));
+  src = ms_replace(src, "@NIN@", std::to_string(NIN));
+  src = ms_replace(src, "@F@", std::to_string(F));
+  src = ms_replace(src, "@METHOD@", std::to_string(method == INSITE_METHOD_EULER ? 0 : 1));
+  src = ms_replace(src, "@CI@", ci);
+  src = ms_replace(src, "@CK@", ck);
+  src = ms_replace(src, "@SUPLO@", std::to_string(sup[0]));
+  src = ms_replace(src, "@SUPHI@", std::to_string(sup[1]));
+  src = ms_replace(src, "@AUX@", std::to_string(kStoreAux));
+  src = ms_replace(src, "@COEFS@", coefs);
+  src = ms_replace(src, "@BODY@", body);
+  return src;
+}
+
+// Compiled kernels, one per (device, source); compiled once under the lock and never evicted.
+struct MsJitCache {
+  std::mutex mu;
+  std::map<std::pair<int, std::string>, hipFunction_t> fns;
+};
+MsJitCache& ms_jit_cache() {
+  static MsJitCache c;
+  return c;
+}
+
+hipFunction_t ms_jit_function(const std::string& src) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  MsJitCache& c = ms_jit_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  const auto key = std::make_pair(dev, src);
+  auto it = c.fns.find(key);
+  if (it != c.fns.end()) return it->second;
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "insite_ms_sparse.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+    return nullptr;
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast-honor-pragmas"};
+  const bool ok = hiprtcCompileProgram(prog, 4, opts) == HIPRTC_SUCCESS;
+  std::vector<char> code;
+  if (ok) {
+    size_t n = 0;
+    if (hiprtcGetCodeSize(prog, &n) == HIPRTC_SUCCESS && n > 0) {
+      code.resize(n);
+      if (hiprtcGetCode(prog, code.data()) != HIPRTC_SUCCESS) code.clear();
+    }
+  }
+  hiprtcDestroyProgram(&prog);
+  if (code.empty()) return nullptr;
+  hipModule_t mod;
+  hipFunction_t fn;
+  if (hipModuleLoadData(&mod, code.data()) != hipSuccess) return nullptr;
+  if (hipModuleGetFunction(&fn, mod, "ms_rollout_sparse") != hipSuccess) return nullptr;
+  c.fns.emplace(key, fn);
+  return fn;
+}
+
 }  // namespace
 
 extern "C" {
@@ -657,6 +896,36 @@ int32_t insite_rollout_ms_f32(const float* y0, int64_t ld_y0, const uint32_t* in
   if (nin == 1) rollout_ms_kernel<5, 1, true><<<grid, kBlock, 0, hs>>>(ra);
   else rollout_ms_kernel<5, 0, true><<<grid, kBlock, 0, hs>>>(ra);
   return launch_status();
+}
+
+int32_t insite_rollout_ms_sparse_f32(const float* y0, int64_t ld_y0, const uint32_t* inp_bits, int64_t ld_bits,
+                                     const double* coef, const int8_t* support, const int8_t* exps, int32_t n_terms,
+                                     int32_t n_states, int64_t n_rows, int32_t T, double dt, int32_t method,
+                                     int32_t substeps, double drop_below, float* y_out, int64_t ld_y, void* stream) {
+  if (n_states != 5) return INSITE_E_UNSUPPORTED;
+  if (n_rows < 0 || T < 0 || substeps < 1 || !(dt >= 0.0) || ld_y0 < n_rows || ld_y < n_rows || !exps || !support)
+    return INSITE_E_INVALID_ARG;
+  if (inp_bits && ld_bits < (n_rows + 31) / 32) return INSITE_E_INVALID_ARG;
+  if (method != INSITE_METHOD_EULER && method != INSITE_METHOD_RK4) return INSITE_E_UNSUPPORTED;
+  const int nin = inp_bits ? 1 : 0;
+  if (ms_library_kind(exps, n_terms, n_states, nin) != 1) return INSITE_E_UNSUPPORTED;
+  if (n_rows == 0 || T == 0) return INSITE_OK;
+  if (!y0 || !coef || !y_out) return INSITE_E_INVALID_ARG;
+  if ((int64_t)n_states * ld_y * 4 >= ((int64_t)1 << 31)) return INSITE_E_UNSUPPORTED;  // 32-bit step offsets
+  const std::string src = nin ? ms_sparse_source<5, 1>(method, support) : ms_sparse_source<5, 0>(method, support);
+  hipFunction_t fn = ms_jit_function(src);
+  if (!fn) return INSITE_E_HIP;
+  long long ld0 = ld_y0, lda = ld_bits, ldy = ld_y, N = n_rows;
+  int Ti = T, sub = substeps;
+  double dti = dt, drop = drop_below;
+  const unsigned* ab = inp_bits;
+  void* args[] = {(void*)&y0, &ld0, (void*)&ab, &lda, (void*)&coef, (void*)&y_out, &ldy, &N, &Ti, &sub, &dti, &drop};
+  const int64_t waves = (n_rows + kWave - 1) / kWave;
+  const unsigned grid = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+  if (hipModuleLaunchKernel(fn, grid, 1, 1, kBlock, 1, 1, 0, reinterpret_cast<hipStream_t>(stream), args, nullptr) !=
+      hipSuccess)
+    return INSITE_E_HIP;
+  return INSITE_OK;
 }
 
 }  // extern "C"

@@ -51,6 +51,7 @@ EXPORTS = (
     "insite_gram_ms_f32",
     "insite_stlsq_wave_f64",
     "insite_rollout_ms_f32",
+    "insite_rollout_ms_sparse_f32",
 )
 
 
@@ -107,6 +108,8 @@ _SIGNATURES = {
                                        _vp]),
     "insite_rollout_ms_f32": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _vp, _vp, _c_i32, _c_i32, _c_i64, _c_i32, _c_f64,
                                        _c_i32, _c_i32, _c_f64, _vp, _c_i64, _vp]),
+    "insite_rollout_ms_sparse_f32": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _c_i32, _c_i32, _c_i64, _c_i32,
+                                              _c_f64, _c_i32, _c_i32, _c_f64, _vp, _c_i64, _vp]),
 }
 
 

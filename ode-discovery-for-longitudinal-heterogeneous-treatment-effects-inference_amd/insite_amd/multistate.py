@@ -164,9 +164,13 @@ def fit_ms(x, a, lib: MsLibrary, dt: float, threshold: float = THRESHOLD_C3, alp
 
 def rollout_ms(y0: torch.Tensor, a: torch.Tensor | None, coef: torch.Tensor, lib: MsLibrary, dt: float,
                T: int, method: str = "rk4", substeps: int | None = None, drop_below: float = 1e-3,
-               out: torch.Tensor | None = None, n_rows: int | None = None):
+               out: torch.Tensor | None = None, n_rows: int | None = None, support=None):
     """S-state open-loop rollout (insite_rollout_ms_f32).  y0 [S, >=N] float32, a bits [T, W] or None,
-    coef [S, F] f64.  Returns y [T, S, N] float32 (state after each interval)."""
+    coef [S, F] f64.  Returns y [T, S, N] float32 (state after each interval).
+
+    ``support`` (host [S, F] bool/int, e.g. the STLSQ mask): the support-specialised kernel
+    (insite_rollout_ms_sparse_f32, generated with hipRTC on first use per support) — same results, only
+    the model's terms evaluated; a coefficient outside ``support`` makes that launch run the dense RHS."""
     L = _lib.load()
     S = lib.n_states
     _dev("y0", y0, torch.float32, 2)
@@ -186,6 +190,15 @@ def rollout_ms(y0: torch.Tensor, a: torch.Tensor | None, coef: torch.Tensor, lib
         if out.size(0) < T or out.size(2) < N:
             raise ValueError("out must be [>=T, S, >=N]")
     tab = lib.table()
+    if support is not None:
+        sup = np.ascontiguousarray(np.asarray(support) != 0, dtype=np.int8)
+        if sup.shape != (S, lib.n_terms):
+            raise ValueError("support must be a host [S, F] mask")
+        st = L.insite_rollout_ms_sparse_f32(_p(y0), y0.stride(0), ap, lda, _p(coef), sup.ctypes.data_as(ctypes.c_void_p),
+                                            tab.ctypes.data_as(ctypes.c_void_p), lib.n_terms, S, N, int(T), float(dt), m,
+                                            sub, float(drop_below), _p(out), out.size(2), _stream(y0.device))
+        _lib.check("insite_rollout_ms_sparse_f32", st)
+        return out
     st = L.insite_rollout_ms_f32(_p(y0), y0.stride(0), ap, lda, _p(coef), tab.ctypes.data_as(ctypes.c_void_p),
                                  lib.n_terms, S, N, int(T), float(dt), m, sub, float(drop_below), _p(out),
                                  out.size(2), _stream(y0.device))

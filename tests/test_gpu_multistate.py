@@ -176,3 +176,41 @@ def test_synthetic_c3_device_cohort_recovers_truth(dev):
     truth = MS.c3_truth_coef(coh.lib, device=dev)
     assert torch.equal(mask != 0, truth != 0)
     assert (coef[1:] - truth[1:]).abs().max().item() < 5e-3
+
+
+@pytest.mark.parametrize("method,sub", [("rk4", 1), ("euler", 2)])
+@pytest.mark.parametrize("inputs", [True, False])
+def test_sparse_rollout_equals_dense(dev, method, sub, inputs):
+    """insite_rollout_ms_sparse_f32 (support-specialised kernel generated with hipRTC) evaluates only the
+    model's terms in the library's column order: bitwise the dense kernel's trajectories; an extra small
+    term above the drop threshold outside the given support makes the launch take the dense RHS (still
+    equal); a term below the threshold is dropped either way."""
+    from insite_amd import multistate as MS
+    rng = np.random.default_rng(7)
+    ex = M.c3_library()
+    truth = M.c3_truth_coef(ex)
+    coef = truth * (1 + 0.1 * rng.normal(size=truth.shape) * (truth != 0))
+    coef[3, 12] = 5e-4                       # below drop: not in the model
+    N, T = 3000, 97
+    a = M.treatment_markov(N, T, rng, 0.3, 0.05)
+    bits = _bits(a, dev) if inputs else None
+    lib = _lib() if inputs else _lib(n_inputs=0)
+    if not inputs:                           # a sparse model over the 16 state-only columns
+        coef = np.zeros((5, lib.n_terms))
+        for s_ in range(5):
+            coef[s_, 1 + s_] = -0.5
+        coef[1, 1], coef[4, 10], coef[2, 0] = 0.4, -0.2, 0.05
+    y0 = torch.tensor(np.stack([rng.uniform(0, 1, N) for _ in range(4)] + [rng.uniform(1, 5, N)]).astype(np.float32),
+                      device=dev)
+    c = torch.tensor(coef, device=dev)
+    support = np.abs(coef) > 1e-3
+    y_dense = MS.rollout_ms(y0, bits, c, lib, M.DT_C3, T, method=method, substeps=sub)
+    y_sparse = MS.rollout_ms(y0, bits, c, lib, M.DT_C3, T, method=method, substeps=sub, support=support)
+    torch.cuda.synchronize()
+    assert torch.equal(y_sparse, y_dense)
+    # a stale support (one model term missing): the launch falls back to the dense RHS
+    stale = support.copy()
+    stale[np.argwhere(support)[0][0], np.argwhere(support)[0][1]] = False
+    y_stale = MS.rollout_ms(y0, bits, c, lib, M.DT_C3, T, method=method, substeps=sub, support=stale)
+    torch.cuda.synchronize()
+    assert torch.equal(y_stale, y_dense)
