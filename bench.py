@@ -51,7 +51,7 @@ def parse():
                          "overlapped (default); seq: eager launches on one stream; graph: the seq step in a HIP graph")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5", "insite", "f4"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "insite", "f4"],
                     help="c2: BASELINE configs[1], the headline line (default); c3: configs[2], the 5-state fp32 "
                          "system (parity-test configuration, measured separately)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
@@ -457,10 +457,122 @@ def f4_main(args):
     print(json.dumps(res))
 
 
+def c4_main(args):
+    """Configuration C4 (BASELINE.json configs[3]): PK/PD EQ_4_C, 1M patients, heterogeneous per-patient
+    coefficients.  One step = global discovery (Gram [-> RCCL all-reduce of G|b when N > 1] -> STLSQ),
+    per-patient STLSQ from the global support (LSQIntialMask, pkpd_simulation.py:791-800; moments pass +
+    one fit per patient), then the per-patient-coefficient Euler-5 counterfactual rollout
+    (predict_with_reduced_coefs, sindy.py:767-778).  Patients shard contiguously over ranks
+    (N_total / world per rank: strong scaling, as configs[3] fixes 1M patients on 8 GPUs)."""
+    from insite_amd import ops, cohort
+    from insite_amd import dist as idist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = 0 if os.environ.get("INSITE_REHEARSE_ONE_GPU") else int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        backend = os.environ.get("INSITE_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
+    N_total = args.patients if args.patients != 100_000 else 1_000_000
+    T = args.T if args.T != 200 else 60
+    lo, hi = idist.shard_bounds(N_total, rank, world)
+    N = hi - lo
+    coh = cohort.synthetic_pkpd(N, T, seed=args.seed * 1000 + 3 + rank, device=dev, equation="EQ_4_C", layout="time")
+    arm_cf = cohort.counterfactual_arms(coh.arm, T, seed=args.seed * 1000 + 3 + rank, layout="time_bits")
+    lib, F = coh.lib, coh.lib.n_terms
+    buf = idist.MomentBuffer(2, F, dev)
+    gout = (torch.empty((2, F), dtype=torch.float64, device=dev), torch.empty((2, F), dtype=torch.int8, device=dev),
+            torch.empty((2,), dtype=torch.int32, device=dev))
+    pout = (torch.empty((N, 2, F), dtype=torch.float64, device=dev), torch.empty((N, F), dtype=torch.int8, device=dev),
+            torch.empty((N,), dtype=torch.int32, device=dev))
+    y = torch.empty((T, N), dtype=torch.float64, device=dev)
+    ws, wsp = ops.Workspace(), ops.Workspace()
+
+    def step():
+        idist.discover_sharded(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, buf, workspace=ws, out=gout,
+                               layout="time")
+        ops.sindy_fit_per_patient(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, gout[0], 0.1, 0.5, workspace=wsp,
+                                  out=pout, layout="time")
+        ops.rollout(coh.y0, coh.u, arm_cf, pout[0], lib, coh.dt, method="euler5", T=T, out=y, layout="time_bits")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = idist.max_over_ranks(time.perf_counter() - t0, dev)
+    ms_step = el / args.steps * 1e3
+    st = torch.cuda.current_stream(dev)
+
+    def timed(fn, n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(n):
+            fn()
+        e1.record(st)
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / n
+
+    n_roof = max(args.steps, 5)
+    pp_ms = timed(lambda: ops.sindy_fit_per_patient(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, gout[0], 0.1, 0.5,
+                                                    workspace=wsp, out=pout, layout="time"), n_roof)
+    roll_ms = timed(lambda: ops.rollout(coh.y0, coh.u, arm_cf, pout[0], lib, coh.dt, method="euler5", T=T, out=y,
+                                        layout="time_bits"), n_roof)
+    it = pout[2].to(torch.float64)
+    if rank == 0:
+        rb = rollout_bytes(N, T, arm_bits=1) + N * 2 * F * 8          # + the per-patient coefficient rows
+        pb = N * T * 8 + N * (2 * 8 + 1 + 4) + N * (2 * F * 8 + F + 4)  # x + statics/arm/rows + coef/mask/iters out
+        res = {
+            "metric": METRIC, "value": N_total / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: on-device EQ_4_C PK/PD cohort (reference distributions, Euler-5 truth + 0.01 noise)",
+            "config": {"workload": f"C4: PK/PD {N_total // 1000}k patients x {T} steps: global discovery "
+                                   f"(+ RCCL all-reduce when N>1) + per-patient STLSQ + per-patient-coefficient "
+                                   f"Euler-5 rollout", "patients_total": N_total, "patients_per_gpu": N, "T": T,
+                       "parallelism": f"patient-shard x{world}",
+                       "global_support": (gout[1].cpu().numpy() != 0).astype(int).tolist(),
+                       "mean_per_patient_iterations": float(it.mean())},
+            "roofline": {"kernel": "rollout_tm_kernel (euler5, per-patient coef, bit arms)", "bound": "hbm",
+                         "achieved": rb / (roll_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": rb / (roll_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": None,
+                         "algorithmic_bytes_per_launch": rb, "avg_launch_ms": roll_ms},
+            "per_patient_fit": {"kernels": "gram_kernel<MOM> + patient_fit_kernel<7>", "avg_ms": pp_ms,
+                                "algorithmic_bytes": pb, "achieved_GBps": pb / (pp_ms * 1e-3) / 1e9},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, ROOT)
+            from oracle import insite_ref as R
+            n_s = min(100_000, N)                      # ~5 s of one host core
+            xs = coh.x[:T, :n_s].T.contiguous().cpu().numpy()
+            us, ar, rw = coh.u[:n_s].cpu().numpy(), coh.arm[:n_s].cpu().numpy(), coh.rows[:n_s].cpu().numpy()
+            gc = gout[0].cpu().numpy()
+            t1 = time.perf_counter()
+            R.per_patient_fit(xs, us, ar, rw, coh.dt, lib.exps.astype(np.int64), gc, 0.1, 0.5)
+            el1 = time.perf_counter() - t1
+            res["cpu_baseline"] = {"value": n_s / el1, "unit": "patients/s (per-patient STLSQ only)", "cores": 1,
+                                   "kind": "port", "sample": f"oracle/insite_ref.per_patient_fit (row-form pysindy-style "
+                                                            f"STLSQ per patient) on {n_s} patients, {el1:.2f} s"}
+        print(json.dumps(res))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.config == "f4":
         return f4_main(args)
+    if args.config == "c4":
+        return c4_main(args)
     if args.config == "insite":
         return insite_main(args)
     if args.config == "c3":
