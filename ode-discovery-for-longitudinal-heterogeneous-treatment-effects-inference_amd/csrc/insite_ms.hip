@@ -5,10 +5,10 @@
 //   gram_ms_kernel     fused savgol(5,3) smoothing + FD4 derivatives of S states + degree-2 polynomial
 //                      library over (x_1..x_S, a) + the Gram Y^T Z, Y = Theta, Z = [Theta | xdot], on
 //                      v_mfma_f64_16x16x4f64.  Lane = patient; every step the wave stages its 64 library
-//                      rows [Theta | xdot] (<= 32 doubles each) in LDS and issues 16 x 3 MFMAs (tiles
-//                      Y0^T Z0, Y0^T Z1, Y1^T Z1 of the 32 x 32 padded product; the Y1^T Z0 tile is the
-//                      transpose of part of Y0^T Z1).  Interior rows stream through compile-time register
-//                      rings; the 4 + 4 edge rows per patient use the one-sided stencils from directly
+//                      rows [Theta | xdot] (<= 32 doubles each) in LDS and issues 16 x 2 or 3 MFMAs (tiles
+//                      Y0^T Z0, Y0^T Z1 of the 32 x 32 padded product; the Y1^T Z0 tile is the
+//                      transpose of part of Y0^T Z1) and, for F > 16, the Y1^T Z1 tile (MsTail).
+//                      Interior rows stream through compile-time register rings; the 4 + 4 edge rows per patient use the one-sided stencils from directly
 //                      loaded end windows.  Replaces pysindy SmoothedFiniteDifference + PolynomialLibrary
 //                      + X^T X (reference sindy.py:186-192) generalised to S states.
 //   ms_finalize        fixed-order reduction of the per-block tile partials -> G [F, F], B [F, S].
@@ -69,14 +69,36 @@ __device__ __forceinline__ double input_bit(const uint32_t* __restrict__ abits, 
   return (double)((abits[(int64_t)k * lda + (p >> 5)] >> (p & 31)) & 1u);
 }
 
-// Stage this lane's library row into LDS and run the 16 x 3 MFMAs over the wave's 64 rows.
+// Rows 16.. of Y (F1 = F - 16 library columns) against [Theta_16.. | xdot]: on the VALU, one fp64 FMA
+// per upper-triangle entry and per (column, state) pair into per-lane accumulators, when there are at
+// most INSITE_MS_VALU_TAIL of them.  The 16 x 16 MFMA tile it replaces has 16 - F1 padding rows
+// (F = 22: 10 of 16; F <= 16: all of them).  Default 0: only the all-padding tile (F <= 16) is dropped.
+// Measured at F = 22 (C3, 1M x 500): the 51 accumulators (102 VGPRs) push the occupancy-2 kernel into
+// scratch spills, 15.5 -> 33.2 ms; at occupancy 1 it is 15.8 ms (tile on MFMA at occupancy 1: 18.7 ms).
+#ifndef INSITE_MS_VALU_TAIL
+#define INSITE_MS_VALU_TAIL 0
+#endif
+#ifndef INSITE_MS_WPE
+#define INSITE_MS_WPE 2
+#endif
+template <int S, int F>
+struct MsTail {
+  static constexpr int F1 = F > 16 ? F - 16 : 0;
+  static constexpr int NACC = F1 * (F1 + 1) / 2 + F1 * S;
+  static constexpr bool kValu = NACC <= INSITE_MS_VALU_TAIL;
+  static constexpr int NA = NACC > 0 ? NACC : 1;
+};
+
+// Stage this lane's library row into LDS and run the 16 x 2 (+ 16) MFMAs over the wave's 64 rows.
 // Row layout: [Theta_0..Theta_{F-1}, xdot_0..xdot_{S-1}, 0 ...] (32 doubles).  A[m][k] = Y_m of row
 // 4g + k (m = lane & 15, k = lane >> 4); B[k][n] = Z_n of the same row; C[(lane>>4) + 4j][lane & 15].
+// With MsTail::kValu the Y1^T Z1 tile is accumulated per lane in acc (see MsTail) instead.
 template <int S, int F>
 __device__ __forceinline__ void ms_emit(double* __restrict__ wrow, const double* __restrict__ wbase, bool valid,
                                         const double (&th)[F], const double (&xd)[S], dbl4& c00, dbl4& c01,
-                                        dbl4& c11, int lane) {
+                                        dbl4& c11, double (&acc)[MsTail<S, F>::NA], int lane) {
   static_assert(F + S <= kMsMaxF, "Theta + xdot must fit two 16-column tiles");
+  using Tail = MsTail<S, F>;
   wave_lds_sync();  // every lane finished reading the previous rows
 #pragma unroll
   for (int j = 0; j < kMsMaxF; ++j) {
@@ -86,6 +108,19 @@ __device__ __forceinline__ void ms_emit(double* __restrict__ wrow, const double*
     wrow[j] = valid ? v : 0.0;
   }
   wave_lds_sync();
+  if constexpr (Tail::kValu && Tail::F1 > 0) {
+    double y1[Tail::F1];
+#pragma unroll
+    for (int i = 0; i < Tail::F1; ++i) y1[i] = valid ? th[16 + i] : 0.0;
+    int q = 0;
+#pragma unroll
+    for (int i = 0; i < Tail::F1; ++i) {
+#pragma unroll
+      for (int j = i; j < Tail::F1; ++j, ++q) acc[q] = fma(y1[i], th[16 + j], acc[q]);
+#pragma unroll
+      for (int s = 0; s < S; ++s, ++q) acc[q] = fma(y1[i], xd[s], acc[q]);
+    }
+  }
   const int m = lane & 15, k = lane >> 4;
   const bool y1ok = 16 + m < F;
 #pragma unroll
@@ -93,10 +128,12 @@ __device__ __forceinline__ void ms_emit(double* __restrict__ wrow, const double*
     const double* src = wbase + (4 * g + k) * kMsRowStride;
     const double y0 = src[m];
     const double z1 = src[16 + m];
-    const double y1 = y1ok ? z1 : 0.0;
     c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(y0, y0, c00, 0, 0, 0);
     c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(y0, z1, c01, 0, 0, 0);
-    c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(y1, z1, c11, 0, 0, 0);
+    if constexpr (!Tail::kValu) {
+      const double y1 = y1ok ? z1 : 0.0;
+      c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(y1, z1, c11, 0, 0, 0);
+    }
   }
 }
 
@@ -130,7 +167,7 @@ __device__ __forceinline__ void ms_small(const double (&xv)[8], const GramW& w, 
 //     just consumed), smoothed ring sr[8][S] (fp64); row r leaves at step t = r + 4
 //   edge rows 0..3 and L-4..L-1 (all rows when L < 8): one-sided stencils from end windows
 template <int S, int NIN, bool INTER>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_MS_WPE)))
 gram_ms_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint32_t* __restrict__ abits,
                int64_t lda, const int32_t* __restrict__ rows, int64_t N, GramW w, double* __restrict__ partial) {
   constexpr int NZ = S + NIN;
@@ -141,6 +178,10 @@ gram_ms_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint
   double* wbase = stage + wid * kWave * kMsRowStride;
   double* wrow = wbase + lane * kMsRowStride;
   dbl4 c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00, c11 = c00;
+  using Tail = MsTail<S, F>;
+  double acc[Tail::NA];
+#pragma unroll
+  for (int q = 0; q < Tail::NA; ++q) acc[q] = 0.0;
   const int64_t n_tiles = (N + kWave - 1) / kWave;
   const int64_t sstride = ldx;              // between states of one step
   const int64_t kstride = (int64_t)S * ldx; // between steps
@@ -202,7 +243,7 @@ gram_ms_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint
               for (int q = 0; q < NIN; ++q) z[1 + S + q] = (double)((wcur >> (r & 31)) & 1u);
               double th[F];
               poly_row<NZ, INTER>(z, th);
-              ms_emit<S, F>(wrow, wbase, t <= L - 1, th, xd, c00, c01, c11, lane);
+              ms_emit<S, F>(wrow, wbase, t <= L - 1, th, xd, c00, c01, c11, acc, lane);
             }
             // x[t + 4] is loaded straight into the slot x[t - 4] occupied (read above): the wait
             // for it falls 4 steps later, at its first use
@@ -285,7 +326,7 @@ gram_ms_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint
           for (int qq = 0; qq < NIN; ++qq) z[1 + S + qq] = (L > 0 && step < n_steps) ? input_bit(abits, lda, step, pc) : 0.0;
           double th[F];
           poly_row<NZ, INTER>(z, th);
-          ms_emit<S, F>(wrow, wbase, L > 0 && valid, th, xd, c00, c01, c11, lane);
+          ms_emit<S, F>(wrow, wbase, L > 0 && valid, th, xd, c00, c01, c11, acc, lane);
         }
       }
     }
@@ -300,6 +341,26 @@ gram_ms_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint
     red[(wid * kMsTiles + 0) * 256 + e] = c00[j];
     red[(wid * kMsTiles + 1) * 256 + e] = c01[j];
     red[(wid * kMsTiles + 2) * 256 + e] = c11[j];
+  }
+  if constexpr (Tail::kValu && Tail::F1 > 0) {
+    // wave sums of the VALU tail into tile 2 ([row - 16][col - 16], both triangles), fixed order
+    wave_lds_sync();  // after this wave's (zero) c11 writes
+    double* t2 = red + (wid * kMsTiles + 2) * 256;
+    int q = 0;
+#pragma unroll
+    for (int i = 0; i < Tail::F1; ++i) {
+#pragma unroll
+      for (int j = i; j < Tail::F1 + S; ++j, ++q) {
+        double v = acc[q];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+        if (lane == 0) {
+          const int c = j < Tail::F1 ? j : F - 16 + (j - Tail::F1);
+          t2[i * 16 + c] = v;
+          if (j < Tail::F1) t2[j * 16 + i] = v;
+        }
+      }
+    }
   }
   __syncthreads();
   for (int q = threadIdx.x; q < kMsTiles * 256; q += kBlock) {

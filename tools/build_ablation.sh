@@ -4,7 +4,7 @@ set -e
 R="$(cd "$(dirname "$0")/.." && pwd)"
 P="$R/ode-discovery-for-longitudinal-heterogeneous-treatment-effects-inference_amd"
 rm -rf "$P/lib/ablate"; mkdir -p "$P/lib/ablate"
-build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC "$@" -I "$R/include" -o "$P/lib/ablate/libinsite_hip_$NAME.so" "$P/csrc/insite_hip.hip" "$P/csrc/insite_ms.hip" & }
+build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC "$@" -I "$R/include" -o "$P/lib/ablate/libinsite_hip_$NAME.so" "$P/csrc/insite_hip.hip" "$P/csrc/insite_ms.hip" -lhiprtc & }
 for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
   case $v in
     NOSTORE) NAME=$v build -DINSITE_ABLATE_NOSTORE ;;
@@ -13,6 +13,9 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     SEGKC16) NAME=$v build -DINSITE_SEG_KC=16 -DINSITE_SEG_WPE=2 ;;
     SEGNOPF) NAME=$v build -DINSITE_SEG_PF=0 -DINSITE_SEG_WPE=4 ;;
     SEGKC16NOPF) NAME=$v build -DINSITE_SEG_KC=16 -DINSITE_SEG_PF=0 -DINSITE_SEG_WPE=3 ;;
+    MSTAIL64) NAME=$v build -DINSITE_MS_VALU_TAIL=64 ;;
+    MSTAIL64WPE1) NAME=$v build -DINSITE_MS_VALU_TAIL=64 -DINSITE_MS_WPE=1 ;;
+    MSWPE1) NAME=$v build -DINSITE_MS_WPE=1 ;;
     NOARM) NAME=$v build -DINSITE_ABLATE_NOARM ;;
     TIMING) NAME=$v build -DINSITE_TIMING ;;
     LATE) NAME=$v build -DINSITE_GRAM_LATE_ISSUE ;;
