@@ -229,7 +229,7 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
  * of its (refined or global) model over all T steps.
  *   V        [T, ld_v] f64 unscaled observations, time-major (ld_v >= n_rows)
  *   arm_bits TIME_MAJOR_BITS [T, ld_arm] per-step arm (n_arms <= 2)
- *   coef0    HOST [n_arms, F] f64: the global model (at most 8 active coefficients)
+ *   coef0    HOST [n_arms, F] f64: the global model (at most 16 active coefficients)
  *   preds    [T, ld_p] f64 (row k = state after step k); coef_out [n_rows, n_arms, F] (may be NULL);
  *   status_out [n_rows] int32 (-1 = not refined: seq_len <= tau; else the BFGS status: 0 converged,
  *   1 maxiter, 3 zoom failed, 5 line-search maxiter), iters_out [n_rows] int32 (may be NULL). */
@@ -238,6 +238,16 @@ int32_t insite_refine_f64(const double* V, int64_t ld_v, int32_t T, const uint32
                           int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam, int32_t tau,
                           int32_t substeps, double* preds, int64_t ld_p, double* coef_out, int32_t* status_out,
                           int32_t* iters_out, void* stream);
+
+/* INSITE refinement with int8 per-step arms, n_arms <= 4: the cancer_sim / EQ_5 branches of
+ * _get_fine_tuned_predictions (sindy.py:484-550: pred_dy_dt picks all_reduced_coefs[argmax(treatment)])
+ * with the same objective, BFGS and outputs as insite_refine_f64.
+ *   arm [T, ld_arm] int8 time-major per-step arm in [0, n_arms) (ld_arm >= n_rows); the rest as above. */
+int32_t insite_refine_arms_f64(const double* V, int64_t ld_v, int32_t T, const int8_t* arm, int64_t ld_arm,
+                               const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
+                               const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt,
+                               double lam, int32_t tau, int32_t substeps, double* preds, int64_t ld_p,
+                               double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream);
 
 /* Masked squared-error sums for the RMSE metrics (time_varying_model.py:236-313):
  *   err[r,k]  = (pred[r, k] * scale + shift - target[r, k])^2 * active[r, k]

@@ -1818,14 +1818,16 @@ __global__ void __launch_bounds__(kBlock) rollout_rk45_kernel(Rk45Args ra, LibDe
 //   mse  = mean over k < min(sl - tau, T - 1) of (V[k+1] - pred_k)^2, pred = Euler-5 scan from V[0],
 // minimised by jax.scipy.optimize.minimize(method='BFGS') restated (oracle docstring): BFGS with the
 // inverse-Hessian update, strong-Wolfe line search, cubic/quadratic/bisection zoom.  The objective
-// depends on c only through (alpha_a, beta_a) of the state-affine RHS, so one forward pass with four
-// tangents d y / d(alpha_0, beta_0, alpha_1, beta_1) gives f and the exact gradient (what jax's
-// autodiff computes).  Only the m active coefficients move (the search runs in that subspace; oracle
+// depends on c only through (alpha_a, beta_a) of the state-affine RHS, so one forward pass with 2 NA
+// tangents d y / d(alpha_a, beta_a) gives f and the exact gradient (what jax's autodiff computes).
+// NA = 2: TIME_MAJOR_BITS arms (PK/PD EQ_4); NA = 4: int8 arms, the 4-valued treatment of cancer_sim /
+// EQ_5 (sindy.py:484-550, argmax(treatment) selects the arm's coefficients).  Only the m active coefficients move (the search runs in that subspace; oracle
 // docstring); every lane runs its own optimiser — lanes finishing early idle until the wave's last.
-constexpr int kRefineMaxActive = 8;
+constexpr int kRefineMaxActive = 16;
 struct RefineArgs {
   const double* V;      // [T, ldv] unscaled observations (time-major)
-  const uint32_t* arm;  // TIME_MAJOR_BITS [T, lda] per-step arm
+  const uint32_t* arm;  // TIME_MAJOR_BITS [T, lda] per-step arm (NA = 2)
+  const int8_t* arm8;   // [T, lda] int8 per-step arm (NA = 4)
   const double* u;      // [N, U]
   const int32_t* sl;    // [N] sequence lengths
   double* preds;        // [T, ldp]
@@ -1839,7 +1841,7 @@ struct RefineArgs {
   double c0[INSITE_MAX_ARMS * INSITE_MAX_TERMS];  // the global model [A, F]
 };
 
-template <int M>
+template <int M, int NA>
 struct RefineLane {
   const RefineArgs& ra;
   const LibDesc& lib;
@@ -1849,49 +1851,60 @@ struct RefineLane {
   double mono[M];
   double c0a[M];
   __device__ int armbit(int k) const {
-    return (int)((ra.arm[(int64_t)k * ra.lda + (p >> 5)] >> (p & 31)) & 1u);
+    if constexpr (NA == 2) return (int)((ra.arm[(int64_t)k * ra.lda + (p >> 5)] >> (p & 31)) & 1u);
+    else return (int)ra.arm8[(int64_t)k * ra.lda + p];
   }
   // f and gradient at c (active coordinates)
   __device__ double fg(const double (&c)[M], double (&g)[M]) const {
-    double al0 = 0.0, al1 = 0.0, be0 = 0.0, be1 = 0.0;
+    double al[NA], be[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) al[a] = be[a] = 0.0;
 #pragma unroll
     for (int i = 0; i < M; ++i) {
       if (i >= ra.m) break;
       const double t = c[i] * mono[i];
-      if (ra.t_ex[i] == 0) {
-        if (ra.t_arm[i] == 0) al0 += t; else al1 += t;
-      } else {
-        if (ra.t_arm[i] == 0) be0 += t; else be1 += t;
-      }
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+        if (ra.t_arm[i] == a) {
+          if (ra.t_ex[i] == 0) al[a] += t;
+          else be[a] += t;
+        }
     }
     const double h = ra.dt / (double)ra.sub;
     double y = ra.V[p];
-    double da0 = 0.0, da1 = 0.0, db0 = 0.0, db1 = 0.0;
-    double L = 0.0, gA0 = 0.0, gA1 = 0.0, gB0 = 0.0, gB1 = 0.0;
+    double da[NA], db[NA], gA[NA], gB[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) da[a] = db[a] = gA[a] = gB[a] = 0.0;
+    double L = 0.0;
     for (int k = 0; k < K; ++k) {
-      const int a = armbit(k);
-      const double al = a ? al1 : al0, be = a ? be1 : be0;
-      const double hb = h * be;
-      for (int s = 0; s < ra.sub; ++s) {
-        da0 = da0 + hb * da0;
-        da1 = da1 + hb * da1;
-        db0 = db0 + hb * db0;
-        db1 = db1 + hb * db1;
-        if (a) {
-          da1 += h;
-          db1 += h * y;
-        } else {
-          da0 += h;
-          db0 += h * y;
+      const int ak = armbit(k);
+      double alk = al[0], bek = be[0];
+#pragma unroll
+      for (int a = 1; a < NA; ++a)
+        if (ak == a) {
+          alk = al[a];
+          bek = be[a];
         }
-        y = y + h * (al + be * y);
+      const double hb = h * bek;
+      for (int s = 0; s < ra.sub; ++s) {
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+          da[a] = da[a] + hb * da[a];
+          db[a] = db[a] + hb * db[a];
+          if (ak == a) {
+            da[a] += h;
+            db[a] += h * y;
+          }
+        }
+        y = y + h * (alk + bek * y);
       }
       const double r = ra.V[(int64_t)(k + 1) * ra.ldv + p] - y;
       L += r * r;
-      gA0 += -2.0 * r * da0;
-      gA1 += -2.0 * r * da1;
-      gB0 += -2.0 * r * db0;
-      gB1 += -2.0 * r * db1;
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        gA[a] += -2.0 * r * da[a];
+        gB[a] += -2.0 * r * db[a];
+      }
     }
     const double iK = 1.0 / (double)K;
     L *= iK;
@@ -1904,7 +1917,10 @@ struct RefineLane {
       }
       const double d = c0a[i] - c[i];
       pen += d * d;
-      const double gd = ra.t_ex[i] == 0 ? (ra.t_arm[i] ? gA1 : gA0) : (ra.t_arm[i] ? gB1 : gB0);
+      double gd = 0.0;
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+        if (ra.t_arm[i] == a) gd = ra.t_ex[i] == 0 ? gA[a] : gB[a];
       g[i] = gd * iK * mono[i] / norm + 2.0 * ra.lam * (c[i] - c0a[i]) / (double)ra.n_total;
     }
     return L / norm + ra.lam * pen / (double)ra.n_total;
@@ -1940,14 +1956,14 @@ __device__ __forceinline__ double quadmin(double a, double fa, double fpa, doubl
   return a - fpa / (2.0 * B);
 }
 
-template <int M>
+template <int M, int NA>
 __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, LibDesc lib) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ra.N) return;
   double uu[INSITE_MAX_STATICS];
 #pragma unroll
   for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < lib.U ? ra.u[p * lib.U + t] : 0.0;
-  RefineLane<M> ln{ra, lib, p, 0, 1.0, {}, {}};
+  RefineLane<M, NA> ln{ra, lib, p, 0, 1.0, {}, {}};
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     ln.mono[i] = i < ra.m ? monomial(lib, ra.t_col[i], uu) : 0.0;
@@ -2158,8 +2174,10 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
 #pragma unroll
   for (int i = 0; i < M; ++i)
     if (i < ra.m) cf[ra.t_flat[i]] = x[i];
-  double al[2] = {0.0, 0.0}, be[2] = {0.0, 0.0};
-  for (int a = 0; a < ra.A && a < 2; ++a)
+  double al[NA], be[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) al[a] = be[a] = 0.0;
+  for (int a = 0; a < ra.A && a < NA; ++a)
     for (int j = 0; j < lib.F; ++j) {
       const double t = cf[a * lib.F + j] * monomial(lib, j, uu);
       if (lib.ex[j] == 0) al[a] += t;
@@ -2168,8 +2186,15 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
   const double h = ra.dt / (double)ra.sub;
   double y = ra.V[p];
   for (int k = 0; k < ra.T; ++k) {
-    const int a = ln.armbit(k);
-    for (int s = 0; s < ra.sub; ++s) y = y + h * (al[a] + be[a] * y);
+    const int ak = ln.armbit(k);
+    double alk = al[0], bek = be[0];
+#pragma unroll
+    for (int a = 1; a < NA; ++a)
+      if (ak == a) {
+        alk = al[a];
+        bek = be[a];
+      }
+    for (int s = 0; s < ra.sub; ++s) y = y + h * (alk + bek * y);
     ra.preds[(int64_t)k * ra.ldp + p] = y;
   }
   if (ra.coef_out)
@@ -2996,22 +3021,28 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
   return launch_status();
 }
 
-int32_t insite_refine_f64(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, int64_t ld_arm,
-                          const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics, const int8_t* exps,
-                          int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam, int32_t tau,
-                          int32_t substeps, double* preds, int64_t ld_p, double* coef_out, int32_t* status_out,
-                          int32_t* iters_out, void* stream) {
-  if (n_rows < 0 || T < 1 || n_arms < 1 || n_arms > 2 || substeps < 1 || !(dt > 0.0) || !(lam >= 0.0) || tau < 0 ||
-      ld_v < n_rows || ld_p < n_rows || ld_arm < (n_rows + 31) / 32 || !coef0)
+namespace {
+// Shared argument checks and launch of insite_refine_f64 (NA = 2, bit arms) and
+// insite_refine_arms_f64 (NA = 4, int8 arms).
+int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, const int8_t* arm8,
+                      int64_t ld_arm, const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
+                      const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam,
+                      int32_t tau, int32_t substeps, double* preds, int64_t ld_p, double* coef_out,
+                      int32_t* status_out, int32_t* iters_out, void* stream) {
+  const bool bits = arm8 == nullptr;
+  if (n_rows < 0 || T < 1 || n_arms < 1 || n_arms > (bits ? 2 : 4) || substeps < 1 || !(dt > 0.0) ||
+      !(lam >= 0.0) || tau < 0 || ld_v < n_rows || ld_p < n_rows ||
+      ld_arm < (bits ? (n_rows + 31) / 32 : n_rows) || !coef0)
     return INSITE_E_INVALID_ARG;
   LibDesc lib;
   int32_t st = build_lib(exps, n_terms, n_statics, &lib);
   if (st != INSITE_OK) return st;
   if (n_rows == 0) return INSITE_OK;
-  if (!V || !arm_bits || !seq_len || !preds || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
+  if (!V || (bits && !arm_bits) || !seq_len || !preds || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
   RefineArgs ra{};
   ra.V = V;
   ra.arm = arm_bits;
+  ra.arm8 = arm8;
   ra.u = n_statics > 0 ? u : V;
   ra.sl = seq_len;
   ra.preds = preds;
@@ -3046,9 +3077,39 @@ int32_t insite_refine_f64(const double* V, int64_t ld_v, int32_t T, const uint32
   ra.m = m;
   const dim3 grid((unsigned)((n_rows + kBlock - 1) / kBlock));
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
-  if (m <= 4) insite_refine_kernel<4><<<grid, kBlock, 0, hs>>>(ra, lib);
-  else insite_refine_kernel<8><<<grid, kBlock, 0, hs>>>(ra, lib);
+  if (bits) {
+    if (m <= 4) insite_refine_kernel<4, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else if (m <= 8) insite_refine_kernel<8, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else insite_refine_kernel<16, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
+  } else {
+    if (m <= 4) insite_refine_kernel<4, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else if (m <= 8) insite_refine_kernel<8, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else insite_refine_kernel<16, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
+  }
   return launch_status();
+}
+}  // namespace
+
+int32_t insite_refine_f64(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, int64_t ld_arm,
+                          const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics, const int8_t* exps,
+                          int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam, int32_t tau,
+                          int32_t substeps, double* preds, int64_t ld_p, double* coef_out, int32_t* status_out,
+                          int32_t* iters_out, void* stream) {
+  if (!arm_bits && n_rows > 0) return INSITE_E_INVALID_ARG;
+  return refine_launch(V, ld_v, T, arm_bits, nullptr, ld_arm, u, seq_len, n_rows, n_statics, exps, n_terms, coef0,
+                       n_arms, dt, lam, tau, substeps, preds, ld_p, coef_out, status_out, iters_out, stream);
+}
+
+int32_t insite_refine_arms_f64(const double* V, int64_t ld_v, int32_t T, const int8_t* arm, int64_t ld_arm,
+                               const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
+                               const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt,
+                               double lam, int32_t tau, int32_t substeps, double* preds, int64_t ld_p,
+                               double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream) {
+  if (!arm && n_rows > 0) return INSITE_E_INVALID_ARG;
+  static const int8_t kNoArms = 0;  // non-null marker for the int8 format when n_rows == 0
+  return refine_launch(V, ld_v, T, nullptr, arm ? arm : &kNoArms, ld_arm, u, seq_len, n_rows, n_statics, exps,
+                       n_terms, coef0, n_arms, dt, lam, tau, substeps, preds, ld_p, coef_out, status_out, iters_out,
+                       stream);
 }
 
 size_t insite_masked_sse_workspace_bytes(int64_t n_rows, int32_t T) {

@@ -45,6 +45,7 @@ EXPORTS = (
     "insite_rollout_f64",
     "insite_rollout_rk45_f64",
     "insite_refine_f64",
+    "insite_refine_arms_f64",
     "insite_masked_sse_workspace_bytes",
     "insite_masked_sse_f64",
     "insite_gram_ms_workspace_bytes",
@@ -98,6 +99,8 @@ _SIGNATURES = {
                                          _c_i32, _c_i32, _c_i32, _c_f64, _c_f64, _c_f64, _vp, _c_i64, _vp, _vp]),
     "insite_refine_f64": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _c_i64, _vp, _vp, _c_i64, _c_i32, _vp, _c_i32, _vp,
                                    _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _c_i64, _vp, _vp, _vp, _vp]),
+    "insite_refine_arms_f64": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _c_i64, _vp, _vp, _c_i64, _c_i32, _vp, _c_i32,
+                                        _vp, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _c_i64, _vp, _vp, _vp, _vp]),
     "insite_masked_sse_workspace_bytes": (_c_size, [_c_i64, _c_i32]),
     "insite_masked_sse_f64": (_c_i32, [_vp, _c_i64, _c_f64, _c_f64, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _vp,
                                        _vp, _c_size, _vp]),

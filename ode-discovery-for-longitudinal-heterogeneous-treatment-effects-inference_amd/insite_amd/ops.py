@@ -476,10 +476,11 @@ def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_ob
 
 def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: torch.Tensor, coef0: np.ndarray,
                   lib: PolyLibrary, dt: float, lam: float, tau: int, substeps: int = 5):
-    """INSITE per-patient refinement (insite_refine_f64; reference sindy.py:433-715).  V [N, T] f64
-    unscaled observations and arm [N, T] int8 per-step arms in the reference's patient-major layout
-    (transposed to the kernel's time-major layout here), u [N, U], seq_len [N], coef0 the HOST global
-    model [A, F].  Returns (preds [N, T], coef [N, A, F], status [N], iterations [N])."""
+    """INSITE per-patient refinement (reference sindy.py:433-715).  V [N, T] f64 unscaled observations
+    and arm [N, T] int8 per-step arms in the reference's patient-major layout (transposed to the
+    kernel's time-major layout here), u [N, U], seq_len [N], coef0 the HOST global model [A, F].
+    A <= 2: insite_refine_f64 on bit-packed arms; A <= 4 (cancer_sim / EQ_5): insite_refine_arms_f64
+    on int8 arms.  Returns (preds [N, T], coef [N, A, F], status [N], iterations [N])."""
     _dev("V", V, torch.float64, 2)
     _dev("arm", arm, torch.int8, 2)
     N, T = V.shape
@@ -494,19 +495,25 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
     if c0.ndim != 2 or c0.shape[1] != lib.n_terms:
         raise ValueError("coef0 must be a host [A, F] array")
     A = c0.shape[0]
+    if A > 4:
+        raise ValueError("at most 4 treatment arms")
     Vt = V.t().contiguous()
-    bits = pack_arm_bits(arm.t().contiguous(), N)
+    arm_t = arm.t().contiguous()
+    if A <= 2:
+        name, arms = "insite_refine_f64", pack_arm_bits(arm_t, N)
+    else:
+        name, arms = "insite_refine_arms_f64", arm_t
     dev = V.device
     preds = torch.empty((T, N), dtype=torch.float64, device=dev)
     coef = torch.empty((N, A, lib.n_terms), dtype=torch.float64, device=dev)
     status = torch.empty((N,), dtype=torch.int32, device=dev)
     iters = torch.empty((N,), dtype=torch.int32, device=dev)
     tab = lib.ctypes_table()
-    args = (_p(Vt), Vt.stride(0), T, _p(bits), bits.stride(0), _p(u) if lib.n_statics else ctypes.c_void_p(0),
+    args = (_p(Vt), Vt.stride(0), T, _p(arms), arms.stride(0), _p(u) if lib.n_statics else ctypes.c_void_p(0),
             _p(seq_len), N, lib.n_statics, tab.ctypes.data_as(ctypes.c_void_p), lib.n_terms,
             c0.ctypes.data_as(ctypes.c_void_p), A, float(dt), float(lam), int(tau), int(substeps), _p(preds),
             preds.stride(0), _p(coef), _p(status), _p(iters))
-    _run(("insite_refine_f64", args, dev, None))
+    _run((name, args, dev, None))
     return preds.t(), coef, status, iters
 
 

@@ -14,14 +14,15 @@ through the C ABI (include/insite_hip.h):
   kernel, then the reduction fused with STLSQ + unbias for every arm.
 * ``jit(vmap(simulate_cancer_volume))`` (sindy.py:413-431) -> ``insite_rollout_f64`` (Euler-5).
 * ``insite: true`` — ``pmap(vmap(simulate_cancer_volume_with_fine_tuning))`` (sindy.py:433-715): the
-  per-patient BFGS refinement -> ``insite_refine_f64`` (one lane per patient).
+  per-patient BFGS refinement -> ``insite_refine_f64`` (one lane per patient; 4-arm datasets:
+  ``insite_refine_arms_f64``).
 
 The DE-format extraction (A1, pkpd/utils.py:523-606), the tau-step slice (A9) and the masked
 squared-error sums of the metrics (A10) also run on the device; only scalars and the returned
 prediction arrays cross back to the host.  Out of scope in this build (raise
-``NotImplementedError``): weak SINDy, the joint model, the degree-4 ablation library and the
-``insite: true`` on the 4-arm datasets.  The cancer_sim / EQ_5 datasets run the
-treatment-segment discovery (``insite_sindy_fit_segments_f64``) and the 4-arm rollout.
+``NotImplementedError``): weak SINDy, the joint model and the degree-4 ablation library.  The
+cancer_sim / EQ_5 datasets run the treatment-segment discovery
+(``insite_sindy_fit_segments_f64``), the 4-arm rollout and, with ``insite: true``, the 4-arm refinement.
 """
 from __future__ import annotations
 
@@ -156,9 +157,6 @@ class SINDY:
         if not (self.segment_mode or "EQ_4" in self.dataset_name.upper()):
             raise NotImplementedError(f"dataset {self.dataset_name!r}: this build covers the PK/PD EQ_4 family and "
                                       "the treatment-segment datasets (cancer_sim, EQ_5_*)")
-        if self.segment_mode and self.insite:
-            raise NotImplementedError("insite: true on the 4-arm cancer_sim / EQ_5 datasets (the refinement kernel "
-                                      "takes bit-packed arms, n_arms <= 2)")
         if self.wsindy:
             raise NotImplementedError("weak SINDy (wsindy: true) is not on the MI355X path")
         if self.joint_model:
@@ -288,6 +286,10 @@ class SINDY:
         prev, stat, std, mean = self._unscaled_inputs(dataset)
         if self.smooth_input_data:      # applied here in the reference (sindy.py:557-560), unlike the DE format
             prev = savgol_5_3_rows(prev)
+        if self.segment_mode and "EQ_5" in self.dataset_name.upper() and stat.shape[1] >= 2:
+            # the reference's EQ_5 refinement binds u1 to static_features[0] (sindy.py:536), unlike its
+            # global-model rollout (sindy.py:302): kept, so refined EQ_5 predictions match the reference
+            stat = stat[:, :1].expand(-1, stat.shape[1]).contiguous()
         arm = torch.as_tensor(np.argmax(d["current_treatments"], axis=-1).astype(np.int8), device=self.device)
         sl = torch.as_tensor(np.asarray(d["sequence_lengths"]).astype(np.int32), device=self.device)
         preds, coef, status, iters = ops.insite_refine(prev.contiguous(), arm.contiguous(), stat, sl, self.joint_coefs,

@@ -33,7 +33,7 @@ def _header_functions():
 def test_header_declares_the_abi():
     fns = _header_functions()
     assert "insite_rollout_f64" in fns and "insite_sindy_fit_f64" in fns
-    assert len(fns) == 22
+    assert len(fns) == 23
 
 
 def test_library_exports_every_header_symbol(L):

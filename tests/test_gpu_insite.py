@@ -116,3 +116,90 @@ def test_log_anchor_insite_vs_sindy_eq4a(dev):
     assert 0.05 < s < 0.3 and i < 0.05 and i < s / 3, (s, i)
     assert res["insite"]["fine_tuned"] is True
     assert all(np.isfinite(res["insite"][f"decoder_test_rmse_{k}-step"]) for k in range(2, 7))
+
+
+def _four_arm_problem(n_statics, n, seed):
+    """A cancer_sim-like (n_statics = 1, F = 4) or EQ_5-like (n_statics = 2, F = 7) 4-arm cohort with
+    per-step arm switches, and a global model off the planted one so the refinement has work to do."""
+    from oracle import segments_ref as S
+    rng = np.random.default_rng(seed)
+    if n_statics == 1:
+        coef = S.TRUE_COEF_U1
+    else:
+        coef = np.zeros((4, 7))
+        coef[:, 1] = [0.2, -0.3, -0.25, 0.1]
+        coef[:, 4] = [-0.4, 0.0, -0.6, -0.2]
+        coef[1:, 5] = [0.3, -0.2, 0.25]
+        coef[::2, 0] = [0.05, -0.05]
+    x, u, arm, _ = S.synthetic_cohort(n, 60, rng, switch_p=0.1, noise=0.01, dt=1 / 6, coef=coef,
+                                      n_statics=n_statics)
+    c0 = coef * (1.0 + rng.normal(0.0, 0.1, size=coef.shape))
+    c0[np.abs(coef) == 0] = 0.0
+    c0[0, -1] = 5e-4                              # below the 1e-3 mask: never refined, kept as is
+    return x[:, :60].copy(), u, arm.astype(np.int8), c0, R.poly_library(1 + n_statics, 2, True)
+
+
+@pytest.mark.parametrize("n_statics,tau", [(1, 1), (1, 5), (2, 5)])
+def test_refine_four_arms_matches_oracle(dev, n_statics, tau):
+    """insite_refine_arms_f64 (int8 arms, NA = 4; sindy.py:484-550) against the oracle per row:
+    cancer_sim (4 x 4 model, 6 active) and EQ_5-like (4 x 7 model, 12 active: the M = 16 kernel)."""
+    from insite_amd import ops
+    from insite_amd.library import polynomial_library
+    V, u, arms, c0, ex = _four_arm_problem(n_statics, 48, 3 + n_statics)
+    N, T = V.shape
+    rng = np.random.default_rng(tau)
+    sl = rng.integers(1, T + 1, N).astype(np.int32)
+    sl[:3] = [tau, tau + 1, T]
+    lib = polynomial_library(n_statics, 2, True)
+    preds, coef, status, iters = ops.insite_refine(torch.tensor(V, device=dev), torch.tensor(arms, device=dev),
+                                                   torch.tensor(u, device=dev), torch.tensor(sl, device=dev), c0, lib,
+                                                   1 / 6, 10.0, tau)
+    torch.cuda.synchronize()
+    preds, coef, status = preds.cpu().numpy(), coef.cpu().numpy(), status.cpu().numpy()
+    for p in range(N):
+        rp, rc, rs, _ = Q.refine_patient(V[p], arms[p], u[p], sl[p], c0, ex, 1 / 6, 10.0, tau)
+        assert status[p] == rs, (p, status[p], rs)
+        assert np.abs(coef[p] - rc).max() <= 1e-7 * max(1.0, np.abs(rc).max()), p
+        assert np.sqrt(np.mean((preds[p] - rp) ** 2)) <= 1e-6
+    assert (coef[:, 0, -1] == c0[0, -1]).all()
+    assert (status[sl <= tau] == -1).all() and (status[sl > tau] == 0).mean() > 0.8
+
+
+def test_refine_four_arms_rejects_more_than_16_active(dev):
+    from insite_amd import ops
+    from insite_amd.library import polynomial_library
+    V, u, arms, _, _ = _four_arm_problem(2, 8, 1)
+    c0 = np.full((4, 7), 0.01)                     # 28 active coefficients
+    with pytest.raises(Exception):
+        ops.insite_refine(torch.tensor(V, device=dev), torch.tensor(arms, device=dev), torch.tensor(u, device=dev),
+                          torch.full((8,), 60, dtype=torch.int32, device=dev), c0, polynomial_library(2, 2, True),
+                          1 / 6, 10.0, 5)
+
+
+@pytest.mark.parametrize("name,n_statics", [("cancer_sim", 1), ("EQ_5_B", 2)])
+def test_plugin_insite_four_arms(dev, name, n_statics):
+    """+backbone=insite on a 4-arm dataset: segment discovery, then per-row refinement; the EQ_5
+    refinement binds u1 to static_features[0] as the reference does (sindy.py:536)."""
+    from insite_amd.sindy import SINDY
+    from test_gpu_segments import _Subset
+    V, u, arms, c0, ex = _four_arm_problem(n_statics, 300, 7)
+    N, T = V.shape
+    x = np.concatenate([V, V[:, -1:]], axis=1)          # [N, T + 1]: prev_outputs = V
+    sl = np.full(N, T, dtype=np.int64)
+    sl[::4] = 3
+    args = {"model": {"dataset_name": name, "dim_treatments": 4, "dim_static_features": n_statics,
+                      "dim_outcomes": 1, "sindy_threshold": 0.001, "sindy_alpha": 0.5, "insite": True,
+                      "lam": 10.0},
+            "dataset": {"projection_horizon": 5}, "exp": {"unscale_rmse": True, "percentage_rmse": True}}
+    m = SINDY(args, device=dev)
+    ds = _Subset(x, u, arms, sl)
+    m.fit(ds)
+    assert m.joint_coefs.shape == (4, ex.shape[0])
+    m.joint_coefs = c0.copy()                          # a global model with <= 16 active coefficients
+    p = m.get_predictions(ds)[..., 0]
+    uq = u.copy()
+    if n_statics == 2:
+        uq[:, 1] = uq[:, 0]
+    for i in range(0, N, 23):
+        rp, *_ = Q.refine_patient(V[i], arms[i], uq[i], int(sl[i]), c0, ex, m.dt, 10.0, 1)
+        assert np.sqrt(np.mean((p[i] - rp) ** 2)) <= 1e-6, i

@@ -58,8 +58,8 @@ def test_sindy_reads_config_and_rejects_unsupported_modes():
     seg = SINDY(a, device="cpu")                 # F4: the treatment-segment path
     assert seg.segment_mode and seg.feature_library_names == ["1", "x0", "u0", "x0 u0"]
     a["model"]["insite"] = True
-    with pytest.raises(NotImplementedError):     # INSITE refinement takes <= 2 arms
-        SINDY(a, device="cpu")
+    seg_ins = SINDY(a, device="cpu")             # INSITE on 4 arms: insite_refine_arms_f64
+    assert seg_ins.segment_mode and seg_ins.insite
     a = _args()
     a["model"]["dataset_name"] = "mimic3"
     with pytest.raises(NotImplementedError):
