@@ -201,7 +201,12 @@ def c3_main(args):
     truth = MS.c3_truth_coef(lib, device=dev)
     rows = N * T
     gflop = 2.0 * (F * (F + 1) / 2 + F * S) * rows          # algorithmic: G upper triangle + B per row
-    mfma_flop = 3 * 16 * 16 * 4 * 2 * rows / 4               # issued: 3 f64 16x16x4 tiles per 4 rows
+    # issued: 2 f64 16x16x4 tiles per 4 rows, plus (F > 16) the tail's 4x4x4 blocks (MsTail, insite_ms.hip):
+    # NT4 block types x 4 instructions of 512 flop per 64 rows
+    f1 = max(F - 16, 0)
+    rg, cg = (f1 + 3) // 4, (f1 + S + 3) // 4
+    nt4 = rg * cg - rg * (rg - 1) // 2 if f1 else 0
+    mfma_flop = (2 * 16 * 16 * 4 * 2 + nt4 * 4 * 512 / 16) * rows / 4
     roll_bytes = T * N * S * 4 + N * S * 4 + T * ((N + 31) // 32) * 4
     gram_bytes = T * N * S * 4 + T * ((N + 31) // 32) * 4
     out = {

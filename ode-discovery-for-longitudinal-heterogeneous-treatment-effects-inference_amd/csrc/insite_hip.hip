@@ -2169,20 +2169,26 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
     }
   }
   // ---------------- final Euler scan with the (refined) model, every coefficient (sindy.py:668) ----------------
-  double cf[INSITE_MAX_ARMS * INSITE_MAX_TERMS];
-  for (int q = 0; q < ra.A * lib.F; ++q) cf[q] = ra.c0[q];
+  // coefficient (a, j): the refined value if active, else the global one; resolved by comparison
+  // against the active list (no dynamically indexed per-lane array, which would live in scratch)
+  auto coef_at = [&](int q) -> double {
+    double c = ra.c0[q];
 #pragma unroll
-  for (int i = 0; i < M; ++i)
-    if (i < ra.m) cf[ra.t_flat[i]] = x[i];
+    for (int i = 0; i < M; ++i)
+      if (i < ra.m && ra.t_flat[i] == q) c = x[i];
+    return c;
+  };
   double al[NA], be[NA];
 #pragma unroll
   for (int a = 0; a < NA; ++a) al[a] = be[a] = 0.0;
-  for (int a = 0; a < ra.A && a < NA; ++a)
-    for (int j = 0; j < lib.F; ++j) {
-      const double t = cf[a * lib.F + j] * monomial(lib, j, uu);
-      if (lib.ex[j] == 0) al[a] += t;
-      else be[a] += t;
-    }
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+    if (a < ra.A)
+      for (int j = 0; j < lib.F; ++j) {
+        const double t = coef_at(a * lib.F + j) * monomial(lib, j, uu);
+        if (lib.ex[j] == 0) al[a] += t;
+        else be[a] += t;
+      }
   const double h = ra.dt / (double)ra.sub;
   double y = ra.V[p];
   for (int k = 0; k < ra.T; ++k) {
@@ -2198,7 +2204,7 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
     ra.preds[(int64_t)k * ra.ldp + p] = y;
   }
   if (ra.coef_out)
-    for (int q = 0; q < ra.A * lib.F; ++q) ra.coef_out[p * ra.A * lib.F + q] = cf[q];
+    for (int q = 0; q < ra.A * lib.F; ++q) ra.coef_out[p * ra.A * lib.F + q] = coef_at(q);
   if (ra.status) ra.status[p] = status;
   if (ra.iters) ra.iters[p] = nit;
 }

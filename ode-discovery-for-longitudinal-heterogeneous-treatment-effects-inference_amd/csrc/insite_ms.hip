@@ -69,30 +69,41 @@ __device__ __forceinline__ double input_bit(const uint32_t* __restrict__ abits, 
   return (double)((abits[(int64_t)k * lda + (p >> 5)] >> (p & 31)) & 1u);
 }
 
-// Rows 16.. of Y (F1 = F - 16 library columns) against [Theta_16.. | xdot]: on the VALU, one fp64 FMA
-// per upper-triangle entry and per (column, state) pair into per-lane accumulators, when there are at
-// most INSITE_MS_VALU_TAIL of them.  The 16 x 16 MFMA tile it replaces has 16 - F1 padding rows
-// (F = 22: 10 of 16; F <= 16: all of them).  Default 0: only the all-padding tile (F <= 16) is dropped.
-// Measured at F = 22 (C3, 1M x 500): the 51 accumulators (102 VGPRs) push the occupancy-2 kernel into
-// scratch spills, 15.5 -> 33.2 ms; at occupancy 1 it is 15.8 ms (tile on MFMA at occupancy 1: 18.7 ms).
-#ifndef INSITE_MS_VALU_TAIL
-#define INSITE_MS_VALU_TAIL 0
+// The tail: rows 16.. of Y (F1 = F - 16 library columns) against Z1 = [Theta_16.. | xdot]
+// (F = 22: 6 rows x 11 columns).  As a 16 x 16 f64 MFMA tile it has 16 - F1 padding rows (F = 22:
+// 10 of 16, a third of the kernel's MFMA work; F <= 16: all of them, so it is never issued then).
+// INSITE_MS_TAIL selects how it is computed when F > 16:
+//   0  the 16 x 16 x 4 tile (16 MFMAs per 64 rows);
+//   1  per-lane VALU FMAs into F1 (F1 + 1) / 2 + F1 S accumulators; at F = 22 the 51 accumulators
+//      (102 VGPRs) push the occupancy-2 kernel into scratch (C3: 15.5 -> 33.2 ms; at occupancy 1
+//      15.8 ms, the 16 x 16 tile at occupancy 1 18.7 ms);
+//   2  v_mfma_f64_4x4x4f64 (4 blocks of 4 x 4 x 4; A[b][m][k] in lane 16k + 4b + m, B[b][k][n] in
+//      lane 16k + 4b + n, D[b][m][n] in lane 16m + 4b + n: tools/probe/mfma_f64_4x4_probe.hip): the
+//      tail cut into 4 x 4 blocks (row group rg < RG, column group cg >= rg: the upper triangle and
+//      every xdot column; F = 22: 5 blocks), each block type one accumulator double per lane whose 4
+//      MFMA blocks take different rows; 20 MFMAs of 1/4 the work per 64 rows (default).
+#ifndef INSITE_MS_TAIL
+#define INSITE_MS_TAIL 2
 #endif
 #ifndef INSITE_MS_WPE
 #define INSITE_MS_WPE 2
 #endif
+constexpr int kTailMfma16 = 0, kTailValu = 1, kTailMfma4 = 2, kTailNone = 3;
 template <int S, int F>
 struct MsTail {
   static constexpr int F1 = F > 16 ? F - 16 : 0;
-  static constexpr int NACC = F1 * (F1 + 1) / 2 + F1 * S;
-  static constexpr bool kValu = NACC <= INSITE_MS_VALU_TAIL;
-  static constexpr int NA = NACC > 0 ? NACC : 1;
+  static constexpr int mode = F1 == 0 ? kTailNone : INSITE_MS_TAIL;
+  static constexpr int NACC = F1 * (F1 + 1) / 2 + F1 * S;                     // VALU accumulators
+  static constexpr int RG = (F1 + 3) / 4, CG = (F1 + S + 3) / 4;             // 4 x 4 block grid
+  static constexpr int NT4 = RG * CG - RG * (RG - 1) / 2;                     // blocks with cg >= rg
+  static constexpr int NA = mode == kTailValu ? NACC : (mode == kTailMfma4 ? NT4 : 1);
+  static_assert(mode != kTailMfma4 || 16 + 4 * CG <= kMsMaxF, "tail column groups must stay in the staged row");
 };
 
 // Stage this lane's library row into LDS and run the 16 x 2 (+ 16) MFMAs over the wave's 64 rows.
 // Row layout: [Theta_0..Theta_{F-1}, xdot_0..xdot_{S-1}, 0 ...] (32 doubles).  A[m][k] = Y_m of row
 // 4g + k (m = lane & 15, k = lane >> 4); B[k][n] = Z_n of the same row; C[(lane>>4) + 4j][lane & 15].
-// With MsTail::kValu the Y1^T Z1 tile is accumulated per lane in acc (see MsTail) instead.
+// The Y1^T Z1 tail as MsTail::mode selects (acc: VALU or 4 x 4 x 4 MFMA accumulators).
 template <int S, int F>
 __device__ __forceinline__ void ms_emit(double* __restrict__ wrow, const double* __restrict__ wbase, bool valid,
                                         const double (&th)[F], const double (&xd)[S], dbl4& c00, dbl4& c01,
@@ -108,7 +119,7 @@ __device__ __forceinline__ void ms_emit(double* __restrict__ wrow, const double*
     wrow[j] = valid ? v : 0.0;
   }
   wave_lds_sync();
-  if constexpr (Tail::kValu && Tail::F1 > 0) {
+  if constexpr (Tail::mode == kTailValu) {
     double y1[Tail::F1];
 #pragma unroll
     for (int i = 0; i < Tail::F1; ++i) y1[i] = valid ? th[16 + i] : 0.0;
@@ -130,9 +141,26 @@ __device__ __forceinline__ void ms_emit(double* __restrict__ wrow, const double*
     const double z1 = src[16 + m];
     c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(y0, y0, c00, 0, 0, 0);
     c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(y0, z1, c01, 0, 0, 0);
-    if constexpr (!Tail::kValu) {
+    if constexpr (Tail::mode == kTailMfma16) {
       const double y1 = y1ok ? z1 : 0.0;
       c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(y1, z1, c11, 0, 0, 0);
+    }
+  }
+  if constexpr (Tail::mode == kTailMfma4) {
+    // lane = 16k + 4b + i: in pass r, block b reduces rows 16r + 4b + k; operand i of column group q is
+    // Z1 column 4q + i (= Y1 row 4q + i for q < RG): one LDS read per group serves A and B
+    const int kk = lane >> 4, bb = (lane >> 2) & 3, ii = lane & 3;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double* src = wbase + (16 * r + 4 * bb + kk) * kMsRowStride + 16 + ii;
+      double v[Tail::CG];
+#pragma unroll
+      for (int q = 0; q < Tail::CG; ++q) v[q] = src[4 * q];
+      int t = 0;
+#pragma unroll
+      for (int rg = 0; rg < Tail::RG; ++rg)
+#pragma unroll
+        for (int cg = rg; cg < Tail::CG; ++cg, ++t) acc[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(v[rg], v[cg], acc[t], 0, 0, 0);
     }
   }
 }
@@ -342,7 +370,7 @@ gram_ms_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint
     red[(wid * kMsTiles + 1) * 256 + e] = c01[j];
     red[(wid * kMsTiles + 2) * 256 + e] = c11[j];
   }
-  if constexpr (Tail::kValu && Tail::F1 > 0) {
+  if constexpr (Tail::mode == kTailValu) {
     // wave sums of the VALU tail into tile 2 ([row - 16][col - 16], both triangles), fixed order
     wave_lds_sync();  // after this wave's (zero) c11 writes
     double* t2 = red + (wid * kMsTiles + 2) * 256;
@@ -361,6 +389,28 @@ gram_ms_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint
         }
       }
     }
+  }
+  if constexpr (Tail::mode == kTailMfma4) {
+    // block sums (lanes 16m + 4b + n over b) into tile 2: entry (4 rg + m, 4 cg + n) is Y1 row 4 rg + m
+    // against Z1 column 4 cg + n, i.e. tile 2 [4 rg + m][4 cg + n] (Z1 column j is tile column j since
+    // xdot_s sits at Z column F + s = 16 + F1 + s); the skipped cg < rg blocks by symmetry
+    wave_lds_sync();  // after this wave's (zero) c11 writes
+    double* t2 = red + (wid * kMsTiles + 2) * 256;
+    const int m = lane >> 4, n = lane & 3;
+    int t = 0;
+#pragma unroll
+    for (int rg = 0; rg < Tail::RG; ++rg)
+#pragma unroll
+      for (int cg = rg; cg < Tail::CG; ++cg, ++t) {
+        double v = acc[t];
+        v += __shfl_xor(v, 4, kWave);
+        v += __shfl_xor(v, 8, kWave);
+        const int row = 4 * rg + m, col = 4 * cg + n;
+        if (((lane >> 2) & 3) == 0 && row < Tail::F1 && col < Tail::F1 + S) {
+          t2[row * 16 + col] = v;
+          if (cg != rg && col < Tail::F1) t2[col * 16 + row] = v;
+        }
+      }
   }
   __syncthreads();
   for (int q = threadIdx.x; q < kMsTiles * 256; q += kBlock) {

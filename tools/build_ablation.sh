@@ -13,9 +13,9 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     SEGKC16) NAME=$v build -DINSITE_SEG_KC=16 -DINSITE_SEG_WPE=2 ;;
     SEGNOPF) NAME=$v build -DINSITE_SEG_PF=0 -DINSITE_SEG_WPE=4 ;;
     SEGKC16NOPF) NAME=$v build -DINSITE_SEG_KC=16 -DINSITE_SEG_PF=0 -DINSITE_SEG_WPE=3 ;;
-    MSTAIL64) NAME=$v build -DINSITE_MS_VALU_TAIL=64 ;;
-    MSTAIL64WPE1) NAME=$v build -DINSITE_MS_VALU_TAIL=64 -DINSITE_MS_WPE=1 ;;
-    MSWPE1) NAME=$v build -DINSITE_MS_WPE=1 ;;
+    MSTAIL0) NAME=$v build -DINSITE_MS_TAIL=0 ;;
+    MSTAIL1) NAME=$v build -DINSITE_MS_TAIL=1 ;;
+    MSTAIL1WPE1) NAME=$v build -DINSITE_MS_TAIL=1 -DINSITE_MS_WPE=1 ;;
     NOARM) NAME=$v build -DINSITE_ABLATE_NOARM ;;
     TIMING) NAME=$v build -DINSITE_TIMING ;;
     LATE) NAME=$v build -DINSITE_GRAM_LATE_ISSUE ;;
