@@ -229,7 +229,8 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
  * of its (refined or global) model over all T steps.
  *   V        [T, ld_v] f64 unscaled observations, time-major (ld_v >= n_rows)
  *   arm_bits TIME_MAJOR_BITS [T, ld_arm] per-step arm (n_arms <= 2)
- *   coef0    HOST [n_arms, F] f64: the global model (at most 16 active coefficients)
+ *   coef0    HOST [n_arms, F] f64: the global model (any number of active coefficients: up to 16
+ *            run register-resident, denser models up to n_arms * F run the scratch-resident kernel)
  *   preds    [T, ld_p] f64 (row k = state after step k); coef_out [n_rows, n_arms, F] (may be NULL);
  *   status_out [n_rows] int32 (-1 = not refined: seq_len <= tau; else the BFGS status: 0 converged,
  *   1 maxiter, 3 zoom failed, 5 line-search maxiter), iters_out [n_rows] int32 (may be NULL). */

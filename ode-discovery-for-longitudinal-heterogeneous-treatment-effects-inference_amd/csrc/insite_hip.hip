@@ -1823,7 +1823,12 @@ __global__ void __launch_bounds__(kBlock) rollout_rk45_kernel(Rk45Args ra, LibDe
 // NA = 2: TIME_MAJOR_BITS arms (PK/PD EQ_4); NA = 4: int8 arms, the 4-valued treatment of cancer_sim /
 // EQ_5 (sindy.py:484-550, argmax(treatment) selects the arm's coefficients).  Only the m active coefficients move (the search runs in that subspace; oracle
 // docstring); every lane runs its own optimiser — lanes finishing early idle until the wave's last.
-constexpr int kRefineMaxActive = 16;
+// M <= 16 (the sparse models of the paper): the whole optimiser state lives in VGPRs, every loop unrolled.
+// Dense global models (up to A * F = 36 active coefficients, e.g. a 4-arm EQ_5 fit with every term kept)
+// use M = 36 with rolled loops (RU = 1): the arrays are then dynamically indexed and live in per-lane
+// scratch — same arithmetic in the same order, slower, never rejected.
+constexpr int kRefineMaxActive = INSITE_MAX_ARMS * INSITE_MAX_TERMS;
+constexpr int kRefineRegActive = 16;
 struct RefineArgs {
   const double* V;      // [T, ldv] unscaled observations (time-major)
   const uint32_t* arm;  // TIME_MAJOR_BITS [T, lda] per-step arm (NA = 2)
@@ -1843,6 +1848,7 @@ struct RefineArgs {
 
 template <int M, int NA>
 struct RefineLane {
+  static constexpr int RU = M <= kRefineRegActive ? M : 1;
   const RefineArgs& ra;
   const LibDesc& lib;
   int64_t p;
@@ -1857,13 +1863,13 @@ struct RefineLane {
   // f and gradient at c (active coordinates)
   __device__ double fg(const double (&c)[M], double (&g)[M]) const {
     double al[NA], be[NA];
-#pragma unroll
+#pragma unroll RU
     for (int a = 0; a < NA; ++a) al[a] = be[a] = 0.0;
-#pragma unroll
+#pragma unroll RU
     for (int i = 0; i < M; ++i) {
       if (i >= ra.m) break;
       const double t = c[i] * mono[i];
-#pragma unroll
+#pragma unroll RU
       for (int a = 0; a < NA; ++a)
         if (ra.t_arm[i] == a) {
           if (ra.t_ex[i] == 0) al[a] += t;
@@ -1873,13 +1879,13 @@ struct RefineLane {
     const double h = ra.dt / (double)ra.sub;
     double y = ra.V[p];
     double da[NA], db[NA], gA[NA], gB[NA];
-#pragma unroll
+#pragma unroll RU
     for (int a = 0; a < NA; ++a) da[a] = db[a] = gA[a] = gB[a] = 0.0;
     double L = 0.0;
     for (int k = 0; k < K; ++k) {
       const int ak = armbit(k);
       double alk = al[0], bek = be[0];
-#pragma unroll
+#pragma unroll RU
       for (int a = 1; a < NA; ++a)
         if (ak == a) {
           alk = al[a];
@@ -1887,7 +1893,7 @@ struct RefineLane {
         }
       const double hb = h * bek;
       for (int s = 0; s < ra.sub; ++s) {
-#pragma unroll
+#pragma unroll RU
         for (int a = 0; a < NA; ++a) {
           da[a] = da[a] + hb * da[a];
           db[a] = db[a] + hb * db[a];
@@ -1900,7 +1906,7 @@ struct RefineLane {
       }
       const double r = ra.V[(int64_t)(k + 1) * ra.ldv + p] - y;
       L += r * r;
-#pragma unroll
+#pragma unroll RU
       for (int a = 0; a < NA; ++a) {
         gA[a] += -2.0 * r * da[a];
         gB[a] += -2.0 * r * db[a];
@@ -1909,7 +1915,7 @@ struct RefineLane {
     const double iK = 1.0 / (double)K;
     L *= iK;
     double pen = 0.0;
-#pragma unroll
+#pragma unroll RU
     for (int i = 0; i < M; ++i) {
       if (i >= ra.m) {
         g[i] = 0.0;
@@ -1918,7 +1924,7 @@ struct RefineLane {
       const double d = c0a[i] - c[i];
       pen += d * d;
       double gd = 0.0;
-#pragma unroll
+#pragma unroll RU
       for (int a = 0; a < NA; ++a)
         if (ra.t_arm[i] == a) gd = ra.t_ex[i] == 0 ? gA[a] : gB[a];
       g[i] = gd * iK * mono[i] / norm + 2.0 * ra.lam * (c[i] - c0a[i]) / (double)ra.n_total;
@@ -1927,14 +1933,14 @@ struct RefineLane {
   }
   __device__ double dot(const double (&a)[M], const double (&b)[M]) const {
     double s = 0.0;
-#pragma unroll
+#pragma unroll RU
     for (int i = 0; i < M; ++i) s += a[i] * b[i];
     return s;
   }
   // phi(t) = f(x + t pk), dphi = g . pk
   __device__ double phi(const double (&x)[M], const double (&pk)[M], double t, double& dphi, double (&g)[M]) const {
     double xt[M];
-#pragma unroll
+#pragma unroll RU
     for (int i = 0; i < M; ++i) xt[i] = x[i] + t * pk[i];
     const double f = fg(xt, g);
     dphi = dot(g, pk);
@@ -1958,19 +1964,20 @@ __device__ __forceinline__ double quadmin(double a, double fa, double fpa, doubl
 
 template <int M, int NA>
 __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, LibDesc lib) {
+  constexpr int RU = RefineLane<M, NA>::RU;
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ra.N) return;
   double uu[INSITE_MAX_STATICS];
-#pragma unroll
+#pragma unroll RU
   for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < lib.U ? ra.u[p * lib.U + t] : 0.0;
   RefineLane<M, NA> ln{ra, lib, p, 0, 1.0, {}, {}};
-#pragma unroll
+#pragma unroll RU
   for (int i = 0; i < M; ++i) {
     ln.mono[i] = i < ra.m ? monomial(lib, ra.t_col[i], uu) : 0.0;
     ln.c0a[i] = i < ra.m ? ra.c0[ra.t_flat[i]] : 0.0;
   }
   double x[M];
-#pragma unroll
+#pragma unroll RU
   for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
   const int sl = ra.sl[p];
   int status = -1, nit = 0;
@@ -1981,13 +1988,13 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
     ln.norm = start * 2.5;
     // ---------------- BFGS (jax minimize_bfgs, norm = inf, gtol 1e-5) ----------------
     double H[M][M];
-#pragma unroll
+#pragma unroll RU
     for (int i = 0; i < M; ++i)
-#pragma unroll
+#pragma unroll RU
       for (int j = 0; j < M; ++j) H[i][j] = i == j ? 1.0 : 0.0;
     double f = ln.fg(x, g);
     double gmax = 0.0, g2 = 0.0;
-#pragma unroll
+#pragma unroll RU
     for (int i = 0; i < M; ++i) {
       gmax = fmax(gmax, fabs(g[i]));
       g2 += g[i] * g[i];
@@ -1999,10 +2006,10 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
     int k = 0;
     while (!converged && !failed && k < maxiter) {
       double pk[M];
-#pragma unroll
+#pragma unroll RU
       for (int i = 0; i < M; ++i) {
         double s = 0.0;
-#pragma unroll
+#pragma unroll RU
         for (int j = 0; j < M; ++j) s += H[i][j] * g[j];
         pk[i] = -s;
       }
@@ -2015,7 +2022,7 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
       double a_i1 = 0.0, phi_i1 = phi0, dphi_i1 = dphi0;
       double a_star = 0.0, phi_star = phi0;
       double g_star[M];
-#pragma unroll
+#pragma unroll RU
       for (int i = 0; i < M; ++i) g_star[i] = g[i];
       auto wolfe_one = [&](double a_, double ph) { return ph > phi0 + 1e-4 * a_ * dphi0; };
       auto wolfe_two = [&](double dph) { return fabs(dph) <= -0.9 * dphi0; };
@@ -2028,7 +2035,7 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
         double a_rec = (a_lo + a_hi) / 2.0, phi_rec = (phi_lo + phi_hi) / 2.0;
         double za = 1.0, zphi = phi_lo;
         double zg[M];
-#pragma unroll
+#pragma unroll RU
         for (int i = 0; i < M; ++i) zg[i] = g[i];
         while (!done && !z_failed) {
           const double dalpha = a_hi - a_lo;
@@ -2060,7 +2067,7 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
           if (star_to_j) {
             za = a_j;
             zphi = phi_j;
-#pragma unroll
+#pragma unroll RU
             for (int i = 0; i < M; ++i) zg[i] = g_j[i];
           }
           if (hi_to_lo) {
@@ -2082,7 +2089,7 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
         }
         a_star = za;
         phi_star = zphi;
-#pragma unroll
+#pragma unroll RU
         for (int i = 0; i < M; ++i) g_star[i] = zg[i];
       };
       while (!ls_done && li <= 10 && !ls_failed) {
@@ -2100,7 +2107,7 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
         if (s_i) {
           a_star = a_i;
           phi_star = phi_i;
-#pragma unroll
+#pragma unroll RU
           for (int i = 0; i < M; ++i) g_star[i] = g_i[i];
         }
         if (s_z2) {
@@ -2118,7 +2125,7 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
       failed = ls_failed || !ls_done;
       // ---- BFGS update ----
       double sk[M], yk[M];
-#pragma unroll
+#pragma unroll RU
       for (int i = 0; i < M; ++i) {
         sk[i] = a_star * pk[i];
         yk[i] = g_star[i] - g[i];
@@ -2126,31 +2133,31 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
       const double rho = 1.0 / ln.dot(yk, sk);
       if (isfinite(rho)) {
         double W[M][M], WH[M][M];
-#pragma unroll
+#pragma unroll RU
         for (int i = 0; i < M; ++i)
-#pragma unroll
+#pragma unroll RU
           for (int j = 0; j < M; ++j) W[i][j] = (i == j ? 1.0 : 0.0) - rho * (sk[i] * yk[j]);
-#pragma unroll
+#pragma unroll RU
         for (int i = 0; i < M; ++i)
-#pragma unroll
+#pragma unroll RU
           for (int j = 0; j < M; ++j) {
             double s = 0.0;
-#pragma unroll
+#pragma unroll RU
             for (int q = 0; q < M; ++q) s += W[i][q] * H[q][j];
             WH[i][j] = s;
           }
-#pragma unroll
+#pragma unroll RU
         for (int i = 0; i < M; ++i)
-#pragma unroll
+#pragma unroll RU
           for (int j = 0; j < M; ++j) {
             double s = 0.0;
-#pragma unroll
+#pragma unroll RU
             for (int q = 0; q < M; ++q) s += WH[i][q] * W[j][q];
             H[i][j] = s + rho * (sk[i] * sk[j]);
           }
       }
       double gm = 0.0;
-#pragma unroll
+#pragma unroll RU
       for (int i = 0; i < M; ++i) {
         x[i] = x[i] + sk[i];
         g[i] = g_star[i];
@@ -2164,7 +2171,7 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
     nit = k;
     status = converged ? 0 : (k == maxiter ? 1 : (failed ? 2 + ls_status : -1));
     if (status == 3) {  // zoom failed: the reference keeps the global coefficients (sindy.py:628-631)
-#pragma unroll
+#pragma unroll RU
       for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
     }
   }
@@ -2173,15 +2180,15 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
   // against the active list (no dynamically indexed per-lane array, which would live in scratch)
   auto coef_at = [&](int q) -> double {
     double c = ra.c0[q];
-#pragma unroll
+#pragma unroll RU
     for (int i = 0; i < M; ++i)
       if (i < ra.m && ra.t_flat[i] == q) c = x[i];
     return c;
   };
   double al[NA], be[NA];
-#pragma unroll
+#pragma unroll RU
   for (int a = 0; a < NA; ++a) al[a] = be[a] = 0.0;
-#pragma unroll
+#pragma unroll RU
   for (int a = 0; a < NA; ++a)
     if (a < ra.A)
       for (int j = 0; j < lib.F; ++j) {
@@ -2194,7 +2201,7 @@ __global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, Li
   for (int k = 0; k < ra.T; ++k) {
     const int ak = ln.armbit(k);
     double alk = al[0], bek = be[0];
-#pragma unroll
+#pragma unroll RU
     for (int a = 1; a < NA; ++a)
       if (ak == a) {
         alk = al[a];
@@ -3086,11 +3093,13 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
   if (bits) {
     if (m <= 4) insite_refine_kernel<4, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
     else if (m <= 8) insite_refine_kernel<8, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
-    else insite_refine_kernel<16, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else if (m <= kRefineRegActive) insite_refine_kernel<16, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else insite_refine_kernel<kRefineMaxActive, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
   } else {
     if (m <= 4) insite_refine_kernel<4, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
     else if (m <= 8) insite_refine_kernel<8, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
-    else insite_refine_kernel<16, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else if (m <= kRefineRegActive) insite_refine_kernel<16, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else insite_refine_kernel<kRefineMaxActive, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
   }
   return launch_status();
 }

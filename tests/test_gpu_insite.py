@@ -165,15 +165,35 @@ def test_refine_four_arms_matches_oracle(dev, n_statics, tau):
     assert (status[sl <= tau] == -1).all() and (status[sl > tau] == 0).mean() > 0.8
 
 
-def test_refine_four_arms_rejects_more_than_16_active(dev):
+@pytest.mark.parametrize("n_arms", [2, 4])
+def test_refine_dense_model_matches_oracle(dev, n_arms):
+    """A dense global model (every coefficient above the 1e-3 mask: 14 or 28 active, the latter past the
+    16-coefficient register kernel) is refined, not rejected: the M = 36 scratch-resident instantiation
+    runs the same BFGS arithmetic as the oracle."""
     from insite_amd import ops
     from insite_amd.library import polynomial_library
-    V, u, arms, _, _ = _four_arm_problem(2, 8, 1)
-    c0 = np.full((4, 7), 0.01)                     # 28 active coefficients
-    with pytest.raises(Exception):
-        ops.insite_refine(torch.tensor(V, device=dev), torch.tensor(arms, device=dev), torch.tensor(u, device=dev),
-                          torch.full((8,), 60, dtype=torch.int32, device=dev), c0, polynomial_library(2, 2, True),
-                          1 / 6, 10.0, 5)
+    V, u, arms, c0, ex = _four_arm_problem(2, 40, 11)
+    tau = 5
+    if n_arms == 2:
+        arms = (arms % 2).astype(np.int8)
+    c0 = c0[:n_arms].copy()
+    c0[np.abs(c0) <= 1e-3] = 0.02                  # every term active
+    N, T = V.shape
+    sl = np.full(N, T, dtype=np.int32)
+    sl[:2] = [tau, tau + 1]
+    lib = polynomial_library(2, 2, True)
+    preds, coef, status, iters = ops.insite_refine(torch.tensor(V, device=dev), torch.tensor(arms, device=dev),
+                                                   torch.tensor(u, device=dev),
+                                                   torch.tensor(sl, device=dev), c0, lib, 1 / 6, 10.0, tau)
+    torch.cuda.synchronize()
+    preds, coef, status = preds.cpu().numpy(), coef.cpu().numpy(), status.cpu().numpy()
+    assert coef.shape == (N, n_arms, 7)
+    for p in range(N):
+        rp, rc, rs, _ = Q.refine_patient(V[p], arms[p], u[p], sl[p], c0, ex, 1 / 6, 10.0, tau)
+        assert status[p] == rs, (p, status[p], rs)
+        assert np.abs(coef[p] - rc).max() <= 1e-7 * max(1.0, np.abs(rc).max()), p
+        assert np.sqrt(np.mean((preds[p] - rp) ** 2)) <= 1e-6
+    assert status[0] == -1 and (status[1:] >= 0).all()
 
 
 @pytest.mark.parametrize("name,n_statics", [("cancer_sim", 1), ("EQ_5_B", 2)])
