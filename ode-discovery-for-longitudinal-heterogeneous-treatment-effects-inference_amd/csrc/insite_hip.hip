@@ -1689,6 +1689,29 @@ struct Rk45Args {
   double rtol, atol, drop;
 };
 
+// e^(-1/5) for the RK45 step-size rules (scipy rk.py: `error_norm ** error_exponent`, exponent -1/5, once
+// per attempt; common.py select_initial_step: `(0.01 / max(d1, d2)) ** (1 / (order + 1))`, once per
+// interval).  e = m 2^(5q) with m in [1, 64) (exact power-of-two scaling), so e^(-1/5) = m^(-1/5) 2^(-q);
+// a fp32 hardware estimate of m^(-1/5) (v_log_f32 / v_exp_f32, relative error ~1e-7) is refined by two
+// division-free Newton steps on x^5 m = 1, x <- x (1 - r / 5), r = x^5 m - 1 (error 3 delta^2 per step):
+// fp64 accuracy of the exact fifth root (pow's exponent is the double 0.2 = 1/5 + 1.1e-17, i.e. a
+// relative 1.1e-17 |ln e| away: < 1 ulp for controller errors in [1e-6, 1e4]) in ~20 VALU ops instead of ocml's double-double pow_f64 (>100), the
+// per-attempt cost that dominated the step loop.  Zero, infinite and NaN inputs take pow itself.
+__device__ __forceinline__ double rk45_inv_root5(double e) {
+  if (!(e > 0.0 && e < INFINITY)) return pow(e, -0.2);
+  const int k = ilogb(e);
+  const int q = (k >= 0 ? k : k - 4) / 5;  // floor(k / 5)
+  const double m = ldexp(e, -5 * q);
+  double x = (double)__builtin_amdgcn_exp2f(-0.2f * __builtin_amdgcn_logf((float)m));
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double x2 = x * x;
+    const double r = fma(x2 * x2 * x, m, -1.0);
+    x = fma(-0.2 * x, r, x);
+  }
+  return ldexp(x, -q);
+}
+
 template <int NARM, bool PERROW>
 __global__ void __launch_bounds__(kBlock) rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
   constexpr double a21 = 1.0 / 5.0;
@@ -1765,7 +1788,7 @@ __global__ void __launch_bounds__(kBlock) rollout_rk45_kernel(Rk45Args ra, LibDe
         h0 = fmin(h0, interval);
         const double f1 = fma(be, y + h0 * f, al);
         const double d2 = fabs((f1 - f) / scale) / h0;
-        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
+        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : rk45_inv_root5(fmax(d1, d2) * 100.0);
         h_abs = fmin(fmin(100.0 * h0, h1), interval);
       }
       // ---- accepted steps until t reaches t1 ----
@@ -1791,7 +1814,7 @@ __global__ void __launch_bounds__(kBlock) rollout_rk45_kernel(Rk45Args ra, LibDe
           const double err = fabs(e * h / scale);
           ++attempts;
           if (err < 1.0) {
-            double factor = err == 0.0 ? 10.0 : fmin(10.0, 0.9 * pow(err, -0.2));
+            double factor = err == 0.0 ? 10.0 : fmin(10.0, 0.9 * rk45_inv_root5(err));
             if (rejected) factor = fmin(1.0, factor);
             h_abs *= factor;
             t = t_new;
@@ -1799,7 +1822,7 @@ __global__ void __launch_bounds__(kBlock) rollout_rk45_kernel(Rk45Args ra, LibDe
             f = f_new;
             break;
           }
-          h_abs *= fmax(0.2, 0.9 * pow(err, -0.2));
+          h_abs *= fmax(0.2, 0.9 * rk45_inv_root5(err));
           rejected = true;
         }
       }
