@@ -1905,8 +1905,17 @@ struct RefineLane {
 #pragma unroll RU
     for (int a = 0; a < NA; ++a) da[a] = db[a] = gA[a] = gB[a] = 0.0;
     double L = 0.0;
+    // step k's arm and target are requested one step ahead (issued before step k - 1's sub-steps) so the
+    // dependent Euler chain does not wait on a load per step
+    int ak_nx = armbit(0);
+    double v_nx = ra.V[ra.ldv + p];
     for (int k = 0; k < K; ++k) {
-      const int ak = armbit(k);
+      const int ak = ak_nx;
+      const double vk1 = v_nx;
+      if (k + 1 < K) {
+        ak_nx = armbit(k + 1);
+        v_nx = ra.V[(int64_t)(k + 2) * ra.ldv + p];
+      }
       double alk = al[0], bek = be[0];
 #pragma unroll RU
       for (int a = 1; a < NA; ++a)
@@ -1927,7 +1936,7 @@ struct RefineLane {
         }
         y = y + h * (alk + bek * y);
       }
-      const double r = ra.V[(int64_t)(k + 1) * ra.ldv + p] - y;
+      const double r = vk1 - y;
       L += r * r;
 #pragma unroll RU
       for (int a = 0; a < NA; ++a) {
