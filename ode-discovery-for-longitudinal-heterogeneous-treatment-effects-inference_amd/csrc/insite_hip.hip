@@ -1712,8 +1712,12 @@ __device__ __forceinline__ double rk45_inv_root5(double e) {
   return ldexp(x, -q);
 }
 
+#ifndef INSITE_RK45_WPE
+#define INSITE_RK45_WPE 1  // waves per SIMD the register budget is sized for (1: unconstrained)
+#endif
 template <int NARM, bool PERROW>
-__global__ void __launch_bounds__(kBlock) rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_RK45_WPE)))
+rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
   constexpr double a21 = 1.0 / 5.0;
   constexpr double a31 = 3.0 / 40.0, a32 = 9.0 / 40.0;
   constexpr double a41 = 44.0 / 45.0, a42 = -56.0 / 15.0, a43 = 32.0 / 9.0;
@@ -1994,8 +1998,15 @@ __device__ __forceinline__ double quadmin(double a, double fa, double fpa, doubl
   return a - fpa / (2.0 * B);
 }
 
+#ifndef INSITE_REFINE_WPE4
+#define INSITE_REFINE_WPE4 4
+#endif
+// M <= 4 (the EQ_4 models: two terms per arm) is sized for INSITE_REFINE_WPE4 waves per SIMD (<= 128
+// VGPRs; unconstrained the compiler takes 202 and runs 2 waves): the objective scan is a dependent fp64
+// chain per lane, hidden only by other waves.
 template <int M, int NA>
-__global__ void __launch_bounds__(kBlock) insite_refine_kernel(RefineArgs ra, LibDesc lib) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M <= 4 ? INSITE_REFINE_WPE4 : 1)))
+insite_refine_kernel(RefineArgs ra, LibDesc lib) {
   constexpr int RU = RefineLane<M, NA>::RU;
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ra.N) return;

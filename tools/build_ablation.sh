@@ -37,6 +37,15 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     PPL1) NAME=$v build -DINSITE_FORCE_PPL=1 ;;
     PPL2) NAME=$v build -DINSITE_FORCE_PPL=2 ;;
     PPL4) NAME=$v build -DINSITE_FORCE_PPL=4 ;;
+    RWPE1) NAME=$v build -DINSITE_REFINE_WPE4=1 ;;
+    RWPE2) NAME=$v build -DINSITE_REFINE_WPE4=2 ;;
+    RWPE3) NAME=$v build -DINSITE_REFINE_WPE4=3 ;;
+    RWPE5) NAME=$v build -DINSITE_REFINE_WPE4=5 ;;
+    RWPE6) NAME=$v build -DINSITE_REFINE_WPE4=6 ;;
+    RWPE8) NAME=$v build -DINSITE_REFINE_WPE4=8 ;;
+    KWPE5) NAME=$v build -DINSITE_RK45_WPE=5 ;;
+    KWPE6) NAME=$v build -DINSITE_RK45_WPE=6 ;;
+    KWPE8) NAME=$v build -DINSITE_RK45_WPE=8 ;;
   esac
 done
 wait
