@@ -1850,12 +1850,18 @@ rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
 // NA = 2: TIME_MAJOR_BITS arms (PK/PD EQ_4); NA = 4: int8 arms, the 4-valued treatment of cancer_sim /
 // EQ_5 (sindy.py:484-550, argmax(treatment) selects the arm's coefficients).  Only the m active coefficients move (the search runs in that subspace; oracle
 // docstring); every lane runs its own optimiser — lanes finishing early idle until the wave's last.
-// M <= 16 (the sparse models of the paper): the whole optimiser state lives in VGPRs, every loop unrolled.
-// Dense global models (up to A * F = 36 active coefficients, e.g. a 4-arm EQ_5 fit with every term kept)
-// use M = 36 with rolled loops (RU = 1): the arrays are then dynamically indexed and live in per-lane
-// scratch — same arithmetic in the same order, slower, never rejected.
+// M <= 8 (the sparse models of the paper): the whole optimiser state lives in VGPRs, every loop unrolled,
+// and the inverse-Hessian update is the oracle's w @ H @ w.T.  M = 16 and M = 36 (dense global models, up
+// to A * F = 36 active coefficients, e.g. a 4-arm EQ_5 fit keeping every term) use rolled loops (RU = 1):
+// the arrays are dynamically indexed and live in per-lane scratch, and the update is the O(M^2) expansion
+// (one H y product, no M x M temporaries).  Measured at 200k 4-arm rows (tools/refine_arms_bench.py):
+// M = 16 unrolled 80 ms (512 VGPRs + 5.5k spilled) vs rolled 62 ms; M = 36 rolled O(M^3) 1437 ms vs
+// O(M^2) 108 ms; M = 8 5.5 ms.
 constexpr int kRefineMaxActive = INSITE_MAX_ARMS * INSITE_MAX_TERMS;
-constexpr int kRefineRegActive = 16;
+#ifndef INSITE_REFINE_REG
+#define INSITE_REFINE_REG 8  // largest M whose loops are fully unrolled (register-resident state)
+#endif
+constexpr int kRefineRegActive = INSITE_REFINE_REG;
 struct RefineArgs {
   const double* V;      // [T, ldv] unscaled observations (time-major)
   const uint32_t* arm;  // TIME_MAJOR_BITS [T, lda] per-step arm (NA = 2)
@@ -2001,11 +2007,14 @@ __device__ __forceinline__ double quadmin(double a, double fa, double fpa, doubl
 #ifndef INSITE_REFINE_WPE4
 #define INSITE_REFINE_WPE4 4
 #endif
+#ifndef INSITE_REFINE_WPE8
+#define INSITE_REFINE_WPE8 1
+#endif
 // M <= 4 (the EQ_4 models: two terms per arm) is sized for INSITE_REFINE_WPE4 waves per SIMD (<= 128
 // VGPRs; unconstrained the compiler takes 202 and runs 2 waves): the objective scan is a dependent fp64
 // chain per lane, hidden only by other waves.
 template <int M, int NA>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M <= 4 ? INSITE_REFINE_WPE4 : 1)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M <= 4 ? INSITE_REFINE_WPE4 : (M <= 8 ? INSITE_REFINE_WPE8 : 1))))
 insite_refine_kernel(RefineArgs ra, LibDesc lib) {
   constexpr int RU = RefineLane<M, NA>::RU;
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2174,7 +2183,25 @@ insite_refine_kernel(RefineArgs ra, LibDesc lib) {
         yk[i] = g_star[i] - g[i];
       }
       const double rho = 1.0 / ln.dot(yk, sk);
-      if (isfinite(rho)) {
+      if (isfinite(rho) && RU == 1) {
+        // rolled (scratch-resident) kernels: the same update expanded to O(M^2) with one matrix-vector
+        // product, (I - rho s y^T) H (I - rho y s^T) + rho s s^T
+        //   = H - rho (s (H y)^T + (H y) s^T) + (rho^2 y^T H y + rho) s s^T   (H symmetric),
+        // instead of two O(M^3) products through two more M x M scratch matrices; the association order
+        // differs from the oracle's w @ H @ w.T (jax's three-operand einsum fixes none either)
+        double hy[M];
+        double yhy = 0.0;
+        for (int i = 0; i < M; ++i) {
+          double t = 0.0;
+          for (int j = 0; j < M; ++j) t += H[i][j] * yk[j];
+          hy[i] = t;
+          yhy += yk[i] * t;
+        }
+        const double cs = rho * rho * yhy + rho;
+        for (int i = 0; i < M; ++i)
+          for (int j = 0; j < M; ++j)
+            H[i][j] = H[i][j] - rho * (sk[i] * hy[j] + hy[i] * sk[j]) + cs * (sk[i] * sk[j]);
+      } else if (isfinite(rho)) {
         double W[M][M], WH[M][M];
 #pragma unroll RU
         for (int i = 0; i < M; ++i)
@@ -3136,12 +3163,12 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
   if (bits) {
     if (m <= 4) insite_refine_kernel<4, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
     else if (m <= 8) insite_refine_kernel<8, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
-    else if (m <= kRefineRegActive) insite_refine_kernel<16, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else if (m <= 16) insite_refine_kernel<16, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
     else insite_refine_kernel<kRefineMaxActive, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
   } else {
     if (m <= 4) insite_refine_kernel<4, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
     else if (m <= 8) insite_refine_kernel<8, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
-    else if (m <= kRefineRegActive) insite_refine_kernel<16, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else if (m <= 16) insite_refine_kernel<16, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
     else insite_refine_kernel<kRefineMaxActive, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
   }
   return launch_status();

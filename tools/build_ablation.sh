@@ -44,6 +44,8 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     RWPE6) NAME=$v build -DINSITE_REFINE_WPE4=6 ;;
     RWPE8) NAME=$v build -DINSITE_REFINE_WPE4=8 ;;
     KWPE5) NAME=$v build -DINSITE_RK45_WPE=5 ;;
+    RW8_2) NAME=$v build -DINSITE_REFINE_WPE8=2 ;;
+    RREG8) NAME=$v build -DINSITE_REFINE_REG=8 ;;
     KWPE6) NAME=$v build -DINSITE_RK45_WPE=6 ;;
     KWPE8) NAME=$v build -DINSITE_RK45_WPE=8 ;;
   esac
