@@ -2010,6 +2010,9 @@ __device__ __forceinline__ double quadmin(double a, double fa, double fpa, doubl
 #ifndef INSITE_REFINE_WPE8
 #define INSITE_REFINE_WPE8 1
 #endif
+#ifndef INSITE_REFINE_QUAD
+#define INSITE_REFINE_QUAD 0  // 1: the O(M^2) inverse-Hessian update for the unrolled kernels too
+#endif
 // M <= 4 (the EQ_4 models: two terms per arm) is sized for INSITE_REFINE_WPE4 waves per SIMD (<= 128
 // VGPRs; unconstrained the compiler takes 202 and runs 2 waves): the objective scan is a dependent fp64
 // chain per lane, hidden only by other waves.
@@ -2183,7 +2186,7 @@ insite_refine_kernel(RefineArgs ra, LibDesc lib) {
         yk[i] = g_star[i] - g[i];
       }
       const double rho = 1.0 / ln.dot(yk, sk);
-      if (isfinite(rho) && RU == 1) {
+      if (isfinite(rho) && (RU == 1 || INSITE_REFINE_QUAD)) {
         // rolled (scratch-resident) kernels: the same update expanded to O(M^2) with one matrix-vector
         // product, (I - rho s y^T) H (I - rho y s^T) + rho s s^T
         //   = H - rho (s (H y)^T + (H y) s^T) + (rho^2 y^T H y + rho) s s^T   (H symmetric),
@@ -2191,14 +2194,18 @@ insite_refine_kernel(RefineArgs ra, LibDesc lib) {
         // differs from the oracle's w @ H @ w.T (jax's three-operand einsum fixes none either)
         double hy[M];
         double yhy = 0.0;
+#pragma unroll RU
         for (int i = 0; i < M; ++i) {
           double t = 0.0;
+#pragma unroll RU
           for (int j = 0; j < M; ++j) t += H[i][j] * yk[j];
           hy[i] = t;
           yhy += yk[i] * t;
         }
         const double cs = rho * rho * yhy + rho;
+#pragma unroll RU
         for (int i = 0; i < M; ++i)
+#pragma unroll RU
           for (int j = 0; j < M; ++j)
             H[i][j] = H[i][j] - rho * (sk[i] * hy[j] + hy[i] * sk[j]) + cs * (sk[i] * sk[j]);
       } else if (isfinite(rho)) {

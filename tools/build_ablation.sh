@@ -46,6 +46,8 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     KWPE5) NAME=$v build -DINSITE_RK45_WPE=5 ;;
     RW8_2) NAME=$v build -DINSITE_REFINE_WPE8=2 ;;
     RREG8) NAME=$v build -DINSITE_REFINE_REG=8 ;;
+    RQUAD) NAME=$v build -DINSITE_REFINE_QUAD=1 ;;
+    RQUAD5) NAME=$v build -DINSITE_REFINE_QUAD=1 -DINSITE_REFINE_WPE4=5 ;;
     KWPE6) NAME=$v build -DINSITE_RK45_WPE=6 ;;
     KWPE8) NAME=$v build -DINSITE_RK45_WPE=8 ;;
   esac
