@@ -1882,6 +1882,9 @@ struct RefineArgs {
 template <int M, int NA>
 struct RefineLane {
   static constexpr int RU = M <= kRefineRegActive ? M : 1;
+  // sub-step loop unrolled by odeint's 5 (the default): measured 12 active 62 -> 43 ms, 6 active 5.5 -> 5.2 ms;
+  // for M = 4 (EQ_4 bench, 9.6 -> 10.1 ms) and M = 36 (110 -> 117 ms) it is slower and stays rolled
+  static constexpr int SU = (M > 4 && M <= 16) ? 5 : 1;
   const RefineArgs& ra;
   const LibDesc& lib;
   int64_t p;
@@ -1934,6 +1937,7 @@ struct RefineLane {
           bek = be[a];
         }
       const double hb = h * bek;
+#pragma unroll SU
       for (int s = 0; s < ra.sub; ++s) {
 #pragma unroll RU
         for (int a = 0; a < NA; ++a) {
