@@ -141,7 +141,7 @@ __device__ void small_trajectory(const double* __restrict__ xrow, int64_t step, 
     else if (k == LL - 2) d = fd_pos3(xs[LL - 5], xs[LL - 4], xs[LL - 3], xs[LL - 2], xs[LL - 1]) * w.inv_dt;
     else if (k == LL - 1) d = fd_pos4(xs[LL - 5], xs[LL - 4], xs[LL - 3], xs[LL - 2], xs[LL - 1]) * w.inv_dt;
     else d = fd_int(w, xs[k - 2], xs[k - 1], xs[k + 1], xs[k + 2]);
-    add_row(xs[k], d, Sx, Sxx, Sd, Sdx);
+    add_row(xv[k], d, Sx, Sxx, Sd, Sdx);  // library on the raw sample (pysindy: x_dot only is smoothed)
   }
 }
 
@@ -374,7 +374,6 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
           if constexpr (SMOOTH) {
             if (i >= 4) sr[(i - 2) & 7] = sg_int(w, xr[(i - 4) & 7], xr[(i - 3) & 7], xr[(i - 2) & 7], xr[(i - 1) & 7], xr[i & 7]);
             if (i == 7) {
-              tele_lo(w, sr[2], sr[3], sr[4], sr[5], loSd, loSdx);  // xs[a-2..a+1], a = tb + 4
               if (sidx == 0) {  // head rows kd = 0..3 from x[0..7], xs[2..5]
                 const double xs0 = sg_pos0(xr[0], xr[1], xr[2], xr[3], xr[4]);
                 const double xs1 = sg_pos1(xr[0], xr[1], xr[2], xr[3], xr[4]);
@@ -383,17 +382,20 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
                 const double d2 = fd_int(w, xs0, xs1, sr[3], sr[4]);
                 const double d3 = fd_int(w, xs1, sr[2], sr[4], sr[5]);
                 const bool on = Lm > 0;
-                add_row(on ? xs0 : 0.0, on ? d0 : 0.0, Sx, Sxx, Sd, Sdx);
-                add_row(on ? xs1 : 0.0, on ? d1 : 0.0, Sx, Sxx, Sd, Sdx);
-                add_row(on ? sr[2] : 0.0, on ? d2 : 0.0, Sx, Sxx, Sd, Sdx);
-                add_row(on ? sr[3] : 0.0, on ? d3 : 0.0, Sx, Sxx, Sd, Sdx);
+                add_row(on ? xr[0] : 0.0, on ? d0 : 0.0, Sx, Sxx, Sd, Sdx);
+                add_row(on ? xr[1] : 0.0, on ? d1 : 0.0, Sx, Sxx, Sd, Sdx);
+                add_row(on ? xr[2] : 0.0, on ? d2 : 0.0, Sx, Sxx, Sd, Sdx);
+                add_row(on ? xr[3] : 0.0, on ? d3 : 0.0, Sx, Sxx, Sd, Sdx);
               }
             }
-            if (i >= 8) {  // body row kd = t - 4
-              double xk = sr[(i - 4) & 7];
-              if (masked) xk = (t < e) ? xk : 0.0;
-              Sx += xk;
-              Sxx = fma(xk, xk, Sxx);
+            if (i >= 8) {  // body row kd = t - 4: raw x[kd], x_dot from xs[kd-2 .. kd+2]
+              double xk = xr[(i - 4) & 7];
+              double dk = fd_int(w, sr[(i - 6) & 7], sr[(i - 5) & 7], sr[(i - 3) & 7], sr[(i - 2) & 7]);
+              if (masked) {
+                xk = (t < e) ? xk : 0.0;
+                dk = (t < e) ? dk : 0.0;
+              }
+              add_row(xk, dk, Sx, Sxx, Sd, Sdx);
             }
           } else {
             if (i == 3) tele_lo(w, xr[0], xr[1], xr[2], xr[3], loSd, loSdx);  // x[a-2..a+1], a = tb + 2
@@ -420,31 +422,31 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
 #pragma unroll
           for (int i = 0; i < kGT; ++i) {
             xr[i & 7] = sample(v, i);
-            double xk;
             if constexpr (SMOOTH) {
               sr[(i - 2) & 7] = sg_int(w, xr[(i - 4) & 7], xr[(i - 3) & 7], xr[(i - 2) & 7], xr[(i - 1) & 7], xr[i & 7]);
-              xk = sr[(i - 4) & 7];
+              add_row(xr[(i - 4) & 7], fd_int(w, sr[(i - 6) & 7], sr[(i - 5) & 7], sr[(i - 3) & 7], sr[(i - 2) & 7]),
+                      Sx, Sxx, Sd, Sdx);
             } else {
-              xk = xr[(i - 2) & 7];
+              const double xk = xr[(i - 2) & 7];
+              Sx += xk;
+              Sxx = fma(xk, xk, Sxx);
             }
-            Sx += xk;
-            Sxx = fma(xk, xk, Sxx);
           }
         } else {
 #pragma unroll
           for (int i = 0; i < kGT; ++i) {
             if (t0 + i < s1) {
               xr[i & 7] = sample(v, i);
-              double xk;
+              const bool own = t0 + i < e;
               if constexpr (SMOOTH) {
                 sr[(i - 2) & 7] = sg_int(w, xr[(i - 4) & 7], xr[(i - 3) & 7], xr[(i - 2) & 7], xr[(i - 1) & 7], xr[i & 7]);
-                xk = sr[(i - 4) & 7];
+                const double dk = fd_int(w, sr[(i - 6) & 7], sr[(i - 5) & 7], sr[(i - 3) & 7], sr[(i - 2) & 7]);
+                add_row(own ? xr[(i - 4) & 7] : 0.0, own ? dk : 0.0, Sx, Sxx, Sd, Sdx);
               } else {
-                xk = xr[(i - 2) & 7];
+                const double xk = own ? xr[(i - 2) & 7] : 0.0;
+                Sx += xk;
+                Sxx = fma(xk, xk, Sxx);
               }
-              xk = (t0 + i < e) ? xk : 0.0;
-              Sx += xk;
-              Sxx = fma(xk, xk, Sxx);
             }
           }
         }
@@ -497,19 +499,13 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
           const double a1 = sg_int(w, q[1], q[2], q[3], q[4], q[5]);  // xs[e-5]
           const double a2 = sg_int(w, q[2], q[3], q[4], q[5], q[6]);  // xs[e-4]
           const double a3 = sg_int(w, q[3], q[4], q[5], q[6], q[7]);  // xs[e-3]
-          if (has_body) {  // body rows a..b, b = e - 5
-            double hiSd, hiSdx;
-            tele_hi(w, a0, a1, a2, a3, hiSd, hiSdx);
-            Sd += hiSd - loSd;
-            Sdx += hiSdx - loSdx;
-          }
-          if (tail) {  // rows L-4 .. L-1
+          if (tail) {  // rows L-4 .. L-1: raw x[L-4 .. L-1] = q[4 .. 7]
             const double a4 = sg_pos3(q[3], q[4], q[5], q[6], q[7]);  // xs[L-2]
             const double a5 = sg_pos4(q[3], q[4], q[5], q[6], q[7]);  // xs[L-1]
-            add_row(a2, fd_int(w, a0, a1, a3, a4), Sx, Sxx, Sd, Sdx);
-            add_row(a3, fd_int(w, a1, a2, a4, a5), Sx, Sxx, Sd, Sdx);
-            add_row(a4, fd_pos3(a1, a2, a3, a4, a5) * w.inv_dt, Sx, Sxx, Sd, Sdx);
-            add_row(a5, fd_pos4(a1, a2, a3, a4, a5) * w.inv_dt, Sx, Sxx, Sd, Sdx);
+            add_row(q[4], fd_int(w, a0, a1, a3, a4), Sx, Sxx, Sd, Sdx);
+            add_row(q[5], fd_int(w, a1, a2, a4, a5), Sx, Sxx, Sd, Sdx);
+            add_row(q[6], fd_pos3(a1, a2, a3, a4, a5) * w.inv_dt, Sx, Sxx, Sd, Sdx);
+            add_row(q[7], fd_pos4(a1, a2, a3, a4, a5) * w.inv_dt, Sx, Sxx, Sd, Sdx);
           }
         } else {
           const double* q = qe;  // x[e-5 .. e-1]
@@ -872,7 +868,8 @@ discovery_finalize(const double* __restrict__ partial, int nblk, int narm_pad, i
 //   last sample: input x_{j+1}, derivative d_j (the backward difference at a segment end equals the
 //   forward difference of the sample before it).
 // So per step the lane adds (n, sx, sxx, n d, d sx), n = 1 + end, to arm a_j: one select per arm.
-// Smoothed: inside a segment xs_i = (x_i + x_{i+1}) / 2 except at its first and last sample (raw).
+// Smoothed: inside a segment xs_i = (x_i + x_{i+1}) / 2 except at its first and last sample (raw);
+// the derivative uses xs, the library the raw samples (pysindy smooths only for x_dot).
 // Per 64-patient tile the per-(patient, arm) moments are contracted to Gram entries (one entry per
 // lane, patients staged through LDS in two halves); block partials in the gram_kernel scalar layout
 // feed discovery_finalize.
@@ -980,16 +977,17 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
           const double x1 = (k0 + 1 + j <= L) ? xr[j] : 0.0;
           const int a1 = (k0 + 1 + j < L) ? ar[j] : -1;
           const bool endf = a1 != aj;  // sample j+1 closes j's segment (also at j+1 = L)
-          double xo, xs1;
+          const double xo = xj;  // library input: the raw sample (the smoothing feeds x_dot only)
+          double xso, xs1;
           if constexpr (SMOOTH1) {
             const double x2 = (k0 + 2 + j <= L) ? xr[j + 1] : 0.0;
-            xo = (aj != aprev) ? xj : 0.5 * (xj + x1);
+            xso = (aj != aprev) ? xj : 0.5 * (xj + x1);
             xs1 = endf ? x1 : 0.5 * (x1 + x2);
           } else {
-            xo = xj;
+            xso = xj;
             xs1 = x1;
           }
-          const double d = (xs1 - xo) * inv_dt;
+          const double d = (xs1 - xso) * inv_dt;
           const double xc = endf ? x1 : 0.0;
           const double n = endf ? 2.0 : 1.0;
           const double sx = xo + xc;

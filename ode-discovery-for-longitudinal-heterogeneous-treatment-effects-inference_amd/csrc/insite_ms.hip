@@ -264,7 +264,7 @@ gram_ms_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint
               z[0] = 1.0;
 #pragma unroll
               for (int s = 0; s < S; ++s) {
-                z[1 + s] = sr[(i + 4) & 7][s];
+                z[1 + s] = (double)xr[(i + 4) & 7][s];  // raw x[r]: the library sees the raw states
                 xd[s] = fd_int(w, sr[(i + 2) & 7][s], sr[(i + 3) & 7][s], sr[(i + 5) & 7][s], sr[(i + 6) & 7][s]);
               }
 #pragma unroll
@@ -288,7 +288,7 @@ gram_ms_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint
       // head window x[0..7] (clamped to the stored steps; values past L are never used)
 #pragma unroll
       for (int part = 0; part < 2; ++part) {
-        double xs[4][S], xdd[4][S];  // the 4 rows this part emits
+        double xs[4][S], xdd[4][S];  // the 4 rows this part emits: raw states, derivatives
         int base = 0;  // first step of the window
         if (part == 1) base = L >= 8 ? L - 8 : 0;
 #pragma unroll
@@ -333,7 +333,7 @@ gram_ms_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint
           }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            xs[q][s] = a8[4 * part + q];
+            xs[q][s] = xv[4 * part + q];  // raw sample of the row (smoothing feeds x_dot only)
             xdd[q][s] = d8[4 * part + q];
           }
         }

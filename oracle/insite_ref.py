@@ -25,23 +25,23 @@ lives in third-party **pysindy** (not vendored, version unpinned:
   sklearn's Cholesky solver, thresholding, stop rule) and the post-fit unbias
   (unregularised least squares on the support).
 
-It is pinned by (tests/test_oracle.py): the sub-oracles the reference's
-dependencies delegate to (``scipy.signal.savgol_filter``,
-``sklearn.linear_model.ridge_regression``, ``numpy.linalg.lstsq``,
-``scipy.integrate.solve_ivp``); the reference's own in-module known-answer
-tests for the integrator (``libs_m/ct/src/data/pkpd/utils.py:759-858``: y(t)=t
-for f≡1, MSE<1e-16); the analytic Euler-5 known answer for EQ_4_A
-(coefficient ≈ 30·ln(1−c/30)/c); and the reference's published
-run logs (``results/2_main_table/final_with_insite.txt:126,182``: discovered
-support and coefficients for EQ_4_A/EQ_4_C, RMSE anchors).  The exact pysindy
-end-stencil choice is "parity unpinned" beyond those anchors (SURVEY.md
-Appendix B).
+It is pinned against REFERENCE-HELD OUTPUTS: ``oracle/ref_cohort.py`` regenerates the
+reference's own EQ_4_A..D cohorts bit for bit (jax threefry restated in ``oracle/jax_prng.py``,
+seed 1 as logged), and this module's discovery on them returns the 16-digit equations of
+``results/2_main_table/final_with_insite.txt:126,154,182,210`` to ~1e-15, and its rollout +
+metrics the logged RMSEs (tests/test_reference_cohort.py).  That pins the savgol(5,3) stencils,
+pysindy's one-sided 5-point FD4 end stencils, the library on the RAW x (smoothing feeds x_dot
+only), STLSQ + unbias, the Euler-5 rollout and the metric definitions.  Further pins
+(tests/test_oracle.py): the sub-oracles the reference's dependencies delegate to
+(``scipy.signal.savgol_filter``, ``sklearn.linear_model.ridge_regression``,
+``numpy.linalg.lstsq``, ``scipy.integrate.solve_ivp``) and the reference's in-module
+known-answer test for the integrator (``libs_m/ct/src/data/pkpd/utils.py:759-858``).
 
-Deviations (documented in DESIGN.md): cohorts are drawn with numpy PCG64 in a
-fixed order instead of JAX threefry (not reproducible without jax); the time
-grid is ``k*dt`` with a constant Euler sub-step ``dt/5`` (the reference's
-``arange`` grid differs by ulps); ``dt`` is passed consistently to model and
-generator (reference hard-codes ``STANDARD_DT``).
+``make_collection`` below draws cohorts with numpy PCG64 (same distributions, fast, any size);
+``ref_cohort.make_collection`` is the bit-faithful variant.  The PCG64 path uses the time grid
+``k*dt`` with a constant Euler sub-step ``dt/5`` (the reference's ``arange`` grid differs by ulps)
+and passes ``dt`` consistently to model and generator (reference hard-codes ``STANDARD_DT``;
+SURVEY.md F9).
 """
 from __future__ import annotations
 
@@ -457,8 +457,11 @@ def fd_order1(x, dt):
 
 
 def smoothed_fd4(x, dt):
-    """SmoothedFiniteDifference(savgol 5/3, order=4): returns (smoothed x, x_dot).
-    pysindy's ``calc_trajectory`` feeds the smoothed x to the library."""
+    """SmoothedFiniteDifference(savgol 5/3, order=4): returns (smoothed x, x_dot).  Only x_dot
+    comes from the smoothed series: the library is evaluated on the RAW x (``build_regression``) —
+    pinned by reproducing the reference's logged EQ_4_A..D equations to ~1e-15 on its own
+    threefry cohorts (oracle/ref_cohort.py, tests/test_reference_cohort.py); evaluating the
+    library on the smoothed x misses them by 3e-6..4e-5."""
     xs = savgol_5_3(x)
     return xs, fd_order4(xs, dt)
 
@@ -658,20 +661,21 @@ def stlsq_gram(G, b, threshold, alpha, max_iter=100, unbias=True):
 # SINDy.fit equivalent (sindy.py:190-192) — multiple trajectories, per arm
 # --------------------------------------------------------------------------------------
 def build_regression(X_list, U_list, dt, fd="smoothed4"):
-    """Concatenate per-trajectory rows (multiple_trajectories=True): library inputs
-    [x (smoothed for SmoothedFiniteDifference), u] and targets x_dot."""
+    """Concatenate per-trajectory rows (multiple_trajectories=True): library inputs [x, u] with
+    the RAW x (also for SmoothedFiniteDifference, whose smoothing only feeds x_dot — pinned, see
+    ``smoothed_fd4``) and targets x_dot."""
     Z, Y = [], []
     for X, U in zip(X_list, U_list):
         x = X[:, 0]
         if fd == "smoothed4":
-            xs, xd = smoothed_fd4(x, dt)
+            _, xd = smoothed_fd4(x, dt)
         elif fd == "order4":
-            xs, xd = x, fd_order4(x, dt)
+            xd = fd_order4(x, dt)
         elif fd == "order1":
-            xs, xd = x, fd_order1(x, dt)
+            xd = fd_order1(x, dt)
         else:
             raise ValueError(fd)
-        Z.append(np.concatenate([xs[:, None], U], axis=1))
+        Z.append(np.concatenate([x[:, None], U], axis=1))
         Y.append(xd)
     return np.concatenate(Z, axis=0), np.concatenate(Y, axis=0)
 
@@ -704,7 +708,8 @@ def gram_moments(x, u, arm, rows, dt, exps, n_arms=2, fd="smoothed4"):
 
 
 def gram_moments_vectorized(x, u, arm, rows_const, dt, exps, n_arms=2):
-    """Vectorised variant for equal row counts (CPU baseline timing); smoothed FD4."""
+    """Vectorised variant for equal row counts (CPU baseline timing); smoothed FD4, library on
+    the raw x."""
     L = int(rows_const)
     X = x[:, :L]
     xs = np.empty_like(X)
@@ -729,7 +734,7 @@ def gram_moments_vectorized(x, u, arm, rows_const, dt, exps, n_arms=2):
     b = np.zeros((n_arms, F))
     for a in range(n_arms):
         sel = arm == a
-        Z = np.concatenate([xs[sel].reshape(-1, 1), np.repeat(u[sel], L, axis=0)], axis=1)
+        Z = np.concatenate([X[sel].reshape(-1, 1), np.repeat(u[sel], L, axis=0)], axis=1)
         th = eval_library(exps, Z)
         G[a] = th.T @ th
         b[a] = th.T @ D[sel].reshape(-1)

@@ -11,8 +11,9 @@ system.  It extends the reference's discovery semantics (pysindy SmoothedFiniteD
   * library = pysindy PolynomialLibrary(degree=2, interaction_only=True) over the inputs (x_1..x_5, a):
     F = 22 columns in pysindy order (``insite_ref.poly_library(6)``); joint (not arm-split) regression with
     the treatment as an input column, as the reference's joint mode does (pkpd/utils.py:488-497);
-  * derivative: savgol(5,3)-smoothed 4th-order FD per state over the patient's rows (the library sees the
-    smoothed states, as pysindy's calc_trajectory does — insite_ref.smoothed_fd4);
+  * derivative: savgol(5,3)-smoothed 4th-order FD per state over the patient's rows; the library sees the
+    RAW states (the smoothing feeds x_dot only — pinned on the reference's one-state cohorts, see
+    insite_ref.smoothed_fd4);
   * one STLSQ per target state on the shared Gram (insite_ref.stlsq_gram; pysindy fits targets separately);
   * rollout: RK4 (or Euler) of the discovered S-state system, treatment a_k held over interval k, RHS terms
     with |c| > 1e-3 (pkpd/utils.py:388), output = state after each interval (insite_ref.rollout convention).
@@ -110,14 +111,13 @@ def c3_cohort(N, T, seed=2, dt=DT_C3, substeps=10, p1=0.3, p_switch=0.01):
 
 
 def ms_regression(x, a, L, dt):
-    """Rows of one patient: library inputs Z [L, S+1] = (smoothed states, a) and targets xdot [L, S]
+    """Rows of one patient: library inputs Z [L, S+1] = (raw states, a) and targets xdot [L, S]
     (savgol(5,3) + FD4 per state, insite_ref.smoothed_fd4)."""
     X = np.asarray(x[:L], dtype=np.float64)
-    xs = np.empty_like(X)
     xd = np.empty_like(X)
     for s in range(X.shape[1]):
-        xs[:, s], xd[:, s] = R.smoothed_fd4(X[:, s], dt)
-    Z = np.concatenate([xs, np.asarray(a[:L], dtype=np.float64)[:, None]], axis=1)
+        _, xd[:, s] = R.smoothed_fd4(X[:, s], dt)
+    Z = np.concatenate([X, np.asarray(a[:L], dtype=np.float64)[:, None]], axis=1)
     return Z, xd
 
 
@@ -147,7 +147,7 @@ def ms_gram_vectorized(x, a, dt, exps):
     for s in range(S):
         xs[:, :, s] = R._stencil5(X[:, :, s].T, R.SAVGOL_5_3).T
         xd[:, :, s] = R._stencil5(xs[:, :, s].T, R.FD4).T / dt
-    Z = np.concatenate([xs, np.asarray(a, dtype=np.float64)[:, :, None]], axis=2).reshape(N * T, S + 1)
+    Z = np.concatenate([X, np.asarray(a, dtype=np.float64)[:, :, None]], axis=2).reshape(N * T, S + 1)
     th = R.eval_library(exps, Z)
     return th.T @ th, th.T @ xd.reshape(N * T, S)
 

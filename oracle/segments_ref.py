@@ -125,9 +125,8 @@ def derivative(x, dt, fd="order1"):
     """(library input, x_dot) of one segment."""
     if fd == "order1":
         return np.asarray(x, dtype=np.float64), R.fd_order1(x, dt)
-    if fd == "smoothed1":
-        xs = savgol_2_1(x)
-        return xs, R.fd_order1(xs, dt)
+    if fd == "smoothed1":   # the smoothing feeds x_dot only; the library takes the raw x (insite_ref.smoothed_fd4)
+        return np.asarray(x, dtype=np.float64), R.fd_order1(savgol_2_1(x), dt)
     raise ValueError(fd)
 
 
