@@ -51,6 +51,8 @@ def parse():
                          "overlapped (default); seq: eager launches on one stream; graph: the seq step in a HIP graph")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
+    ap.add_argument("--isolated", action="store_true",
+                    help="also time each C2 kernel in isolation (back-to-back launches on one stream)")
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "insite", "f4"],
                     help="c2: BASELINE configs[1], the headline line (default); c3: configs[2], the 5-state fp32 "
                          "system (parity-test configuration, measured separately)")
@@ -70,14 +72,22 @@ class HipEvents:
         self._hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         self._hip.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
         self._hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        self._hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
         self._events = []
 
-    def create(self):
+    def create(self, timing=False):
         e = self._c.c_void_p()
-        if self._hip.hipEventCreateWithFlags(self._c.byref(e), 0x2) != 0:   # hipEventDisableTiming
+        flags = 0x0 if timing else 0x2                                      # hipEventDisableTiming
+        if self._hip.hipEventCreateWithFlags(self._c.byref(e), flags) != 0:
             raise RuntimeError("hipEventCreateWithFlags failed")
         self._events.append(e)
         return e
+
+    def elapsed_ms(self, e0, e1):
+        ms = self._c.c_float()
+        if self._hip.hipEventElapsedTime(self._c.byref(ms), e0, e1) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return float(ms.value)
 
     def record(self, e, stream):
         if self._hip.hipEventRecord(e, self._c.c_void_p(stream)) != 0:
@@ -105,36 +115,134 @@ def gram_bytes(N, L, U=2, w=8):
     return N * L * w + N * (U * w + 1 + 4)
 
 
-def cpu_baseline(n_sample, T, method, seed):
-    """The oracle (numpy restatement) on a bounded sample of the same workload, 1 thread."""
-    sys.path.insert(0, ROOT)
-    from oracle import insite_ref as R
+# --------------------------------------------------------------------------------------------------
+# CPU baseline: the oracle's numpy restatement on every worker the host grants this
+# job, plus the scipy.integrate.solve_ivp(RK45) leg the north star names.  Run on rank 0 at N = 1,
+# BEFORE the GPU is initialised (the worker pool forks a GPU-free process).
+# --------------------------------------------------------------------------------------------------
+def host_info():
+    """CPU model, os.cpu_count(), the affinity mask and the worker count used."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0))
+    # the box grants a CPU share (OMP_NUM_THREADS is set to it there); os.cpu_count() is the machine
+    share = os.environ.get("INSITE_CPU_WORKERS") or os.environ.get("OMP_NUM_THREADS")
+    workers = max(1, min(aff, int(share))) if share else aff
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "sched_affinity": aff, "workers": workers}
+
+
+_CPU = {}
+
+
+def _cpu_worker_init():
+    """One BLAS thread per worker process (the pool supplies the parallelism)."""
     try:
         from threadpoolctl import threadpool_limits
-        limiter = threadpool_limits(limits=1)
+        _CPU["limiter"] = threadpool_limits(limits=1)
     except Exception:  # pragma: no cover
-        limiter = None
+        pass
+
+
+def _cpu_gram_chunk(bounds):
+    from oracle import insite_ref as R
+    lo, hi = bounds
+    d = _CPU
+    return R.gram_moments_vectorized(d["x"][lo:hi], d["u"][lo:hi], d["arm"][lo:hi], d["T"] - 2, d["dt"], d["exps"])
+
+
+def _cpu_rollout_chunk(bounds):
+    from oracle import insite_ref as R
+    lo, hi = bounds
+    d = _CPU
+    y = R.rollout(d["x"][lo:hi, 0], d["u"][lo:hi], d["arms"][lo:hi], d["coef"], d["exps"], d["dt"], method=d["method"])
+    return float(y[:, -1].sum())
+
+
+def _cpu_ivp_chunk(bounds):
+    """scipy.integrate.solve_ivp(RK45, rtol = atol = 1.4e-8) per patient over the whole horizon with the
+    piecewise-constant per-step arm, t_eval on the observation grid and max_step = dt/10 — the
+    reference's own call pattern (utils/exp_utils.py:140)."""
+    from scipy.integrate import solve_ivp
+    lo, hi = bounds
+    d = _CPU
+    T, dt, coef, exps = d["T"], d["dt"], d["coef"], d["exps"]
+    grid = np.arange(1, T + 1) * dt
+    acc = 0.0
+    for p in range(lo, hi):
+        u = d["u"][p]
+        arms = d["arms"][p]
+        mono = np.array([np.prod([u[i - 1] ** e[i] for i in range(1, e.size)]) for e in exps])
+        al = np.array([sum(coef[a, j] * mono[j] for j in range(exps.shape[0]) if exps[j, 0] == 0 and abs(coef[a, j]) > 1e-3)
+                       for a in range(coef.shape[0])])
+        be = np.array([sum(coef[a, j] * mono[j] for j in range(exps.shape[0]) if exps[j, 0] == 1 and abs(coef[a, j]) > 1e-3)
+                       for a in range(coef.shape[0])])
+
+        def f(t, y):
+            a = arms[min(int(t / dt), T - 1)]
+            return al[a] + be[a] * y
+        sol = solve_ivp(f, (0.0, T * dt), [d["x"][p, 0]], method="RK45", t_eval=grid, rtol=1.4e-8, atol=1.4e-8,
+                        max_step=dt / 10.0)
+        acc += float(sol.y[0, -1])
+    return acc
+
+
+def cpu_baseline(n_sample, T, method, seed, ivp_per_worker=100):
+    """Bounded CPU sample of the C2 workload (EQ_4_C cohort, T steps) on the host's workers:
+    (1) the oracle's numpy restatement, patients chunked over a process pool (partial Grams summed,
+        STLSQ, chunked rollout) — ``value``;
+    (2) scipy.integrate.solve_ivp(RK45, rtol = atol = 1.4e-8) per patient (the rollout only) on
+        ``ivp_per_worker`` patients per worker, extrapolated linearly — ``scipy_solve_ivp``."""
+    import multiprocessing as mp
+    sys.path.insert(0, ROOT)
+    from oracle import insite_ref as R
+    info = host_info()
+    W = info["workers"]
     rng = np.random.default_rng(seed)
     p = R.draw_params(n_sample, "EQ_4_C", rng)
     sim = R.simulate_factual(p, T, rng, "EQ_4_C", 2.0)
-    x = sim["cancer_volume"]
-    u = np.stack([sim["observed_static_c_0"], sim["observed_static_c_1"]], axis=1)
     arm = sim["treatment_application"][:, 0].astype(np.int64)
     flip = rng.integers(0, T, size=(n_sample, 1))
-    arms = np.where(np.arange(T)[None, :] >= flip, 1 - arm[:, None], arm[:, None])
-    exps = R.poly_library(3, 2, True)
-    dt = R.MAX_TIME_HORIZON / T
-    t0 = time.perf_counter()
-    G, b = R.gram_moments_vectorized(x, u, arm, T - 2, dt, exps)
-    coef = np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)])
-    R.rollout(x[:, 0], u, arms, coef, exps, dt, method=method)
-    el = time.perf_counter() - t0
-    if limiter is not None:
-        limiter.unregister()
-    return {"value": n_sample / el, "unit": "patient-trajectories/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/insite_ref.py numpy fp64 (vectorised over patients, 1 BLAS thread): "
-                      f"{n_sample} EQ_4_C patients x {T} steps, discovery + STLSQ + {method} rollout, "
-                      f"{el:.2f} s; host cpus={os.cpu_count()}"}
+    _CPU.update(x=sim["cancer_volume"], u=np.stack([sim["observed_static_c_0"], sim["observed_static_c_1"]], axis=1),
+                arm=arm, arms=np.where(np.arange(T)[None, :] >= flip, 1 - arm[:, None], arm[:, None]),
+                exps=R.poly_library(3, 2, True), dt=R.MAX_TIME_HORIZON / T, T=T, method=method)
+    chunks = [(int(a[0]), int(a[-1]) + 1) for a in np.array_split(np.arange(n_sample), W) if a.size]
+    ctx = mp.get_context("fork")          # no GPU context exists yet in this process
+    with ctx.Pool(W, initializer=_cpu_worker_init) as pool:
+        pool.map(abs, range(W))           # workers up before the clock starts
+        t0 = time.perf_counter()
+        parts = pool.map(_cpu_gram_chunk, chunks)
+        G = sum(q[0] for q in parts)
+        b = sum(q[1] for q in parts)
+        _CPU["coef"] = np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)])
+        el_disc = time.perf_counter() - t0
+    with ctx.Pool(W, initializer=_cpu_worker_init) as pool:   # forked after the fit: workers see the coefficients
+        pool.map(abs, range(W))
+        t1 = time.perf_counter()
+        pool.map(_cpu_rollout_chunk, chunks)
+        el_roll = time.perf_counter() - t1
+        n_ivp = min(n_sample, ivp_per_worker * W)
+        ivp_chunks = [(int(a[0]), int(a[-1]) + 1) for a in np.array_split(np.arange(n_ivp), W) if a.size]
+        t2 = time.perf_counter()
+        pool.map(_cpu_ivp_chunk, ivp_chunks)
+        el_ivp = time.perf_counter() - t2
+    total = el_disc + el_roll
+    return {"value": n_sample / total, "unit": "patient-trajectories/s", "cores": W, "kind": "port",
+            "sample": f"oracle/insite_ref.py numpy fp64 over a {W}-process pool: {n_sample} EQ_4_C patients x {T} "
+                      f"steps, discovery (chunked Gram + STLSQ) {el_disc:.2f} s + {method} rollout {el_roll:.2f} s",
+            "host": info,
+            "scipy_solve_ivp": {
+                "value": n_ivp / el_ivp, "unit": "patient-trajectories/s (rollout only)", "cores": W,
+                "kind": "scipy.integrate.solve_ivp(method='RK45', rtol=atol=1.4e-8, max_step=dt/10, t_eval=grid)",
+                "sample": f"{n_ivp} patients x {T} steps on {W} workers in {el_ivp:.2f} s; the rate extrapolates "
+                          f"linearly in patients (independent solves); {n_sample} patients would take "
+                          f"{el_ivp * n_sample / n_ivp:.1f} s"}}
 
 
 def c3_main(args):
@@ -232,19 +340,68 @@ def c3_main(args):
     print(json.dumps(out))
 
 
+C5_COEF = (-1.1108, -0.1454, -1.0235)   # the EQ_4_C model of the reference log (final_with_insite.txt:182)
+# fp64 VALU work of one RK45 step attempt (rollout_rk45_kernel, rk45_ref.rk45_interval): 6 stage RHS
+# evaluations of alpha + beta*y (1 FMA each), 21 stage-combination FMAs (Dormand-Prince a_ij), 5th-order
+# update (6 FMA), error estimate (7 FMA), error norm (scale, ratio, square: 4 ops), step-size factor
+# (rk45_inv_root5: ~20 ops), accept/reject bookkeeping (~6 ops) -> ~71 fp64 ops, 2 flops per FMA:
+RK45_FLOP_PER_ATTEMPT = 2 * (6 + 21 + 6 + 7) + 4 + 20 + 6
+FP64_VALU_PEAK_TFLOPS = 78.6            # MI355X spec FP64 vector
+
+
+def _cpu_rk45_chunk(bounds):
+    from oracle import rk45_ref as K
+    lo, hi = bounds
+    d = _CPU
+    K.rollout_rk45(d["y0"][lo:hi], d["u"][lo:hi], d["arm"][lo:hi], d["t"][lo:hi], d["n"][lo:hi], d["coef"], d["exps"])
+    return hi - lo
+
+
+def c5_cpu_baseline(n_sample, seed):
+    """oracle/rk45_ref.py (scipy 1.15 RK45 restated, pinned to solve_ivp at 1e-13) on a process pool over
+    a bounded sample of the C5 workload, before any GPU context exists."""
+    import multiprocessing as mp
+    sys.path.insert(0, ROOT)
+    from oracle import insite_ref as R
+    from oracle import rk45_ref as K
+    info = host_info()
+    W = info["workers"]
+    rng = np.random.default_rng(seed)
+    t, n = K.irregular_grid(n_sample, rng)
+    coef = np.zeros((2, 7))
+    coef[0, 4], coef[1, 1], coef[1, 5] = C5_COEF
+    _CPU.update(t=t, n=n, y0=rng.uniform(1, 50, n_sample), u=rng.normal(0.5, 0.05, (n_sample, 2)),
+                arm=rng.integers(0, 2, (n_sample, t.shape[1])), coef=coef, exps=R.poly_library(3, 2, True))
+    chunks = [(int(c[0]), int(c[-1]) + 1) for c in np.array_split(np.arange(n_sample), W) if c.size]
+    with mp.get_context("fork").Pool(W, initializer=_cpu_worker_init) as pool:
+        pool.map(abs, range(W))
+        t0 = time.perf_counter()
+        pool.map(_cpu_rk45_chunk, chunks)
+        el = time.perf_counter() - t0
+    return {"value": n_sample / el, "unit": "patient-trajectories/s", "cores": W, "kind": "port",
+            "sample": f"oracle/rk45_ref.py (scipy RK45 restated) on {n_sample} irregular-grid patients over {W} "
+                      f"worker processes, {el:.2f} s", "host": info}
+
+
 def c5_main(args):
     """Configuration C5 (BASELINE.json configs[4]): PK/PD EQ_4_C model rolled out with the adaptive
     RK45 controller (scipy solve_ivp semantics, rtol = atol = 1.4e-8) on per-patient irregular grids
-    (20..60 observations on [0, 10]), 1M patients; arms switch per interval.  One step = one rollout
-    of every patient.  Lane-level step-size control: waves run until their slowest lane finishes."""
+    (20..60 observations on [0, 10]), 1M patients sharded over the ranks (strong scaling: configs[4] fixes
+    1M patients on 8 GPUs; no collective on the data path); arms switch per interval.  One step = one
+    rollout of every patient.  Lane-level step-size control: waves run until their slowest lane finishes."""
+    cpu = None
+    if os.environ.get("WORLD_SIZE", "1") == "1" and not args.no_cpu_baseline:
+        cpu = c5_cpu_baseline(min(args.cpu_sample, 4000), args.seed + 4)
+    world, rank, dev = dist_setup()
     from insite_amd import ops, cohort
+    from insite_amd import dist as idist
     from insite_amd.library import polynomial_library
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
-    N = args.patients if args.patients != 100_000 else 1_000_000
+    N_total = args.patients if args.patients != 100_000 else 1_000_000
+    lo, hi = idist.shard_bounds(N_total, rank, world)
+    N = hi - lo
     g = torch.Generator(device=dev)
-    g.manual_seed(args.seed + 5)
-    t_obs, n_obs = cohort.irregular_grid(N, seed=args.seed + 4, device=dev)
+    g.manual_seed(args.seed * 1000 + 5 + rank)
+    t_obs, n_obs = cohort.irregular_grid(N, seed=args.seed * 1000 + 4 + rank, device=dev)
     Tm = t_obs.size(0)
     t_dev = torch.nan_to_num(t_obs, nan=0.0)
     u = torch.randn((N, 2), generator=g, device=dev, dtype=torch.float64) * 0.05 + 0.5
@@ -253,7 +410,7 @@ def c5_main(args):
     bits = ops.pack_arm_bits(arm, N)
     lib = polynomial_library(2, 2, True)
     coef = torch.zeros((2, lib.n_terms), dtype=torch.float64, device=dev)
-    coef[0, 4], coef[1, 1], coef[1, 5] = -1.1108, -0.1454, -1.0235   # the EQ_4_C model (log :182)
+    coef[0, 4], coef[1, 1], coef[1, 5] = C5_COEF
     y = torch.empty((Tm, N), dtype=torch.float64, device=dev)
     steps = torch.empty((N,), dtype=torch.int32, device=dev)
 
@@ -263,39 +420,57 @@ def c5_main(args):
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run()
     torch.cuda.synchronize(dev)
-    ms_step = (time.perf_counter() - t0) / args.steps * 1e3
+    if world > 1:
+        dist.barrier()
+    ms_step = idist.max_over_ranks(time.perf_counter() - t0, dev) / args.steps * 1e3
+    # per-launch duration with HIP events on the launch stream (instrumented pass after the timed region)
+    st_ = torch.cuda.current_stream(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(max(args.steps, 5))]
+    for e0, e1 in evs:
+        e0.record(st_)
+        run()
+        e1.record(st_)
+    torch.cuda.synchronize(dev)
+    launch_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     st = steps.to(torch.float64)
     per_wave = st[: N // 64 * 64].view(-1, 64)
     intervals = (n_obs - 1).to(torch.float64)
+    attempts = float(st.sum())
+    flop = attempts * RK45_FLOP_PER_ATTEMPT
+    issued = float(per_wave.max(dim=1).values.sum()) * 64 * RK45_FLOP_PER_ATTEMPT   # lanes idle behind the slowest
     out = {
-        "metric": METRIC, "value": N / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": 1,
+        "metric": METRIC, "value": N_total / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: irregular grids T_p ~ U{20..60} on [0,10], EQ_4_C statics, random per-interval arms",
-        "config": {"workload": f"C5: adaptive RK45 (rtol=atol=1.4e-8) on irregular grids, {N // 1000}k patients",
-                   "patients": N, "max_obs": Tm, "mean_intervals": float(intervals.mean())},
+        "config": {"workload": f"C5: adaptive RK45 (rtol=atol=1.4e-8) on irregular grids, {N_total // 1000}k patients",
+                   "patients_total": N_total, "patients_per_gpu": N, "max_obs": Tm,
+                   "mean_intervals": float(intervals.mean()), "parallelism": f"patient-shard x{world}"},
+        "roofline": {"kernel": "rollout_rk45_kernel", "bound": "valu-f64", "unit": "TFLOP/s",
+                     "achieved": flop / (launch_ms * 1e-3) / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
+                     "frac": flop / (launch_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS, "traffic": None,
+                     "avg_launch_ms": launch_ms, "flop_per_attempt": RK45_FLOP_PER_ATTEMPT,
+                     "issued_incl_divergence_TFLOPs": issued / (launch_ms * 1e-3) / 1e12,
+                     "algorithmic_bytes": N * (8 * 3 + 4) + N * Tm * 8 * 2 + Tm * ((N + 31) // 32) * 4,
+                     "achieved_GBps": (N * (8 * 3 + 4) + N * Tm * 8 * 2 + Tm * ((N + 31) // 32) * 4) / (launch_ms * 1e-3) / 1e9},
         "rk45": {"mean_attempts_per_patient": float(st.mean()),
                  "mean_attempts_per_interval": float(st.sum() / intervals.sum()),
                  "wave_divergence": float((per_wave.max(dim=1).values.mean() / per_wave.mean()).item()),
-                 "rhs_evals_per_s": float(st.sum() * 6 / (ms_step * 1e-3))},
+                 "rhs_evals_per_s": float(st.sum() * 6 / (launch_ms * 1e-3))},
     }
-    if not args.no_cpu_baseline:
-        sys.path.insert(0, ROOT)
-        from oracle import rk45_ref as K
-        n_s = min(args.cpu_sample, 2000)
-        tc, nc = t_obs[:, :n_s].T.cpu().numpy(), n_obs[:n_s].cpu().numpy()
-        t1 = time.perf_counter()
-        K.rollout_rk45(y0[:n_s].cpu().numpy(), u[:n_s].cpu().numpy(), arm[:, :n_s].T.cpu().numpy(), tc, nc,
-                       coef.cpu().numpy(), lib.exps.astype(np.int64))
-        el = time.perf_counter() - t1
-        out["cpu_baseline"] = {"value": n_s / el, "unit": "patient-trajectories/s", "cores": 1, "kind": "port",
-                               "sample": f"oracle/rk45_ref.py (scalar restatement of scipy RK45) on {n_s} patients, "
-                                         f"{el:.2f} s"}
-    print(json.dumps(out))
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def insite_main(args):
@@ -471,14 +646,7 @@ def c4_main(args):
     (N_total / world per rank: strong scaling, as configs[3] fixes 1M patients on 8 GPUs)."""
     from insite_amd import ops, cohort
     from insite_amd import dist as idist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = 0 if os.environ.get("INSITE_REHEARSE_ONE_GPU") else int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        backend = os.environ.get("INSITE_DIST_BACKEND", "nccl")
-        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
+    world, rank, dev = dist_setup()
     N_total = args.patients if args.patients != 100_000 else 1_000_000
     T = args.T if args.T != 200 else 60
     lo, hi = idist.shard_bounds(N_total, rank, world)
@@ -572,8 +740,46 @@ def c4_main(args):
         dist.destroy_process_group()
 
 
+def launch_ranks(args):
+    """``--gpus N`` (N > 1) without a torch.distributed environment: start N ranks (one per GPU) through
+    torchrun as a CHILD process — before anything touches the GPU — and exit with its status.  Inside a
+    distributed launch, WORLD_SIZE must equal --gpus (exit 2 otherwise)."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is None:
+        if args.gpus <= 1:
+            return
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+        sys.exit(subprocess.call(cmd))
+    if int(world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a mislabelled run",
+              file=sys.stderr)
+        sys.exit(2)
+
+
+def dist_setup():
+    """(world, rank, device) of this process; joins the process group when world > 1.  Rehearsal knobs
+    for a one-GPU box (never set by the driver): INSITE_REHEARSE_ONE_GPU puts every rank on cuda:0 and
+    INSITE_DIST_BACKEND=gloo swaps RCCL for gloo."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = 0 if os.environ.get("INSITE_REHEARSE_ONE_GPU") else int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        backend = os.environ.get("INSITE_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
+    return world, rank, dev
+
+
 def main():
     args = parse()
+    launch_ranks(args)
     if args.config == "f4":
         return f4_main(args)
     if args.config == "c4":
@@ -584,23 +790,11 @@ def main():
         return c3_main(args)
     if args.config == "c5":
         return c5_main(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    # rehearsal knobs for a one-GPU box (never set by the driver): every rank on cuda:0 over gloo, which
-    # exercises the multi-rank step (shards, the all-reduce on the STLSQ stream, max-over-ranks timing)
-    if os.environ.get("INSITE_REHEARSE_ONE_GPU"):
-        local = 0
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        backend = os.environ.get("INSITE_DIST_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+    # the CPU leg runs first, while this process has no GPU context (its worker pool forks)
+    cpu = None
+    if os.environ.get("WORLD_SIZE", "1") == "1" and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_sample, args.T, args.method, args.seed)
+    world, rank, dev = dist_setup()
 
     from insite_amd import ops, cohort
     from insite_amd import dist as idist
@@ -668,16 +862,29 @@ def main():
                 idist.reduce_moments(bufs[j])       # the only collective
             stlsq_plans[j](st)
 
-    def step(i):
+    def step(i, tev=None):
+        """One step; ``tev`` = (gram start, gram end, rollout start, rollout end) timing events recorded
+        on the streams those kernels run on (the instrumented pass)."""
         j = i % 2
         if mode != "pipeline":                      # current stream: the capture stream under graph capture
             st = torch.cuda.current_stream(dev)
+            if tev:
+                hip.record(tev[0], st.cuda_stream)
             discover(i, st)
+            if tev:
+                hip.record(tev[1], st.cuda_stream)
+                hip.record(tev[2], st.cuda_stream)
             roll_plans[j](st)
+            if tev:
+                hip.record(tev[3], st.cuda_stream)
             return
         if last_c[j] is not None:
             hip.wait(hs["g"], last_c[j])            # step i-2's STLSQ has read G|b[j]
+        if tev:
+            hip.record(tev[0], hs["g"])
         g_fast[j]()
+        if tev:
+            hip.record(tev[1], hs["g"])
         hip.record(ev["g", j], hs["g"])
         hip.wait(hs["c"], ev["g", j])
         if world > 1:
@@ -689,7 +896,11 @@ def main():
         hip.record(ev["c", j], hs["c"])
         last_c[j] = ev["c", j]
         hip.wait(hs["r"], ev["c", j])
+        if tev:
+            hip.record(tev[2], hs["r"])
         r_fast[j]()
+        if tev:
+            hip.record(tev[3], hs["r"])
         hip.record(ev["r", j], hs["r"])
         last_r[j] = ev["r", j]
 
@@ -722,8 +933,28 @@ def main():
     coef = coefs[0] if mode == "graph" else coefs[(args.steps - 1) % 2]
     mask = masks[0] if mode == "graph" else masks[(args.steps - 1) % 2]
 
-    # roofline pass (outside the timed region): each phase's kernels launched back to back on one
-    # stream between two HIP events; avg = elapsed / launches.  Same kernels, same inputs.
+    # instrumented pass (after the timed region): the same schedule again — same streams, same overlap —
+    # with HIP timing events around the gram and rollout launches on the streams they run on.  Per-launch
+    # averages of the kernels exactly as they run in the step; a rocprofv3 --kernel-trace --stats run of
+    # this bench (--no-north-star) averages the same pipelined launches (profiles/).
+    n_inst = max(args.steps, 10)
+    tevs = [tuple(hip.create(timing=True) for _ in range(4)) for _ in range(n_inst)]
+    if mode == "graph":
+        for i in range(n_inst):
+            hip.record(tevs[i][0], torch.cuda.current_stream(dev).cuda_stream)
+            graph.replay()
+            hip.record(tevs[i][3], torch.cuda.current_stream(dev).cuda_stream)
+    else:
+        for i in range(n_inst):
+            step(args.steps + i, tevs[i])
+    torch.cuda.synchronize(dev)
+    if mode == "graph":
+        roll_ms = disc_ms = float(np.mean([hip.elapsed_ms(t[0], t[3]) for t in tevs]))
+    else:
+        disc_ms = float(np.mean([hip.elapsed_ms(t[0], t[1]) for t in tevs]))
+        roll_ms = float(np.mean([hip.elapsed_ms(t[2], t[3]) for t in tevs]))
+
+    # isolated launches (reported beside it, not as the roofline): each kernel back to back on one stream
     def timed(fn, n):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st = torch.cuda.current_stream(dev)
@@ -734,9 +965,10 @@ def main():
         torch.cuda.synchronize(dev)
         return e0.elapsed_time(e1) / n
 
-    n_roof = max(args.steps, 10)
-    roll_ms = timed(roll_plans[0], n_roof)
-    disc_ms = timed(lambda st: discover(0, st), n_roof)
+    iso = None
+    if args.isolated:
+        iso = {"rollout_avg_launch_ms": timed(roll_plans[0], n_inst),
+               "gram_avg_launch_ms": timed(gram_plans[0], n_inst)}
 
     # sanity on the measured result: discovered support is the EQ_4_C one, no NaN
     sup = mask.cpu().numpy()
@@ -786,6 +1018,8 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": rb,
                 "avg_launch_ms": roll_ms,
+                "avg_ms_source": "instrumented pass: the timed schedule replayed with HIP timing events around "
+                                 "each rollout launch on its own stream (concurrent with the next step's gram)",
                 "layout": {"time_bits": "time-major x[T,N], 1-bit arm mask [T,N/32], y[T,N]",
                            "time": "time-major x[T,N], int8 arm[T,N], y[T,N]",
                            "patient": "patient-major x[N,T], int8 arm[N,T], y[N,T]"}[roll_layout],
@@ -797,13 +1031,22 @@ def main():
                                  "seq": "eager launches, one stream, strictly sequential",
                                  "pipeline": "gram+reduce | [all-reduce+] STLSQ | rollout on three streams, "
                                              "double-buffered, consecutive steps overlapped"}[mode],
-                "avg_ms_source": "roofline pass: back-to-back launches between two HIP events",
+                "avg_ms_source": "instrumented pass: HIP timing events around each gram launch on its stream "
+                                 "(gram + block partials; the finalize/STLSQ launch runs on the next stream)"
+                                 if mode == "pipeline" else "instrumented pass: HIP timing events around discovery",
                 "avg_ms": disc_ms,
                 "algorithmic_bytes": gram_bytes(N, T),
                 "achieved_GBps": gram_bytes(N, T) / (disc_ms * 1e-3) / 1e9,
                 "frac": gram_bytes(N, T) / (disc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
             },
+            # both kernels share HBM inside a step: the step's whole algorithmic traffic over its time
+            "step_aggregate": {"algorithmic_bytes": rb + gram_bytes(N, T),
+                               "achieved_GBps": (rb + gram_bytes(N, T)) / (ms_step * 1e-3) / 1e9,
+                               "frac": (rb + gram_bytes(N, T)) / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS},
         }
+        if iso is not None:
+            out["isolated"] = dict(iso, rollout_frac=rb / (iso["rollout_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                                   gram_frac=gram_bytes(N, T) / (iso["gram_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS)
     # north-star probe: 1M x 500 RK4 rollout alone (the >= 40 % roofline target), rank 0, N = 1
     if rank == 0 and world == 1 and not args.no_north_star:
         del y
@@ -837,8 +1080,8 @@ def main():
                                      "algorithmic_bytes": bn, "achieved_GBps": bn / (ms * 1e-3) / 1e9,
                                      "frac_of_8TBps": bn / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                                      "patient_trajectories_per_s": Nn / (ms * 1e-3)}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_sample, T, args.method, args.seed)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

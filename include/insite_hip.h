@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define INSITE_ABI_VERSION 1
+#define INSITE_ABI_VERSION 2
 
 /* status codes */
 #define INSITE_OK 0
@@ -225,7 +225,10 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
  *   f(c) = mse(c) / (2.5 mse(coef0)) + lam * mean((coef0 - c)^2),
  *   mse  = mean_{k < min(seq_len - tau, T - 1)} (V[k + 1] - pred_k)^2, pred = the Euler scan
  *          (`substeps` sub-steps per dt; 5 = odeint) from V[0] under the row's per-step arms;
- * BFGS status 3 (zoom failed) keeps coef0 (sindy.py:628-631).  Every row then gets the Euler scan
+ * revert_on_zoom_fail != 0: BFGS status 3 (zoom failed) keeps coef0, as the reference CODE reads
+ * (sindy.py:628-631); 0: the row keeps its BFGS iterate, which is what the reference's PUBLISHED runs
+ * show (all eight EQ_4 INSITE metrics of results/2_main_table/final_with_insite.txt:2387-2402 are
+ * reproduced to 1e-10 only without the revert).  Every row then gets the Euler scan
  * of its (refined or global) model over all T steps.
  *   V        [T, ld_v] f64 unscaled observations, time-major (ld_v >= n_rows)
  *   arm_bits TIME_MAJOR_BITS [T, ld_arm] per-step arm (n_arms <= 2)
@@ -237,8 +240,8 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
 int32_t insite_refine_f64(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, int64_t ld_arm,
                           const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics, const int8_t* exps,
                           int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam, int32_t tau,
-                          int32_t substeps, double* preds, int64_t ld_p, double* coef_out, int32_t* status_out,
-                          int32_t* iters_out, void* stream);
+                          int32_t substeps, int32_t revert_on_zoom_fail, double* preds, int64_t ld_p,
+                          double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream);
 
 /* INSITE refinement with int8 per-step arms, n_arms <= 4: the cancer_sim / EQ_5 branches of
  * _get_fine_tuned_predictions (sindy.py:484-550: pred_dy_dt picks all_reduced_coefs[argmax(treatment)])
@@ -247,8 +250,8 @@ int32_t insite_refine_f64(const double* V, int64_t ld_v, int32_t T, const uint32
 int32_t insite_refine_arms_f64(const double* V, int64_t ld_v, int32_t T, const int8_t* arm, int64_t ld_arm,
                                const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
                                const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt,
-                               double lam, int32_t tau, int32_t substeps, double* preds, int64_t ld_p,
-                               double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream);
+                               double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail, double* preds,
+                               int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream);
 
 /* Masked squared-error sums for the RMSE metrics (time_varying_model.py:236-313):
  *   err[r,k]  = (pred[r, k] * scale + shift - target[r, k])^2 * active[r, k]
@@ -315,8 +318,10 @@ int32_t insite_rollout_ms_f32(const float* y0, int64_t ld_y0, const uint32_t* in
  * supported terms, in the library's column order — the same fp32 sums as the dense kernel, whose dropped
  * terms add fmaf(0, th, f) = f.  Coefficient values are read from `coef` (device) at every launch; if
  * any coefficient outside the support is above drop_below, the launch runs the dense RHS instead (a
- * stale support costs speed, not correctness).  Other arguments and results as insite_rollout_ms_f32;
- * INSITE_E_HIP if hipRTC or the module load fails. */
+ * stale support costs speed, not correctness).  Other arguments and results as insite_rollout_ms_f32.
+ * The kernel is compiled for the current device's ISA (hipDeviceProp_t.gcnArchName); if hipRTC or the
+ * module load fails, or 64 supports are already cached, the launch runs insite_rollout_ms_f32 (dense
+ * RHS, bitwise the same result). */
 int32_t insite_rollout_ms_sparse_f32(const float* y0, int64_t ld_y0, const uint32_t* inp_bits, int64_t ld_bits,
                                      const double* coef, const int8_t* support, const int8_t* exps, int32_t n_terms,
                                      int32_t n_states, int64_t n_rows, int32_t T, double dt, int32_t method,

@@ -1872,6 +1872,7 @@ struct RefineArgs {
   int32_t* iters;       // [N] or NULL
   int64_t ldv, lda, ldp, N;
   int32_t T, tau, sub, A, m, n_total;
+  int32_t revert3;      // 1: BFGS status 3 reverts to the global model (sindy.py:628-631); 0: keep the iterate
   double dt, lam;
   int32_t t_flat[kRefineMaxActive], t_arm[kRefineMaxActive], t_ex[kRefineMaxActive], t_col[kRefineMaxActive];
   double c0[INSITE_MAX_ARMS * INSITE_MAX_TERMS];  // the global model [A, F]
@@ -2249,7 +2250,7 @@ insite_refine_kernel(RefineArgs ra, LibDesc lib) {
     }
     nit = k;
     status = converged ? 0 : (k == maxiter ? 1 : (failed ? 2 + ls_status : -1));
-    if (status == 3) {  // zoom failed: the reference keeps the global coefficients (sindy.py:628-631)
+    if (status == 3 && ra.revert3) {  // zoom failed: the reference code keeps the global coefficients (sindy.py:628-631)
 #pragma unroll RU
       for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
     }
@@ -3119,8 +3120,8 @@ namespace {
 int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, const int8_t* arm8,
                       int64_t ld_arm, const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
                       const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam,
-                      int32_t tau, int32_t substeps, double* preds, int64_t ld_p, double* coef_out,
-                      int32_t* status_out, int32_t* iters_out, void* stream) {
+                      int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail, double* preds, int64_t ld_p,
+                      double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream) {
   const bool bits = arm8 == nullptr;
   if (n_rows < 0 || T < 1 || n_arms < 1 || n_arms > (bits ? 2 : 4) || substeps < 1 || !(dt > 0.0) ||
       !(lam >= 0.0) || tau < 0 || ld_v < n_rows || ld_p < n_rows ||
@@ -3148,6 +3149,7 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
   ra.T = T;
   ra.tau = tau;
   ra.sub = substeps;
+  ra.revert3 = revert_on_zoom_fail != 0;
   ra.A = n_arms;
   ra.n_total = n_arms * n_terms;
   ra.dt = dt;
@@ -3187,23 +3189,24 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
 int32_t insite_refine_f64(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, int64_t ld_arm,
                           const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics, const int8_t* exps,
                           int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam, int32_t tau,
-                          int32_t substeps, double* preds, int64_t ld_p, double* coef_out, int32_t* status_out,
-                          int32_t* iters_out, void* stream) {
+                          int32_t substeps, int32_t revert_on_zoom_fail, double* preds, int64_t ld_p,
+                          double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream) {
   if (!arm_bits && n_rows > 0) return INSITE_E_INVALID_ARG;
   return refine_launch(V, ld_v, T, arm_bits, nullptr, ld_arm, u, seq_len, n_rows, n_statics, exps, n_terms, coef0,
-                       n_arms, dt, lam, tau, substeps, preds, ld_p, coef_out, status_out, iters_out, stream);
+                       n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds, ld_p, coef_out, status_out,
+                       iters_out, stream);
 }
 
 int32_t insite_refine_arms_f64(const double* V, int64_t ld_v, int32_t T, const int8_t* arm, int64_t ld_arm,
                                const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
                                const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt,
-                               double lam, int32_t tau, int32_t substeps, double* preds, int64_t ld_p,
-                               double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream) {
+                               double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail, double* preds,
+                               int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream) {
   if (!arm && n_rows > 0) return INSITE_E_INVALID_ARG;
   static const int8_t kNoArms = 0;  // non-null marker for the int8 format when n_rows == 0
   return refine_launch(V, ld_v, T, nullptr, arm ? arm : &kNoArms, ld_arm, u, seq_len, n_rows, n_statics, exps,
-                       n_terms, coef0, n_arms, dt, lam, tau, substeps, preds, ld_p, coef_out, status_out, iters_out,
-                       stream);
+                       n_terms, coef0, n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds, ld_p, coef_out,
+                       status_out, iters_out, stream);
 }
 
 size_t insite_masked_sse_workspace_bytes(int64_t n_rows, int32_t T) {

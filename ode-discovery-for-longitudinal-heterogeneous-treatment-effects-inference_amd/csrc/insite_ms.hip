@@ -882,7 +882,11 @@ std::string ms_sparse_source(int method, const int8_t* support) {
   return src;
 }
 
-// Compiled kernels, one per (device, source); compiled once under the lock and never evicted.
+// Compiled kernels, one per (device, source), compiled once under the lock.  A support that fails to
+// compile or load is remembered as nullptr (the caller then takes the dense kernel and the compile is not
+// retried).  The cache is bounded: past kMsJitMax entries new supports run the dense kernel (a model
+// family has few distinct supports; the entries' modules stay loaded for the process lifetime).
+constexpr size_t kMsJitMax = 64;
 struct MsJitCache {
   std::mutex mu;
   std::map<std::pair<int, std::string>, hipFunction_t> fns;
@@ -900,26 +904,35 @@ hipFunction_t ms_jit_function(const std::string& src) {
   const auto key = std::make_pair(dev, src);
   auto it = c.fns.find(key);
   if (it != c.fns.end()) return it->second;
+  if (c.fns.size() >= kMsJitMax) return nullptr;
+  hipFunction_t fn = nullptr;
+  // the target is the current device's own ISA (gcnArchName, e.g. "gfx950:sramecc+:xnack-")
+  hipDeviceProp_t prop;
+  std::string arch = "--offload-arch=gfx950";
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.gcnArchName[0])
+    arch = std::string("--offload-arch=") + std::string(prop.gcnArchName).substr(0, std::string(prop.gcnArchName).find(':'));
   hiprtcProgram prog;
-  if (hiprtcCreateProgram(&prog, src.c_str(), "insite_ms_sparse.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
-    return nullptr;
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast-honor-pragmas"};
-  const bool ok = hiprtcCompileProgram(prog, 4, opts) == HIPRTC_SUCCESS;
   std::vector<char> code;
-  if (ok) {
-    size_t n = 0;
-    if (hiprtcGetCodeSize(prog, &n) == HIPRTC_SUCCESS && n > 0) {
-      code.resize(n);
-      if (hiprtcGetCode(prog, code.data()) != HIPRTC_SUCCESS) code.clear();
+  if (hiprtcCreateProgram(&prog, src.c_str(), "insite_ms_sparse.hip", 0, nullptr, nullptr) == HIPRTC_SUCCESS) {
+    const char* opts[] = {arch.c_str(), "-O3", "-std=c++17", "-ffp-contract=fast-honor-pragmas"};
+    if (hiprtcCompileProgram(prog, 4, opts) == HIPRTC_SUCCESS) {
+      size_t n = 0;
+      if (hiprtcGetCodeSize(prog, &n) == HIPRTC_SUCCESS && n > 0) {
+        code.resize(n);
+        if (hiprtcGetCode(prog, code.data()) != HIPRTC_SUCCESS) code.clear();
+      }
+    }
+    hiprtcDestroyProgram(&prog);
+  }
+  hipModule_t mod = nullptr;
+  if (!code.empty() && hipModuleLoadData(&mod, code.data()) == hipSuccess) {
+    if (hipModuleGetFunction(&fn, mod, "ms_rollout_sparse") != hipSuccess) {
+      fn = nullptr;
+      (void)hipModuleUnload(mod);
     }
   }
-  hiprtcDestroyProgram(&prog);
-  if (code.empty()) return nullptr;
-  hipModule_t mod;
-  hipFunction_t fn;
-  if (hipModuleLoadData(&mod, code.data()) != hipSuccess) return nullptr;
-  if (hipModuleGetFunction(&fn, mod, "ms_rollout_sparse") != hipSuccess) return nullptr;
-  c.fns.emplace(key, fn);
+  (void)hipGetLastError();  // a failed compile / load must not leak into the caller's launch status
+  c.fns.emplace(key, fn);   // nullptr remembered: the dense kernel serves this support
   return fn;
 }
 
@@ -1025,7 +1038,9 @@ int32_t insite_rollout_ms_sparse_f32(const float* y0, int64_t ld_y0, const uint3
   if ((int64_t)n_states * ld_y * 4 >= ((int64_t)1 << 31)) return INSITE_E_UNSUPPORTED;  // 32-bit step offsets
   const std::string src = nin ? ms_sparse_source<5, 1>(method, support) : ms_sparse_source<5, 0>(method, support);
   hipFunction_t fn = ms_jit_function(src);
-  if (!fn) return INSITE_E_HIP;
+  if (!fn)  // no specialised kernel for this support (compile / load failure, cache full): dense RHS
+    return insite_rollout_ms_f32(y0, ld_y0, inp_bits, ld_bits, coef, exps, n_terms, n_states, n_rows, T, dt, method,
+                                 substeps, drop_below, y_out, ld_y, stream);
   long long ld0 = ld_y0, lda = ld_bits, ldy = ld_y, N = n_rows;
   int Ti = T, sub = substeps;
   double dti = dt, drop = drop_below;

@@ -37,11 +37,69 @@ def shard_bounds(n_total: int, rank: int, world: int) -> tuple[int, int]:
     return lo, lo + q + (1 if rank < r else 0)
 
 
-def reduce_moments(buf: MomentBuffer, group=None) -> MomentBuffer:
-    """Sum the per-rank partial (G, b) over all ranks in place (one all-reduce)."""
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(buf.flat, op=dist.ReduceOp.SUM, group=group)
+def _world(group=None) -> int:
+    return dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+
+
+def fixed_order_sum(t: torch.Tensor, group=None) -> torch.Tensor:
+    """Deterministic cross-rank sum in place: all-gather the per-rank buffers and add them in rank
+    order on every rank (bitwise reproducible, and equal to a fixed-order CPU sum of the same partials;
+    SURVEY.md §5 "deterministic option")."""
+    W = _world(group)
+    if W > 1:
+        parts = [torch.empty_like(t) for _ in range(W)]
+        dist.all_gather(parts, t.contiguous(), group=group)
+        acc = parts[0].clone()
+        for q in parts[1:]:
+            acc += q
+        t.copy_(acc)
+    return t
+
+
+def reduce_moments(buf: MomentBuffer, group=None, deterministic: bool = False) -> MomentBuffer:
+    """Sum the per-rank partial (G, b) over all ranks in place: one all-reduce (RCCL picks ring/tree),
+    or with ``deterministic`` one all-gather + rank-ordered sum."""
+    if _world(group) > 1:
+        if deterministic:
+            fixed_order_sum(buf.flat, group)
+        else:
+            dist.all_reduce(buf.flat, op=dist.ReduceOp.SUM, group=group)
     return buf
+
+
+def reduce_metric_sums(per_step: torch.Tensor, count: torch.Tensor, last: torch.Tensor | None = None, group=None,
+                       deterministic: bool = False):
+    """The masked-RMSE partial sums of a rank's shard (``ops.masked_sse``: per-step SSE [T], per-step
+    active count [T], last-entry (SSE, count) [2]) summed over ranks in ONE collective of 2T (+2) doubles
+    (SURVEY.md §8 E1 "Metrics: all-reduce of (SSE, count)"); predictions stay sharded.  Returns the
+    reduced (per_step, count, last)."""
+    T = per_step.numel()
+    pieces = [per_step.reshape(-1), count.reshape(-1)] + ([last.reshape(-1)] if last is not None else [])
+    flat = torch.cat([q.to(torch.float64) for q in pieces])
+    if _world(group) > 1:
+        if deterministic:
+            fixed_order_sum(flat, group)
+        else:
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    out = (flat[:T], flat[T:2 * T])
+    return out + ((flat[2 * T:2 * T + 2],) if last is not None else (None,))
+
+
+def rmse_from_sums(per_step, count, last=None, norm_const: float = 50.0, percentage: bool = True):
+    """The reference's metric definitions (time_varying_model.py:236-313) from (reduced) sums: ``orig``
+    = sqrt(mean_k(SSE_k / n_k)), ``all`` = sqrt(sum SSE / sum n), ``last`` = sqrt(SSE_last / n_last),
+    each / norm_const (x100 as a percentage)."""
+    import numpy as np
+    per = per_step.detach().cpu().numpy()
+    cnt = count.detach().cpu().numpy()
+    scale = 100.0 if percentage else 1.0
+    with np.errstate(invalid="ignore", divide="ignore"):
+        orig = float(np.sqrt((per / cnt).mean()) / norm_const * scale)
+        allv = float(np.sqrt(per.sum() / cnt.sum()) / norm_const * scale)
+        if last is None:
+            return orig, allv
+        lh = last.detach().cpu().numpy()
+        return orig, allv, float(np.sqrt(lh[0] / lh[1]) / norm_const * scale)
 
 
 def max_over_ranks(seconds: float, device=None, group=None) -> float:
@@ -54,12 +112,15 @@ def max_over_ranks(seconds: float, device=None, group=None) -> float:
 
 
 def discover_sharded(x, u, arm, rows, dt, lib, threshold, alpha, buf: MomentBuffer, max_iter=100,
-                     unbias=True, fd="smoothed4", workspace=None, group=None, out=None, layout="patient"):
-    """Per-rank Gram over the local shard -> one all-reduce -> replicated STLSQ.
+                     unbias=True, fd="smoothed4", workspace=None, group=None, out=None, layout="patient",
+                     deterministic=False):
+    """Per-rank Gram over the local shard -> one all-reduce (or, ``deterministic``, the rank-ordered
+    all-gather sum) -> replicated STLSQ.  The reference's intended parallel path is the pmap over
+    virtual devices at sindy.py:687-699 (dead there, F8); here the shards are real GPUs.
 
     Single rank: the fused ``sindy_fit`` (Gram kernel + finalize/STLSQ in two launches)."""
     from . import ops
-    world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+    world = _world(group)
     if out is None:
         A, F = buf.n_arms, buf.n_terms
         out = (torch.empty((A, F), dtype=torch.float64, device=buf.flat.device),
@@ -70,5 +131,5 @@ def discover_sharded(x, u, arm, rows, dt, lib, threshold, alpha, buf: MomentBuff
                                                 buf.n_arms, fd, workspace, out=(*out, buf.G, buf.b), layout=layout)
         return coef, mask, iters
     ops.gram(x, u, arm, rows, dt, lib, buf.n_arms, fd, workspace, out=(buf.G, buf.b), layout=layout)
-    reduce_moments(buf, group)
+    reduce_moments(buf, group, deterministic)
     return ops.stlsq(buf.G, buf.b, threshold, alpha, max_iter, unbias, out=out)

@@ -59,7 +59,8 @@ def _dev(name, t, dtype, ndim=None):
 
 
 class Workspace:
-    """Grow-only device scratch buffer (the library never allocates)."""
+    """Grow-only device scratch buffer (the library never allocates).  A buffer handed to a ``Plan`` is
+    referenced by that plan, so growing the workspace later never frees memory a plan still writes to."""
 
     def __init__(self):
         self._buf = {}
@@ -73,18 +74,32 @@ class Workspace:
         return b
 
 
-_WS = Workspace()
+# eager ops without an explicit workspace: one per (device, stream), so launches on different streams
+# never share scratch
+_WS_BY_STREAM: dict = {}
+
+
+def _default_ws(device) -> Workspace:
+    dev = torch.device(device)
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    ws = _WS_BY_STREAM.get(key)
+    if ws is None:
+        ws = _WS_BY_STREAM[key] = Workspace()
+    return ws
 
 
 class Plan:
-    """A prepared launch: arguments validated and packed once (tensors referenced by the plan stay
-    alive); each call enqueues the kernel(s) on the current stream of the plan's device (or the
-    given stream) with nothing but the C call left on the host path.  ``out`` holds the outputs."""
+    """A prepared launch: arguments validated and packed once; the plan holds references to every
+    tensor and host table its packed pointers address (inputs, outputs, workspace), so none can be freed
+    while the plan lives.  Each call enqueues the kernel(s) on the current stream of the plan's device (or
+    the given stream) with nothing but the C call left on the host path.  ``out`` holds the outputs.
+    Plans made without a workspace get a private one (never the shared per-stream default)."""
 
-    def __init__(self, fn_name: str, args: tuple, device, out):
+    def __init__(self, fn_name: str, args: tuple, device, out, keep=()):
         self.fn_name = fn_name
         self._fn = getattr(_lib.load(), fn_name)
         self._args = args
+        self._keep = tuple(keep)
         self.device = torch.device(device)
         self.out = out
 
@@ -96,18 +111,21 @@ class Plan:
         return self.out
 
     def bind(self, stream: torch.cuda.Stream):
-        """A zero-argument launcher with the stream handle packed too (hot loops: one C call)."""
+        """A zero-argument launcher with the stream handle packed too (hot loops: one C call).  The
+        launcher keeps the plan (and so its tensors) alive."""
         fn, args, name = self._fn, self._args + (ctypes.c_void_p(stream.cuda_stream),), self.fn_name
+        plan = self
 
         def launch():
             st = fn(*args)
             if st:
                 _lib.check(name, st)
+        launch.plan = plan
         return launch
 
 
 def _run(prep):
-    name, args, dev, out = prep
+    name, args, dev, out = prep[:4]
     st = getattr(_lib.load(), name)(*args, _stream(dev))
     _lib.check(name, st)
     return out
@@ -141,7 +159,7 @@ def _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout, stl
     F = lib.n_terms
     dev = x.device
     nbytes = L.insite_gram_workspace_bytes(N, n_arms, F)
-    ws = (workspace or _WS).get(nbytes, dev)
+    ws = (workspace or _default_ws(dev)).get(nbytes, dev)
     tab = lib.ctypes_table()
     head = (_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), _p(rows), N,
             lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p), F, FD_KINDS[fd], float(dt))
@@ -150,7 +168,7 @@ def _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout, stl
             out = (torch.empty((n_arms, F, F), dtype=torch.float64, device=dev),
                    torch.empty((n_arms, F), dtype=torch.float64, device=dev))
         G, b = out
-        return "insite_gram_f64", head + (_p(G), _p(b), _p(ws), ws.numel()), dev, out
+        return "insite_gram_f64", head + (_p(G), _p(b), _p(ws), ws.numel()), dev, out, (x, u, arm, rows, tab, ws, *out)
     threshold, alpha, max_iter, unbias = stlsq_args
     if out is None:
         out = (torch.empty((n_arms, F), dtype=torch.float64, device=dev),
@@ -161,7 +179,7 @@ def _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout, stl
     coef, mask, iters, G, b = out
     args = head + (float(threshold), float(alpha), int(max_iter), int(bool(unbias)), _p(G), _p(b), _p(coef),
                    _p(mask), _p(iters), _p(ws), ws.numel())
-    return "insite_sindy_fit_f64", args, dev, out
+    return "insite_sindy_fit_f64", args, dev, out, (x, u, arm, rows, tab, ws, *out)
 
 
 def gram(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor, dt: float,
@@ -187,16 +205,17 @@ def sindy_fit(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.T
 def plan_gram(x, u, arm, rows, dt, lib, n_arms=2, fd="smoothed4", workspace=None, out=None,
               layout="patient") -> Plan:
     """``gram`` as a prepared launch (``Plan``); ``plan.out`` = (G, b)."""
-    name, args, dev, out = _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout)
-    return Plan(name, args, dev, out)
+    name, args, dev, out, keep = _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace or Workspace(), out,
+                                            layout)
+    return Plan(name, args, dev, out, keep)
 
 
 def plan_sindy_fit(x, u, arm, rows, dt, lib, threshold, alpha, max_iter=100, unbias=True, n_arms=2,
                    fd="smoothed4", workspace=None, out=None, layout="patient") -> Plan:
     """``sindy_fit`` as a prepared launch; ``plan.out`` = (coef, mask, iters, G, b)."""
-    name, args, dev, out = _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout,
-                                      (threshold, alpha, max_iter, unbias))
-    return Plan(name, args, dev, out)
+    name, args, dev, out, keep = _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace or Workspace(), out,
+                                            layout, (threshold, alpha, max_iter, unbias))
+    return Plan(name, args, dev, out, keep)
 
 
 def sindy_fit_per_patient(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor, dt: float,
@@ -218,7 +237,7 @@ def sindy_fit_per_patient(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, r
                torch.empty((N, F), dtype=torch.int8, device=dev),
                torch.empty((N,), dtype=torch.int32, device=dev))
     coef, mask, iters = out
-    ws = (workspace or _WS).get(L.insite_per_patient_workspace_bytes(N), dev)
+    ws = (workspace or _default_ws(dev)).get(L.insite_per_patient_workspace_bytes(N), dev)
     tab = lib.ctypes_table()
     args = (_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), _p(rows), N,
             lib.n_statics, A, tab.ctypes.data_as(ctypes.c_void_p), F, FD_KINDS[fd], float(dt), _p(global_coef),
@@ -259,7 +278,7 @@ def _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layo
     L = _lib.load()
     F = lib.n_terms
     dev = x.device
-    ws = (workspace or _WS).get(L.insite_gram_segments_workspace_bytes(N, n_arms, F), dev)
+    ws = (workspace or _default_ws(dev)).get(L.insite_gram_segments_workspace_bytes(N, n_arms, F), dev)
     tab = lib.ctypes_table()
     head = (_p(x), x.stride(0), _p(arm), arm.stride(0), LAYOUTS[layout], n_steps, _p(seq_len),
             _p(u) if lib.n_statics else ctypes.c_void_p(0), N, lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p),
@@ -269,7 +288,8 @@ def _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layo
             out = (torch.empty((n_arms, F, F), dtype=torch.float64, device=dev),
                    torch.empty((n_arms, F), dtype=torch.float64, device=dev))
         G, b = out
-        return "insite_gram_segments_f64", head + (_p(G), _p(b), _p(ws), ws.numel()), dev, out
+        return ("insite_gram_segments_f64", head + (_p(G), _p(b), _p(ws), ws.numel()), dev, out,
+                (x, arm, seq_len, u, tab, ws, *out))
     threshold, alpha, max_iter, unbias = stlsq_args
     if out is None:
         out = (torch.empty((n_arms, F), dtype=torch.float64, device=dev),
@@ -280,7 +300,7 @@ def _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layo
     coef, mask, iters, G, b = out
     args = head + (float(threshold), float(alpha), int(max_iter), int(bool(unbias)), _p(G), _p(b), _p(coef), _p(mask),
                    _p(iters), _p(ws), ws.numel())
-    return "insite_sindy_fit_segments_f64", args, dev, out
+    return "insite_sindy_fit_segments_f64", args, dev, out, (x, arm, seq_len, u, tab, ws, *out)
 
 
 def gram_segments(x: torch.Tensor, arm: torch.Tensor, seq_len: torch.Tensor, u: torch.Tensor, dt: float,
@@ -308,16 +328,17 @@ def sindy_fit_segments(x: torch.Tensor, arm: torch.Tensor, seq_len: torch.Tensor
 def plan_gram_segments(x, arm, seq_len, u, dt, lib, n_arms=4, fd="order1", workspace=None, out=None,
                        layout="patient") -> Plan:
     """``gram_segments`` as a prepared launch; ``plan.out`` = (G, b)."""
-    name, args, dev, out = _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layout)
-    return Plan(name, args, dev, out)
+    name, args, dev, out, keep = _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace or Workspace(),
+                                                out, layout)
+    return Plan(name, args, dev, out, keep)
 
 
 def plan_sindy_fit_segments(x, arm, seq_len, u, dt, lib, threshold, alpha, max_iter=100, unbias=True, n_arms=4,
                             fd="order1", workspace=None, out=None, layout="patient") -> Plan:
     """``sindy_fit_segments`` as a prepared launch; ``plan.out`` = (coef, mask, iters, G, b)."""
-    name, args, dev, out = _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layout,
-                                          (threshold, alpha, max_iter, unbias))
-    return Plan(name, args, dev, out)
+    name, args, dev, out, keep = _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace or Workspace(),
+                                                out, layout, (threshold, alpha, max_iter, unbias))
+    return Plan(name, args, dev, out, keep)
 
 
 def _prep_stlsq(G, b, threshold, alpha, max_iter, unbias, out):
@@ -334,7 +355,7 @@ def _prep_stlsq(G, b, threshold, alpha, max_iter, unbias, out):
     coef, mask, iters = out
     args = (_p(G), _p(b), S, F, float(threshold), float(alpha), int(max_iter), int(bool(unbias)), _p(coef), _p(mask),
             _p(iters))
-    return "insite_stlsq_f64", args, G.device, out
+    return "insite_stlsq_f64", args, G.device, out, (G, b, *out)
 
 
 def stlsq(G: torch.Tensor, b: torch.Tensor, threshold: float, alpha: float, max_iter: int = 100,
@@ -344,8 +365,8 @@ def stlsq(G: torch.Tensor, b: torch.Tensor, threshold: float, alpha: float, max_
 
 
 def plan_stlsq(G, b, threshold, alpha, max_iter=100, unbias=True, out=None) -> Plan:
-    name, args, dev, out = _prep_stlsq(G, b, threshold, alpha, max_iter, unbias, out)
-    return Plan(name, args, dev, out)
+    name, args, dev, out, keep = _prep_stlsq(G, b, threshold, alpha, max_iter, unbias, out)
+    return Plan(name, args, dev, out, keep)
 
 
 def _prep_rollout(y0, u, arm, coef, lib, dt, method, substeps, drop_below, T, out, layout):
@@ -402,7 +423,7 @@ def _prep_rollout(y0, u, arm, coef, lib, dt, method, substeps, drop_below, T, ou
     args = (_p(y0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), arm.stride(0), _p(coef), stride,
             tab.ctypes.data_as(ctypes.c_void_p), F, N, T, lib.n_statics, A, float(dt), m, sub, float(drop_below),
             _p(out), out.stride(0), ROLLOUT_LAYOUTS[layout])
-    return "insite_rollout_f64", args, y0.device, out
+    return "insite_rollout_f64", args, y0.device, out, (y0, u, arm, coef, tab, out)
 
 
 def rollout(y0: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, coef: torch.Tensor, lib: PolyLibrary,
@@ -422,8 +443,8 @@ def rollout(y0: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, coef: torch.Te
 def plan_rollout(y0, u, arm, coef, lib, dt, method="euler5", substeps=None, drop_below=1e-3, T=None, out=None,
                  layout="patient") -> Plan:
     """``rollout`` as a prepared launch; ``plan.out`` = y."""
-    name, args, dev, out = _prep_rollout(y0, u, arm, coef, lib, dt, method, substeps, drop_below, T, out, layout)
-    return Plan(name, args, dev, out)
+    name, args, dev, out, keep = _prep_rollout(y0, u, arm, coef, lib, dt, method, substeps, drop_below, T, out, layout)
+    return Plan(name, args, dev, out, keep)
 
 
 def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_obs: torch.Tensor,
@@ -475,12 +496,15 @@ def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_ob
 
 
 def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: torch.Tensor, coef0: np.ndarray,
-                  lib: PolyLibrary, dt: float, lam: float, tau: int, substeps: int = 5):
+                  lib: PolyLibrary, dt: float, lam: float, tau: int, substeps: int = 5,
+                  revert_on_zoom_fail: bool = False):
     """INSITE per-patient refinement (reference sindy.py:433-715).  V [N, T] f64 unscaled observations
     and arm [N, T] int8 per-step arms in the reference's patient-major layout (transposed to the
     kernel's time-major layout here), u [N, U], seq_len [N], coef0 the HOST global model [A, F].
     A <= 2: insite_refine_f64 on bit-packed arms; A <= 4 (cancer_sim / EQ_5): insite_refine_arms_f64
-    on int8 arms.  Returns (preds [N, T], coef [N, A, F], status [N], iterations [N])."""
+    on int8 arms.  ``revert_on_zoom_fail``: BFGS status 3 falls back to coef0 as sindy.py:628-631 reads;
+    the default (False) keeps the iterate, which reproduces the reference's published runs.
+    Returns (preds [N, T], coef [N, A, F], status [N], iterations [N])."""
     _dev("V", V, torch.float64, 2)
     _dev("arm", arm, torch.int8, 2)
     N, T = V.shape
@@ -511,7 +535,8 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
     tab = lib.ctypes_table()
     args = (_p(Vt), Vt.stride(0), T, _p(arms), arms.stride(0), _p(u) if lib.n_statics else ctypes.c_void_p(0),
             _p(seq_len), N, lib.n_statics, tab.ctypes.data_as(ctypes.c_void_p), lib.n_terms,
-            c0.ctypes.data_as(ctypes.c_void_p), A, float(dt), float(lam), int(tau), int(substeps), _p(preds),
+            c0.ctypes.data_as(ctypes.c_void_p), A, float(dt), float(lam), int(tau), int(substeps),
+            int(bool(revert_on_zoom_fail)), _p(preds),
             preds.stride(0), _p(coef), _p(status), _p(iters))
     _run((name, args, dev, None))
     return preds.t(), coef, status, iters
@@ -533,7 +558,7 @@ def masked_sse(pred: torch.Tensor, target: torch.Tensor, active: torch.Tensor, s
     cnt = torch.empty(T, dtype=torch.float64, device=pred.device)
     last = torch.empty(2, dtype=torch.float64, device=pred.device)
     nbytes = L.insite_masked_sse_workspace_bytes(N, T)
-    ws = (workspace or _WS).get(nbytes, pred.device)
+    ws = (workspace or _default_ws(pred.device)).get(nbytes, pred.device)
     st = L.insite_masked_sse_f64(_p(pred), pred.stride(0), float(scale), float(shift), _p(target), _p(active), N, T,
                                  _p(per), _p(cnt), _p(last), _p(ws), ws.numel(), _stream(pred.device))
     _lib.check("insite_masked_sse_f64", st)

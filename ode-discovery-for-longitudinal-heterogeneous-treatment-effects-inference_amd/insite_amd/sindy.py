@@ -144,6 +144,9 @@ class SINDY:
         self.unscale_rmse = bool(_get(args, "exp.unscale_rmse", True))
         self.percentage_rmse = bool(_get(args, "exp.percentage_rmse", True))
         self.integrator = str(m("integrator", "euler5"))   # reference: Euler-5 (pkpd/utils.py:68-94)
+        # BFGS status 3 -> global model (the code at sindy.py:628-631) or keep the iterate (the published
+        # runs): default follows the published outputs
+        self.insite_revert_on_zoom_fail = bool(m("insite_revert_on_zoom_fail", False))
         self.library = polynomial_library(self.dim_static_features, 2, True)
         self.feature_library_names = self.library.get_feature_names()
         self.feature_names = ["x0"] + [f"u{i}" for i in range(self.dim_static_features)]
@@ -293,7 +296,8 @@ class SINDY:
         arm = torch.as_tensor(np.argmax(d["current_treatments"], axis=-1).astype(np.int8), device=self.device)
         sl = torch.as_tensor(np.asarray(d["sequence_lengths"]).astype(np.int32), device=self.device)
         preds, coef, status, iters = ops.insite_refine(prev.contiguous(), arm.contiguous(), stat, sl, self.joint_coefs,
-                                                       self.library, self.dt, float(self.lam), int(tau), substeps=5)
+                                                       self.library, self.dt, float(self.lam), int(tau), substeps=5,
+                                                       revert_on_zoom_fail=self.insite_revert_on_zoom_fail)
         self.insite_status, self.insite_iters, self.insite_coefs = status, iters, coef
         return ((preds - mean) / std).contiguous()
 

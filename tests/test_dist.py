@@ -98,3 +98,54 @@ def test_sharded_discovery_gloo_world2():
     np.testing.assert_array_equal(res[0][4], res[1][4])                 # replicated STLSQ identical
     assert np.max(np.abs(res[0][4] - g["coef"])) < 1e-8
     assert np.array_equal(res[0][4] != 0, g["mask"].astype(bool))
+
+
+def _metric_worker(rank, world, port, q):
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from oracle import insite_ref as R
+    from insite_amd import dist as idist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        g = np.load(os.path.join(ROOT, "tests", "golden", "metrics.npz"))
+        pred, target, active = g["pred"][..., 0], g["target"][..., 0], g["active"][..., 0]
+        lo, hi = idist.shard_bounds(pred.shape[0], rank, world)
+        err = (pred[lo:hi] - target[lo:hi]) ** 2 * active[lo:hi]
+        nxt = np.concatenate([active[lo:hi, 1:], np.zeros((hi - lo, 1))], axis=1)
+        lastm = active[lo:hi] - nxt                              # the final active entry of each row
+        per = torch.from_numpy(err.sum(0))
+        cnt = torch.from_numpy(active[lo:hi].sum(0))
+        last = torch.tensor([(err * lastm).sum(), lastm.sum()], dtype=torch.float64)
+        red = idist.reduce_metric_sums(per, cnt, last)
+        det = idist.reduce_metric_sums(per, cnt, last, deterministic=True)
+        x = torch.full((5,), 0.1 * (rank + 1), dtype=torch.float64)
+        idist.fixed_order_sum(x)
+        q.put((rank, idist.rmse_from_sums(*red), idist.rmse_from_sums(*det), x.numpy().copy()))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_metric_sums_all_reduce_gloo_world3():
+    """each rank's masked (SSE, count) partial sums, reduced in one collective (all-reduce
+    or the deterministic rank-ordered all-gather sum), give the full-cohort RMSE metrics (golden
+    fixture tests/golden/metrics.npz); the fixed-order sum equals the rank-ordered CPU sum bitwise."""
+    world = 3
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_metric_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = np.load(os.path.join(ROOT, "tests", "golden", "metrics.npz"))
+    want = [float(g["rmse_orig"]), float(g["rmse_all"]), float(g["rmse_last"])]
+    for _, red, det, x in res:
+        np.testing.assert_allclose(red, want, rtol=1e-12)
+        np.testing.assert_allclose(det, want, rtol=1e-12)
+        assert np.array_equal(x, np.full(5, (0.1 + 0.2) + 0.3))

@@ -79,3 +79,26 @@ def test_abi_discovery_reproduces_logged_equation(dev, case, layout):
     c = coef.cpu().numpy()
     assert np.array_equal(mask.cpu().numpy() != 0, ref != 0)
     assert np.max(np.abs(c - ref)) < 1e-10
+
+
+def _insite_args(eq):
+    from insite_amd import config as C
+    return C.compose(["+backbone=insite", "+dataset=pkpd_sim", f"dataset.equation_str={eq}", f"model.dataset_name={eq}",
+                      "model.sindy_threshold=0.1", "model.sindy_alpha=0.5", "model.lam=10.0"])
+
+
+def test_insite_plugin_reproduces_logged_run(dev, case):
+    """INSITE (+backbone=insite) end to end on the GPU — global fit, per-row BFGS refinement of the one-step
+    (tau = 1) and tau-step (tau = 5) sets, metrics — against the published INSITE run
+    (final_with_insite.txt:2387-2402): 70,800 refinements per cohort."""
+    from insite_amd.sindy import SINDY
+    eq, coll = case
+    anchor = ANCHORS[f"{eq}/insite"]
+    m = SINDY(_insite_args(eq), device=dev)
+    m.fit(coll["train"], coll["val"])
+    o, a, last = m.get_normalised_masked_rmse(coll["test_cf_one_step"], one_step_counterfactual=True)
+    got = {"encoder_test_rmse_orig": o, "encoder_test_rmse_all": a, "encoder_test_rmse_last": last}
+    r = m.get_normalised_n_step_rmses(coll["test_cf_treatment_seq"])
+    got.update({f"decoder_test_rmse_{k + 2}-step": v for k, v in enumerate(r)})
+    for k in METRICS:
+        assert got[k] == pytest.approx(anchor[k], rel=1e-8), k
