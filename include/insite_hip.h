@@ -60,7 +60,8 @@ extern "C" {
 #define INSITE_E_HIP (-4)
 
 /* derivative estimators (pysindy differentiation methods used at sindy.py:190-203) */
-#define INSITE_FD_SMOOTHED4 0 /* SmoothedFiniteDifference(savgol 5/3, order=4); library on smoothed x */
+#define INSITE_FD_SMOOTHED4 0 /* SmoothedFiniteDifference(savgol 5/3, order=4); x_dot from the smoothed
+                                 series, library on the RAW x (pinned: tests/test_reference_cohort.py) */
 #define INSITE_FD_ORDER4 1    /* FiniteDifference(order=4) */
 #define INSITE_FD_ORDER1 2    /* FiniteDifference(order=1): forward, backward at the last sample */
 #define INSITE_FD_SMOOTHED1 3 /* SmoothedFiniteDifference(savgol window 2, polyorder 1) + order 1 */
@@ -80,10 +81,12 @@ extern "C" {
 #define INSITE_LAYOUT_TIME_MAJOR_BITS 2
 
 /* limits of this ABI version */
-#define INSITE_MAX_TERMS 9  /* F: one Gram/moment entry per wavefront lane (F(F+1)/2 + F <= 64) */
+#define INSITE_MAX_TERMS 9  /* F of the fused affine path (one Gram/moment entry per lane, F(F+1)/2 + F <= 64);
+                               insite_gen_gram_f64 / STLSQ take F <= 64 */
 #define INSITE_MAX_STATICS 3
 #define INSITE_MAX_ARMS 4
-#define INSITE_MAX_STATE_DEGREE 1 /* max exponent of x in a column (Theta affine in x) */
+#define INSITE_MAX_STATE_DEGREE 1 /* max exponent of x of the fused affine kernels; the general path
+                                     (insite_gen_gram_f64, insite_rollout_f64's polynomial dispatch) takes 4 */
 
 int32_t insite_abi_version(void);
 const char* insite_strerror(int32_t code);
@@ -98,8 +101,8 @@ int32_t insite_poly_library(int32_t n_statics, int32_t degree, int32_t interacti
  * row materialisation and Theta^T Theta of SINDy.fit.  For every patient p with
  * L = min(rows[p], n_steps) >= 5 observation rows x[p, 0..L-1] and training arm a = arm[p]:
  *     G_out[a] += Theta_p^T Theta_p,   b_out[a] += Theta_p^T xdot_p
- * where Theta_p[k, j] = column j evaluated at (xs[k], u[p, :]) and xs = x (or the savgol
- * 5/3-smoothed x for INSITE_FD_SMOOTHED4).  Patients with L < 5 contribute nothing
+ * where Theta_p[k, j] = column j evaluated at (x[k], u[p, :]) — the raw samples; only x_dot
+ * comes from the savgol 5/3-smoothed series for INSITE_FD_SMOOTHED4.  Patients with L < 5 contribute nothing
  * (pysindy raises; the caller validates).  Deterministic: fixed-order reductions.
  *   x     f64, `layout` (INSITE_LAYOUT_*) with n_steps stored steps:
  *           PATIENT_MAJOR x[p * ldx + k], ldx >= n_steps  (the reference's [N, T] array)
@@ -252,6 +255,40 @@ int32_t insite_refine_arms_f64(const double* V, int64_t ld_v, int32_t T, const i
                                const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt,
                                double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail, double* preds,
                                int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream);
+
+/* General one-state discovery (insite_gen.hip): libraries with state exponents up to 4 and/or per-step
+ * binary treatment INPUTS — the reference's degree-4 ablation (PolynomialLibrary(degree=4,
+ * interaction_only=False), sindy.py:185-186, run.py:208) and joint "one ODE" model (joint_model with
+ * multilabel treatments, pkpd/utils.py:486-497, 639-672; run.py:198-201).  For every patient p with
+ * L = min(rows[p], n_steps) >= 5 rows (>= 2 for the order-1 methods) and group g = group[p] (0 when
+ * group is NULL):   G_out[g] += Theta_p^T Theta_p,  b_out[g] += Theta_p^T xdot_p,  where row k of
+ * Theta_p evaluates column j = x^exps[j][0] * prod_i in_i(k)^exps[j][1+i] * prod_t u_t^exps[j][1+n_in+t]
+ * on the RAW x[k] (x_dot by fd_kind over the whole row), in_i(k) = bit i of step_in(p, k) (binary).
+ *   x, step_in: `layout` PATIENT_MAJOR ([p * ld + k]) or TIME_MAJOR ([k * ld + p]); n_inputs <= 2
+ *   exps [n_terms][1 + n_inputs + n_statics] int8 (HOST), n_terms <= 64
+ *   G_out [n_groups, F, F], b_out [n_groups, F] (overwritten); deterministic fixed-order sums.   */
+size_t insite_gen_gram_workspace_bytes(int64_t n_patients, int32_t n_steps, int32_t n_groups, int32_t n_terms);
+int32_t insite_gen_gram_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,
+                            int32_t n_statics, const int8_t* step_in, int64_t ld_in, int32_t n_inputs,
+                            const int8_t* group, int32_t n_groups, const int32_t* rows, int64_t n_patients,
+                            const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt, double* G_out,
+                            double* b_out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Batched STLSQ for INSITE_MAX_TERMS < F <= 64 (one wavefront per system); insite_stlsq_f64 dispatches
+ * here on its own, same arguments and semantics. */
+int32_t insite_stlsq_wave64_f64(const double* G, const double* b, int64_t n_sys, int32_t n_terms, double threshold,
+                                double alpha, int32_t max_iter, int32_t unbias, double* coef_out, int8_t* mask_out,
+                                int32_t* iters_out, void* stream);
+
+/* Stage-evaluated rollout of a library with state degree 2..4 (Euler / RK4 on f_a(y) = sum_e P_a[e] y^e,
+ * P_a folded per patient from the columns with |coef| > drop_below), PATIENT_MAJOR or TIME_MAJOR layouts;
+ * insite_rollout_f64 dispatches here on its own when exps has a state exponent > 1.  Arguments as
+ * insite_rollout_f64. */
+int32_t insite_rollout_poly_f64(const double* y0, const double* u, const int8_t* arm, int64_t ld_arm,
+                                const double* coef, int64_t coef_row_stride, const int8_t* exps, int32_t n_terms,
+                                int64_t n_rows, int32_t T, int32_t n_statics, int32_t n_arms, double dt, int32_t method,
+                                int32_t substeps, double drop_below, double* y_out, int64_t ld_y, int32_t layout,
+                                void* stream);
 
 /* Masked squared-error sums for the RMSE metrics (time_varying_model.py:236-313):
  *   err[r,k]  = (pred[r, k] * scale + shift - target[r, k])^2 * active[r, k]

@@ -2988,6 +2988,9 @@ int32_t insite_stlsq_f64(const double* G, const double* b, int64_t n_sys, int32_
   if (n_sys < 0 || max_iter < 0 || !(threshold >= 0.0) || !(alpha >= 0.0)) return INSITE_E_INVALID_ARG;
   if (n_sys == 0) return INSITE_OK;
   if (!G || !b || !coef_out) return INSITE_E_INVALID_ARG;
+  if (n_terms > INSITE_MAX_TERMS)  // F <= 64: one wavefront per system (insite_gen.hip)
+    return insite_stlsq_wave64_f64(G, b, n_sys, n_terms, threshold, alpha, max_iter, unbias, coef_out, mask_out,
+                                   iters_out, stream);
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((unsigned)((n_sys + kBlock - 1) / kBlock));
   switch (n_terms) {
@@ -3028,10 +3031,19 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
   if (method != INSITE_METHOD_EULER && method != INSITE_METHOD_RK4) return INSITE_E_UNSUPPORTED;
   if (n_rows == 0 || T == 0) return INSITE_OK;
   if (!y0 || !arm || !coef || !y_out || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
+  if (coef_row_stride != 0 && coef_row_stride < (int64_t)n_arms * n_terms) return INSITE_E_INVALID_ARG;
+  if (exps && n_terms > 0 && n_statics >= 0) {  // state degree > 1: the stage-evaluated polynomial rollout
+    int deg = 0;
+    for (int j = 0; j < n_terms; ++j) deg = exps[j * (1 + n_statics)] > deg ? exps[j * (1 + n_statics)] : deg;
+    if (deg > INSITE_MAX_STATE_DEGREE) {
+      if (bits) return INSITE_E_UNSUPPORTED;
+      return insite_rollout_poly_f64(y0, u, arm, ld_arm, coef, coef_row_stride, exps, n_terms, n_rows, T, n_statics,
+                                     n_arms, dt, method, substeps, drop_below, y_out, ld_y, layout, stream);
+    }
+  }
   LibDesc lib;
   int32_t st = build_lib(exps, n_terms, n_statics, &lib);
   if (st != INSITE_OK) return st;
-  if (coef_row_stride != 0 && coef_row_stride < (int64_t)n_arms * n_terms) return INSITE_E_INVALID_ARG;
   RolloutArgs ra;
   ra.y0 = y0;
   ra.u = u;

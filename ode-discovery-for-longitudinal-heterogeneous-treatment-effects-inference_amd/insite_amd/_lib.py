@@ -28,6 +28,7 @@ FD_SMOOTHED4, FD_ORDER4, FD_ORDER1, FD_SMOOTHED1 = 0, 1, 2, 3
 METHOD_EULER, METHOD_RK4 = 0, 1
 LAYOUT_PATIENT_MAJOR, LAYOUT_TIME_MAJOR, LAYOUT_TIME_MAJOR_BITS = 0, 1, 2
 MAX_TERMS, MAX_STATICS, MAX_ARMS, MAX_STATE_DEGREE = 9, 3, 4, 1
+GEN_MAX_TERMS, GEN_MAX_STATE_DEGREE, GEN_MAX_INPUTS = 64, 4, 2   # insite_gen.hip
 
 EXPORTS = (
     "insite_abi_version",
@@ -53,6 +54,10 @@ EXPORTS = (
     "insite_stlsq_wave_f64",
     "insite_rollout_ms_f32",
     "insite_rollout_ms_sparse_f32",
+    "insite_gen_gram_workspace_bytes",
+    "insite_gen_gram_f64",
+    "insite_stlsq_wave64_f64",
+    "insite_rollout_poly_f64",
 )
 
 
@@ -114,6 +119,13 @@ _SIGNATURES = {
                                        _c_i32, _c_i32, _c_f64, _vp, _c_i64, _vp]),
     "insite_rollout_ms_sparse_f32": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _c_i32, _c_i32, _c_i64, _c_i32,
                                               _c_f64, _c_i32, _c_i32, _c_f64, _vp, _c_i64, _vp]),
+    "insite_gen_gram_workspace_bytes": (_c_size, [_c_i64, _c_i32, _c_i32, _c_i32]),
+    "insite_gen_gram_f64": (_c_i32, [_vp, _c_i64, _c_i32, _c_i32, _vp, _c_i32, _vp, _c_i64, _c_i32, _vp, _c_i32, _vp,
+                                     _c_i64, _vp, _c_i32, _c_i32, _c_f64, _vp, _vp, _vp, _c_size, _vp]),
+    "insite_stlsq_wave64_f64": (_c_i32, [_vp, _vp, _c_i64, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp,
+                                         _vp]),
+    "insite_rollout_poly_f64": (_c_i32, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _vp, _c_i32, _c_i64, _c_i32, _c_i32,
+                                         _c_i32, _c_f64, _c_i32, _c_i32, _c_f64, _vp, _c_i64, _c_i32, _vp]),
 }
 
 

@@ -341,6 +341,70 @@ def plan_sindy_fit_segments(x, arm, seq_len, u, dt, lib, threshold, alpha, max_i
     return Plan(name, args, dev, out, keep)
 
 
+GEN_FD_KINDS = {"smoothed4": _lib.FD_SMOOTHED4, "order4": _lib.FD_ORDER4, "order1": _lib.FD_ORDER1,
+                "smoothed1": _lib.FD_SMOOTHED1}
+
+
+def gen_gram(x: torch.Tensor, u: torch.Tensor | None, rows: torch.Tensor, dt: float, lib: PolyLibrary,
+             group: torch.Tensor | None = None, n_groups: int = 1, step_in: torch.Tensor | None = None,
+             fd: str = "smoothed4", layout: str = "patient", workspace: Workspace | None = None,
+             out: tuple | None = None):
+    """General one-state Gram (insite_gen_gram_f64): libraries with state exponents up to 4 (the degree-4
+    ablation, reference sindy.py:185-186) and/or ``lib.n_inputs`` per-step binary inputs (the joint model,
+    pkpd/utils.py:486-497).  x [N, T] ("patient") or [T, >=N] ("time") f64; step_in int8 in the same
+    layout, bit i = input i; group [N] int8 (regression of each patient, e.g. its arm; None = one
+    regression); rows [N] int32.  Returns (G [n_groups, F, F], b [n_groups, F])."""
+    if layout not in LAYOUTS:
+        raise ValueError(f"layout must be one of {sorted(LAYOUTS)}")
+    if fd not in GEN_FD_KINDS:
+        raise ValueError(f"fd must be one of {sorted(GEN_FD_KINDS)}")
+    _dev("x", x, torch.float64, 2)
+    _dev("rows", rows, torch.int32, 1)
+    N = rows.numel()
+    n_steps = x.size(0) if layout == "time" else x.size(1)
+    if (x.size(1) < N) if layout == "time" else (x.size(0) != N):
+        raise ValueError("x must hold one series per patient ([T, >=N] time-major, [N, T] patient-major)")
+    if group is not None:
+        _dev("group", group, torch.int8, 1)
+        if group.numel() != N:
+            raise ValueError("group must have one entry per patient")
+    if not 1 <= n_groups <= _lib.MAX_ARMS:
+        raise ValueError(f"n_groups must be in [1, {_lib.MAX_ARMS}]")
+    U = lib.n_statics
+    if U:
+        _dev("u", u, torch.float64, 2)
+        if u.size(0) != N or u.size(1) != U or u.stride(0) != U:
+            raise ValueError("u must be a contiguous [N, n_statics] tensor")
+    if lib.n_inputs:
+        _dev("step_in", step_in, torch.int8, 2)
+        if (step_in.size(1) < N or step_in.size(0) < n_steps) if layout == "time" else \
+                (step_in.size(0) != N or step_in.size(1) < n_steps):
+            raise ValueError("step_in must cover every (patient, step) of x")
+    L = _lib.load()
+    F = lib.n_terms
+    dev = x.device
+    ws = (workspace or _default_ws(dev)).get(L.insite_gen_gram_workspace_bytes(N, n_steps, n_groups, F), dev)
+    if out is None:
+        out = (torch.empty((n_groups, F, F), dtype=torch.float64, device=dev),
+               torch.empty((n_groups, F), dtype=torch.float64, device=dev))
+    G, b = out
+    tab = lib.ctypes_table()
+    args = (_p(x), x.stride(0), LAYOUTS[layout], n_steps, _p(u) if U else ctypes.c_void_p(0), U,
+            _p(step_in) if lib.n_inputs else ctypes.c_void_p(0), step_in.stride(0) if lib.n_inputs else 0,
+            lib.n_inputs, _p(group), n_groups, _p(rows), N, tab.ctypes.data_as(ctypes.c_void_p), F, GEN_FD_KINDS[fd],
+            float(dt), _p(G), _p(b), _p(ws), ws.numel())
+    return _run(("insite_gen_gram_f64", args, dev, out))
+
+
+def gen_sindy_fit(x, u, rows, dt, lib, threshold, alpha, group=None, n_groups=1, step_in=None, fd="smoothed4",
+                  layout="patient", max_iter=100, unbias=True, workspace=None):
+    """``gen_gram`` then the batched STLSQ (insite_stlsq_f64; F > 9 runs one wavefront per system).
+    Returns (coef [n_groups, F], mask, iters, G, b)."""
+    G, b = gen_gram(x, u, rows, dt, lib, group, n_groups, step_in, fd, layout, workspace)
+    coef, mask, iters = stlsq(G, b, threshold, alpha, max_iter, unbias)
+    return coef, mask, iters, G, b
+
+
 def _prep_stlsq(G, b, threshold, alpha, max_iter, unbias, out):
     _dev("G", G, torch.float64)
     _dev("b", b, torch.float64)

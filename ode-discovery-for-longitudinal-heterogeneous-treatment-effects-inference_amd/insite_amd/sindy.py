@@ -19,10 +19,15 @@ through the C ABI (include/insite_hip.h):
 
 The DE-format extraction (A1, pkpd/utils.py:523-606), the tau-step slice (A9) and the masked
 squared-error sums of the metrics (A10) also run on the device; only scalars and the returned
-prediction arrays cross back to the host.  Out of scope in this build (raise
-``NotImplementedError``): weak SINDy, the joint model and the degree-4 ablation library.  The
-cancer_sim / EQ_5 datasets run the treatment-segment discovery
-(``insite_sindy_fit_segments_f64``), the 4-arm rollout and, with ``insite: true``, the 4-arm refinement.
+prediction arrays cross back to the host.  The cancer_sim / EQ_5 datasets run the
+treatment-segment discovery (``insite_sindy_fit_segments_f64``), the 4-arm rollout and, with
+``insite: true``, the 4-arm refinement.  The ablations run through the general one-state path
+(``insite_gen_gram_f64``): ``ablation_more_complex_basis_functions`` (PolynomialLibrary(degree=4,
+interaction_only=False), sindy.py:185-186; EQ_4) and ``joint_model`` (one regression with the multilabel
+treatment(s) as library inputs, pkpd/utils.py:486-497, 639-672; sindy.py:283-288, 313-322), whose RHS
+is folded per treatment combination into the per-arm rollout.  Not on the MI355X path (raise
+``NotImplementedError``): weak SINDy, INSITE refinement of the two ablation models, and the degree-4
+library on the treatment-segment datasets.
 """
 from __future__ import annotations
 
@@ -147,8 +152,11 @@ class SINDY:
         # BFGS status 3 -> global model (the code at sindy.py:628-631) or keep the iterate (the published
         # runs): default follows the published outputs
         self.insite_revert_on_zoom_fail = bool(m("insite_revert_on_zoom_fail", False))
-        self.library = polynomial_library(self.dim_static_features, 2, True)
+        # PolynomialLibrary(**PolynomialLibrary_kw) of sindy.py:185-188
+        self.lib_degree, self.lib_interaction_only = (4, False) if self.ablation_more_complex_basis_functions else (2, True)
+        self.library = polynomial_library(self.dim_static_features, self.lib_degree, self.lib_interaction_only)
         self.feature_library_names = self.library.get_feature_names()
+        self._roll_library = self.library   # the library the rollout evaluates (joint: folded per combination)
         self.feature_names = ["x0"] + [f"u{i}" for i in range(self.dim_static_features)]
         self.joint_coefs = None
         self.n_iter = None
@@ -162,11 +170,12 @@ class SINDY:
                                       "the treatment-segment datasets (cancer_sim, EQ_5_*)")
         if self.wsindy:
             raise NotImplementedError("weak SINDy (wsindy: true) is not on the MI355X path")
-        if self.joint_model:
-            raise NotImplementedError("joint_model: true (treatment as a library input) is not on the MI355X path")
-        if self.ablation_more_complex_basis_functions:
-            raise NotImplementedError("the degree-4 ablation library has state exponents > 1 "
-                                      "(outside INSITE_MAX_STATE_DEGREE)")
+        if self.insite and (self.joint_model or self.ablation_more_complex_basis_functions):
+            raise NotImplementedError("INSITE refinement of the joint / degree-4 ablation models is not on the "
+                                      "MI355X path (the refinement kernel takes per-arm affine models)")
+        if self.ablation_more_complex_basis_functions and self.segment_mode and not self.joint_model:
+            raise NotImplementedError("the degree-4 library on the treatment-segment datasets (cancer_sim / EQ_5) "
+                                      "is not on the MI355X path")
         if self.integrator not in ops.METHODS:
             raise ValueError(f"integrator must be one of {sorted(ops.METHODS)}")
 
@@ -227,9 +236,74 @@ class SINDY:
                                       max_iter=100, unbias=True, n_arms=self.dim_treatments, fd=fd)
 
     # ------------------------------------------------------------------ discovery
+    def _fit_joint(self, train_f):
+        """The joint ("one ODE") model (sindy.py:190, 203 with joint_model; DE format pkpd/utils.py:639-672):
+        ONE regression over the rows x = unscaled_outputs[:seq_len - offset] (offset 1 for EQ_4, 0 for
+        cancer_sim / EQ_5) with library inputs (x0, treatment bits, statics) — the multilabel treatments of
+        ``dataset.treatment_mode=multilabel`` (run.py:198-201).  General one-state Gram + STLSQ on the GPU."""
+        d = train_f.data
+        ct = np.asarray(d["current_treatments"])
+        if ct.ndim != 3 or ct.shape[-1] > 2 or not np.all((ct == 0) | (ct == 1)):
+            raise NotImplementedError("joint_model needs binary multilabel treatments (dataset.treatment_mode="
+                                      "multilabel, at most 2 treatment columns)")
+        n_in = ct.shape[-1]
+        self.library = polynomial_library(self.dim_static_features, self.lib_degree, self.lib_interaction_only,
+                                          n_inputs=n_in)
+        self.feature_library_names = self.library.get_feature_names()
+        self.feature_names = list(self.library.input_names)
+        _, stat, _, _ = self._unscaled_inputs(train_f)
+        x = torch.as_tensor(np.ascontiguousarray(d["unscaled_outputs"][..., 0]), device=self.device)
+        code = torch.as_tensor(self._treatment_code(ct), device=self.device)
+        offset = 0 if self.segment_mode else 1
+        rows = (torch.as_tensor(np.asarray(d["sequence_lengths"]), device=self.device).to(torch.int64) - offset)
+        if self.segment_mode:
+            fd, need = ("smoothed1" if self.use_smoothed_finite_difference else "order1"), 2
+        else:
+            fd, need = "smoothed4", 5
+        if int(rows.min().item()) < need:
+            raise ValueError(f"a training trajectory has fewer than {need} rows for the {fd} derivative")
+        coef, mask, iters, _, _ = ops.gen_sindy_fit(x, stat, rows.to(torch.int32), self.dt, self.library,
+                                                    self.sindy_threshold, self.sindy_alpha, step_in=code, fd=fd)
+        return self._finish_fit(coef, mask, iters)
+
+    @staticmethod
+    def _treatment_code(ct) -> np.ndarray:
+        """Per-step input code of binary multilabel treatments [N, T, n_in]: bit i = treatment i."""
+        ct = np.asarray(ct)
+        code = np.zeros(ct.shape[:2], dtype=np.int8)
+        for i in range(ct.shape[-1]):
+            code |= (ct[..., i].astype(np.int8) << i)
+        return np.ascontiguousarray(code)
+
+    def _fold_joint(self, rhs):
+        """The joint RHS sum_j c_j x^e_j in(k)^tau_j m_j(u) as per-combination (arm) coefficients over the
+        library with the input columns dropped: combination c keeps the columns whose inputs are all on in
+        c (binary inputs), so the per-arm rollout kernels evaluate the same f(y, in_k, u)."""
+        lib = self.library
+        n_in, U = lib.n_inputs, lib.n_statics
+        e = lib.exps
+        keep_cols = [0] + list(range(1 + n_in, 1 + n_in + U))
+        red_rows, index = [], []
+        for row in e[:, keep_cols].tolist():
+            if row not in red_rows:
+                red_rows.append(row)
+            index.append(red_rows.index(row))
+        from .library import PolyLibrary
+        red = PolyLibrary(np.array(red_rows, dtype=np.int8), (lib.input_names[0],) + tuple(lib.input_names[1 + n_in:]))
+        NC = 1 << n_in
+        folded = np.zeros((NC, len(red_rows)))
+        tin = [(sum(1 << i for i in range(n_in) if e[j, 1 + i] > 0)) for j in range(lib.n_terms)]
+        for c in range(NC):
+            for j in range(lib.n_terms):
+                if (tin[j] & ~c) == 0:
+                    folded[c, index[j]] += rhs[0, j]
+        return red, folded
+
     def fit(self, train_f, val_f=None):
         """Global discovery per arm (sindy.py:145-336): one Gram pass + STLSQ on the GPU."""
         self.prepare_data()
+        if self.joint_model:
+            return self._fit_joint(train_f)
         if self.segment_mode:
             coef, mask, iters, G, _ = self._fit_segments(train_f)
             empty = np.nonzero(G[:, 0, 0].cpu().numpy() == 0)[0]
@@ -241,6 +315,11 @@ class SINDY:
         if int(rows.min().item()) < 5:
             raise ValueError("a training trajectory has fewer than 5 rows: the savgol(5, 3) smoother "
                              "and the 5-point derivative need at least 5 samples")
+        if self.library.state_degree > 1:     # the degree-4 ablation library: the general path
+            coef, mask, iters, _, _ = ops.gen_sindy_fit(x, u, rows, self.dt, self.library, self.sindy_threshold,
+                                                        self.sindy_alpha, group=arm, n_groups=self.dim_treatments,
+                                                        fd="smoothed4")
+            return self._finish_fit(coef, mask, iters)
         coef, mask, iters, _, _ = ops.sindy_fit(x, u, arm, rows, self.dt, self.library, self.sindy_threshold,
                                                 self.sindy_alpha, max_iter=100, unbias=True,
                                                 n_arms=self.dim_treatments, fd="smoothed4")
@@ -254,9 +333,16 @@ class SINDY:
         self.coef_mask = mask.cpu().numpy().astype(bool)
         self.n_iter = iters_h
         rhs = rhs_coefficients(self.joint_coefs, self.sindy_quantize, self.sindy_quantize_global_model_round_to)
-        self._coef_dev = torch.as_tensor(rhs, device=self.device)
-        self.global_equation_string = equation_string(self.joint_coefs, self.feature_library_names,
-                                                      self.sindy_quantize, self.sindy_quantize_global_model_round_to)
+        if self.joint_model:
+            self._roll_library, rhs = self._fold_joint(rhs)
+            self.global_equation_string = "Joint Model: x_dot = " + equation_terms(
+                self.joint_coefs[0], self.feature_library_names, self.sindy_quantize,
+                self.sindy_quantize_global_model_round_to)                           # sindy.py:285, 315
+        else:
+            self._roll_library = self.library
+            self.global_equation_string = equation_string(self.joint_coefs, self.feature_library_names,
+                                                          self.sindy_quantize, self.sindy_quantize_global_model_round_to)
+        self._coef_dev = torch.as_tensor(np.ascontiguousarray(rhs), device=self.device)
         logger.info("[Model]: %s", self.global_equation_string)
         return self
 
@@ -272,8 +358,11 @@ class SINDY:
         d = dataset.data
         prev, stat, std, mean = self._unscaled_inputs(dataset)
         T = d["prev_outputs"].shape[1]
-        arm = torch.as_tensor(np.argmax(d["current_treatments"], axis=-1).astype(np.int8), device=self.device)
-        y = ops.rollout(prev[:, 0].contiguous(), stat, arm, self._coef_dev, self.library, self.dt,
+        if self.joint_model:   # per-step treatment combination = the folded model's arm
+            arm = torch.as_tensor(self._treatment_code(d["current_treatments"]), device=self.device)
+        else:
+            arm = torch.as_tensor(np.argmax(d["current_treatments"], axis=-1).astype(np.int8), device=self.device)
+        y = ops.rollout(prev[:, 0].contiguous(), stat, arm.contiguous(), self._coef_dev, self._roll_library, self.dt,
                         method=self.integrator, drop_below=0.0, T=T)
         return (y - mean) / std
 

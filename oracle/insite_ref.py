@@ -274,17 +274,24 @@ def get_scaling_params(sim):
     return means, stds
 
 
-def process_data(sim, scaling):
-    """Layout of ``SyntheticPkpdDataset.process_data`` (pkpd/dataset.py:96-192), multiclass."""
+def process_data(sim, scaling, treatment_mode="multiclass"):
+    """Layout of ``SyntheticPkpdDataset.process_data`` (pkpd/dataset.py:96-192): multiclass one-hot
+    treatments [N, T-1, 2] (:135-147) or multilabel [N, T-1, 1] (:149-151, the joint-model ablation's
+    ``dataset.treatment_mode=multilabel``, run.py:198-201)."""
     mean, std = scaling
     d = dict(sim)
     V = (sim["cancer_volume"] - mean["cancer_volume"]) / std["cancer_volume"]
     c0 = (sim["observed_static_c_0"] - mean["observed_static_c_0"]) / std["observed_static_c_0"]
     c1 = (sim["observed_static_c_1"] - mean["observed_static_c_1"]) / std["observed_static_c_1"]
     app = sim["treatment_application"][:, :-1]                       # :132-133
-    onehot = np.zeros(app.shape + (2,))
-    onehot[..., 0] = (app == 0)
-    onehot[..., 1] = (app == 1)
+    if treatment_mode == "multiclass":
+        onehot = np.zeros(app.shape + (2,))
+        onehot[..., 0] = (app == 0)
+        onehot[..., 1] = (app == 1)
+    elif treatment_mode == "multilabel":
+        onehot = app[..., None].astype(np.float64)
+    else:
+        raise ValueError(treatment_mode)
     seq = sim["sequence_lengths"]
     Tm1 = V.shape[1] - 1
     cur_cov = np.stack([V[:, :-1], np.repeat(c0[:, None], Tm1, 1), np.repeat(c1[:, None], Tm1, 1)], axis=-1)
@@ -293,7 +300,7 @@ def process_data(sim, scaling):
     for i in range(seq.shape[0]):
         active[i, :int(seq[i]), :] = 1
     d["current_treatments"] = onehot
-    d["prev_treatments"] = np.concatenate([np.zeros((V.shape[0], 1, 2)), onehot[:, :-1, :]], axis=1)
+    d["prev_treatments"] = np.concatenate([np.zeros((V.shape[0], 1, onehot.shape[-1])), onehot[:, :-1, :]], axis=1)
     d["current_covariates"] = cur_cov
     d["outputs"] = outputs
     d["active_entries"] = active
@@ -332,7 +339,7 @@ class Subset:
 
 
 def make_collection(equation="EQ_4_A", num_patients=None, seq_length=60, projection_horizon=5,
-                    conf_coeff=2.0, seed=0, with_tests=True):
+                    conf_coeff=2.0, seed=0, with_tests=True, treatment_mode="multiclass"):
     """``SyntheticPkpdDatasetCollection`` + ``process_data_multi`` (pkpd/dataset.py:557-607;
     dataset_collection.py:74-86).  Subsets use independent child streams of ``seed``."""
     num_patients = num_patients or {"train": 500, "val": 100, "test": 100}
@@ -354,7 +361,7 @@ def make_collection(equation="EQ_4_A", num_patients=None, seq_length=60, project
             p, seq_length, projection_horizon, rng, equation, conf_coeff)
     scaling = get_scaling_params(sims["train"])
     for name, sim in sims.items():
-        d, sp = process_data(sim, scaling)
+        d, sp = process_data(sim, scaling, treatment_mode)
         out[name] = Subset(name, d, sp)
     if with_tests:
         s = out["test_cf_treatment_seq"]
@@ -742,6 +749,66 @@ def gram_moments_vectorized(x, u, arm, rows_const, dt, exps, n_arms=2):
 
 
 # --------------------------------------------------------------------------------------
+# Joint ("one ODE") model — ABLATION_ONE_ODE (run.py:198-201: joint_model=true, multilabel treatments)
+# --------------------------------------------------------------------------------------
+def de_format_joint(data, scaling_params, sequence_lengths_offset=1):
+    """The joint branch of ``process_dataset_into_de_format`` (pkpd/utils.py:639-672, 486-497): per patient
+    X = unscaled_outputs[:L] (the OUTPUTS V[1:], not the reconstructed series), U = concat(treatments[:L],
+    statics[:L]) with the multilabel (binary) treatments, L = seq_len - offset (1 for EQ_4, 0 for
+    cancer_sim / EQ_5).  Returns x [N, T-1], inputs [N, T-1, n_in] (0/1), statics [N, U], rows [N]."""
+    _, stat = unscale_inputs(data, scaling_params)
+    x = data["unscaled_outputs"][..., 0]
+    inputs = np.asarray(data["current_treatments"], dtype=np.float64)
+    rows = data["sequence_lengths"].astype(np.int64) - sequence_lengths_offset
+    return x, inputs, stat, rows
+
+
+def build_regression_joint(x, inputs, stat, rows, dt, fd="smoothed4"):
+    """Concatenated joint regression rows: library inputs [x, inputs_k, statics], targets x_dot (pysindy
+    multiple_trajectories over the patients; the raw x in the library, x_dot by ``fd``)."""
+    X = [x[i, :int(rows[i])].reshape(-1, 1) for i in range(x.shape[0]) if int(rows[i]) >= (5 if "4" in fd else 2)]
+    U = [np.concatenate([inputs[i, :int(rows[i])], np.repeat(stat[i][None, :], int(rows[i]), 0)], axis=1)
+         for i in range(x.shape[0]) if int(rows[i]) >= (5 if "4" in fd else 2)]
+    if fd == "smoothed1" or fd == "order1":
+        from . import segments_ref as SG
+        Z, Y = [], []
+        for Xi, Ui in zip(X, U):
+            zi, yi = SG.derivative(Xi[:, 0], dt, fd)
+            Z.append(np.concatenate([zi[:, None], Ui], axis=1))
+            Y.append(yi)
+        return np.concatenate(Z), np.concatenate(Y)
+    return build_regression(X, U, dt, fd)
+
+
+def rollout_inputs(y0, stat, inputs, coef, exps, dt, method="euler5", substeps=None):
+    """Open-loop rollout of a model whose library has per-step inputs (the joint model's
+    pred_dy_dt = mod_0(x0=y, u0=treatment_k, u1.. = statics), sindy.py:283-288, 317-322): step k evaluates
+    the RHS on u_k = [inputs[:, k], statics].  coef [F] (the joint model's single row)."""
+    N, T = inputs.shape[:2]
+    y = np.asarray(y0, dtype=np.float64).copy()
+    out = np.empty((N, T))
+    cr = np.repeat(np.asarray(coef, dtype=np.float64)[None, :], N, axis=0)
+    for k in range(T):
+        uk = np.concatenate([inputs[:, k], stat], axis=1)
+        if method in ("euler5", "euler"):
+            n_sub = STEPS_FOR_DT if method == "euler5" else int(substeps or 1)
+            h = dt / n_sub
+            for _ in range(n_sub):
+                y = y + rhs_literal(y, uk, cr, exps) * h
+        else:
+            n_sub = int(substeps or 1)
+            h = dt / n_sub
+            for _ in range(n_sub):
+                k1 = rhs_literal(y, uk, cr, exps)
+                k2 = rhs_literal(y + 0.5 * h * k1, uk, cr, exps)
+                k3 = rhs_literal(y + 0.5 * h * k2, uk, cr, exps)
+                k4 = rhs_literal(y + h * k3, uk, cr, exps)
+                y = y + (h / 6.0) * (k1 + 2.0 * k2 + 2.0 * k3 + k4)
+        out[:, k] = y
+    return out
+
+
+# --------------------------------------------------------------------------------------
 # A6 — model -> RHS and global_equation_string (pkpd/utils.py:372-397; sindy.py:272-282)
 # --------------------------------------------------------------------------------------
 def equation_terms(coefs, names, quantize=False, round_to=3):
@@ -877,25 +944,44 @@ def n_step_rmses(pred_unscaled, target_unscaled, active, norm_const=MAX_VALUE, p
 # --------------------------------------------------------------------------------------
 # End-to-end: train_sindy.main equivalent (runnables/train_sindy.py:21-113), SINDy backbone
 # --------------------------------------------------------------------------------------
-def sindy_pipeline(coll, threshold=0.1, alpha=0.5, dt=None, method="euler5"):
+def sindy_pipeline(coll, threshold=0.1, alpha=0.5, dt=None, method="euler5", joint_model=False, degree=2,
+                   interaction_only=True):
+    """train_sindy.main for the EQ_4 SINDy backbone: per-arm fits (default), the degree-4 ablation library
+    (``degree=4, interaction_only=False``, sindy.py:185-186) or the joint model (``joint_model``: one fit
+    with the multilabel treatment as library input u0, pkpd/utils.py:486-497, on a multilabel collection)."""
     train = coll["train"]
     T = train.data["prev_outputs"].shape[1] + 1
     dt = MAX_TIME_HORIZON / T if dt is None else dt
-    x, u, arm, rows = de_format(train.data, train.scaling_params)
-    X, U = de_lists(x, u, arm, rows)
-    exps = poly_library(3, 2, True)
-    names = library_names(exps, ["x0", "u0", "u1"])
-    coefs = []
-    for a in range(2):
-        c, _, _, _ = sindy_fit(X[a], U[a], dt, threshold, alpha)
-        coefs.append(c)
-    joint = np.stack(coefs)
-    res = {"joint_coefs": joint, "global_equation_string": global_equation_string(joint, names)}
+    if joint_model:
+        x, inputs, stat, rows = de_format_joint(train.data, train.scaling_params)
+        n_in = inputs.shape[-1]
+        exps = poly_library(1 + n_in + stat.shape[1], degree, interaction_only)
+        names = library_names(exps, ["x0"] + [f"u{i}" for i in range(n_in + stat.shape[1])])
+        Z, Y = build_regression_joint(x, inputs, stat, rows, dt)
+        c, _, _ = stlsq(eval_library(exps, Z), Y, threshold, alpha)
+        joint = c[None, :]
+        res = {"joint_coefs": joint, "global_equation_string": f"Joint Model: x_dot = {equation_terms(c, names)}"}
 
-    def predict(sub):
-        prev, stat = unscale_inputs(sub.data, sub.scaling_params)
-        arms = np.argmax(sub.data["current_treatments"], axis=-1)
-        return rollout(prev[:, 0], stat, arms, joint, exps, dt, method)
+        def predict(sub):
+            prev, st = unscale_inputs(sub.data, sub.scaling_params)
+            return rollout_inputs(prev[:, 0], st, np.asarray(sub.data["current_treatments"], dtype=np.float64), c,
+                                  exps, dt, method)
+    else:
+        x, u, arm, rows = de_format(train.data, train.scaling_params)
+        X, U = de_lists(x, u, arm, rows)
+        exps = poly_library(3, degree, interaction_only)
+        names = library_names(exps, ["x0", "u0", "u1"])
+        coefs = []
+        for a in range(2):
+            c, _, _, _ = sindy_fit(X[a], U[a], dt, threshold, alpha, degree=degree, interaction_only=interaction_only)
+            coefs.append(c)
+        joint = np.stack(coefs)
+        res = {"joint_coefs": joint, "global_equation_string": global_equation_string(joint, names)}
+
+        def predict(sub):
+            prev, stat = unscale_inputs(sub.data, sub.scaling_params)
+            arms = np.argmax(sub.data["current_treatments"], axis=-1)
+            return rollout(prev[:, 0], stat, arms, joint, exps, dt, method)
 
     one = coll.get("test_cf_one_step")
     if one is not None:

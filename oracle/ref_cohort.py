@@ -232,7 +232,7 @@ def _subset_keys(seed):
 
 
 def make_collection(equation="EQ_4_A", num_patients=None, seq_length=60, projection_horizon=5, conf_coeff=2,
-                    seed=1, with_tests=True):
+                    seed=1, with_tests=True, treatment_mode="multiclass"):
     """``SyntheticPkpdDatasetCollection`` + ``process_data_multi`` with the reference's draws.
     Returns the same {name: insite_ref.Subset} mapping as ``insite_ref.make_collection``."""
     num_patients = num_patients or {"train": 1000, "val": 100, "test": 100}
@@ -252,7 +252,7 @@ def make_collection(equation="EQ_4_A", num_patients=None, seq_length=60, project
     scaling = R.get_scaling_params(sims["train"])                          # dataset.py:607
     out = {}
     for name, sim in sims.items():                                         # process_data_multi
-        d, sp = R.process_data(sim, scaling)
+        d, sp = R.process_data(sim, scaling, treatment_mode)
         out[name] = R.Subset(name, d, sp)
     if with_tests:
         s = out["test_cf_treatment_seq"]

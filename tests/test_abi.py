@@ -30,10 +30,15 @@ def _header_functions():
     return sorted(set(re.findall(r"^\s*(?:const\s+char\s*\*|int32_t|size_t)\s+(insite_\w+)\s*\(", src, re.M)))
 
 
+def _lib_exports():
+    from insite_amd import _lib
+    return _lib.EXPORTS
+
+
 def test_header_declares_the_abi():
     fns = _header_functions()
     assert "insite_rollout_f64" in fns and "insite_sindy_fit_f64" in fns
-    assert len(fns) == 23
+    assert len(fns) == 27 and set(fns) == set(_lib_exports())
 
 
 def test_library_exports_every_header_symbol(L):

@@ -46,9 +46,15 @@ def test_sindy_reads_config_and_rejects_unsupported_modes():
     assert (m.sindy_threshold, m.sindy_alpha, m.dt) == (0.1, 0.5, 10.0 / 60)
     assert m.feature_library_names == ["1", "x0", "u0", "u1", "x0 u0", "x0 u1", "u0 u1"]
     assert m.model_type == "sindy_regressor" and m.insite is False
-    for flag in ("wsindy", "joint_model", "ablation_more_complex_basis_functions"):
-        with pytest.raises(NotImplementedError):
-            SINDY(_args(**{flag: True}), device="cpu")
+    with pytest.raises(NotImplementedError):
+        SINDY(_args(wsindy=True), device="cpu")
+    for flag in ("joint_model", "ablation_more_complex_basis_functions"):   # the ablations run (insite_gen.hip) ...
+        m2 = SINDY(_args(**{flag: True}), device="cpu")
+        assert getattr(m2, flag) is True
+        with pytest.raises(NotImplementedError):                           # ... but not their INSITE refinement
+            SINDY(_args(insite=True, **{flag: True}), device="cpu")
+    m4 = SINDY(_args(ablation_more_complex_basis_functions=True), device="cpu")
+    assert m4.library.n_terms == 35 and m4.feature_library_names[4] == "x0^2"
     ins = SINDY(_args(insite=True), device="cpu")   # the INSITE refinement (F2) is on the GPU path
     assert ins.insite is True
     with pytest.raises(RuntimeError):               # refined predictions before fit()
