@@ -77,6 +77,8 @@ def run_one(driver: dict, dataset_name: str, method_name: str, seed: int, domain
     try:
         args = C.compose(C.run_overrides(driver, dataset_name, method_name, seed, int(domain_conf)) + list(extra))
         result = train_sindy_main(args, dataset_name=dataset_name, device=device)
+        # run_exp_ct's tail (reference run.py:305-306): method, seed, seconds_taken (wall time of the run)
+        result.update({"method": method_name, "seed": seed, "seconds_taken": time.perf_counter() - t0})
         result["errored"] = False
     except Exception as e:  # noqa: BLE001 - mirrors the reference's catch-all outside debug mode
         if driver["setup"].get("debug_mode", True):
@@ -84,8 +86,8 @@ def run_one(driver: dict, dataset_name: str, method_name: str, seed: int, domain
         logger.exception(f"[Error] {e}")
         traceback.print_exc()
         result = {"errored": True}
-    result.update({"dataset_name": dataset_name, "seed": seed, "method_name": method_name,
-                   "domain_conf": domain_conf, "time_s": time.perf_counter() - t0})
+    # run_exp_wrapper_outer's keys (reference run.py:154-169), in the logged order
+    result.update({"dataset_name": dataset_name, "method_name": method_name, "domain_conf": domain_conf})
     return result
 
 
@@ -109,9 +111,11 @@ def main(argv=None):
         # single composed run, like `compose(config_name='ct_config', overrides=...)`
         args = C.compose(a.overrides)
         name = C.get_path(args, "dataset.equation_str")
+        t1 = time.perf_counter()
         r = train_sindy_main(args, dataset_name=name, device=a.device)
-        r.update({"errored": False, "dataset_name": name, "seed": C.get_path(args, "exp.seed", 0),
-                  "method_name": C.get_path(args, "model.name", "").lower()})
+        mname = C.get_path(args, "model.name", "").lower()
+        r.update({"method": mname, "seed": C.get_path(args, "exp.seed", 0), "seconds_taken": time.perf_counter() - t1,
+                  "errored": False, "dataset_name": name, "method_name": mname})
         results.append(r)
         logger.info(f"[Exp evaluation complete] {_printable(r)}")
     else:

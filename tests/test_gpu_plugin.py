@@ -93,3 +93,19 @@ def test_run_driver_end_to_end(dev):
         assert k in r
     assert np.isfinite(r["encoder_test_rmse_last"]) and r["fine_tuned"] is False
     assert r["global_equation_string"].startswith("Treatment 0: x_dot = +-1.0")
+
+
+def test_run_one_log_keys_match_reference(dev):
+    """run.py's per-run dict carries the reference's keys in its logged order (reference run.py:305-306 +
+    run_exp_wrapper_outer; results/2_main_table/final_with_insite.txt:126): ..., 'global_equation_string',
+    'fine_tuned', 'method', 'seed', 'seconds_taken', 'errored', 'dataset_name', 'method_name', 'domain_conf'."""
+    import run
+    from insite_amd import config as C
+    drv = C.driver_config()
+    r = run.run_one(drv, "EQ_4_A", "sindy", 0, 2.0, extra=["dataset.num_patients.train=100",
+                                                             "dataset.num_patients.val=10",
+                                                             "dataset.num_patients.test=10"], device=dev)
+    keys = list(r)
+    assert keys[-9:] == ["global_equation_string", "fine_tuned", "method", "seed", "seconds_taken", "errored",
+                         "dataset_name", "method_name", "domain_conf"]
+    assert r["method"] == "sindy" and r["errored"] is False and r["seconds_taken"] > 0
