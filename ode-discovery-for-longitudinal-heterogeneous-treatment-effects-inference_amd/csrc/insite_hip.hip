@@ -1834,6 +1834,174 @@ rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
   if (act && ra.steps) ra.steps[p] = attempts;
 }
 
+// Flat-loop form of the same controller (the default).  Each lane runs its own state machine over
+// (interval k, accepted step, attempt); one loop iteration = one step attempt of every lane, whatever
+// interval each lane is in.  The per-interval form above synchronises the wave at every interval
+// boundary AND at every accepted step (nested divergent loops: each accepted step waits for the lane
+// with the most rejections, each interval for the lane with the most steps), so a wave paid
+// sum_k sum_steps max_lanes(...); here it pays max_lanes(total attempts) plus the masked interval
+// set-up (select_initial_step) of whichever lanes start a new interval in that iteration.
+// Closed-form attempt: the RHS is affine in y on an interval, f(y) = al + be y, so the Dormand-Prince
+// stages are k_i = F q_i(z) with F = f(y), z = h be, and the tableau collapses (exact rational algebra,
+// tools/ derivation in DESIGN.md §5) to
+//   y_new = y + h F Q(z),  Q = 1 + z/2 + z^2/6 + z^3/24 + z^4/120 + z^5/600,
+//   f_new = F (1 + z Q(z)),   error = h F z^4 (97/120000 - 13 z/40000 + z^2/24000):
+// ~20 fp64 ops per attempt instead of ~60 (the kernel is VALU-bound: 1.87 ms at C5 with the stage form),
+// and the error estimate loses the stage form's cancellation (sum e_i = 0 over O(F) stages leaves an
+// O(F z^4) result with ~eps/z^4 relative rounding; here it is exact to rounding).  Step-size rules,
+// acceptance and select_initial_step are scipy's (rk.py / common.py), as in the per-interval kernel;
+// attempt counts agree with the stage-form oracle except where an err sits within its rounding of 1.
+template <int NARM, bool PERROW>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_RK45_WPE)))
+rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
+  constexpr double q2 = 1.0 / 2.0, q3 = 1.0 / 6.0, q4 = 1.0 / 24.0, q5 = 1.0 / 120.0, q6 = 1.0 / 600.0;
+  constexpr double p0 = 97.0 / 120000.0, p1 = -13.0 / 40000.0, p2 = 1.0 / 24000.0;
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool act = p < ra.N;
+  const int64_t pc = act ? p : ra.N - 1;
+  double uu[INSITE_MAX_STATICS];
+#pragma unroll
+  for (int t = 0; t < INSITE_MAX_STATICS; ++t) {
+    const double v = ra.u[pc * lib.U + (t < lib.U ? t : 0)];
+    uu[t] = (act && t < lib.U) ? v : 0.0;
+  }
+  double alpha[NARM], beta[NARM];
+  const double* cbase = ra.coef + (PERROW ? pc * ra.coef_stride : 0);
+#pragma unroll
+  for (int a = 0; a < NARM; ++a) {
+    alpha[a] = 0.0;
+    beta[a] = 0.0;
+    if (a >= ra.A) continue;
+    for (int j = 0; j < lib.F; ++j) {
+      const double c = cbase[a * lib.F + j];
+      if (fabs(c) > ra.drop) {
+        const double t = c * monomial(lib, j, uu);
+        if (lib.ex[j] == 0) alpha[a] += t;
+        else beta[a] += t;
+      }
+    }
+  }
+  int n = act ? ra.nobs[pc] : 0;
+  if (n > ra.Tmax) n = ra.Tmax;
+  const double rtol = ra.rtol, atol = ra.atol;
+  const int64_t wrd = pc >> 5;
+  const unsigned bit = (unsigned)(pc & 31);
+  // arms of up to 64 intervals gathered once into a per-lane mask (every wave load reads the 2 words of
+  // its 64 patients); longer grids read each interval's bit when the interval opens
+  const bool amask_ok = ra.Tmax <= 64;
+  unsigned long long amask = 0ull;
+  if (amask_ok)
+    for (int k = 0; k + 1 < ra.Tmax; ++k)
+      amask |= (unsigned long long)((ra.arm[(int64_t)k * ra.lda + wrd] >> bit) & 1u) << k;
+  double y = act ? ra.y0[pc] : 0.0;
+  int attempts = 0;
+  // state: interval k (its end t1, rates al/be), time t, f = f(y), h_abs; fresh = the next attempt starts
+  // an accepted step (min-step clamp, rejected flag reset); init = the interval's first step needs
+  // select_initial_step.  t_pf = t[k + 2] is requested when interval k opens (one interval of latency
+  // slack, ~3 attempts): the load is issued before y's store, so its wait never drains the stores.
+  int k = 0;
+  double t = 0.0, t1 = 0.0, al = alpha[0], be = beta[0], f = 0.0, h_abs = 0.0;
+  double t_pf = 0.0;
+  bool fresh = true, rejected = false, init = false;
+  auto t_at = [&](int kk) -> double { return kk < n ? ra.t[(int64_t)kk * ra.ldt + pc] : 0.0; };
+  // enter interval k (t1 = t_{k+1} known): rates of its arm, prefetch t_{k+2}; returns t < t1
+  auto enter = [&]() -> bool {
+    const int a = amask_ok ? (int)((amask >> k) & 1ull) : (int)((ra.arm[(int64_t)k * ra.lda + wrd] >> bit) & 1u);
+    al = alpha[0];
+    be = beta[0];
+#pragma unroll
+    for (int aa = 1; aa < NARM; ++aa) {
+      al = (a == aa) ? alpha[aa] : al;
+      be = (a == aa) ? beta[aa] : be;
+    }
+    t_pf = t_at(k + 2);
+    return t < t1;
+  };
+  // advance to the next interval that needs integration, storing y of every finished one (zero-length
+  // intervals: the per-interval kernel's `on && t < t1` test); returns whether one remains
+  auto open_interval = [&](bool first) -> bool {
+    if (first) {
+      if (!(1 < n)) return false;
+      t = t_at(0);
+      t1 = t_at(1);
+      if (enter()) {
+        init = true;
+        return true;
+      }
+    }
+    for (;;) {
+      const int kd = k;
+      ++k;
+      if (!(k + 1 < n)) {
+        __builtin_nontemporal_store(y, ra.y + (int64_t)kd * ra.ldy + p);
+        return false;
+      }
+      t = t1;          // t_k = t_{(k-1)+1}
+      t1 = t_pf;
+      const bool go = enter();   // issues the t_{k+2} load before the store below
+      __builtin_nontemporal_store(y, ra.y + (int64_t)kd * ra.ldy + p);
+      if (go) {
+        init = true;
+        return true;
+      }
+    }
+  };
+  bool live = act && open_interval(true);
+  while (__builtin_amdgcn_ballot_w64(live) != 0ull) {
+    if (live) {
+      if (init) {  // ---- select_initial_step (order 4, n = 1; common.py) ----
+        // affine RHS: f(y + h0 f) - f = be h0 f, so d2 = |f(y + h0 f) - f| / scale / h0 = |be| d1 exactly
+        f = fma(be, y, al);
+        const double interval = t1 - t;
+        const double scale = atol + fabs(y) * rtol;
+        const double d1 = fabs(f) / scale;
+        const bool tiny = fabs(y) < 1e-5 * scale || d1 < 1e-5;  // d0 < 1e-5 or d1 < 1e-5
+        const double h0 = fmin(tiny ? 1e-6 : 0.01 * fabs(y) / fabs(f), interval);  // 0.01 d0 / d1
+        const double d2 = fabs(be) * d1;
+        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : rk45_inv_root5(fmax(d1, d2) * 100.0);
+        h_abs = fmin(fmin(100.0 * h0, h1), interval);
+        init = false;
+        fresh = true;
+      }
+      if (fresh) {  // 10 ulp(t) minimum step (t >= 0: the next double up is the bit pattern + 1)
+        const double min_step = 10.0 * (__longlong_as_double(__double_as_longlong(t) + 1ll) - t);
+        if (h_abs < min_step) h_abs = min_step;
+        rejected = false;
+        fresh = false;
+      }
+      // ---- one attempt (closed form of the Dormand-Prince stages for the affine RHS) ----
+      double t_new = t + h_abs;
+      if (t_new > t1) t_new = t1;
+      const double h = t_new - t;
+      h_abs = fabs(h);
+      const double z = h * be;
+      const double Q = fma(fma(fma(fma(fma(q6, z, q5), z, q4), z, q3), z, q2), z, 1.0);
+      const double hF = h * f;
+      const double y_new = fma(hF, Q, y);
+      const double f_new = fma(f * z, Q, f);
+      const double z2 = z * z;
+      const double scale = atol + fmax(fabs(y), fabs(y_new)) * rtol;
+      const double err = fabs(hF * (z2 * z2) * fma(fma(p2, z, p1), z, p0)) / scale;
+      ++attempts;
+      const double r5 = rk45_inv_root5(err);
+      if (err < 1.0) {
+        double factor = err == 0.0 ? 10.0 : fmin(10.0, 0.9 * r5);
+        if (rejected) factor = fmin(1.0, factor);
+        h_abs *= factor;
+        t = t_new;
+        y = y_new;
+        f = f_new;
+        fresh = true;
+        if (!(t < t1)) live = open_interval(false);
+      } else {
+        h_abs *= fmax(0.2, 0.9 * r5);
+        rejected = true;
+      }
+    }
+  }
+  if (act && ra.steps) ra.steps[p] = attempts;
+}
+
 // =============================================================================================
 // INSITE per-patient refinement
 // =============================================================================================
@@ -3116,6 +3284,7 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   const bool perrow = coef_row_stride != 0;
+#ifdef INSITE_RK45_PER_INTERVAL  // the per-interval form (A/B builds, tools/build_ablation.sh)
   if (n_arms == 1) {
     if (perrow) rollout_rk45_kernel<1, true><<<grid, kBlock, 0, hs>>>(ra, lib);
     else rollout_rk45_kernel<1, false><<<grid, kBlock, 0, hs>>>(ra, lib);
@@ -3123,6 +3292,15 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
     if (perrow) rollout_rk45_kernel<2, true><<<grid, kBlock, 0, hs>>>(ra, lib);
     else rollout_rk45_kernel<2, false><<<grid, kBlock, 0, hs>>>(ra, lib);
   }
+#else
+  if (n_arms == 1) {
+    if (perrow) rollout_rk45_flat_kernel<1, true><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else rollout_rk45_flat_kernel<1, false><<<grid, kBlock, 0, hs>>>(ra, lib);
+  } else {
+    if (perrow) rollout_rk45_flat_kernel<2, true><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else rollout_rk45_flat_kernel<2, false><<<grid, kBlock, 0, hs>>>(ra, lib);
+  }
+#endif
   return launch_status();
 }
 

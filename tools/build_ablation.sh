@@ -4,10 +4,11 @@ set -e
 R="$(cd "$(dirname "$0")/.." && pwd)"
 P="$R/ode-discovery-for-longitudinal-heterogeneous-treatment-effects-inference_amd"
 rm -rf "$P/lib/ablate"; mkdir -p "$P/lib/ablate"
-build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC "$@" -I "$R/include" -o "$P/lib/ablate/libinsite_hip_$NAME.so" "$P/csrc/insite_hip.hip" "$P/csrc/insite_ms.hip" -lhiprtc & }
+build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC "$@" -I "$R/include" -o "$P/lib/ablate/libinsite_hip_$NAME.so" "$P/csrc/insite_hip.hip" "$P/csrc/insite_ms.hip" "$P/csrc/insite_gen.hip" -lhiprtc & }
 for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
   case $v in
     NOSTORE) NAME=$v build -DINSITE_ABLATE_NOSTORE ;;
+    RK45PI) NAME=$v build -DINSITE_RK45_PER_INTERVAL ;;
     SEGKC8) NAME=$v build -DINSITE_SEG_KC=8 -DINSITE_SEG_WPE=3 ;;
     SEGKC4) NAME=$v build -DINSITE_SEG_KC=4 -DINSITE_SEG_WPE=4 ;;
     SEGKC16) NAME=$v build -DINSITE_SEG_KC=16 -DINSITE_SEG_WPE=2 ;;
