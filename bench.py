@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rk45-identity-order", action="store_true",
+                    help="C5 ablation: lane r runs row r (no binning by n_obs)")
     ap.add_argument("--patients", type=int, default=100_000, help="patients per GPU (C2: 100k)")
     ap.add_argument("--T", type=int, default=200)
     ap.add_argument("--method", default="rk4", choices=["rk4", "euler5"])
@@ -403,19 +405,22 @@ def c5_main(args):
     g.manual_seed(args.seed * 1000 + 5 + rank)
     t_obs, n_obs = cohort.irregular_grid(N, seed=args.seed * 1000 + 4 + rank, device=dev)
     Tm = t_obs.size(0)
-    t_dev = torch.nan_to_num(t_obs, nan=0.0)
+    # patient-major grids, arms and outputs (INSITE_LAYOUT_PATIENT_MAJOR_BITS)
+    t_dev = torch.nan_to_num(t_obs, nan=0.0).t().contiguous()
     u = torch.randn((N, 2), generator=g, device=dev, dtype=torch.float64) * 0.05 + 0.5
     y0 = torch.rand((N,), generator=g, device=dev, dtype=torch.float64) * 49 + 1
-    arm = (torch.rand((Tm, N), generator=g, device=dev) < 0.5).to(torch.int8)
-    bits = ops.pack_arm_bits(arm, N)
+    arm = (torch.rand((N, Tm), generator=g, device=dev) < 0.5).to(torch.int8)
+    bits = ops.pack_arm_bits(arm, Tm)
     lib = polynomial_library(2, 2, True)
     coef = torch.zeros((2, lib.n_terms), dtype=torch.float64, device=dev)
     coef[0, 4], coef[1, 1], coef[1, 5] = C5_COEF
-    y = torch.empty((Tm, N), dtype=torch.float64, device=dev)
+    y = torch.empty((N, Tm), dtype=torch.float64, device=dev)
     steps = torch.empty((N,), dtype=torch.int32, device=dev)
 
-    def run():
-        ops.rollout_rk45(y0, u, bits, t_dev, n_obs, coef, lib, out=y, steps=steps)
+    order = not args.rk45_identity_order
+
+    def run():   # binning by n_obs (ops.rk45_order) runs inside every step
+        ops.rollout_rk45(y0, u, bits, t_dev, n_obs, coef, lib, out=y, steps=steps, layout="patient", order=order)
 
     for _ in range(args.warmup):
         run()
@@ -439,7 +444,8 @@ def c5_main(args):
     torch.cuda.synchronize(dev)
     launch_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     st = steps.to(torch.float64)
-    per_wave = st[: N // 64 * 64].view(-1, 64)
+    # waves as the kernel formed them: lanes take rows in the binned order (ops.rk45_order)
+    per_wave = (st[ops.rk45_order(n_obs, Tm).long()] if order else st)[: N // 64 * 64].view(-1, 64)
     intervals = (n_obs - 1).to(torch.float64)
     attempts = float(st.sum())
     flop = attempts * RK45_FLOP_PER_ATTEMPT
@@ -457,8 +463,8 @@ def c5_main(args):
                      "frac": flop / (launch_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS, "traffic": None,
                      "avg_launch_ms": launch_ms, "flop_per_attempt": RK45_FLOP_PER_ATTEMPT,
                      "issued_incl_divergence_TFLOPs": issued / (launch_ms * 1e-3) / 1e12,
-                     "algorithmic_bytes": N * (8 * 3 + 4) + N * Tm * 8 * 2 + Tm * ((N + 31) // 32) * 4,
-                     "achieved_GBps": (N * (8 * 3 + 4) + N * Tm * 8 * 2 + Tm * ((N + 31) // 32) * 4) / (launch_ms * 1e-3) / 1e9},
+                     "algorithmic_bytes": N * (8 * 3 + 4) + N * Tm * 8 * 2 + N * ((Tm + 30) // 32) * 4,
+                     "achieved_GBps": (N * (8 * 3 + 4) + N * Tm * 8 * 2 + N * ((Tm + 30) // 32) * 4) / (launch_ms * 1e-3) / 1e9},
         "rk45": {"mean_attempts_per_patient": float(st.mean()),
                  "mean_attempts_per_interval": float(st.sum() / intervals.sum()),
                  "wave_divergence": float((per_wave.max(dim=1).values.mean() / per_wave.mean()).item()),

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define INSITE_ABI_VERSION 2
+#define INSITE_ABI_VERSION 3
 
 /* status codes */
 #define INSITE_OK 0
@@ -79,6 +79,8 @@ extern "C" {
 #define INSITE_LAYOUT_PATIENT_MAJOR 0
 #define INSITE_LAYOUT_TIME_MAJOR 1
 #define INSITE_LAYOUT_TIME_MAJOR_BITS 2
+#define INSITE_LAYOUT_PATIENT_MAJOR_BITS 3 /* insite_rollout_rk45_f64 only: t_obs / y_out [n_rows, ld],
+                                            arm bits [n_rows, ld_arm] words, bit k & 31 of word k >> 5 */
 
 /* limits of this ABI version */
 #define INSITE_MAX_TERMS 9  /* F of the fused affine path (one Gram/moment entry per lane, F(F+1)/2 + F <= 64);
@@ -206,20 +208,37 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
                            double drop_below, double* y_out, int64_t ld_y, int32_t layout, void* stream);
 
 /* Adaptive RK45 rollout on irregular observation grids (configuration C5): for patient r and
- * interval k < n_obs[r] - 1, y advances from t_obs[k, r] to t_obs[k + 1, r] under the arm of bit
- * (r, k) of arm_bits (TIME_MAJOR_BITS [T_max, ld_arm], n_arms <= 2) by scipy's
+ * interval k < n_obs[r] - 1, y advances from t_obs(r, k) to t_obs(r, k + 1) under the arm of bit
+ * (r, k) of arm_bits (n_arms <= 2) by scipy's
  * solve_ivp(method='RK45', rtol, atol) controller (Dormand-Prince 5(4), select_initial_step per
  * interval; the reference odeint's tolerances are rtol = atol = 1.4e-8, pkpd/utils.py:87).  This
  * replaces the fixed-grid odeint scan (sindy.py:413-424) when the observation times are irregular.
- *   t_obs [T_max, ld_t] f64 time-major (ld_t >= n_rows), n_obs [n_rows] int32 in [1, T_max]
+ *   layout INSITE_LAYOUT_TIME_MAJOR_BITS: t_obs [T_max, ld_t] f64 (ld_t >= n_rows), y_out [T_max, ld_y],
+ *          arm_bits [T_max, ld_arm >= ceil(n_rows / 32)] (bit r & 31 of word r >> 5 in row k);
+ *   layout INSITE_LAYOUT_PATIENT_MAJOR_BITS (ABI 3; the fast one): t_obs [n_rows, ld_t >= T_max],
+ *          y_out [n_rows, ld_y >= T_max], arm_bits [n_rows, ld_arm >= ceil((T_max - 1) / 32)] (bit k & 31
+ *          of word k >> 5 in row r).  A lane's window refills and stores stay within its own row, so
+ *          binned row orders cost no coalescing.
+ *   n_obs [n_rows] int32 in [1, T_max]
  *   coef  [n_arms, F] or per row [n_rows, n_arms, F] (coef_row_stride = n_arms * F)
- *   y_out [T_max, ld_y] f64: row k = state at t_obs[k + 1] (rows >= n_obs[r] - 1 untouched)
- *   steps_out [n_rows] int32 step attempts (accepted + rejected) per row, may be NULL        */
+ *   y_out element (r, k) = state at t_obs(r, k + 1) (elements k >= n_obs[r] - 1 untouched)
+ *   steps_out [n_rows] int32 step attempts (accepted + rejected) per row, may be NULL
+ *   row_order [n_rows] int32 lane -> row map, a permutation of [0, n_rows) (insite_rk45_order_i32), or
+ *             NULL for lane r = row r.  Outputs do not depend on it; rows binned by n_obs keep the
+ *             wavefronts' step counts uniform (a wave runs until its slowest lane has finished).  (ABI 3) */
 int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_t* arm_bits, int64_t ld_arm,
                                 const double* t_obs, int64_t ld_t, const int32_t* n_obs, const double* coef,
                                 int64_t coef_row_stride, const int8_t* exps, int32_t n_terms, int64_t n_rows,
                                 int32_t T_max, int32_t n_statics, int32_t n_arms, double rtol, double atol,
-                                double drop_below, double* y_out, int64_t ld_y, int32_t* steps_out, void* stream);
+                                double drop_below, double* y_out, int64_t ld_y, int32_t* steps_out,
+                                const int32_t* row_order, int32_t layout, void* stream);
+
+/* Lane order for insite_rollout_rk45_f64: rows sorted by n_obs, descending (counting sort on the
+ * device; bins min(n_obs, 1023)).  No reference counterpart (scheduling only).  n_rows <= INT32_MAX.
+ *   n_obs [n_rows] int32, order_out [n_rows] int32; workspace >= insite_rk45_order_workspace_bytes. */
+size_t insite_rk45_order_workspace_bytes(int32_t T_max);
+int32_t insite_rk45_order_i32(const int32_t* n_obs, int64_t n_rows, int32_t T_max, int32_t* order_out, void* workspace,
+                              size_t workspace_bytes, void* stream);
 
 /* INSITE per-patient refinement (reference SINDY._get_fine_tuned_predictions /
  * f_to_min_func / predict_with_reduced_coefs, sindy.py:433-715, 767-794): for every row r with

@@ -1676,12 +1676,13 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
 struct Rk45Args {
   const double* y0;
   const double* u;
-  const uint32_t* arm;  // TIME_MAJOR_BITS [T_max, lda]: arm of interval k
-  const double* t;      // [T_max, ldt] observation times (time-major)
+  const uint32_t* arm;  // TIME_MAJOR_BITS [T_max, lda] / PATIENT_MAJOR_BITS [N, lda]: arm of interval k
+  const double* t;      // [T_max, ldt] (time-major) / [N, ldt] (patient-major) observation times
   const int32_t* nobs;  // [N] observations per patient (intervals = nobs - 1)
   const double* coef;
-  double* y;            // [T_max, ldy]: row k = state at t[k + 1]
+  double* y;            // [T_max, ldy] / [N, ldy]: element k = state at t[k + 1]
   int32_t* steps;       // [N] RK45 step attempts (may be NULL)
+  const int32_t* order; // [N] lane -> row (rows binned by n_obs, insite_rk45_order_i32), NULL = identity
   int64_t lda, ldt, ldy, coef_stride, N;
   int32_t Tmax, A;
   double rtol, atol, drop;
@@ -1689,17 +1690,24 @@ struct Rk45Args {
 
 // e^(-1/5) for the RK45 step-size rules (scipy rk.py: `error_norm ** error_exponent`, exponent -1/5, once
 // per attempt; common.py select_initial_step: `(0.01 / max(d1, d2)) ** (1 / (order + 1))`, once per
-// interval).  e = m 2^(5q) with m in [1, 64) (exact power-of-two scaling), so e^(-1/5) = m^(-1/5) 2^(-q);
-// a fp32 hardware estimate of m^(-1/5) (v_log_f32 / v_exp_f32, relative error ~1e-7) is refined by two
-// division-free Newton steps on x^5 m = 1, x <- x (1 - r / 5), r = x^5 m - 1 (error 3 delta^2 per step):
-// fp64 accuracy of the exact fifth root (pow's exponent is the double 0.2 = 1/5 + 1.1e-17, i.e. a
-// relative 1.1e-17 |ln e| away: < 1 ulp for controller errors in [1e-6, 1e4]) in ~20 VALU ops instead of ocml's double-double pow_f64 (>100), the
-// per-attempt cost that dominated the step loop.  Zero, infinite and NaN inputs take pow itself.
+// interval).  A fp32 hardware estimate (v_log_f32 / v_exp_f32 on the rounded argument, relative error
+// ~1e-6 for |log2 e| <= 120) is refined by two division-free Newton steps on x^5 e = 1,
+// x <- x (1 - r / 5), r = x^5 e - 1 (error 3 delta^2 per step): fp64 accuracy of the exact fifth root
+// (pow's exponent is the double 0.2 = 1/5 + 1.1e-17, i.e. a relative 1.1e-17 |ln e| away: < 1 ulp for
+// controller errors in [1e-6, 1e4]) in ~16 VALU ops instead of ocml's double-double pow_f64 (>100), the
+// per-attempt cost that dominated the step loop.  Arguments outside [2^-120, 2^120] (x^5 e would leave
+// the fp64 range's comfort zone / the fp32 estimate would flush) take the exactly range-reduced form
+// e = m 2^(5q), m in [1, 64), on a branch no realistic controller error reaches; zero, infinite and NaN
+// inputs get pow's values (inf, 0, NaN) by select, so no pow body is inlined into the loop's registers.
 __device__ __forceinline__ double rk45_inv_root5(double e) {
-  if (!(e > 0.0 && e < INFINITY)) return pow(e, -0.2);
-  const int k = ilogb(e);
-  const int q = (k >= 0 ? k : k - 4) / 5;  // floor(k / 5)
-  const double m = ldexp(e, -5 * q);
+  double m = e;
+  int q = 0;
+  if (!(e >= 0x1p-120 && e <= 0x1p120)) {
+    if (!(e > 0.0 && e < INFINITY)) return e == 0.0 ? INFINITY : e == INFINITY ? 0.0 : __builtin_nan("");
+    const int k = ilogb(e);
+    q = (k >= 0 ? k : k - 4) / 5;  // floor(k / 5)
+    m = ldexp(e, -5 * q);
+  }
   double x = (double)__builtin_amdgcn_exp2f(-0.2f * __builtin_amdgcn_logf((float)m));
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -1707,7 +1715,16 @@ __device__ __forceinline__ double rk45_inv_root5(double e) {
     const double r = fma(x2 * x2 * x, m, -1.0);
     x = fma(-0.2 * x, r, x);
   }
-  return ldexp(x, -q);
+  return q == 0 ? x : ldexp(x, -q);
+}
+
+// 1 / b for the controller's norms (b a positive normal double: atol + |y| rtol, |f| > 0): the hardware
+// v_rcp_f64 estimate and two Newton steps, ~1 ulp, 5 VALU ops against the 11 of an IEEE division -- the
+// quotients feed comparisons with 1 and 1e-5 and the fifth root, where an ulp only matters at exact ties.
+__device__ __forceinline__ double rk45_rcp(double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  r = fma(fma(-b, r, 1.0), r, r);
+  return fma(fma(-b, r, 1.0), r, r);
 }
 
 #ifndef INSITE_RK45_WPE
@@ -1834,31 +1851,83 @@ rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
   if (act && ra.steps) ra.steps[p] = attempts;
 }
 
+// Per-patient affine rates of every arm, f_a(y) = alpha_a + beta_a y: columns with x-exponent 0 feed alpha,
+// exponent 1 beta.  Loops run over the descriptor's compile-time bounds (F <= INSITE_MAX_TERMS, U <=
+// INSITE_MAX_STATICS, u-exponents <= 8 checked by build_lib) so every descriptor byte is read at a constant
+// kernel-argument offset (scalar loads issued together), not one dependent vector load per term.
+template <int NARM>
+__device__ __forceinline__ void affine_rates(const LibDesc& lib, const double* cbase, int A, double drop,
+                                             const double* uu, double* alpha, double* beta) {
+#pragma unroll
+  for (int a = 0; a < NARM; ++a) alpha[a] = beta[a] = 0.0;
+#pragma unroll
+  for (int j = 0; j < INSITE_MAX_TERMS; ++j) {
+    if (j >= lib.F) break;
+    double m = 1.0;
+#pragma unroll
+    for (int i = 0; i < INSITE_MAX_STATICS; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m *= e < lib.eu[j][i] ? uu[i] : 1.0;
+    const bool lin = lib.ex[j] != 0;
+#pragma unroll
+    for (int a = 0; a < NARM; ++a) {
+      if (a >= A) break;
+      const double c = cbase[a * lib.F + j];
+      const double v = fabs(c) > drop ? c * m : 0.0;
+      if (lin) beta[a] += v;
+      else alpha[a] += v;
+    }
+  }
+}
+
 // Flat-loop form of the same controller (the default).  Each lane runs its own state machine over
 // (interval k, accepted step, attempt); one loop iteration = one step attempt of every lane, whatever
 // interval each lane is in.  The per-interval form above synchronises the wave at every interval
 // boundary AND at every accepted step (nested divergent loops: each accepted step waits for the lane
 // with the most rejections, each interval for the lane with the most steps), so a wave paid
-// sum_k sum_steps max_lanes(...); here it pays max_lanes(total attempts) plus the masked interval
-// set-up (select_initial_step) of whichever lanes start a new interval in that iteration.
+// sum_k sum_steps max_lanes(...); here it pays max_lanes(total attempts).
 // Closed-form attempt: the RHS is affine in y on an interval, f(y) = al + be y, so the Dormand-Prince
 // stages are k_i = F q_i(z) with F = f(y), z = h be, and the tableau collapses (exact rational algebra,
-// tools/ derivation in DESIGN.md §5) to
+// DESIGN.md §5) to
 //   y_new = y + h F Q(z),  Q = 1 + z/2 + z^2/6 + z^3/24 + z^4/120 + z^5/600,
 //   f_new = F (1 + z Q(z)),   error = h F z^4 (97/120000 - 13 z/40000 + z^2/24000):
-// ~20 fp64 ops per attempt instead of ~60 (the kernel is VALU-bound: 1.87 ms at C5 with the stage form),
-// and the error estimate loses the stage form's cancellation (sum e_i = 0 over O(F) stages leaves an
-// O(F z^4) result with ~eps/z^4 relative rounding; here it is exact to rounding).  Step-size rules,
-// acceptance and select_initial_step are scipy's (rk.py / common.py), as in the per-interval kernel;
-// attempt counts agree with the stage-form oracle except where an err sits within its rounding of 1.
-template <int NARM, bool PERROW>
+// ~20 fp64 ops per attempt instead of ~60, and the error estimate loses the stage form's cancellation
+// (sum e_i = 0 over O(F) stages leaves an O(F z^4) result with ~eps/z^4 relative rounding; here it is
+// exact to rounding).  Step-size rules, acceptance and select_initial_step are scipy's (rk.py /
+// common.py), as in the per-interval kernel; attempt counts agree with the stage-form oracle except where
+// an err sits within its rounding of 1.
+// One fifth root per iteration: every branch any lane takes is issued for the whole wave, and the two
+// e^(-1/5) of the controller never meet in one lane-iteration -- the step factor of an accepted step that
+// ENDS its interval is discarded (solve_ivp restarts per interval, so the next interval's h comes from
+// select_initial_step), so that lane roots the initial-step argument instead.  The accept / reject / open
+// updates of h_abs are selects; only the interval close (a store and an LDS read) branches.
+// Observation times come from a per-lane LDS window t[base .. base + kRkWin) ([slot][lane] layout: a wave's
+// ds_read_b64 is conflict-free), refilled for every live lane of the wave at once when some lane's next close
+// would run past its window: a vector-memory wait is paid once per refill (every ~kRkWin intervals of the
+// fastest lane), not once per iteration.  (vmcnt is per wave: with a load issued at every close, and some
+// lane closing in nearly every iteration, a register queue waits on the previous iteration's load.)
+#ifndef INSITE_RK45_WIN
+#define INSITE_RK45_WIN 16
+#endif
+// PM: patient-major t / y / arm bits (INSITE_LAYOUT_PATIENT_MAJOR_BITS): a lane's window refill reads one
+// contiguous run and its y elements share lines that only this lane writes, whatever rows the lanes hold
+// -- the layout that lets rows be binned by n_obs without scattering the memory traffic.
+#ifndef INSITE_RK45_PM_NT
+#define INSITE_RK45_PM_NT 0
+#endif
+constexpr int kRkWin = INSITE_RK45_WIN;
+template <int NARM, bool PERROW, bool PM>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_RK45_WPE)))
 rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
   constexpr double q2 = 1.0 / 2.0, q3 = 1.0 / 6.0, q4 = 1.0 / 24.0, q5 = 1.0 / 120.0, q6 = 1.0 / 600.0;
   constexpr double p0 = 97.0 / 120000.0, p1 = -13.0 / 40000.0, p2 = 1.0 / 24000.0;
-  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const bool act = p < ra.N;
-  const int64_t pc = act ? p : ra.N - 1;
+  __shared__ double t_win[kWavesPerBlock * kRkWin * kWave];
+  const int64_t lane_id = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool act = lane_id < ra.N;
+  int64_t p = act ? (ra.order ? (int64_t)ra.order[lane_id] : lane_id) : ra.N - 1;  // this lane's row
+  p = p < 0 ? 0 : p >= ra.N ? ra.N - 1 : p;  // memory-safe on a malformed order (documented: a permutation)
+  const int64_t pc = p;
+  double* tw = t_win + (threadIdx.x / kWave) * (kRkWin * kWave) + (threadIdx.x & (kWave - 1));
   double uu[INSITE_MAX_STATICS];
 #pragma unroll
   for (int t = 0; t < INSITE_MAX_STATICS; ++t) {
@@ -1866,112 +1935,115 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
     uu[t] = (act && t < lib.U) ? v : 0.0;
   }
   double alpha[NARM], beta[NARM];
-  const double* cbase = ra.coef + (PERROW ? pc * ra.coef_stride : 0);
-#pragma unroll
-  for (int a = 0; a < NARM; ++a) {
-    alpha[a] = 0.0;
-    beta[a] = 0.0;
-    if (a >= ra.A) continue;
-    for (int j = 0; j < lib.F; ++j) {
-      const double c = cbase[a * lib.F + j];
-      if (fabs(c) > ra.drop) {
-        const double t = c * monomial(lib, j, uu);
-        if (lib.ex[j] == 0) alpha[a] += t;
-        else beta[a] += t;
-      }
-    }
-  }
+  affine_rates<NARM>(lib, ra.coef + (PERROW ? pc * ra.coef_stride : 0), ra.A, ra.drop, uu, alpha, beta);
   int n = act ? ra.nobs[pc] : 0;
   if (n > ra.Tmax) n = ra.Tmax;
   const double rtol = ra.rtol, atol = ra.atol;
-  const int64_t wrd = pc >> 5;
-  const unsigned bit = (unsigned)(pc & 31);
-  // arms of up to 64 intervals gathered once into a per-lane mask (every wave load reads the 2 words of
-  // its 64 patients); longer grids read each interval's bit when the interval opens
+  const int64_t wrd = PM ? pc * ra.lda : pc >> 5;  // PM: the row's first word; else the word column
+  const unsigned bit = PM ? 0u : (unsigned)(pc & 31);
+  // arms of up to 64 intervals gathered once into a per-lane mask (PM: the row's two words; time-major:
+  // 16 independent loads in flight per round, clamped rows, masked bits); longer grids read each
+  // interval's bit when the interval opens
   const bool amask_ok = ra.Tmax <= 64;
   unsigned long long amask = 0ull;
-  if (amask_ok)
-    for (int k = 0; k + 1 < ra.Tmax; ++k)
-      amask |= (unsigned long long)((ra.arm[(int64_t)k * ra.lda + wrd] >> bit) & 1u) << k;
+  if (PM && NARM > 1 && amask_ok) {
+    const uint32_t w0 = ra.arm[wrd], w1 = ra.Tmax > 33 ? ra.arm[wrd + 1] : 0u;
+    amask = (unsigned long long)w0 | ((unsigned long long)w1 << 32);
+  }
+  if (!PM && NARM > 1 && amask_ok) {
+    for (int k0 = 0; k0 + 1 < ra.Tmax; k0 += 16) {
+      uint32_t w[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int kk = k0 + j < ra.Tmax - 1 ? k0 + j : ra.Tmax - 2;
+        w[j] = ra.arm[(int64_t)(kk < 0 ? 0 : kk) * ra.lda + wrd];
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (k0 + j + 1 < ra.Tmax) amask |= (unsigned long long)((w[j] >> bit) & 1u) << (k0 + j);
+    }
+  }
   double y = act ? ra.y0[pc] : 0.0;
   int attempts = 0;
-  // state: interval k (its end t1, rates al/be), time t, f = f(y), h_abs; fresh = the next attempt starts
-  // an accepted step (min-step clamp, rejected flag reset); init = the interval's first step needs
-  // select_initial_step.  t_pf = t[k + 2] is requested when interval k opens (one interval of latency
-  // slack, ~3 attempts): the load is issued before y's store, so its wait never drains the stores.
-  int k = 0;
+  // lane state: interval k with end t1 and rates al/be; time t, f = f(y), h_abs; rejected = the current
+  // step has had a rejected attempt; the window holds t[base .. base + kRkWin); yp = row k of y
+  int k = 0, base = 0;
   double t = 0.0, t1 = 0.0, al = alpha[0], be = beta[0], f = 0.0, h_abs = 0.0;
-  double t_pf = 0.0;
-  bool fresh = true, rejected = false, init = false;
-  auto t_at = [&](int kk) -> double { return kk < n ? ra.t[(int64_t)kk * ra.ldt + pc] : 0.0; };
-  // enter interval k (t1 = t_{k+1} known): rates of its arm, prefetch t_{k+2}; returns t < t1
-  auto enter = [&]() -> bool {
-    const int a = amask_ok ? (int)((amask >> k) & 1ull) : (int)((ra.arm[(int64_t)k * ra.lda + wrd] >> bit) & 1u);
-    al = alpha[0];
-    be = beta[0];
+  bool rejected = false;
+  double* yp = ra.y + (PM ? p * ra.ldy : p);
+  const int64_t ystep = PM ? 1 : ra.ldy;
+  const int64_t tstep = PM ? 1 : ra.ldt;
+  const double* trow = ra.t + (PM ? pc * ra.ldt : pc);
+  auto refill = [&](int from) {  // elements clamped to n - 1 (n >= 2 for a live lane)
+    base = from;
 #pragma unroll
-    for (int aa = 1; aa < NARM; ++aa) {
-      al = (a == aa) ? alpha[aa] : al;
-      be = (a == aa) ? beta[aa] : be;
+    for (int j0 = 0; j0 < kRkWin; j0 += 8) {
+      double v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = from + j0 + j < n ? from + j0 + j : n - 1;
+        v[j] = trow[(int64_t)r * tstep];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tw[(j0 + j) * kWave] = v[j];
     }
-    t_pf = t_at(k + 2);
-    return t < t1;
   };
-  // advance to the next interval that needs integration, storing y of every finished one (zero-length
-  // intervals: the per-interval kernel's `on && t < t1` test); returns whether one remains
-  auto open_interval = [&](bool first) -> bool {
-    if (first) {
-      if (!(1 < n)) return false;
-      t = t_at(0);
-      t1 = t_at(1);
-      if (enter()) {
-        init = true;
-        return true;
-      }
-    }
-    for (;;) {
-      const int kd = k;
-      ++k;
-      if (!(k + 1 < n)) {
-        __builtin_nontemporal_store(y, ra.y + (int64_t)kd * ra.ldy + p);
-        return false;
-      }
-      t = t1;          // t_k = t_{(k-1)+1}
-      t1 = t_pf;
-      const bool go = enter();   // issues the t_{k+2} load before the store below
-      __builtin_nontemporal_store(y, ra.y + (int64_t)kd * ra.ldy + p);
-      if (go) {
-        init = true;
-        return true;
+  auto rates = [&]() {
+    if (NARM > 1) {
+      const int a = amask_ok ? (int)((amask >> k) & 1ull)
+                    : PM ? (int)((ra.arm[wrd + (k >> 5)] >> (k & 31)) & 1u)
+                         : (int)((ra.arm[(int64_t)k * ra.lda + wrd] >> bit) & 1u);
+      al = alpha[0];
+      be = beta[0];
+#pragma unroll
+      for (int aa = 1; aa < NARM; ++aa) {
+        al = (a == aa) ? alpha[aa] : al;
+        be = (a == aa) ? beta[aa] : be;
       }
     }
   };
-  bool live = act && open_interval(true);
+  // select_initial_step (order 4, n = 1; common.py), split around the shared fifth root.  Affine RHS:
+  // f(y + h0 f) - f = be h0 f, so d2 = |f(y + h0 f) - f| / scale / h0 = |be| d1 exactly.
+  double h0 = 0.0, span = 0.0;
+  bool small = false;
+  auto init_front = [&]() -> double {  // returns the root argument max(d1, d2) * 100 = (0.01 / max)^-1
+    f = fma(be, y, al);
+    span = t1 - t;
+    const double scale = atol + fabs(y) * rtol;
+    const double d1 = fabs(f) * rk45_rcp(scale);
+    const bool tiny = fabs(y) < 1e-5 * scale || d1 < 1e-5;  // d0 < 1e-5 or d1 < 1e-5
+    h0 = fmin(tiny ? 1e-6 : 0.01 * fabs(y) * rk45_rcp(fabs(f)), span);  // 0.01 d0 / d1 (|f| > 0 when used)
+    const double d2 = fabs(be) * d1;
+    small = d1 <= 1e-15 && d2 <= 1e-15;
+    return small ? 1.0 : fmax(d1, d2) * 100.0;
+  };
+  auto init_h = [&](double r) { return fmin(fmin(100.0 * h0, small ? fmax(1e-6, h0 * 1e-3) : r), span); };
+  // start of a step (rk.py _step_impl): min_step = 10 |nextafter(t, inf) - t|, the neighbour taken on the
+  // bit pattern of |t| (+1 above a non-negative t, -1 below |t| for a negative one)
+  auto min_step = [&]() {
+    const double at = fabs(t);
+    const long long tb = __double_as_longlong(at);
+    return 10.0 * (t >= 0.0 ? __longlong_as_double(tb + 1ll) - at : at - __longlong_as_double(tb - 1ll));
+  };
+  bool live = false;
+  if (act && 1 < n) {
+    t = trow[0];
+    refill(1);
+    t1 = tw[0];
+    rates();
+    live = true;
+    h_abs = fmax(init_h(rk45_inv_root5(init_front())), min_step());
+  }
   while (__builtin_amdgcn_ballot_w64(live) != 0ull) {
+    // a close in this iteration reads t[k + 2]: refill every live lane when some lane's window ends before
+    if (__builtin_amdgcn_ballot_w64(live && k + 2 >= base + kRkWin) != 0ull)
+      if (live) refill(k + 2);
     if (live) {
-      if (init) {  // ---- select_initial_step (order 4, n = 1; common.py) ----
-        // affine RHS: f(y + h0 f) - f = be h0 f, so d2 = |f(y + h0 f) - f| / scale / h0 = |be| d1 exactly
-        f = fma(be, y, al);
-        const double interval = t1 - t;
-        const double scale = atol + fabs(y) * rtol;
-        const double d1 = fabs(f) / scale;
-        const bool tiny = fabs(y) < 1e-5 * scale || d1 < 1e-5;  // d0 < 1e-5 or d1 < 1e-5
-        const double h0 = fmin(tiny ? 1e-6 : 0.01 * fabs(y) / fabs(f), interval);  // 0.01 d0 / d1
-        const double d2 = fabs(be) * d1;
-        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : rk45_inv_root5(fmax(d1, d2) * 100.0);
-        h_abs = fmin(fmin(100.0 * h0, h1), interval);
-        init = false;
-        fresh = true;
-      }
-      if (fresh) {  // 10 ulp(t) minimum step (t >= 0: the next double up is the bit pattern + 1)
-        const double min_step = 10.0 * (__longlong_as_double(__double_as_longlong(t) + 1ll) - t);
-        if (h_abs < min_step) h_abs = min_step;
-        rejected = false;
-        fresh = false;
-      }
       // ---- one attempt (closed form of the Dormand-Prince stages for the affine RHS) ----
+      const bool open = t < t1;  // false: zero-length / reversed interval, closed with h = 0, no attempt
       double t_new = t + h_abs;
       if (t_new > t1) t_new = t1;
+      if (!open) t_new = t;
       const double h = t_new - t;
       h_abs = fabs(h);
       const double z = h * be;
@@ -1981,25 +2053,91 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
       const double f_new = fma(f * z, Q, f);
       const double z2 = z * z;
       const double scale = atol + fmax(fabs(y), fabs(y_new)) * rtol;
-      const double err = fabs(hF * (z2 * z2) * fma(fma(p2, z, p1), z, p0)) / scale;
-      ++attempts;
-      const double r5 = rk45_inv_root5(err);
-      if (err < 1.0) {
-        double factor = err == 0.0 ? 10.0 : fmin(10.0, 0.9 * r5);
-        if (rejected) factor = fmin(1.0, factor);
-        h_abs *= factor;
+      const double err = fabs(hF * (z2 * z2) * fma(fma(p2, z, p1), z, p0)) * rk45_rcp(scale);
+      attempts += open;
+      const bool acc = err < 1.0;
+      const bool close = acc && !(t_new < t1);  // the interval is done: its step factor is discarded
+      double rarg = err == 0.0 ? 1.0 : err;
+      if (acc) {
         t = t_new;
         y = y_new;
         f = f_new;
-        fresh = true;
-        if (!(t < t1)) live = open_interval(false);
-      } else {
-        h_abs *= fmax(0.2, 0.9 * r5);
-        rejected = true;
       }
+      if (close) {  // store y at t_{k+1} (row k), open interval k + 1 from the window
+        if (PM && !INSITE_RK45_PM_NT) *yp = y;  // PM: cached store, the lane's own line fills in L2
+        else __builtin_nontemporal_store(y, yp);
+        yp += ystep;
+        t = t1;
+        ++k;
+        t1 = tw[(k + 1 - base) * kWave];
+        rates();
+        live = k + 1 < n;
+        rarg = init_front();
+      }
+      const double r5 = rk45_inv_root5(rarg);
+      double factor = err == 0.0 ? 10.0 : fmin(10.0, 0.9 * r5);
+      if (rejected) factor = fmin(1.0, factor);
+      const double h_next = close ? init_h(r5) : acc ? h_abs * factor : h_abs * fmax(0.2, 0.9 * r5);
+      h_abs = acc ? fmax(h_next, min_step()) : h_next;  // a new step starts after an accept or a close
+      rejected = !acc;
     }
   }
   if (act && ra.steps) ra.steps[p] = attempts;
+}
+
+// Row binning for the RK45 rollout: a wave runs until its slowest lane has finished, and a patient's
+// attempt count grows with its number of observation intervals, so lanes are given rows grouped by n_obs
+// (descending: the longest waves are dispatched first and short ones fill the tail).  Counting sort in two
+// passes over n_obs; the order inside a bin is whatever the atomics give -- every row's trajectory is
+// independent of the lane it runs on, so outputs do not depend on it.
+constexpr int kRkBinMax = 1024;   // bins: key = min(n_obs, min(T_max, kRkBinMax - 1))
+constexpr int kRkBinChunk = 4096; // rows per block
+__device__ __forceinline__ int rk45_bin(int32_t n, int nb) { return nb - 1 - (n < 0 ? 0 : n > nb - 1 ? nb - 1 : n); }
+
+__global__ void __launch_bounds__(kBlock) rk45_bin_count_kernel(const int32_t* __restrict__ nobs, int64_t N, int nb,
+                                                                 unsigned* __restrict__ hist) {
+  __shared__ unsigned h[kRkBinMax];
+  for (int b = threadIdx.x; b < nb; b += kBlock) h[b] = 0u;
+  __syncthreads();
+  const int64_t lo = (int64_t)blockIdx.x * kRkBinChunk;
+  for (int j = threadIdx.x; j < kRkBinChunk; j += kBlock)
+    if (lo + j < N) atomicAdd(&h[rk45_bin(nobs[lo + j], nb)], 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += kBlock)
+    if (h[b]) atomicAdd(&hist[b], h[b]);
+}
+
+__global__ void __launch_bounds__(kBlock) rk45_bin_scatter_kernel(const int32_t* __restrict__ nobs, int64_t N, int nb,
+                                                                   const unsigned* __restrict__ hist,
+                                                                   unsigned* __restrict__ cursor,
+                                                                   int32_t* __restrict__ order) {
+  __shared__ unsigned base[kRkBinMax], cnt[kRkBinMax];
+  constexpr int kPer = kRkBinChunk / kBlock;
+  for (int b = threadIdx.x; b < nb; b += kBlock) cnt[b] = 0u;
+  if (threadIdx.x == 0) {  // exclusive scan of the global histogram (nb <= 1024 serial adds, once per block)
+    unsigned acc = 0u;
+    for (int b = 0; b < nb; ++b) {
+      base[b] = acc;
+      acc += hist[b];
+    }
+  }
+  __syncthreads();
+  const int64_t lo = (int64_t)blockIdx.x * kRkBinChunk;
+  int bin[kPer];
+  unsigned rank[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int64_t i = lo + q * kBlock + threadIdx.x;
+    bin[q] = i < N ? rk45_bin(nobs[i], nb) : -1;
+    rank[q] = bin[q] >= 0 ? atomicAdd(&cnt[bin[q]], 1u) : 0u;
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += kBlock)
+    if (cnt[b]) base[b] += atomicAdd(&cursor[b], cnt[b]);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kPer; ++q)
+    if (bin[q] >= 0) order[base[bin[q]] + rank[q]] = (int32_t)(lo + q * kBlock + threadIdx.x);
 }
 
 // =============================================================================================
@@ -3264,13 +3402,33 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
   return launch_status();
 }
 
+extern "C++" {
+namespace {
+template <bool PM>
+void launch_rk45_flat(int32_t n_arms, bool perrow, dim3 grid, hipStream_t hs, const Rk45Args& ra, const LibDesc& lib) {
+  if (n_arms == 1) {
+    if (perrow) rollout_rk45_flat_kernel<1, true, PM><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else rollout_rk45_flat_kernel<1, false, PM><<<grid, kBlock, 0, hs>>>(ra, lib);
+  } else {
+    if (perrow) rollout_rk45_flat_kernel<2, true, PM><<<grid, kBlock, 0, hs>>>(ra, lib);
+    else rollout_rk45_flat_kernel<2, false, PM><<<grid, kBlock, 0, hs>>>(ra, lib);
+  }
+}
+}  // namespace
+}  // extern "C++"
+
 int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_t* arm_bits, int64_t ld_arm,
                                 const double* t_obs, int64_t ld_t, const int32_t* n_obs, const double* coef,
                                 int64_t coef_row_stride, const int8_t* exps, int32_t n_terms, int64_t n_rows,
                                 int32_t T_max, int32_t n_statics, int32_t n_arms, double rtol, double atol,
-                                double drop_below, double* y_out, int64_t ld_y, int32_t* steps_out, void* stream) {
+                                double drop_below, double* y_out, int64_t ld_y, int32_t* steps_out,
+                                const int32_t* row_order, int32_t layout, void* stream) {
+  const bool pm = layout == INSITE_LAYOUT_PATIENT_MAJOR_BITS;
+  if (!pm && layout != INSITE_LAYOUT_TIME_MAJOR_BITS) return INSITE_E_INVALID_ARG;
+  const int64_t words = pm ? ((int64_t)T_max - 1 + 31) / 32 : (n_rows + 31) / 32;
   if (n_rows < 0 || T_max < 1 || n_arms < 1 || n_arms > 2 || !(rtol > 0.0) || !(atol > 0.0) ||
-      ld_t < n_rows || ld_y < n_rows || ld_arm < (n_rows + 31) / 32 || coef_row_stride < 0)
+      ld_t < (pm ? T_max : n_rows) || ld_y < (pm ? T_max : n_rows) || ld_arm < (words > 0 ? words : 1) ||
+      coef_row_stride < 0)
     return INSITE_E_INVALID_ARG;
   if (n_rows == 0) return INSITE_OK;
   if (!y0 || !arm_bits || !t_obs || !n_obs || !coef || !y_out || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
@@ -3278,13 +3436,14 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
   int32_t st = build_lib(exps, n_terms, n_statics, &lib);
   if (st != INSITE_OK) return st;
   if (coef_row_stride != 0 && coef_row_stride < (int64_t)n_arms * n_terms) return INSITE_E_INVALID_ARG;
-  Rk45Args ra{y0, n_statics > 0 ? u : y0, arm_bits, t_obs, n_obs, coef, y_out, steps_out, ld_arm, ld_t, ld_y,
+  Rk45Args ra{y0, n_statics > 0 ? u : y0, arm_bits, t_obs, n_obs, coef, y_out, steps_out, row_order, ld_arm, ld_t, ld_y,
               coef_row_stride, n_rows, T_max, n_arms, rtol, atol, drop_below};
   const int64_t waves = (n_rows + kWave - 1) / kWave;
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   const bool perrow = coef_row_stride != 0;
-#ifdef INSITE_RK45_PER_INTERVAL  // the per-interval form (A/B builds, tools/build_ablation.sh)
+#ifdef INSITE_RK45_PER_INTERVAL  // the per-interval form (A/B builds, tools/build_ablation.sh): time-major only
+  if (pm) return INSITE_E_UNSUPPORTED;
   if (n_arms == 1) {
     if (perrow) rollout_rk45_kernel<1, true><<<grid, kBlock, 0, hs>>>(ra, lib);
     else rollout_rk45_kernel<1, false><<<grid, kBlock, 0, hs>>>(ra, lib);
@@ -3293,14 +3452,30 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
     else rollout_rk45_kernel<2, false><<<grid, kBlock, 0, hs>>>(ra, lib);
   }
 #else
-  if (n_arms == 1) {
-    if (perrow) rollout_rk45_flat_kernel<1, true><<<grid, kBlock, 0, hs>>>(ra, lib);
-    else rollout_rk45_flat_kernel<1, false><<<grid, kBlock, 0, hs>>>(ra, lib);
-  } else {
-    if (perrow) rollout_rk45_flat_kernel<2, true><<<grid, kBlock, 0, hs>>>(ra, lib);
-    else rollout_rk45_flat_kernel<2, false><<<grid, kBlock, 0, hs>>>(ra, lib);
-  }
+  if (pm) launch_rk45_flat<true>(n_arms, perrow, grid, hs, ra, lib);
+  else launch_rk45_flat<false>(n_arms, perrow, grid, hs, ra, lib);
 #endif
+  return launch_status();
+}
+
+size_t insite_rk45_order_workspace_bytes(int32_t T_max) {
+  const int nb = (T_max < kRkBinMax - 1 ? (T_max < 1 ? 1 : T_max) : kRkBinMax - 1) + 1;
+  return (size_t)2 * nb * sizeof(unsigned);
+}
+
+int32_t insite_rk45_order_i32(const int32_t* n_obs, int64_t n_rows, int32_t T_max, int32_t* order_out, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  if (n_rows < 0 || n_rows > INT32_MAX || T_max < 1) return INSITE_E_INVALID_ARG;
+  if (n_rows == 0) return INSITE_OK;
+  if (!n_obs || !order_out || !workspace) return INSITE_E_INVALID_ARG;
+  if (workspace_bytes < insite_rk45_order_workspace_bytes(T_max)) return INSITE_E_WORKSPACE;
+  const int nb = (T_max < kRkBinMax - 1 ? T_max : kRkBinMax - 1) + 1;
+  unsigned* hist = static_cast<unsigned*>(workspace);
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(hist, 0, (size_t)2 * nb * sizeof(unsigned), hs) != hipSuccess) return INSITE_E_HIP;
+  const dim3 grid((unsigned)((n_rows + kRkBinChunk - 1) / kRkBinChunk));
+  rk45_bin_count_kernel<<<grid, kBlock, 0, hs>>>(n_obs, n_rows, nb, hist);
+  rk45_bin_scatter_kernel<<<grid, kBlock, 0, hs>>>(n_obs, n_rows, nb, hist, hist + nb, order_out);
   return launch_status();
 }
 

@@ -20,13 +20,13 @@ LIB_PATH = os.path.join(LIB_DIR, "libinsite_hip.so")
 if os.environ.get("INSITE_LIB_OVERRIDE"):
     LIB_PATH = os.environ["INSITE_LIB_OVERRIDE"]
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # status codes / enums (insite_hip.h)
 INSITE_OK = 0
 FD_SMOOTHED4, FD_ORDER4, FD_ORDER1, FD_SMOOTHED1 = 0, 1, 2, 3
 METHOD_EULER, METHOD_RK4 = 0, 1
-LAYOUT_PATIENT_MAJOR, LAYOUT_TIME_MAJOR, LAYOUT_TIME_MAJOR_BITS = 0, 1, 2
+LAYOUT_PATIENT_MAJOR, LAYOUT_TIME_MAJOR, LAYOUT_TIME_MAJOR_BITS, LAYOUT_PATIENT_MAJOR_BITS = 0, 1, 2, 3
 MAX_TERMS, MAX_STATICS, MAX_ARMS, MAX_STATE_DEGREE = 9, 3, 4, 1
 GEN_MAX_TERMS, GEN_MAX_STATE_DEGREE, GEN_MAX_INPUTS = 64, 4, 2   # insite_gen.hip
 
@@ -45,6 +45,8 @@ EXPORTS = (
     "insite_stlsq_f64",
     "insite_rollout_f64",
     "insite_rollout_rk45_f64",
+    "insite_rk45_order_workspace_bytes",
+    "insite_rk45_order_i32",
     "insite_refine_f64",
     "insite_refine_arms_f64",
     "insite_masked_sse_workspace_bytes",
@@ -101,7 +103,10 @@ _SIGNATURES = {
     "insite_rollout_f64": (_c_i32, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _vp, _c_i32, _c_i64, _c_i32, _c_i32,
                                     _c_i32, _c_f64, _c_i32, _c_i32, _c_f64, _vp, _c_i64, _c_i32, _vp]),
     "insite_rollout_rk45_f64": (_c_i32, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _c_i64, _vp, _c_i32, _c_i64,
-                                         _c_i32, _c_i32, _c_i32, _c_f64, _c_f64, _c_f64, _vp, _c_i64, _vp, _vp]),
+                                         _c_i32, _c_i32, _c_i32, _c_f64, _c_f64, _c_f64, _vp, _c_i64, _vp, _vp,
+                                         _c_i32, _vp]),
+    "insite_rk45_order_workspace_bytes": (_c_size, [_c_i32]),
+    "insite_rk45_order_i32": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _vp, _c_size, _vp]),
     "insite_refine_f64": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _c_i64, _vp, _vp, _c_i64, _c_i32, _vp, _c_i32, _vp,
                                    _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _c_i32, _vp, _c_i64, _vp, _vp, _vp, _vp]),
     "insite_refine_arms_f64": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _c_i64, _vp, _vp, _c_i64, _c_i32, _vp, _c_i32,

@@ -511,21 +511,47 @@ def plan_rollout(y0, u, arm, coef, lib, dt, method="euler5", substeps=None, drop
     return Plan(name, args, dev, out, keep)
 
 
+def rk45_order(n_obs: torch.Tensor, T_max: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Lane order for ``rollout_rk45``: rows sorted by n_obs, descending (insite_rk45_order_i32, a
+    counting sort on the device).  Scheduling only: the rollout's outputs do not depend on it."""
+    _dev("n_obs", n_obs, torch.int32, 1)
+    N = n_obs.numel()
+    if out is None:
+        out = torch.empty((N,), dtype=torch.int32, device=n_obs.device)
+    nb = _lib.load().insite_rk45_order_workspace_bytes(int(T_max))
+    ws = _default_ws(n_obs.device).get(nb, n_obs.device)
+    args = (_p(n_obs), N, int(T_max), _p(out), _p(ws), ws.numel())
+    return _run(("insite_rk45_order_i32", args, n_obs.device, out))
+
+
 def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_obs: torch.Tensor,
                  n_obs: torch.Tensor, coef: torch.Tensor, lib: PolyLibrary, rtol: float = 1.4e-8, atol: float = 1.4e-8,
-                 drop_below: float = 1e-3, out: torch.Tensor | None = None, steps: torch.Tensor | None = None):
+                 drop_below: float = 1e-3, out: torch.Tensor | None = None, steps: torch.Tensor | None = None,
+                 order: torch.Tensor | bool | None = True, layout: str = "time"):
     """Adaptive RK45 rollout on per-patient irregular observation grids (insite_rollout_rk45_f64;
-    configuration C5).  y0 [N] f64, u [N,U] f64, arm_bits [T_max, >=ceil(N/32)] int32 (arm of each
-    interval, pack_arm_bits), t_obs [T_max, >=N] f64 time-major, n_obs [N] int32, coef [A,F] or
-    [N,A,F].  Returns (y [T_max, N] — row k = state at t_obs[k + 1] —, step attempts [N] int32)."""
+    configuration C5).  y0 [N] f64, u [N,U] f64, n_obs [N] int32, coef [A,F] or [N,A,F].
+    layout "time":    t_obs [T_max, >=N] f64, arm_bits [T_max, >=ceil(N/32)] int32 (pack_arm_bits of the
+                      time-major arms), y [T_max, N] (row k = state at t_obs[k + 1]);
+    layout "patient": t_obs [N, >=T_max] f64, arm_bits [N, >=ceil((T_max-1)/32)] int32 (pack_arm_bits of
+                      the patient-major arms [N, T]), y [N, T_max] -- the fast layout.
+    ``order``: True bins the rows by n_obs on the device first (``rk45_order``, part of the call), a [N]
+    int32 permutation is used as given, None/False runs lane r on row r.  Outputs do not depend on it.
+    Returns (y, step attempts [N] int32); y elements past a patient's grid are left as they were (NaN
+    when ``out`` is None)."""
+    if layout not in ("time", "patient"):
+        raise ValueError("layout must be 'time' or 'patient'")
+    pm = layout == "patient"
     _dev("y0", y0, torch.float64, 1)
     N = y0.numel()
     _dev("t_obs", t_obs, torch.float64, 2)
-    Tm = t_obs.size(0)
-    if t_obs.size(1) < N:
-        raise ValueError("t_obs must be [T_max, >=N]")
+    Tm = t_obs.size(1) if pm else t_obs.size(0)
+    if (t_obs.size(0) if pm else t_obs.size(1)) < N or (pm and t_obs.size(0) != N):
+        raise ValueError("t_obs must be [N, T_max]" if pm else "t_obs must be [T_max, >=N]")
     _dev("arm_bits", arm_bits, torch.int32, 2)
-    if arm_bits.size(0) < Tm or arm_bits.size(1) < (N + 31) // 32:
+    if pm:
+        if arm_bits.size(0) != N or arm_bits.size(1) < max(1, (Tm - 1 + 31) // 32):
+            raise ValueError("arm_bits must be [N, >=ceil((T_max-1)/32)] int32")
+    elif arm_bits.size(0) < Tm or arm_bits.size(1) < (N + 31) // 32:
         raise ValueError("arm_bits must be [>=T_max, >=ceil(N/32)] int32")
     _dev("n_obs", n_obs, torch.int32, 1)
     if n_obs.numel() != N:
@@ -544,18 +570,28 @@ def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_ob
         raise ValueError("coef must be [A,F] or [N,A,F]")
     if coef.size(-1) != F or not coef.is_contiguous():
         raise ValueError("coef must be contiguous with the library's F columns")
+    shape = (N, Tm) if pm else (Tm, N)
     if out is None:
-        out = torch.full((Tm, N), float("nan"), dtype=torch.float64, device=y0.device)
+        out = torch.full(shape, float("nan"), dtype=torch.float64, device=y0.device)
     else:
         _dev("out", out, torch.float64, 2)
-        if out.size(0) < Tm or out.size(1) < N:
-            raise ValueError("out must be [T_max, >=N]")
+        if out.size(0) < shape[0] or out.size(1) < shape[1] or (pm and out.size(0) != N):
+            raise ValueError(f"out must be {'[N, >=T_max]' if pm else '[T_max, >=N]'}")
     if steps is None:
         steps = torch.empty((N,), dtype=torch.int32, device=y0.device)
+    if order is True:
+        order = rk45_order(n_obs, Tm)
+    elif order is False:
+        order = None
+    elif order is not None:
+        _dev("order", order, torch.int32, 1)
+        if order.numel() != N:
+            raise ValueError("order must be a [N] int32 permutation")
     tab = lib.ctypes_table()
     args = (_p(y0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm_bits), arm_bits.stride(0), _p(t_obs),
             t_obs.stride(0), _p(n_obs), _p(coef), stride, tab.ctypes.data_as(ctypes.c_void_p), F, N, Tm,
-            lib.n_statics, A, float(rtol), float(atol), float(drop_below), _p(out), out.stride(0), _p(steps))
+            lib.n_statics, A, float(rtol), float(atol), float(drop_below), _p(out), out.stride(0), _p(steps),
+            _p(order), _lib.LAYOUT_PATIENT_MAJOR_BITS if pm else _lib.LAYOUT_TIME_MAJOR_BITS)
     return _run(("insite_rollout_rk45_f64", args, y0.device, (out, steps)))
 
 

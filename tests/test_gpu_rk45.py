@@ -29,24 +29,33 @@ def _setup(N, seed, per_patient=False):
     return ex, t, n, u, arm, y0, coef
 
 
-def _run(dev, ex, t, n, u, arm, y0, coef):
+def _run(dev, ex, t, n, u, arm, y0, coef, order=True, layout="time"):
+    """Both layouts: time-major t/y/arm bits [T, N] or patient-major [N, T] (arm bits [N, words])."""
     from insite_amd import ops
     from insite_amd.library import polynomial_library
     lib = polynomial_library(2, 2, True)
     assert np.array_equal(lib.exps.astype(np.int64), ex)
-    N = y0.size
-    tt = torch.tensor(np.ascontiguousarray(np.nan_to_num(t, nan=0.0).T), device=dev)
-    bits = ops.pack_arm_bits(torch.tensor(np.ascontiguousarray(arm.T), device=dev), N)
+    N, Tm = t.shape
+    tn = np.nan_to_num(t, nan=0.0)
+    if layout == "patient":
+        tt = torch.tensor(np.ascontiguousarray(tn), device=dev)
+        bits = ops.pack_arm_bits(torch.tensor(np.ascontiguousarray(arm[:, :Tm]), device=dev), Tm)
+    else:
+        tt = torch.tensor(np.ascontiguousarray(tn.T), device=dev)
+        bits = ops.pack_arm_bits(torch.tensor(np.ascontiguousarray(arm[:, :Tm].T), device=dev), N)
     y, steps = ops.rollout_rk45(torch.tensor(y0, device=dev), torch.tensor(u, device=dev), bits, tt,
-                                torch.tensor(n, device=dev), torch.tensor(np.ascontiguousarray(coef), device=dev), lib)
+                                torch.tensor(n, device=dev), torch.tensor(np.ascontiguousarray(coef), device=dev), lib,
+                                order=order, layout=layout)
     torch.cuda.synchronize()
-    return y.cpu().numpy().T, steps.cpu().numpy()
+    y = y.cpu().numpy()
+    return (y if layout == "patient" else y.T), steps.cpu().numpy()
 
 
+@pytest.mark.parametrize("layout", ["time", "patient"])
 @pytest.mark.parametrize("N,seed", [(1, 0), (63, 1), (200, 2), (257, 3)])
-def test_rk45_rollout_matches_oracle(dev, N, seed):
+def test_rk45_rollout_matches_oracle(dev, N, seed, layout):
     ex, t, n, u, arm, y0, coef = _setup(N, seed)
-    y, steps = _run(dev, ex, t, n, u, arm, y0, coef)
+    y, steps = _run(dev, ex, t, n, u, arm, y0, coef, layout=layout)
     ref, ref_steps = K.rollout_rk45(y0, u, arm, t, n, coef, ex)
     valid = ~np.isnan(ref)
     assert np.array_equal(np.isnan(y), ~valid)            # rows past each grid untouched (NaN)
@@ -58,7 +67,7 @@ def test_rk45_rollout_matches_oracle(dev, N, seed):
 
 def test_rk45_rollout_per_patient_coefficients(dev):
     ex, t, n, u, arm, y0, coef = _setup(150, 9, per_patient=True)
-    y, _ = _run(dev, ex, t, n, u, arm, y0, coef)
+    y, _ = _run(dev, ex, t, n, u, arm, y0, coef, layout="patient")
     ref, _ = K.rollout_rk45(y0, u, arm, t, n, coef[0], ex) if False else (None, None)
     # per-patient oracle: each patient with its own [A, F] rows
     for p in range(0, 150, 7):
@@ -92,3 +101,71 @@ def test_device_irregular_grid(dev):
         g = tc[: nc[p], p]
         assert g[0] == 0.0 and np.all(np.diff(g) >= 0) and g[-1] <= 10.0
         assert np.isnan(tc[nc[p]:, p]).all()
+
+
+def test_rk45_order_is_a_binned_permutation(dev):
+    from insite_amd import ops
+    rng = np.random.default_rng(11)
+    for N, Tm in [(1, 60), (5000, 60), (70_001, 60), (3000, 2000)]:
+        n = rng.integers(-2, Tm + 5, N).astype(np.int32)
+        o = ops.rk45_order(torch.tensor(n, device=dev), Tm).cpu().numpy()
+        assert np.array_equal(np.sort(o), np.arange(N))
+        key = np.clip(n, 0, min(Tm, 1023))[o]
+        assert np.all(np.diff(key) <= 0)                    # descending n_obs (longest rows first)
+
+
+def test_rk45_row_order_and_layout_do_not_change_outputs(dev):
+    """Lane placement and memory layout are scheduling only: binned, random and identity orders in both
+    layouts give bit-identical results."""
+    ex, t, n, u, arm, y0, coef = _setup(3000, 21)
+    y_id, s_id = _run(dev, ex, t, n, u, arm, y0, coef, order=None)
+    perm = torch.tensor(np.random.default_rng(3).permutation(3000).astype(np.int32), device=dev)
+    runs = [_run(dev, ex, t, n, u, arm, y0, coef, order=o, layout=lay)
+            for lay in ("time", "patient") for o in (True, perm, None)]
+    for y, s in runs:
+        assert np.array_equal(np.isnan(y), np.isnan(y_id))
+        assert np.array_equal(y[~np.isnan(y)], y_id[~np.isnan(y_id)]) and np.array_equal(s, s_id)
+
+
+@pytest.mark.parametrize("layout", ["time", "patient"])
+def test_rk45_zero_length_intervals_and_short_grids(dev, layout):
+    """Repeated and reversed observation times (y carried over, no attempt), grids of 0/1 observations
+    (nothing written), and T_max > 64 (arms read per interval instead of the 64-bit lane mask)."""
+    rng = np.random.default_rng(5)
+    N, Tm = 300, 90
+    ex = R.poly_library(3, 2, True)
+    n = rng.integers(0, Tm + 1, N).astype(np.int32)
+    n[:3] = [0, 1, 2]
+    t = np.full((N, Tm), np.nan)
+    for p in range(N):
+        g = np.sort(rng.uniform(0.0, 10.0, Tm))
+        g[0] = 0.0
+        dup = rng.random(Tm) < 0.15
+        for k in range(1, Tm):
+            if dup[k]:
+                g[k] = g[k - 1]                              # zero-length interval
+        if p % 7 == 0 and n[p] > 4:
+            g[3] = g[2] - 0.5                                # one reversed interval
+        t[p, :n[p]] = g[:n[p]]
+    u = rng.normal(0.5, 0.05, (N, 2))
+    arm = (rng.random((N, Tm)) < 0.5).astype(np.int8)
+    y0 = rng.uniform(1, 50, N)
+    coef = np.zeros((2, 7))
+    coef[0, 4], coef[1, 1], coef[1, 5] = -1.11, -0.146, -1.02
+    y, steps = _run(dev, ex, t, n, u, arm, y0, coef, layout=layout)
+    ref = np.full((N, Tm), np.nan)
+    ref_steps = np.zeros(N, dtype=np.int64)
+    for p in range(N):
+        al, be = K.patient_rates(u[p], coef, ex)
+        v = float(y0[p])
+        for k in range(int(n[p]) - 1):
+            a = int(arm[p, k])
+            if t[p, k + 1] > t[p, k]:
+                v, c = K.rk45_interval(lambda w, a=a: al[a] + be[a] * w, v, t[p, k], t[p, k + 1])
+                ref_steps[p] += c
+            ref[p, k] = v
+    valid = ~np.isnan(ref)
+    assert np.array_equal(np.isnan(y), ~valid)
+    rel = np.abs(y[valid] - ref[valid]) / np.abs(ref[valid])
+    assert rel.max() < 1e-9, rel.max()
+    assert np.mean(steps == ref_steps) >= 0.99

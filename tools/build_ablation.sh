@@ -9,6 +9,10 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
   case $v in
     NOSTORE) NAME=$v build -DINSITE_ABLATE_NOSTORE ;;
     RK45PI) NAME=$v build -DINSITE_RK45_PER_INTERVAL ;;
+    RKW8W6) NAME=$v build -DINSITE_RK45_WIN=8 -DINSITE_RK45_WPE=6 ;;
+    RKPMNT) NAME=$v build -DINSITE_RK45_PM_NT=1 ;;
+    RKW8W8) NAME=$v build -DINSITE_RK45_WIN=8 -DINSITE_RK45_WPE=8 ;;
+    RKW16W5) NAME=$v build -DINSITE_RK45_WIN=16 -DINSITE_RK45_WPE=5 ;;
     SEGKC8) NAME=$v build -DINSITE_SEG_KC=8 -DINSITE_SEG_WPE=3 ;;
     SEGKC4) NAME=$v build -DINSITE_SEG_KC=4 -DINSITE_SEG_WPE=4 ;;
     SEGKC16) NAME=$v build -DINSITE_SEG_KC=16 -DINSITE_SEG_WPE=2 ;;
