@@ -49,7 +49,7 @@ def parse():
                     help="per-step arms of the time-major rollout: 1-bit mask (A <= 2) or int8")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="pipeline", choices=["graph", "seq", "pipeline"],
-                    help="pipeline: gram | [all-reduce +] STLSQ | rollout on three streams, consecutive steps "
+                    help="pipeline: discovery (gram + in-launch reduction [+ all-reduce] + STLSQ) | rollout on two streams, consecutive steps "
                          "overlapped (default); seq: eager launches on one stream; graph: the seq step in a HIP graph")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
@@ -79,7 +79,11 @@ class HipEvents:
 
     def create(self, timing=False):
         e = self._c.c_void_p()
-        flags = 0x0 if timing else 0x2                                      # hipEventDisableTiming
+        # ordering events: hipEventDisableTiming | hipEventReleaseToDevice -- the consumers are queues of
+        # this device, so a device-scope release suffices; the default system-scope release writes back
+        # and invalidates the caches at every record (~20 us of dead queue time per step on ROCm 7.2:
+        # profiles/r02_c2_pipeline_trace.txt)
+        flags = 0x0 if timing else (0x2 | 0x40000000)
         if self._hip.hipEventCreateWithFlags(self._c.byref(e), flags) != 0:
             raise RuntimeError("hipEventCreateWithFlags failed")
         self._events.append(e)
@@ -821,52 +825,63 @@ def main():
     lib = coh.lib
     F = lib.n_terms
     y0 = coh.y0
-    # double-buffered per-step state: discovery of step i+1 may run while step i's STLSQ / rollout read
-    bufs = [idist.MomentBuffer(2, F, dev) for _ in range(2)]      # G|b in one buffer: one all-reduce
-    coefs = [torch.empty((2, F), dtype=torch.float64, device=dev) for _ in range(2)]
-    masks = [torch.empty((2, F), dtype=torch.int8, device=dev) for _ in range(2)]
-    iters = [torch.empty((2,), dtype=torch.int32, device=dev) for _ in range(2)]
+    # per-step state in NB buffers: the discovery of step i writes coefs[i % NB] while older rollouts may
+    # still read theirs (G|b and the gram workspace are only touched by the discovery stream, in order,
+    # but are buffered alike to keep the plans independent); rollouts alternate between RS streams (and
+    # y buffers), so one rollout stream's wait for its discovery overlaps the other's rollout
+    NB, RS, WAR_EVERY = 16, 2, 8
+    bufs = [idist.MomentBuffer(2, F, dev) for _ in range(NB)]     # G|b in one buffer: one all-reduce
+    coefs = [torch.empty((2, F), dtype=torch.float64, device=dev) for _ in range(NB)]
+    masks = [torch.empty((2, F), dtype=torch.int8, device=dev) for _ in range(NB)]
+    iters = [torch.empty((2,), dtype=torch.int32, device=dev) for _ in range(NB)]
     mask = masks[0]
-    y = torch.empty((T, N) if args.layout == "time" else (N, T), dtype=torch.float64, device=dev)
-    wss = [ops.Workspace(), ops.Workspace()]
+    wss = [ops.Workspace() for _ in range(NB)]
     mode = args.mode if (world == 1 or args.mode != "graph") else "seq"   # RCCL stays outside graphs
+    if mode != "pipeline":
+        RS = 1
+    ys = [torch.empty((T, N) if args.layout == "time" else (N, T), dtype=torch.float64, device=dev)
+          for _ in range(RS)]
+    y = ys[0]
     s_g = torch.cuda.current_stream(dev)
-    s_c = torch.cuda.Stream(dev) if mode == "pipeline" else s_g
-    s_r = torch.cuda.Stream(dev) if mode == "pipeline" else s_g
+    s_rs = [torch.cuda.Stream(dev) if mode == "pipeline" else s_g for _ in range(RS)]
 
     # one step = discovery (Gram -> [RCCL all-reduce when N > 1] -> STLSQ) then the rollout with that
     # step's coefficients.  Launches go through prepared plans (arguments validated and packed once).
-    #   pipeline : three streams — gram + partial reduction | [all-reduce +] STLSQ | rollout — with
-    #              double-buffered G|b, workspaces and coefficients, ordered by events: the gram of
-    #              step i+1 streams while step i's STLSQ tail, all-reduce and rollout run, so the
-    #              small-grid tail kernels and the collective's latency leave the critical path
-    #   seq      : gram + fused reduction/STLSQ (N = 1) then the rollout, eagerly on one stream
+    #   pipeline : discovery stream (gram with its in-launch reduction to G|b, [all-reduce,] STLSQ: no
+    #              cross-stream hop inside it) | RS rollout streams taking alternate steps — NB-buffered
+    #              coefficients; each rollout waits for its step's discovery event, and the discovery
+    #              stream waits, every WAR_EVERY steps, for the rollout WAR_EVERY steps back (so a buffer
+    #              is rewritten only after the rollout NB steps back has read it).  A cross-stream wait
+    #              costs ~20 us of dead queue time on ROCm 7 (profiles/), so the waits are spread over
+    #              streams that have other work and thinned to what the buffer reuse needs
+    #   seq      : gram + in-launch reduction + STLSQ (N = 1) then the rollout, eagerly on one stream
     #   graph    : the seq step captured once in a HIP graph and replayed (N = 1)
     # The timed region holds no timing events: per-kernel durations come from the separate
     # roofline pass below (isolated launches) and rocprofv3.
     with torch.cuda.stream(s_g):
         fused = [ops.plan_sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, 100, True, 2,
                                     "smoothed4", wss[j], out=(coefs[j], masks[j], iters[j], bufs[j].G, bufs[j].b),
-                                    layout=args.layout) for j in range(2)]
+                                    layout=args.layout) for j in range(NB)]
         gram_plans = [ops.plan_gram(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 2, "smoothed4", wss[j],
-                                    out=(bufs[j].G, bufs[j].b), layout=args.layout) for j in range(2)]
+                                    out=(bufs[j].G, bufs[j].b), layout=args.layout) for j in range(NB)]
         stlsq_plans = [ops.plan_stlsq(bufs[j].G, bufs[j].b, 0.1, 0.5, 100, True, out=(coefs[j], masks[j], iters[j]))
-                       for j in range(2)]
-    roll_plans = [ops.plan_rollout(y0, coh.u, arm_cf, coefs[j], lib, coh.dt, method=args.method, T=T, out=y,
-                                   layout=roll_layout) for j in range(2)]
+                       for j in range(NB)]
+    roll_plans = [ops.plan_rollout(y0, coh.u, arm_cf, coefs[j], lib, coh.dt, method=args.method, T=T,
+                                   out=ys[j % RS], layout=roll_layout) for j in range(NB)]
     # cross-stream ordering through the HIP runtime directly (torch's Event wrappers cost ~3-5 us of host
     # time each; at N > 1 the host also issues the all-reduce, and must stay ahead of a ~70 us step)
     hip = HipEvents()
-    ev = {k: hip.create() for k in [(n, j) for n in "gcr" for j in range(2)]}
-    hs = {"g": s_g.cuda_stream, "c": s_c.cuda_stream, "r": s_r.cuda_stream}
-    last_c, last_r = [None, None], [None, None]
+    ev = {k: hip.create() for k in [(n, j) for n in "gr" for j in range(NB)]}
+    hs_g = s_g.cuda_stream
+    last_r = [None] * NB
+    f_fast = [p.bind(s_g) for p in fused]
     g_fast = [p.bind(s_g) for p in gram_plans]
-    c_fast = [p.bind(s_c) for p in stlsq_plans]
-    r_fast = [p.bind(s_r) for p in roll_plans]
+    c_fast = [p.bind(s_g) for p in stlsq_plans]
+    r_fast = [p.bind(s_rs[j % RS]) for j, p in enumerate(roll_plans)]
 
     def discover(i, st):
         """Discovery of step i on stream st (used by seq / graph and the roofline pass)."""
-        j = i % 2
+        j = i % NB
         if world == 1:
             fused[j](st)
         else:
@@ -878,7 +893,7 @@ def main():
     def step(i, tev=None):
         """One step; ``tev`` = (gram start, gram end, rollout start, rollout end) timing events recorded
         on the streams those kernels run on (the instrumented pass)."""
-        j = i % 2
+        j = i % NB
         if mode != "pipeline":                      # current stream: the capture stream under graph capture
             st = torch.cuda.current_stream(dev)
             if tev:
@@ -891,30 +906,34 @@ def main():
             if tev:
                 hip.record(tev[3], st.cuda_stream)
             return
-        if last_c[j] is not None:
-            hip.wait(hs["g"], last_c[j])            # step i-2's STLSQ has read G|b[j]
+        if i % WAR_EVERY == 0:
+            # steps i .. i+WAR_EVERY-1 reuse the buffers of steps i-NB .. i-NB+WAR_EVERY-1: wait, on each
+            # rollout stream, for its newest rollout at or below that bound (a stream runs in order)
+            bound = i - NB + WAR_EVERY - 1
+            for r in range(RS):
+                k = bound - ((bound - r) % RS)
+                if k >= 0 and last_r[k % NB] is not None:
+                    hip.wait(hs_g, last_r[k % NB])
+        hs_r = s_rs[i % RS].cuda_stream
         if tev:
-            hip.record(tev[0], hs["g"])
-        g_fast[j]()
-        if tev:
-            hip.record(tev[1], hs["g"])
-        hip.record(ev["g", j], hs["g"])
-        hip.wait(hs["c"], ev["g", j])
-        if world > 1:
-            with torch.cuda.stream(s_c):
+            hip.record(tev[0], hs_g)
+        if world == 1:
+            f_fast[j]()                             # gram + in-launch reduction, STLSQ
+        else:
+            g_fast[j]()
+            with torch.cuda.stream(s_g):
                 idist.reduce_moments(bufs[j])       # the only collective
-        if last_r[j] is not None:
-            hip.wait(hs["c"], last_r[j])            # step i-2's rollout has read coefs[j]
-        c_fast[j]()
-        hip.record(ev["c", j], hs["c"])
-        last_c[j] = ev["c", j]
-        hip.wait(hs["r"], ev["c", j])
+            c_fast[j]()
         if tev:
-            hip.record(tev[2], hs["r"])
+            hip.record(tev[1], hs_g)
+        hip.record(ev["g", j], hs_g)
+        hip.wait(hs_r, ev["g", j])
+        if tev:
+            hip.record(tev[2], hs_r)
         r_fast[j]()
         if tev:
-            hip.record(tev[3], hs["r"])
-        hip.record(ev["r", j], hs["r"])
+            hip.record(tev[3], hs_r)
+        hip.record(ev["r", j], hs_r)
         last_r[j] = ev["r", j]
 
     graph = None
@@ -943,8 +962,8 @@ def main():
         dist.barrier()
     el = idist.max_over_ranks(time.perf_counter() - t0, dev)
     ms_step = el / args.steps * 1e3
-    coef = coefs[0] if mode == "graph" else coefs[(args.steps - 1) % 2]
-    mask = masks[0] if mode == "graph" else masks[(args.steps - 1) % 2]
+    coef = coefs[0] if mode == "graph" else coefs[(args.steps - 1) % NB]
+    mask = masks[0] if mode == "graph" else masks[(args.steps - 1) % NB]
 
     # instrumented pass (after the timed region): the same schedule again — same streams, same overlap —
     # with HIP timing events around the gram and rollout launches on the streams they run on.  Per-launch
@@ -1038,15 +1057,16 @@ def main():
                            "patient": "patient-major x[N,T], int8 arm[N,T], y[N,T]"}[roll_layout],
             },
             "discovery": {
-                "kernels": "gram_kernel + discovery_finalize (fused STLSQ)" if world == 1
-                           else "gram_kernel + RCCL all_reduce + stlsq_kernel",
-                "timed_region": {"graph": "one step (gram, finalize+STLSQ, rollout) captured in a HIP graph, replayed",
+                "kernels": "gram_kernel (in-launch reduction to G|b) + stlsq_kernel" if world == 1
+                           else "gram_kernel (in-launch reduction) + RCCL all_reduce + stlsq_kernel",
+                "timed_region": {"graph": "one step (gram+reduction, STLSQ, rollout) captured in a HIP graph, replayed",
                                  "seq": "eager launches, one stream, strictly sequential",
-                                 "pipeline": "gram+reduce | [all-reduce+] STLSQ | rollout on three streams, "
-                                             "double-buffered, consecutive steps overlapped"}[mode],
-                "avg_ms_source": "instrumented pass: HIP timing events around each gram launch on its stream "
-                                 "(gram + block partials; the finalize/STLSQ launch runs on the next stream)"
-                                 if mode == "pipeline" else "instrumented pass: HIP timing events around discovery",
+                                 "pipeline": "discovery (gram+reduction [+all-reduce] +STLSQ) | rollout on two "
+                                             "streams, triple-buffered coefficients, consecutive steps overlapped"}[mode],
+                "avg_ms_source": "instrumented pass: HIP timing events around each step's whole discovery (memset "
+                                 "node, gram with its in-launch reduction, STLSQ) on its stream, concurrent with the "
+                                 "previous step's rollout" if mode == "pipeline"
+                                 else "instrumented pass: HIP timing events around discovery",
                 "avg_ms": disc_ms,
                 "algorithmic_bytes": gram_bytes(N, T),
                 "achieved_GBps": gram_bytes(N, T) / (disc_ms * 1e-3) / 1e9,

@@ -112,7 +112,10 @@ int32_t insite_poly_library(int32_t n_statics, int32_t degree, int32_t interacti
  *   u     [n_patients, n_statics] f64
  *   arm   [n_patients] int8 in [0, n_arms)
  *   rows  [n_patients] int32
- *   G_out [n_arms, F, F] f64 (overwritten), b_out [n_arms, F] f64 (overwritten)       */
+ *   G_out [n_arms, F, F] f64 (overwritten), b_out [n_arms, F] f64 (overwritten)
+ * Workspace: insite_gram_workspace_bytes; its first 512 bytes (the in-launch reduction's arrival
+ * counters) must be zero before the workspace's first use -- every call leaves them zero (ABI 3).
+ * The same holds for the workspaces of insite_sindy_fit_f64 and the *_segments_* calls.          */
 size_t insite_gram_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms);
 int32_t insite_gram_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,
                         const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics,

@@ -162,6 +162,89 @@ __device__ __forceinline__ void tele_lo(const GramW& w, double vm2, double vm1, 
   sdx = w.fd1 * (vm1 * v0) + w.fd2 * (vm2 * v0 + vm1 * v1);
 }
 
+// In-launch fixed-order reduction of the gram partials (the split-K hand-off of the MI355X HIP guide,
+// §6 Guideline 16, write-through form): every block stores its compact partial (the n_arms * nE Gram
+// entries, a * nE + e) write-through (sc1, agent-scope atomic stores), drains, and takes a ticket; the
+// last of each group of kTailGroup blocks (block-index order) sums the group's partials into a group
+// partial, published the same way; the last group reducer (agent-scope acquire, then plain loads) sums
+// the group partials in group order and writes G (both triangles) and b.  The summation order is fixed
+// by block and group index, never by arrival, so results are deterministic.  The group reductions of
+// all but the last group overlap the other blocks' streaming; after the last block only one group
+// (<= kTailGroup partials of <= kTailMaxEnt doubles) and <= 64 group partials remain, where a separate
+// finalize launch read every block's full tile.  Counters cnt[0] (groups), cnt[1 + g]: the last arriver
+// of each counter resets it (all its arrivals are in), so a call leaves them zero; the workspace header
+// must be zero before its first use (insite_gram_workspace_bytes).  The launcher's alternative, a memset
+// node per call (-DINSITE_GRAM_MEMSET), puts a ~20 us gap in the stream on ROCm 7.2 (profiles/).
+constexpr int kTailGroup = 16;
+constexpr int kTailMaxEnt = INSITE_MAX_ARMS * (INSITE_MAX_TERMS * (INSITE_MAX_TERMS + 1) / 2 + INSITE_MAX_TERMS);
+struct GramOut {
+  double* G;
+  double* b;
+  int n_arms;
+};
+
+__device__ __forceinline__ void tail_store(double* p, double v) {  // sc1 (write-through) 8-byte store
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void gram_tail(double* __restrict__ part, int n_ent, unsigned* __restrict__ cnt,
+                                          const LibDesc& lib, const GramOut& o, double* red) {
+  int* flag = reinterpret_cast<int*>(red + kTailMaxEnt);  // "I am last", through the kernel's LDS array
+  const int nblk = (int)gridDim.x;
+  const int ng = (nblk + kTailGroup - 1) / kTailGroup;
+  const int g = (int)blockIdx.x / kTailGroup;
+  const int g0 = g * kTailGroup;
+  const int gs = nblk - g0 < kTailGroup ? nblk - g0 : kTailGroup;
+  double* gpart = part + (int64_t)nblk * n_ent;
+  auto publish = [&](unsigned* counter, unsigned arrivals) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == arrivals - 1u;
+      if (last) {
+        __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every arrival is in
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    return *flag != 0;
+  };
+  if (!publish(&cnt[1 + g], (unsigned)gs)) return;
+  for (int q = threadIdx.x; q < n_ent; q += kBlock) {  // the group's partials, block-index order
+    double v[kTailGroup];
+#pragma unroll
+    for (int j = 0; j < kTailGroup; ++j) v[j] = part[(int64_t)(g0 + (j < gs ? j : 0)) * n_ent + q];
+    double acc = v[0];
+#pragma unroll
+    for (int j = 1; j < kTailGroup; ++j) acc += j < gs ? v[j] : 0.0;
+    tail_store(gpart + (int64_t)g * n_ent + q, acc);
+  }
+  if (!publish(&cnt[0], (unsigned)ng)) return;
+  for (int q = threadIdx.x; q < n_ent; q += kBlock) {  // the group partials, group order (ng <= 64)
+    double acc = 0.0;
+#pragma unroll 16
+    for (int j = 0; j < ng; ++j) acc += gpart[(int64_t)j * n_ent + q];
+    red[q] = acc;
+  }
+  __syncthreads();
+  const int64_t F = lib.F;
+  for (int idx = threadIdx.x; idx < n_ent; idx += kBlock) {
+    const int a = idx / lib.nE, e = idx - a * lib.nE;
+    const int i = lib.ei[e], k = lib.ek[e];
+    const double v = red[idx];
+    if (k >= 0) {
+      o.G[(a * F + i) * F + k] = v;
+      o.G[(a * F + k) * F + i] = v;
+    } else {
+      o.b[a * F + i] = v;
+    }
+  }
+}
+
 // Lane = patient.  Work item = (64-patient tile, time segment [s*seg, (s+1)*seg)).  Rows are
 // staged [64 x kGT] through LDS (coalesced 16-B loads; the next tile in flight while the current
 // one is consumed); each lane streams its row through 8-deep register rings (compile-time ring
@@ -176,11 +259,12 @@ __device__ __forceinline__ void tele_lo(const GramW& w, double vm2, double vm1, 
 // MOM: per-patient moments mode (one time segment per patient): instead of the Gram contraction
 // every lane writes its patient's moments {L, sum xs, sum xs^2, sum xdot, sum xdot xs} to
 // partial[p * 5 ..] (insite_sindy_fit_per_patient_f64).
+// Otherwise the block partials are reduced inside the launch (gram_tail) into G [A, F, F] and b [A, F].
 template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))  // <= 256 VGPR+AGPR
 gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
             const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, int seg, int n_seg,
-            GramW w, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ ticket) {
+            GramW w, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ cnt, GramOut out) {
   __shared__ double smem[kWavesPerBlock * kWave * kGStride];
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform (SGPR)
@@ -192,7 +276,6 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
   constexpr int RPI = kWave / LPR;          // rows per wave instruction
   constexpr int NLD = kWave / RPI;          // load instructions per tile
   static_assert(!TM || (VEC == 1 && NLD == kGT), "time-major tiles hold the lane's own kGT samples");
-  if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0u;  // consumed by discovery_finalize (next launch)
   INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 0);
   INSITE_TREAL(blockIdx.x * kWavesPerBlock + wid, 8);
 
@@ -615,36 +698,31 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
   }
 
   INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 5);
-  // ---- block reduction (fixed order) -> partial[block][...] ----
+  // ---- block reduction (fixed order) -> compact partial[block][a * nE + e] -> gram_tail ----
   if constexpr (MOM) return;
   __syncthreads();
   double* red = smem;
+  const int n_ent = out.n_arms * lib.nE;  // the Gram entries the tail needs (<= kTailMaxEnt)
   if constexpr (MFMA) {
     // canonical C[row][col], row = (lane >> 4) + 4 j, col = lane & 15
 #pragma unroll
     for (int j = 0; j < 4; ++j) red[wid * 256 + ((lane >> 4) + 4 * j) * 16 + (lane & 15)] = cacc[j];
-    __syncthreads();
-    for (int q = threadIdx.x; q < 256; q += kBlock) {
-      double s = red[q];
-#pragma unroll
-      for (int ww = 1; ww < kWavesPerBlock; ++ww) s += red[ww * 256 + q];
-      partial[(int64_t)blockIdx.x * 256 + q] = s;
-    }
   } else {
 #pragma unroll
     for (int a = 0; a < NARM; ++a) red[(wid * NARM + a) * kWave + lane] = acc[a];
-    __syncthreads();
-    if (wid == 0) {
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < n_ent; idx += kBlock) {
+    const int a = idx / lib.nE, e = idx - a * lib.nE;
+    const int q = MFMA ? (a * lib.F + lib.ei[e]) * 16 + lib.qcol[e] : a * kWave + e;
+    constexpr int stride = MFMA ? 256 : NARM * kWave;
+    double v = red[q];
 #pragma unroll
-      for (int a = 0; a < NARM; ++a) {
-        double s = red[(0 * NARM + a) * kWave + lane];
-#pragma unroll
-        for (int ww = 1; ww < kWavesPerBlock; ++ww) s += red[(ww * NARM + a) * kWave + lane];
-        partial[((int64_t)blockIdx.x * NARM + a) * kWave + lane] = s;
-      }
-    }
+    for (int ww = 1; ww < kWavesPerBlock; ++ww) v += red[ww * stride + q];
+    tail_store(partial + (int64_t)blockIdx.x * n_ent + idx, v);
   }
   INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 6);
+  gram_tail(partial, n_ent, cnt, lib, out, smem);
   INSITE_TREAL(blockIdx.x * kWavesPerBlock + wid, 9);
 }
 
@@ -830,6 +908,7 @@ discovery_finalize(const double* __restrict__ partial, int nblk, int narm_pad, i
     INSITE_TSTAMP(49152 + blockIdx.x, 2);
     INSITE_TREAL(49152 + blockIdx.x, 9);
     if (!last) return;
+    if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // header stays zero
     const int arm_i = threadIdx.x;
     if (arm_i < n_arms) {
       double g[F][F], rhs[F], c[F];
@@ -2798,7 +2877,8 @@ inline GramPlan gram_plan(int64_t N, int64_t n_steps, int resident) {
   return pl;
 }
 
-constexpr size_t kGramWsHeader = 256;  // ticket word (+ padding)
+constexpr size_t kGramWsHeader = 512;  // counters: gram_tail cnt[0..64] / finalize ticket (+ padding; one memset block)
+static_assert((1 + (kGramMaxBlocks + kTailGroup - 1) / kTailGroup) * sizeof(unsigned) <= kGramWsHeader, "counters");
 
 inline int sse_grid(int64_t n_rows) {
   int64_t g = (n_rows + 63) / 64;
@@ -2819,7 +2899,8 @@ struct GramLaunch {
   GramW w;
   LibDesc lib;
   double* part;
-  unsigned* ticket;
+  unsigned* cnt;  // gram_tail counters (zeroed per call); MOM: unused
+  GramOut out;
 };
 
 template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM = false>
@@ -2837,7 +2918,7 @@ int launch_gram4(hipStream_t st, const GramLaunch& g) {
     if (pl.seg < kGT) pl.seg = kGT;
   }
   kern<<<dim3(pl.grid), kBlock, 0, st>>>(g.x, g.ldx, g.n_steps, g.u, g.arm, g.rows, g.N, pl.seg, pl.n_seg, g.w,
-                                          g.lib, g.part, g.ticket);
+                                          g.lib, g.part, g.cnt, g.out);
   return pl.grid;
 }
 
@@ -2874,7 +2955,7 @@ int launch_moments(int mode, hipStream_t st, const GramLaunch& g) {
   return launch_gram4<1, 1, SMOOTH, false, false, true>(st, g);
 }
 
-// gram kernel + fused finalize (+ STLSQ when sp.enabled)
+// gram kernel with its in-launch reduction to G / b (+ the STLSQ launch when sp.enabled)
 int32_t run_discovery(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,
                       const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
                       const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt, double* G_out, double* b_out,
@@ -2895,42 +2976,39 @@ int32_t run_discovery(const double* x, int64_t ldx, int32_t layout, int32_t n_st
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   const int na = narm_pad(n_arms);
   if (na * lib.F > 16) lib.mfma = 0;
-  unsigned* ticket = static_cast<unsigned*>(workspace);
+  unsigned* cnt = static_cast<unsigned*>(workspace);
   double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + kGramWsHeader);
   if (tm && ldx > ((int64_t)1 << 31) / (8 * kGT)) return INSITE_E_UNSUPPORTED;  // 32-bit tile offsets
   const bool vec2 = (ldx % 2 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15u) == 0);
   const int mode = tm ? 2 : (vec2 ? 1 : 0);
   const bool smooth = fd_kind == INSITE_FD_SMOOTHED4;
   if (n_statics == 0) u = x;  // kernels load u unconditionally (values unused when U = 0)
-  const GramLaunch g{x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, part, ticket};
-  int grid = 1;
-  if (na == 1) grid = launch_gram<1>(mode, smooth, hs, g);
-  else if (na == 2) grid = launch_gram<2>(mode, smooth, hs, g);
-  else grid = launch_gram<4>(mode, smooth, hs, g);
+#ifdef INSITE_GRAM_MEMSET  // ablation: re-zero gram_tail's counters with a memset node every call
+  if (hipMemsetAsync(cnt, 0, kGramWsHeader, hs) != hipSuccess) return INSITE_E_HIP;
+#endif
+  const GramLaunch g{x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, part, cnt,
+                     GramOut{G_out, b_out, n_arms}};
+  if (na == 1) launch_gram<1>(mode, smooth, hs, g);
+  else if (na == 2) launch_gram<2>(mode, smooth, hs, g);
+  else launch_gram<4>(mode, smooth, hs, g);
   st = launch_status();
-  if (st != INSITE_OK) return st;
-  const dim3 fg(n_arms * lib.nE);
-  if (!sp.enabled) {
-    discovery_finalize<0><<<fg, kBlock, 0, hs>>>(part, grid, na, n_arms, lib, G_out, b_out, sp, nullptr, nullptr,
-                                                 nullptr, ticket);
-    return launch_status();
-  }
-  switch (n_terms) {
-#define INSITE_FIN_CASE(FF)                                                                          \
-  case FF:                                                                                           \
-    discovery_finalize<FF><<<fg, kBlock, 0, hs>>>(part, grid, na, n_arms, lib, G_out, b_out, sp, coef_out, \
-                                                  mask_out, iters_out, ticket);                      \
+  if (st != INSITE_OK || !sp.enabled) return st;
+  switch (n_terms) {  // one thread per arm, register-resident STLSQ (SINDy.fit: reference sindy.py:190-192)
+#define INSITE_STL_CASE(FF)                                                                             \
+  case FF:                                                                                              \
+    stlsq_kernel<FF><<<1, kBlock, 0, hs>>>(G_out, b_out, n_arms, sp.thr, sp.alpha, sp.max_iter, sp.unbias, \
+                                           coef_out, mask_out, iters_out);                              \
     break;
-    INSITE_FIN_CASE(1)
-    INSITE_FIN_CASE(2)
-    INSITE_FIN_CASE(3)
-    INSITE_FIN_CASE(4)
-    INSITE_FIN_CASE(5)
-    INSITE_FIN_CASE(6)
-    INSITE_FIN_CASE(7)
-    INSITE_FIN_CASE(8)
-    INSITE_FIN_CASE(9)
-#undef INSITE_FIN_CASE
+    INSITE_STL_CASE(1)
+    INSITE_STL_CASE(2)
+    INSITE_STL_CASE(3)
+    INSITE_STL_CASE(4)
+    INSITE_STL_CASE(5)
+    INSITE_STL_CASE(6)
+    INSITE_STL_CASE(7)
+    INSITE_STL_CASE(8)
+    INSITE_STL_CASE(9)
+#undef INSITE_STL_CASE
     default:
       return INSITE_E_UNSUPPORTED;
   }
@@ -3172,7 +3250,8 @@ size_t insite_gram_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n
   (void)n_terms;
   if (n_patients < 0 || n_arms < 1 || n_arms > INSITE_MAX_ARMS) return 0;
   const size_t per_block = narm_pad(n_arms) * kWave > 256 ? (size_t)narm_pad(n_arms) * kWave : 256;
-  return kGramWsHeader + (size_t)kGramMaxBlocks * per_block * sizeof(double);
+  const size_t groups = (kGramMaxBlocks + kTailGroup - 1) / kTailGroup;  // gram_tail's group partials
+  return kGramWsHeader + (size_t)(kGramMaxBlocks + groups) * per_block * sizeof(double);  // >= compact size
 }
 
 int32_t insite_gram_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,
@@ -3259,7 +3338,8 @@ int32_t insite_sindy_fit_per_patient_f64(const double* x, int64_t ldx, int32_t l
   const int mode = tm ? 2 : (vec2 ? 1 : 0);
   if (n_statics == 0) u = x;
   lib.mfma = 0;
-  const GramLaunch g{x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, mom, ticket};
+  const GramLaunch g{x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, mom, ticket,
+                     GramOut{nullptr, nullptr, 0}};
   if (fd_kind == INSITE_FD_SMOOTHED4) launch_moments<true>(mode, hs, g);
   else launch_moments<false>(mode, hs, g);
   st = launch_status();

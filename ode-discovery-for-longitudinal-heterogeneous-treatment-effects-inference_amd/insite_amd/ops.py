@@ -60,7 +60,10 @@ def _dev(name, t, dtype, ndim=None):
 
 class Workspace:
     """Grow-only device scratch buffer (the library never allocates).  A buffer handed to a ``Plan`` is
-    referenced by that plan, so growing the workspace later never frees memory a plan still writes to."""
+    referenced by that plan, so growing the workspace later never frees memory a plan still writes to.
+    Buffers start zeroed: the discovery kernels' arrival counters (the header) must be zero before a
+    workspace's first use, and every call leaves them zero (insite_hip.h) -- so a Workspace given to the
+    discovery family (gram / sindy_fit / segments / per-patient) must not also be given to other ops."""
 
     def __init__(self):
         self._buf = {}
@@ -69,19 +72,21 @@ class Workspace:
         key = torch.device(device).index
         b = self._buf.get(key)
         if b is None or b.numel() < nbytes:
-            b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            b = torch.zeros(max(int(nbytes), 512), dtype=torch.uint8, device=device)
             self._buf[key] = b
         return b
 
 
-# eager ops without an explicit workspace: one per (device, stream), so launches on different streams
-# never share scratch
+# eager ops without an explicit workspace: one per (device, stream, kind), so launches on different
+# streams never share scratch, and the discovery family ("disc": gram / sindy_fit / segments /
+# per-patient, whose header holds the in-launch reduction's counters, zero between calls) never shares a
+# buffer with ops that write scratch from offset 0
 _WS_BY_STREAM: dict = {}
 
 
-def _default_ws(device) -> Workspace:
+def _default_ws(device, kind: str = "misc") -> Workspace:
     dev = torch.device(device)
-    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream, kind)
     ws = _WS_BY_STREAM.get(key)
     if ws is None:
         ws = _WS_BY_STREAM[key] = Workspace()
@@ -159,7 +164,7 @@ def _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout, stl
     F = lib.n_terms
     dev = x.device
     nbytes = L.insite_gram_workspace_bytes(N, n_arms, F)
-    ws = (workspace or _default_ws(dev)).get(nbytes, dev)
+    ws = (workspace or _default_ws(dev, "disc")).get(nbytes, dev)
     tab = lib.ctypes_table()
     head = (_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), _p(rows), N,
             lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p), F, FD_KINDS[fd], float(dt))
@@ -237,7 +242,7 @@ def sindy_fit_per_patient(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, r
                torch.empty((N, F), dtype=torch.int8, device=dev),
                torch.empty((N,), dtype=torch.int32, device=dev))
     coef, mask, iters = out
-    ws = (workspace or _default_ws(dev)).get(L.insite_per_patient_workspace_bytes(N), dev)
+    ws = (workspace or _default_ws(dev, "disc")).get(L.insite_per_patient_workspace_bytes(N), dev)
     tab = lib.ctypes_table()
     args = (_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), _p(rows), N,
             lib.n_statics, A, tab.ctypes.data_as(ctypes.c_void_p), F, FD_KINDS[fd], float(dt), _p(global_coef),
@@ -278,7 +283,7 @@ def _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layo
     L = _lib.load()
     F = lib.n_terms
     dev = x.device
-    ws = (workspace or _default_ws(dev)).get(L.insite_gram_segments_workspace_bytes(N, n_arms, F), dev)
+    ws = (workspace or _default_ws(dev, "disc")).get(L.insite_gram_segments_workspace_bytes(N, n_arms, F), dev)
     tab = lib.ctypes_table()
     head = (_p(x), x.stride(0), _p(arm), arm.stride(0), LAYOUTS[layout], n_steps, _p(seq_len),
             _p(u) if lib.n_statics else ctypes.c_void_p(0), N, lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p),
