@@ -827,9 +827,12 @@ def main():
     y0 = coh.y0
     # per-step state in NB buffers: the discovery of step i writes coefs[i % NB] while older rollouts may
     # still read theirs (G|b and the gram workspace are only touched by the discovery stream, in order,
-    # but are buffered alike to keep the plans independent); rollouts alternate between RS streams (and
-    # y buffers), so one rollout stream's wait for its discovery overlaps the other's rollout
-    NB, RS, WAR_EVERY = 16, 2, 8
+    # but are buffered alike to keep the plans independent).  Steps go in batches of K: one event per batch
+    # each way (an event record costs ~20 us of dead queue time on ROCm 7.2, profiles/
+    # r02_c2_pipeline_trace.txt); batches alternate between RS rollout streams and y buffers.
+    K, RS, WAR_EVERY = 4, 2, 8
+    NB = 3 * K * RS                     # a multiple of K * RS: step k's y buffer (k // K) % RS is fixed per coef slot
+    NBE = NB // K                       # event slots (batches in flight)
     bufs = [idist.MomentBuffer(2, F, dev) for _ in range(NB)]     # G|b in one buffer: one all-reduce
     coefs = [torch.empty((2, F), dtype=torch.float64, device=dev) for _ in range(NB)]
     masks = [torch.empty((2, F), dtype=torch.int8, device=dev) for _ in range(NB)]
@@ -839,6 +842,8 @@ def main():
     mode = args.mode if (world == 1 or args.mode != "graph") else "seq"   # RCCL stays outside graphs
     if mode != "pipeline":
         RS = 1
+    if mode != "pipeline":
+        K = 1
     ys = [torch.empty((T, N) if args.layout == "time" else (N, T), dtype=torch.float64, device=dev)
           for _ in range(RS)]
     y = ys[0]
@@ -848,12 +853,12 @@ def main():
     # one step = discovery (Gram -> [RCCL all-reduce when N > 1] -> STLSQ) then the rollout with that
     # step's coefficients.  Launches go through prepared plans (arguments validated and packed once).
     #   pipeline : discovery stream (gram with its in-launch reduction to G|b, [all-reduce,] STLSQ: no
-    #              cross-stream hop inside it) | RS rollout streams taking alternate steps — NB-buffered
-    #              coefficients; each rollout waits for its step's discovery event, and the discovery
-    #              stream waits, every WAR_EVERY steps, for the rollout WAR_EVERY steps back (so a buffer
-    #              is rewritten only after the rollout NB steps back has read it).  A cross-stream wait
-    #              costs ~20 us of dead queue time on ROCm 7 (profiles/), so the waits are spread over
-    #              streams that have other work and thinned to what the buffer reuse needs
+    #              cross-stream hop inside it) | RS rollout streams taking alternate batches of K steps —
+    #              NB-buffered coefficients; a batch's rollouts wait for one event after its last discovery,
+    #              and the discovery stream waits, every WAR_EVERY steps, for the rollout batches whose
+    #              buffers the next WAR_EVERY steps reuse.  Event records cost ~20 us of dead queue time
+    #              each on ROCm 7.2 (profiles/r02_c2_pipeline_trace.txt), so there is one per batch per
+    #              stream; every step still runs its own discovery and the rollout with its coefficients
     #   seq      : gram + in-launch reduction + STLSQ (N = 1) then the rollout, eagerly on one stream
     #   graph    : the seq step captured once in a HIP graph and replayed (N = 1)
     # The timed region holds no timing events: per-kernel durations come from the separate
@@ -867,17 +872,18 @@ def main():
         stlsq_plans = [ops.plan_stlsq(bufs[j].G, bufs[j].b, 0.1, 0.5, 100, True, out=(coefs[j], masks[j], iters[j]))
                        for j in range(NB)]
     roll_plans = [ops.plan_rollout(y0, coh.u, arm_cf, coefs[j], lib, coh.dt, method=args.method, T=T,
-                                   out=ys[j % RS], layout=roll_layout) for j in range(NB)]
+                                   out=ys[(j // K) % RS], layout=roll_layout) for j in range(NB)]
     # cross-stream ordering through the HIP runtime directly (torch's Event wrappers cost ~3-5 us of host
     # time each; at N > 1 the host also issues the all-reduce, and must stay ahead of a ~70 us step)
     hip = HipEvents()
-    ev = {k: hip.create() for k in [(n, j) for n in "gr" for j in range(NB)]}
+    ev = {k: hip.create() for k in [(n, j) for n in "gr" for j in range(NBE)]}
     hs_g = s_g.cuda_stream
-    last_r = [None] * NB
+    done_r = [None] * NBE                   # (batch, rollout-done event) per event slot
+    pending = []                            # steps discovered, rollouts not yet issued
     f_fast = [p.bind(s_g) for p in fused]
     g_fast = [p.bind(s_g) for p in gram_plans]
     c_fast = [p.bind(s_g) for p in stlsq_plans]
-    r_fast = [p.bind(s_rs[j % RS]) for j, p in enumerate(roll_plans)]
+    r_fast = [p.bind(s_rs[(j // K) % RS]) for j, p in enumerate(roll_plans)]
 
     def discover(i, st):
         """Discovery of step i on stream st (used by seq / graph and the roofline pass)."""
@@ -907,15 +913,15 @@ def main():
                 hip.record(tev[3], st.cuda_stream)
             return
         if i % WAR_EVERY == 0:
-            # steps i .. i+WAR_EVERY-1 reuse the buffers of steps i-NB .. i-NB+WAR_EVERY-1: wait, on each
-            # rollout stream, for its newest rollout at or below that bound (a stream runs in order)
-            bound = i - NB + WAR_EVERY - 1
+            # steps i .. i+WAR_EVERY-1 reuse the buffers of steps i-NB .. bound: wait, on each rollout
+            # stream, for its newest batch at or below bound's batch (a stream runs its batches in order;
+            # NB >= WAR_EVERY + K, so that batch has been issued)
+            bb = (i - NB + WAR_EVERY - 1) // K
             for r in range(RS):
-                k = bound - ((bound - r) % RS)
-                if k >= 0 and last_r[k % NB] is not None:
-                    hip.wait(hs_g, last_r[k % NB])
-        hs_r = s_rs[i % RS].cuda_stream
-        if tev:
+                b = bb - ((bb - r) % RS)
+                if b >= 0 and done_r[b % NBE] is not None and done_r[b % NBE][0] == b:
+                    hip.wait(hs_g, done_r[b % NBE][1])
+        if tev and i % K == 0:
             hip.record(tev[0], hs_g)
         if world == 1:
             f_fast[j]()                             # gram + in-launch reduction, STLSQ
@@ -924,17 +930,29 @@ def main():
             with torch.cuda.stream(s_g):
                 idist.reduce_moments(bufs[j])       # the only collective
             c_fast[j]()
+        pending.append(i)
+        if i % K == K - 1:
+            flush(tev)
+
+    def flush(tev=None):
+        """Issue the rollouts of the pending batch behind one event on the discovery stream."""
+        if not pending:
+            return
+        b = pending[0] // K
         if tev:
             hip.record(tev[1], hs_g)
-        hip.record(ev["g", j], hs_g)
-        hip.wait(hs_r, ev["g", j])
+        hip.record(ev["g", b % NBE], hs_g)
+        hs_r = s_rs[b % RS].cuda_stream
+        hip.wait(hs_r, ev["g", b % NBE])
         if tev:
             hip.record(tev[2], hs_r)
-        r_fast[j]()
+        for k in pending:
+            r_fast[k % NB]()
         if tev:
             hip.record(tev[3], hs_r)
-        hip.record(ev["r", j], hs_r)
-        last_r[j] = ev["r", j]
+        hip.record(ev["r", b % NBE], hs_r)
+        done_r[b % NBE] = (b, ev["r", b % NBE])
+        pending.clear()
 
     graph = None
     if mode == "graph":
@@ -949,6 +967,8 @@ def main():
         run = step
     for i in range(args.warmup):
         run(i)
+    if mode == "pipeline":
+        flush()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -956,6 +976,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         run(i)
+    if mode == "pipeline":
+        flush()                                     # a partial last batch
     host_ms = (time.perf_counter() - t0) / args.steps * 1e3   # submit time per step (no sync)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -969,22 +991,23 @@ def main():
     # with HIP timing events around the gram and rollout launches on the streams they run on.  Per-launch
     # averages of the kernels exactly as they run in the step; a rocprofv3 --kernel-trace --stats run of
     # this bench (--no-north-star) averages the same pipelined launches (profiles/).
-    n_inst = max(args.steps, 10)
-    tevs = [tuple(hip.create(timing=True) for _ in range(4)) for _ in range(n_inst)]
+    n_inst = max(args.steps, 10) // K * K
+    tevs = [tuple(hip.create(timing=True) for _ in range(4)) for _ in range(n_inst // K)]
     if mode == "graph":
         for i in range(n_inst):
             hip.record(tevs[i][0], torch.cuda.current_stream(dev).cuda_stream)
             graph.replay()
             hip.record(tevs[i][3], torch.cuda.current_stream(dev).cuda_stream)
     else:
+        base = (args.steps + K - 1) // K * K       # start on a batch boundary (the timed run flushed its tail)
         for i in range(n_inst):
-            step(args.steps + i, tevs[i])
+            step(base + i, tevs[i // K])
     torch.cuda.synchronize(dev)
     if mode == "graph":
         roll_ms = disc_ms = float(np.mean([hip.elapsed_ms(t[0], t[3]) for t in tevs]))
-    else:
-        disc_ms = float(np.mean([hip.elapsed_ms(t[0], t[1]) for t in tevs]))
-        roll_ms = float(np.mean([hip.elapsed_ms(t[2], t[3]) for t in tevs]))
+    else:                                           # per batch of K, divided by K
+        disc_ms = float(np.mean([hip.elapsed_ms(t[0], t[1]) for t in tevs])) / K
+        roll_ms = float(np.mean([hip.elapsed_ms(t[2], t[3]) for t in tevs])) / K
 
     # isolated launches (reported beside it, not as the roofline): each kernel back to back on one stream
     def timed(fn, n):
