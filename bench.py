@@ -397,7 +397,7 @@ def c5_main(args):
     rollout of every patient.  Lane-level step-size control: waves run until their slowest lane finishes."""
     cpu = None
     if os.environ.get("WORLD_SIZE", "1") == "1" and not args.no_cpu_baseline:
-        cpu = c5_cpu_baseline(min(args.cpu_sample, 4000), args.seed + 4)
+        cpu = c5_cpu_baseline(min(10 * args.cpu_sample, 100_000), args.seed + 4)   # ~10 s on 16 workers
     world, rank, dev = dist_setup()
     from insite_amd import ops, cohort
     from insite_amd import dist as idist

@@ -421,6 +421,265 @@ gram_ms_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// gram_ms4_kernel: the same contraction cut entirely into 4 x 4 blocks (the default form)
+// ---------------------------------------------------------------------------------------------
+// Y^T Z with Y = Theta (F columns) and Z = [Theta | xdot] (F + S columns) is needed on the upper
+// triangle of the Theta block and on every xdot column only.  As 16 x 16 x 4 tiles (gram_ms_kernel) the
+// F = 22 system issues 592 FMA per row for 363 needed: the Y0^T Z0 tile computes its lower triangle,
+// and the Y0^T Z1 tile and the tail carry padding rows / columns.  Cut into 4 x 4 blocks (row group
+// rg < RG over Y, column group cg >= rg over Z) the same system is 27 blocks = 432 FMA per row, and on
+// gfx950 v_mfma_f64_4x4x4f64 retires FMAs at the rate of the 16 x 16 x 4 form (tools/probe/
+// mfma_f64_rate_probe.hip: 17 vs 64 cycles for 1/4 of the work), so the MFMA time drops by the FMA ratio.
+// Operands: lane 16 k + 4 b + i of pass r holds row 16 r + 4 b + k, columns 4 q + i of the staged LDS
+// row (one ds_read_b64 per column group serves A and B); block b of every MFMA takes different rows, so
+// D[b][m][n] accumulates one quarter of the rows and the epilogue sums the four (lanes xor 4, 8).
+// Interior derivatives: savgol(5, 3) then the 5-point FD is one 9-tap antisymmetric filter on the raw
+// samples, xdot[r] = sum_n c_n (x[r+n] - x[r-n]) / dt, c = (37/105, 79/420, -3/35, 1/140) (the exact
+// convolution of the two interior stencils), so the streamed interior needs only the raw fp32 ring
+// (12 slots: x[t-8 .. t] live, x[t+3] prefetched) -- no smoothed fp64 ring, ~40 VGPRs fewer than the 16 x 16
+// form, which spilled at occupancy 2.  Edge rows keep the one-sided stencils (window form, as before).
+template <int S, int F>
+struct Ms4 {
+  static constexpr int RG = (F + 3) / 4;          // Y (Theta) column groups
+  static constexpr int CG = (F + S + 3) / 4;      // Z ([Theta | xdot]) column groups
+  static constexpr int NB = RG * CG - RG * (RG - 1) / 2;  // blocks with cg >= rg
+  static_assert(4 * CG <= kMsMaxF, "staged row");
+};
+#ifndef INSITE_MS4_SCHED
+#define INSITE_MS4_SCHED 1
+#endif
+constexpr int kMs4Stride = 29;   // LDS row stride (doubles): odd, stores conflict-free, 2-way on the reads
+#ifndef INSITE_MS4_RING
+#define INSITE_MS4_RING 12
+#endif
+constexpr int kMs4Ring = INSITE_MS4_RING;  // raw-sample ring slots (interior): x[t-8 .. t] + kMs4Ring - 9 prefetched
+constexpr double kMsC1 = 37.0 / 105.0, kMsC2 = 79.0 / 420.0, kMsC3 = -3.0 / 35.0, kMsC4 = 1.0 / 140.0;
+
+// The library row is formed column by column straight into LDS (Theta_j = z_i z_k, pysindy order), so the
+// F products are never live at once.
+template <int S, int NZ, bool INTER>
+__device__ __forceinline__ void ms_emit4(double* __restrict__ wrow, const double* __restrict__ wbase, bool valid,
+                                         const double (&z)[NZ + 1], const double (&xd)[S],
+                                         double (&acc)[Ms4<S, PolyCols<NZ, INTER>::F>::NB], int lane) {
+  constexpr int F = PolyCols<NZ, INTER>::F;
+  constexpr PolyCols<NZ, INTER> pc;
+  using M4 = Ms4<S, F>;
+  wave_lds_sync();  // every lane finished reading the previous rows
+#pragma unroll
+  for (int j = 0; j < 4 * M4::CG; ++j) {
+    double v = 0.0;
+    if (j < F) v = pc.ck[j] == 0 ? z[pc.ci[j]] : z[pc.ci[j]] * z[pc.ck[j]];
+    else if (j < F + S) v = xd[j - F];
+    wrow[j] = valid ? v : 0.0;
+  }
+  wave_lds_sync();
+  const int kk = lane >> 4, bb = (lane >> 2) & 3, ii = lane & 3;
+  const double* src0 = wbase + (4 * bb + kk) * kMs4Stride + ii;
+  // operands of pass r + 1 are read from LDS before pass r's MFMAs issue (two sets live): the LDS
+  // latency hides behind the 27-MFMA pass instead of stalling the wave at every pass
+  double v[2][M4::CG];
+#pragma unroll
+  for (int q = 0; q < M4::CG; ++q) v[0][q] = src0[4 * q];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#if INSITE_MS4_SCHED
+    __builtin_amdgcn_sched_barrier(0);  // at most two passes' operands live (register budget, occupancy 2)
+#endif
+    if (r < 3) {
+#pragma unroll
+      for (int q = 0; q < M4::CG; ++q) v[(r + 1) & 1][q] = src0[16 * (r + 1) * kMs4Stride + 4 * q];
+    }
+    int t = 0;
+#pragma unroll
+    for (int rg = 0; rg < M4::RG; ++rg)
+#pragma unroll
+      for (int cg = rg; cg < M4::CG; ++cg, ++t)
+        acc[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(v[r & 1][rg], v[r & 1][cg], acc[t], 0, 0, 0);
+  }
+}
+
+template <int S, int NIN, bool INTER>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_MS_WPE)))
+gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint32_t* __restrict__ abits,
+                int64_t lda, const int32_t* __restrict__ rows, int64_t N, GramW w, double* __restrict__ partial) {
+  constexpr int NZ = S + NIN;
+  constexpr int F = PolyCols<NZ, INTER>::F;
+  using M4 = Ms4<S, F>;
+  __shared__ double stage[kWavesPerBlock * kWave * kMs4Stride];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  double* wbase = stage + wid * kWave * kMs4Stride;
+  double* wrow = wbase + lane * kMs4Stride;
+  double acc[M4::NB];
+#pragma unroll
+  for (int q = 0; q < M4::NB; ++q) acc[q] = 0.0;
+  const int64_t n_tiles = (N + kWave - 1) / kWave;
+  const int64_t sstride = ldx;              // between states of one step
+  const int64_t kstride = (int64_t)S * ldx; // between steps
+  const double c1 = kMsC1 * w.inv_dt, c2 = kMsC2 * w.inv_dt, c3 = kMsC3 * w.inv_dt, c4 = kMsC4 * w.inv_dt;
+
+  for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid; tile < n_tiles;
+       tile += (int64_t)gridDim.x * kWavesPerBlock) {
+    const int64_t p0 = tile * kWave;
+    const int64_t p = p0 + lane;
+    const bool in = p < N;
+    const int64_t pc = in ? p : N - 1;
+    int L = rows ? rows[pc] : n_steps;
+    if (L > n_steps) L = n_steps;
+    if (!in || L < 5) L = 0;
+    const int Lmax = wave_max_i(L);
+    const float* xp = x + pc;
+    auto ld = [&](int k, int s) -> double { return (double)xp[(int64_t)k * kstride + s * sstride]; };
+
+    // ---------------- interior rows (L >= 9): r = 4 .. L-5 at steps t = 8 .. L-1 ----------------
+    if (Lmax >= 9) {
+      float xr[kMs4Ring][S];
+      auto word = [&](int g) -> unsigned {  // treatment bits of rows [32 g, 32 g + 32), half-wave transpose
+        if (!abits) return 0u;
+        const int k = 32 * g + (lane & 31);
+        const int kk = k < n_steps ? k : n_steps - 1;
+        const int64_t col = (p0 >> 5) + (lane >> 5);
+        const uint32_t v = col * 32 < N ? abits[(int64_t)kk * lda + col] : 0u;
+        return bit_transpose32(v, lane);
+      };
+#pragma unroll
+      for (int t = 0; t < kMs4Ring - 9; ++t)
+#pragma unroll
+        for (int s = 0; s < S; ++s) xr[t][s] = xp[(int64_t)t * kstride + s * sstride];
+      unsigned wcur = word(0);
+      for (int t0 = 0; t0 < Lmax; t0 += kMs4Ring) {
+#pragma unroll
+        for (int i = 0; i < kMs4Ring; ++i) {
+          const int t = t0 + i;
+          if (t < Lmax) {  // uniform
+            // x[t + PF] into the slot of x[t - 9 + ...] (no longer needed): its wait falls PF steps later
+            constexpr int PF = kMs4Ring - 9;
+            const int tn = t + PF < n_steps ? t + PF : n_steps - 1;
+#pragma unroll
+            for (int s = 0; s < S; ++s) xr[(i + PF) % kMs4Ring][s] = xp[(int64_t)tn * kstride + s * sstride];
+            if (t >= 8) {  // row r = t - 4: raw x[r], xdot from x[r-4 .. r+4] (slots i-8 .. i)
+              const int r = t - 4;
+              if ((r & 31) == 0) wcur = word(r >> 5);
+              double z[NZ + 1], xd[S];
+              z[0] = 1.0;
+#pragma unroll
+              for (int s = 0; s < S; ++s) {
+                auto X = [&](int d) -> double { return (double)xr[(i + kMs4Ring + d) % kMs4Ring][s]; };  // x[t + d]
+                z[1 + s] = X(-4);
+                xd[s] = c1 * (X(-3) - X(-5)) + c2 * (X(-2) - X(-6)) + c3 * (X(-1) - X(-7)) + c4 * (X(0) - X(-8));
+              }
+#pragma unroll
+              for (int q = 0; q < NIN; ++q) z[1 + S + q] = (double)((wcur >> (r & 31)) & 1u);
+              ms_emit4<S, NZ, INTER>(wrow, wbase, t <= L - 1, z, xd, acc, lane);
+            }
+          }
+        }
+      }
+    }
+
+    // ---------------- edge rows: 0..3 and L-4..L-1 (all rows when 5 <= L < 8) ----------------
+    // one row at a time (its window re-read per row from the cache: 8 of ~500 rows per patient), so the
+    // edge path holds one 8-sample window instead of 4 rows x S states of values and derivatives
+    if (Lmax >= 5) {
+      for (int j = 0; j < 8; ++j) {  // window row: part j / 4, position j % 4 within the part
+        const int base = j < 4 ? 0 : (L >= 8 ? L - 8 : 0);
+        const bool valid = (L >= 8) || (j < L);
+        const int step = base + j;
+        double z[NZ + 1], xd[S];
+        z[0] = 1.0;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          double xv[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int k = base + q < n_steps ? base + q : n_steps - 1;
+            xv[q] = ld(k, s);
+          }
+          double a8[8], d8[8];
+          if (L >= 8) {
+            // rows 0..3 from the head window, L-4..L-1 (window rows 4..7) from the tail window
+#pragma unroll
+            for (int k = 2; k < 6; ++k) a8[k] = sg_int(w, xv[k - 2], xv[k - 1], xv[k], xv[k + 1], xv[k + 2]);
+            a8[0] = sg_pos0(xv[0], xv[1], xv[2], xv[3], xv[4]);
+            a8[1] = sg_pos1(xv[0], xv[1], xv[2], xv[3], xv[4]);
+            a8[6] = sg_pos3(xv[3], xv[4], xv[5], xv[6], xv[7]);
+            a8[7] = sg_pos4(xv[3], xv[4], xv[5], xv[6], xv[7]);
+            double d;
+            switch (j) {
+              case 0: d = fd_pos0(a8[0], a8[1], a8[2], a8[3], a8[4]) * w.inv_dt; break;
+              case 1: d = fd_pos1(a8[0], a8[1], a8[2], a8[3], a8[4]) * w.inv_dt; break;
+              case 2: d = fd_int(w, a8[0], a8[1], a8[3], a8[4]); break;
+              case 3: d = fd_int(w, a8[1], a8[2], a8[4], a8[5]); break;
+              case 4: d = fd_int(w, a8[2], a8[3], a8[5], a8[6]); break;
+              case 5: d = fd_int(w, a8[3], a8[4], a8[6], a8[7]); break;
+              case 6: d = fd_pos3(a8[3], a8[4], a8[5], a8[6], a8[7]) * w.inv_dt; break;
+              default: d = fd_pos4(a8[3], a8[4], a8[5], a8[6], a8[7]) * w.inv_dt; break;
+            }
+            xd[s] = d;
+          } else {
+            if (L == 7) ms_small<7>(xv, w, a8, d8);
+            else if (L == 6) ms_small<6>(xv, w, a8, d8);
+            else ms_small<5>(xv, w, a8, d8);
+            xd[s] = d8[j];
+          }
+          z[1 + s] = xv[j];  // raw sample of the row (smoothing feeds x_dot only)
+        }
+#pragma unroll
+        for (int qq = 0; qq < NIN; ++qq) z[1 + S + qq] = (L > 0 && step < n_steps) ? input_bit(abits, lda, step, pc) : 0.0;
+        ms_emit4<S, NZ, INTER>(wrow, wbase, L > 0 && valid, z, xd, acc, lane);
+      }
+    }
+  }
+
+  // ---- block partial (fixed order): partial[block][t * 16 + 4 m + n] = sum over waves and the 4 row quarters
+  // b of D[b][m][n] of block type t ----
+  __syncthreads();
+  double* red = stage;
+  const int m = lane >> 4, n = lane & 3;
+#pragma unroll
+  for (int t = 0; t < M4::NB; ++t) {
+    double v = acc[t];
+    v += __shfl_xor(v, 4, kWave);
+    v += __shfl_xor(v, 8, kWave);
+    if (((lane >> 2) & 3) == 0) red[(wid * M4::NB + t) * 16 + 4 * m + n] = v;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < M4::NB * 16; q += kBlock) {
+    double sum = red[q];
+#pragma unroll
+    for (int ww = 1; ww < kWavesPerBlock; ++ww) sum += red[ww * M4::NB * 16 + q];
+    partial[(int64_t)blockIdx.x * M4::NB * 16 + q] = sum;
+  }
+}
+
+// Fixed-order reduction of gram_ms4_kernel's block partials and scatter into G [F, F] and B [F, S]:
+// entry (t, m, n) of block type t = (rg, cg) is (Y row 4 rg + m, Z column 4 cg + n); the Theta-Theta
+// blocks above the diagonal also fill their mirror.
+__global__ void __launch_bounds__(kWave) ms4_finalize(const double* __restrict__ partial, int nblk, int nb, int rgn,
+                                                      int cgn, int F, int S, double* __restrict__ G,
+                                                      double* __restrict__ B) {
+  const int q = blockIdx.x * kWave + threadIdx.x;
+  if (q >= nb * 16) return;
+  double v = 0.0;
+  for (int g = 0; g < nblk; ++g) v += partial[(int64_t)g * nb * 16 + q];
+  int t = q / 16, rg = 0;
+  while (t >= cgn - rg) {  // block types enumerate rg-major, cg = rg .. cgn-1
+    t -= cgn - rg;
+    ++rg;
+  }
+  const int cg = rg + t;
+  const int row = 4 * rg + (q % 16) / 4, col = 4 * cg + q % 4;
+  (void)rgn;
+  if (row >= F) return;
+  if (col < F) {
+    G[(int64_t)row * F + col] = v;
+    if (cg > rg) G[(int64_t)col * F + row] = v;
+  } else if (col < F + S) {
+    B[(int64_t)row * S + (col - F)] = v;
+  }
+}
+
 // Fixed-order reduction of the tile partials and scatter into G [F, F] (symmetric) and B [F, S].
 __global__ void __launch_bounds__(kWave) ms_finalize(const double* __restrict__ partial, int nblk, int F, int S,
                                                      double* __restrict__ G, double* __restrict__ B) {
@@ -969,12 +1228,12 @@ int32_t insite_gram_ms_f32(const float* x, int64_t ldx, int32_t n_steps, int32_t
   w.inv_dt = 1.0 / dt;
   w.fd1 = (2.0 / 3.0) * w.inv_dt;
   w.fd2 = (-1.0 / 12.0) * w.inv_dt;
+  if (nin == 1 && inter != 1) return INSITE_E_UNSUPPORTED;  // 5 states + input, full degree 2: F + S > 32
+#ifdef INSITE_MS_V1  // the 16 x 16 x 4 tile form (A/B builds, tools/build_ablation.sh)
   if (n_patients == 0 || n_steps < 5) {
     if (hipMemsetAsync(part, 0, (size_t)grid * kMsTiles * 256 * sizeof(double), hs) != hipSuccess) return INSITE_E_HIP;
-  } else if (nin == 1 && inter == 1) {
-    gram_ms_kernel<5, 1, true><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, inp_bits, ld_bits, rows, n_patients, w, part);
   } else if (nin == 1) {
-    return INSITE_E_UNSUPPORTED;  // 5 states + input, full degree 2: F + S > 32
+    gram_ms_kernel<5, 1, true><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, inp_bits, ld_bits, rows, n_patients, w, part);
   } else if (inter == 1) {
     gram_ms_kernel<5, 0, true><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, nullptr, 0, rows, n_patients, w, part);
   } else {
@@ -983,6 +1242,31 @@ int32_t insite_gram_ms_f32(const float* x, int64_t ldx, int32_t n_steps, int32_t
   int32_t st = launch_status();
   if (st != INSITE_OK) return st;
   ms_finalize<<<(kMsTiles * 256 + kWave - 1) / kWave, kWave, 0, hs>>>(part, grid, n_terms, n_states, G_out, B_out);
+#else
+  int nb = 0, rgn = 0, cgn = 0;
+  auto geom = [&](auto m4) {
+    using M4 = decltype(m4);
+    nb = M4::NB;
+    rgn = M4::RG;
+    cgn = M4::CG;
+  };
+  if (nin == 1) geom(Ms4<5, PolyCols<6, true>::F>{});
+  else if (inter == 1) geom(Ms4<5, PolyCols<5, true>::F>{});
+  else geom(Ms4<5, PolyCols<5, false>::F>{});
+  if (n_patients == 0 || n_steps < 5) {
+    if (hipMemsetAsync(part, 0, (size_t)grid * nb * 16 * sizeof(double), hs) != hipSuccess) return INSITE_E_HIP;
+  } else if (nin == 1) {
+    gram_ms4_kernel<5, 1, true><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, inp_bits, ld_bits, rows, n_patients, w, part);
+  } else if (inter == 1) {
+    gram_ms4_kernel<5, 0, true><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, nullptr, 0, rows, n_patients, w, part);
+  } else {
+    gram_ms4_kernel<5, 0, false><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, nullptr, 0, rows, n_patients, w, part);
+  }
+  int32_t st = launch_status();
+  if (st != INSITE_OK) return st;
+  ms4_finalize<<<(nb * 16 + kWave - 1) / kWave, kWave, 0, hs>>>(part, grid, nb, rgn, cgn, n_terms, n_states, G_out,
+                                                                B_out);
+#endif
   return launch_status();
 }
 

@@ -11,6 +11,9 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     RK45PI) NAME=$v build -DINSITE_RK45_PER_INTERVAL ;;
     RKW8W6) NAME=$v build -DINSITE_RK45_WIN=8 -DINSITE_RK45_WPE=6 ;;
     RKPMNT) NAME=$v build -DINSITE_RK45_PM_NT=1 ;;
+    MSV1) NAME=$v build -DINSITE_MS_V1 ;;
+    MS4S0) NAME=$v build -DINSITE_MS4_SCHED=0 ;;
+    MS4R10) NAME=$v build -DINSITE_MS4_RING=10 ;;
     RKW8W8) NAME=$v build -DINSITE_RK45_WIN=8 -DINSITE_RK45_WPE=8 ;;
     RKW16W5) NAME=$v build -DINSITE_RK45_WIN=16 -DINSITE_RK45_WPE=5 ;;
     SEGKC8) NAME=$v build -DINSITE_SEG_KC=8 -DINSITE_SEG_WPE=3 ;;
