@@ -315,12 +315,11 @@ def c3_main(args):
     truth = MS.c3_truth_coef(lib, device=dev)
     rows = N * T
     gflop = 2.0 * (F * (F + 1) / 2 + F * S) * rows          # algorithmic: G upper triangle + B per row
-    # issued: 2 f64 16x16x4 tiles per 4 rows, plus (F > 16) the tail's 4x4x4 blocks (MsTail, insite_ms.hip):
-    # NT4 block types x 4 instructions of 512 flop per 64 rows
-    f1 = max(F - 16, 0)
-    rg, cg = (f1 + 3) // 4, (f1 + S + 3) // 4
-    nt4 = rg * cg - rg * (rg - 1) // 2 if f1 else 0
-    mfma_flop = (2 * 16 * 16 * 4 * 2 + nt4 * 4 * 512 / 16) * rows / 4
+    # issued by gram_ms4_kernel (insite_ms.hip Ms4): NB 4x4 block types (row group rg <= column group cg over
+    # Y = Theta, Z = [Theta | xdot]), 16 FMA = 32 flop each per row
+    rg, cg = (F + 3) // 4, (F + S + 3) // 4
+    nb4 = rg * cg - rg * (rg - 1) // 2
+    mfma_flop = nb4 * 32.0 * rows
     roll_bytes = T * N * S * 4 + N * S * 4 + T * ((N + 31) // 32) * 4
     gram_bytes = T * N * S * 4 + T * ((N + 31) // 32) * 4
     out = {
@@ -332,7 +331,7 @@ def c3_main(args):
                                f"(S-state Gram on f64 MFMA + STLSQ per state) + RK4 counterfactual rollout",
                    "patients": N, "T": T, "states": S, "library_terms": F,
                    "support_equals_truth": bool(torch.equal(mask != 0, truth != 0))},
-        "roofline": {"kernel": "gram_ms_kernel", "bound": "mfma", "achieved": gflop / (gram_ms_t * 1e-3) / 1e12,
+        "roofline": {"kernel": "gram_ms4_kernel", "bound": "mfma", "achieved": gflop / (gram_ms_t * 1e-3) / 1e12,
                      "peak": 78.6, "unit": "TFLOP/s", "frac": gflop / (gram_ms_t * 1e-3) / 1e12 / 78.6,
                      "traffic": None, "avg_launch_ms": gram_ms_t,
                      "issued_mfma_TFLOPs": mfma_flop / (gram_ms_t * 1e-3) / 1e12,
@@ -1074,7 +1073,8 @@ def main():
                 "algorithmic_bytes_per_launch": rb,
                 "avg_launch_ms": roll_ms,
                 "avg_ms_source": "instrumented pass: the timed schedule replayed with HIP timing events around "
-                                 "each rollout launch on its own stream (concurrent with the next step's gram)",
+                                 "each batch of rollout launches on its stream, divided by the batch size "
+                                 "(concurrent with the next batch's discoveries)",
                 "layout": {"time_bits": "time-major x[T,N], 1-bit arm mask [T,N/32], y[T,N]",
                            "time": "time-major x[T,N], int8 arm[T,N], y[T,N]",
                            "patient": "patient-major x[N,T], int8 arm[N,T], y[N,T]"}[roll_layout],
@@ -1084,11 +1084,12 @@ def main():
                            else "gram_kernel (in-launch reduction) + RCCL all_reduce + stlsq_kernel",
                 "timed_region": {"graph": "one step (gram+reduction, STLSQ, rollout) captured in a HIP graph, replayed",
                                  "seq": "eager launches, one stream, strictly sequential",
-                                 "pipeline": "discovery (gram+reduction [+all-reduce] +STLSQ) | rollout on two "
-                                             "streams, triple-buffered coefficients, consecutive steps overlapped"}[mode],
-                "avg_ms_source": "instrumented pass: HIP timing events around each step's whole discovery (memset "
-                                 "node, gram with its in-launch reduction, STLSQ) on its stream, concurrent with the "
-                                 "previous step's rollout" if mode == "pipeline"
+                                 "pipeline": "discovery stream (gram+in-launch reduction [+all-reduce] +STLSQ) | two "
+                                             "rollout streams taking alternate batches of 4 steps, one event per "
+                                             "batch per stream, 24 coefficient buffers"}[mode],
+                "avg_ms_source": "instrumented pass: HIP timing events around each batch's discoveries (gram with its "
+                                 "in-launch reduction, STLSQ) on their stream, divided by the batch size, "
+                                 "concurrent with the previous batch's rollouts" if mode == "pipeline"
                                  else "instrumented pass: HIP timing events around discovery",
                 "avg_ms": disc_ms,
                 "algorithmic_bytes": gram_bytes(N, T),
