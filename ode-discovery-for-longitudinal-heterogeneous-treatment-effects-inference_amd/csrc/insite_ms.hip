@@ -25,6 +25,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "insite_common.h"
@@ -450,6 +451,12 @@ struct Ms4 {
 #define INSITE_MS4_SCHED 1
 #endif
 constexpr int kMs4Stride = 29;   // LDS row stride (doubles): odd, stores conflict-free, 2-way on the reads
+#ifndef INSITE_MS4_ABL_NOMFMA
+#define INSITE_MS4_ABL_NOMFMA 0
+#endif
+#ifndef INSITE_MS4_ABL_NOEMIT
+#define INSITE_MS4_ABL_NOEMIT 0
+#endif
 #ifndef INSITE_MS4_RING
 #define INSITE_MS4_RING 12
 #endif
@@ -495,22 +502,207 @@ __device__ __forceinline__ void ms_emit4(double* __restrict__ wrow, const double
     for (int rg = 0; rg < M4::RG; ++rg)
 #pragma unroll
       for (int cg = rg; cg < M4::CG; ++cg, ++t)
+#if INSITE_MS4_ABL_NOMFMA  // profiling-only ablation (timing without the matrix work; results wrong)
+        if (rg == 0) acc[t] += v[r & 1][cg];
+#else
         acc[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(v[r & 1][rg], v[r & 1][cg], acc[t], 0, 0, 0);
+#endif
   }
 }
+
+// ---- staged-factor form (default): the library products are formed by the READING lanes ----
+// The full-row form above writes F + S doubles per row to LDS and every one is read back once: LDS stores
+// are the expensive direction (ds_write_b64 ~85 B/clk/CU against ~256 B/clk for ds_read_b64), and the
+// stores plus the 27 per-row column selects were a third of the kernel (tools/g_c3var.sh ablations).
+// Here each lane stages only the NPURE = NZ + 1 + S "pure" values of its row,
+//   [z_0 = valid, z_1 .. z_NZ, xdot_0 .. xdot_{S-1}]            (12 doubles for C3 instead of 27),
+// and the MFMA operand of a lane (row R, column slot i of column group g) is read back as
+//   pure group:    P[R][4 p + i]                  (consecutive positions: one read)
+//   product group: P[R][posA(g, i)] * P[R][posB(g, i)]   (two reads + one multiply, pysindy product order)
+// Column groups: the pure groups that hold a library column (z_0 .. z_NZ reach into them), then the
+// product groups, then the xdot-only pure groups (Z side only).  Blocks (rg, cg >= rg) over that order
+// cover every needed pair once (a xdot slot that falls in a Y-side group is read as a row, the pair
+// written to B through the map below).  Products are exact in f64 (f32 factors); pad slots duplicate a
+// real slot and are dropped by the map.
+// LDS banking (stride 13, odd): in pass r the 32 lanes of a half-wave read rows {32 h + 4 m + r : m < 8},
+// whose bank offsets 13 (4 m) mod 32 are distinct multiples of 4, so a read is conflict-free whenever the
+// distinct positions one instruction touches differ mod 4 (true for the C3 layout; same-position lanes
+// of a quad broadcast).  Stores: 16 consecutive lanes x stride 13 cover all 16 bank pairs.
+template <int S, int NZ, bool INTER>
+struct Ms4Z {
+  static constexpr int F = PolyCols<NZ, INTER>::F;
+  static constexpr int NPURE = NZ + 1 + S;
+  static constexpr int NPROD = F - (NZ + 1);
+  static constexpr int PG = (NPURE + 3) / 4;    // pure groups
+  static constexpr int PY = NZ / 4 + 1;         // pure groups holding a library column
+  static constexpr int QG = (NPROD + 3) / 4;    // product groups
+  static constexpr int RG = PY + QG;            // Y side
+  static constexpr int CG = PG + QG;            // Z side
+  static constexpr int NB = RG * CG - RG * (RG - 1) / 2;
+  static constexpr int STRIDE = (4 * PG) | 1;   // odd, >= every pure position
+  static_assert(4 * CG <= kMsMaxF, "column map");
+  int pos_a[CG][4], pos_b[CG][4];  // staged positions of the factors (pure groups: pos_b unused)
+  int col[4 * CG];                 // logical column of slot 4 g + i: 0..F-1 library, F..F+S-1 xdot, -1 pad
+  bool prod[CG];
+  __host__ __device__ constexpr Ms4Z() : pos_a(), pos_b(), col(), prod() {
+    constexpr PolyCols<NZ, INTER> pc{};
+    // pure position -> logical column: z_0 .. z_NZ are library columns 0 .. NZ, xdot_s is F + s
+    auto pure_col = [](int p) { return p <= NZ ? p : (p < NPURE ? F + (p - NZ - 1) : -1); };
+    for (int g = 0; g < CG; ++g) {
+      const bool is_prod = g >= PY && g < PY + QG;
+      prod[g] = is_prod;
+      const int pgi = g < PY ? g : g - QG;  // pure group index
+      for (int i = 0; i < 4; ++i) {
+        if (is_prod) {
+          const int qi = 4 * (g - PY) + i;
+          const int j = qi < NPROD ? NZ + 1 + qi : NZ + 1 + 4 * (g - PY);  // pad: the group's first product
+          pos_a[g][i] = pc.ci[j];
+          pos_b[g][i] = pc.ck[j];
+          col[4 * g + i] = qi < NPROD ? j : -1;
+        } else {
+          const int p = 4 * pgi + i;
+          pos_a[g][i] = p;
+          pos_b[g][i] = p;
+          col[4 * g + i] = pure_col(p);
+        }
+      }
+    }
+  }
+};
+
+// Per-lane LDS read pointers of the staged-factor form (row R0(lane) of pass 0; pass r adds r rows).
+template <int QG>
+struct Ms4ZPtr {
+  const double* pure;    // &P[R0][i]
+  const double* qa[QG];  // &P[R0][pos_a(g, i)]
+  const double* qb[QG];
+};
+
+template <int S, int NZ, bool INTER>
+__device__ __forceinline__ Ms4ZPtr<Ms4Z<S, NZ, INTER>::QG> ms4z_ptrs(const double* wbase, int lane) {
+  using LZ = Ms4Z<S, NZ, INTER>;
+  constexpr LZ lz{};
+  const int k = lane >> 4, b = (lane >> 2) & 3, i = lane & 3;
+  const int r0 = 32 * (k >> 1) + 4 * (4 * (k & 1) + b);
+  const double* row = wbase + r0 * LZ::STRIDE;
+  Ms4ZPtr<LZ::QG> p;
+  p.pure = row + i;
+#pragma unroll
+  for (int g = 0; g < LZ::QG; ++g) {
+    int a = lz.pos_a[LZ::PY + g][0], bb = lz.pos_b[LZ::PY + g][0];
+#pragma unroll
+    for (int ii = 1; ii < 4; ++ii) {
+      if (i == ii) {
+        a = lz.pos_a[LZ::PY + g][ii];
+        bb = lz.pos_b[LZ::PY + g][ii];
+      }
+    }
+    p.qa[g] = row + a;
+    p.qb[g] = row + bb;
+  }
+  return p;
+}
+
+template <int S, int NZ, bool INTER>
+__device__ __forceinline__ void ms_emit4z(double* __restrict__ wrow, const Ms4ZPtr<Ms4Z<S, NZ, INTER>::QG>& pp,
+                                          bool valid, const double (&z)[NZ + 1], const double (&xd)[S],
+                                          double (&acc)[Ms4Z<S, NZ, INTER>::NB]) {
+  using LZ = Ms4Z<S, NZ, INTER>;
+#if INSITE_MS4Z_SYNC
+  wave_lds_sync();
+#else
+  // LDS executes one wave's DS instructions in issue order, so these stores land after the previous
+  // row's reads and before the reads below; only the compiler has to keep the order
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+#endif
+  wrow[0] = valid ? 1.0 : 0.0;
+#pragma unroll
+  for (int s = 1; s <= NZ; ++s) wrow[s] = valid ? z[s] : 0.0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) wrow[NZ + 1 + s] = valid ? xd[s] : 0.0;
+#pragma unroll
+  for (int p = LZ::NPURE; p < 4 * LZ::PG; ++p) wrow[p] = 0.0;
+#if INSITE_MS4Z_SYNC
+  wave_lds_sync();
+#else
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+#endif
+  // operands of pass r + 1 are read before pass r's MFMAs issue (two sets live)
+  double ra[2][LZ::CG], rb[2][LZ::QG];
+  auto fetch = [&](int r, int slot) {
+#pragma unroll
+    for (int g = 0; g < LZ::CG; ++g) {
+      if (g >= LZ::PY && g < LZ::PY + LZ::QG) {
+        ra[slot][g] = pp.qa[g - LZ::PY][r * LZ::STRIDE];
+        rb[slot][g - LZ::PY] = pp.qb[g - LZ::PY][r * LZ::STRIDE];
+      } else {
+        const int pgi = g < LZ::PY ? g : g - LZ::QG;
+        ra[slot][g] = pp.pure[4 * pgi + r * LZ::STRIDE];
+      }
+    }
+  };
+  fetch(0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#if INSITE_MS4_SCHED
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    if (r < 3) fetch(r + 1, (r + 1) & 1);
+    double v[LZ::CG];
+#pragma unroll
+    for (int g = 0; g < LZ::CG; ++g)
+      v[g] = (g >= LZ::PY && g < LZ::PY + LZ::QG) ? ra[r & 1][g] * rb[r & 1][g - LZ::PY] : ra[r & 1][g];
+    int t = 0;
+#pragma unroll
+    for (int rg = 0; rg < LZ::RG; ++rg)
+#pragma unroll
+      for (int cg = rg; cg < LZ::CG; ++cg, ++t)
+#if INSITE_MS4_ABL_NOMFMA
+        if (rg == 0) acc[t] += v[cg];
+#else
+        acc[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(v[rg], v[cg], acc[t], 0, 0, 0);
+#endif
+  }
+}
+
+// The full-row form's geometry in the same vocabulary (column map = identity over [Theta | xdot]).
+template <int S, int NZ, bool INTER>
+struct Ms4Full {
+  static constexpr int F = PolyCols<NZ, INTER>::F;
+  using M4 = Ms4<S, F>;
+  static constexpr int RG = M4::RG, CG = M4::CG, NB = M4::NB, STRIDE = kMs4Stride;
+  int col[4 * CG];
+  __host__ __device__ constexpr Ms4Full() : col() {
+    for (int j = 0; j < 4 * CG; ++j) col[j] = j < F + S ? j : -1;
+  }
+};
+
+#ifndef INSITE_MS4_FULLROW
+#define INSITE_MS4_FULLROW 0
+#endif
+#ifndef INSITE_MS4Z_SYNC
+#define INSITE_MS4Z_SYNC 0
+#endif
+template <int S, int NZ, bool INTER>
+using Ms4Layout = typename std::conditional<INSITE_MS4_FULLROW != 0, Ms4Full<S, NZ, INTER>, Ms4Z<S, NZ, INTER>>::type;
 
 template <int S, int NIN, bool INTER>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_MS_WPE)))
 gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint32_t* __restrict__ abits,
                 int64_t lda, const int32_t* __restrict__ rows, int64_t N, GramW w, double* __restrict__ partial) {
   constexpr int NZ = S + NIN;
-  constexpr int F = PolyCols<NZ, INTER>::F;
-  using M4 = Ms4<S, F>;
-  __shared__ double stage[kWavesPerBlock * kWave * kMs4Stride];
+  using M4 = Ms4Layout<S, NZ, INTER>;
+  static_assert(M4::NB * 16 * kWavesPerBlock <= kWavesPerBlock * kWave * M4::STRIDE, "block reduction fits the stage");
+  __shared__ double stage[kWavesPerBlock * kWave * M4::STRIDE];
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  double* wbase = stage + wid * kWave * kMs4Stride;
-  double* wrow = wbase + lane * kMs4Stride;
+  double* wbase = stage + wid * kWave * M4::STRIDE;
+  double* wrow = wbase + lane * M4::STRIDE;
+#if !INSITE_MS4_FULLROW
+  const auto zptr = ms4z_ptrs<S, NZ, INTER>(wbase, lane);
+#endif
   double acc[M4::NB];
 #pragma unroll
   for (int q = 0; q < M4::NB; ++q) acc[q] = 0.0;
@@ -571,7 +763,18 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
               }
 #pragma unroll
               for (int q = 0; q < NIN; ++q) z[1 + S + q] = (double)((wcur >> (r & 31)) & 1u);
+#if INSITE_MS4_ABL_NOEMIT  // profiling-only ablation (ring + derivative only; results wrong)
+              double sink = 0.0;
+#pragma unroll
+              for (int s = 0; s < S; ++s) sink += z[1 + s] * xd[s];
+              acc[0] += (t <= L - 1) ? sink + z[NZ] : 0.0;
+#else
+#if INSITE_MS4_FULLROW
               ms_emit4<S, NZ, INTER>(wrow, wbase, t <= L - 1, z, xd, acc, lane);
+#else
+              ms_emit4z<S, NZ, INTER>(wrow, zptr, t <= L - 1, z, xd, acc);
+#endif
+#endif
             }
           }
         }
@@ -627,7 +830,11 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
         }
 #pragma unroll
         for (int qq = 0; qq < NIN; ++qq) z[1 + S + qq] = (L > 0 && step < n_steps) ? input_bit(abits, lda, step, pc) : 0.0;
+#if INSITE_MS4_FULLROW
         ms_emit4<S, NZ, INTER>(wrow, wbase, L > 0 && valid, z, xd, acc, lane);
+#else
+        ms_emit4z<S, NZ, INTER>(wrow, zptr, L > 0 && valid, z, xd, acc);
+#endif
       }
     }
   }
@@ -654,10 +861,13 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
 }
 
 // Fixed-order reduction of gram_ms4_kernel's block partials and scatter into G [F, F] and B [F, S]:
-// entry (t, m, n) of block type t = (rg, cg) is (Y row 4 rg + m, Z column 4 cg + n); the Theta-Theta
-// blocks above the diagonal also fill their mirror.
-__global__ void __launch_bounds__(kWave) ms4_finalize(const double* __restrict__ partial, int nblk, int nb, int rgn,
-                                                      int cgn, int F, int S, double* __restrict__ G,
+// entry (t, m, n) of block type t = (rg, cg) pairs Y slot 4 rg + m with Z slot 4 cg + n; the slot -> column
+// map (library 0..F-1, xdot F..F+S-1, -1 pad) places it.  Diagonal blocks hold each pair twice: n >= m only.
+struct Ms4Map {
+  int col[kMsMaxF];
+};
+__global__ void __launch_bounds__(kWave) ms4_finalize(const double* __restrict__ partial, int nblk, int nb, int cgn,
+                                                      int F, int S, Ms4Map map, double* __restrict__ G,
                                                       double* __restrict__ B) {
   const int q = blockIdx.x * kWave + threadIdx.x;
   if (q >= nb * 16) return;
@@ -669,14 +879,17 @@ __global__ void __launch_bounds__(kWave) ms4_finalize(const double* __restrict__
     ++rg;
   }
   const int cg = rg + t;
-  const int row = 4 * rg + (q % 16) / 4, col = 4 * cg + q % 4;
-  (void)rgn;
-  if (row >= F) return;
-  if (col < F) {
-    G[(int64_t)row * F + col] = v;
-    if (cg > rg) G[(int64_t)col * F + row] = v;
-  } else if (col < F + S) {
-    B[(int64_t)row * S + (col - F)] = v;
+  const int m = (q % 16) / 4, n = q % 4;
+  if (cg == rg && n < m) return;
+  const int a = map.col[4 * rg + m], b = map.col[4 * cg + n];
+  if (a < 0 || b < 0) return;
+  if (a < F && b < F) {
+    G[(int64_t)a * F + b] = v;
+    G[(int64_t)b * F + a] = v;
+  } else if (a < F) {
+    B[(int64_t)a * S + (b - F)] = v;
+  } else if (b < F) {
+    B[(int64_t)b * S + (a - F)] = v;
   }
 }
 
@@ -1243,16 +1456,18 @@ int32_t insite_gram_ms_f32(const float* x, int64_t ldx, int32_t n_steps, int32_t
   if (st != INSITE_OK) return st;
   ms_finalize<<<(kMsTiles * 256 + kWave - 1) / kWave, kWave, 0, hs>>>(part, grid, n_terms, n_states, G_out, B_out);
 #else
-  int nb = 0, rgn = 0, cgn = 0;
+  int nb = 0, cgn = 0;
+  Ms4Map map{};
   auto geom = [&](auto m4) {
     using M4 = decltype(m4);
+    static_assert(M4::NB * 16 <= kMsTiles * 256, "workspace holds the block partials");
     nb = M4::NB;
-    rgn = M4::RG;
     cgn = M4::CG;
+    for (int j = 0; j < kMsMaxF; ++j) map.col[j] = j < 4 * M4::CG ? m4.col[j] : -1;
   };
-  if (nin == 1) geom(Ms4<5, PolyCols<6, true>::F>{});
-  else if (inter == 1) geom(Ms4<5, PolyCols<5, true>::F>{});
-  else geom(Ms4<5, PolyCols<5, false>::F>{});
+  if (nin == 1) geom(Ms4Layout<5, 6, true>{});
+  else if (inter == 1) geom(Ms4Layout<5, 5, true>{});
+  else geom(Ms4Layout<5, 5, false>{});
   if (n_patients == 0 || n_steps < 5) {
     if (hipMemsetAsync(part, 0, (size_t)grid * nb * 16 * sizeof(double), hs) != hipSuccess) return INSITE_E_HIP;
   } else if (nin == 1) {
@@ -1264,7 +1479,7 @@ int32_t insite_gram_ms_f32(const float* x, int64_t ldx, int32_t n_steps, int32_t
   }
   int32_t st = launch_status();
   if (st != INSITE_OK) return st;
-  ms4_finalize<<<(nb * 16 + kWave - 1) / kWave, kWave, 0, hs>>>(part, grid, nb, rgn, cgn, n_terms, n_states, G_out,
+  ms4_finalize<<<(nb * 16 + kWave - 1) / kWave, kWave, 0, hs>>>(part, grid, nb, cgn, n_terms, n_states, map, G_out,
                                                                 B_out);
 #endif
   return launch_status();

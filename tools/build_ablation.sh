@@ -14,6 +14,10 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     MSV1) NAME=$v build -DINSITE_MS_V1 ;;
     MS4S0) NAME=$v build -DINSITE_MS4_SCHED=0 ;;
     MS4R10) NAME=$v build -DINSITE_MS4_RING=10 ;;
+    MS4NOMFMA) NAME=$v build -DINSITE_MS4_ABL_NOMFMA=1 ;;
+    MS4FULL) NAME=$v build -DINSITE_MS4_FULLROW=1 ;;
+    MS4ZSYNC) NAME=$v build -DINSITE_MS4Z_SYNC=1 ;;
+    MS4NOEMIT) NAME=$v build -DINSITE_MS4_ABL_NOEMIT=1 ;;
     RKW8W8) NAME=$v build -DINSITE_RK45_WIN=8 -DINSITE_RK45_WPE=8 ;;
     RKW16W5) NAME=$v build -DINSITE_RK45_WIN=16 -DINSITE_RK45_WPE=5 ;;
     SEGKC8) NAME=$v build -DINSITE_SEG_KC=8 -DINSITE_SEG_WPE=3 ;;
