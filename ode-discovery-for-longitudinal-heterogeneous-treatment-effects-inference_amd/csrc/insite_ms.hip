@@ -457,6 +457,15 @@ constexpr int kMs4Stride = 29;   // LDS row stride (doubles): odd, stores confli
 #ifndef INSITE_MS4_ABL_NOEMIT
 #define INSITE_MS4_ABL_NOEMIT 0
 #endif
+#ifndef INSITE_MS4Z_SYNC
+#define INSITE_MS4Z_SYNC 1
+#endif
+#ifndef INSITE_MS4Z_MASKSEL
+#define INSITE_MS4Z_MASKSEL 0
+#endif
+#ifndef INSITE_MS4_PRIO
+#define INSITE_MS4_PRIO 0
+#endif
 #ifndef INSITE_MS4_RING
 #define INSITE_MS4_RING 12
 #endif
@@ -603,19 +612,21 @@ __device__ __forceinline__ Ms4ZPtr<Ms4Z<S, NZ, INTER>::QG> ms4z_ptrs(const doubl
   return p;
 }
 
-template <int S, int NZ, bool INTER>
-__device__ __forceinline__ void ms_emit4z(double* __restrict__ wrow, const Ms4ZPtr<Ms4Z<S, NZ, INTER>::QG>& pp,
-                                          bool valid, const double (&z)[NZ + 1], const double (&xd)[S],
-                                          double (&acc)[Ms4Z<S, NZ, INTER>::NB]) {
-  using LZ = Ms4Z<S, NZ, INTER>;
+__device__ __forceinline__ void ms4z_sync() {
 #if INSITE_MS4Z_SYNC
   wave_lds_sync();
 #else
-  // LDS executes one wave's DS instructions in issue order, so these stores land after the previous
-  // row's reads and before the reads below; only the compiler has to keep the order
+  // LDS executes one wave's DS instructions in issue order; only the compiler has to keep the order
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
 #endif
+}
+
+// Stage one row's pure values: masked (invalid rows staged as zeros) ...
+template <int S, int NZ, bool INTER>
+__device__ __forceinline__ void ms4z_stage_masked(double* __restrict__ wrow, bool valid, const double (&z)[NZ + 1],
+                                                  const double (&xd)[S]) {
+  using LZ = Ms4Z<S, NZ, INTER>;
   wrow[0] = valid ? 1.0 : 0.0;
 #pragma unroll
   for (int s = 1; s <= NZ; ++s) wrow[s] = valid ? z[s] : 0.0;
@@ -623,12 +634,30 @@ __device__ __forceinline__ void ms_emit4z(double* __restrict__ wrow, const Ms4ZP
   for (int s = 0; s < S; ++s) wrow[NZ + 1 + s] = valid ? xd[s] : 0.0;
 #pragma unroll
   for (int p = LZ::NPURE; p < 4 * LZ::PG; ++p) wrow[p] = 0.0;
-#if INSITE_MS4Z_SYNC
-  wave_lds_sync();
-#else
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");
-#endif
+}
+// ... or as they are (the caller routes invalid rows elsewhere)
+template <int S, int NZ, bool INTER>
+__device__ __forceinline__ void ms4z_stage(double* __restrict__ wp, const double (&z)[NZ + 1], const double (&xd)[S]) {
+  using LZ = Ms4Z<S, NZ, INTER>;
+  wp[0] = 1.0;
+#pragma unroll
+  for (int s = 1; s <= NZ; ++s) wp[s] = z[s];
+#pragma unroll
+  for (int s = 0; s < S; ++s) wp[NZ + 1 + s] = xd[s];
+#pragma unroll
+  for (int p = LZ::NPURE; p < 4 * LZ::PG; ++p) wp[p] = 0.0;
+}
+template <int S, int NZ, bool INTER>
+__device__ __forceinline__ void ms4z_zero(double* __restrict__ wrow) {
+#pragma unroll
+  for (int p = 0; p < 4 * Ms4Z<S, NZ, INTER>::PG; ++p) wrow[p] = 0.0;
+}
+
+// The 4 passes over the 64 staged rows: read / form the operands, 4 x 4 x 4 f64 blocks.
+template <int S, int NZ, bool INTER>
+__device__ __forceinline__ void ms4z_passes(const Ms4ZPtr<Ms4Z<S, NZ, INTER>::QG>& pp,
+                                            double (&acc)[Ms4Z<S, NZ, INTER>::NB]) {
+  using LZ = Ms4Z<S, NZ, INTER>;
   // operands of pass r + 1 are read before pass r's MFMAs issue (two sets live)
   double ra[2][LZ::CG], rb[2][LZ::QG];
   auto fetch = [&](int r, int slot) {
@@ -667,6 +696,16 @@ __device__ __forceinline__ void ms_emit4z(double* __restrict__ wrow, const Ms4ZP
   }
 }
 
+template <int S, int NZ, bool INTER>
+__device__ __forceinline__ void ms_emit4z(double* __restrict__ wrow, const Ms4ZPtr<Ms4Z<S, NZ, INTER>::QG>& pp,
+                                          bool valid, const double (&z)[NZ + 1], const double (&xd)[S],
+                                          double (&acc)[Ms4Z<S, NZ, INTER>::NB]) {
+  ms4z_sync();
+  ms4z_stage_masked<S, NZ, INTER>(wrow, valid, z, xd);
+  ms4z_sync();
+  ms4z_passes<S, NZ, INTER>(pp, acc);
+}
+
 // The full-row form's geometry in the same vocabulary (column map = identity over [Theta | xdot]).
 template <int S, int NZ, bool INTER>
 struct Ms4Full {
@@ -682,23 +721,26 @@ struct Ms4Full {
 #ifndef INSITE_MS4_FULLROW
 #define INSITE_MS4_FULLROW 0
 #endif
-#ifndef INSITE_MS4Z_SYNC
-#define INSITE_MS4Z_SYNC 0
-#endif
 template <int S, int NZ, bool INTER>
 using Ms4Layout = typename std::conditional<INSITE_MS4_FULLROW != 0, Ms4Full<S, NZ, INTER>, Ms4Z<S, NZ, INTER>>::type;
 
 template <int S, int NIN, bool INTER>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_MS_WPE)))
 gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uint32_t* __restrict__ abits,
-                int64_t lda, const int32_t* __restrict__ rows, int64_t N, GramW w, double* __restrict__ partial) {
+                int64_t lda, const int32_t* __restrict__ rows, int64_t N, GramW w, double* __restrict__ partial,
+                int nchunk) {
   constexpr int NZ = S + NIN;
   using M4 = Ms4Layout<S, NZ, INTER>;
-  static_assert(M4::NB * 16 * kWavesPerBlock <= kWavesPerBlock * kWave * M4::STRIDE, "block reduction fits the stage");
-  __shared__ double stage[kWavesPerBlock * kWave * M4::STRIDE];
+  // per wave: 64 staged rows, then (staged-factor form) 64 trash rows that invalid interior rows go to
+  constexpr int kWaveStage = (INSITE_MS4_FULLROW ? 1 : 2) * kWave * M4::STRIDE;
+  static_assert(M4::NB * 16 * kWavesPerBlock <= kWavesPerBlock * kWaveStage, "block reduction fits the stage");
+  __shared__ double stage[kWavesPerBlock * kWaveStage];
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  double* wbase = stage + wid * kWave * M4::STRIDE;
+#if INSITE_MS4_PRIO
+  if (blockIdx.x >= gridDim.x / 2) __builtin_amdgcn_s_setprio(1);
+#endif
+  double* wbase = stage + wid * kWaveStage;
   double* wrow = wbase + lane * M4::STRIDE;
 #if !INSITE_MS4_FULLROW
   const auto zptr = ms4z_ptrs<S, NZ, INTER>(wbase, lane);
@@ -711,8 +753,12 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
   const int64_t kstride = (int64_t)S * ldx; // between steps
   const double c1 = kMsC1 * w.inv_dt, c2 = kMsC2 * w.inv_dt, c3 = kMsC3 * w.inv_dt, c4 = kMsC4 * w.inv_dt;
 
-  for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid; tile < n_tiles;
-       tile += (int64_t)gridDim.x * kWavesPerBlock) {
+  // work unit = (tile, chunk): the interior steps of a tile are cut into nchunk consecutive ranges so the
+  // units divide evenly over the resident waves (ms4_chunks); chunk 0 also takes the tile's edge rows
+  for (int64_t unit = (int64_t)blockIdx.x * kWavesPerBlock + wid; unit < n_tiles * nchunk;
+       unit += (int64_t)gridDim.x * kWavesPerBlock) {
+    const int64_t tile = unit / nchunk;
+    const int chunk = (int)(unit - tile * nchunk);
     const int64_t p0 = tile * kWave;
     const int64_t p = p0 + lane;
     const bool in = p < N;
@@ -721,11 +767,18 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
     if (L > n_steps) L = n_steps;
     if (!in || L < 5) L = 0;
     const int Lmax = wave_max_i(L);
+    const int tz = L > 8 ? L : 8;  // first interior step whose row lies past the lane's end
     const float* xp = x + pc;
     auto ld = [&](int k, int s) -> double { return (double)xp[(int64_t)k * kstride + s * sstride]; };
 
     // ---------------- interior rows (L >= 9): r = 4 .. L-5 at steps t = 8 .. L-1 ----------------
-    if (Lmax >= 9) {
+    // this chunk emits steps [ea, eb) and loads from ea - 8 (the 9-sample window of its first row)
+    const int n_emit = Lmax - 8;
+    const int ea = 8 + (int)((int64_t)n_emit * chunk / nchunk);
+    const int eb = 8 + (int)((int64_t)n_emit * (chunk + 1) / nchunk);
+    const int ts = ea - 8;
+    const int tzc = tz > ea ? tz : ea;  // a lane already past its end zeroes its (stale) row at the first emit
+    if (Lmax >= 9 && eb > ea) {
       float xr[kMs4Ring][S];
       auto word = [&](int g) -> unsigned {  // treatment bits of rows [32 g, 32 g + 32), half-wave transpose
         if (!abits) return 0u;
@@ -738,19 +791,19 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
 #pragma unroll
       for (int t = 0; t < kMs4Ring - 9; ++t)
 #pragma unroll
-        for (int s = 0; s < S; ++s) xr[t][s] = xp[(int64_t)t * kstride + s * sstride];
-      unsigned wcur = word(0);
-      for (int t0 = 0; t0 < Lmax; t0 += kMs4Ring) {
+        for (int s = 0; s < S; ++s) xr[t][s] = xp[(int64_t)(ts + t) * kstride + s * sstride];
+      unsigned wcur = word((ea - 4) >> 5);
+      for (int t0 = ts; t0 < eb; t0 += kMs4Ring) {
 #pragma unroll
         for (int i = 0; i < kMs4Ring; ++i) {
           const int t = t0 + i;
-          if (t < Lmax) {  // uniform
+          if (t < eb) {  // uniform
             // x[t + PF] into the slot of x[t - 9 + ...] (no longer needed): its wait falls PF steps later
             constexpr int PF = kMs4Ring - 9;
             const int tn = t + PF < n_steps ? t + PF : n_steps - 1;
 #pragma unroll
             for (int s = 0; s < S; ++s) xr[(i + PF) % kMs4Ring][s] = xp[(int64_t)tn * kstride + s * sstride];
-            if (t >= 8) {  // row r = t - 4: raw x[r], xdot from x[r-4 .. r+4] (slots i-8 .. i)
+            if (t >= ea) {  // row r = t - 4: raw x[r], xdot from x[r-4 .. r+4] (slots i-8 .. i)
               const int r = t - 4;
               if ((r & 31) == 0) wcur = word(r >> 5);
               double z[NZ + 1], xd[S];
@@ -771,8 +824,16 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
 #else
 #if INSITE_MS4_FULLROW
               ms_emit4<S, NZ, INTER>(wrow, wbase, t <= L - 1, z, xd, acc, lane);
-#else
+#elif INSITE_MS4Z_MASKSEL
               ms_emit4z<S, NZ, INTER>(wrow, zptr, t <= L - 1, z, xd, acc);
+#else
+              // rows past a lane's end go to its trash row; its staged row is zeroed once, at the first
+              // such row (t == tz), and stays zero for the rest of the interior
+              ms4z_sync();
+              ms4z_stage<S, NZ, INTER>(t <= L - 1 ? wrow : wrow + kWave * M4::STRIDE, z, xd);
+              if (t == tzc) ms4z_zero<S, NZ, INTER>(wrow);
+              ms4z_sync();
+              ms4z_passes<S, NZ, INTER>(zptr, acc);
 #endif
 #endif
             }
@@ -784,7 +845,7 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
     // ---------------- edge rows: 0..3 and L-4..L-1 (all rows when 5 <= L < 8) ----------------
     // one row at a time (its window re-read per row from the cache: 8 of ~500 rows per patient), so the
     // edge path holds one 8-sample window instead of 4 rows x S states of values and derivatives
-    if (Lmax >= 5) {
+    if (Lmax >= 5 && chunk == 0) {
       for (int j = 0; j < 8; ++j) {  // window row: part j / 4, position j % 4 within the part
         const int base = j < 4 ? 0 : (L >= 8 ? L - 8 : 0);
         const bool valid = (L >= 8) || (j < L);
@@ -1154,6 +1215,27 @@ int ms_library_kind(const int8_t* exps, int F, int S, int NIN) {
   return -1;
 }
 
+// Interior chunks per tile for gram_ms4_kernel: the count (<= 8, >= 48 emitted steps per chunk) whose
+// units fill the last round of resident waves best (15625 tiles on 2048 waves: 7.6 tiles per wave as whole
+// tiles, 30.5 of 31 rounds in quarter tiles).
+inline int ms4_chunks(int64_t N, int n_steps, int grid) {
+  const int64_t tiles = (N + kWave - 1) / kWave;
+  const int64_t waves = (int64_t)grid * kWavesPerBlock;
+  int best = 1;
+  double best_eff = 0.0;
+  for (int c = 1; c <= 8; ++c) {
+    if (c > 1 && (n_steps - 8) / c < 48) break;
+    const int64_t units = tiles * c;
+    const int64_t rounds = (units + waves - 1) / waves;
+    const double eff = (double)units / (double)(rounds * waves) - 0.004 * (c - 1);  // ~1 exposed load latency per chunk
+    if (eff > best_eff + 1e-9) {
+      best_eff = eff;
+      best = c;
+    }
+  }
+  return best;
+}
+
 inline int ms_grid(int64_t N) {
   int64_t tiles = (N + kWave - 1) / kWave;
   int64_t g = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -1465,17 +1547,25 @@ int32_t insite_gram_ms_f32(const float* x, int64_t ldx, int32_t n_steps, int32_t
     cgn = M4::CG;
     for (int j = 0; j < kMsMaxF; ++j) map.col[j] = j < 4 * M4::CG ? m4.col[j] : -1;
   };
+#ifdef INSITE_MS4_NCHUNK
+  const int nchunk = INSITE_MS4_NCHUNK;
+#else
+  const int nchunk = ms4_chunks(n_patients, n_steps, grid);
+#endif
   if (nin == 1) geom(Ms4Layout<5, 6, true>{});
   else if (inter == 1) geom(Ms4Layout<5, 5, true>{});
   else geom(Ms4Layout<5, 5, false>{});
   if (n_patients == 0 || n_steps < 5) {
     if (hipMemsetAsync(part, 0, (size_t)grid * nb * 16 * sizeof(double), hs) != hipSuccess) return INSITE_E_HIP;
   } else if (nin == 1) {
-    gram_ms4_kernel<5, 1, true><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, inp_bits, ld_bits, rows, n_patients, w, part);
+    gram_ms4_kernel<5, 1, true><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, inp_bits, ld_bits, rows, n_patients, w, part,
+                                                              nchunk);
   } else if (inter == 1) {
-    gram_ms4_kernel<5, 0, true><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, nullptr, 0, rows, n_patients, w, part);
+    gram_ms4_kernel<5, 0, true><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, nullptr, 0, rows, n_patients, w, part,
+                                                              nchunk);
   } else {
-    gram_ms4_kernel<5, 0, false><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, nullptr, 0, rows, n_patients, w, part);
+    gram_ms4_kernel<5, 0, false><<<grid, kBlock, 0, hs>>>(x, ldx, n_steps, nullptr, 0, rows, n_patients, w, part,
+                                                              nchunk);
   }
   int32_t st = launch_status();
   if (st != INSITE_OK) return st;

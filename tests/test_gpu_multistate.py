@@ -32,7 +32,7 @@ def _lib(n_inputs=1, inter=True):
 
 
 @pytest.mark.parametrize("n_inputs,inter", [(1, True), (0, True), (0, False)])
-@pytest.mark.parametrize("N,T", [(200, 48), (67, 130)])
+@pytest.mark.parametrize("N,T", [(200, 48), (67, 130), (130, 300)])  # (67, 130) / (130, 300): 2 / 4 time chunks per tile
 def test_gram_ms_matches_oracle(dev, n_inputs, inter, N, T):
     from insite_amd import multistate as MS
     x, a = M.c3_cohort(N, T, seed=11)
