@@ -181,13 +181,24 @@ struct GramOut {
   double* G;
   double* b;
   int n_arms;
+  // STLSQ fused into the tail (gram_kernel STF > 0): the last block solves the n_arms systems
+  double* coef;
+  int8_t* mask;
+  int32_t* iters;
+  StlsqParams sp;
 };
+
+template <int F>
+__device__ int stlsq_solve(const double (&g)[F][F], const double (&rhs)[F], double thr, double alpha,
+                           int max_iter, int unbias, double (&c)[F], unsigned& sup,
+                           unsigned init = (1u << F) - 1u);
 
 __device__ __forceinline__ void tail_store(double* p, double v) {  // sc1 (write-through) 8-byte store
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __double_as_longlong(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
+template <int STF>
 __device__ __forceinline__ void gram_tail(double* __restrict__ part, int n_ent, unsigned* __restrict__ cnt,
                                           const LibDesc& lib, const GramOut& o, double* red) {
   int* flag = reinterpret_cast<int*>(red + kTailMaxEnt);  // "I am last", through the kernel's LDS array
@@ -232,6 +243,8 @@ __device__ __forceinline__ void gram_tail(double* __restrict__ part, int n_ent, 
   }
   __syncthreads();
   const int64_t F = lib.F;
+  double* dense = red + kTailMaxEnt + 8;  // STF: [a][F x F | F] copy in LDS for the fused STLSQ
+  constexpr int kDense = STF * STF + STF;
   for (int idx = threadIdx.x; idx < n_ent; idx += kBlock) {
     const int a = idx / lib.nE, e = idx - a * lib.nE;
     const int i = lib.ei[e], k = lib.ek[e];
@@ -239,11 +252,41 @@ __device__ __forceinline__ void gram_tail(double* __restrict__ part, int n_ent, 
     if (k >= 0) {
       o.G[(a * F + i) * F + k] = v;
       o.G[(a * F + k) * F + i] = v;
+      if constexpr (STF > 0) {
+        dense[a * kDense + i * STF + k] = v;
+        dense[a * kDense + k * STF + i] = v;
+      }
     } else {
       o.b[a * F + i] = v;
+      if constexpr (STF > 0) dense[a * kDense + STF * STF + i] = v;
+    }
+  }
+  if constexpr (STF > 0) {  // one thread per arm, register-resident STLSQ (reference sindy.py:190-192)
+    __syncthreads();
+    const int a = (int)threadIdx.x;
+    if (a < o.n_arms) {
+      const double* d = dense + a * kDense;
+      double g[STF][STF], rhs[STF], c[STF];
+#pragma unroll
+      for (int i = 0; i < STF; ++i) {
+        rhs[i] = d[STF * STF + i];
+#pragma unroll
+        for (int j = 0; j <= i; ++j) g[i][j] = d[i * STF + j];
+      }
+      unsigned sup = 0u;
+      const int it = stlsq_solve<STF>(g, rhs, o.sp.thr, o.sp.alpha, o.sp.max_iter, o.sp.unbias, c, sup);
+#pragma unroll
+      for (int i = 0; i < STF; ++i) {
+        o.coef[a * STF + i] = c[i];
+        if (o.mask) o.mask[a * STF + i] = (int8_t)((sup >> i) & 1u);
+      }
+      if (o.iters) o.iters[a] = it;
     }
   }
 }
+static_assert(kTailMaxEnt + 8 + INSITE_MAX_ARMS * (INSITE_MAX_TERMS * INSITE_MAX_TERMS + INSITE_MAX_TERMS) <=
+                  kWavesPerBlock * kWave * kGStride,
+              "tail scratch fits the gram kernel's LDS array");
 
 // Lane = patient.  Work item = (64-patient tile, time segment [s*seg, (s+1)*seg)).  Rows are
 // staged [64 x kGT] through LDS (coalesced 16-B loads; the next tile in flight while the current
@@ -260,7 +303,7 @@ __device__ __forceinline__ void gram_tail(double* __restrict__ part, int n_ent, 
 // every lane writes its patient's moments {L, sum xs, sum xs^2, sum xdot, sum xdot xs} to
 // partial[p * 5 ..] (insite_sindy_fit_per_patient_f64).
 // Otherwise the block partials are reduced inside the launch (gram_tail) into G [A, F, F] and b [A, F].
-template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM>
+template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM, int STF = 0>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))  // <= 256 VGPR+AGPR
 gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
             const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, int seg, int n_seg,
@@ -722,7 +765,7 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
     tail_store(partial + (int64_t)blockIdx.x * n_ent + idx, v);
   }
   INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 6);
-  gram_tail(partial, n_ent, cnt, lib, out, smem);
+  gram_tail<STF>(partial, n_ent, cnt, lib, out, smem);
   INSITE_TREAL(blockIdx.x * kWavesPerBlock + wid, 9);
 }
 
@@ -788,8 +831,7 @@ __device__ bool masked_cholesky_solve(const double (&g)[F][F], const double (&rh
 // and the unbias solve.  Returns the iteration count, -1 if a solve was not positive definite.
 template <int F>
 __device__ int stlsq_solve(const double (&g)[F][F], const double (&rhs)[F], double thr, double alpha,
-                           int max_iter, int unbias, double (&c)[F], unsigned& sup,
-                           unsigned init = (1u << F) - 1u) {
+                           int max_iter, int unbias, double (&c)[F], unsigned& sup, unsigned init) {
   // init: initial support (all ones = pysindy BaseOptimizer; a global model's support =
   // LSQIntialMask, pkpd/utils.py:250-253).  The stop rule compares the support size with the
   // initial one (:308) and the pattern with the previous iterate (history_[0] = full lstsq guess).
@@ -2903,9 +2945,9 @@ struct GramLaunch {
   GramOut out;
 };
 
-template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM = false>
+template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM = false, int STF = 0>
 int launch_gram4(hipStream_t st, const GramLaunch& g) {
-  auto kern = gram_kernel<VEC, NARM, SMOOTH, MFMA, TM, MOM>;
+  auto kern = gram_kernel<VEC, NARM, SMOOTH, MFMA, TM, MOM, STF>;
   GramPlan pl = gram_plan(g.N, g.n_steps, resident_waves(kern));
   if constexpr (MOM) {  // one segment per patient: the lane holds the patient's complete moments
     const int64_t tiles = (g.N + kWave - 1) / kWave;
@@ -2924,6 +2966,7 @@ int launch_gram4(hipStream_t st, const GramLaunch& g) {
 
 template <int NARM, bool SMOOTH, bool MFMA>
 int launch_gram3(int mode, hipStream_t st, const GramLaunch& g) {  // mode: 0 PM/8-B, 1 PM/16-B, 2 TM
+  if (mode == 3) return launch_gram4<1, NARM, SMOOTH, MFMA, true, false, 7>(st, g);  // TM + fused F = 7 STLSQ
   if (mode == 2) return launch_gram4<1, NARM, SMOOTH, MFMA, true>(st, g);
   if (mode == 1) return launch_gram4<2, NARM, SMOOTH, MFMA, false>(st, g);
   return launch_gram4<1, NARM, SMOOTH, MFMA, false>(st, g);
@@ -2986,13 +3029,20 @@ int32_t run_discovery(const double* x, int64_t ldx, int32_t layout, int32_t n_st
 #ifdef INSITE_GRAM_MEMSET  // ablation: re-zero gram_tail's counters with a memset node every call
   if (hipMemsetAsync(cnt, 0, kGramWsHeader, hs) != hipSuccess) return INSITE_E_HIP;
 #endif
+  // time-major F = 7 (C2): the STLSQ runs in the gram's last block (no second launch, G / b from LDS)
+#ifndef INSITE_STLSQ_SEPARATE
+  const bool fused = sp.enabled && tm && n_terms == 7;
+#else
+  const bool fused = false;
+#endif
   const GramLaunch g{x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, part, cnt,
-                     GramOut{G_out, b_out, n_arms}};
-  if (na == 1) launch_gram<1>(mode, smooth, hs, g);
-  else if (na == 2) launch_gram<2>(mode, smooth, hs, g);
-  else launch_gram<4>(mode, smooth, hs, g);
+                     GramOut{G_out, b_out, n_arms, coef_out, mask_out, iters_out, sp}};
+  const int lmode = fused ? 3 : mode;
+  if (na == 1) launch_gram<1>(lmode, smooth, hs, g);
+  else if (na == 2) launch_gram<2>(lmode, smooth, hs, g);
+  else launch_gram<4>(lmode, smooth, hs, g);
   st = launch_status();
-  if (st != INSITE_OK || !sp.enabled) return st;
+  if (st != INSITE_OK || !sp.enabled || fused) return st;
   switch (n_terms) {  // one thread per arm, register-resident STLSQ (SINDy.fit: reference sindy.py:190-192)
 #define INSITE_STL_CASE(FF)                                                                             \
   case FF:                                                                                              \

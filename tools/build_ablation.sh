@@ -21,6 +21,7 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     MS4MASKSEL) NAME=$v build -DINSITE_MS4Z_MASKSEL=1 ;;
     MS4PRIO) NAME=$v build -DINSITE_MS4_PRIO=1 ;;
     MS4NC1) NAME=$v build -DINSITE_MS4_NCHUNK=1 ;;
+    STLSEP) NAME=$v build -DINSITE_STLSQ_SEPARATE ;;
     MS4NOEMIT) NAME=$v build -DINSITE_MS4_ABL_NOEMIT=1 ;;
     RKW8W8) NAME=$v build -DINSITE_RK45_WIN=8 -DINSITE_RK45_WPE=8 ;;
     RKW16W5) NAME=$v build -DINSITE_RK45_WIN=16 -DINSITE_RK45_WPE=5 ;;
