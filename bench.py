@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "insite", "f4"],
                     help="c2: BASELINE configs[1], the headline line (default); c3: configs[2], the 5-state fp32 "
                          "system (parity-test configuration, measured separately)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"),
                     help="per-launch HBM bytes from the rocprofv3 PMC passes (profiles/), if present")
     return ap.parse_args()
 
@@ -1080,7 +1080,7 @@ def main():
                            "patient": "patient-major x[N,T], int8 arm[N,T], y[N,T]"}[roll_layout],
             },
             "discovery": {
-                "kernels": "gram_kernel (in-launch reduction to G|b) + stlsq_kernel" if world == 1
+                "kernels": "gram_kernel (in-launch reduction to G|b, STLSQ in its last block)" if world == 1
                            else "gram_kernel (in-launch reduction) + RCCL all_reduce + stlsq_kernel",
                 "timed_region": {"graph": "one step (gram+reduction, STLSQ, rollout) captured in a HIP graph, replayed",
                                  "seq": "eager launches, one stream, strictly sequential",
