@@ -48,9 +48,16 @@ def parse():
     ap.add_argument("--arm-format", default="bits", choices=["bits", "int8"],
                     help="per-step arms of the time-major rollout: 1-bit mask (A <= 2) or int8")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", default="pipeline", choices=["graph", "seq", "pipeline"],
-                    help="pipeline: discovery (gram + in-launch reduction [+ all-reduce] + STLSQ) | rollout on two streams, consecutive steps "
-                         "overlapped (default); seq: eager launches on one stream; graph: the seq step in a HIP graph")
+    ap.add_argument("--mode", default=None, choices=["fused", "graph", "seq", "pipeline"],
+                    help="pipeline (default): discovery (gram + in-launch reduction [+ all-reduce] + STLSQ) | "
+                         "rollout on two streams, consecutive steps overlapped; fused (N = 1): ONE step_kernel launch "
+                         "per step -- the discovery of step i and the rollout of step i-1 in the same launch; seq: "
+                         "eager launches on one stream; graph: the seq step in a HIP graph")
+    ap.add_argument("--no-fused", action="store_true",
+                    help="pipeline mode at N = 1: skip the secondary fused-step measurement")
+    ap.add_argument("--gram-blocks", type=int, default=0,
+                    help="fused mode: blocks of the step kernel's resident round given to the discovery (0 = the "
+                         "library's default split)")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
     ap.add_argument("--isolated", action="store_true",
@@ -793,6 +800,183 @@ def dist_setup():
     return world, rank, dev
 
 
+def fused_run(args, dev, coh, arm_cf):
+    """Time the fused step (insite_fit_rollout_f64: step_kernel) on the C2 cohort.  One launch per step runs
+    the discovery of step i (gram + in-launch reduction + the F = 7 STLSQ in its last block) and, on the
+    other blocks of the same resident round, the rollout of step i-1 with the coefficients discovery i-1
+    wrote (two coefficient buffers, ping-pong).  K timed launches = K discoveries + K rollouts."""
+    from insite_amd import ops
+    N, T = args.patients, args.T
+    lib = coh.lib
+    F = lib.n_terms
+    f64 = torch.float64
+    coefs = [torch.zeros((2, F), dtype=f64, device=dev) for _ in range(2)]
+    masks = [torch.zeros((2, F), dtype=torch.int8, device=dev) for _ in range(2)]
+    iters = [torch.zeros((2,), dtype=torch.int32, device=dev) for _ in range(2)]
+    Gs = [torch.zeros((2, F, F), dtype=f64, device=dev) for _ in range(2)]
+    bs = [torch.zeros((2, F), dtype=f64, device=dev) for _ in range(2)]
+    y = torch.empty((T, N), dtype=f64, device=dev)
+    # step -1: a plain discovery gives the first rollout its model
+    ops.sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, out=(coefs[1], masks[1], iters[1], Gs[1],
+                                                                              bs[1]), layout="time")
+    plans = [ops.plan_fit_rollout(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, coh.y0, coh.u, arm_cf,
+                                  coefs[1 - j], coh.dt, method=args.method, T=T, y_out=y,
+                                  out=(coefs[j], masks[j], iters[j], Gs[j], bs[j]), gram_blocks=args.gram_blocks)
+             for j in range(2)]
+    st = torch.cuda.current_stream(dev)
+    fast = [p.bind(st) for p in plans]
+    for i in range(args.warmup):
+        fast[i % 2]()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        fast[i % 2]()
+    host_ms = (time.perf_counter() - t0) / args.steps * 1e3
+    torch.cuda.synchronize(dev)
+    ms_step = (time.perf_counter() - t0) / args.steps * 1e3
+    last = (args.steps - 1) % 2
+    # instrumented pass: HIP timing events on the launch stream around batches of KB back-to-back launches
+    # (an event record costs ~20 us of queue time on ROCm 7.2, so never one per launch), divided by KB
+    hip = HipEvents()
+    KB, NBAT = max(args.steps, 10), 3
+    tevs = [(hip.create(timing=True), hip.create(timing=True)) for _ in range(NBAT)]
+    for e0, e1 in tevs:
+        hip.record(e0, st.cuda_stream)
+        for i in range(KB):
+            fast[i % 2]()
+        hip.record(e1, st.cuda_stream)
+    torch.cuda.synchronize(dev)
+    step_ms = float(np.mean([hip.elapsed_ms(e0, e1) for e0, e1 in tevs])) / KB
+    rb, gb = rollout_bytes(N, T, arm_bits=1), gram_bytes(N, T)
+    return {"ms_step": ms_step, "host_ms": host_ms, "step_ms": step_ms, "KB": KB, "NBAT": NBAT,
+            "coef": coefs[last], "mask": masks[last], "y": y, "rb": rb, "gb": gb,
+            "frac": (rb + gb) / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+
+
+def c2_fused(args, dev, coh, arm_cf, cpu):
+    """C2 at N = 1 with one step_kernel launch per step (--mode fused); see fused_run."""
+    from insite_amd import ops
+    N, T = args.patients, args.T
+    lib = coh.lib
+    F = lib.n_terms
+    fr = fused_run(args, dev, coh, arm_cf)
+    ms_step, host_ms, step_ms, KB, NBAT = fr["ms_step"], fr["host_ms"], fr["step_ms"], fr["KB"], fr["NBAT"]
+    y = fr["y"]
+    st = torch.cuda.current_stream(dev)
+
+    iso = None
+    if args.isolated:   # the two halves as separate launches, back to back on one stream
+        def timed(fn, n):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(n):
+                fn()
+            e1.record(st)
+            torch.cuda.synchronize(dev)
+            return e0.elapsed_time(e1) / n
+        gp = ops.plan_sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, layout="time").bind(st)
+        rp = ops.plan_rollout(coh.y0, coh.u, arm_cf, fr["coef"], lib, coh.dt, method=args.method, T=T, out=y,
+                              layout="time_bits").bind(st)
+        iso = {"discovery_avg_launch_ms": timed(gp, 20), "rollout_avg_launch_ms": timed(rp, 20)}
+
+    sup = fr["mask"].cpu().numpy()
+    ok = bool(torch.isfinite(y).all().item())
+    rb, gb = fr["rb"], fr["gb"]
+    achieved = (rb + gb) / (step_ms * 1e-3) / 1e9
+    out = {
+        "metric": METRIC,
+        "value": N / (ms_step * 1e-3),
+        "unit": "patient-trajectories/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: on-device EQ_4_C PK/PD cohort (reference distributions, Euler-5 truth + 0.01 noise)",
+        "config": {
+            "workload": f"C2: PK/PD {N // 1000}k patients/GPU x {T} steps fp64 - discovery (savgol+FD4+poly2 "
+                        f"library+Gram, STLSQ) + {args.method.upper()} counterfactual rollout",
+            "patients_per_gpu": N, "T": T, "rows_per_patient": T - 2, "library_terms": F,
+            "parallelism": "patient-shard x1", "mode": "fused", "gram_blocks": args.gram_blocks or "default",
+            "discovered_support": sup.tolist(), "finite": ok,
+        },
+        "host_submit_ms_per_step": host_ms,
+        "roofline": {
+            "kernel": f"step_kernel (discovery: gram + in-launch reduction + STLSQ | {args.method} bit-arm rollout)",
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS,
+            "traffic": None,
+            "algorithmic_bytes_per_launch": rb + gb,
+            "algorithmic_bytes_split": {"discovery_x_read": gb, "rollout_y_written": rb},
+            "avg_launch_ms": step_ms,
+            "avg_ms_source": f"HIP timing events on the launch stream around {NBAT} batches of {KB} back-to-back "
+                             "step_kernel launches, divided by the batch size (one launch = one step)",
+            "layout": "time-major x[T,N] read, 1-bit arm mask [T,N/32], y[T,N] written",
+        },
+        "timed_region": "one step_kernel launch per step on one stream: discovery of step i | rollout of step i-1 "
+                        "(two coefficient buffers); no events or cross-stream waits inside the timed region",
+    }
+    tj = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+        except Exception:
+            tj = None
+    if tj and tj.get("workload") == f"step_{args.method}_{N}x{T}":
+        out["roofline"]["traffic"] = tj.get("hbm_bytes_per_launch")
+    if iso is not None:
+        out["isolated"] = dict(iso, discovery_frac=gb / (iso["discovery_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                               rollout_frac=rb / (iso["rollout_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS)
+    if not args.no_north_star:
+        del y
+        torch.cuda.empty_cache()
+        out["north_star_rollout"] = north_star_rollout(args, dev, fr["coef"], lib)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+    print(json.dumps(out))
+
+
+def north_star_rollout(args, dev, coef, lib):
+    """The 1M x 500 RK4 rollout alone (the north star's >= 40 % roofline target), events around each launch."""
+    from insite_amd import ops
+    Nn, Tn = 1_000_000, 500
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    y0n = torch.rand(Nn, generator=g, device=dev, dtype=torch.float64) * 49 + 1
+    un = torch.rand((Nn, 2), generator=g, device=dev, dtype=torch.float64) * 0.1 + 0.45
+    flip = torch.randint(0, Tn, (Nn, 1), generator=g, device=dev)
+    armn = torch.zeros((Tn, Nn), dtype=torch.int8, device=dev)
+    armn[:] = (torch.arange(Tn, device=dev)[:, None] >= flip[:, 0][None, :]).to(torch.int8)
+    nlay = "time_bits" if args.arm_format == "bits" else "time"
+    if nlay == "time_bits":
+        armn = ops.pack_arm_bits(armn, Nn)
+    yn = torch.empty((Tn, Nn), dtype=torch.float64, device=dev)
+    for _ in range(3):
+        ops.rollout(y0n, un, armn, coef, lib, 10.0 / Tn, method="rk4", out=yn, layout=nlay)
+    evs = []
+    for _ in range(10):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream(dev))
+        ops.rollout(y0n, un, armn, coef, lib, 10.0 / Tn, method="rk4", out=yn, layout=nlay)
+        e1.record(torch.cuda.current_stream(dev))
+        evs.append((e0, e1))
+    torch.cuda.synchronize(dev)
+    ms = float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))
+    bn = rollout_bytes(Nn, Tn, arm_bits=1 if nlay == "time_bits" else 8)
+    return {"patients": Nn, "T": Tn, "method": "rk4", "layout": nlay, "avg_launch_ms": ms,
+            "algorithmic_bytes": bn, "achieved_GBps": bn / (ms * 1e-3) / 1e9,
+            "frac_of_8TBps": bn / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "patient_trajectories_per_s": Nn / (ms * 1e-3)}
+
+
 def main():
     args = parse()
     launch_ranks(args)
@@ -824,6 +1008,13 @@ def main():
     lib = coh.lib
     F = lib.n_terms
     y0 = coh.y0
+    if args.mode is None:
+        args.mode = "pipeline"
+    if args.mode == "fused" and world > 1:
+        raise SystemExit("--mode fused is single-GPU (the all-reduce sits between the gram and STLSQ): "
+                         "use --mode pipeline at N > 1")
+    if args.mode == "fused":
+        return c2_fused(args, dev, coh, arm_cf, cpu)
     # per-step state in NB buffers: the discovery of step i writes coefs[i % NB] while older rollouts may
     # still read theirs (G|b and the gram workspace are only touched by the discovery stream, in order,
     # but are buffered alike to keep the plans independent).  Steps go in batches of K: one event per batch
@@ -1104,39 +1295,25 @@ def main():
         if iso is not None:
             out["isolated"] = dict(iso, rollout_frac=rb / (iso["rollout_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                                    gram_frac=gram_bytes(N, T) / (iso["gram_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS)
+    # the same step as ONE fused launch (step_kernel, insite_fit_rollout_f64), measured beside the headline
+    if rank == 0 and world == 1 and mode == "pipeline" and not args.no_fused:
+        fr = fused_run(args, dev, coh, arm_cf)
+        out["fused_step_kernel"] = {
+            "kernel": "step_kernel (discovery of step i | rollout of step i-1, one launch per step)",
+            "ms_per_step": fr["ms_step"], "avg_launch_ms": fr["step_ms"],
+            "algorithmic_bytes_per_launch": fr["rb"] + fr["gb"],
+            "achieved_GBps": (fr["rb"] + fr["gb"]) / (fr["step_ms"] * 1e-3) / 1e9, "frac": fr["frac"],
+            "gram_blocks": args.gram_blocks or "default",
+            "avg_ms_source": f"HIP timing events around {fr['NBAT']} batches of {fr['KB']} back-to-back launches",
+            "why_not_headline": "one launch holds both roles at the gram's 2 waves/SIMD register budget; the two-stream "
+                                "pipeline keeps more rollout waves resident and measures faster",
+        }
+        del fr
     # north-star probe: 1M x 500 RK4 rollout alone (the >= 40 % roofline target), rank 0, N = 1
     if rank == 0 and world == 1 and not args.no_north_star:
         del y
         torch.cuda.empty_cache()
-        Nn, Tn = 1_000_000, 500
-        g = torch.Generator(device=dev)
-        g.manual_seed(7)
-        y0n = torch.rand(Nn, generator=g, device=dev, dtype=torch.float64) * 49 + 1
-        un = torch.rand((Nn, 2), generator=g, device=dev, dtype=torch.float64) * 0.1 + 0.45
-        flip = torch.randint(0, Tn, (Nn, 1), generator=g, device=dev)
-        armn = torch.zeros((Tn, Nn), dtype=torch.int8, device=dev)
-        armn[:] = (torch.arange(Tn, device=dev)[:, None] >= flip[:, 0][None, :]).to(torch.int8)
-        nlay = "time_bits" if args.arm_format == "bits" else "time"
-        if nlay == "time_bits":
-            armn = ops.pack_arm_bits(armn, Nn)
-        yn = torch.empty((Tn, Nn), dtype=torch.float64, device=dev)
-        for _ in range(3):
-            ops.rollout(y0n, un, armn, coef, lib, 10.0 / Tn, method="rk4", out=yn, layout=nlay)
-        evs = []
-        for _ in range(10):
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(torch.cuda.current_stream(dev))
-            ops.rollout(y0n, un, armn, coef, lib, 10.0 / Tn, method="rk4", out=yn, layout=nlay)
-            e1.record(torch.cuda.current_stream(dev))
-            evs.append((e0, e1))
-        torch.cuda.synchronize(dev)
-        ms = float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))
-        bn = rollout_bytes(Nn, Tn, arm_bits=1 if nlay == "time_bits" else 8)
-        out["north_star_rollout"] = {"patients": Nn, "T": Tn, "method": "rk4", "layout": nlay, "avg_launch_ms": ms,
-                                     "algorithmic_bytes": bn, "achieved_GBps": bn / (ms * 1e-3) / 1e9,
-                                     "frac_of_8TBps": bn / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-                                     "patient_trajectories_per_s": Nn / (ms * 1e-3)}
+        out["north_star_rollout"] = north_star_rollout(args, dev, coef, lib)
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:

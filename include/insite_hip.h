@@ -135,6 +135,31 @@ int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, int32_t layout, int32
                              double* G_out, double* b_out, double* coef_out, int8_t* mask_out,
                              int32_t* iters_out, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Fused step for a stream of cohorts (the C2 pipeline; a serving loop): ONE launch that runs the
+ * discovery of one cohort (insite_sindy_fit_f64 semantics, TIME_MAJOR x) and, concurrently, the
+ * rollout of another cohort with already-known coefficients coef_in (insite_rollout_f64 semantics,
+ * TIME_MAJOR_BITS arms, coef_row_stride 0).  The reference runs these as SINDy.fit (sindy.py:190-192)
+ * then the counterfactual scan (sindy.py:413-431, 767-778) per dataset; here cohort k's discovery
+ * overlaps cohort k-1's rollout inside one kernel (two independent HBM streams: x read, y written),
+ * replacing a two-stream pipeline and its events.  Typical use: coef_out of call k is coef_in of call
+ * k + 1 (double-buffered by the caller).  Shape restrictions of this entry point (others return
+ * INSITE_E_UNSUPPORTED; use the two separate calls): n_arms = 2, n_terms = 7 (the degree-2 library
+ * over [x, u0, u1]), state degree <= 1.  The library (exps, n_statics) is shared by both halves; ru
+ * [n_rows, n_statics] are the rollout cohort's statics.  n_rows = 0 or T = 0 skips the rollout (then
+ * its pointers may be NULL).  gram_blocks: blocks given to the discovery (0 = the library's default
+ * split).  Outputs are those of the separate calls: y_out bitwise; G/b/coef as insite_sindy_fit_f64
+ * with the same block count (fixed-order sums).  Workspace: insite_gram_workspace_bytes(n_patients, 2,
+ * 7), header zero as for insite_sindy_fit_f64. */
+int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, const double* u, const int8_t* arm,
+                               const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
+                               const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt, double threshold,
+                               double alpha, int32_t max_iter, int32_t unbias, double* G_out, double* b_out,
+                               double* coef_out, int8_t* mask_out, int32_t* iters_out, const double* y0,
+                               const double* ru, const uint32_t* arm_bits, int64_t ld_arm, const double* coef_in,
+                               int64_t n_rows, int32_t T, double rdt, int32_t method, int32_t substeps,
+                               double drop_below, double* y_out, int64_t ld_y, int32_t gram_blocks, void* workspace,
+                               size_t workspace_bytes, void* stream);
+
 /* Treatment-segment discovery for the cancer_sim / EQ_5 datasets, replacing
  * process_sindy_training_data's segment split (libs_m/ct/src/data/pkpd/utils.py:433-462, 607-637)
  * and the four per-arm SINDy(FiniteDifference(order=1)).fit calls (libs_m/ct/src/models/sindy.py:

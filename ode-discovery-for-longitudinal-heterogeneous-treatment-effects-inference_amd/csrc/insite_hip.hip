@@ -101,6 +101,9 @@ __device__ __forceinline__ double monomial(const LibDesc& lib, int j, const doub
 #endif
 constexpr int kGT = INSITE_GT;     // time tile in steps: a multiple of the register ring length (8)
 constexpr int kGStride = kGT + 1;  // LDS row stride in doubles (odd -> lane-per-row reads conflict free)
+// per-wave LDS slot: 64 rows of max(kGStride, 17) doubles -- also the MFMA contraction's staging rows
+// (32 x 23) and the scalar path's 64 x kPsStride rows
+constexpr int kGSlot = kGStride > 17 ? kGStride : 17;
 constexpr int kGPF = INSITE_PF;    // tiles in flight (register prefetch depth, 1 or 2)
 #ifndef INSITE_TM_DEPTH
 #define INSITE_TM_DEPTH 2
@@ -199,12 +202,12 @@ __device__ __forceinline__ void tail_store(double* p, double v) {  // sc1 (write
 }
 
 template <int STF>
-__device__ __forceinline__ void gram_tail(double* __restrict__ part, int n_ent, unsigned* __restrict__ cnt,
-                                          const LibDesc& lib, const GramOut& o, double* red) {
+__device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double* __restrict__ part, int n_ent,
+                                          unsigned* __restrict__ cnt, const LibDesc& lib, const GramOut& o,
+                                          double* red) {
   int* flag = reinterpret_cast<int*>(red + kTailMaxEnt);  // "I am last", through the kernel's LDS array
-  const int nblk = (int)gridDim.x;
   const int ng = (nblk + kTailGroup - 1) / kTailGroup;
-  const int g = (int)blockIdx.x / kTailGroup;
+  const int g = vblk / kTailGroup;
   const int g0 = g * kTailGroup;
   const int gs = nblk - g0 < kTailGroup ? nblk - g0 : kTailGroup;
   double* gpart = part + (int64_t)nblk * n_ent;
@@ -285,7 +288,7 @@ __device__ __forceinline__ void gram_tail(double* __restrict__ part, int n_ent, 
   }
 }
 static_assert(kTailMaxEnt + 8 + INSITE_MAX_ARMS * (INSITE_MAX_TERMS * INSITE_MAX_TERMS + INSITE_MAX_TERMS) <=
-                  kWavesPerBlock * kWave * kGStride,
+                  kWavesPerBlock * kWave * kGSlot,
               "tail scratch fits the gram kernel's LDS array");
 
 // Lane = patient.  Work item = (64-patient tile, time segment [s*seg, (s+1)*seg)).  Rows are
@@ -303,15 +306,18 @@ static_assert(kTailMaxEnt + 8 + INSITE_MAX_ARMS * (INSITE_MAX_TERMS * INSITE_MAX
 // every lane writes its patient's moments {L, sum xs, sum xs^2, sum xdot, sum xdot xs} to
 // partial[p * 5 ..] (insite_sindy_fit_per_patient_f64).
 // Otherwise the block partials are reduced inside the launch (gram_tail) into G [A, F, F] and b [A, F].
+// The body is a device function of a virtual block index / grid size (vblk, vgrid) and the block's LDS,
+// so the fused step kernel (step_kernel) can run it on a subset of its blocks.
+constexpr int kGramSmem = kWavesPerBlock * kWave * kGSlot;  // doubles of LDS per block
 template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM, int STF = 0>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))  // <= 256 VGPR+AGPR
-gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
+__device__ __forceinline__ void gram_body(const int vblk, const int vgrid, double* __restrict__ smem,
+            const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
             const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, int seg, int n_seg,
-            GramW w, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ cnt, GramOut out) {
-  __shared__ double smem[kWavesPerBlock * kWave * kGStride];
+            const GramW& w, const LibDesc& lib, double* __restrict__ partial, unsigned* __restrict__ cnt,
+            const GramOut& out) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform (SGPR)
-  double* xt = smem + wid * (kWave * kGStride);
+  double* xt = smem + wid * (kWave * kGSlot);
   constexpr int kMinMain = SMOOTH ? 8 : 5;  // shorter (5..7, smoothed) rows take small_trajectory
   constexpr int kWarm = SMOOTH ? 8 : 4;     // warm-up steps of a segment's first tile
   constexpr int kLag = SMOOTH ? 4 : 2;      // body row kd = t - kLag
@@ -343,8 +349,8 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
 
   const int64_t n_tiles = (N + kWave - 1) / kWave;
   const int64_t n_items = n_tiles * n_seg;
-  for (int64_t item = (int64_t)blockIdx.x * kWavesPerBlock + wid; item < n_items;
-       item += (int64_t)gridDim.x * kWavesPerBlock) {
+  for (int64_t item = (int64_t)vblk * kWavesPerBlock + wid; item < n_items;
+       item += (int64_t)vgrid * kWavesPerBlock) {
     const int64_t tile = item / n_seg;
     const int sidx = (int)(item - tile * n_seg);
     const int64_t p0 = tile * kWave;
@@ -762,11 +768,21 @@ gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
     double v = red[q];
 #pragma unroll
     for (int ww = 1; ww < kWavesPerBlock; ++ww) v += red[ww * stride + q];
-    tail_store(partial + (int64_t)blockIdx.x * n_ent + idx, v);
+    tail_store(partial + (int64_t)vblk * n_ent + idx, v);
   }
   INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 6);
-  gram_tail<STF>(partial, n_ent, cnt, lib, out, smem);
+  gram_tail<STF>(vblk, vgrid, partial, n_ent, cnt, lib, out, smem);
   INSITE_TREAL(blockIdx.x * kWavesPerBlock + wid, 9);
+}
+
+template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM, int STF = 0>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))  // <= 256 VGPR+AGPR
+gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
+            const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, int seg, int n_seg,
+            GramW w, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ cnt, GramOut out) {
+  __shared__ double smem[kGramSmem];
+  gram_body<VEC, NARM, SMOOTH, MFMA, TM, MOM, STF>((int)blockIdx.x, (int)gridDim.x, smem, x, ldx, n_steps, u, arm, rows,
+                                                  N, seg, n_seg, w, lib, partial, cnt, out);
 }
 
 // =============================================================================================
@@ -1561,6 +1577,112 @@ constexpr int64_t kTmMaxLd = ((int64_t)1 << 31) / (8 * kTG);  // group offsets s
 // arms), kArmBits (time-major bitmask, n_arms <= 2: bit r & 31 of word r >> 5 of the step row).
 constexpr int kArmByte = 0, kArmDword = 1, kArmBits = 2;
 
+// Bit-packed arms, one patient per lane (the C2 / north-star layout): the 64-patient tile `tile`, its
+// 32-step arm groups [g_begin, g_end).  Arm bits 32 steps at a time: lane l loads word (k0 + (l & 31),
+// p0/32 + (l >> 5)) of the [T, N/32] mask (one 256-B request per wave), and a 32x32 bit transpose per
+// half-wave leaves the lane's own 32 steps in one register.  Groups are requested kAG groups (128
+// steps) ahead into compile-time ring slots, so the time loop never waits on arm data; per step it is
+// one select + one FMA + one 512-B store per wave.  A range that starts inside the trajectory
+// (g_begin > 0: the fused step kernel's balanced split of tiles x groups over waves) integrates the
+// groups before it without storing them -- the same FMA sequence from y0, so the stored states are
+// bitwise those of a whole-trajectory pass (32 FMAs per skipped group against 32 x 512 B of stores).
+constexpr int kRollGS = 32;  // steps per arm group
+template <int METHOD, int NARM, bool PERROW>
+__device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const LibDesc& lib, const int lane,
+                                                   const int64_t tile, const int g_begin, const int g_end) {
+  const int64_t p0 = tile * kWave;
+  const int64_t p = p0 + lane;
+  const bool act = p < ra.N;
+  const int64_t pc = act ? p : ra.N - 1;
+  double PA[NARM], PB[NARM], y;
+  {
+    double uu[INSITE_MAX_STATICS];
+#pragma unroll
+    for (int t = 0; t < INSITE_MAX_STATICS; ++t) {
+      const double v = ra.u[pc * lib.U + (t < lib.U ? t : 0)];
+      uu[t] = (act && t < lib.U) ? v : 0.0;
+    }
+    const double* cbase = ra.coef + (PERROW ? pc * ra.coef_stride : 0);
+    const double h = ra.dt / (double)ra.substeps;
+#pragma unroll
+    for (int a = 0; a < NARM; ++a) {
+      double al = 0.0, be = 0.0;
+      if (a < ra.A) {
+        for (int j = 0; j < lib.F; ++j) {
+          const double c = cbase[a * lib.F + j];
+          if (fabs(c) > ra.drop) {
+            const double t = c * monomial(lib, j, uu);
+            if (lib.ex[j] == 0) al += t;
+            else be += t;
+          }
+        }
+      }
+      interval_propagator(METHOD, ra.substeps, h, al, be, PA[a], PB[a]);
+    }
+    const double v0 = ra.y0[pc];
+    y = act ? v0 : 0.0;
+  }
+  const int nvalid = (int)(ra.N - p0 < kWave ? ra.N - p0 : kWave);
+  const unsigned yoff = act ? (unsigned)(lane * 8) : kOOB;
+  const int64_t arow = ra.lda * 4;   // bit rows: lda counts 32-bit words
+  const int64_t abase = (p0 >> 5) * 4;
+  const int arec_tail = ((nvalid + 31) >> 5) * 4;
+  const int kend = g_end * kRollGS < ra.T ? g_end * kRollGS : ra.T;  // one past the last step of the range
+  const int kbeg = g_begin * kRollGS;                                // first stored step
+  auto y_rsrc = [&](int k0) {  // rows [k0, min(k0 + kTG, T)); empty (all stores dropped) past T
+    const int rows = ra.T - k0 < kTG ? ra.T - k0 : kTG;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(ra.y + (int64_t)(rows > 0 ? k0 : 0) * ra.ldy + p0), (short)0,
+                                             rows > 0 ? (int)(((int64_t)(rows - 1) * ra.ldy + nvalid) * 8) : 0,
+                                             0x00020000);
+  };
+  constexpr int kAG = 4;
+  const unsigned goff = (unsigned)((lane & 31) * arow + (lane >> 5) * 4);
+  auto grp_load = [&](int k0) -> unsigned {  // empty past the range: returns 0
+    const int rows = kend - k0 < kRollGS ? kend - k0 : kRollGS;
+    const int bytes = rows > 0 ? (int)((int64_t)(rows - 1) * arow + arec_tail) : 0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(ra.arm + (int64_t)(rows > 0 ? k0 : 0) * arow + abase), (short)0, bytes, 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, goff, 0, 0);
+  };
+  auto step = [&](int a) {
+    double A = PA[0], B = PB[0];
+#pragma unroll
+    for (int aa = 1; aa < NARM; ++aa) {
+      A = (a == aa) ? PA[aa] : A;
+      B = (a == aa) ? PB[aa] : B;
+    }
+    y = fma(A, y, B);
+  };
+  unsigned aring[kAG];
+#pragma unroll
+  for (int d = 0; d < kAG; ++d) aring[d] = grp_load(d * kRollGS);
+  for (int k0 = 0; k0 < kend;) {
+#pragma unroll
+    for (int d = 0; d < kAG; ++d) {
+      if (k0 < kend) {  // uniform
+        const unsigned wb = bit_transpose32(aring[d], lane);
+        aring[d] = grp_load(k0 + kAG * kRollGS);
+        if (k0 >= kbeg) {  // uniform: a stored group
+#pragma unroll
+          for (int hh = 0; hh < kRollGS / kTG; ++hh) {
+            const __amdgpu_buffer_rsrc_t ys = y_rsrc(k0 + hh * kTG);
+#pragma unroll
+            for (int i = 0; i < kTG; ++i) {
+              step((int)((wb >> (hh * kTG + i)) & 1u));
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y), ys, yoff + (unsigned)(i * ra.ldy * 8),
+                                                    0, kStoreAux);
+            }
+          }
+        } else {  // a group before the range: integrate only
+#pragma unroll
+          for (int i = 0; i < kRollGS; ++i) step((int)((wb >> i) & 1u));
+        }
+        k0 += kRollGS;
+      }
+    }
+  }
+}
+
 template <int METHOD, int NARM, bool PERROW, int PPL, int AFMT>
 __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibDesc lib) {
   constexpr bool AW4 = AFMT != kArmByte;  // 32-bit ring elements
@@ -1568,6 +1690,10 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform (SGPR)
   const int64_t p0 = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * (kWave * PPL);
   if (p0 >= ra.N) return;
+  if constexpr (AFMT == kArmBits && PPL == 1) {
+    rollout_bits_range<METHOD, NARM, PERROW>(ra, lib, lane, p0 / kWave, 0, (ra.T + kRollGS - 1) / kRollGS);
+    return;
+  }
   INSITE_TSTAMP(32768 + blockIdx.x * kWavesPerBlock + wid, 0);
   INSITE_TREAL(32768 + blockIdx.x * kWavesPerBlock + wid, 8);
   double y[PPL], alpha[PPL][NARM], beta[PPL][NARM];
@@ -1691,57 +1817,6 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
 #endif
 
   INSITE_TSTAMP(32768 + blockIdx.x * kWavesPerBlock + wid, 1);
-  if constexpr (AFMT == kArmBits && PPL == 1) {
-    // Arm bits 32 steps at a time: lane l loads word (k0 + (l & 31), p0/32 + (l >> 5)) of the
-    // [T, N/32] mask (one 256-B request per wave), and a 32x32 bit transpose per half-wave leaves
-    // the lane's own 32 steps in one register.  Groups are requested kAG groups (128 steps) ahead
-    // into compile-time ring slots, so the time loop never waits on arm data; per step it is one
-    // select + one FMA + one 512-B store per wave.
-    constexpr int kAG = 4;
-    constexpr int kGS = 32;  // steps per arm group
-    const unsigned goff = (unsigned)((lane & 31) * arow + (lane >> 5) * 4);
-    auto grp_load = [&](int k0) -> unsigned {
-      const int rows = ra.T - k0 < kGS ? ra.T - k0 : kGS;
-      const int bytes = rows > 0 ? (int)((int64_t)(rows - 1) * arow + arec_tail) : 0;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(ra.arm + (int64_t)(rows > 0 ? k0 : 0) * arow + abase), (short)0, bytes, 0x00020000);
-      return __builtin_amdgcn_raw_buffer_load_b32(rs, goff, 0, 0);
-    };
-    unsigned aring[kAG];
-#pragma unroll
-    for (int d = 0; d < kAG; ++d) aring[d] = grp_load(d * kGS);
-    for (int k0 = 0; k0 < ra.T;) {
-#pragma unroll
-      for (int d = 0; d < kAG; ++d) {
-        if (k0 < ra.T) {  // uniform
-          const unsigned wb = bit_transpose32(aring[d], lane);
-          aring[d] = grp_load(k0 + kAG * kGS);  // empty past T: returns 0
-#pragma unroll
-          for (int hh = 0; hh < kGS / kTG; ++hh) {
-            const __amdgpu_buffer_rsrc_t ys = y_rsrc(k0 + hh * kTG);
-#pragma unroll
-            for (int i = 0; i < kTG; ++i) {
-#ifndef INSITE_ABLATE_NOCOMPUTE
-              step(0, (int)((wb >> (hh * kTG + i)) & 1u));
-#else
-              y[0] += (double)((wb >> (hh * kTG + i)) & 1u);
-#endif
-#ifndef INSITE_ABLATE_NOSTORE
-              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y[0]), ys,
-                                                    yoff + (unsigned)(i * ra.ldy * 8), 0, kStoreAux);
-#else
-              if (y[0] == 12345.678) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y[0]), ys, yoff, 0, 0);
-#endif
-            }
-          }
-          k0 += kGS;
-        }
-      }
-    }
-    INSITE_TSTAMP(32768 + blockIdx.x * kWavesPerBlock + wid, 2);
-    INSITE_TREAL(32768 + blockIdx.x * kWavesPerBlock + wid, 9);
-    return;
-  }
   ArmT ring[kTG];
   {
     const __amdgpu_buffer_rsrc_t rs = arm_rsrc(0);
@@ -1782,6 +1857,52 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
       if (y[0] == 12345.678) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y[0]), ys, off, 0, 0);
 #endif
     }
+  }
+}
+
+// =============================================================================================
+// Fused step: the discovery of one cohort and the rollout of another in ONE launch (C2 pipeline)
+// =============================================================================================
+// A stream of cohorts (the C2 bench; a serving loop) discovers cohort k while it rolls out cohort
+// k - 1 with the coefficients that discovery k - 1 wrote.  The two halves are independent HBM streams
+// (the gram reads x, the rollout writes y), so one launch runs both at once: blocks [0, gblocks) run
+// gram_body (in-launch fixed-order reduction and the fused F = 7 STLSQ, exactly as gram_kernel) and the
+// other blocks the bit-arm rollout.  The grid is one resident round (every block persistent), and the
+// rollout's work -- 64-patient tiles x 32-step arm groups, tile-major -- is cut into equal contiguous
+// ranges, one per rollout wave, so both roles end together whatever the cohort size; a range that
+// starts mid-trajectory re-integrates its tile's earlier groups without storing (rollout_bits_range),
+// so every stored state is bitwise that of the standalone rollout.  Results do not depend on gblocks
+// except through the gram's block count (the fixed-order reduction's association, as for gram_kernel's
+// grid).  Replaces, per step, the gram + rollout launch pair on two streams and the events between them.
+#ifndef INSITE_STEP_WPE
+#define INSITE_STEP_WPE 2  // waves per SIMD the step kernel's register budget is sized for
+#endif
+template <bool SMOOTH, int METHOD>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_STEP_WPE)))
+step_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
+            const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, int seg, int n_seg,
+            GramW w, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ cnt, GramOut out,
+            RolloutArgs ra, int gblocks) {
+  __shared__ double smem[kGramSmem];
+  if ((int)blockIdx.x < gblocks) {
+    gram_body<1, 2, SMOOTH, true, true, false, 7>((int)blockIdx.x, gblocks, smem, x, ldx, n_steps, u, arm, rows, N,
+                                                 seg, n_seg, w, lib, partial, cnt, out);
+    return;
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t RW = (int64_t)(gridDim.x - gblocks) * kWavesPerBlock;
+  const int64_t rw = (int64_t)((int)blockIdx.x - gblocks) * kWavesPerBlock + wid;
+  const int ng = (ra.T + kRollGS - 1) / kRollGS;
+  const int64_t units = (ra.N + kWave - 1) / kWave * ng;  // (tile, arm group) pairs, tile-major
+  int64_t q = rw * units / RW;
+  const int64_t q1 = (rw + 1) * units / RW;
+  while (q < q1) {
+    const int64_t tile = q / ng;
+    const int gb = (int)(q - tile * ng);
+    const int ge = q1 - q < (int64_t)(ng - gb) ? gb + (int)(q1 - q) : ng;
+    rollout_bits_range<METHOD, 2, false>(ra, lib, lane, tile, gb, ge);
+    q += ge - gb;
   }
 }
 
@@ -2869,6 +2990,49 @@ int build_lib(const int8_t* exps, int32_t F, int32_t U, LibDesc* lib) {
 }
 
 inline int narm_pad(int n_arms) { return n_arms <= 1 ? 1 : (n_arms <= 2 ? 2 : 4); }
+// step_kernel work split over one resident round of `resident` blocks: gblocks run the gram (default
+// INSITE_STEP_GSHARE per mille of the round; gram_blocks > 0 overrides), the rest the rollout.  The
+// gram's time segments are chosen so its (tile, segment) items spread evenly over the gram waves
+// (a wave that takes one item more than the others sets the gram's end): the segment count with the
+// smallest max/mean items per wave, a small charge per extra segment for its warm-up and contraction.
+#ifndef INSITE_STEP_GSHARE
+#define INSITE_STEP_GSHARE 600
+#endif
+struct StepPlan {
+  int grid, gblocks, seg, n_seg;
+};
+inline StepPlan step_plan(int64_t N, int64_t n_steps, int resident, int gram_blocks) {
+  StepPlan pl;
+  if (resident < 2) resident = 2;
+  int gb = gram_blocks > 0 ? gram_blocks : (int)(((int64_t)resident * INSITE_STEP_GSHARE + 500) / 1000);
+  if (gb < 1) gb = 1;
+  if (gb > resident - 1) gb = resident - 1;
+  if (gb > kGramMaxBlocks) gb = kGramMaxBlocks;
+  pl.gblocks = gb;
+  pl.grid = resident;
+  const int64_t tiles = (N + kWave - 1) / kWave;
+  const int64_t T = n_steps > 0 ? n_steps : 1;
+  const int64_t gw = (int64_t)gb * kWavesPerBlock;
+  const int64_t ns_max = T / 48 > 1 ? T / 48 : 1;
+  double best = 1e30;
+  pl.seg = (int)((T + kGT - 1) / kGT * kGT);
+  pl.n_seg = 1;
+  for (int64_t ns = 1; ns <= ns_max && tiles > 0; ++ns) {
+    int64_t seg = (T + ns - 1) / ns;
+    seg = (seg + kGT - 1) / kGT * kGT;
+    const int64_t nseg = (T + seg - 1) / seg;
+    const int64_t items = tiles * nseg;
+    const int64_t per = (items + gw - 1) / gw;  // items of the busiest gram wave
+    const double cost = (double)per * (double)seg + 24.0 * (double)(per - 1);  // steps (+ warm-up/contraction)
+    if (cost < best - 1e-9) {
+      best = cost;
+      pl.seg = (int)seg;
+      pl.n_seg = (int)nseg;
+    }
+  }
+  return pl;
+}
+
 
 struct GramPlan {
   int grid, seg, n_seg;
@@ -3312,6 +3476,79 @@ int32_t insite_gram_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_
   StlsqParams sp{0.0, 0.0, 0, 0, 0};
   return run_discovery(x, ldx, layout, n_steps, u, arm, rows, n_patients, n_statics, n_arms, exps, n_terms, fd_kind,
                        dt, G_out, b_out, workspace, workspace_bytes, stream, sp, nullptr, nullptr, nullptr);
+}
+
+int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, const double* u, const int8_t* arm,
+                               const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
+                               const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt, double threshold,
+                               double alpha, int32_t max_iter, int32_t unbias, double* G_out, double* b_out,
+                               double* coef_out, int8_t* mask_out, int32_t* iters_out, const double* y0,
+                               const double* ru, const uint32_t* arm_bits, int64_t ld_arm, const double* coef_in,
+                               int64_t n_rows, int32_t T, double rdt, int32_t method, int32_t substeps,
+                               double drop_below, double* y_out, int64_t ld_y, int32_t gram_blocks, void* workspace,
+                               size_t workspace_bytes, void* stream) {
+  // ---- discovery half: insite_sindy_fit_f64's checks, restricted to the fused kernel's shape ----
+  if (n_patients < 0 || !G_out || !b_out || !coef_out || n_arms != 2 || ldx < 1 || !(dt > 0.0) || n_steps < 0 ||
+      ldx < n_patients || max_iter < 0 || !(threshold >= 0.0) || !(alpha >= 0.0))
+    return INSITE_E_INVALID_ARG;
+  if (n_patients > 0 && (!x || !arm || !rows || (n_statics > 0 && !u))) return INSITE_E_INVALID_ARG;
+  if (fd_kind != INSITE_FD_SMOOTHED4 && fd_kind != INSITE_FD_ORDER4) return INSITE_E_UNSUPPORTED;
+  if (n_terms != 7) return INSITE_E_UNSUPPORTED;  // the fused STLSQ is instantiated for F = 7 (C2's library)
+  LibDesc lib;
+  int32_t st = build_lib(exps, n_terms, n_statics, &lib);
+  if (st != INSITE_OK) return st;
+  if (!lib.mfma) return INSITE_E_UNSUPPORTED;
+  {  // state degree <= 1 (the affine rollout)
+    for (int j = 0; j < n_terms; ++j)
+      if (exps[j * (1 + n_statics)] > INSITE_MAX_STATE_DEGREE) return INSITE_E_UNSUPPORTED;
+  }
+  if (!workspace || workspace_bytes < insite_gram_workspace_bytes(n_patients, n_arms, n_terms))
+    return INSITE_E_WORKSPACE;
+  if (ldx > ((int64_t)1 << 31) / (8 * kGT)) return INSITE_E_UNSUPPORTED;
+  // ---- rollout half: insite_rollout_f64's checks for TIME_MAJOR_BITS, shared library ----
+  if (n_rows < 0 || T < 0 || substeps < 1 || !(rdt >= 0.0) || ld_arm < (n_rows + 31) / 32 || ld_y < n_rows)
+    return INSITE_E_INVALID_ARG;
+  if (method != INSITE_METHOD_EULER && method != INSITE_METHOD_RK4) return INSITE_E_UNSUPPORTED;
+  const bool roll = n_rows > 0 && T > 0;
+  if (roll && (!y0 || !arm_bits || !coef_in || !y_out || (n_statics > 0 && !ru))) return INSITE_E_INVALID_ARG;
+  if (roll && (reinterpret_cast<uintptr_t>(arm_bits) & 3u) != 0) return INSITE_E_INVALID_ARG;
+  if (ld_arm * 4 > kTmMaxLd || ld_y > kTmMaxLd) return INSITE_E_UNSUPPORTED;
+  if (gram_blocks < 0) return INSITE_E_INVALID_ARG;
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  RolloutArgs ra;
+  ra.y0 = roll ? y0 : coef_out;  // empty rollout: pointers never dereferenced (no units)
+  ra.u = (roll && n_statics > 0) ? ru : ra.y0;
+  ra.arm = reinterpret_cast<const int8_t*>(roll ? (const void*)arm_bits : (const void*)coef_out);
+  ra.coef = roll ? coef_in : coef_out;
+  ra.y = roll ? y_out : coef_out;
+  ra.lda = ld_arm;
+  ra.ldy = ld_y;
+  ra.coef_stride = 0;
+  ra.N = roll ? n_rows : 0;
+  ra.T = roll ? T : 1;
+  ra.substeps = substeps;
+  ra.A = n_arms;
+  ra.dt = rdt;
+  ra.drop = drop_below;
+  const StlsqParams sp{threshold, alpha, max_iter, unbias, 1};
+  const GramOut go{G_out, b_out, n_arms, coef_out, mask_out, iters_out, sp};
+  unsigned* cnt = static_cast<unsigned*>(workspace);
+  double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + kGramWsHeader);
+  const bool smooth = fd_kind == INSITE_FD_SMOOTHED4;
+  // (a two-patients-per-lane rollout role with 16-B stores measured slower: 46 vs 37 us rollout-only)
+  auto kern = smooth ? (method == INSITE_METHOD_RK4 ? step_kernel<true, INSITE_METHOD_RK4> : step_kernel<true, INSITE_METHOD_EULER>)
+                     : (method == INSITE_METHOD_RK4 ? step_kernel<false, INSITE_METHOD_RK4> : step_kernel<false, INSITE_METHOD_EULER>);
+  const StepPlan pl = step_plan(n_patients, n_steps, resident_waves(kern) / kWavesPerBlock, gram_blocks);
+  if (n_statics == 0) u = x ? x : G_out;
+  if (n_patients == 0) {  // G = b = 0 and the fit of the zero system, through the same tail
+    x = G_out;
+    arm = reinterpret_cast<const int8_t*>(G_out);
+    rows = reinterpret_cast<const int32_t*>(G_out);
+    u = G_out;
+  }
+  kern<<<dim3(pl.grid), kBlock, 0, hs>>>(x, ldx, n_steps, u, arm, rows, n_patients, pl.seg, pl.n_seg,
+                                        make_gram_w(dt), lib, part, cnt, go, ra, pl.gblocks);
+  return launch_status();
 }
 
 int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,

@@ -37,6 +37,7 @@ EXPORTS = (
     "insite_gram_workspace_bytes",
     "insite_gram_f64",
     "insite_sindy_fit_f64",
+    "insite_fit_rollout_f64",
     "insite_gram_segments_workspace_bytes",
     "insite_gram_segments_f64",
     "insite_sindy_fit_segments_f64",
@@ -89,6 +90,10 @@ _SIGNATURES = {
                                       _c_i32, _c_i32,
                                       _c_f64, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _c_size,
                                       _vp]),
+    "insite_fit_rollout_f64": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp, _c_i32,
+                                        _c_i32, _c_f64, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp,
+                                        _vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_f64, _c_i32, _c_i32, _c_f64,
+                                        _vp, _c_i64, _c_i32, _vp, _c_size, _vp]),
     "insite_gram_segments_workspace_bytes": (_c_size, [_c_i64, _c_i32, _c_i32]),
     "insite_gram_segments_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i64, _c_i32, _c_i32,
                                           _vp, _c_i32, _c_i32, _c_f64, _vp, _vp, _vp, _c_size, _vp]),

@@ -516,6 +516,48 @@ def plan_rollout(y0, u, arm, coef, lib, dt, method="euler5", substeps=None, drop
     return Plan(name, args, dev, out, keep)
 
 
+def _prep_fit_rollout(x, u, arm, rows, dt, lib, threshold, alpha, max_iter, unbias, fd, workspace, out,
+                      y0, ru, arm_bits, coef_in, rdt, method, substeps, drop_below, T, y_out, gram_blocks):
+    gname, gargs, dev, gout, gkeep = _prep_gram(x, u, arm, rows, dt, lib, 2, fd, workspace, out, "time",
+                                               (threshold, alpha, max_iter, unbias))
+    rname, rargs, rdev, y_out, rkeep = _prep_rollout(y0, ru, arm_bits, coef_in, lib, rdt, method, substeps,
+                                                     drop_below, T, y_out, "time_bits")
+    if rdev != dev:
+        raise ValueError("both cohorts must live on one device")
+    if coef_in.dim() != 2 or coef_in.size(0) != 2:
+        raise ValueError("coef_in must be a contiguous [2, F] global model")
+    # insite_sindy_fit_f64 args: x ldx layout n_steps u arm rows N U A tab F fd dt thr alpha it unbias G b coef mask
+    # iters ws wsb;  insite_rollout_f64 args: y0 u arm lda coef stride tab F N T U A dt method sub drop y ldy layout
+    g, r = gargs, rargs
+    args = (g[0], g[1], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10], g[11], g[12], g[13], g[14], g[15], g[16],
+            g[17], g[18], g[19], g[20], g[21], g[22],
+            r[0], r[1], r[2], r[3], r[4], r[8], r[9], r[12], r[13], r[14], r[15], r[16], r[17],
+            int(gram_blocks), g[23], g[24])
+    return "insite_fit_rollout_f64", args, dev, (gout, y_out), gkeep + rkeep
+
+
+def fit_rollout(x, u, arm, rows, dt, lib, threshold, alpha, y0, ru, arm_bits, coef_in, rdt, method="rk4",
+                max_iter=100, unbias=True, fd="smoothed4", substeps=None, drop_below=1e-3, T=None, workspace=None,
+                out=None, y_out=None, gram_blocks=0):
+    """Fused step (insite_fit_rollout_f64): in ONE launch, the discovery of cohort (x [T, >=N]
+    time-major, u, arm, rows) -- ``sindy_fit`` with 2 arms and the 7-term library -- and the rollout
+    of another cohort (y0, ru, arm_bits [T, >=ceil(N/32)] int32) with the known global model coef_in
+    [2, F] -- ``rollout(layout="time_bits")``.  Returns ((coef, mask, iters, G, b), y)."""
+    return _run(_prep_fit_rollout(x, u, arm, rows, dt, lib, threshold, alpha, max_iter, unbias, fd, workspace, out,
+                                  y0, ru, arm_bits, coef_in, rdt, method, substeps, drop_below, T, y_out,
+                                  gram_blocks))
+
+
+def plan_fit_rollout(x, u, arm, rows, dt, lib, threshold, alpha, y0, ru, arm_bits, coef_in, rdt, method="rk4",
+                     max_iter=100, unbias=True, fd="smoothed4", substeps=None, drop_below=1e-3, T=None,
+                     workspace=None, out=None, y_out=None, gram_blocks=0) -> Plan:
+    """``fit_rollout`` as a prepared launch; ``plan.out`` = ((coef, mask, iters, G, b), y)."""
+    name, args, dev, out, keep = _prep_fit_rollout(x, u, arm, rows, dt, lib, threshold, alpha, max_iter, unbias, fd,
+                                                   workspace or Workspace(), out, y0, ru, arm_bits, coef_in, rdt,
+                                                   method, substeps, drop_below, T, y_out, gram_blocks)
+    return Plan(name, args, dev, out, keep)
+
+
 def rk45_order(n_obs: torch.Tensor, T_max: int, out: torch.Tensor | None = None) -> torch.Tensor:
     """Lane order for ``rollout_rk45``: rows sorted by n_obs, descending (insite_rk45_order_i32, a
     counting sort on the device).  Scheduling only: the rollout's outputs do not depend on it."""

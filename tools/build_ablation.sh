@@ -22,6 +22,10 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     MS4PRIO) NAME=$v build -DINSITE_MS4_PRIO=1 ;;
     MS4NC1) NAME=$v build -DINSITE_MS4_NCHUNK=1 ;;
     STLSEP) NAME=$v build -DINSITE_STLSQ_SEPARATE ;;
+    STEPDEPTH3) NAME=$v build -DINSITE_TM_DEPTH=3 ;;
+    GT8D4) NAME=$v build -DINSITE_GT=8 -DINSITE_TM_DEPTH=4 ;;
+    GT8D3) NAME=$v build -DINSITE_GT=8 -DINSITE_TM_DEPTH=3 ;;
+    GT8D5) NAME=$v build -DINSITE_GT=8 -DINSITE_TM_DEPTH=5 ;;
     MS4NOEMIT) NAME=$v build -DINSITE_MS4_ABL_NOEMIT=1 ;;
     RKW8W8) NAME=$v build -DINSITE_RK45_WIN=8 -DINSITE_RK45_WPE=8 ;;
     RKW16W5) NAME=$v build -DINSITE_RK45_WIN=16 -DINSITE_RK45_WPE=5 ;;
