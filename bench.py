@@ -512,17 +512,21 @@ def insite_main(args):
     c0[0, 4], c0[1, 1], c0[1, 5] = -1.1107592869834308, -0.14540553723951796, -1.0234639833519243  # log :182
     dt = 10.0 / T
 
-    def run():
-        return ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5)
+    def run(binned=False):   # binned=True: rows binned by seq_len on the device (inside every step)
+        return ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, binned=binned)
 
-    for _ in range(args.warmup):
-        run()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        preds, coef, status, iters = run()
-    torch.cuda.synchronize(dev)
-    ms_step = (time.perf_counter() - t0) / args.steps * 1e3
+    def timed(binned):
+        for _ in range(args.warmup):
+            run(binned)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            r = run(binned)
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / args.steps * 1e3, r
+
+    ms_binned, _ = timed(True)
+    ms_step, (preds, coef, status, iters) = timed(False)
     st = status.cpu().numpy()
     it = iters.cpu().numpy()
     out = {
@@ -534,6 +538,8 @@ def insite_main(args):
                                f"{N // 1000}k rows", "rows": N, "T": T},
         "insite": {"refined_rows": int((st >= 0).sum()), "converged": int((st == 0).sum()),
                    "zoom_failed_fallback": int((st == 3).sum()), "mean_bfgs_iterations": float(it[st >= 0].mean()),
+                   "lane_order": "identity (lane = row: coalesced time-major V)",
+                   "binned_by_seq_len_ms_per_step": ms_binned,
                    "reference_wall_time_s": "88.96 s per INSITE EQ_4_A run incl. 59,000 + 11,800 refinements "
                                             "(results/2_main_table/final_with_insite.txt:2346; SURVEY.md §6)"},
     }

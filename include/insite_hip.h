@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define INSITE_ABI_VERSION 3
+#define INSITE_ABI_VERSION 4
 
 /* status codes */
 #define INSITE_OK 0
@@ -286,12 +286,16 @@ int32_t insite_rk45_order_i32(const int32_t* n_obs, int64_t n_rows, int32_t T_ma
  *            run register-resident, denser models up to n_arms * F run the scratch-resident kernel)
  *   preds    [T, ld_p] f64 (row k = state after step k); coef_out [n_rows, n_arms, F] (may be NULL);
  *   status_out [n_rows] int32 (-1 = not refined: seq_len <= tau; else the BFGS status: 0 converged,
- *   1 maxiter, 3 zoom failed, 5 line-search maxiter), iters_out [n_rows] int32 (may be NULL). */
+ *   1 maxiter, 3 zoom failed, 5 line-search maxiter), iters_out [n_rows] int32 (may be NULL).
+ *   row_order [n_rows] int32 (ABI 4; may be NULL = identity): lane i refines row row_order[i], a
+ *   permutation of 0..n_rows-1 -- scheduling only (outputs are per row, bitwise independent of it); rows
+ *   binned by seq_len (insite_rk45_order_i32 on seq_len) keep a wave's objective scans equally long. */
 int32_t insite_refine_f64(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, int64_t ld_arm,
                           const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics, const int8_t* exps,
                           int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam, int32_t tau,
                           int32_t substeps, int32_t revert_on_zoom_fail, double* preds, int64_t ld_p,
-                          double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream);
+                          double* coef_out, int32_t* status_out, int32_t* iters_out, const int32_t* row_order,
+                          void* stream);
 
 /* INSITE refinement with int8 per-step arms, n_arms <= 4: the cancer_sim / EQ_5 branches of
  * _get_fine_tuned_predictions (sindy.py:484-550: pred_dy_dt picks all_reduced_coefs[argmax(treatment)])
@@ -301,7 +305,8 @@ int32_t insite_refine_arms_f64(const double* V, int64_t ld_v, int32_t T, const i
                                const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
                                const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt,
                                double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail, double* preds,
-                               int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream);
+                               int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out,
+                               const int32_t* row_order, void* stream);
 
 /* General one-state discovery (insite_gen.hip): libraries with state exponents up to 4 and/or per-step
  * binary treatment INPUTS — the reference's degree-4 ablation (PolynomialLibrary(degree=4,

@@ -2418,6 +2418,7 @@ struct RefineArgs {
   double* coef_out;     // [N, A, F] or NULL
   int32_t* status;      // [N] or NULL (-1 skipped, else the BFGS status)
   int32_t* iters;       // [N] or NULL
+  const int32_t* order; // [N] lane -> row (rows binned by seq_len, insite_rk45_order_i32), NULL = identity
   int64_t ldv, lda, ldp, N;
   int32_t T, tau, sub, A, m, n_total;
   int32_t revert3;      // 1: BFGS status 3 reverts to the global model (sindy.py:628-631); 0: keep the iterate
@@ -2571,8 +2572,12 @@ template <int M, int NA>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M <= 4 ? INSITE_REFINE_WPE4 : (M <= 8 ? INSITE_REFINE_WPE8 : 1))))
 insite_refine_kernel(RefineArgs ra, LibDesc lib) {
   constexpr int RU = RefineLane<M, NA>::RU;
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= ra.N) return;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= ra.N) return;
+  // lane -> row: with rows binned by seq_len the lanes of a wave scan similar prefixes (K = sl - tau steps
+  // per objective evaluation), so a wave no longer runs every evaluation to its longest row's length;
+  // every row's computation is independent of its lane, so outputs are bitwise the same in any order
+  const int64_t p = ra.order ? (int64_t)ra.order[gid] : gid;
   double uu[INSITE_MAX_STATICS];
 #pragma unroll RU
   for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < lib.U ? ra.u[p * lib.U + t] : 0.0;
@@ -3853,7 +3858,8 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
                       int64_t ld_arm, const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
                       const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam,
                       int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail, double* preds, int64_t ld_p,
-                      double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream) {
+                      double* coef_out, int32_t* status_out, int32_t* iters_out, const int32_t* row_order,
+                      void* stream) {
   const bool bits = arm8 == nullptr;
   if (n_rows < 0 || T < 1 || n_arms < 1 || n_arms > (bits ? 2 : 4) || substeps < 1 || !(dt > 0.0) ||
       !(lam >= 0.0) || tau < 0 || ld_v < n_rows || ld_p < n_rows ||
@@ -3874,6 +3880,7 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
   ra.coef_out = coef_out;
   ra.status = status_out;
   ra.iters = iters_out;
+  ra.order = row_order;
   ra.ldv = ld_v;
   ra.lda = ld_arm;
   ra.ldp = ld_p;
@@ -3922,23 +3929,25 @@ int32_t insite_refine_f64(const double* V, int64_t ld_v, int32_t T, const uint32
                           const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics, const int8_t* exps,
                           int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam, int32_t tau,
                           int32_t substeps, int32_t revert_on_zoom_fail, double* preds, int64_t ld_p,
-                          double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream) {
+                          double* coef_out, int32_t* status_out, int32_t* iters_out, const int32_t* row_order,
+                          void* stream) {
   if (!arm_bits && n_rows > 0) return INSITE_E_INVALID_ARG;
   return refine_launch(V, ld_v, T, arm_bits, nullptr, ld_arm, u, seq_len, n_rows, n_statics, exps, n_terms, coef0,
                        n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds, ld_p, coef_out, status_out,
-                       iters_out, stream);
+                       iters_out, row_order, stream);
 }
 
 int32_t insite_refine_arms_f64(const double* V, int64_t ld_v, int32_t T, const int8_t* arm, int64_t ld_arm,
                                const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
                                const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt,
                                double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail, double* preds,
-                               int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out, void* stream) {
+                               int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out,
+                               const int32_t* row_order, void* stream) {
   if (!arm && n_rows > 0) return INSITE_E_INVALID_ARG;
   static const int8_t kNoArms = 0;  // non-null marker for the int8 format when n_rows == 0
   return refine_launch(V, ld_v, T, nullptr, arm ? arm : &kNoArms, ld_arm, u, seq_len, n_rows, n_statics, exps,
                        n_terms, coef0, n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds, ld_p, coef_out,
-                       status_out, iters_out, stream);
+                       status_out, iters_out, row_order, stream);
 }
 
 size_t insite_masked_sse_workspace_bytes(int64_t n_rows, int32_t T) {

@@ -644,13 +644,17 @@ def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_ob
 
 def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: torch.Tensor, coef0: np.ndarray,
                   lib: PolyLibrary, dt: float, lam: float, tau: int, substeps: int = 5,
-                  revert_on_zoom_fail: bool = False):
+                  revert_on_zoom_fail: bool = False, binned: bool = False):
     """INSITE per-patient refinement (reference sindy.py:433-715).  V [N, T] f64 unscaled observations
     and arm [N, T] int8 per-step arms in the reference's patient-major layout (transposed to the
     kernel's time-major layout here), u [N, U], seq_len [N], coef0 the HOST global model [A, F].
     A <= 2: insite_refine_f64 on bit-packed arms; A <= 4 (cancer_sim / EQ_5): insite_refine_arms_f64
     on int8 arms.  ``revert_on_zoom_fail``: BFGS status 3 falls back to coef0 as sindy.py:628-631 reads;
     the default (False) keeps the iterate, which reproduces the reference's published runs.
+    ``binned``: lanes take the rows sorted by seq_len (insite_rk45_order_i32 on the device), so a wave's
+    objective scans have similar lengths; scheduling only, the outputs are bitwise the same.  Off by
+    default: on the time-major V the binned lanes' scattered loads cost more than the shorter scans save
+    (1M rows, seq_len U{1..59}: 10.7 vs 9.5 ms, profiles/r02_v10_insite_bench.log).
     Returns (preds [N, T], coef [N, A, F], status [N], iterations [N])."""
     _dev("V", V, torch.float64, 2)
     _dev("arm", arm, torch.int8, 2)
@@ -685,7 +689,8 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
             c0.ctypes.data_as(ctypes.c_void_p), A, float(dt), float(lam), int(tau), int(substeps),
             int(bool(revert_on_zoom_fail)), _p(preds),
             preds.stride(0), _p(coef), _p(status), _p(iters))
-    _run((name, args, dev, None))
+    order = rk45_order(seq_len, T) if (binned and N > 64) else None
+    _run((name, args + (_p(order) if order is not None else ctypes.c_void_p(0),), dev, None))
     return preds.t(), coef, status, iters
 
 

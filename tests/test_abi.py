@@ -62,7 +62,7 @@ def test_nm_shows_c_linkage():
 
 def test_version_and_strerror(L):
     from insite_amd import _lib
-    assert L.insite_abi_version() == _lib.ABI_VERSION == 3
+    assert L.insite_abi_version() == _lib.ABI_VERSION == 4
     assert L.insite_strerror(0) == b"ok"
     for code in (-1, -2, -3, -4):
         s = L.insite_strerror(code)

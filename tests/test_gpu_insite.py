@@ -223,3 +223,33 @@ def test_plugin_insite_four_arms(dev, name, n_statics):
     for i in range(0, N, 23):
         rp, *_ = Q.refine_patient(V[i], arms[i], uq[i], int(sl[i]), c0, ex, m.dt, 10.0, 1)
         assert np.sqrt(np.mean((p[i] - rp) ** 2)) <= 1e-6, i
+
+
+@pytest.mark.parametrize("n_arms", [2, 4])
+def test_refine_binned_rows_bitwise_equal_identity_order(dev, n_arms):
+    """Rows binned by seq_len (ABI 4 row_order, the default) are scheduling only: preds, coefficients,
+    statuses and iteration counts are bitwise those of the identity lane order (ragged seq_len, incl.
+    rows <= tau that are skipped)."""
+    from insite_amd import ops, cohort
+    from insite_amd.library import polynomial_library
+    N, T, tau = 20_000, 60, 5
+    coh = cohort.synthetic_pkpd(N, T, seed=4, device=dev, equation="EQ_4_C")
+    V = coh.x[:, :T].contiguous()
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    flip = torch.randint(1, T, (N, 1), generator=g, device=dev)
+    base = coh.arm[:, None].to(torch.int64)
+    if n_arms == 4:
+        base = torch.randint(0, 4, (N, 1), generator=g, device=dev)
+    arm = torch.where(torch.arange(T, device=dev)[None, :] >= flip, (base + 1) % n_arms, base).to(torch.int8)
+    sl = torch.randint(1, T + 1, (N,), generator=g, device=dev, dtype=torch.int32)
+    lib = polynomial_library(2, 2, True)
+    c0 = np.zeros((n_arms, lib.n_terms))
+    c0[:, 4] = -1.1
+    c0[1, 1], c0[1, 5] = -0.145, -1.02
+    outs = [ops.insite_refine(V, arm.contiguous(), coh.u, sl, c0, lib, 10.0 / T, 10.0, tau, binned=b)
+            for b in (True, False)]
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert (outs[0][2][sl <= tau] == -1).all() and (outs[0][2][sl > tau] >= 0).all()
