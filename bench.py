@@ -53,6 +53,10 @@ def parse():
                          "rollout on two streams, consecutive steps overlapped; fused (N = 1): ONE step_kernel launch "
                          "per step -- the discovery of step i and the rollout of step i-1 in the same launch; seq: "
                          "eager launches on one stream; graph: the seq step in a HIP graph")
+    ap.add_argument("--stlsq-stream", default="discovery", choices=["discovery", "rollout"],
+                    help="pipeline mode, N = 1: run each step's STLSQ in the gram's last block on the discovery "
+                         "stream (default) or as its own launch on the rollout stream ahead of that step's rollout "
+                         "(off the discovery stream's critical path)")
     ap.add_argument("--no-fused", action="store_true",
                     help="pipeline mode at N = 1: skip the secondary fused-step measurement")
     ap.add_argument("--gram-blocks", type=int, default=0,
@@ -1080,6 +1084,8 @@ def main():
     g_fast = [p.bind(s_g) for p in gram_plans]
     c_fast = [p.bind(s_g) for p in stlsq_plans]
     r_fast = [p.bind(s_rs[(j // K) % RS]) for j, p in enumerate(roll_plans)]
+    stl_roll = world == 1 and mode == "pipeline" and args.stlsq_stream == "rollout"
+    c_roll = [p.bind(s_rs[(j // K) % RS]) for j, p in enumerate(stlsq_plans)] if stl_roll else None
 
     def discover(i, st):
         """Discovery of step i on stream st (used by seq / graph and the roofline pass)."""
@@ -1119,7 +1125,9 @@ def main():
                     hip.wait(hs_g, done_r[b % NBE][1])
         if tev and i % K == 0:
             hip.record(tev[0], hs_g)
-        if world == 1:
+        if stl_roll:
+            g_fast[j]()                             # gram + in-launch reduction (STLSQ: rollout stream)
+        elif world == 1:
             f_fast[j]()                             # gram + in-launch reduction, STLSQ
         else:
             g_fast[j]()
@@ -1143,6 +1151,8 @@ def main():
         if tev:
             hip.record(tev[2], hs_r)
         for k in pending:
+            if stl_roll:
+                c_roll[k % NB]()
             r_fast[k % NB]()
         if tev:
             hip.record(tev[3], hs_r)
@@ -1256,7 +1266,8 @@ def main():
                 "workload": f"C2: PK/PD {N // 1000}k patients/GPU x {T} steps fp64 - discovery (savgol+FD4+poly2 "
                             f"library+Gram, RCCL all-reduce when N>1, STLSQ) + {args.method.upper()} counterfactual rollout",
                 "patients_per_gpu": N, "T": T, "rows_per_patient": T - 2, "library_terms": F,
-                "parallelism": f"patient-shard x{world}", "mode": mode, "discovered_support": sup.tolist(), "finite": ok,
+                "parallelism": f"patient-shard x{world}", "mode": mode, "stlsq_stream": "rollout" if stl_roll else "discovery",
+                "discovered_support": sup.tolist(), "finite": ok,
             },
             "host_submit_ms_per_step": host_ms,
             "roofline": {

@@ -81,14 +81,28 @@ struct LibDesc {
   int8_t qatom[16];                            // Q column c = atom[qatom] * moment[qmom]
   int8_t qmom[16];  // 0: row count, 1: sum xs, 2: sum xs^2, 3: sum xdot, 4: sum xdot*xs
   int8_t qcol[kMaxEntries];
+  // the same exponents packed into aligned dwords for loops with a run-time (wave-uniform) column or atom
+  // index: a dynamically indexed int8 field of the by-value kernel argument compiles to a VECTOR byte load
+  // plus s_waitcnt vmcnt(0) per iteration (no scalar byte loads on gfx9), which drained the gram's load
+  // queue per atom of every work item; dword fields become scalar loads.
+  int32_t ucode[INSITE_MAX_TERMS];  // column j: eu[j][0] | eu[j][1] << 8 | eu[j][2] << 16 | ex[j] << 24
+  int32_t acode[16];                // atom a: atom_exp[a][0] | [1] << 8 | [2] << 16
 };
 
-__device__ __forceinline__ double monomial(const LibDesc& lib, int j, const double* u) {
+// prod_i u[i]^((code >> 8 i) & 0xff): the u-monomial of a packed column / atom code
+__device__ __forceinline__ double monomial_code(int code, const double* u) {
   double m = 1.0;
-  for (int i = 0; i < lib.U; ++i)
-    for (int e = 0; e < lib.eu[j][i]; ++e) m *= u[i];
+#pragma unroll
+  for (int i = 0; i < INSITE_MAX_STATICS; ++i) {
+    const int e = (code >> (8 * i)) & 0xff;
+    for (int k = 0; k < e; ++k) m *= u[i];
+  }
   return m;
 }
+__device__ __forceinline__ double monomial(const LibDesc& lib, int j, const double* u) {
+  return monomial_code(lib.ucode[j] & 0xffffff, u);
+}
+__device__ __forceinline__ int col_ex(const LibDesc& lib, int j) { return (lib.ucode[j] >> 24) & 0xff; }
 
 // =============================================================================================
 // Discovery: fused smoothing + FD + library + Gram
@@ -551,6 +565,11 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
       // ---- remaining tiles of the segment (buffers alternate A, B; two tiles in flight) ----
       auto consume = [&](int t0, const auto& v) {
         if (t0 + kGT <= Lmin) {
+#ifdef INSITE_ABLATE_GRAM_NOCOMPUTE  // profiling only: stream the samples, one add per step
+#pragma unroll
+          for (int i = 0; i < kGT; ++i) Sx += sample(v, i);
+          return;
+#endif
 #pragma unroll
           for (int i = 0; i < kGT; ++i) {
             xr[i & 7] = sample(v, i);
@@ -693,9 +712,10 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
         wave_lds_sync();
         if ((lane >> 5) == h) {
           double* row = ps + (lane & 31) * kRS;
-          for (int a = 0; a < lib.n_atoms; ++a) {  // uniform loop; exponents <= 2
+          for (int a = 0; a < lib.n_atoms; ++a) {  // uniform loop; exponents <= 2 (scalar loads of acode)
+            const int c = lib.acode[a];
+            const int e0 = c & 0xff, e1 = (c >> 8) & 0xff, e2 = (c >> 16) & 0xff;
             double m = 1.0;
-            const int e0 = lib.atom_exp[a][0], e1 = lib.atom_exp[a][1], e2 = lib.atom_exp[a][2];
             if (e0 >= 1) m *= uu[0];
             if (e0 >= 2) m *= uu[0];
             if (e1 >= 1) m *= uu[1];
@@ -1259,7 +1279,7 @@ patient_fit_kernel(const double* __restrict__ mom, const double* __restrict__ u,
 #pragma unroll
   for (int j = 0; j < F; ++j) {
     m[j] = monomial(lib, j, uu);
-    e[j] = lib.ex[j];
+    e[j] = col_ex(lib, j);
   }
 #pragma unroll
   for (int i = 0; i < F; ++i) {
@@ -1456,7 +1476,7 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(RolloutArgs ra, LibDesc
       const double c = cbase[a * lib.F + j];
       if (fabs(c) > ra.drop) {
         const double t = c * monomial(lib, j, uu);
-        if (lib.ex[j] == 0) alpha[a] += t;
+        if (col_ex(lib, j) == 0) alpha[a] += t;
         else beta[a] += t;
       }
     }
@@ -1612,7 +1632,7 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
           const double c = cbase[a * lib.F + j];
           if (fabs(c) > ra.drop) {
             const double t = c * monomial(lib, j, uu);
-            if (lib.ex[j] == 0) al += t;
+            if (col_ex(lib, j) == 0) al += t;
             else be += t;
           }
         }
@@ -1719,7 +1739,7 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
         const double c = cbase[a * lib.F + j];
         if (fabs(c) > ra.drop) {
           const double t = c * monomial(lib, j, uu);
-          if (lib.ex[j] == 0) alpha[q][a] += t;
+          if (col_ex(lib, j) == 0) alpha[q][a] += t;
           else beta[q][a] += t;
         }
       }
@@ -2008,7 +2028,7 @@ rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
       const double c = cbase[a * lib.F + j];
       if (fabs(c) > ra.drop) {
         const double t = c * monomial(lib, j, uu);
-        if (lib.ex[j] == 0) alpha[a] += t;
+        if (col_ex(lib, j) == 0) alpha[a] += t;
         else beta[a] += t;
       }
     }
@@ -2826,7 +2846,7 @@ insite_refine_kernel(RefineArgs ra, LibDesc lib) {
     if (a < ra.A)
       for (int j = 0; j < lib.F; ++j) {
         const double t = coef_at(a * lib.F + j) * monomial(lib, j, uu);
-        if (lib.ex[j] == 0) al[a] += t;
+        if (col_ex(lib, j) == 0) al[a] += t;
         else be[a] += t;
       }
   const double h = ra.dt / (double)ra.sub;
@@ -2959,6 +2979,11 @@ int build_lib(const int8_t* exps, int32_t F, int32_t U, LibDesc* lib) {
     }
     lib->col_atom[j] = (int8_t)found;
   }
+  for (int j = 0; j < F; ++j) {
+    int c = (int)lib->ex[j] << 24;
+    for (int t = 0; t < U; ++t) c |= (int)lib->eu[j][t] << (8 * t);
+    lib->ucode[j] = c;
+  }
   // Q columns: (atom of the column index, moment) pairs, deduplicated; the atom of "1" for b
   int one_atom = -1;
   for (int a = 0; a < lib->n_atoms; ++a)
@@ -2971,6 +2996,8 @@ int build_lib(const int8_t* exps, int32_t F, int32_t U, LibDesc* lib) {
       fits = false;
     }
   }
+  for (int a = 0; a < lib->n_atoms; ++a)
+    lib->acode[a] = (int)lib->atom_exp[a][0] | (int)lib->atom_exp[a][1] << 8 | (int)lib->atom_exp[a][2] << 16;
   lib->nq = 0;
   for (int q = 0; q < lib->nE && fits; ++q) {
     const int i = lib->ei[q], k = lib->ek[q];

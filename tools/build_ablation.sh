@@ -24,6 +24,9 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     STLSEP) NAME=$v build -DINSITE_STLSQ_SEPARATE ;;
     STEPDEPTH3) NAME=$v build -DINSITE_TM_DEPTH=3 ;;
     GT8D4) NAME=$v build -DINSITE_GT=8 -DINSITE_TM_DEPTH=4 ;;
+    GNOCOMP) NAME=$v build -DINSITE_ABLATE_GRAM_NOCOMPUTE ;;
+    GNS2) NAME=$v build -DINSITE_GRAM_NS_MIN=2 ;;
+    GNOGPH) NAME=$v build -DINSITE_ABLATE_NOGPHASE ;;
     GT8D3) NAME=$v build -DINSITE_GT=8 -DINSITE_TM_DEPTH=3 ;;
     GT8D5) NAME=$v build -DINSITE_GT=8 -DINSITE_TM_DEPTH=5 ;;
     MS4NOEMIT) NAME=$v build -DINSITE_MS4_ABL_NOEMIT=1 ;;
