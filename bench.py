@@ -1033,7 +1033,10 @@ def main():
     K, RS, WAR_EVERY = 4, 2, 8
     NB = 3 * K * RS                     # a multiple of K * RS: step k's y buffer (k // K) % RS is fixed per coef slot
     NBE = NB // K                       # event slots (batches in flight)
-    bufs = [idist.MomentBuffer(2, F, dev) for _ in range(NB)]     # G|b in one buffer: one all-reduce
+    # G|b of K consecutive steps in one flat bucket: at N > 1 the pipeline all-reduces a batch's K systems in
+    # ONE collective (the ~1 KB all-reduce is latency-bound: once per batch, not once per step)
+    buckets = [idist.MomentBucket(K, 2, F, dev) for _ in range(NB // K)]
+    bufs = [buckets[j // K].bufs[j % K] for j in range(NB)]
     coefs = [torch.empty((2, F), dtype=torch.float64, device=dev) for _ in range(NB)]
     masks = [torch.empty((2, F), dtype=torch.int8, device=dev) for _ in range(NB)]
     iters = [torch.empty((2,), dtype=torch.int32, device=dev) for _ in range(NB)]
@@ -1130,10 +1133,7 @@ def main():
         elif world == 1:
             f_fast[j]()                             # gram + in-launch reduction, STLSQ
         else:
-            g_fast[j]()
-            with torch.cuda.stream(s_g):
-                idist.reduce_moments(bufs[j])       # the only collective
-            c_fast[j]()
+            g_fast[j]()                             # gram; the batch's all-reduce + STLSQs in flush()
         pending.append(i)
         if i % K == K - 1:
             flush(tev)
@@ -1143,6 +1143,11 @@ def main():
         if not pending:
             return
         b = pending[0] // K
+        if world > 1:                               # the batch's K systems: one collective, then K STLSQs
+            with torch.cuda.stream(s_g):
+                idist.reduce_bucket(buckets[(pending[0] % NB) // K])   # the only data-path collective
+            for k in pending:
+                c_fast[k % NB]()
         if tev:
             hip.record(tev[1], hs_g)
         hip.record(ev["g", b % NBE], hs_g)

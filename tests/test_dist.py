@@ -149,3 +149,44 @@ def test_metric_sums_all_reduce_gloo_world3():
         np.testing.assert_allclose(red, want, rtol=1e-12)
         np.testing.assert_allclose(det, want, rtol=1e-12)
         assert np.array_equal(x, np.full(5, (0.1 + 0.2) + 0.3))
+
+
+def _bucket_worker(rank, world, port, q):
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from insite_amd import dist as idist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        bk = idist.MomentBucket(4, 2, 7, "cpu")
+        for k, buf in enumerate(bk.bufs):   # every fit's partial: distinct per (rank, step)
+            buf.G.copy_(torch.full((2, 7, 7), 10.0 * k + rank))
+            buf.b.copy_(torch.full((2, 7), -(10.0 * k + rank)))
+        idist.reduce_bucket(bk)
+        q.put((rank, [(b.G.clone().numpy(), b.b.clone().numpy()) for b in bk.bufs]))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_reduces_every_fit_in_one_collective():
+    """The C2 pipeline's N > 1 batching: K fits' G|b views of one flat buffer, one all-reduce (gloo, 2
+    ranks): every view holds the sum over ranks of its own fit's partial."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        for k, (G, b) in enumerate(res[r]):
+            want = sum(10.0 * k + rr for rr in range(world))
+            assert np.all(G == want) and np.all(b == -want)
+
