@@ -795,8 +795,11 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
   INSITE_TREAL(blockIdx.x * kWavesPerBlock + wid, 9);
 }
 
+#ifndef INSITE_GRAM_WPE
+#define INSITE_GRAM_WPE 2  // waves per SIMD the gram's register budget is sized for (2: <= 256 VGPR+AGPR)
+#endif
 template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM, int STF = 0>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2)))  // <= 256 VGPR+AGPR
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_GRAM_WPE)))
 gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
             const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, int seg, int n_seg,
             GramW w, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ cnt, GramOut out) {
