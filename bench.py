@@ -493,12 +493,58 @@ def c5_main(args):
         dist.destroy_process_group()
 
 
+def _cpu_refine_chunk(bounds):
+    from oracle import insite_ref as R
+    from oracle import insite_refine_ref as Q
+    lo, hi = bounds
+    d = _CPU
+    ex = R.poly_library(3, 2, True)
+    for i in range(lo, hi):
+        Q.refine_patient(d["V"][i], d["arm"][i], d["u"][i], int(d["sl"][i]), d["c0"], ex, d["dt"], 10.0, 5)
+    return hi - lo
+
+
+def insite_cpu_baseline(seed, per_worker=2000):
+    """Bounded CPU sample of the F2 workload on the host's workers: the oracle's restatement of the jax
+    BFGS refinement (oracle/insite_refine_ref.py) on rows of the same shape (EQ_4_C, T = 60, seq_len
+    U{1..59}, arm flipped at a random step), per_worker rows per worker."""
+    import multiprocessing as mp
+    sys.path.insert(0, ROOT)
+    from oracle import insite_ref as R
+    info = host_info()
+    W = info["workers"]
+    n = W * per_worker
+    rng = np.random.default_rng(seed + 9)
+    T = 60
+    p = R.draw_params(n, "EQ_4_C", rng)
+    sim = R.simulate_factual(p, T, rng, "EQ_4_C", 2.0)
+    arm0 = sim["treatment_application"][:, 0].astype(np.int64)
+    flip = rng.integers(1, T, size=(n, 1))
+    c0 = np.zeros((2, 7))
+    c0[0, 4], c0[1, 1], c0[1, 5] = -1.1107592869834308, -0.14540553723951796, -1.0234639833519243
+    _CPU.update(V=sim["cancer_volume"][:, :T], arm=np.where(np.arange(T)[None, :] >= flip, 1 - arm0[:, None],
+                                                             arm0[:, None]).astype(np.int8),
+                u=np.stack([sim["observed_static_c_0"], sim["observed_static_c_1"]], axis=1),
+                sl=rng.integers(1, T, size=n), c0=c0, dt=10.0 / T)
+    chunks = [(int(a[0]), int(a[-1]) + 1) for a in np.array_split(np.arange(n), W) if a.size]
+    with mp.get_context("fork").Pool(W, initializer=_cpu_worker_init) as pool:
+        pool.map(abs, range(W))
+        t0 = time.perf_counter()
+        pool.map(_cpu_refine_chunk, chunks)
+        el = time.perf_counter() - t0
+    return {"value": n / el, "unit": "patient-trajectories/s", "cores": W, "kind": "port",
+            "sample": f"oracle/insite_refine_ref.py (jax BFGS restated, numpy) on {n} EQ_4_C rows (T = 60, seq_len "
+                      f"U{{1..59}}) over a {W}-process pool, {el:.2f} s", "host": info}
+
+
 def insite_main(args):
     """INSITE per-patient refinement (reference sindy.py:433-715): every row of a
     counterfactual evaluation set refines the global EQ_4_C model by BFGS on its observed prefix
     (tau = 5) and rolls its model out with Euler-5.  Rows: PK/PD trajectories of T = 60 observations,
     sequence lengths U{1..59}, per-step arms (factual arm, flipped at a random step).  One step = one
     refinement of every row (1M rows; the reference's tau-step test set has 59,000)."""
+    # the CPU leg first, while this process has no GPU context (its worker pool forks)
+    cpu = None if args.no_cpu_baseline else insite_cpu_baseline(args.seed)
     from insite_amd import ops, cohort
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -547,20 +593,8 @@ def insite_main(args):
                    "reference_wall_time_s": "88.96 s per INSITE EQ_4_A run incl. 59,000 + 11,800 refinements "
                                             "(results/2_main_table/final_with_insite.txt:2346; SURVEY.md §6)"},
     }
-    if not args.no_cpu_baseline:
-        sys.path.insert(0, ROOT)
-        from oracle import insite_ref as R
-        from oracle import insite_refine_ref as Q
-        n_s = 300
-        Vh, ah, uh, sh = V[:n_s].cpu().numpy(), arm[:n_s].cpu().numpy(), coh.u[:n_s].cpu().numpy(), sl[:n_s].cpu().numpy()
-        ex = R.poly_library(3, 2, True)
-        t1 = time.perf_counter()
-        for i in range(n_s):
-            Q.refine_patient(Vh[i], ah[i], uh[i], int(sh[i]), c0, ex, dt, 10.0, 5)
-        el = time.perf_counter() - t1
-        out["cpu_baseline"] = {"value": n_s / el, "unit": "patient-trajectories/s", "cores": 1, "kind": "port",
-                               "sample": f"oracle/insite_refine_ref.py (jax BFGS restated, numpy) on {n_s} rows, "
-                                         f"{el:.2f} s"}
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     print(json.dumps(out))
 
 
