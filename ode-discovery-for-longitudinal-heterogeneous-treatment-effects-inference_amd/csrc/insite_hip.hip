@@ -1370,6 +1370,44 @@ struct RolloutArgs {
 };
 
 
+// Per-patient affine rates of every arm, f_a(y) = alpha_a + beta_a y: columns with x-exponent 0 feed alpha,
+// exponent 1 beta (terms with |c| <= drop dropped, sindy.py:388).  The lane's A x F coefficients are loaded
+// first, every load from a clamped (valid) index so all of them are in flight at once -- a loop over the
+// run-time F with the load inside issued one load and one wait per term (a per-patient-coefficient row at
+// C4 sizes: 14 dependent HBM round trips before the first step); the column codes are dword scalar loads.
+// Accumulation order (j ascending per arm) is that of the reference's term sum.
+template <int NARM>
+__device__ __forceinline__ void affine_rates(const LibDesc& lib, const double* cbase, int A, double drop,
+                                             const double* uu, double* alpha, double* beta) {
+  double cv[NARM][INSITE_MAX_TERMS];
+#pragma unroll
+  for (int a = 0; a < NARM; ++a)
+#pragma unroll
+    for (int j = 0; j < INSITE_MAX_TERMS; ++j) {
+      const int aa = a < A ? a : 0, jj = j < lib.F ? j : 0;
+      cv[a][j] = cbase[aa * lib.F + jj];
+    }
+#pragma unroll
+  for (int a = 0; a < NARM; ++a) alpha[a] = beta[a] = 0.0;
+#pragma unroll
+  for (int j = 0; j < INSITE_MAX_TERMS; ++j) {
+    if (j < lib.F) {
+      const int code = lib.ucode[j];
+      const double m = monomial_code(code & 0xffffff, uu);
+      const bool lin = (code >> 24) != 0;
+#pragma unroll
+      for (int a = 0; a < NARM; ++a) {
+        if (a < A) {
+          const double c = cv[a][j];
+          const double v = fabs(c) > drop ? c * m : 0.0;
+          if (lin) beta[a] += v;
+          else alpha[a] += v;
+        }
+      }
+    }
+  }
+}
+
 // Interval propagator.  Every library of this ABI is affine in the state (INSITE_MAX_STATE_DEGREE
 // 1), so per arm the RHS is f(y) = al + be * y with al, be fixed per patient, and one observation
 // interval of either integrator is an affine map y <- A y + B whose coefficients are loop
@@ -1468,22 +1506,8 @@ __global__ void __launch_bounds__(kBlock) rollout_kernel(RolloutArgs ra, LibDesc
     const double q = ra.u[pc * lib.U + (t < lib.U ? t : 0)];
     uu[t] = (active && t < lib.U) ? q : 0.0;
   }
-  double alpha[NARM], beta[NARM];
-  const double* cbase = ra.coef + (PERROW ? pc * ra.coef_stride : 0);
-#pragma unroll
-  for (int a = 0; a < NARM; ++a) {
-    alpha[a] = 0.0;
-    beta[a] = 0.0;
-    if (a >= ra.A) continue;  // padded arm slot (n_arms = 3 -> NARM = 4)
-    for (int j = 0; j < lib.F; ++j) {
-      const double c = cbase[a * lib.F + j];
-      if (fabs(c) > ra.drop) {
-        const double t = c * monomial(lib, j, uu);
-        if (col_ex(lib, j) == 0) alpha[a] += t;
-        else beta[a] += t;
-      }
-    }
-  }
+  double alpha[NARM], beta[NARM];  // padded arm slots (n_arms = 3 -> NARM = 4) stay 0
+  affine_rates<NARM>(lib, ra.coef + (PERROW ? pc * ra.coef_stride : 0), ra.A, ra.drop, uu, alpha, beta);
   const double y0 = ra.y0[pc];
   double y = active ? y0 : 0.0;
   const double h = ra.dt / (double)ra.substeps;
@@ -1625,23 +1649,11 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
       const double v = ra.u[pc * lib.U + (t < lib.U ? t : 0)];
       uu[t] = (act && t < lib.U) ? v : 0.0;
     }
-    const double* cbase = ra.coef + (PERROW ? pc * ra.coef_stride : 0);
+    double al[NARM], be[NARM];
+    affine_rates<NARM>(lib, ra.coef + (PERROW ? pc * ra.coef_stride : 0), ra.A, ra.drop, uu, al, be);
     const double h = ra.dt / (double)ra.substeps;
 #pragma unroll
-    for (int a = 0; a < NARM; ++a) {
-      double al = 0.0, be = 0.0;
-      if (a < ra.A) {
-        for (int j = 0; j < lib.F; ++j) {
-          const double c = cbase[a * lib.F + j];
-          if (fabs(c) > ra.drop) {
-            const double t = c * monomial(lib, j, uu);
-            if (col_ex(lib, j) == 0) al += t;
-            else be += t;
-          }
-        }
-      }
-      interval_propagator(METHOD, ra.substeps, h, al, be, PA[a], PB[a]);
-    }
+    for (int a = 0; a < NARM; ++a) interval_propagator(METHOD, ra.substeps, h, al[a], be[a], PA[a], PB[a]);
     const double v0 = ra.y0[pc];
     y = act ? v0 : 0.0;
   }
@@ -1732,21 +1744,7 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
       const double v = ra.u[pc * lib.U + (t < lib.U ? t : 0)];
       uu[t] = (act[q] && t < lib.U) ? v : 0.0;
     }
-    const double* cbase = ra.coef + (PERROW ? pc * ra.coef_stride : 0);
-#pragma unroll
-    for (int a = 0; a < NARM; ++a) {
-      alpha[q][a] = 0.0;
-      beta[q][a] = 0.0;
-      if (a >= ra.A) continue;
-      for (int j = 0; j < lib.F; ++j) {
-        const double c = cbase[a * lib.F + j];
-        if (fabs(c) > ra.drop) {
-          const double t = c * monomial(lib, j, uu);
-          if (col_ex(lib, j) == 0) alpha[q][a] += t;
-          else beta[q][a] += t;
-        }
-      }
-    }
+    affine_rates<NARM>(lib, ra.coef + (PERROW ? pc * ra.coef_stride : 0), ra.A, ra.drop, uu, alpha[q], beta[q]);
     const double v0 = ra.y0[pc];
     y[q] = act[q] ? v0 : 0.0;
   }
@@ -2114,35 +2112,6 @@ rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
     if (on) __builtin_nontemporal_store(y, ra.y + (int64_t)k * ra.ldy + p);
   }
   if (act && ra.steps) ra.steps[p] = attempts;
-}
-
-// Per-patient affine rates of every arm, f_a(y) = alpha_a + beta_a y: columns with x-exponent 0 feed alpha,
-// exponent 1 beta.  Loops run over the descriptor's compile-time bounds (F <= INSITE_MAX_TERMS, U <=
-// INSITE_MAX_STATICS, u-exponents <= 8 checked by build_lib) so every descriptor byte is read at a constant
-// kernel-argument offset (scalar loads issued together), not one dependent vector load per term.
-template <int NARM>
-__device__ __forceinline__ void affine_rates(const LibDesc& lib, const double* cbase, int A, double drop,
-                                             const double* uu, double* alpha, double* beta) {
-#pragma unroll
-  for (int a = 0; a < NARM; ++a) alpha[a] = beta[a] = 0.0;
-#pragma unroll
-  for (int j = 0; j < INSITE_MAX_TERMS; ++j) {
-    if (j >= lib.F) break;
-    double m = 1.0;
-#pragma unroll
-    for (int i = 0; i < INSITE_MAX_STATICS; ++i)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) m *= e < lib.eu[j][i] ? uu[i] : 1.0;
-    const bool lin = lib.ex[j] != 0;
-#pragma unroll
-    for (int a = 0; a < NARM; ++a) {
-      if (a >= A) break;
-      const double c = cbase[a * lib.F + j];
-      const double v = fabs(c) > drop ? c * m : 0.0;
-      if (lin) beta[a] += v;
-      else alpha[a] += v;
-    }
-  }
 }
 
 // Flat-loop form of the same controller (the default).  Each lane runs its own state machine over
