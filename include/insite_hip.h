@@ -211,6 +211,26 @@ int32_t insite_sindy_fit_per_patient_f64(const double* x, int64_t ldx, int32_t l
                                          double* coef_out, int8_t* mask_out, int32_t* iters_out, void* workspace,
                                          size_t workspace_bytes, void* stream);
 
+/* Global and per-patient fits from ONE pass over x (config C4, ABI 4).  insite_gram_moments_f64 is
+ * insite_gram_f64 (coef_out NULL) or insite_sindy_fit_f64 (coef_out set) that also writes every patient's
+ * moments mom_out [n_patients, 5] f64 = {rows, sum x, sum x^2, sum xdot, sum xdot x} (the state the
+ * per-patient refit needs); insite_fit_per_patient_moments_f64 is the per-patient STLSQ of
+ * insite_sindy_fit_per_patient_f64 from those moments (global_coef on the device: the fused fit's
+ * coef_out, or the all-reduced model at N > 1).  Together they replace insite_sindy_fit_f64 +
+ * insite_sindy_fit_per_patient_f64, which read x twice.  Requires the library to fit the MFMA Gram plan
+ * (n_arms * n_terms <= 16; else INSITE_E_UNSUPPORTED).  Workspace: insite_gram_workspace_bytes. */
+int32_t insite_gram_moments_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,
+                                const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics,
+                                int32_t n_arms, const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
+                                double threshold, double alpha, int32_t max_iter, int32_t unbias, double* G_out,
+                                double* b_out, double* coef_out, int8_t* mask_out, int32_t* iters_out, double* mom_out,
+                                void* workspace, size_t workspace_bytes, void* stream);
+int32_t insite_fit_per_patient_moments_f64(const double* mom, const double* u, const int8_t* arm, const int32_t* rows,
+                                           int64_t n_patients, int32_t n_steps, int32_t n_statics, int32_t n_arms,
+                                           const int8_t* exps, int32_t n_terms, const double* global_coef,
+                                           double threshold, double alpha, int32_t max_iter, int32_t unbias,
+                                           double* coef_out, int8_t* mask_out, int32_t* iters_out, void* stream);
+
 /* Batched sequentially-thresholded least squares on Gram systems (one system per thread):
  * STLSQ._reduce semantics (all-ones initial support; ridge (G_SS + alpha I) c = b_S by
  * Cholesky; zero |c| < threshold; stop when nothing was removed in the first pass or the

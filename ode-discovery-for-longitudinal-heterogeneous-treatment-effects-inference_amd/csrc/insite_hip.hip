@@ -203,6 +203,7 @@ struct GramOut {
   int8_t* mask;
   int32_t* iters;
   StlsqParams sp;
+  double* mom;  // MOM = 2: per-patient moments [N, 5]
 };
 
 template <int F>
@@ -316,14 +317,16 @@ static_assert(kTailMaxEnt + 8 + INSITE_MAX_ARMS * (INSITE_MAX_TERMS * INSITE_MAX
 // when the library fits (lib.mfma), else one Gram entry per lane.
 // TM (time-major x[k * ldx + p]): a lane loads its own patient's kGT samples of a tile directly
 // (each wave instruction reads 64 consecutive doubles of one step); no LDS staging or wave sync.
-// MOM: per-patient moments mode (one time segment per patient): instead of the Gram contraction
+// MOM = 1: per-patient moments mode (one time segment per patient): instead of the Gram contraction
 // every lane writes its patient's moments {L, sum xs, sum xs^2, sum xdot, sum xdot xs} to
-// partial[p * 5 ..] (insite_sindy_fit_per_patient_f64).
+// partial[p * 5 ..] (insite_sindy_fit_per_patient_f64).  MOM = 2: both from the same pass -- the moments
+// to out.mom and the Gram with its reduction (insite_gram_moments_f64: C4's global + per-patient fits
+// read x once).
 // Otherwise the block partials are reduced inside the launch (gram_tail) into G [A, F, F] and b [A, F].
 // The body is a device function of a virtual block index / grid size (vblk, vgrid) and the block's LDS,
 // so the fused step kernel (step_kernel) can run it on a subset of its blocks.
 constexpr int kGramSmem = kWavesPerBlock * kWave * kGSlot;  // doubles of LDS per block
-template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM, int STF = 0>
+template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, int MOM, int STF = 0>
 __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, double* __restrict__ smem,
             const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
             const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, int seg, int n_seg,
@@ -683,16 +686,16 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
       }
     }
     if (s0 >= Lmax && !(SMOOTH && sidx == 0)) continue;  // nothing owned by this work item (uniform)
-    if constexpr (MOM) {
+    if constexpr (MOM != 0) {  // 1: moments only (partial = the [N, 5] moments); 2: moments to out.mom + the Gram
       if (p < N) {
-        double* mrow = partial + p * 5;
+        double* mrow = (MOM == 1 ? partial : out.mom) + p * 5;
         mrow[0] = (double)L;
         mrow[1] = Sx;
         mrow[2] = Sxx;
         mrow[3] = Sd;
         mrow[4] = Sdx;
       }
-      continue;
+      if constexpr (MOM == 1) continue;
     }
 #ifdef INSITE_ABLATE_NOGPHASE
     acc[0] += Sx + Sxx + Sd + Sdx;
@@ -768,7 +771,7 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
 
   INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 5);
   // ---- block reduction (fixed order) -> compact partial[block][a * nE + e] -> gram_tail ----
-  if constexpr (MOM) return;
+  if constexpr (MOM == 1) return;
   __syncthreads();
   double* red = smem;
   const int n_ent = out.n_arms * lib.nE;  // the Gram entries the tail needs (<= kTailMaxEnt)
@@ -798,8 +801,11 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
 #ifndef INSITE_GRAM_WPE
 #define INSITE_GRAM_WPE 2  // waves per SIMD the gram's register budget is sized for (2: <= 256 VGPR+AGPR)
 #endif
-template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM, int STF = 0>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_GRAM_WPE)))
+#ifndef INSITE_MOM_WPE
+#define INSITE_MOM_WPE 2  // the per-patient-moments instance (no contraction phase)
+#endif
+template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, int MOM, int STF = 0>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MOM == 1 ? INSITE_MOM_WPE : INSITE_GRAM_WPE)))
 gram_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
             const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, int seg, int n_seg,
             GramW w, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ cnt, GramOut out) {
@@ -1906,7 +1912,7 @@ step_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
             RolloutArgs ra, int gblocks) {
   __shared__ double smem[kGramSmem];
   if ((int)blockIdx.x < gblocks) {
-    gram_body<1, 2, SMOOTH, true, true, false, 7>((int)blockIdx.x, gblocks, smem, x, ldx, n_steps, u, arm, rows, N,
+    gram_body<1, 2, SMOOTH, true, true, 0, 7>((int)blockIdx.x, gblocks, smem, x, ldx, n_steps, u, arm, rows, N,
                                                  seg, n_seg, w, lib, partial, cnt, out);
     return;
   }
@@ -3113,11 +3119,11 @@ struct GramLaunch {
   GramOut out;
 };
 
-template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, bool MOM = false, int STF = 0>
+template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, int MOM = 0, int STF = 0>
 int launch_gram4(hipStream_t st, const GramLaunch& g) {
   auto kern = gram_kernel<VEC, NARM, SMOOTH, MFMA, TM, MOM, STF>;
   GramPlan pl = gram_plan(g.N, g.n_steps, resident_waves(kern));
-  if constexpr (MOM) {  // one segment per patient: the lane holds the patient's complete moments
+  if constexpr (MOM != 0) {  // one segment per patient: the lane holds the patient's complete moments
     const int64_t tiles = (g.N + kWave - 1) / kWave;
     const int64_t gres = resident_waves(kern) / kWavesPerBlock;
     int64_t gb = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -3134,7 +3140,11 @@ int launch_gram4(hipStream_t st, const GramLaunch& g) {
 
 template <int NARM, bool SMOOTH, bool MFMA>
 int launch_gram3(int mode, hipStream_t st, const GramLaunch& g) {  // mode: 0 PM/8-B, 1 PM/16-B, 2 TM
-  if (mode == 3) return launch_gram4<1, NARM, SMOOTH, MFMA, true, false, 7>(st, g);  // TM + fused F = 7 STLSQ
+  if (mode == 3) return launch_gram4<1, NARM, SMOOTH, MFMA, true, 0, 7>(st, g);  // TM + fused F = 7 STLSQ
+  // moments + Gram in one pass (insite_gram_moments_f64): 4 TM + fused F = 7 STLSQ, 5 TM, 6 patient-major
+  if (mode == 4) return launch_gram4<1, NARM, SMOOTH, MFMA, true, 2, 7>(st, g);
+  if (mode == 5) return launch_gram4<1, NARM, SMOOTH, MFMA, true, 2>(st, g);
+  if (mode == 6) return launch_gram4<1, NARM, SMOOTH, MFMA, false, 2>(st, g);
   if (mode == 2) return launch_gram4<1, NARM, SMOOTH, MFMA, true>(st, g);
   if (mode == 1) return launch_gram4<2, NARM, SMOOTH, MFMA, false>(st, g);
   return launch_gram4<1, NARM, SMOOTH, MFMA, false>(st, g);
@@ -3161,9 +3171,9 @@ inline GramW make_gram_w(double dt) {
 
 template <bool SMOOTH>
 int launch_moments(int mode, hipStream_t st, const GramLaunch& g) {
-  if (mode == 2) return launch_gram4<1, 1, SMOOTH, false, true, true>(st, g);
-  if (mode == 1) return launch_gram4<2, 1, SMOOTH, false, false, true>(st, g);
-  return launch_gram4<1, 1, SMOOTH, false, false, true>(st, g);
+  if (mode == 2) return launch_gram4<1, 1, SMOOTH, false, true, 1>(st, g);
+  if (mode == 1) return launch_gram4<2, 1, SMOOTH, false, false, 1>(st, g);
+  return launch_gram4<1, 1, SMOOTH, false, false, 1>(st, g);
 }
 
 // gram kernel with its in-launch reduction to G / b (+ the STLSQ launch when sp.enabled)
@@ -3171,7 +3181,7 @@ int32_t run_discovery(const double* x, int64_t ldx, int32_t layout, int32_t n_st
                       const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
                       const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt, double* G_out, double* b_out,
                       void* workspace, size_t workspace_bytes, void* stream, const StlsqParams& sp,
-                      double* coef_out, int8_t* mask_out, int32_t* iters_out) {
+                      double* coef_out, int8_t* mask_out, int32_t* iters_out, double* mom_out = nullptr) {
   const bool tm = layout == INSITE_LAYOUT_TIME_MAJOR;
   if (layout != INSITE_LAYOUT_PATIENT_MAJOR && !tm) return INSITE_E_INVALID_ARG;
   if (n_patients < 0 || !G_out || !b_out || n_arms < 1 || n_arms > INSITE_MAX_ARMS || ldx < 1 || !(dt > 0.0) ||
@@ -3204,8 +3214,12 @@ int32_t run_discovery(const double* x, int64_t ldx, int32_t layout, int32_t n_st
   const bool fused = false;
 #endif
   const GramLaunch g{x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, part, cnt,
-                     GramOut{G_out, b_out, n_arms, coef_out, mask_out, iters_out, sp}};
-  const int lmode = fused ? 3 : mode;
+                     GramOut{G_out, b_out, n_arms, coef_out, mask_out, iters_out, sp, mom_out}};
+  int lmode = fused ? 3 : mode;
+  if (mom_out) {  // moments + Gram in one pass (the moments need whole trajectories: one segment per patient)
+    if (!lib.mfma) return INSITE_E_UNSUPPORTED;
+    lmode = tm ? (fused ? 4 : 5) : 6;
+  }
   if (na == 1) launch_gram<1>(lmode, smooth, hs, g);
   else if (na == 2) launch_gram<2>(lmode, smooth, hs, g);
   else launch_gram<4>(lmode, smooth, hs, g);
@@ -3392,6 +3406,34 @@ void launch_rollout_tm_m(int narm, bool perrow, int ppl, int afmt, dim3 grid, hi
   else launch_rollout_tm<METHOD, 4>(perrow, ppl, afmt, grid, st, ra, lib);
 }
 
+// one thread per patient: STLSQ from the global support on the patient's moments (patient_fit_kernel)
+int32_t launch_patient_fit(const double* mom, const double* u, const int8_t* arm, const int32_t* rows, int64_t n_patients,
+                           int32_t n_steps, int32_t n_arms, const LibDesc& lib, const double* global_coef,
+                           const StlsqParams& sp, double* coef_out, int8_t* mask_out, int32_t* iters_out,
+                           hipStream_t hs) {
+  const dim3 grid((unsigned)((n_patients + kBlock - 1) / kBlock));
+  switch (lib.F) {
+#define INSITE_PP_CASE(FF)                                                                                      \
+  case FF:                                                                                                     \
+    patient_fit_kernel<FF><<<grid, kBlock, 0, hs>>>(mom, u, arm, rows, n_patients, n_steps, n_arms, lib,        \
+                                                    global_coef, sp, coef_out, mask_out, iters_out);           \
+    break;
+    INSITE_PP_CASE(1)
+    INSITE_PP_CASE(2)
+    INSITE_PP_CASE(3)
+    INSITE_PP_CASE(4)
+    INSITE_PP_CASE(5)
+    INSITE_PP_CASE(6)
+    INSITE_PP_CASE(7)
+    INSITE_PP_CASE(8)
+    INSITE_PP_CASE(9)
+#undef INSITE_PP_CASE
+    default:
+      return INSITE_E_UNSUPPORTED;
+  }
+  return launch_status();
+}
+
 }  // namespace
 
 // =============================================================================================
@@ -3567,6 +3609,37 @@ int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, int32_t layout, int32
                        dt, G_out, b_out, workspace, workspace_bytes, stream, sp, coef_out, mask_out, iters_out);
 }
 
+int32_t insite_gram_moments_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,
+                                const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics,
+                                int32_t n_arms, const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
+                                double threshold, double alpha, int32_t max_iter, int32_t unbias, double* G_out,
+                                double* b_out, double* coef_out, int8_t* mask_out, int32_t* iters_out, double* mom_out,
+                                void* workspace, size_t workspace_bytes, void* stream) {
+  if (!mom_out || max_iter < 0 || !(threshold >= 0.0) || !(alpha >= 0.0)) return INSITE_E_INVALID_ARG;
+  const StlsqParams sp{threshold, alpha, max_iter, unbias, coef_out ? 1 : 0};
+  return run_discovery(x, ldx, layout, n_steps, u, arm, rows, n_patients, n_statics, n_arms, exps, n_terms, fd_kind,
+                       dt, G_out, b_out, workspace, workspace_bytes, stream, sp, coef_out, mask_out, iters_out, mom_out);
+}
+
+int32_t insite_fit_per_patient_moments_f64(const double* mom, const double* u, const int8_t* arm, const int32_t* rows,
+                                           int64_t n_patients, int32_t n_steps, int32_t n_statics, int32_t n_arms,
+                                           const int8_t* exps, int32_t n_terms, const double* global_coef,
+                                           double threshold, double alpha, int32_t max_iter, int32_t unbias,
+                                           double* coef_out, int8_t* mask_out, int32_t* iters_out, void* stream) {
+  if (n_patients < 0 || n_arms < 1 || n_arms > INSITE_MAX_ARMS || n_steps < 0 || max_iter < 0 ||
+      !(threshold >= 0.0) || !(alpha >= 0.0))
+    return INSITE_E_INVALID_ARG;
+  LibDesc lib;
+  int32_t st = build_lib(exps, n_terms, n_statics, &lib);
+  if (st != INSITE_OK) return st;
+  if (n_patients == 0) return INSITE_OK;
+  if (!mom || !arm || !rows || !global_coef || !coef_out || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
+  if (n_statics == 0) u = mom;
+  return launch_patient_fit(mom, u, arm, rows, n_patients, n_steps, n_arms, lib, global_coef,
+                            StlsqParams{threshold, alpha, max_iter, unbias, 1}, coef_out, mask_out, iters_out,
+                            reinterpret_cast<hipStream_t>(stream));
+}
+
 size_t insite_gram_segments_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms) {
   (void)n_terms;
   if (n_patients < 0 || n_arms < 1 || n_arms > INSITE_MAX_ARMS) return 0;
@@ -3635,28 +3708,8 @@ int32_t insite_sindy_fit_per_patient_f64(const double* x, int64_t ldx, int32_t l
   else launch_moments<false>(mode, hs, g);
   st = launch_status();
   if (st != INSITE_OK) return st;
-  const StlsqParams sp{threshold, alpha, max_iter, unbias, 1};
-  const dim3 grid((unsigned)((n_patients + kBlock - 1) / kBlock));
-  switch (n_terms) {
-#define INSITE_PP_CASE(FF)                                                                                      \
-  case FF:                                                                                                     \
-    patient_fit_kernel<FF><<<grid, kBlock, 0, hs>>>(mom, u, arm, rows, n_patients, n_steps, n_arms, lib,        \
-                                                    global_coef, sp, coef_out, mask_out, iters_out);           \
-    break;
-    INSITE_PP_CASE(1)
-    INSITE_PP_CASE(2)
-    INSITE_PP_CASE(3)
-    INSITE_PP_CASE(4)
-    INSITE_PP_CASE(5)
-    INSITE_PP_CASE(6)
-    INSITE_PP_CASE(7)
-    INSITE_PP_CASE(8)
-    INSITE_PP_CASE(9)
-#undef INSITE_PP_CASE
-    default:
-      return INSITE_E_UNSUPPORTED;
-  }
-  return launch_status();
+  return launch_patient_fit(mom, u, arm, rows, n_patients, n_steps, n_arms, lib, global_coef,
+                            StlsqParams{threshold, alpha, max_iter, unbias, 1}, coef_out, mask_out, iters_out, hs);
 }
 
 int32_t insite_stlsq_f64(const double* G, const double* b, int64_t n_sys, int32_t n_terms,

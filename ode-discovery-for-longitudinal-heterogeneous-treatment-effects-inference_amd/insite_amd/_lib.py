@@ -43,6 +43,8 @@ EXPORTS = (
     "insite_sindy_fit_segments_f64",
     "insite_per_patient_workspace_bytes",
     "insite_sindy_fit_per_patient_f64",
+    "insite_gram_moments_f64",
+    "insite_fit_per_patient_moments_f64",
     "insite_stlsq_f64",
     "insite_rollout_f64",
     "insite_rollout_rk45_f64",
@@ -104,6 +106,11 @@ _SIGNATURES = {
     "insite_sindy_fit_per_patient_f64": (_c_i32, [_vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32,
                                                   _vp, _c_i32, _c_i32, _c_f64, _vp, _c_f64, _c_f64, _c_i32, _c_i32,
                                                   _vp, _vp, _vp, _vp, _c_size, _vp]),
+    "insite_gram_moments_f64": (_c_i32, [_vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp,
+                                         _c_i32, _c_i32, _c_f64, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _vp,
+                                         _vp, _vp, _vp, _c_size, _vp]),
+    "insite_fit_per_patient_moments_f64": (_c_i32, [_vp, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32, _c_i32, _vp, _c_i32,
+                                                    _vp, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _vp]),
     "insite_stlsq_f64": (_c_i32, [_vp, _vp, _c_i64, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _vp]),
     "insite_rollout_f64": (_c_i32, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _vp, _c_i32, _c_i64, _c_i32, _c_i32,
                                     _c_i32, _c_f64, _c_i32, _c_i32, _c_f64, _vp, _c_i64, _c_i32, _vp]),

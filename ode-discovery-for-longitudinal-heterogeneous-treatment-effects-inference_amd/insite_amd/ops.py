@@ -251,6 +251,63 @@ def sindy_fit_per_patient(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, r
     return _run(("insite_sindy_fit_per_patient_f64", args, dev, out))
 
 
+def gram_moments(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor, dt: float,
+                 lib: PolyLibrary, threshold: float | None = None, alpha: float = 0.5, max_iter: int = 100,
+                 unbias: bool = True, n_arms: int = 2, fd: str = "smoothed4", workspace: Workspace | None = None,
+                 out: tuple | None = None, layout: str = "patient"):
+    """One pass over x for C4's two fits (insite_gram_moments_f64): the per-arm Gram (G, b) -- plus the global
+    STLSQ when ``threshold`` is given (single rank; at N > 1 all-reduce G|b and call ``stlsq``) -- and every
+    patient's moments [N, 5] for ``fit_per_patient_moments``.  Returns (coef, mask, iters, G, b, mom) (the
+    first three None without threshold)."""
+    L = _lib.load()
+    N, n_steps, lay = _discovery_inputs(x, u, arm, rows, lib, layout)
+    F = lib.n_terms
+    dev = x.device
+    if out is None:
+        out = (torch.empty((n_arms, F), dtype=torch.float64, device=dev) if threshold is not None else None,
+               torch.empty((n_arms, F), dtype=torch.int8, device=dev) if threshold is not None else None,
+               torch.empty((n_arms,), dtype=torch.int32, device=dev) if threshold is not None else None,
+               torch.empty((n_arms, F, F), dtype=torch.float64, device=dev),
+               torch.empty((n_arms, F), dtype=torch.float64, device=dev),
+               torch.empty((N, 5), dtype=torch.float64, device=dev))
+    coef, mask, iters, G, b, mom = out
+    ws = (workspace or _default_ws(dev, "disc")).get(L.insite_gram_workspace_bytes(N, n_arms, F), dev)
+    tab = lib.ctypes_table()
+    nul = ctypes.c_void_p(0)
+    args = (_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else nul, _p(arm), _p(rows), N, lib.n_statics,
+            n_arms, tab.ctypes.data_as(ctypes.c_void_p), F, FD_KINDS[fd], float(dt),
+            float(threshold if threshold is not None else 0.0), float(alpha), int(max_iter), int(bool(unbias)),
+            _p(G), _p(b), _p(coef) if coef is not None else nul, _p(mask) if mask is not None else nul,
+            _p(iters) if iters is not None else nul, _p(mom), _p(ws), ws.numel())
+    return _run(("insite_gram_moments_f64", args, dev, out))
+
+
+def fit_per_patient_moments(mom: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor, n_steps: int,
+                            lib: PolyLibrary, global_coef: torch.Tensor, threshold: float, alpha: float,
+                            max_iter: int = 100, unbias: bool = True, out: tuple | None = None):
+    """Per-patient refit from ``gram_moments``' moments (insite_fit_per_patient_moments_f64): the same result
+    as ``sindy_fit_per_patient`` without a second pass over x.  Returns (coef[N, A, F], mask[N, F], iters[N])."""
+    _dev("mom", mom, torch.float64, 2)
+    N = mom.size(0)
+    _dev("global_coef", global_coef, torch.float64, 2)
+    A, F = global_coef.shape
+    if mom.size(1) != 5 or not mom.is_contiguous() or F != lib.n_terms or not global_coef.is_contiguous():
+        raise ValueError("mom must be contiguous [N, 5]; global_coef a contiguous [n_arms, F] tensor")
+    if arm.numel() != N or rows.numel() != N:
+        raise ValueError("arm/rows must have one entry per patient")
+    dev = mom.device
+    if out is None:
+        out = (torch.empty((N, A, F), dtype=torch.float64, device=dev),
+               torch.empty((N, F), dtype=torch.int8, device=dev),
+               torch.empty((N,), dtype=torch.int32, device=dev))
+    coef, mask, iters = out
+    tab = lib.ctypes_table()
+    args = (_p(mom), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), _p(rows), N, int(n_steps), lib.n_statics,
+            A, tab.ctypes.data_as(ctypes.c_void_p), F, _p(global_coef), float(threshold), float(alpha), int(max_iter),
+            int(bool(unbias)), _p(coef), _p(mask), _p(iters))
+    return _run(("insite_fit_per_patient_moments_f64", args, dev, out))
+
+
 SEGMENT_FD_KINDS = {"order1": _lib.FD_ORDER1, "smoothed1": _lib.FD_SMOOTHED1}
 
 
