@@ -366,6 +366,23 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
 
   const int64_t n_tiles = (N + kWave - 1) / kWave;
   const int64_t n_items = n_tiles * n_seg;
+  // time-major register ring, live across work items: a wave with several items requests the next item's
+  // first tiles as soon as the current item's last tile is consumed, so they stream in under the current
+  // item's tail rows and Gram contraction (per-item start-up latency hidden; C4: ~8 items per wave)
+  typedef double TmTile[kGT];
+  TmTile vr[TM ? kTmDepth : 1];
+  bool prefetched = false;  // wave-uniform: vr holds the current item's first kTmDepth tiles already
+  // wave-uniform descriptor over steps [t0, min(t0 + kGT, lim)) based at column q0 (valid columns qv): steps
+  // past lim and lanes past N (out-of-range offset) read as 0
+  auto tm_load_for = [&](TmTile& v, int t0, int lim, int64_t q0, int qv, unsigned qoff) {
+    const int nrow = lim - t0 < kGT ? lim - t0 : kGT;
+    const int bytes = nrow > 0 ? (int)(((int64_t)(nrow - 1) * ldx + qv) * 8) : 0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(x + (int64_t)(nrow > 0 ? t0 : 0) * ldx + q0), (short)0, bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < kGT; ++i)
+      v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, qoff + (unsigned)(i * ldx * 8), 0, 0));
+  };
   for (int64_t item = (int64_t)vblk * kWavesPerBlock + wid; item < n_items;
        item += (int64_t)vgrid * kWavesPerBlock) {
     const int64_t tile = item / n_seg;
@@ -378,27 +395,18 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
     const int tb = (sidx == 0) ? 0 : s0 - kWarm;
     const int tm_valid = (int)(N - p0 < kWave ? N - p0 : kWave);
     const unsigned tm_off = p < N ? (unsigned)lane * 8u : kOOB;
-    typedef double TmTile[kGT];
-    TmTile vr[TM ? kTmDepth : 1];
-    // wave-uniform descriptor over steps [t0, min(t0 + kGT, lim)) based at column p0: steps past
-    // lim and lanes past N (out-of-range offset) read as 0
-    auto tm_load = [&](TmTile& v, int t0, int lim) {
-      const int nrow = lim - t0 < kGT ? lim - t0 : kGT;
-      const int bytes = nrow > 0 ? (int)(((int64_t)(nrow - 1) * ldx + tm_valid) * 8) : 0;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(x + (int64_t)(nrow > 0 ? t0 : 0) * ldx + p0), (short)0, bytes, 0x00020000);
-#pragma unroll
-      for (int i = 0; i < kGT; ++i)
-        v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, tm_off + (unsigned)(i * ldx * 8), 0, 0));
-    };
+    auto tm_load = [&](TmTile& v, int t0, int lim) { tm_load_for(v, t0, lim, p0, tm_valid, tm_off); };
 #ifndef INSITE_GRAM_LATE_ISSUE
     if constexpr (TM) {
       const int s1p = min(s0 + seg, n_steps);
+      if (!prefetched) {
 #pragma unroll
-      for (int d = 0; d < kTmDepth; ++d)
-        if (tb + d * kGT < s1p) tm_load(vr[d], tb + d * kGT, s1p);
+        for (int d = 0; d < kTmDepth; ++d)
+          if (tb + d * kGT < s1p) tm_load(vr[d], tb + d * kGT, s1p);
+      }
     }
 #endif
+    prefetched = false;
     int L = 0;
     int arm_p = -1;
     double uu[INSITE_MAX_STATICS] = {0.0, 0.0, 0.0};
@@ -621,6 +629,25 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
             }
           }
         }
+#ifndef INSITE_GRAM_NO_XPREFETCH
+        {  // every tile of this item consumed: request the wave's next item's first tiles
+          const int64_t nitem = item + (int64_t)vgrid * kWavesPerBlock;
+          if (nitem < n_items) {  // uniform
+            const int64_t ntile = nitem / n_seg;
+            const int nsidx = (int)(nitem - ntile * n_seg);
+            const int64_t np0 = ntile * kWave;
+            const int ns0 = nsidx * seg;
+            const int ntb = nsidx == 0 ? 0 : ns0 - kWarm;
+            const int ns1p = min(ns0 + seg, n_steps);
+            const int nvalid = (int)(N - np0 < kWave ? N - np0 : kWave);
+            const unsigned noff = np0 + lane < N ? (unsigned)lane * 8u : kOOB;
+#pragma unroll
+            for (int d = 0; d < kTmDepth; ++d)
+              if (ntb + d * kGT < ns1p) tm_load_for(vr[d], ntb + d * kGT, ns1p, np0, nvalid, noff);
+            prefetched = true;
+          }
+        }
+#endif
       } else if constexpr (kGPF == 2) {
         for (int t0 = tb + kGT; t0 < s1;) {
           store_tile(vA);
