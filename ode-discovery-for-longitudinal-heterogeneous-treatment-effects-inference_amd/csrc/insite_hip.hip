@@ -1685,8 +1685,16 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
     double al[NARM], be[NARM];
     affine_rates<NARM>(lib, ra.coef + (PERROW ? pc * ra.coef_stride : 0), ra.A, ra.drop, uu, al, be);
     const double h = ra.dt / (double)ra.substeps;
+#ifndef INSITE_ROLLOUT_STAGEWISE
 #pragma unroll
     for (int a = 0; a < NARM; ++a) interval_propagator(METHOD, ra.substeps, h, al[a], be[a], PA[a], PB[a]);
+#else  // ablation: PA / PB carry the rates, every step evaluates the method's stages explicitly
+#pragma unroll
+    for (int a = 0; a < NARM; ++a) {
+      PA[a] = al[a];
+      PB[a] = be[a];
+    }
+#endif
     const double v0 = ra.y0[pc];
     y = act ? v0 : 0.0;
   }
@@ -1712,6 +1720,7 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
         (void*)(ra.arm + (int64_t)(rows > 0 ? k0 : 0) * arow + abase), (short)0, bytes, 0x00020000);
     return __builtin_amdgcn_raw_buffer_load_b32(rs, goff, 0, 0);
   };
+#ifndef INSITE_ROLLOUT_STAGEWISE
   auto step = [&](int a) {
     double A = PA[0], B = PB[0];
 #pragma unroll
@@ -1721,6 +1730,28 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
     }
     y = fma(A, y, B);
   };
+#else
+  const double hs = ra.dt / (double)ra.substeps, hs2 = 0.5 * hs, hs6 = hs / 6.0;
+  auto step = [&](int a) {  // the reference's stage arithmetic: Euler sub-steps / classical RK4 stages
+    double al = PA[0], be = PB[0];
+#pragma unroll
+    for (int aa = 1; aa < NARM; ++aa) {
+      al = (a == aa) ? PA[aa] : al;
+      be = (a == aa) ? PB[aa] : be;
+    }
+    for (int s = 0; s < ra.substeps; ++s) {
+      if constexpr (METHOD == INSITE_METHOD_EULER) {
+        y = fma(fma(be, y, al), hs, y);
+      } else {
+        const double k1 = fma(be, y, al);
+        const double k2 = fma(be, fma(hs2, k1, y), al);
+        const double k3 = fma(be, fma(hs2, k2, y), al);
+        const double k4 = fma(be, fma(hs, k3, y), al);
+        y = fma(hs6, (k1 + 2.0 * k2) + (2.0 * k3 + k4), y);
+      }
+    }
+  };
+#endif
   unsigned aring[kAG];
 #pragma unroll
   for (int d = 0; d < kAG; ++d) aring[d] = grp_load(d * kRollGS);

@@ -25,6 +25,7 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     STEPDEPTH3) NAME=$v build -DINSITE_TM_DEPTH=3 ;;
     GT8D4) NAME=$v build -DINSITE_GT=8 -DINSITE_TM_DEPTH=4 ;;
     GNOCOMP) NAME=$v build -DINSITE_ABLATE_GRAM_NOCOMPUTE ;;
+    STAGEWISE) NAME=$v build -DINSITE_ROLLOUT_STAGEWISE ;;
     WPE3) NAME=$v build -DINSITE_GRAM_WPE=3 -DINSITE_STEP_WPE=3 ;;
     SWPE3) NAME=$v build -DINSITE_STEP_WPE=3 ;;
     GNS2) NAME=$v build -DINSITE_GRAM_NS_MIN=2 ;;
