@@ -57,6 +57,8 @@ def parse():
                     help="pipeline mode, N = 1: run each step's STLSQ in the gram's last block on the discovery "
                          "stream (default) or as its own launch on the rollout stream ahead of that step's rollout "
                          "(off the discovery stream's critical path)")
+    ap.add_argument("--fused-graph", action="store_true",
+                    help="fused mode: replay the ping-pong pair of step launches from a HIP graph")
     ap.add_argument("--no-fused", action="store_true",
                     help="pipeline mode at N = 1: skip the secondary fused-step measurement")
     ap.add_argument("--gram-blocks", type=int, default=0,
@@ -888,12 +890,27 @@ def fused_run(args, dev, coh, arm_cf):
              for j in range(2)]
     st = torch.cuda.current_stream(dev)
     fast = [p.bind(st) for p in plans]
-    for i in range(args.warmup):
-        fast[i % 2]()
+    if args.fused_graph:    # the ping-pong pair of launches captured once in a HIP graph, replayed
+        for p in plans:
+            p()
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            gs = torch.cuda.current_stream(dev)
+            plans[0](gs)
+            plans[1](gs)
+        pair = graph.replay
+        fast = [pair, lambda: None]     # step 2i replays the pair (steps 2i, 2i+1); step 2i+1 is already in it
+    def run_steps(n):                   # n steps = n launches (graph: n // 2 pair replays + an odd last one)
+        for i in range(n - (n % 2 if args.fused_graph else 0)):
+            fast[i % 2]()
+        if args.fused_graph and n % 2:
+            plans[0](st)
+
+    run_steps(args.warmup)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        fast[i % 2]()
+    run_steps(args.steps)
     host_ms = (time.perf_counter() - t0) / args.steps * 1e3
     torch.cuda.synchronize(dev)
     ms_step = (time.perf_counter() - t0) / args.steps * 1e3
@@ -905,8 +922,7 @@ def fused_run(args, dev, coh, arm_cf):
     tevs = [(hip.create(timing=True), hip.create(timing=True)) for _ in range(NBAT)]
     for e0, e1 in tevs:
         hip.record(e0, st.cuda_stream)
-        for i in range(KB):
-            fast[i % 2]()
+        run_steps(KB)
         hip.record(e1, st.cuda_stream)
     torch.cuda.synchronize(dev)
     step_ms = float(np.mean([hip.elapsed_ms(e0, e1) for e0, e1 in tevs])) / KB
