@@ -57,6 +57,8 @@ def parse():
                     help="pipeline mode, N = 1: run each step's STLSQ in the gram's last block on the discovery "
                          "stream (default) or as its own launch on the rollout stream ahead of that step's rollout "
                          "(off the discovery stream's critical path)")
+    ap.add_argument("--pipe-k", type=int, default=4, help="pipeline: steps per batch (one event per batch per stream)")
+    ap.add_argument("--pipe-rs", type=int, default=2, help="pipeline: rollout streams taking alternate batches")
     ap.add_argument("--fused-graph", action="store_true",
                     help="fused mode: replay the ping-pong pair of step launches from a HIP graph")
     ap.add_argument("--no-fused", action="store_true",
@@ -1099,7 +1101,8 @@ def main():
     # but are buffered alike to keep the plans independent).  Steps go in batches of K: one event per batch
     # each way (an event record costs ~20 us of dead queue time on ROCm 7.2, profiles/
     # r02_c2_pipeline_trace.txt); batches alternate between RS rollout streams and y buffers.
-    K, RS, WAR_EVERY = 4, 2, 8
+    K, RS = args.pipe_k, args.pipe_rs
+    WAR_EVERY = 2 * K
     NB = 3 * K * RS                     # a multiple of K * RS: step k's y buffer (k // K) % RS is fixed per coef slot
     NBE = NB // K                       # event slots (batches in flight)
     # G|b of K consecutive steps in one flat bucket: at N > 1 the pipeline all-reduces a batch's K systems in
@@ -1366,9 +1369,10 @@ def main():
                            else "gram_kernel (in-launch reduction) + RCCL all_reduce + stlsq_kernel",
                 "timed_region": {"graph": "one step (gram+reduction, STLSQ, rollout) captured in a HIP graph, replayed",
                                  "seq": "eager launches, one stream, strictly sequential",
-                                 "pipeline": "discovery stream (gram+in-launch reduction [+all-reduce] +STLSQ) | two "
-                                             "rollout streams taking alternate batches of 4 steps, one event per "
-                                             "batch per stream, 24 coefficient buffers"}[mode],
+                                 "pipeline": f"discovery stream (gram+in-launch reduction [N>1: one all-reduce per "
+                                             f"batch] +STLSQ) | {args.pipe_rs} rollout streams taking alternate "
+                                             f"batches of {args.pipe_k} steps, one event per batch per stream, "
+                                             f"{3 * args.pipe_k * args.pipe_rs} coefficient buffers"}[mode],
                 "avg_ms_source": "instrumented pass: HIP timing events around each batch's discoveries (gram with its "
                                  "in-launch reduction, STLSQ) on their stream, divided by the batch size, "
                                  "concurrent with the previous batch's rollouts" if mode == "pipeline"
