@@ -3861,9 +3861,10 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
 #ifdef INSITE_FORCE_PPL
     ppl = INSITE_FORCE_PPL;
 #else
-    // bit-packed arms take the transposed-word path (one patient per lane: with the interval
-    // propagator the time loop is store-bound, more chains per lane buy nothing)
-    if (n_rows >= 256 * 1024 && !bits) ppl = 2;
+    // one patient per lane: with the interval propagator the time loop is store-bound, more chains per
+    // lane buy nothing; since the prologue loads its coefficient row in one burst (affine_rates), two
+    // patients per lane (16-B stores) is slower too: F4's 1M x 60 4-arm int8 rollout 0.117 ms at PPL 2,
+    // 0.094 ms at PPL 1, 0.168 ms at PPL 4 (profiles/r02_ppl/); INSITE_FORCE_PPL keeps the others
 #endif
     if (ppl >= 2 && !(y16 && aw4 && n_rows % ppl == 0)) ppl = 1;
     const int64_t per_block = (int64_t)kBlock * ppl;
