@@ -1275,8 +1275,11 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
 // groups and c_j = m_j * alpha / sum m_k^2 (e_j = 0), m_j * beta / sum m_k^2 (e_j = 1).  If
 // sum |c| > 10 the reference refits without unbias (:795-798): the last ridge iterate is kept.
 // Other arms keep the global coefficients; patients with < 5 rows keep the global model.
+#ifndef INSITE_PP_WPE
+#define INSITE_PP_WPE 2  // waves per SIMD the per-patient fit's register budget is sized for
+#endif
 template <int F>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_PP_WPE)))
 patient_fit_kernel(const double* __restrict__ mom, const double* __restrict__ u, const int8_t* __restrict__ arm,
                    const int32_t* __restrict__ rows, int64_t N, int n_steps, int n_arms, LibDesc lib,
                    const double* __restrict__ gcoef, StlsqParams sp, double* __restrict__ coef,

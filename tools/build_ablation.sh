@@ -62,6 +62,8 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     SC1) NAME=$v build -DINSITE_STORE_AUX=1 ;;
     NT3) NAME=$v build -DINSITE_STORE_AUX=3 ;;
     PPL1) NAME=$v build -DINSITE_FORCE_PPL=1 ;;
+    PPW3) NAME=$v build -DINSITE_PP_WPE=3 ;;
+    PPW4) NAME=$v build -DINSITE_PP_WPE=4 ;;
     PPL2) NAME=$v build -DINSITE_FORCE_PPL=2 ;;
     PPL4) NAME=$v build -DINSITE_FORCE_PPL=4 ;;
     RWPE1) NAME=$v build -DINSITE_REFINE_WPE4=1 ;;
