@@ -913,6 +913,20 @@ def dist_setup():
     return world, rank, dev
 
 
+def step_traffic(args):
+    """HBM bytes per step_kernel launch from the committed PMC passes (profiles/traffic_r02_step.json), if
+    they were taken on this workload."""
+    path = os.path.join(ROOT, "profiles", "traffic_r02_step.json")
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+        if tj.get("workload") == f"step_{args.method}_{args.patients}x{args.T}":
+            return tj.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
 def fused_run(args, dev, coh, arm_cf):
     """Time the fused step (insite_fit_rollout_f64: step_kernel) on the C2 cohort.  One launch per step runs
     the discovery of step i (gram + in-launch reduction + the F = 7 STLSQ in its last block) and, on the
@@ -1049,15 +1063,7 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
         "timed_region": "one step_kernel launch per step on one stream: discovery of step i | rollout of step i-1 "
                         "(two coefficient buffers); no events or cross-stream waits inside the timed region",
     }
-    tj = None
-    if os.path.exists(args.traffic_json):
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-        except Exception:
-            tj = None
-    if tj and tj.get("workload") == f"step_{args.method}_{N}x{T}":
-        out["roofline"]["traffic"] = tj.get("hbm_bytes_per_launch")
+    out["roofline"]["traffic"] = step_traffic(args)
     if iso is not None:
         out["isolated"] = dict(iso, discovery_frac=gb / (iso["discovery_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                                rollout_frac=rb / (iso["rollout_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS)
@@ -1449,7 +1455,7 @@ def main():
             "ms_per_step": fr["ms_step"], "avg_launch_ms": fr["step_ms"],
             "algorithmic_bytes_per_launch": fr["rb"] + fr["gb"],
             "achieved_GBps": (fr["rb"] + fr["gb"]) / (fr["step_ms"] * 1e-3) / 1e9, "frac": fr["frac"],
-            "gram_blocks": args.gram_blocks or "default",
+            "gram_blocks": args.gram_blocks or "default", "traffic": step_traffic(args),
             "avg_ms_source": f"HIP timing events around {fr['NBAT']} batches of {fr['KB']} back-to-back launches",
             "why_not_headline": "one launch holds both roles at the gram's 2 waves/SIMD register budget; the two-stream "
                                 "pipeline keeps more rollout waves resident and measures faster",

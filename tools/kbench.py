@@ -9,7 +9,7 @@ import torch
 from insite_amd import ops, cohort
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--op", default="gram", choices=["gram", "sindy_fit", "rollout", "stlsq", "step", "gram_seg"])
+ap.add_argument("--op", default="gram", choices=["gram", "sindy_fit", "rollout", "stlsq", "step", "gram_seg", "fused"])
 ap.add_argument("--patients", type=int, default=100_000)
 ap.add_argument("--T", type=int, default=200)
 ap.add_argument("--iters", type=int, default=50)
@@ -40,7 +40,13 @@ step_out = (torch.empty((2, lib.n_terms), dtype=torch.float64, device=dev),
 if a.op == "gram_seg":   # F4: 4-arm treatment-segment Gram, time-major (bench.py --config f4 cohort)
     seg = cohort.synthetic_segments(a.patients, a.T, seed=31, device=dev,
                                     coef=[[0, .2, 0, 0], [0, 0, 0, -.6], [0, -.3, 0, 0], [0, -.25, 0, -.9]])
+if a.op == "fused":   # the fused step kernel (insite_fit_rollout_f64): discovery of coh | bit-arm rollout of coh
+    fplan = ops.plan_fit_rollout(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, coh.y0, coh.u, arm_cf, coef,
+                                 coh.dt, method=a.method, T=a.T, y_out=y, out=step_out, workspace=ws)
 def run():
+    if a.op == "fused":
+        fplan()
+        return
     if a.op == "gram_seg":
         ops.gram_segments(seg.x, seg.arm, seg.seq_len, seg.u, seg.dt, seg.lib, 4, "order1", ws, layout="time")
     elif a.op == "gram":
