@@ -1457,8 +1457,9 @@ def main():
             "achieved_GBps": (fr["rb"] + fr["gb"]) / (fr["step_ms"] * 1e-3) / 1e9, "frac": fr["frac"],
             "gram_blocks": args.gram_blocks or "default", "traffic": step_traffic(args),
             "avg_ms_source": f"HIP timing events around {fr['NBAT']} batches of {fr['KB']} back-to-back launches",
-            "why_not_headline": "one launch holds both roles at the gram's 2 waves/SIMD register budget; the two-stream "
-                                "pipeline keeps more rollout waves resident and measures faster",
+            "why_not_headline": "one launch holds both roles at the gram's 2 waves/SIMD register budget, the two-stream "
+                                "pipeline keeps more rollout waves resident: the two measure within a few % of each "
+                                "other, the pipeline ahead on most boxes (profiles/r02_fused_sweep/)",
         }
         del fr
     # north-star probe: 1M x 500 RK4 rollout alone (the >= 40 % roofline target), rank 0, N = 1
