@@ -49,10 +49,11 @@ def parse():
                     help="per-step arms of the time-major rollout: 1-bit mask (A <= 2) or int8")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default=None, choices=["fused", "graph", "seq", "pipeline"],
-                    help="pipeline (default): discovery (gram + in-launch reduction [+ all-reduce] + STLSQ) | "
-                         "rollout on two streams, consecutive steps overlapped; fused (N = 1): ONE step_kernel launch "
-                         "per step -- the discovery of step i and the rollout of step i-1 in the same launch; seq: "
-                         "eager launches on one stream; graph: the seq step in a HIP graph")
+                    help="fused (default at N = 1): ONE step_kernel launch per step -- the discovery of step i and "
+                         "the rollout of step i-1 in the same launch; pipeline (default at N > 1, where the RCCL "
+                         "all-reduce sits between the gram and STLSQ): discovery | rollout on two streams, "
+                         "consecutive steps overlapped; seq: eager launches on one stream; graph: the seq step in a "
+                         "HIP graph")
     ap.add_argument("--stlsq-stream", default="discovery", choices=["discovery", "rollout"],
                     help="pipeline mode, N = 1: run each step's STLSQ in the gram's last block on the discovery "
                          "stream (default) or as its own launch on the rollout stream ahead of that step's rollout "
@@ -1062,6 +1063,10 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
         },
         "timed_region": "one step_kernel launch per step on one stream: discovery of step i | rollout of step i-1 "
                         "(two coefficient buffers); no events or cross-stream waits inside the timed region",
+        "step_aggregate": {"algorithmic_bytes": rb + gb, "achieved_GBps": (rb + gb) / (ms_step * 1e-3) / 1e9,
+                           "frac": (rb + gb) / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS},
+        "pipeline_alternative": "bench.py --mode pipeline: gram | rollout on two streams (the N > 1 schedule); "
+                                "within a few % of this line, ahead over long runs (profiles/r02_fused_sweep/)",
     }
     out["roofline"]["traffic"] = step_traffic(args)
     if iso is not None:
@@ -1141,8 +1146,8 @@ def main():
     lib = coh.lib
     F = lib.n_terms
     y0 = coh.y0
-    if args.mode is None:
-        args.mode = "pipeline"
+    if args.mode is None:   # N = 1: one fused launch per step; N > 1: the all-reduce splits the step -> pipeline
+        args.mode = "fused" if world == 1 else "pipeline"
     if args.mode == "fused" and world > 1:
         raise SystemExit("--mode fused is single-GPU (the all-reduce sits between the gram and STLSQ): "
                          "use --mode pipeline at N > 1")
