@@ -230,6 +230,9 @@ __device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
     if (threadIdx.x == 0) {
+      // release at agent scope before the ticket (the HIP memory model's guarantee that the block's
+      // partial stores are visible to the last arriver on another XCD, not only the sc1 write-through)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = t == arrivals - 1u;
       if (last) {

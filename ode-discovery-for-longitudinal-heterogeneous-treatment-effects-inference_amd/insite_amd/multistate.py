@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .ops import METHODS, Workspace, _default_ws, _dev, _p, _stream, pack_arm_bits
+from .ops import METHODS, Workspace, _default_ws, _ws, _dev, _p, _stream, pack_arm_bits
 
 RATES_C3 = {"k1": 1.2, "k2": 0.8, "k3": 0.5, "k4": 0.6, "k5": 0.1, "e": 0.4, "D": 2.0}
 THRESHOLD_C3 = 0.05
@@ -125,7 +125,7 @@ def gram_ms(x: torch.Tensor, a: torch.Tensor | None, lib: MsLibrary, dt: float, 
     if out is None:
         out = (torch.empty((F, F), dtype=torch.float64, device=dev), torch.empty((F, S), dtype=torch.float64, device=dev))
     G, B = out
-    ws = (workspace or _default_ws(dev)).get(L.insite_gram_ms_workspace_bytes(N), dev)
+    ws = _ws(workspace, dev, "scratch").get(L.insite_gram_ms_workspace_bytes(N), dev)
     tab = lib.table()
     st = L.insite_gram_ms_f32(_p(x), ldx, T, S, ap, lda, _p(rows), N, tab.ctypes.data_as(ctypes.c_void_p), F, 0,
                               float(dt), _p(G), _p(B), _p(ws), ws.numel(), _stream(dev))

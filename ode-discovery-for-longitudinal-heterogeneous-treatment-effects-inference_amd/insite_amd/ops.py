@@ -62,11 +62,22 @@ class Workspace:
     """Grow-only device scratch buffer (the library never allocates).  A buffer handed to a ``Plan`` is
     referenced by that plan, so growing the workspace later never frees memory a plan still writes to.
     Buffers start zeroed: the discovery kernels' arrival counters (the header) must be zero before a
-    workspace's first use, and every call leaves them zero (insite_hip.h) -- so a Workspace given to the
-    discovery family (gram / sindy_fit / segments / per-patient) must not also be given to other ops."""
+    workspace's first use, and every call leaves them zero (insite_hip.h).  The invariant is enforced: a
+    workspace takes the kind of the first op family it serves ("disc": gram / sindy_fit / segments /
+    per-patient / fused step, whose header holds the counters; "scratch": ops that write from offset 0) and
+    a later op of the other family raises ``ValueError`` instead of silently corrupting the counters."""
 
-    def __init__(self):
+    def __init__(self, kind: str | None = None):
         self._buf = {}
+        self.kind = kind
+
+    def claim(self, kind: str) -> "Workspace":
+        if self.kind is None:
+            self.kind = kind
+        elif self.kind != kind:
+            raise ValueError(f"workspace serves the {self.kind!r} op family; a {kind!r} op would overwrite "
+                             "its scratch (use a separate Workspace)")
+        return self
 
     def get(self, nbytes: int, device) -> torch.Tensor:
         key = torch.device(device).index
@@ -84,13 +95,23 @@ class Workspace:
 _WS_BY_STREAM: dict = {}
 
 
-def _default_ws(device, kind: str = "misc") -> Workspace:
+def _default_ws(device, kind: str = "scratch") -> Workspace:
     dev = torch.device(device)
     key = (dev.index, torch.cuda.current_stream(dev).cuda_stream, kind)
     ws = _WS_BY_STREAM.get(key)
     if ws is None:
-        ws = _WS_BY_STREAM[key] = Workspace()
+        ws = _WS_BY_STREAM[key] = Workspace(kind)
     return ws
+
+
+def _ws(workspace: Workspace | None, device, kind: str) -> Workspace:
+    """The caller's workspace (claimed for ``kind``) or the per-stream default of that kind."""
+    return workspace.claim(kind) if workspace is not None else _default_ws(device, kind)
+
+
+def _plan_ws(workspace: Workspace | None) -> Workspace:
+    """A plan of the discovery family: the caller's workspace (claimed) or a private one."""
+    return workspace.claim("disc") if workspace is not None else Workspace("disc")
 
 
 class Plan:
@@ -164,7 +185,7 @@ def _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout, stl
     F = lib.n_terms
     dev = x.device
     nbytes = L.insite_gram_workspace_bytes(N, n_arms, F)
-    ws = (workspace or _default_ws(dev, "disc")).get(nbytes, dev)
+    ws = _ws(workspace, dev, "disc").get(nbytes, dev)
     tab = lib.ctypes_table()
     head = (_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), _p(rows), N,
             lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p), F, FD_KINDS[fd], float(dt))
@@ -210,7 +231,7 @@ def sindy_fit(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.T
 def plan_gram(x, u, arm, rows, dt, lib, n_arms=2, fd="smoothed4", workspace=None, out=None,
               layout="patient") -> Plan:
     """``gram`` as a prepared launch (``Plan``); ``plan.out`` = (G, b)."""
-    name, args, dev, out, keep = _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace or Workspace(), out,
+    name, args, dev, out, keep = _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, _plan_ws(workspace), out,
                                             layout)
     return Plan(name, args, dev, out, keep)
 
@@ -218,7 +239,7 @@ def plan_gram(x, u, arm, rows, dt, lib, n_arms=2, fd="smoothed4", workspace=None
 def plan_sindy_fit(x, u, arm, rows, dt, lib, threshold, alpha, max_iter=100, unbias=True, n_arms=2,
                    fd="smoothed4", workspace=None, out=None, layout="patient") -> Plan:
     """``sindy_fit`` as a prepared launch; ``plan.out`` = (coef, mask, iters, G, b)."""
-    name, args, dev, out, keep = _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace or Workspace(), out,
+    name, args, dev, out, keep = _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, _plan_ws(workspace), out,
                                             layout, (threshold, alpha, max_iter, unbias))
     return Plan(name, args, dev, out, keep)
 
@@ -242,7 +263,7 @@ def sindy_fit_per_patient(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, r
                torch.empty((N, F), dtype=torch.int8, device=dev),
                torch.empty((N,), dtype=torch.int32, device=dev))
     coef, mask, iters = out
-    ws = (workspace or _default_ws(dev, "disc")).get(L.insite_per_patient_workspace_bytes(N), dev)
+    ws = _ws(workspace, dev, "disc").get(L.insite_per_patient_workspace_bytes(N), dev)
     tab = lib.ctypes_table()
     args = (_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), _p(rows), N,
             lib.n_statics, A, tab.ctypes.data_as(ctypes.c_void_p), F, FD_KINDS[fd], float(dt), _p(global_coef),
@@ -271,7 +292,7 @@ def gram_moments(x: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torc
                torch.empty((n_arms, F), dtype=torch.float64, device=dev),
                torch.empty((N, 5), dtype=torch.float64, device=dev))
     coef, mask, iters, G, b, mom = out
-    ws = (workspace or _default_ws(dev, "disc")).get(L.insite_gram_workspace_bytes(N, n_arms, F), dev)
+    ws = _ws(workspace, dev, "disc").get(L.insite_gram_workspace_bytes(N, n_arms, F), dev)
     tab = lib.ctypes_table()
     nul = ctypes.c_void_p(0)
     args = (_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else nul, _p(arm), _p(rows), N, lib.n_statics,
@@ -340,7 +361,7 @@ def _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layo
     L = _lib.load()
     F = lib.n_terms
     dev = x.device
-    ws = (workspace or _default_ws(dev, "disc")).get(L.insite_gram_segments_workspace_bytes(N, n_arms, F), dev)
+    ws = _ws(workspace, dev, "disc").get(L.insite_gram_segments_workspace_bytes(N, n_arms, F), dev)
     tab = lib.ctypes_table()
     head = (_p(x), x.stride(0), _p(arm), arm.stride(0), LAYOUTS[layout], n_steps, _p(seq_len),
             _p(u) if lib.n_statics else ctypes.c_void_p(0), N, lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p),
@@ -390,7 +411,7 @@ def sindy_fit_segments(x: torch.Tensor, arm: torch.Tensor, seq_len: torch.Tensor
 def plan_gram_segments(x, arm, seq_len, u, dt, lib, n_arms=4, fd="order1", workspace=None, out=None,
                        layout="patient") -> Plan:
     """``gram_segments`` as a prepared launch; ``plan.out`` = (G, b)."""
-    name, args, dev, out, keep = _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace or Workspace(),
+    name, args, dev, out, keep = _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, _plan_ws(workspace),
                                                 out, layout)
     return Plan(name, args, dev, out, keep)
 
@@ -398,7 +419,7 @@ def plan_gram_segments(x, arm, seq_len, u, dt, lib, n_arms=4, fd="order1", works
 def plan_sindy_fit_segments(x, arm, seq_len, u, dt, lib, threshold, alpha, max_iter=100, unbias=True, n_arms=4,
                             fd="order1", workspace=None, out=None, layout="patient") -> Plan:
     """``sindy_fit_segments`` as a prepared launch; ``plan.out`` = (coef, mask, iters, G, b)."""
-    name, args, dev, out, keep = _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace or Workspace(),
+    name, args, dev, out, keep = _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, _plan_ws(workspace),
                                                 out, layout, (threshold, alpha, max_iter, unbias))
     return Plan(name, args, dev, out, keep)
 
@@ -445,7 +466,7 @@ def gen_gram(x: torch.Tensor, u: torch.Tensor | None, rows: torch.Tensor, dt: fl
     L = _lib.load()
     F = lib.n_terms
     dev = x.device
-    ws = (workspace or _default_ws(dev)).get(L.insite_gen_gram_workspace_bytes(N, n_steps, n_groups, F), dev)
+    ws = _ws(workspace, dev, "scratch").get(L.insite_gen_gram_workspace_bytes(N, n_steps, n_groups, F), dev)
     if out is None:
         out = (torch.empty((n_groups, F, F), dtype=torch.float64, device=dev),
                torch.empty((n_groups, F), dtype=torch.float64, device=dev))
@@ -610,7 +631,7 @@ def plan_fit_rollout(x, u, arm, rows, dt, lib, threshold, alpha, y0, ru, arm_bit
                      workspace=None, out=None, y_out=None, gram_blocks=0) -> Plan:
     """``fit_rollout`` as a prepared launch; ``plan.out`` = ((coef, mask, iters, G, b), y)."""
     name, args, dev, out, keep = _prep_fit_rollout(x, u, arm, rows, dt, lib, threshold, alpha, max_iter, unbias, fd,
-                                                   workspace or Workspace(), out, y0, ru, arm_bits, coef_in, rdt,
+                                                   _plan_ws(workspace), out, y0, ru, arm_bits, coef_in, rdt,
                                                    method, substeps, drop_below, T, y_out, gram_blocks)
     return Plan(name, args, dev, out, keep)
 
@@ -767,7 +788,7 @@ def masked_sse(pred: torch.Tensor, target: torch.Tensor, active: torch.Tensor, s
     cnt = torch.empty(T, dtype=torch.float64, device=pred.device)
     last = torch.empty(2, dtype=torch.float64, device=pred.device)
     nbytes = L.insite_masked_sse_workspace_bytes(N, T)
-    ws = (workspace or _default_ws(pred.device)).get(nbytes, pred.device)
+    ws = _ws(workspace, pred.device, "scratch").get(nbytes, pred.device)
     st = L.insite_masked_sse_f64(_p(pred), pred.stride(0), float(scale), float(shift), _p(target), _p(active), N, T,
                                  _p(per), _p(cnt), _p(last), _p(ws), ws.numel(), _stream(pred.device))
     _lib.check("insite_masked_sse_f64", st)

@@ -84,10 +84,11 @@ def run_one(driver: dict, dataset_name: str, method_name: str, seed: int, domain
         if driver["setup"].get("debug_mode", True):
             raise
         logger.exception(f"[Error] {e}")
+        logger.info(f"[Failed evaluating exp] {(dataset_name, method_name, seed, domain_conf)}\t| error={e}")
         traceback.print_exc()
         result = {"errored": True}
-    # run_exp_wrapper_outer's keys (reference run.py:154-169), in the logged order
-    result.update({"dataset_name": dataset_name, "method_name": method_name, "domain_conf": domain_conf})
+    # run_exp_wrapper_outer's keys (reference run.py:170), in the logged order -- a failed run keeps its seed
+    result.update({"dataset_name": dataset_name, "seed": seed, "method_name": method_name, "domain_conf": domain_conf})
     return result
 
 

@@ -186,3 +186,29 @@ def test_savgol_rows_matches_scipy():
     V = np.random.default_rng(0).normal(size=(7, 23))
     got = savgol_5_3_rows(torch.tensor(V)).numpy()
     assert np.allclose(got, savgol_filter(V, 5, 3, axis=1), rtol=1e-12, atol=1e-12)
+
+
+def test_workspace_kind_is_enforced():
+    """A workspace serves one op family: the discovery kernels' zero counter header must never be
+    overwritten by an op that writes scratch from offset 0."""
+    from insite_amd import ops
+    ws = ops.Workspace()
+    assert ws.claim("disc") is ws and ws.claim("disc") is ws
+    with pytest.raises(ValueError, match="separate Workspace"):
+        ws.claim("scratch")
+    ws2 = ops.Workspace("scratch")
+    with pytest.raises(ValueError):
+        ops._plan_ws(ws2)
+    assert ops._plan_ws(None).kind == "disc"
+
+
+def test_failed_run_keeps_its_seed():
+    """run_exp_wrapper_outer (reference run.py:159-170): outside debug mode a failed run logs
+    {'errored': True} plus dataset_name, seed, method_name and domain_conf, in that order."""
+    import run
+    from insite_amd import config as C
+    drv = C.driver_config()
+    drv["setup"]["debug_mode"] = False
+    r = run.run_one(drv, "EQ_4_A", "sindy", 3, 2.0, extra=["+backbone=no_such_backbone"])
+    assert list(r) == ["errored", "dataset_name", "seed", "method_name", "domain_conf"]
+    assert r["errored"] is True and r["seed"] == 3
