@@ -45,8 +45,10 @@ TUMOUR_SIZE_DISTRIBUTIONS = {"I": (1.72, 4.70, 0.3, 5.0), "II": (1.96, 1.63, 0.3
 CANCER_STAGE_OBSERVATIONS = {"I": 1432, "II": 128, "IIIA": 1306, "IIIB": 7248, "IV": 12840}
 
 
-def get_standard_params(num_patients, rs):
-    """cancer_simulation.py:96-215 with the draws taken from RandomState ``rs`` in the reference order."""
+def get_standard_params(num_patients, rs, equation=None):
+    """cancer_simulation.py:96-215 with the draws taken from RandomState ``rs`` in the reference order.
+    ``equation`` "EQ_5_A".."EQ_5_D": the continuous variant (continuous.py:98-224): patient type always 1
+    for A / B (:178-181), the truncated-normal beta_c draw only for D (:195-201)."""
     total = sum(CANCER_STAGE_OBSERVATIONS.values())
     props = {k: CANCER_STAGE_OBSERVATIONS[k] / total for k in CANCER_STAGE_OBSERVATIONS}
     stages = sorted(TUMOUR_SIZE_DISTRIBUTIONS)
@@ -76,16 +78,19 @@ def get_standard_params(num_patients, rs):
         for i in range(holder.shape[0]):
             if holder[i, 0] > lower and holder[i, 1] > lower:
                 sim.append(holder[i, :])
-    patient_types = rs.choice([1, 2, 3], num_patients)
+    patient_types = rs.choice([1] if equation in ("EQ_5_A", "EQ_5_B") else [1, 2, 3], num_patients)
     chemo_adj = np.array([0.0 if i < 3 else 0.1 for i in patient_types])
     radio_adj = np.array([0.0 if i > 1 else 0.1 for i in patient_types])
     sim = np.array(sim)[:num_patients, :]
     alpha = sim[:, 0] + alpha_params[0] * radio_adj
     rho = sim[:, 1]
     beta = alpha / alpha_beta_ratio
-    beta_c = beta_c_params[0] + beta_c_params[1] * truncnorm.rvs(
-        (lower - beta_c_params[0]) / beta_c_params[1], (upper - beta_c_params[0]) / beta_c_params[1],
-        size=num_patients, random_state=rs) + beta_c_params[0] * chemo_adj
+    if equation is None or equation == "EQ_5_D":
+        beta_c = beta_c_params[0] + beta_c_params[1] * truncnorm.rvs(
+            (lower - beta_c_params[0]) / beta_c_params[1], (upper - beta_c_params[0]) / beta_c_params[1],
+            size=num_patients, random_state=rs) + beta_c_params[0] * chemo_adj
+    else:
+        beta_c = beta_c_params[0] + beta_c_params[0] * chemo_adj
     holder = {"patient_types": patient_types, "initial_stages": np.array(sim_stages),
               "initial_volumes": calc_volume(np.array(diam)), "alpha": alpha, "rho": rho, "beta": beta,
               "beta_c": beta_c, "K": np.array([K for _ in range(num_patients)])}
@@ -94,9 +99,9 @@ def get_standard_params(num_patients, rs):
     return {k: v[idx] for k, v in holder.items()}
 
 
-def generate_params(num_patients, chemo_coeff, radio_coeff, window_size, lag, rs):
-    """cancer_simulation.py:66-93."""
-    p = get_standard_params(num_patients, rs)
+def generate_params(num_patients, chemo_coeff, radio_coeff, window_size, lag, rs, equation=None):
+    """cancer_simulation.py:66-93 (continuous.py:68-95)."""
+    p = get_standard_params(num_patients, rs, equation)
     n = len(p["patient_types"])
     d_max = calc_diameter(TUMOUR_DEATH_THRESHOLD)
     p["chemo_sigmoid_intercepts"] = np.full(n, d_max / 2.0)
@@ -105,7 +110,17 @@ def generate_params(num_patients, chemo_coeff, radio_coeff, window_size, lag, rs
     p["radio_sigmoid_betas"] = np.full(n, radio_coeff / d_max)
     p["window_size"] = window_size
     p["lag"] = lag
+    p["equation"] = equation
     return p
+
+
+def _observation_noise(V, p, rs):
+    """EQ_5_B/C/D: 0.01 * N(0, 1) added to the whole volume array after the simulation (continuous.py:366-367,
+    568-569, 784-785); cancer_sim and EQ_5_A are noise-free."""
+    eq = p.get("equation")
+    if eq is not None and eq.split("_")[-1] in ("B", "C", "D"):
+        return V + 0.01 * rs.normal(size=V.shape)
+    return V
 
 
 def _assign_prob(p, i, volumes_used):
@@ -167,6 +182,7 @@ def simulate_factual(p, seq_length, rs):
         sl[i] = int(t + 1)
         death[i, t] = 1 if b_death else 0
         recov[i, t] = 1 if b_recover else 0
+    V = _observation_noise(V, p, rs)
     return {"cancer_volume": V, "chemo_dosage": chemo_d, "radio_dosage": radio_d, "chemo_application": chemo_a,
             "radio_application": radio_a, "chemo_probabilities": chemo_p, "radio_probabilities": radio_p,
             "sequence_lengths": sl, "death_flags": death, "recovery_flags": recov,
@@ -189,9 +205,12 @@ def get_scaling_params(sim):
     return means, stds
 
 
-def process_data(sim, scaling, treatment_mode="multiclass"):
-    """SyntheticCancerDataset.process_data (dataset.py:96-185) for one-step-ahead data."""
+def process_data(sim, scaling, treatment_mode="multiclass", equation=None):
+    """SyntheticCancerDataset.process_data (dataset.py:96-185) for one-step-ahead data (continuous
+    dataset.py:96-200: EQ_5_A / B set the patient-type std to 1, their single type has std 0)."""
     mean, std = dict(scaling[0]), dict(scaling[1])
+    if equation in ("EQ_5_A", "EQ_5_B"):
+        std["patient_types"] = 1
     offset = horizon = 1
     for k in ("chemo_application", "radio_application"):
         mean[k], std[k] = 0, 1
@@ -320,7 +339,8 @@ def simulate_counterfactual_1_step(p, seq_length, rs):
                 idx += 1
             if fV[t + 1] >= TUMOUR_DEATH_THRESHOLD or recovery_rvs[t] <= np.exp(-fV[t + 1] * TUMOUR_CELL_DENSITY):
                 break
-    return {"cancer_volume": V[:idx], "chemo_application": chemo_a[:idx], "radio_application": radio_a[:idx],
+    V = _observation_noise(V, p, rs)[:idx]          # drawn over the whole preallocated array
+    return {"cancer_volume": V, "chemo_application": chemo_a[:idx], "radio_application": radio_a[:idx],
             "sequence_lengths": sl[:idx], "patient_types": ptypes[:idx]}
 
 
@@ -410,35 +430,46 @@ def simulate_counterfactuals_treatment_seq(p, seq_length, projection_horizon, rs
                 idx += 1
             if fV[t + 1] >= TUMOUR_DEATH_THRESHOLD or recovery_rvs[t] <= np.exp(-fV[t + 1] * TUMOUR_CELL_DENSITY):
                 break
-    return {"cancer_volume": V[:idx], "chemo_application": chemo_a[:idx], "radio_application": radio_a[:idx],
+    V = _observation_noise(V, p, rs)[:idx]          # drawn over the whole preallocated array
+    return {"cancer_volume": V, "chemo_application": chemo_a[:idx], "radio_application": radio_a[:idx],
             "sequence_lengths": sl[:idx], "patient_types": ptypes[:idx], "patient_ids_all_trajectories": pids[:idx],
             "patient_current_t": pcur[:idx]}
 
 
 def make_collection(seed=1, num_patients=None, coeff=2.0, window_size=15, lag=0, seq_length=60, projection_horizon=5,
-                    treatment_mode="multiclass", with_tests=True):
+                    treatment_mode="multiclass", with_tests=True, equation=None):
     """SyntheticCancerDatasetCollection (dataset.py:556-605) + process_data_multi (dataset_collection.py:74-86):
     one np.random.seed(seed) stream for train / val (factual), test one-step and test tau-step
     counterfactual subsets; every subset scaled with the train statistics; the tau-step set's
-    ``data_processed_seq`` holds the last-tau targets (process_sequential_test).  Returns a dict of
-    ``insite_ref.Subset`` with norm_const = TUMOUR_DEATH_THRESHOLD."""
+    ``data_processed_seq`` holds the last-tau targets (process_sequential_test).  ``equation``
+    "EQ_5_A".."EQ_5_D": SyntheticContinuousDatasetCollection (continuous/dataset.py:565-618), whose every
+    subset re-seeds np.random.seed(seed) (:51).  Returns a dict of ``insite_ref.Subset`` with norm_const =
+    TUMOUR_DEATH_THRESHOLD."""
     from . import insite_ref as R
     num_patients = num_patients or {"train": 1000, "val": 100, "test": 100}
     rs = np.random.RandomState(seed)
+
+    def stream():
+        return np.random.RandomState(seed) if equation is not None else rs
+
     sims = {}
-    p = generate_params(num_patients["train"], coeff, coeff, window_size, lag, rs)
-    sims["train"] = simulate_factual(p, seq_length, rs)
-    p = generate_params(num_patients["val"], coeff, coeff, window_size, lag, rs)
-    sims["val"] = simulate_factual(p, seq_length, rs)
+    r = stream()
+    sims["train"] = simulate_factual(generate_params(num_patients["train"], coeff, coeff, window_size, lag, r, equation),
+                                     seq_length, r)
+    r = stream()
+    sims["val"] = simulate_factual(generate_params(num_patients["val"], coeff, coeff, window_size, lag, r, equation),
+                                   seq_length, r)
     if with_tests:
-        p = generate_params(num_patients["test"], coeff, coeff, window_size, lag, rs)
-        sims["test_cf_one_step"] = simulate_counterfactual_1_step(p, seq_length, rs)
-        p = generate_params(num_patients["test"], coeff, coeff, window_size, lag, rs)
-        sims["test_cf_treatment_seq"] = simulate_counterfactuals_treatment_seq(p, seq_length, projection_horizon, rs)
+        r = stream()
+        p = generate_params(num_patients["test"], coeff, coeff, window_size, lag, r, equation)
+        sims["test_cf_one_step"] = simulate_counterfactual_1_step(p, seq_length, r)
+        r = stream()
+        p = generate_params(num_patients["test"], coeff, coeff, window_size, lag, r, equation)
+        sims["test_cf_treatment_seq"] = simulate_counterfactuals_treatment_seq(p, seq_length, projection_horizon, r)
     scaling = get_scaling_params(sims["train"])
     out = {}
     for name, sim in sims.items():
-        data, sp = process_data(sim, scaling, treatment_mode)
+        data, sp = process_data(sim, scaling, treatment_mode, equation)
         seq = R.process_sequential_test(data, sp, projection_horizon) if name == "test_cf_treatment_seq" else None
         out[name] = R.Subset(name, data, sp, seq, TUMOUR_DEATH_THRESHOLD)
     return out
@@ -458,6 +489,50 @@ def sindy_pipeline(coll, threshold=1e-3, alpha=0.5, dt=None, fd="order1"):
     def predict(sub):
         prev, st = R.unscale_inputs(sub.data, sub.scaling_params, 1, 1)
         return R.rollout(prev[:, 0], st, np.argmax(sub.data["current_treatments"], axis=-1), joint, exps, dt, "euler5")
+
+    norm = TUMOUR_DEATH_THRESHOLD
+    one = coll.get("test_cf_one_step")
+    if one is not None:
+        pu = predict(one)
+        o, a_, l_ = R.masked_rmse(pu[..., None], one.data["unscaled_outputs"], one.data["active_entries"], norm,
+                                  one_step_counterfactual=True)
+        res.update(encoder_test_rmse_orig=o, encoder_test_rmse_all=a_, encoder_test_rmse_last=l_)
+    seqs = coll.get("test_cf_treatment_seq")
+    if seqs is not None:
+        pu = predict(seqs)
+        tau = seqs.data_processed_seq["outputs"].shape[1]
+        sl_ = R.autoregressive_slice(pu[..., None], seqs.data["sequence_lengths"], tau)
+        r = R.n_step_rmses(sl_, seqs.data_processed_seq["unscaled_outputs"], seqs.data_processed_seq["active_entries"],
+                           norm)
+        for k, v in enumerate(r):
+            res[f"decoder_test_rmse_{k + 2}-step"] = v
+    return res
+
+
+def joint_pipeline(coll, threshold=1e-3, alpha=0.5, dt=None, fd="order1"):
+    """The one-ODE ablation (run.py:198-201: joint_model, multilabel treatments) on cancer_sim: ONE fit
+    over X = unscaled_outputs[:seq_len] with library inputs (x0, chemo, radio, patient type)
+    (pkpd/utils.py:493-497, 664-672; sindy.py:203), rolled out with the per-step treatments as inputs
+    (sindy.py:317-322).  ``coll`` from ``make_collection(treatment_mode="multilabel")``."""
+    from . import insite_ref as R
+    dt = R.STANDARD_DT if dt is None else dt
+    tr = coll["train"]
+    _, stat = R.unscale_inputs(tr.data, tr.scaling_params, 1, 1)
+    x = tr.data["unscaled_outputs"][..., 0]
+    inputs = np.asarray(tr.data["current_treatments"], dtype=np.float64)
+    rows = tr.data["sequence_lengths"].astype(np.int64)
+    n_in = inputs.shape[-1]
+    exps = R.poly_library(1 + n_in + stat.shape[1], 2, True)
+    names = R.library_names(exps, ["x0"] + [f"u{i}" for i in range(n_in + stat.shape[1])])
+    Z, Y = R.build_regression_joint(x, inputs, stat, rows, dt, fd)
+    c, _, _ = R.stlsq(R.eval_library(exps, Z), Y, threshold, alpha)
+    res = {"joint_coefs": c[None, :], "exps": exps,
+           "global_equation_string": f"Joint Model: x_dot = {R.equation_terms(c, names)}"}
+
+    def predict(sub):
+        prev, st = R.unscale_inputs(sub.data, sub.scaling_params, 1, 1)
+        return R.rollout_inputs(prev[:, 0], st, np.asarray(sub.data["current_treatments"], dtype=np.float64), c, exps,
+                                dt, "euler5")
 
     norm = TUMOUR_DEATH_THRESHOLD
     one = coll.get("test_cf_one_step")

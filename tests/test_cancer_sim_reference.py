@@ -1,0 +1,74 @@
+"""Parity against REFERENCE-HELD OUTPUTS for the treatment-segment family: the
+reference's own cancer_sim and EQ_5_* cohorts, regenerated bit for bit (oracle/cancer_sim_ref.py: the
+Geng tumour simulator and its continuous EQ_5 variant restated with numpy's legacy RandomState draw order,
+np.random.seed(1)), through the oracle pipeline (segment split, FD order 1, 4-arm STLSQ, Euler-5 4-arm
+rollout, the reference's metrics) must reproduce the published runs
+``results/2_main_table/final_with_insite.txt:6`` (cancer_sim), ``:54, :78, :102`` (EQ_5_B..D):
+16-digit equations to 1e-10 and every RMSE metric to 1e-11 relative.
+
+EQ_5_A (``:30``): its single patient type makes the static column u0 == 1, so the library columns
+{1, u0} and {x0, x0 u0} coincide and pysindy's unbias lstsq is singular.  Arms 1 and 2 reproduce the log
+(where the logged solve landed on the minimum-norm split, equal halves, as here); arms 0 and 3 are logged
+as +-1.4e8 / +-3.8e12 and +-1.7e9 / +-1.8e13 pairs -- rounding artefacts of the noise-free, exactly
+singular solve that no restatement can pin.  EQ_5_A's metrics depend on them and are not checked.
+"""
+import json
+import os
+import warnings
+
+import numpy as np
+import pytest
+
+from oracle import cancer_sim_ref as CS
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ANCHORS = json.load(open(os.path.join(HERE, "golden", "reference_log_anchors.json")))
+NAMES = ["1", "x0", "u0", "x0 u0"]
+METRICS = ["encoder_test_rmse_orig", "encoder_test_rmse_all", "encoder_test_rmse_last"] + \
+          [f"decoder_test_rmse_{k}-step" for k in range(2, 7)]
+
+
+def logged_coefs(eq_string, names=NAMES):
+    parts = eq_string.split(" | ")
+    out = np.zeros((len(parts), len(names)))
+    for a, part in enumerate(parts):
+        for term in part.split("= ", 1)[1].split("+")[1:]:
+            c, name = term.split("*", 1)
+            out[a, names.index(name.replace("*", " "))] = float(c)
+    return out
+
+
+@pytest.fixture(scope="module", params=["cancer_sim", "EQ_5_B", "EQ_5_C", "EQ_5_D", "EQ_5_A"])
+def pipeline(request):
+    eq = request.param
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)     # exp overflow of the recovery test, as in the reference
+        coll = CS.make_collection(1, equation=None if eq == "cancer_sim" else eq)
+        return eq, coll, CS.sindy_pipeline(coll)
+
+
+def test_segment_equation_and_metrics_equal_log(pipeline):
+    eq, _, res = pipeline
+    anchor = ANCHORS[f"{eq}/sindy"]
+    ref = logged_coefs(anchor["global_equation_string"])
+    got = res["joint_coefs"]
+    arms = [1, 2] if eq == "EQ_5_A" else [0, 1, 2, 3]
+    assert np.array_equal(got[arms] != 0, ref[arms] != 0)
+    assert np.max(np.abs(got[arms] - ref[arms]) / np.maximum(1.0, np.abs(ref[arms]))) < 1e-10
+    if eq == "EQ_5_A":       # the singular arms 0 / 3: the duplicated columns' halves are equal here
+        np.testing.assert_allclose(got[[0, 3]][:, [0, 1]], got[[0, 3]][:, [2, 3]], rtol=1e-9)
+        return
+    for k in METRICS:
+        assert res[k] == pytest.approx(anchor[k], rel=1e-11), k
+
+
+def test_cohort_layout(pipeline):
+    """The collection's shapes and scaling follow SyntheticCancerDataset.process_data (dataset.py:96-185)."""
+    eq, coll, _ = pipeline
+    tr = coll["train"]
+    assert tr.data["outputs"].shape == (1000, 59, 1)
+    assert tr.data["current_treatments"].shape == (1000, 59, 4)
+    assert np.all(tr.data["current_treatments"].sum(-1) == 1)
+    assert coll["test_cf_treatment_seq"].data_processed_seq["outputs"].shape[1:] == (5, 1)
+    assert coll["val"].scaling_params["output_means"] == tr.scaling_params["output_means"]
+    assert tr.norm_const == pytest.approx(CS.calc_volume(13))

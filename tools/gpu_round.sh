@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU call: selected parity tests, then bench lines.  Every GPU step has its own time limit and the first
+# failure (test failure, crash, timeout) ends the call.
+#   OUT=r03_x TESTS="tests/test_gpu_foo.py" BENCH="--config c5;--config c4 --T 60" bash tools/gpu_round.sh
+# TESTS="all" runs the whole -m gpu suite; empty skips tests.  BENCH is a ';'-separated list of bench.py
+# argument strings ("default" = the driver's default line).
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/${OUT:-round}
+mkdir -p "$O"
+if [ -n "$TESTS" ]; then
+  sel="$TESTS"; [ "$TESTS" = "all" ] && sel="tests"
+  timeout -k 10 ${TEST_LIMIT:-600} python -u -m pytest $sel -m gpu -x -v --timeout 300 --timeout-method thread \
+    -p no:cacheprovider > "$O/tests.log" 2>&1 || { grep -E "PASSED|FAILED|ERROR" "$O/tests.log" | tail -15; tail -40 "$O/tests.log"; exit 1; }
+  grep -cE "PASSED" "$O/tests.log"; tail -2 "$O/tests.log"
+fi
+i=0
+IFS=';' read -ra LINES <<< "$BENCH"
+for b in "${LINES[@]}"; do
+  [ -z "$b" ] && continue
+  [ "$b" = "default" ] && b=""
+  i=$((i + 1))
+  timeout -k 10 ${BENCH_LIMIT:-400} python bench.py $b > "$O/bench_$i.log" 2> "$O/bench_$i.err" || { echo "bench $i failed: $b"; tail -20 "$O/bench_$i.err"; exit 1; }
+  echo "bench $i ($b):"; tail -1 "$O/bench_$i.log" | cut -c1-600
+done
+echo ALLOK
