@@ -49,15 +49,45 @@ LS_MAXITER = 10
 MASK_EPS = 1e-3
 
 
-def active_terms(c0, exps):
-    """Active coefficients (|c0| > 1e-3): list of (flat index, arm, state exponent, column)."""
+def coef_terms(c0, exps, n_inputs=0):
+    """Per flat coefficient q of the global model c0 [A, F]: (arm mask, state exponent, static exponents).
+
+    Separate models (n_inputs = 0, sindy.py:457-467, 489-499, 523-533): coefficient (a, j) acts on arm a
+    only, mask 1 << a.  The joint model (n_inputs > 0, c0 [1, F], library inputs (x0, in_1..in_n, statics),
+    sindy.py:469-483, 503-517, 537-551): the per-step treatments are binary library inputs, so column j,
+    x^e in^tau m(u), contributes m(u) x^e on every treatment combination c (arm = bit code of the step's
+    treatments) whose bits cover tau's inputs -- the fold of ``insite_amd.sindy.SINDY._fold_joint``."""
     A, F = c0.shape
     out = []
     for a in range(A):
         for j in range(F):
-            if abs(c0[a, j]) > MASK_EPS:
-                out.append((a * F + j, a, int(exps[j, 0]), j))
+            e = exps[j]
+            if n_inputs:
+                tin = sum(1 << i for i in range(n_inputs) if e[1 + i] > 0)
+                mask = sum(1 << c for c in range(1 << n_inputs) if (tin & ~c) == 0)
+                ue = tuple(int(v) for v in e[1 + n_inputs:])
+            else:
+                mask, ue = 1 << a, tuple(int(v) for v in e[1:])
+            out.append((mask, int(e[0]), ue))
     return out
+
+
+def n_arms_of(c0, n_inputs=0):
+    return (1 << n_inputs) if n_inputs else c0.shape[0]
+
+
+def active_terms(c0, exps, n_inputs=0):
+    """Active coefficients (|c0| > 1e-3): list of (flat index, arm mask, state exponent, static exponents)."""
+    terms = coef_terms(c0, exps, n_inputs)
+    return [(q, *terms[q]) for q in range(c0.size) if abs(c0.flat[q]) > MASK_EPS]
+
+
+def static_monomial(u, ue):
+    m = 1.0
+    for i, k in enumerate(ue):
+        for _ in range(int(k)):
+            m *= u[i]
+    return m
 
 
 def monomials(u, exps):
@@ -69,15 +99,35 @@ def monomials(u, exps):
     return m
 
 
-class PatientProblem:
-    """f(c_active) and its gradient for one patient: V [T'] unscaled observations, arms [T'] per step,
-    K = min(sl - tau, T' - 1) loss terms."""
+def _poly(g, y):
+    """sum_e g[e] y^e by Horner (the state-polynomial RHS of one arm)."""
+    f = g[-1]
+    for e in range(len(g) - 2, -1, -1):
+        f = g[e] + f * y
+    return f
 
-    def __init__(self, V, arms, u, c0, exps, K, dt, lam, substeps=R.STEPS_FOR_DT):
+
+def _dpoly(g, y):
+    """d/dy sum_e g[e] y^e by Horner."""
+    D = len(g) - 1
+    f = D * g[D]
+    for e in range(D - 1, 0, -1):
+        f = e * g[e] + f * y
+    return f
+
+
+class PatientProblem:
+    """f(c_active) and its gradient for one patient: V [T'] unscaled observations, arms [T'] per step (the
+    arm index, or the treatment combination's bit code for the joint model), K = min(sl - tau, T' - 1)
+    loss terms.  The RHS of arm a is the state polynomial sum_e gamma_{a,e} y^e, gamma_{a,e} = sum over the
+    active coefficients q with arm a in mask_q and exponent e of c_q m_q(u); degree 1 is the affine
+    (alpha_a, beta_a) of the paper's libraries, degree 4 the ABLATION_MORE_COMPLEX_BASIS_FUNCTIONS library."""
+
+    def __init__(self, V, arms, u, c0, exps, K, dt, lam, substeps=R.STEPS_FOR_DT, n_inputs=0):
         self.V = np.asarray(V, dtype=np.float64)
         self.arms = np.asarray(arms, dtype=np.int64)
-        self.terms = active_terms(c0, exps)
-        self.mono = monomials(u, exps)
+        self.terms = active_terms(c0, exps, n_inputs)
+        self.mono = np.array([static_monomial(u, t[3]) for t in self.terms])
         self.c0 = np.array([c0.flat[t[0]] for t in self.terms])
         self.n_total = c0.size
         self.K = int(K)
@@ -85,51 +135,60 @@ class PatientProblem:
         self.sub = substeps
         self.lam = lam
         self.norm = 1.0
-        self.A = c0.shape[0]
+        self.A = n_arms_of(c0, n_inputs)
+        self.D = max(1, int(np.max(exps[:, 0])))
 
     def rates(self, c):
-        al = np.zeros(self.A)
-        be = np.zeros(self.A)
-        for ci, (_, a, ex, j) in zip(c, self.terms):
-            if ex == 0:
-                al[a] += ci * self.mono[j]
-            else:
-                be[a] += ci * self.mono[j]
-        return al, be
+        gam = np.zeros((self.A, self.D + 1))
+        for ci, mi, (_, mask, ex, _) in zip(c, self.mono, self.terms):
+            for a in range(self.A):
+                if (mask >> a) & 1:
+                    gam[a, ex] += ci * mi
+        return gam
 
     def mse_and_grad(self, c):
-        """Euler-5 rollout with forward sensitivities d y / d(alpha_a, beta_a)."""
-        al, be = self.rates(c)
-        A = self.A
+        """Euler-5 rollout with forward sensitivities d y / d gamma_{a,e}."""
+        gam = self.rates(c)
+        A, D = self.A, self.D
         y = self.V[0]
-        dya = np.zeros(A)
-        dyb = np.zeros(A)
+        d = np.zeros((A, D + 1))
         L = 0.0
-        gA = np.zeros(A)
-        gB = np.zeros(A)
+        gG = np.zeros((A, D + 1))
         h = self.h
         for k in range(self.K):
             a = self.arms[k]
+            g = gam[a]
             for _ in range(self.sub):
-                b = be[a]
-                ndya = dya + h * b * dya
-                ndyb = dyb + h * b * dyb
-                ndya[a] += h
-                ndyb[a] += h * y
-                y = y + h * (al[a] + b * y)
-                dya, dyb = ndya, ndyb
+                if D == 1:
+                    hb = h * g[1]
+                    nd = d + hb * d
+                    nd[a, 0] += h
+                    nd[a, 1] += h * y
+                    y = y + h * (g[0] + g[1] * y)
+                else:
+                    hf = h * _dpoly(g, y)
+                    nd = d + hf * d
+                    ye = 1.0
+                    for e in range(D + 1):
+                        nd[a, e] += h * ye
+                        ye *= y
+                    y = y + h * _poly(g, y)
+                d = nd
             r = self.V[k + 1] - y
             L += r * r
-            gA += -2.0 * r * dya
-            gB += -2.0 * r * dyb
-        return L / self.K, gA / self.K, gB / self.K
+            gG += -2.0 * r * d
+        return L / self.K, gG / self.K
 
     def value_and_grad(self, c):
-        L, gA, gB = self.mse_and_grad(c)
+        L, gG = self.mse_and_grad(c)
         f = L / self.norm + self.lam * np.sum((self.c0 - c) ** 2) / self.n_total
         g = np.empty_like(c)
-        for i, (_, a, ex, j) in enumerate(self.terms):
-            g[i] = (gA[a] if ex == 0 else gB[a]) * self.mono[j] / self.norm
+        for i, (_, mask, ex, _) in enumerate(self.terms):
+            gd = 0.0
+            for a in range(self.A):
+                if (mask >> a) & 1:
+                    gd += gG[a, ex]
+            g[i] = gd * self.mono[i] / self.norm
         g += 2.0 * self.lam * (c - self.c0) / self.n_total
         return f, g
 
@@ -283,38 +342,44 @@ def minimize_bfgs(fg, x0, maxiter, gtol=GTOL):
     return x, f, status, k, nfev
 
 
-def euler5_rollout(V0, arms, u, coef, exps, dt, T):
-    """predict_with_reduced_coefs (sindy.py:767-778): Euler-5 scan with every coefficient (no RHS drop)."""
-    mono = monomials(u, exps)
+def euler5_rollout(V0, arms, u, coef, exps, dt, T, n_inputs=0):
+    """predict_with_reduced_coefs (sindy.py:767-778): Euler-5 scan with every coefficient (no RHS drop);
+    arms [T] per-step arm index (joint model: treatment bit code)."""
+    terms = coef_terms(coef, exps, n_inputs)
+    A = n_arms_of(coef, n_inputs)
+    D = max(1, int(np.max(exps[:, 0])))
+    gam = np.zeros((A, D + 1))
+    for q, (mask, ex, ue) in enumerate(terms):
+        for a in range(A):
+            if (mask >> a) & 1:
+                gam[a, ex] += coef.flat[q] * static_monomial(u, ue)
     y = float(V0)
     out = np.empty(T)
     h = dt / R.STEPS_FOR_DT
     for k in range(T):
-        a = int(arms[k])
-        al = sum(coef[a, j] * mono[j] for j in range(exps.shape[0]) if exps[j, 0] == 0)
-        be = sum(coef[a, j] * mono[j] for j in range(exps.shape[0]) if exps[j, 0] == 1)
+        g = gam[int(arms[k])]
         for _ in range(R.STEPS_FOR_DT):
-            y = y + h * (al + be * y)
+            y = y + h * (g[0] + g[1] * y) if D == 1 else y + h * _poly(g, y)
         out[k] = y
     return out
 
 
-def refine_patient(V, arms, u, sl, c0, exps, dt, lam, tau, revert_on_zoom_fail=False):
+def refine_patient(V, arms, u, sl, c0, exps, dt, lam, tau, revert_on_zoom_fail=False, n_inputs=0):
     """One patient of ``simulate_cancer_volume_with_fine_tuning`` (sindy.py:570-668).  Returns
     (preds [T'], refined coefficients [A, F], status, iterations); status -1 = skipped (sl <= tau).
     ``revert_on_zoom_fail``: status 3 keeps c0 (sindy.py:628-631); default False = the published runs
-    (module docstring)."""
+    (module docstring).  ``n_inputs`` > 0: the joint model (c0 [1, F], arms = treatment bit codes)."""
     T = V.shape[0]
     c0 = np.asarray(c0, dtype=np.float64)
     if sl <= tau:
-        return euler5_rollout(V[0], arms, u, c0, exps, dt, T), c0.copy(), -1, 0
+        return euler5_rollout(V[0], arms, u, c0, exps, dt, T, n_inputs), c0.copy(), -1, 0
     K = min(int(sl) - tau, T - 1)
-    pb = PatientProblem(V, arms, u, c0, exps, K, dt, lam)
+    pb = PatientProblem(V, arms, u, c0, exps, K, dt, lam, n_inputs=n_inputs)
     start, _ = pb.value_and_grad(pb.c0)          # norm_const = 1, penalty 0 at c0
     pb.norm = start * 2.5
     x, f, status, k, _ = minimize_bfgs(pb.value_and_grad, pb.c0.copy(), maxiter=200 * c0.size)
     c = c0.copy()
     if status != 3 or not revert_on_zoom_fail:
-        for xi, (flat, _, _, _) in zip(x, pb.terms):
-            c.flat[flat] = xi
-    return euler5_rollout(V[0], arms, u, c, exps, dt, T), c, status, k
+        for xi, t in zip(x, pb.terms):
+            c.flat[t[0]] = xi
+    return euler5_rollout(V[0], arms, u, c, exps, dt, T, n_inputs), c, status, k
