@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define INSITE_ABI_VERSION 4
+#define INSITE_ABI_VERSION 5
 
 /* status codes */
 #define INSITE_OK 0
@@ -327,6 +327,26 @@ int32_t insite_refine_arms_f64(const double* V, int64_t ld_v, int32_t T, const i
                                double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail, double* preds,
                                int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out,
                                const int32_t* row_order, void* stream);
+
+/* INSITE refinement of ANY global model of the reference (ABI 5, csrc/insite_refine.hip): the joint
+ * "one ODE" model (sindy.py:469-483, 503-517, 537-551: one coefficient row over a library whose inputs
+ * include the per-step binary treatments) and the degree-4 library (ABLATION_MORE_COMPLEX_BASIS_FUNCTIONS,
+ * sindy.py:185-186), besides the per-arm models of the two calls above (which it generalises).  Coefficient
+ * q of coef0 [n_coef] contributes c_q * x^coef_exps[q][0] * prod_t u_t^coef_exps[q][1 + t] to the RHS on
+ * every step whose arm a has bit a set in coef_arm_mask[q]; per-arm models: q = a * F + j, mask 1 << a;
+ * the joint model: arm = the step's treatment bit code, mask = the codes that switch on column j's
+ * treatment inputs (their exponents dropped, binary inputs).  State exponents <= 4 (a model with a
+ * non-zero coefficient of exponent >= 2 runs the state-polynomial kernels).  Objective, BFGS, status and
+ * outputs as insite_refine_f64; coef_out [n_rows, n_coef].
+ *   arm_bits TIME_MAJOR_BITS [T, ld_arm] (n_arms <= 2)  XOR  arm [T, ld_arm] int8 (n_arms <= 4)
+ *   coef0 / coef_arm_mask [n_coef] / coef_exps [n_coef][1 + n_statics]: HOST arrays, n_coef <= 72  */
+int32_t insite_refine_general_f64(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits,
+                                  const int8_t* arm, int64_t ld_arm, const double* u, const int32_t* seq_len,
+                                  int64_t n_rows, int32_t n_statics, int32_t n_coef, const double* coef0,
+                                  const int32_t* coef_arm_mask, const int8_t* coef_exps, int32_t n_arms, double dt,
+                                  double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail,
+                                  double* preds, int64_t ld_p, double* coef_out, int32_t* status_out,
+                                  int32_t* iters_out, const int32_t* row_order, void* stream);
 
 /* General one-state discovery (insite_gen.hip): libraries with state exponents up to 4 and/or per-step
  * binary treatment INPUTS — the reference's degree-4 ablation (PolynomialLibrary(degree=4,

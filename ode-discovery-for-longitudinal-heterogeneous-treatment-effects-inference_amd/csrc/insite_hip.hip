@@ -2447,473 +2447,6 @@ __global__ void __launch_bounds__(kBlock) rk45_bin_scatter_kernel(const int32_t*
 }
 
 // =============================================================================================
-// INSITE per-patient refinement
-// =============================================================================================
-// Reference: SINDY._get_fine_tuned_predictions / f_to_min_func / predict_with_reduced_coefs
-// (sindy.py:433-715, 767-794); restatement oracle/insite_refine_ref.py.  Lane = patient.  Objective
-//   f(c) = mse(c * mask) / (2.5 mse(c0)) + lam * mean((c0 - c)^2),  mask = |c0| > 1e-3,
-//   mse  = mean over k < min(sl - tau, T - 1) of (V[k+1] - pred_k)^2, pred = Euler-5 scan from V[0],
-// minimised by jax.scipy.optimize.minimize(method='BFGS') restated (oracle docstring): BFGS with the
-// inverse-Hessian update, strong-Wolfe line search, cubic/quadratic/bisection zoom.  The objective
-// depends on c only through (alpha_a, beta_a) of the state-affine RHS, so one forward pass with 2 NA
-// tangents d y / d(alpha_a, beta_a) gives f and the exact gradient (what jax's autodiff computes).
-// NA = 2: TIME_MAJOR_BITS arms (PK/PD EQ_4); NA = 4: int8 arms, the 4-valued treatment of cancer_sim /
-// EQ_5 (sindy.py:484-550, argmax(treatment) selects the arm's coefficients).  Only the m active coefficients move (the search runs in that subspace; oracle
-// docstring); every lane runs its own optimiser — lanes finishing early idle until the wave's last.
-// M <= 8 (the sparse models of the paper): the whole optimiser state lives in VGPRs, every loop unrolled,
-// and the inverse-Hessian update is the oracle's w @ H @ w.T.  M = 16 and M = 36 (dense global models, up
-// to A * F = 36 active coefficients, e.g. a 4-arm EQ_5 fit keeping every term) use rolled loops (RU = 1):
-// the arrays are dynamically indexed and live in per-lane scratch, and the update is the O(M^2) expansion
-// (one H y product, no M x M temporaries).  Measured at 200k 4-arm rows (tools/refine_arms_bench.py):
-// M = 16 unrolled 80 ms (512 VGPRs + 5.5k spilled) vs rolled 62 ms; M = 36 rolled O(M^3) 1437 ms vs
-// O(M^2) 108 ms; M = 8 5.5 ms.
-constexpr int kRefineMaxActive = INSITE_MAX_ARMS * INSITE_MAX_TERMS;
-#ifndef INSITE_REFINE_REG
-#define INSITE_REFINE_REG 8  // largest M whose loops are fully unrolled (register-resident state)
-#endif
-constexpr int kRefineRegActive = INSITE_REFINE_REG;
-struct RefineArgs {
-  const double* V;      // [T, ldv] unscaled observations (time-major)
-  const uint32_t* arm;  // TIME_MAJOR_BITS [T, lda] per-step arm (NA = 2)
-  const int8_t* arm8;   // [T, lda] int8 per-step arm (NA = 4)
-  const double* u;      // [N, U]
-  const int32_t* sl;    // [N] sequence lengths
-  double* preds;        // [T, ldp]
-  double* coef_out;     // [N, A, F] or NULL
-  int32_t* status;      // [N] or NULL (-1 skipped, else the BFGS status)
-  int32_t* iters;       // [N] or NULL
-  const int32_t* order; // [N] lane -> row (rows binned by seq_len, insite_rk45_order_i32), NULL = identity
-  int64_t ldv, lda, ldp, N;
-  int32_t T, tau, sub, A, m, n_total;
-  int32_t revert3;      // 1: BFGS status 3 reverts to the global model (sindy.py:628-631); 0: keep the iterate
-  double dt, lam;
-  int32_t t_flat[kRefineMaxActive], t_arm[kRefineMaxActive], t_ex[kRefineMaxActive], t_col[kRefineMaxActive];
-  double c0[INSITE_MAX_ARMS * INSITE_MAX_TERMS];  // the global model [A, F]
-};
-
-template <int M, int NA>
-struct RefineLane {
-  static constexpr int RU = M <= kRefineRegActive ? M : 1;
-  // sub-step loop unrolled by odeint's 5 (the default): measured 12 active 62 -> 43 ms, 6 active 5.5 -> 5.2 ms;
-  // for M = 4 (EQ_4 bench, 9.6 -> 10.1 ms) and M = 36 (110 -> 117 ms) it is slower and stays rolled
-  static constexpr int SU = (M > 4 && M <= 16) ? 5 : 1;
-  const RefineArgs& ra;
-  const LibDesc& lib;
-  int64_t p;
-  int K;
-  double norm;
-  double mono[M];
-  double c0a[M];
-  __device__ int armbit(int k) const {
-    if constexpr (NA == 2) return (int)((ra.arm[(int64_t)k * ra.lda + (p >> 5)] >> (p & 31)) & 1u);
-    else return (int)ra.arm8[(int64_t)k * ra.lda + p];
-  }
-  // f and gradient at c (active coordinates)
-  __device__ double fg(const double (&c)[M], double (&g)[M]) const {
-    double al[NA], be[NA];
-#pragma unroll RU
-    for (int a = 0; a < NA; ++a) al[a] = be[a] = 0.0;
-#pragma unroll RU
-    for (int i = 0; i < M; ++i) {
-      if (i >= ra.m) break;
-      const double t = c[i] * mono[i];
-#pragma unroll RU
-      for (int a = 0; a < NA; ++a)
-        if (ra.t_arm[i] == a) {
-          if (ra.t_ex[i] == 0) al[a] += t;
-          else be[a] += t;
-        }
-    }
-    const double h = ra.dt / (double)ra.sub;
-    double y = ra.V[p];
-    double da[NA], db[NA], gA[NA], gB[NA];
-#pragma unroll RU
-    for (int a = 0; a < NA; ++a) da[a] = db[a] = gA[a] = gB[a] = 0.0;
-    double L = 0.0;
-    // step k's arm and target are requested one step ahead (issued before step k - 1's sub-steps) so the
-    // dependent Euler chain does not wait on a load per step
-    int ak_nx = armbit(0);
-    double v_nx = ra.V[ra.ldv + p];
-    for (int k = 0; k < K; ++k) {
-      const int ak = ak_nx;
-      const double vk1 = v_nx;
-      if (k + 1 < K) {
-        ak_nx = armbit(k + 1);
-        v_nx = ra.V[(int64_t)(k + 2) * ra.ldv + p];
-      }
-      double alk = al[0], bek = be[0];
-#pragma unroll RU
-      for (int a = 1; a < NA; ++a)
-        if (ak == a) {
-          alk = al[a];
-          bek = be[a];
-        }
-      const double hb = h * bek;
-#pragma unroll SU
-      for (int s = 0; s < ra.sub; ++s) {
-#pragma unroll RU
-        for (int a = 0; a < NA; ++a) {
-          da[a] = da[a] + hb * da[a];
-          db[a] = db[a] + hb * db[a];
-          if (ak == a) {
-            da[a] += h;
-            db[a] += h * y;
-          }
-        }
-        y = y + h * (alk + bek * y);
-      }
-      const double r = vk1 - y;
-      L += r * r;
-#pragma unroll RU
-      for (int a = 0; a < NA; ++a) {
-        gA[a] += -2.0 * r * da[a];
-        gB[a] += -2.0 * r * db[a];
-      }
-    }
-    const double iK = 1.0 / (double)K;
-    L *= iK;
-    double pen = 0.0;
-#pragma unroll RU
-    for (int i = 0; i < M; ++i) {
-      if (i >= ra.m) {
-        g[i] = 0.0;
-        continue;
-      }
-      const double d = c0a[i] - c[i];
-      pen += d * d;
-      double gd = 0.0;
-#pragma unroll RU
-      for (int a = 0; a < NA; ++a)
-        if (ra.t_arm[i] == a) gd = ra.t_ex[i] == 0 ? gA[a] : gB[a];
-      g[i] = gd * iK * mono[i] / norm + 2.0 * ra.lam * (c[i] - c0a[i]) / (double)ra.n_total;
-    }
-    return L / norm + ra.lam * pen / (double)ra.n_total;
-  }
-  __device__ double dot(const double (&a)[M], const double (&b)[M]) const {
-    double s = 0.0;
-#pragma unroll RU
-    for (int i = 0; i < M; ++i) s += a[i] * b[i];
-    return s;
-  }
-  // phi(t) = f(x + t pk), dphi = g . pk
-  __device__ double phi(const double (&x)[M], const double (&pk)[M], double t, double& dphi, double (&g)[M]) const {
-    double xt[M];
-#pragma unroll RU
-    for (int i = 0; i < M; ++i) xt[i] = x[i] + t * pk[i];
-    const double f = fg(xt, g);
-    dphi = dot(g, pk);
-    return f;
-  }
-};
-
-__device__ __forceinline__ double cubicmin(double a, double fa, double fpa, double b, double fb, double c, double fc) {
-  const double C = fpa, db = b - a, dc = c - a;
-  const double denom = (db * dc) * (db * dc) * (db - dc);
-  const double A = (dc * dc * (fb - fa - C * db) + (-db * db) * (fc - fa - C * dc)) / denom;
-  const double B = ((-dc * dc * dc) * (fb - fa - C * db) + (db * db * db) * (fc - fa - C * dc)) / denom;
-  const double radical = B * B - 3.0 * A * C;
-  return a + (-B + sqrt(radical)) / (3.0 * A);
-}
-__device__ __forceinline__ double quadmin(double a, double fa, double fpa, double b, double fb) {
-  const double db = b - a;
-  const double B = (fb - fa - fpa * db) / (db * db);
-  return a - fpa / (2.0 * B);
-}
-
-#ifndef INSITE_REFINE_WPE4
-#define INSITE_REFINE_WPE4 4
-#endif
-#ifndef INSITE_REFINE_WPE8
-#define INSITE_REFINE_WPE8 1
-#endif
-#ifndef INSITE_REFINE_QUAD
-#define INSITE_REFINE_QUAD 0  // 1: the O(M^2) inverse-Hessian update for the unrolled kernels too
-#endif
-// M <= 4 (the EQ_4 models: two terms per arm) is sized for INSITE_REFINE_WPE4 waves per SIMD (<= 128
-// VGPRs; unconstrained the compiler takes 202 and runs 2 waves): the objective scan is a dependent fp64
-// chain per lane, hidden only by other waves.
-template <int M, int NA>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(M <= 4 ? INSITE_REFINE_WPE4 : (M <= 8 ? INSITE_REFINE_WPE8 : 1))))
-insite_refine_kernel(RefineArgs ra, LibDesc lib) {
-  constexpr int RU = RefineLane<M, NA>::RU;
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= ra.N) return;
-  // lane -> row: with rows binned by seq_len the lanes of a wave scan similar prefixes (K = sl - tau steps
-  // per objective evaluation), so a wave no longer runs every evaluation to its longest row's length;
-  // every row's computation is independent of its lane, so outputs are bitwise the same in any order
-  const int64_t p = ra.order ? (int64_t)ra.order[gid] : gid;
-  double uu[INSITE_MAX_STATICS];
-#pragma unroll RU
-  for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < lib.U ? ra.u[p * lib.U + t] : 0.0;
-  RefineLane<M, NA> ln{ra, lib, p, 0, 1.0, {}, {}};
-#pragma unroll RU
-  for (int i = 0; i < M; ++i) {
-    ln.mono[i] = i < ra.m ? monomial(lib, ra.t_col[i], uu) : 0.0;
-    ln.c0a[i] = i < ra.m ? ra.c0[ra.t_flat[i]] : 0.0;
-  }
-  double x[M];
-#pragma unroll RU
-  for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
-  const int sl = ra.sl[p];
-  int status = -1, nit = 0;
-  if (sl > ra.tau && ra.T >= 2) {
-    ln.K = min(sl - ra.tau, ra.T - 1);
-    double g[M];
-    const double start = ln.fg(x, g);  // norm 1, penalty 0 at c0
-    ln.norm = start * 2.5;
-    // ---------------- BFGS (jax minimize_bfgs, norm = inf, gtol 1e-5) ----------------
-    double H[M][M];
-#pragma unroll RU
-    for (int i = 0; i < M; ++i)
-#pragma unroll RU
-      for (int j = 0; j < M; ++j) H[i][j] = i == j ? 1.0 : 0.0;
-    double f = ln.fg(x, g);
-    double gmax = 0.0, g2 = 0.0;
-#pragma unroll RU
-    for (int i = 0; i < M; ++i) {
-      gmax = fmax(gmax, fabs(g[i]));
-      g2 += g[i] * g[i];
-    }
-    bool converged = gmax < 1e-5, failed = false;
-    double old_old = f + sqrt(g2) / 2.0;
-    int ls_status = 0;
-    const int maxiter = 200 * ra.n_total;
-    int k = 0;
-    while (!converged && !failed && k < maxiter) {
-      double pk[M];
-#pragma unroll RU
-      for (int i = 0; i < M; ++i) {
-        double s = 0.0;
-#pragma unroll RU
-        for (int j = 0; j < M; ++j) s += H[i][j] * g[j];
-        pk[i] = -s;
-      }
-      // ---- line search (jax line_search, c1 1e-4, c2 0.9, maxiter 10) ----
-      const double phi0 = f, dphi0 = ln.dot(g, pk);
-      const double cand = 1.01 * 2.0 * (phi0 - old_old) / dphi0;
-      const double start_a = cand > 1.0 ? 1.0 : cand;
-      bool ls_done = false, ls_failed = false;
-      int li = 1;
-      double a_i1 = 0.0, phi_i1 = phi0, dphi_i1 = dphi0;
-      double a_star = 0.0, phi_star = phi0;
-      double g_star[M];
-#pragma unroll RU
-      for (int i = 0; i < M; ++i) g_star[i] = g[i];
-      auto wolfe_one = [&](double a_, double ph) { return ph > phi0 + 1e-4 * a_ * dphi0; };
-      auto wolfe_two = [&](double dph) { return fabs(dph) <= -0.9 * dphi0; };
-      // zoom between (lo, hi); returns failure, fills the star point on success
-      auto zoom = [&](double a_lo, double phi_lo, double dphi_lo, double a_hi, double phi_hi, double dphi_hi,
-                      bool& z_failed) {
-        bool done = false;
-        z_failed = false;
-        int j = 0;
-        double a_rec = (a_lo + a_hi) / 2.0, phi_rec = (phi_lo + phi_hi) / 2.0;
-        double za = 1.0, zphi = phi_lo;
-        double zg[M];
-#pragma unroll RU
-        for (int i = 0; i < M; ++i) zg[i] = g[i];
-        while (!done && !z_failed) {
-          const double dalpha = a_hi - a_lo;
-          const double lo = fmin(a_hi, a_lo), hi = fmax(a_hi, a_lo);
-          const double cchk = 0.2 * dalpha, qchk = 0.1 * dalpha;
-          z_failed = z_failed || (dalpha <= 1e-10);
-          const double a_cub = cubicmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi, a_rec, phi_rec);
-          const bool use_cubic = (j > 0) && (a_cub > lo + cchk) && (a_cub < hi - cchk);
-          const double a_quad = quadmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi);
-          const bool use_quad = !use_cubic && (a_quad > lo + qchk) && (a_quad < hi - qchk);
-          double a_j = a_rec;
-          if (use_cubic) a_j = a_cub;
-          if (use_quad) a_j = a_quad;
-          if (!use_cubic && !use_quad) a_j = (a_lo + a_hi) / 2.0;
-          double dphi_j, g_j[M];
-          const double phi_j = ln.phi(x, pk, a_j, dphi_j, g_j);
-          const bool hi_to_j = wolfe_one(a_j, phi_j) || (phi_j >= phi_lo);
-          const bool star_to_j = wolfe_two(dphi_j) && !hi_to_j;
-          const bool hi_to_lo = (dphi_j * (a_hi - a_lo) >= 0.0) && !hi_to_j && !star_to_j;
-          const bool lo_to_j = !hi_to_j && !star_to_j;
-          if (hi_to_j) {
-            a_rec = a_hi;
-            phi_rec = phi_hi;
-            a_hi = a_j;
-            phi_hi = phi_j;
-            dphi_hi = dphi_j;
-          }
-          done = done || star_to_j;
-          if (star_to_j) {
-            za = a_j;
-            zphi = phi_j;
-#pragma unroll RU
-            for (int i = 0; i < M; ++i) zg[i] = g_j[i];
-          }
-          if (hi_to_lo) {
-            a_rec = a_hi;
-            phi_rec = phi_hi;
-            a_hi = a_lo;
-            phi_hi = phi_lo;
-            dphi_hi = dphi_lo;
-          }
-          if (lo_to_j) {
-            a_rec = a_lo;
-            phi_rec = phi_lo;
-            a_lo = a_j;
-            phi_lo = phi_j;
-            dphi_lo = dphi_j;
-          }
-          ++j;
-          z_failed = ((z_failed ? 1 : 0) | j) >= 30;  // jax: `failed | j >= 30` (no parentheses)
-        }
-        a_star = za;
-        phi_star = zphi;
-#pragma unroll RU
-        for (int i = 0; i < M; ++i) g_star[i] = zg[i];
-      };
-      while (!ls_done && li <= 10 && !ls_failed) {
-        const double a_i = li == 1 ? start_a : a_i1 * 2.0;
-        double dphi_i, g_i[M];
-        const double phi_i = ln.phi(x, pk, a_i, dphi_i, g_i);
-        const bool s_z1 = wolfe_one(a_i, phi_i) || ((phi_i >= phi_i1) && (li > 1));
-        const bool s_i = wolfe_two(dphi_i) && !s_z1;
-        const bool s_z2 = (dphi_i >= 0.0) && !s_z1 && !s_i;
-        if (s_z1) {
-          bool zf;
-          zoom(a_i1, phi_i1, dphi_i1, a_i, phi_i, dphi_i, zf);
-          ls_failed = ls_failed || zf;
-        }
-        if (s_i) {
-          a_star = a_i;
-          phi_star = phi_i;
-#pragma unroll RU
-          for (int i = 0; i < M; ++i) g_star[i] = g_i[i];
-        }
-        if (s_z2) {
-          bool zf;
-          zoom(a_i, phi_i, dphi_i, a_i1, phi_i1, dphi_i1, zf);
-          ls_failed = ls_failed || zf;
-        }
-        ls_done = s_z1 || ls_done || s_i || s_z2;
-        ++li;
-        a_i1 = a_i;
-        phi_i1 = phi_i;
-        dphi_i1 = dphi_i;
-      }
-      ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
-      failed = ls_failed || !ls_done;
-      // ---- BFGS update ----
-      double sk[M], yk[M];
-#pragma unroll RU
-      for (int i = 0; i < M; ++i) {
-        sk[i] = a_star * pk[i];
-        yk[i] = g_star[i] - g[i];
-      }
-      const double rho = 1.0 / ln.dot(yk, sk);
-      if (isfinite(rho) && (RU == 1 || INSITE_REFINE_QUAD)) {
-        // rolled (scratch-resident) kernels: the same update expanded to O(M^2) with one matrix-vector
-        // product, (I - rho s y^T) H (I - rho y s^T) + rho s s^T
-        //   = H - rho (s (H y)^T + (H y) s^T) + (rho^2 y^T H y + rho) s s^T   (H symmetric),
-        // instead of two O(M^3) products through two more M x M scratch matrices; the association order
-        // differs from the oracle's w @ H @ w.T (jax's three-operand einsum fixes none either)
-        double hy[M];
-        double yhy = 0.0;
-#pragma unroll RU
-        for (int i = 0; i < M; ++i) {
-          double t = 0.0;
-#pragma unroll RU
-          for (int j = 0; j < M; ++j) t += H[i][j] * yk[j];
-          hy[i] = t;
-          yhy += yk[i] * t;
-        }
-        const double cs = rho * rho * yhy + rho;
-#pragma unroll RU
-        for (int i = 0; i < M; ++i)
-#pragma unroll RU
-          for (int j = 0; j < M; ++j)
-            H[i][j] = H[i][j] - rho * (sk[i] * hy[j] + hy[i] * sk[j]) + cs * (sk[i] * sk[j]);
-      } else if (isfinite(rho)) {
-        double W[M][M], WH[M][M];
-#pragma unroll RU
-        for (int i = 0; i < M; ++i)
-#pragma unroll RU
-          for (int j = 0; j < M; ++j) W[i][j] = (i == j ? 1.0 : 0.0) - rho * (sk[i] * yk[j]);
-#pragma unroll RU
-        for (int i = 0; i < M; ++i)
-#pragma unroll RU
-          for (int j = 0; j < M; ++j) {
-            double s = 0.0;
-#pragma unroll RU
-            for (int q = 0; q < M; ++q) s += W[i][q] * H[q][j];
-            WH[i][j] = s;
-          }
-#pragma unroll RU
-        for (int i = 0; i < M; ++i)
-#pragma unroll RU
-          for (int j = 0; j < M; ++j) {
-            double s = 0.0;
-#pragma unroll RU
-            for (int q = 0; q < M; ++q) s += WH[i][q] * W[j][q];
-            H[i][j] = s + rho * (sk[i] * sk[j]);
-          }
-      }
-      double gm = 0.0;
-#pragma unroll RU
-      for (int i = 0; i < M; ++i) {
-        x[i] = x[i] + sk[i];
-        g[i] = g_star[i];
-        gm = fmax(gm, fabs(g[i]));
-      }
-      converged = gm < 1e-5;
-      old_old = f;
-      f = phi_star;
-      ++k;
-    }
-    nit = k;
-    status = converged ? 0 : (k == maxiter ? 1 : (failed ? 2 + ls_status : -1));
-    if (status == 3 && ra.revert3) {  // zoom failed: the reference code keeps the global coefficients (sindy.py:628-631)
-#pragma unroll RU
-      for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
-    }
-  }
-  // ---------------- final Euler scan with the (refined) model, every coefficient (sindy.py:668) ----------------
-  // coefficient (a, j): the refined value if active, else the global one; resolved by comparison
-  // against the active list (no dynamically indexed per-lane array, which would live in scratch)
-  auto coef_at = [&](int q) -> double {
-    double c = ra.c0[q];
-#pragma unroll RU
-    for (int i = 0; i < M; ++i)
-      if (i < ra.m && ra.t_flat[i] == q) c = x[i];
-    return c;
-  };
-  double al[NA], be[NA];
-#pragma unroll RU
-  for (int a = 0; a < NA; ++a) al[a] = be[a] = 0.0;
-#pragma unroll RU
-  for (int a = 0; a < NA; ++a)
-    if (a < ra.A)
-      for (int j = 0; j < lib.F; ++j) {
-        const double t = coef_at(a * lib.F + j) * monomial(lib, j, uu);
-        if (col_ex(lib, j) == 0) al[a] += t;
-        else be[a] += t;
-      }
-  const double h = ra.dt / (double)ra.sub;
-  double y = ra.V[p];
-  for (int k = 0; k < ra.T; ++k) {
-    const int ak = ln.armbit(k);
-    double alk = al[0], bek = be[0];
-#pragma unroll RU
-    for (int a = 1; a < NA; ++a)
-      if (ak == a) {
-        alk = al[a];
-        bek = be[a];
-      }
-    for (int s = 0; s < ra.sub; ++s) y = y + h * (alk + bek * y);
-    ra.preds[(int64_t)k * ra.ldp + p] = y;
-  }
-  if (ra.coef_out)
-    for (int q = 0; q < ra.A * lib.F; ++q) ra.coef_out[p * ra.A * lib.F + q] = coef_at(q);
-  if (ra.status) ra.status[p] = status;
-  if (ra.iters) ra.iters[p] = nit;
-}
-
-// =============================================================================================
 // Masked squared-error sums (metrics)
 // =============================================================================================
 __global__ void __launch_bounds__(kBlock)
@@ -3970,104 +3503,6 @@ int32_t insite_rk45_order_i32(const int32_t* n_obs, int64_t n_rows, int32_t T_ma
   return launch_status();
 }
 
-namespace {
-// Shared argument checks and launch of insite_refine_f64 (NA = 2, bit arms) and
-// insite_refine_arms_f64 (NA = 4, int8 arms).
-int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, const int8_t* arm8,
-                      int64_t ld_arm, const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
-                      const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam,
-                      int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail, double* preds, int64_t ld_p,
-                      double* coef_out, int32_t* status_out, int32_t* iters_out, const int32_t* row_order,
-                      void* stream) {
-  const bool bits = arm8 == nullptr;
-  if (n_rows < 0 || T < 1 || n_arms < 1 || n_arms > (bits ? 2 : 4) || substeps < 1 || !(dt > 0.0) ||
-      !(lam >= 0.0) || tau < 0 || ld_v < n_rows || ld_p < n_rows ||
-      ld_arm < (bits ? (n_rows + 31) / 32 : n_rows) || !coef0)
-    return INSITE_E_INVALID_ARG;
-  LibDesc lib;
-  int32_t st = build_lib(exps, n_terms, n_statics, &lib);
-  if (st != INSITE_OK) return st;
-  if (n_rows == 0) return INSITE_OK;
-  if (!V || (bits && !arm_bits) || !seq_len || !preds || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
-  RefineArgs ra{};
-  ra.V = V;
-  ra.arm = arm_bits;
-  ra.arm8 = arm8;
-  ra.u = n_statics > 0 ? u : V;
-  ra.sl = seq_len;
-  ra.preds = preds;
-  ra.coef_out = coef_out;
-  ra.status = status_out;
-  ra.iters = iters_out;
-  ra.order = row_order;
-  ra.ldv = ld_v;
-  ra.lda = ld_arm;
-  ra.ldp = ld_p;
-  ra.N = n_rows;
-  ra.T = T;
-  ra.tau = tau;
-  ra.sub = substeps;
-  ra.revert3 = revert_on_zoom_fail != 0;
-  ra.A = n_arms;
-  ra.n_total = n_arms * n_terms;
-  ra.dt = dt;
-  ra.lam = lam;
-  int m = 0;
-  for (int a = 0; a < n_arms; ++a)
-    for (int j = 0; j < n_terms; ++j) {
-      const double c = coef0[a * n_terms + j];
-      ra.c0[a * n_terms + j] = c;
-      if (fabs(c) > 1e-3) {  // coef_sparse_mask (sindy.py:587)
-        if (m >= kRefineMaxActive) return INSITE_E_UNSUPPORTED;
-        ra.t_flat[m] = a * n_terms + j;
-        ra.t_arm[m] = a;
-        ra.t_ex[m] = lib.ex[j];
-        ra.t_col[m] = j;
-        ++m;
-      }
-    }
-  ra.m = m;
-  const dim3 grid((unsigned)((n_rows + kBlock - 1) / kBlock));
-  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
-  if (bits) {
-    if (m <= 4) insite_refine_kernel<4, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
-    else if (m <= 8) insite_refine_kernel<8, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
-    else if (m <= 16) insite_refine_kernel<16, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
-    else insite_refine_kernel<kRefineMaxActive, 2><<<grid, kBlock, 0, hs>>>(ra, lib);
-  } else {
-    if (m <= 4) insite_refine_kernel<4, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
-    else if (m <= 8) insite_refine_kernel<8, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
-    else if (m <= 16) insite_refine_kernel<16, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
-    else insite_refine_kernel<kRefineMaxActive, 4><<<grid, kBlock, 0, hs>>>(ra, lib);
-  }
-  return launch_status();
-}
-}  // namespace
-
-int32_t insite_refine_f64(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, int64_t ld_arm,
-                          const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics, const int8_t* exps,
-                          int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam, int32_t tau,
-                          int32_t substeps, int32_t revert_on_zoom_fail, double* preds, int64_t ld_p,
-                          double* coef_out, int32_t* status_out, int32_t* iters_out, const int32_t* row_order,
-                          void* stream) {
-  if (!arm_bits && n_rows > 0) return INSITE_E_INVALID_ARG;
-  return refine_launch(V, ld_v, T, arm_bits, nullptr, ld_arm, u, seq_len, n_rows, n_statics, exps, n_terms, coef0,
-                       n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds, ld_p, coef_out, status_out,
-                       iters_out, row_order, stream);
-}
-
-int32_t insite_refine_arms_f64(const double* V, int64_t ld_v, int32_t T, const int8_t* arm, int64_t ld_arm,
-                               const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
-                               const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt,
-                               double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail, double* preds,
-                               int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out,
-                               const int32_t* row_order, void* stream) {
-  if (!arm && n_rows > 0) return INSITE_E_INVALID_ARG;
-  static const int8_t kNoArms = 0;  // non-null marker for the int8 format when n_rows == 0
-  return refine_launch(V, ld_v, T, nullptr, arm ? arm : &kNoArms, ld_arm, u, seq_len, n_rows, n_statics, exps,
-                       n_terms, coef0, n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds, ld_p, coef_out,
-                       status_out, iters_out, row_order, stream);
-}
 
 size_t insite_masked_sse_workspace_bytes(int64_t n_rows, int32_t T) {
   if (n_rows < 0 || T < 0) return 0;

@@ -1,0 +1,704 @@
+// insite_refine.hip — INSITE per-patient refinement on MI355X (gfx950): one lane per row, the BFGS
+// optimiser state in VGPRs (sparse models) or per-lane scratch (dense ones).
+//
+// Reference: SINDY._get_fine_tuned_predictions / f_to_min_func / predict_with_reduced_coefs
+// (libs_m/ct/src/models/sindy.py:433-715, 767-794); restatement oracle/insite_refine_ref.py.  Per row
+//   f(c) = mse(c * mask) / (2.5 mse(c0)) + lam * mean((c0 - c)^2),  mask = |c0| > 1e-3,
+//   mse  = mean over k < min(sl - tau, T - 1) of (V[k+1] - pred_k)^2, pred = Euler-5 scan from V[0],
+// minimised by jax.scipy.optimize.minimize(method='BFGS') restated: BFGS with the inverse-Hessian update,
+// strong-Wolfe line search, cubic / quadratic / bisection zoom (oracle docstring).
+//
+// Every model of the reference is described per global coefficient q by (arm mask, state exponent e_q,
+// static monomial m_q(u)): on a step whose arm is a the RHS is the state polynomial
+//   f_a(y) = sum_e gamma_{a,e} y^e,   gamma_{a,e} = sum_{q : a in mask_q, e_q = e} c_q m_q(u).
+//   * separate per-arm models (sindy.py:457-467, 489-499, 523-533): q = (a, j), mask 1 << a;
+//   * the joint "one ODE" model (sindy.py:469-483, 503-517, 537-551): one coefficient row whose library
+//     takes the per-step binary treatments as inputs; "arm" = the step's treatment bit code, and column j
+//     (x^e in^tau m(u)) acts on every code covering tau's inputs (the fold of insite_amd SINDY._fold_joint);
+//   * the degree-4 library (ABLATION_MORE_COMPLEX_BASIS_FUNCTIONS, sindy.py:185-186): e_q up to 4.
+// The objective depends on c only through gamma, so one forward pass with NA (D + 1) tangents
+// d y / d gamma_{a,e} gives f and its exact gradient (what jax's autodiff computes):
+//   d <- d (1 + h f_a'(y)) + [arm == a] h y^e,  then y <- y + h f_a(y)   (D = 1: f' = gamma_{a,1}).
+// Only the m active coefficients move (inactive ones have zero data gradient and start at c0, so BFGS
+// with H0 = I keeps their block fixed): the search runs in the m-dimensional active subspace.
+// M <= 8: the optimiser state lives in VGPRs, every loop unrolled, inverse-Hessian update w @ H @ w.T as in
+// the oracle.  M = 16 / 72 (dense global models): rolled loops (RU = 1), per-lane scratch, the O(M^2)
+// update.  Measured at 200k 4-arm rows (tools/refine_arms_bench.py): M = 16 unrolled 80 ms (512 VGPRs +
+// spills) vs rolled 62 ms; M = 36 rolled O(M^3) 1437 ms vs O(M^2) 108 ms; M = 8 5.5 ms.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+
+#include "insite_hip.h"
+#include "insite_common.h"
+
+namespace {
+
+constexpr int kRefineMaxCoef = 72;  // n_arms * F of a global model: the degree-4 library, 2 arms x 35 terms
+#ifndef INSITE_REFINE_REG
+#define INSITE_REFINE_REG 8  // largest M whose loops are fully unrolled (register-resident state)
+#endif
+constexpr int kRefineRegActive = INSITE_REFINE_REG;
+
+struct RefineArgs {
+  const double* V;      // [T, ldv] unscaled observations (time-major)
+  const uint32_t* arm;  // TIME_MAJOR_BITS [T, lda] per-step arm (NA = 2)
+  const int8_t* arm8;   // [T, lda] int8 per-step arm (NA = 4)
+  const double* u;      // [N, U]
+  const int32_t* sl;    // [N] sequence lengths
+  double* preds;        // [T, ldp]
+  double* coef_out;     // [N, n_coef] or NULL
+  int32_t* status;      // [N] or NULL (-1 skipped, else the BFGS status)
+  int32_t* iters;       // [N] or NULL
+  const int32_t* order; // [N] lane -> row (rows binned by seq_len), NULL = identity
+  int64_t ldv, lda, ldp, N;
+  int32_t T, tau, sub, U, A, m, n_coef;
+  int32_t revert3;      // 1: BFGS status 3 reverts to the global model (sindy.py:628-631); 0: keep the iterate
+  double dt, lam;
+  // active coefficients i < m: flat index, arm mask, state exponent, static-monomial code
+  int32_t t_flat[kRefineMaxCoef], t_mask[kRefineMaxCoef], t_ex[kRefineMaxCoef], t_ucode[kRefineMaxCoef];
+  // every coefficient q < n_coef: arm mask, static-monomial code | state exponent << 24
+  int32_t q_mask[kRefineMaxCoef], q_code[kRefineMaxCoef];
+  double c0[kRefineMaxCoef];
+};
+
+__device__ __forceinline__ double monomial_code(int code, const double* u) {
+  double m = 1.0;
+#pragma unroll
+  for (int i = 0; i < INSITE_MAX_STATICS; ++i) {
+    const int e = (code >> (8 * i)) & 0xff;
+    for (int k = 0; k < e; ++k) m *= u[i];
+  }
+  return m;
+}
+
+// sum_e g[e] y^e and its derivative by Horner (the oracle's _poly / _dpoly)
+template <int D>
+__device__ __forceinline__ double poly(const double (&g)[D + 1], double y) {
+  double f = g[D];
+#pragma unroll
+  for (int e = D - 1; e >= 0; --e) f = g[e] + f * y;
+  return f;
+}
+template <int D>
+__device__ __forceinline__ double dpoly(const double (&g)[D + 1], double y) {
+  double f = (double)D * g[D];
+#pragma unroll
+  for (int e = D - 1; e >= 1; --e) f = (double)e * g[e] + f * y;
+  return f;
+}
+
+template <int M, int NA, int D>
+struct RefineLane {
+  static constexpr int RU = M <= kRefineRegActive ? M : 1;
+  // sub-step loop unrolled by odeint's 5 (the default): measured 12 active 62 -> 43 ms, 6 active 5.5 -> 5.2 ms;
+  // for M = 4 (EQ_4 bench, 9.6 -> 10.1 ms) and dense models it is slower and stays rolled
+  static constexpr int SU = (M > 4 && M <= 16) ? 5 : 1;
+  const RefineArgs& ra;
+  int64_t p;
+  int K;
+  double norm;
+  double mono[M];
+  double c0a[M];
+  __device__ int armbit(int k) const {
+    if constexpr (NA == 2) return (int)((ra.arm[(int64_t)k * ra.lda + (p >> 5)] >> (p & 31)) & 1u);
+    else return (int)ra.arm8[(int64_t)k * ra.lda + p];
+  }
+  // f and gradient at c (active coordinates)
+  __device__ double fg(const double (&c)[M], double (&g)[M]) const {
+    double gam[NA][D + 1];
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int e = 0; e <= D; ++e) gam[a][e] = 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      if (i >= ra.m) break;
+      const double t = c[i] * mono[i];
+      const int mk = ra.t_mask[i], ex = ra.t_ex[i];
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+        if ((mk >> a) & 1)
+#pragma unroll
+          for (int e = 0; e <= D; ++e)
+            if (ex == e) gam[a][e] += t;
+    }
+    const double h = ra.dt / (double)ra.sub;
+    double y = ra.V[p];
+    double d[NA][D + 1], gG[NA][D + 1];
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int e = 0; e <= D; ++e) d[a][e] = gG[a][e] = 0.0;
+    double L = 0.0;
+    // step k's arm and target are requested one step ahead (issued before step k - 1's sub-steps) so the
+    // dependent Euler chain does not wait on a load per step
+    int ak_nx = armbit(0);
+    double v_nx = ra.V[ra.ldv + p];
+    for (int k = 0; k < K; ++k) {
+      const int ak = ak_nx;
+      const double vk1 = v_nx;
+      if (k + 1 < K) {
+        ak_nx = armbit(k + 1);
+        v_nx = ra.V[(int64_t)(k + 2) * ra.ldv + p];
+      }
+      double gk[D + 1];
+#pragma unroll
+      for (int e = 0; e <= D; ++e) gk[e] = gam[0][e];
+#pragma unroll
+      for (int a = 1; a < NA; ++a)
+        if (ak == a)
+#pragma unroll
+          for (int e = 0; e <= D; ++e) gk[e] = gam[a][e];
+      if constexpr (D == 1) {
+        const double hb = h * gk[1];
+#pragma unroll SU
+        for (int s = 0; s < ra.sub; ++s) {
+#pragma unroll
+          for (int a = 0; a < NA; ++a) {
+            d[a][0] = d[a][0] + hb * d[a][0];
+            d[a][1] = d[a][1] + hb * d[a][1];
+            if (ak == a) {
+              d[a][0] += h;
+              d[a][1] += h * y;
+            }
+          }
+          y = y + h * (gk[0] + gk[1] * y);
+        }
+      } else {
+        for (int s = 0; s < ra.sub; ++s) {
+          const double hf = h * dpoly<D>(gk, y);
+#pragma unroll
+          for (int a = 0; a < NA; ++a) {
+            double ye = 1.0;
+#pragma unroll
+            for (int e = 0; e <= D; ++e) {
+              d[a][e] = d[a][e] + hf * d[a][e];
+              if (ak == a) d[a][e] += h * ye;
+              ye *= y;
+            }
+          }
+          y = y + h * poly<D>(gk, y);
+        }
+      }
+      const double r = vk1 - y;
+      L += r * r;
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int e = 0; e <= D; ++e) gG[a][e] += -2.0 * r * d[a][e];
+    }
+    const double iK = 1.0 / (double)K;
+    L *= iK;
+    double pen = 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      if (i >= ra.m) {
+        g[i] = 0.0;
+        continue;
+      }
+      const double dd = c0a[i] - c[i];
+      pen += dd * dd;
+      const int mk = ra.t_mask[i], ex = ra.t_ex[i];
+      double gd = 0.0;
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+        if ((mk >> a) & 1)
+#pragma unroll
+          for (int e = 0; e <= D; ++e)
+            if (ex == e) gd += gG[a][e];
+      g[i] = gd * iK * mono[i] / norm + 2.0 * ra.lam * (c[i] - c0a[i]) / (double)ra.n_coef;
+    }
+    return L / norm + ra.lam * pen / (double)ra.n_coef;
+  }
+  __device__ double dot(const double (&a)[M], const double (&b)[M]) const {
+    double s = 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) s += a[i] * b[i];
+    return s;
+  }
+  // phi(t) = f(x + t pk), dphi = g . pk
+  __device__ double phi(const double (&x)[M], const double (&pk)[M], double t, double& dphi, double (&g)[M]) const {
+    double xt[M];
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) xt[i] = x[i] + t * pk[i];
+    const double f = fg(xt, g);
+    dphi = dot(g, pk);
+    return f;
+  }
+};
+
+__device__ __forceinline__ double cubicmin(double a, double fa, double fpa, double b, double fb, double c, double fc) {
+  const double C = fpa, db = b - a, dc = c - a;
+  const double denom = (db * dc) * (db * dc) * (db - dc);
+  const double A = (dc * dc * (fb - fa - C * db) + (-db * db) * (fc - fa - C * dc)) / denom;
+  const double B = ((-dc * dc * dc) * (fb - fa - C * db) + (db * db * db) * (fc - fa - C * dc)) / denom;
+  const double radical = B * B - 3.0 * A * C;
+  return a + (-B + sqrt(radical)) / (3.0 * A);
+}
+__device__ __forceinline__ double quadmin(double a, double fa, double fpa, double b, double fb) {
+  const double db = b - a;
+  const double B = (fb - fa - fpa * db) / (db * db);
+  return a - fpa / (2.0 * B);
+}
+
+#ifndef INSITE_REFINE_WPE4
+#define INSITE_REFINE_WPE4 4
+#endif
+#ifndef INSITE_REFINE_WPE8
+#define INSITE_REFINE_WPE8 1
+#endif
+#ifndef INSITE_REFINE_QUAD
+#define INSITE_REFINE_QUAD 0  // 1: the O(M^2) inverse-Hessian update for the unrolled kernels too
+#endif
+// M <= 4 with the affine RHS (the EQ_4 models: two terms per arm) is sized for INSITE_REFINE_WPE4 waves per
+// SIMD (<= 128 VGPRs; unconstrained the compiler takes 202 and runs 2 waves): the objective scan is a
+// dependent fp64 chain per lane, hidden only by other waves.
+template <int M, int NA, int D>
+__global__ void __launch_bounds__(kBlock)
+__attribute__((amdgpu_waves_per_eu(M <= 4 && D == 1 ? INSITE_REFINE_WPE4 : (M <= 8 ? INSITE_REFINE_WPE8 : 1))))
+insite_refine_kernel(RefineArgs ra) {
+  constexpr int RU = RefineLane<M, NA, D>::RU;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= ra.N) return;
+  // lane -> row: with rows binned by seq_len the lanes of a wave scan similar prefixes; every row's
+  // computation is independent of its lane, so outputs are bitwise the same in any order
+  const int64_t p = ra.order ? (int64_t)ra.order[gid] : gid;
+  double uu[INSITE_MAX_STATICS];
+#pragma unroll
+  for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < ra.U ? ra.u[p * ra.U + t] : 0.0;
+  RefineLane<M, NA, D> ln{ra, p, 0, 1.0, {}, {}};
+#pragma unroll RU
+  for (int i = 0; i < M; ++i) {
+    ln.mono[i] = i < ra.m ? monomial_code(ra.t_ucode[i], uu) : 0.0;
+    ln.c0a[i] = i < ra.m ? ra.c0[ra.t_flat[i]] : 0.0;
+  }
+  double x[M];
+#pragma unroll RU
+  for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
+  const int sl = ra.sl[p];
+  int status = -1, nit = 0;
+  if (sl > ra.tau && ra.T >= 2) {
+    ln.K = min(sl - ra.tau, ra.T - 1);
+    double g[M];
+    const double start = ln.fg(x, g);  // norm 1, penalty 0 at c0
+    ln.norm = start * 2.5;
+    // ---------------- BFGS (jax minimize_bfgs, norm = inf, gtol 1e-5) ----------------
+    double H[M][M];
+#pragma unroll RU
+    for (int i = 0; i < M; ++i)
+#pragma unroll RU
+      for (int j = 0; j < M; ++j) H[i][j] = i == j ? 1.0 : 0.0;
+    double f = ln.fg(x, g);
+    double gmax = 0.0, g2 = 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      gmax = fmax(gmax, fabs(g[i]));
+      g2 += g[i] * g[i];
+    }
+    bool converged = gmax < 1e-5, failed = false;
+    double old_old = f + sqrt(g2) / 2.0;
+    int ls_status = 0;
+    const int maxiter = 200 * ra.n_coef;
+    int k = 0;
+    while (!converged && !failed && k < maxiter) {
+      double pk[M];
+#pragma unroll RU
+      for (int i = 0; i < M; ++i) {
+        double s = 0.0;
+#pragma unroll RU
+        for (int j = 0; j < M; ++j) s += H[i][j] * g[j];
+        pk[i] = -s;
+      }
+      // ---- line search (jax line_search, c1 1e-4, c2 0.9, maxiter 10) ----
+      const double phi0 = f, dphi0 = ln.dot(g, pk);
+      const double cand = 1.01 * 2.0 * (phi0 - old_old) / dphi0;
+      const double start_a = cand > 1.0 ? 1.0 : cand;
+      bool ls_done = false, ls_failed = false;
+      int li = 1;
+      double a_i1 = 0.0, phi_i1 = phi0, dphi_i1 = dphi0;
+      double a_star = 0.0, phi_star = phi0;
+      double g_star[M];
+#pragma unroll RU
+      for (int i = 0; i < M; ++i) g_star[i] = g[i];
+      auto wolfe_one = [&](double a_, double ph) { return ph > phi0 + 1e-4 * a_ * dphi0; };
+      auto wolfe_two = [&](double dph) { return fabs(dph) <= -0.9 * dphi0; };
+      // zoom between (lo, hi); returns failure, fills the star point on success
+      auto zoom = [&](double a_lo, double phi_lo, double dphi_lo, double a_hi, double phi_hi, double dphi_hi,
+                      bool& z_failed) {
+        bool done = false;
+        z_failed = false;
+        int j = 0;
+        double a_rec = (a_lo + a_hi) / 2.0, phi_rec = (phi_lo + phi_hi) / 2.0;
+        double za = 1.0, zphi = phi_lo;
+        double zg[M];
+#pragma unroll RU
+        for (int i = 0; i < M; ++i) zg[i] = g[i];
+        while (!done && !z_failed) {
+          const double dalpha = a_hi - a_lo;
+          const double lo = fmin(a_hi, a_lo), hi = fmax(a_hi, a_lo);
+          const double cchk = 0.2 * dalpha, qchk = 0.1 * dalpha;
+          z_failed = z_failed || (dalpha <= 1e-10);
+          const double a_cub = cubicmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi, a_rec, phi_rec);
+          const bool use_cubic = (j > 0) && (a_cub > lo + cchk) && (a_cub < hi - cchk);
+          const double a_quad = quadmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi);
+          const bool use_quad = !use_cubic && (a_quad > lo + qchk) && (a_quad < hi - qchk);
+          double a_j = a_rec;
+          if (use_cubic) a_j = a_cub;
+          if (use_quad) a_j = a_quad;
+          if (!use_cubic && !use_quad) a_j = (a_lo + a_hi) / 2.0;
+          double dphi_j, g_j[M];
+          const double phi_j = ln.phi(x, pk, a_j, dphi_j, g_j);
+          const bool hi_to_j = wolfe_one(a_j, phi_j) || (phi_j >= phi_lo);
+          const bool star_to_j = wolfe_two(dphi_j) && !hi_to_j;
+          const bool hi_to_lo = (dphi_j * (a_hi - a_lo) >= 0.0) && !hi_to_j && !star_to_j;
+          const bool lo_to_j = !hi_to_j && !star_to_j;
+          if (hi_to_j) {
+            a_rec = a_hi;
+            phi_rec = phi_hi;
+            a_hi = a_j;
+            phi_hi = phi_j;
+            dphi_hi = dphi_j;
+          }
+          done = done || star_to_j;
+          if (star_to_j) {
+            za = a_j;
+            zphi = phi_j;
+#pragma unroll RU
+            for (int i = 0; i < M; ++i) zg[i] = g_j[i];
+          }
+          if (hi_to_lo) {
+            a_rec = a_hi;
+            phi_rec = phi_hi;
+            a_hi = a_lo;
+            phi_hi = phi_lo;
+            dphi_hi = dphi_lo;
+          }
+          if (lo_to_j) {
+            a_rec = a_lo;
+            phi_rec = phi_lo;
+            a_lo = a_j;
+            phi_lo = phi_j;
+            dphi_lo = dphi_j;
+          }
+          ++j;
+          z_failed = ((z_failed ? 1 : 0) | j) >= 30;  // jax: `failed | j >= 30` (no parentheses)
+        }
+        a_star = za;
+        phi_star = zphi;
+#pragma unroll RU
+        for (int i = 0; i < M; ++i) g_star[i] = zg[i];
+      };
+      while (!ls_done && li <= 10 && !ls_failed) {
+        const double a_i = li == 1 ? start_a : a_i1 * 2.0;
+        double dphi_i, g_i[M];
+        const double phi_i = ln.phi(x, pk, a_i, dphi_i, g_i);
+        const bool s_z1 = wolfe_one(a_i, phi_i) || ((phi_i >= phi_i1) && (li > 1));
+        const bool s_i = wolfe_two(dphi_i) && !s_z1;
+        const bool s_z2 = (dphi_i >= 0.0) && !s_z1 && !s_i;
+        if (s_z1) {
+          bool zf;
+          zoom(a_i1, phi_i1, dphi_i1, a_i, phi_i, dphi_i, zf);
+          ls_failed = ls_failed || zf;
+        }
+        if (s_i) {
+          a_star = a_i;
+          phi_star = phi_i;
+#pragma unroll RU
+          for (int i = 0; i < M; ++i) g_star[i] = g_i[i];
+        }
+        if (s_z2) {
+          bool zf;
+          zoom(a_i, phi_i, dphi_i, a_i1, phi_i1, dphi_i1, zf);
+          ls_failed = ls_failed || zf;
+        }
+        ls_done = s_z1 || ls_done || s_i || s_z2;
+        ++li;
+        a_i1 = a_i;
+        phi_i1 = phi_i;
+        dphi_i1 = dphi_i;
+      }
+      ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
+      failed = ls_failed || !ls_done;
+      // ---- BFGS update ----
+      double sk[M], yk[M];
+#pragma unroll RU
+      for (int i = 0; i < M; ++i) {
+        sk[i] = a_star * pk[i];
+        yk[i] = g_star[i] - g[i];
+      }
+      const double rho = 1.0 / ln.dot(yk, sk);
+      if (isfinite(rho) && (RU == 1 || INSITE_REFINE_QUAD)) {
+        // rolled (scratch-resident) kernels: the same update expanded to O(M^2) with one matrix-vector
+        // product, (I - rho s y^T) H (I - rho y s^T) + rho s s^T
+        //   = H - rho (s (H y)^T + (H y) s^T) + (rho^2 y^T H y + rho) s s^T   (H symmetric),
+        // instead of two O(M^3) products through two more M x M scratch matrices; the association order
+        // differs from the oracle's w @ H @ w.T (jax's three-operand einsum fixes none either)
+        double hy[M];
+        double yhy = 0.0;
+#pragma unroll RU
+        for (int i = 0; i < M; ++i) {
+          double t = 0.0;
+#pragma unroll RU
+          for (int j = 0; j < M; ++j) t += H[i][j] * yk[j];
+          hy[i] = t;
+          yhy += yk[i] * t;
+        }
+        const double cs = rho * rho * yhy + rho;
+#pragma unroll RU
+        for (int i = 0; i < M; ++i)
+#pragma unroll RU
+          for (int j = 0; j < M; ++j)
+            H[i][j] = H[i][j] - rho * (sk[i] * hy[j] + hy[i] * sk[j]) + cs * (sk[i] * sk[j]);
+      } else if (isfinite(rho)) {
+        double W[M][M], WH[M][M];
+#pragma unroll RU
+        for (int i = 0; i < M; ++i)
+#pragma unroll RU
+          for (int j = 0; j < M; ++j) W[i][j] = (i == j ? 1.0 : 0.0) - rho * (sk[i] * yk[j]);
+#pragma unroll RU
+        for (int i = 0; i < M; ++i)
+#pragma unroll RU
+          for (int j = 0; j < M; ++j) {
+            double s = 0.0;
+#pragma unroll RU
+            for (int q = 0; q < M; ++q) s += W[i][q] * H[q][j];
+            WH[i][j] = s;
+          }
+#pragma unroll RU
+        for (int i = 0; i < M; ++i)
+#pragma unroll RU
+          for (int j = 0; j < M; ++j) {
+            double s = 0.0;
+#pragma unroll RU
+            for (int q = 0; q < M; ++q) s += WH[i][q] * W[j][q];
+            H[i][j] = s + rho * (sk[i] * sk[j]);
+          }
+      }
+      double gm = 0.0;
+#pragma unroll RU
+      for (int i = 0; i < M; ++i) {
+        x[i] = x[i] + sk[i];
+        g[i] = g_star[i];
+        gm = fmax(gm, fabs(g[i]));
+      }
+      converged = gm < 1e-5;
+      old_old = f;
+      f = phi_star;
+      ++k;
+    }
+    nit = k;
+    status = converged ? 0 : (k == maxiter ? 1 : (failed ? 2 + ls_status : -1));
+    if (status == 3 && ra.revert3) {  // zoom failed: the reference code keeps the global coefficients (sindy.py:628-631)
+#pragma unroll RU
+      for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
+    }
+  }
+  // ---------------- final Euler scan with the (refined) model, every coefficient (sindy.py:668) ----------------
+  // coefficient q: the refined value if active, else the global one; resolved by comparison against the
+  // active list (no dynamically indexed per-lane array, which would live in scratch)
+  auto coef_at = [&](int q) -> double {
+    double c = ra.c0[q];
+#pragma unroll RU
+    for (int i = 0; i < M; ++i)
+      if (i < ra.m && ra.t_flat[i] == q) c = x[i];
+    return c;
+  };
+  double gam[NA][D + 1];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int e = 0; e <= D; ++e) gam[a][e] = 0.0;
+  for (int q = 0; q < ra.n_coef; ++q) {
+    const int code = ra.q_code[q], mk = ra.q_mask[q], ex = code >> 24;
+    const double t = coef_at(q) * monomial_code(code & 0xffffff, uu);
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+      if ((mk >> a) & 1)
+#pragma unroll
+        for (int e = 0; e <= D; ++e)
+          if (ex == e) gam[a][e] += t;
+  }
+  const double h = ra.dt / (double)ra.sub;
+  double y = ra.V[p];
+  for (int k = 0; k < ra.T; ++k) {
+    const int ak = ln.armbit(k);
+    double gk[D + 1];
+#pragma unroll
+    for (int e = 0; e <= D; ++e) gk[e] = gam[0][e];
+#pragma unroll
+    for (int a = 1; a < NA; ++a)
+      if (ak == a)
+#pragma unroll
+        for (int e = 0; e <= D; ++e) gk[e] = gam[a][e];
+    for (int s = 0; s < ra.sub; ++s) {
+      if constexpr (D == 1) y = y + h * (gk[0] + gk[1] * y);
+      else y = y + h * poly<D>(gk, y);
+    }
+    ra.preds[(int64_t)k * ra.ldp + p] = y;
+  }
+  if (ra.coef_out)
+    for (int q = 0; q < ra.n_coef; ++q) ra.coef_out[p * ra.n_coef + q] = coef_at(q);
+  if (ra.status) ra.status[p] = status;
+  if (ra.iters) ra.iters[p] = nit;
+}
+
+template <int NA, int D>
+void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
+  const int m = ra.m;
+  if constexpr (D == 1) {
+    if (m <= 4) insite_refine_kernel<4, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+    else if (m <= 8) insite_refine_kernel<8, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+    else if (m <= 16) insite_refine_kernel<16, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+    else if (m <= 36) insite_refine_kernel<36, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+    else insite_refine_kernel<kRefineMaxCoef, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+  } else {
+    if (m <= 8) insite_refine_kernel<8, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+    else insite_refine_kernel<kRefineMaxCoef, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+  }
+}
+
+// Shared argument checks and launch.  Coefficient q of coef0 [n_coef] acts on the arms of mask[q] with
+// state exponent exps[q][0] and static exponents exps[q][1..].
+int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, const int8_t* arm8,
+                      int64_t ld_arm, const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
+                      int32_t n_coef, const double* coef0, const int32_t* mask, const int8_t* exps, int32_t n_arms,
+                      double dt, double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail,
+                      double* preds, int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out,
+                      const int32_t* row_order, void* stream) {
+  const bool bits = arm8 == nullptr;
+  if (n_rows < 0 || T < 1 || n_arms < 1 || n_arms > (bits ? 2 : 4) || substeps < 1 || !(dt > 0.0) ||
+      !(lam >= 0.0) || tau < 0 || ld_v < n_rows || ld_p < n_rows || n_statics < 0 ||
+      n_statics > INSITE_MAX_STATICS || ld_arm < (bits ? (n_rows + 31) / 32 : n_rows) || !coef0 || !mask ||
+      !exps || n_coef < 1)
+    return INSITE_E_INVALID_ARG;
+  if (n_coef > kRefineMaxCoef) return INSITE_E_UNSUPPORTED;
+  RefineArgs ra{};
+  int D = 1, m = 0;
+  for (int q = 0; q < n_coef; ++q) {
+    const int8_t* e = exps + (int64_t)q * (1 + n_statics);
+    if (e[0] < 0) return INSITE_E_INVALID_ARG;
+    if (e[0] > 4) return INSITE_E_UNSUPPORTED;
+    int code = 0;
+    for (int i = 0; i < n_statics; ++i) {
+      if (e[1 + i] < 0 || e[1 + i] > 8) return INSITE_E_INVALID_ARG;
+      code |= (int)e[1 + i] << (8 * i);
+    }
+    if (mask[q] < 0 || mask[q] >= (1 << n_arms)) return INSITE_E_INVALID_ARG;
+    const double c = coef0[q];
+    ra.c0[q] = c;
+    ra.q_mask[q] = mask[q];
+    ra.q_code[q] = code | ((int)e[0] << 24);
+    if (c != 0.0 && e[0] > 1) D = 4;  // a non-affine term in the model: the state-polynomial kernels
+    if (fabs(c) > 1e-3) {             // coef_sparse_mask (sindy.py:587)
+      ra.t_flat[m] = q;
+      ra.t_mask[m] = mask[q];
+      ra.t_ex[m] = e[0];
+      ra.t_ucode[m] = code;
+      ++m;
+    }
+  }
+  if (n_rows == 0) return INSITE_OK;
+  if (!V || (bits && !arm_bits) || !seq_len || !preds || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
+  ra.V = V;
+  ra.arm = arm_bits;
+  ra.arm8 = arm8;
+  ra.u = n_statics > 0 ? u : V;
+  ra.sl = seq_len;
+  ra.preds = preds;
+  ra.coef_out = coef_out;
+  ra.status = status_out;
+  ra.iters = iters_out;
+  ra.order = row_order;
+  ra.ldv = ld_v;
+  ra.lda = ld_arm;
+  ra.ldp = ld_p;
+  ra.N = n_rows;
+  ra.T = T;
+  ra.tau = tau;
+  ra.sub = substeps;
+  ra.U = n_statics;
+  ra.revert3 = revert_on_zoom_fail != 0;
+  ra.A = n_arms;
+  ra.n_coef = n_coef;
+  ra.dt = dt;
+  ra.lam = lam;
+  ra.m = m;
+  const dim3 grid((unsigned)((n_rows + kBlock - 1) / kBlock));
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  if (bits) {
+    if (D == 1) launch_refine<2, 1>(ra, grid, hs);
+    else launch_refine<2, 4>(ra, grid, hs);
+  } else {
+    if (D == 1) launch_refine<4, 1>(ra, grid, hs);
+    else launch_refine<4, 4>(ra, grid, hs);
+  }
+  return launch_status();
+}
+
+// separate per-arm models [n_arms, F] over the library exps [F][1 + U]: coefficient (a, j) acts on arm a
+int32_t refine_per_arm(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, const int8_t* arm8,
+                       int64_t ld_arm, const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
+                       const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam,
+                       int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail, double* preds, int64_t ld_p,
+                       double* coef_out, int32_t* status_out, int32_t* iters_out, const int32_t* row_order,
+                       void* stream) {
+  if (!exps || n_terms < 1 || n_arms < 1 || n_arms > INSITE_MAX_ARMS || n_statics < 0 ||
+      n_statics > INSITE_MAX_STATICS)
+    return INSITE_E_INVALID_ARG;
+  const int n_coef = n_arms * n_terms;
+  if (n_coef > kRefineMaxCoef) return INSITE_E_UNSUPPORTED;
+  int32_t mask[kRefineMaxCoef];
+  int8_t qe[kRefineMaxCoef * (1 + INSITE_MAX_STATICS)];
+  for (int a = 0; a < n_arms; ++a)
+    for (int j = 0; j < n_terms; ++j) {
+      const int q = a * n_terms + j;
+      mask[q] = 1 << a;
+      std::memcpy(qe + q * (1 + n_statics), exps + j * (1 + n_statics), (size_t)(1 + n_statics));
+    }
+  return refine_launch(V, ld_v, T, arm_bits, arm8, ld_arm, u, seq_len, n_rows, n_statics, n_coef, coef0, mask, qe,
+                       n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds, ld_p, coef_out, status_out,
+                       iters_out, row_order, stream);
+}
+}  // namespace
+
+int32_t insite_refine_f64(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits, int64_t ld_arm,
+                          const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics, const int8_t* exps,
+                          int32_t n_terms, const double* coef0, int32_t n_arms, double dt, double lam, int32_t tau,
+                          int32_t substeps, int32_t revert_on_zoom_fail, double* preds, int64_t ld_p,
+                          double* coef_out, int32_t* status_out, int32_t* iters_out, const int32_t* row_order,
+                          void* stream) {
+  if (!arm_bits && n_rows > 0) return INSITE_E_INVALID_ARG;
+  return refine_per_arm(V, ld_v, T, arm_bits, nullptr, ld_arm, u, seq_len, n_rows, n_statics, exps, n_terms, coef0,
+                        n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds, ld_p, coef_out, status_out,
+                        iters_out, row_order, stream);
+}
+
+int32_t insite_refine_arms_f64(const double* V, int64_t ld_v, int32_t T, const int8_t* arm, int64_t ld_arm,
+                               const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
+                               const int8_t* exps, int32_t n_terms, const double* coef0, int32_t n_arms, double dt,
+                               double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail, double* preds,
+                               int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out,
+                               const int32_t* row_order, void* stream) {
+  if (!arm && n_rows > 0) return INSITE_E_INVALID_ARG;
+  static const int8_t kNoArms = 0;  // non-null marker for the int8 format when n_rows == 0
+  return refine_per_arm(V, ld_v, T, nullptr, arm ? arm : &kNoArms, ld_arm, u, seq_len, n_rows, n_statics, exps, n_terms, coef0,
+                        n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds, ld_p, coef_out, status_out,
+                        iters_out, row_order, stream);
+}
+
+int32_t insite_refine_general_f64(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits,
+                                  const int8_t* arm, int64_t ld_arm, const double* u, const int32_t* seq_len,
+                                  int64_t n_rows, int32_t n_statics, int32_t n_coef, const double* coef0,
+                                  const int32_t* coef_arm_mask, const int8_t* coef_exps, int32_t n_arms, double dt,
+                                  double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail,
+                                  double* preds, int64_t ld_p, double* coef_out, int32_t* status_out,
+                                  int32_t* iters_out, const int32_t* row_order, void* stream) {
+  if ((arm_bits == nullptr) == (arm == nullptr) && n_rows > 0) return INSITE_E_INVALID_ARG;
+  static const int8_t kNoArms = 0;  // non-null marker for the int8 format when n_rows == 0
+  return refine_launch(V, ld_v, T, arm_bits, arm_bits ? nullptr : (arm ? arm : &kNoArms), ld_arm, u, seq_len, n_rows, n_statics, n_coef,
+                       coef0, coef_arm_mask, coef_exps, n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds,
+                       ld_p, coef_out, status_out, iters_out, row_order, stream);
+}

@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(LIB_DIR, "libinsite_hip.so")
 if os.environ.get("INSITE_LIB_OVERRIDE"):
     LIB_PATH = os.environ["INSITE_LIB_OVERRIDE"]
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # status codes / enums (insite_hip.h)
 INSITE_OK = 0
@@ -52,6 +52,7 @@ EXPORTS = (
     "insite_rk45_order_i32",
     "insite_refine_f64",
     "insite_refine_arms_f64",
+    "insite_refine_general_f64",
     "insite_masked_sse_workspace_bytes",
     "insite_masked_sse_f64",
     "insite_gram_ms_workspace_bytes",
@@ -125,6 +126,9 @@ _SIGNATURES = {
     "insite_refine_arms_f64": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _c_i64, _vp, _vp, _c_i64, _c_i32, _vp, _c_i32,
                                         _vp, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _c_i32, _vp, _c_i64, _vp, _vp, _vp,
                                         _vp, _vp]),
+    "insite_refine_general_f64": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _vp, _c_i64, _vp, _vp, _c_i64, _c_i32, _c_i32,
+                                           _vp, _vp, _vp, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _c_i32, _vp, _c_i64,
+                                           _vp, _vp, _vp, _vp, _vp]),
     "insite_masked_sse_workspace_bytes": (_c_size, [_c_i64, _c_i32]),
     "insite_masked_sse_f64": (_c_i32, [_vp, _c_i64, _c_f64, _c_f64, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _vp,
                                        _vp, _c_size, _vp]),

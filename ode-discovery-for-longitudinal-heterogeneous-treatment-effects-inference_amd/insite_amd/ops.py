@@ -720,19 +720,45 @@ def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_ob
     return _run(("insite_rollout_rk45_f64", args, y0.device, (out, steps)))
 
 
+def refine_terms(lib: PolyLibrary, n_coef_rows: int):
+    """Per-coefficient description of a global model for ``insite_refine_general_f64``: (arm mask int32
+    [n_coef], exponents int8 [n_coef, 1 + n_statics], number of arms).  Per-arm models (lib.n_inputs = 0):
+    coefficient (a, j) acts on arm a.  The joint model (lib.n_inputs > 0, one coefficient row): the arm of
+    a step is its treatment bit code and column j acts on every code that switches its treatment inputs
+    on (binary inputs: their exponents drop out) -- the fold of ``SINDY._fold_joint``."""
+    e = lib.exps.astype(np.int64)
+    n_in, U, F = lib.n_inputs, lib.n_statics, lib.n_terms
+    keep = [0] + list(range(1 + n_in, 1 + n_in + U))
+    if n_in == 0:
+        A = n_coef_rows
+        mask = np.array([1 << a for a in range(A) for _ in range(F)], dtype=np.int32)
+        exps = np.tile(e[:, keep], (A, 1))
+    else:
+        if n_coef_rows != 1:
+            raise ValueError("the joint model has one coefficient row")
+        A = 1 << n_in
+        tin = [sum(1 << i for i in range(n_in) if e[j, 1 + i] > 0) for j in range(F)]
+        mask = np.array([sum(1 << c for c in range(A) if (tin[j] & ~c) == 0) for j in range(F)], dtype=np.int32)
+        exps = e[:, keep]
+    return np.ascontiguousarray(mask), np.ascontiguousarray(exps, dtype=np.int8), A
+
+
 def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: torch.Tensor, coef0: np.ndarray,
                   lib: PolyLibrary, dt: float, lam: float, tau: int, substeps: int = 5,
                   revert_on_zoom_fail: bool = False, binned: bool = False):
     """INSITE per-patient refinement (reference sindy.py:433-715).  V [N, T] f64 unscaled observations
     and arm [N, T] int8 per-step arms in the reference's patient-major layout (transposed to the
     kernel's time-major layout here), u [N, U], seq_len [N], coef0 the HOST global model [A, F].
-    A <= 2: insite_refine_f64 on bit-packed arms; A <= 4 (cancer_sim / EQ_5): insite_refine_arms_f64
-    on int8 arms.  ``revert_on_zoom_fail``: BFGS status 3 falls back to coef0 as sindy.py:628-631 reads;
-    the default (False) keeps the iterate, which reproduces the reference's published runs.
-    ``binned``: lanes take the rows sorted by seq_len (insite_rk45_order_i32 on the device), so a wave's
-    objective scans have similar lengths; scheduling only, the outputs are bitwise the same.  Off by
-    default: on the time-major V the binned lanes' scattered loads cost more than the shorter scans save
-    (1M rows, seq_len U{1..59}: 10.7 vs 9.5 ms, profiles/r02_v10_insite_bench.log).
+    Per-arm models: A <= 2 runs insite_refine_f64 on bit-packed arms, A <= 4 (cancer_sim / EQ_5)
+    insite_refine_arms_f64 on int8 arms; libraries with state exponents up to 4 (the degree-4 ablation)
+    run the state-polynomial kernels.  The joint model (``lib.n_inputs`` > 0, coef0 [1, F], arm = the
+    per-step treatment bit code, ``SINDY._treatment_code``): insite_refine_general_f64 with the folded
+    per-coefficient arm masks.  ``revert_on_zoom_fail``: BFGS status 3 falls back to coef0 as
+    sindy.py:628-631 reads; the default (False) keeps the iterate, which reproduces the reference's published
+    runs.  ``binned``: lanes take the rows sorted by seq_len (insite_rk45_order_i32 on the
+    device), so a wave's objective scans have similar lengths; scheduling only, the outputs are bitwise the
+    same.  Off by default: on the time-major V the binned lanes' scattered loads cost more than the shorter
+    scans save (1M rows, seq_len U{1..59}: 10.7 vs 9.5 ms, profiles/r02_v10_insite_bench.log).
     Returns (preds [N, T], coef [N, A, F], status [N], iterations [N])."""
     _dev("V", V, torch.float64, 2)
     _dev("arm", arm, torch.int8, 2)
@@ -747,28 +773,34 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
     c0 = np.ascontiguousarray(coef0, dtype=np.float64)
     if c0.ndim != 2 or c0.shape[1] != lib.n_terms:
         raise ValueError("coef0 must be a host [A, F] array")
-    A = c0.shape[0]
+    mask, qexps, A = refine_terms(lib, c0.shape[0])
     if A > 4:
-        raise ValueError("at most 4 treatment arms")
+        raise ValueError("at most 4 treatment arms (joint model: 2 binary treatment inputs)")
     Vt = V.t().contiguous()
     arm_t = arm.t().contiguous()
-    if A <= 2:
-        name, arms = "insite_refine_f64", pack_arm_bits(arm_t, N)
-    else:
-        name, arms = "insite_refine_arms_f64", arm_t
+    arms = pack_arm_bits(arm_t, N) if A <= 2 else arm_t
     dev = V.device
     preds = torch.empty((T, N), dtype=torch.float64, device=dev)
-    coef = torch.empty((N, A, lib.n_terms), dtype=torch.float64, device=dev)
+    coef = torch.empty((N,) + c0.shape, dtype=torch.float64, device=dev)
     status = torch.empty((N,), dtype=torch.int32, device=dev)
     iters = torch.empty((N,), dtype=torch.int32, device=dev)
-    tab = lib.ctypes_table()
-    args = (_p(Vt), Vt.stride(0), T, _p(arms), arms.stride(0), _p(u) if lib.n_statics else ctypes.c_void_p(0),
-            _p(seq_len), N, lib.n_statics, tab.ctypes.data_as(ctypes.c_void_p), lib.n_terms,
-            c0.ctypes.data_as(ctypes.c_void_p), A, float(dt), float(lam), int(tau), int(substeps),
-            int(bool(revert_on_zoom_fail)), _p(preds),
-            preds.stride(0), _p(coef), _p(status), _p(iters))
+    nul = ctypes.c_void_p(0)
+    ustat = _p(u) if lib.n_statics else nul
     order = rk45_order(seq_len, T) if (binned and N > 64) else None
-    _run((name, args + (_p(order) if order is not None else ctypes.c_void_p(0),), dev, None))
+    tail = (c0.ctypes.data_as(ctypes.c_void_p),)
+    common = (float(dt), float(lam), int(tau), int(substeps), int(bool(revert_on_zoom_fail)), _p(preds),
+              preds.stride(0), _p(coef), _p(status), _p(iters), _p(order) if order is not None else nul)
+    if lib.n_inputs:
+        args = (_p(Vt), Vt.stride(0), T, _p(arms) if A <= 2 else nul, _p(arms) if A > 2 else nul, arms.stride(0),
+                ustat, _p(seq_len), N, lib.n_statics, c0.size, *tail, mask.ctypes.data_as(ctypes.c_void_p),
+                qexps.ctypes.data_as(ctypes.c_void_p), A) + common
+        _run(("insite_refine_general_f64", args, dev, None))
+    else:
+        tab = lib.ctypes_table()
+        name = "insite_refine_f64" if A <= 2 else "insite_refine_arms_f64"
+        args = (_p(Vt), Vt.stride(0), T, _p(arms), arms.stride(0), ustat, _p(seq_len), N, lib.n_statics,
+                tab.ctypes.data_as(ctypes.c_void_p), lib.n_terms, *tail, A) + common
+        _run((name, args, dev, None))
     return preds.t(), coef, status, iters
 
 

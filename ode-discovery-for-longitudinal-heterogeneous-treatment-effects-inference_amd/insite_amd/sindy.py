@@ -25,9 +25,11 @@ treatment-segment discovery (``insite_sindy_fit_segments_f64``), the 4-arm rollo
 (``insite_gen_gram_f64``): ``ablation_more_complex_basis_functions`` (PolynomialLibrary(degree=4,
 interaction_only=False), sindy.py:185-186; EQ_4) and ``joint_model`` (one regression with the multilabel
 treatment(s) as library inputs, pkpd/utils.py:486-497, 639-672; sindy.py:283-288, 313-322), whose RHS
-is folded per treatment combination into the per-arm rollout.  Not on the MI355X path (raise
-``NotImplementedError``): weak SINDy, INSITE refinement of the two ablation models, and the degree-4
-library on the treatment-segment datasets.
+is folded per treatment combination into the per-arm rollout; with ``insite: true`` both refine on the
+GPU (``insite_refine_general_f64``: the joint model's coefficients act on the treatment combinations their
+inputs switch on; the degree-4 library runs the state-polynomial refinement kernels).  Not on the MI355X
+path (raise ``NotImplementedError``): weak SINDy and the degree-4 library on the treatment-segment
+datasets.
 """
 from __future__ import annotations
 
@@ -170,9 +172,6 @@ class SINDY:
                                       "the treatment-segment datasets (cancer_sim, EQ_5_*)")
         if self.wsindy:
             raise NotImplementedError("weak SINDy (wsindy: true) is not on the MI355X path")
-        if self.insite and (self.joint_model or self.ablation_more_complex_basis_functions):
-            raise NotImplementedError("INSITE refinement of the joint / degree-4 ablation models is not on the "
-                                      "MI355X path (the refinement kernel takes per-arm affine models)")
         if self.ablation_more_complex_basis_functions and self.segment_mode and not self.joint_model:
             raise NotImplementedError("the degree-4 library on the treatment-segment datasets (cancer_sim / EQ_5) "
                                       "is not on the MI355X path")
@@ -382,7 +381,10 @@ class SINDY:
             # the reference's EQ_5 refinement binds u1 to static_features[0] (sindy.py:536), unlike its
             # global-model rollout (sindy.py:302): kept, so refined EQ_5 predictions match the reference
             stat = stat[:, :1].expand(-1, stat.shape[1]).contiguous()
-        arm = torch.as_tensor(np.argmax(d["current_treatments"], axis=-1).astype(np.int8), device=self.device)
+        if self.joint_model:   # the per-step treatment bit code selects the folded combination (sindy.py:469-551)
+            arm = torch.as_tensor(self._treatment_code(d["current_treatments"]), device=self.device)
+        else:
+            arm = torch.as_tensor(np.argmax(d["current_treatments"], axis=-1).astype(np.int8), device=self.device)
         sl = torch.as_tensor(np.asarray(d["sequence_lengths"]).astype(np.int32), device=self.device)
         preds, coef, status, iters = ops.insite_refine(prev.contiguous(), arm.contiguous(), stat, sl, self.joint_coefs,
                                                        self.library, self.dt, float(self.lam), int(tau), substeps=5,

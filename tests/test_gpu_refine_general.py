@@ -1,0 +1,158 @@
+"""GPU parity of the INSITE refinement of the reference's ablation models (ABI 5,
+insite_refine_general_f64 / the state-polynomial kernels of csrc/insite_refine.hip) against the
+generalised restatement oracle/insite_refine_ref.py (per-coefficient arm masks; state-polynomial RHS):
+
+* the joint "one ODE" model (sindy.py:469-483 EQ_4, :503-517 cancer_sim): one coefficient row over a
+  library with the per-step binary treatments as inputs -- EQ_4_C (1 input, 2 combinations, bit arms) and
+  cancer_sim (chemo + radio, 4 combinations, int8 arms), global models fitted by the oracle;
+* the degree-4 library (sindy.py:185-186) with active x^2 / x^3 terms (a logistic-type system on a unit
+  scale), 2 arms (bit arms) and 4 arms (int8 arms);
+* the plugin end to end (+backbone=insite with model.joint_model=true) on an EQ_4_C multilabel collection.
+Tolerances as tests/test_gpu_insite.py: identical BFGS statuses, refined coefficients to 1e-7 relative,
+prediction RMSE <= 1e-6."""
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import cancer_sim_ref as CS
+from oracle import insite_ref as R
+from oracle import insite_refine_ref as Q
+
+pytestmark = pytest.mark.gpu
+DT = R.STANDARD_DT
+
+
+def _run(dev, V, arms, u, sl, c0, lib, tau, lam=10.0):
+    from insite_amd import ops
+    preds, coef, status, iters = ops.insite_refine(torch.tensor(V, device=dev), torch.tensor(arms, device=dev),
+                                                   torch.tensor(np.ascontiguousarray(u), device=dev),
+                                                   torch.tensor(sl, device=dev), c0, lib, DT, lam, tau)
+    torch.cuda.synchronize()
+    return preds.cpu().numpy(), coef.cpu().numpy(), status.cpu().numpy(), iters.cpu().numpy()
+
+
+def _check(dev, V, arms, u, sl, c0, lib, tau, n_inputs=0):
+    preds, coef, status, iters = _run(dev, V, arms, u, sl, c0, lib, tau)
+    ex = lib.exps.astype(np.int64)
+    agree = 0
+    for p in range(V.shape[0]):
+        rp, rc, rs, ri = Q.refine_patient(V[p], arms[p], u[p], sl[p], c0, ex, DT, 10.0, tau, n_inputs=n_inputs)
+        assert status[p] == rs, (p, status[p], rs)
+        if np.abs(coef[p] - rc).max() <= 1e-7 * max(1.0, np.abs(rc).max()):
+            agree += 1
+        assert np.sqrt(np.mean((preds[p] - rp) ** 2)) <= 1e-6, p
+    assert agree == V.shape[0]
+    assert (status[sl <= tau] == -1).all() and (iters[sl > tau] > 0).all()
+    return status
+
+
+def _rows(V, seed, tau, N):
+    rng = np.random.default_rng(seed)
+    T = V.shape[1]
+    sl = rng.integers(1, T + 1, N).astype(np.int32)
+    sl[:4] = [1, tau, tau + 1, T]
+    return sl
+
+
+@pytest.fixture(scope="module")
+def joint_eq4():
+    coll = R.make_collection("EQ_4_C", {"train": 200, "val": 4, "test": 4}, seed=2, with_tests=False,
+                             treatment_mode="multilabel")
+    tr = coll["train"]
+    x, inputs, stat, rows = R.de_format_joint(tr.data, tr.scaling_params)
+    ex = R.poly_library(1 + inputs.shape[-1] + stat.shape[1], 2, True)
+    Z, Y = R.build_regression_joint(x, inputs, stat, rows, DT)
+    c, _, _ = R.stlsq(R.eval_library(ex, Z), Y, 0.1, 0.5)
+    prev, _ = R.unscale_inputs(tr.data, tr.scaling_params)
+    return prev, inputs[..., 0].astype(np.int8), stat, c[None, :]
+
+
+@pytest.mark.parametrize("tau", [1, 5])
+def test_joint_eq4_refinement_matches_oracle(dev, joint_eq4, tau):
+    from insite_amd.library import polynomial_library
+    prev, code, stat, c0 = joint_eq4
+    lib = polynomial_library(2, 2, True, n_inputs=1)
+    assert np.array_equal(lib.exps.astype(np.int64), R.poly_library(4, 2, True))
+    N = 120
+    V = np.ascontiguousarray(prev[:N])
+    _check(dev, V, np.ascontiguousarray(code[:N]), stat[:N], _rows(V, tau, tau, N), c0, lib, tau, n_inputs=1)
+
+
+def test_joint_cancer_sim_refinement_matches_oracle(dev):
+    """4 treatment combinations (chemo | radio << 1), int8 arms, the cancer_sim joint model."""
+    from insite_amd.library import polynomial_library
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        coll = CS.make_collection(1, {"train": 400, "val": 10, "test": 10}, treatment_mode="multilabel",
+                                  with_tests=False)
+    res = CS.joint_pipeline(coll)
+    c0 = res["joint_coefs"]
+    tr = coll["train"]
+    prev, stat = R.unscale_inputs(tr.data, tr.scaling_params, 1, 1)
+    ct = tr.data["current_treatments"]
+    code = (ct[..., 0] + 2 * ct[..., 1]).astype(np.int8)
+    lib = polynomial_library(1, 2, True, n_inputs=2)
+    N, tau = 100, 5
+    V = np.ascontiguousarray(prev[:N])
+    _check(dev, V, np.ascontiguousarray(code[:N]), stat[:N], _rows(V, 9, tau, N), c0, lib, tau, n_inputs=2)
+
+
+@pytest.mark.parametrize("n_arms", [2, 4])
+def test_degree4_refinement_matches_oracle(dev, n_arms):
+    """Active x^2 and x^3 terms: the D = 4 state-polynomial kernels (per-arm models, degree-4 library)."""
+    from insite_amd.library import polynomial_library
+    rng = np.random.default_rng(n_arms)
+    U = 2 if n_arms == 2 else 1
+    lib = polynomial_library(U, 4, False)
+    ex = lib.exps.astype(np.int64)
+    N, T = 96, 40
+    col = {tuple(e): j for j, e in enumerate(ex.tolist())}
+    c0 = np.zeros((n_arms, lib.n_terms))
+    for a in range(n_arms):
+        c0[a, col[(1,) + (0,) * U]] = 0.6 + 0.1 * a             # r x
+        c0[a, col[(2,) + (0,) * U]] = -0.5 - 0.05 * a           # -k x^2
+        c0[a, col[(3,) + (0,) * U]] = 0.02 * (a + 1)             # a small cubic term (active)
+        c0[a, col[(1, 1) + (0,) * (U - 1)]] = -0.1                # x u0
+    c0[0, col[(4,) + (0,) * U]] = 5e-4                           # inactive x^4 term: final scan only
+    u = rng.uniform(0.4, 0.6, (N, U))
+    arms = rng.integers(0, n_arms, (N, 1)).repeat(T, axis=1).astype(np.int8)
+    sw = rng.integers(5, T, N)
+    for i in range(0, N, 2):
+        arms[i, sw[i]:] = rng.integers(0, n_arms)
+    V = np.empty((N, T))
+    for p in range(N):                                          # a noisy trajectory of a perturbed model
+        ct = c0 * rng.uniform(0.9, 1.1, c0.shape)
+        V[p] = np.concatenate([[rng.uniform(0.2, 0.8)], Q.euler5_rollout(rng.uniform(0.2, 0.8), arms[p], u[p], ct,
+                                                                          ex, DT, T - 1)])
+        V[p] += 1e-3 * rng.normal(size=T)
+    tau = 3
+    st = _check(dev, V, arms, u, _rows(V, 11, tau, N), c0, lib, tau)
+    assert (st >= 0).sum() > N // 2
+
+
+def test_plugin_joint_insite_end_to_end(dev):
+    """+backbone=insite model.joint_model=true dataset.treatment_mode=multilabel (run.py:198-201): refined
+    one-step and tau-step predictions against the oracle per row."""
+    from insite_amd import config as C
+    from insite_amd.sindy import SINDY
+    coll = R.make_collection("EQ_4_C", {"train": 200, "val": 4, "test": 6}, seed=3, treatment_mode="multilabel")
+    args = C.compose(["+backbone=insite", "+dataset=pkpd_sim", "dataset.equation_str=EQ_4_C",
+                      "model.dataset_name=EQ_4_C", "model.sindy_threshold=0.1", "model.sindy_alpha=0.5",
+                      "model.lam=10.0", "model.joint_model=true", "dataset.treatment_mode=multilabel"])
+    m = SINDY(args, device=dev)
+    m.fit(coll["train"], coll["val"])
+    c0 = m.joint_coefs
+    assert c0.shape == (1, m.library.n_terms) and m.library.n_inputs == 1
+    ex = m.library.exps.astype(np.int64)
+    one = coll["test_cf_one_step"]
+    p_scaled = m.get_predictions(one)[..., 0]
+    sp = one.scaling_params
+    prev, stat = R.unscale_inputs(one.data, sp)
+    code = np.asarray(one.data["current_treatments"])[..., 0].astype(np.int64)
+    sl = one.data["sequence_lengths"].astype(np.int64)
+    for p in range(0, prev.shape[0], max(1, prev.shape[0] // 60)):
+        rp, _, _, _ = Q.refine_patient(prev[p], code[p], stat[p], sl[p], c0, ex, DT, 10.0, 1, n_inputs=1)
+        got = p_scaled[p] * sp["output_stds"] + sp["output_means"]
+        assert np.sqrt(np.mean((got - rp) ** 2)) <= 1e-6, p

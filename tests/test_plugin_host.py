@@ -51,8 +51,8 @@ def test_sindy_reads_config_and_rejects_unsupported_modes():
     for flag in ("joint_model", "ablation_more_complex_basis_functions"):   # the ablations run (insite_gen.hip) ...
         m2 = SINDY(_args(**{flag: True}), device="cpu")
         assert getattr(m2, flag) is True
-        with pytest.raises(NotImplementedError):                           # ... but not their INSITE refinement
-            SINDY(_args(insite=True, **{flag: True}), device="cpu")
+        m3 = SINDY(_args(insite=True, **{flag: True}), device="cpu")          # ... and so does their INSITE refinement
+        assert m3.insite and getattr(m3, flag)
     m4 = SINDY(_args(ablation_more_complex_basis_functions=True), device="cpu")
     assert m4.library.n_terms == 35 and m4.feature_library_names[4] == "x0^2"
     ins = SINDY(_args(insite=True), device="cpu")   # the INSITE refinement (F2) is on the GPU path
@@ -212,3 +212,21 @@ def test_failed_run_keeps_its_seed():
     r = run.run_one(drv, "EQ_4_A", "sindy", 3, 2.0, extra=["+backbone=no_such_backbone"])
     assert list(r) == ["errored", "dataset_name", "seed", "method_name", "domain_conf"]
     assert r["errored"] is True and r["seed"] == 3
+
+
+def test_refine_terms_fold_matches_the_oracle():
+    """ops.refine_terms (the product's per-coefficient arm masks) equals the oracle's coef_terms for per-arm,
+    degree-4 and joint libraries."""
+    from insite_amd import ops
+    from insite_amd.library import polynomial_library
+    from oracle import insite_refine_ref as Q
+    for lib, A in ((polynomial_library(2, 2, True), 2), (polynomial_library(2, 4, False), 2),
+                   (polynomial_library(1, 2, True), 4), (polynomial_library(2, 2, True, n_inputs=1), 1),
+                   (polynomial_library(1, 2, True, n_inputs=2), 1)):
+        mask, qexps, n_arms = ops.refine_terms(lib, A)
+        c0 = np.ones((A, lib.n_terms))
+        ref = Q.coef_terms(c0, lib.exps.astype(np.int64), lib.n_inputs)
+        assert n_arms == Q.n_arms_of(c0, lib.n_inputs)
+        assert mask.tolist() == [t[0] for t in ref]
+        assert qexps[:, 0].tolist() == [t[1] for t in ref]
+        assert [tuple(r) for r in qexps[:, 1:].tolist()] == [t[2] for t in ref]
