@@ -328,6 +328,20 @@ int32_t insite_refine_arms_f64(const double* V, int64_t ld_v, int32_t T, const i
                                int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out,
                                const int32_t* row_order, void* stream);
 
+/* Treatment-segment discovery with a GENERAL library (ABI 5, insite_gen.hip): the degree-4 ablation
+ * (PolynomialLibrary(degree=4, interaction_only=False), sindy.py:185-186) on the cancer_sim / EQ_5 datasets
+ * (run.py:96-104, 208; their DE format pkpd/utils.py:433-462, 607-637).  Same segment walk, derivative
+ * (fd_kind INSITE_FD_ORDER1 / INSITE_FD_SMOOTHED1) and arrays as insite_gram_segments_f64, any library with
+ * state exponents <= 4 over [x, statics] (exps [n_terms][1 + n_statics], n_terms <= 64): per arm a
+ *   G_out[a] = sum over arm-a segment rows of Theta^T Theta,  b_out[a] = Theta^T x_dot  (overwritten),
+ * from per-patient power moments (sum x^e, e <= 8; sum x_dot x^e, e <= 4) contracted in a fixed order. */
+size_t insite_gen_gram_segments_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms);
+int32_t insite_gen_gram_segments_f64(const double* x, int64_t ldx, const int8_t* arm, int64_t ld_arm, int32_t layout,
+                                     int32_t n_steps, const int32_t* seq_len, const double* u, int32_t n_statics,
+                                     int64_t n_patients, int32_t n_arms, const int8_t* exps, int32_t n_terms,
+                                     int32_t fd_kind, double dt, double* G_out, double* b_out, void* workspace,
+                                     size_t workspace_bytes, void* stream);
+
 /* INSITE refinement of ANY global model of the reference (ABI 5, csrc/insite_refine.hip): the joint
  * "one ODE" model (sindy.py:469-483, 503-517, 537-551: one coefficient row over a library whose inputs
  * include the per-step binary treatments) and the degree-4 library (ABLATION_MORE_COMPLEX_BASIS_FUNCTIONS,

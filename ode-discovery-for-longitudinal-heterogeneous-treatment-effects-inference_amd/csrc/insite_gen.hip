@@ -177,6 +177,76 @@ gen_moments_kernel(XView xv, const double* __restrict__ d, int64_t ldd, const in
   }
 }
 
+// Treatment-segment moments (the cancer_sim / EQ_5 DE format, pkpd/utils.py:433-462, 607-637, with a general
+// library: the degree-4 ablation on those datasets, sindy.py:185-186 + run.py:96-104, 208).  Lane = patient,
+// one walk over its samples j < L = seq_len: sample j (arm a_j) is a row (x_j, d_j), d_j the forward
+// difference of its segment ((xs_{j+1} - xs_j) / dt); when sample j + 1 closes the segment (j + 1 = L or
+// a_{j+1} != a_j) it is a row of the same arm with the backward difference d_j -- the index form of the
+// reference's walk (oracle/segments_ref.segment_bounds).  SMOOTH1: savgol(2, 1) inside a segment,
+// xs_i = (x_i + x_{i+1}) / 2 except at its first and last sample (raw); the library takes the raw x.
+// Arm a's power moments go to record slot a (the contraction reads slot g for group g).
+__global__ void __launch_bounds__(kBlock)
+gen_seg_moments_kernel(XView xv, const int8_t* __restrict__ arm, int64_t asp, int64_t ask,
+                       const int32_t* __restrict__ seq_len, int n_steps, const double* __restrict__ u, int U, int64_t N,
+                       int D, int n_arms, int smooth1, double inv_dt, double* __restrict__ rec) {
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (p >= N) return;
+  int L = seq_len[p];
+  if (L > n_steps - 1) L = n_steps - 1;
+  if (L < 0) L = 0;
+  double S[kGenMaxNC][kGenNS], T[kGenMaxNC][kGenNT];
+#pragma unroll
+  for (int c = 0; c < kGenMaxNC; ++c) {
+#pragma unroll
+    for (int e = 0; e < kGenNS; ++e) S[c][e] = 0.0;
+#pragma unroll
+    for (int e = 0; e < kGenNT; ++e) T[c][e] = 0.0;
+  }
+  int aprev = -1;
+  for (int j = 0; j < L; ++j) {
+    const int aj = (int)arm[p * asp + (int64_t)j * ask];
+    const bool start = j == 0 || aj != aprev;
+    const bool end = j + 1 == L || (int)arm[p * asp + (int64_t)(j + 1) * ask] != aj;
+    aprev = aj;
+    const double xj = xv.at(p, j), xj1 = xv.at(p, j + 1);
+    double xs0 = xj, xs1 = xj1;
+    if (smooth1) {
+      if (!start) xs0 = 0.5 * (xj + xj1);
+      if (!end) xs1 = 0.5 * (xj1 + xv.at(p, j + 2));
+    }
+    const double dj = (xs1 - xs0) * inv_dt;
+    if (aj < 0 || aj >= n_arms) continue;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {  // the sample, then (segment end) the closing sample
+      if (r == 1 && !end) break;
+      const double x = r == 0 ? xj : xj1;
+      double pw[kGenNS];
+      pw[0] = 1.0;
+#pragma unroll
+      for (int e = 1; e < kGenNS; ++e) pw[e] = pw[e - 1] * x;
+#pragma unroll
+      for (int c = 0; c < kGenMaxNC; ++c) {
+        const double w = (c == aj) ? 1.0 : 0.0;  // compile-time arm slots: no dynamic indexing
+#pragma unroll
+        for (int e = 0; e < kGenNS; ++e) S[c][e] = fma(w, e <= 2 * D ? pw[e] : 0.0, S[c][e]);
+#pragma unroll
+        for (int e = 0; e < kGenNT; ++e) T[c][e] = fma(w * dj, e <= D ? pw[e] : 0.0, T[c][e]);
+      }
+    }
+  }
+  double* r = rec + p * kGenRec;
+  r[0] = L >= 1 ? 0.0 : -1.0;
+#pragma unroll
+  for (int t = 0; t < kGenMaxU; ++t) r[1 + t] = t < U ? u[p * U + t] : 0.0;
+#pragma unroll
+  for (int c = 0; c < kGenMaxNC; ++c) {
+#pragma unroll
+    for (int e = 0; e < kGenNS; ++e) r[kGenHdr + c * (kGenNS + kGenNT) + e] = S[c][e];
+#pragma unroll
+    for (int e = 0; e < kGenNT; ++e) r[kGenHdr + c * (kGenNS + kGenNT) + kGenNS + e] = T[c][e];
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // contraction + finalize
 // ---------------------------------------------------------------------------------------------
@@ -205,7 +275,7 @@ __device__ __forceinline__ void decode_entry(const GenLib& lib, int e, int& i, i
 
 __global__ void __launch_bounds__(kBlock)
 gen_contract_kernel(const double* __restrict__ rec, int64_t N, GenLib lib, int n_groups, int64_t chunk,
-                    double* __restrict__ part) {
+                    int slot_groups, double* __restrict__ part) {
   __shared__ double srec[kGenTile * kGenRec];
   __shared__ double smon[kGenTile * kGenMaxF];
   const int NE = n_groups * lib.nEg;
@@ -236,11 +306,15 @@ gen_contract_kernel(const double* __restrict__ rec, int64_t N, GenLib lib, int n
     if (ent) {
       for (int q = 0; q < nq; ++q) {
         const double* r = srec + q * kGenRec;
-        if ((int)r[0] != g) continue;
+        if (slot_groups ? (r[0] < 0.0) : ((int)r[0] != g)) continue;
         const double m = smon[q * kGenMaxF + i] * (k >= 0 ? smon[q * kGenMaxF + k] : 1.0);
         double s = 0.0;
-        for (int c = 0; c < NC; ++c)  // combinations in which every needed (binary) input is on
-          if ((need & ~c) == 0) s += r[kGenHdr + c * (kGenNS + kGenNT) + moff];
+        if (slot_groups) {  // segment records: group g's moments sit in slot g
+          s = r[kGenHdr + g * (kGenNS + kGenNT) + moff];
+        } else {
+          for (int c = 0; c < NC; ++c)  // combinations in which every needed (binary) input is on
+            if ((need & ~c) == 0) s += r[kGenHdr + c * (kGenNS + kGenNT) + moff];
+        }
         acc = fma(m, s, acc);
       }
     }
@@ -520,10 +594,56 @@ int32_t insite_gen_gram_f64(const double* x, int64_t ldx, int32_t layout, int32_
   }
   const int64_t chunk = (n_patients + kGenChunks - 1) / kGenChunks > 0 ? (n_patients + kGenChunks - 1) / kGenChunks : 1;
   gen_contract_kernel<<<dim3((unsigned)((NE + kBlock - 1) / kBlock), kGenChunks), kBlock, 0, hs>>>(
-      rec, n_patients, lib, n_groups, chunk, part);
+      rec, n_patients, lib, n_groups, chunk, 0, part);
   st = launch_status();
   if (st != INSITE_OK) return st;
   gen_finalize_kernel<<<(NE + kBlock - 1) / kBlock, kBlock, 0, hs>>>(part, kGenChunks, lib, n_groups, G_out, b_out);
+  return launch_status();
+}
+
+size_t insite_gen_gram_segments_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms) {
+  if (n_patients < 0 || n_arms < 1 || n_terms < 1) return 0;
+  const size_t NE = (size_t)n_arms * ((size_t)n_terms * (n_terms + 1) / 2 + n_terms);
+  return gen_rec_bytes(n_patients) + (size_t)kGenChunks * NE * sizeof(double);
+}
+
+int32_t insite_gen_gram_segments_f64(const double* x, int64_t ldx, const int8_t* arm, int64_t ld_arm, int32_t layout,
+                                     int32_t n_steps, const int32_t* seq_len, const double* u, int32_t n_statics,
+                                     int64_t n_patients, int32_t n_arms, const int8_t* exps, int32_t n_terms,
+                                     int32_t fd_kind, double dt, double* G_out, double* b_out, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  if (layout != INSITE_LAYOUT_PATIENT_MAJOR && layout != INSITE_LAYOUT_TIME_MAJOR) return INSITE_E_INVALID_ARG;
+  if (n_patients < 0 || n_steps < 1 || n_arms < 1 || n_arms > kGenMaxNC || !(dt > 0.0) || !G_out || !b_out)
+    return INSITE_E_INVALID_ARG;
+  if (fd_kind != INSITE_FD_ORDER1 && fd_kind != INSITE_FD_SMOOTHED1) return INSITE_E_INVALID_ARG;
+  GenLib lib;
+  int32_t st = build_gen_lib(exps, n_terms, 0, n_statics, &lib);
+  if (st != INSITE_OK) return st;
+  const bool tm = layout == INSITE_LAYOUT_TIME_MAJOR;
+  if (tm ? (ldx < n_patients || ld_arm < n_patients) : (ldx < n_steps || ld_arm < n_steps - 1))
+    return INSITE_E_INVALID_ARG;
+  if (!workspace || workspace_bytes < insite_gen_gram_segments_workspace_bytes(n_patients, n_arms, n_terms))
+    return INSITE_E_WORKSPACE;
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  const int NE = n_arms * lib.nEg;
+  double* rec = static_cast<double*>(workspace);
+  double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + gen_rec_bytes(n_patients));
+  if (n_patients > 0) {
+    if (!x || !arm || !seq_len || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
+    const XView xv{x, tm ? 1 : ldx, tm ? ldx : 1};
+    const unsigned gx = (unsigned)((n_patients + kBlock - 1) / kBlock);
+    gen_seg_moments_kernel<<<gx, kBlock, 0, hs>>>(xv, arm, tm ? 1 : ld_arm, tm ? ld_arm : 1, seq_len, n_steps,
+                                                  n_statics > 0 ? u : x, n_statics, n_patients, lib.D, n_arms,
+                                                  fd_kind == INSITE_FD_SMOOTHED1 ? 1 : 0, 1.0 / dt, rec);
+    st = launch_status();
+    if (st != INSITE_OK) return st;
+  }
+  const int64_t chunk = (n_patients + kGenChunks - 1) / kGenChunks > 0 ? (n_patients + kGenChunks - 1) / kGenChunks : 1;
+  gen_contract_kernel<<<dim3((unsigned)((NE + kBlock - 1) / kBlock), kGenChunks), kBlock, 0, hs>>>(
+      rec, n_patients, lib, n_arms, chunk, 1, part);
+  st = launch_status();
+  if (st != INSITE_OK) return st;
+  gen_finalize_kernel<<<(NE + kBlock - 1) / kBlock, kBlock, 0, hs>>>(part, kGenChunks, lib, n_arms, G_out, b_out);
   return launch_status();
 }
 

@@ -53,6 +53,8 @@ EXPORTS = (
     "insite_refine_f64",
     "insite_refine_arms_f64",
     "insite_refine_general_f64",
+    "insite_gen_gram_segments_workspace_bytes",
+    "insite_gen_gram_segments_f64",
     "insite_masked_sse_workspace_bytes",
     "insite_masked_sse_f64",
     "insite_gram_ms_workspace_bytes",
@@ -129,6 +131,9 @@ _SIGNATURES = {
     "insite_refine_general_f64": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _vp, _c_i64, _vp, _vp, _c_i64, _c_i32, _c_i32,
                                            _vp, _vp, _vp, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _c_i32, _vp, _c_i64,
                                            _vp, _vp, _vp, _vp, _vp]),
+    "insite_gen_gram_segments_workspace_bytes": (_c_size, [_c_i64, _c_i32, _c_i32]),
+    "insite_gen_gram_segments_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i32, _c_i64,
+                                              _c_i32, _vp, _c_i32, _c_i32, _c_f64, _vp, _vp, _vp, _c_size, _vp]),
     "insite_masked_sse_workspace_bytes": (_c_size, [_c_i64, _c_i32]),
     "insite_masked_sse_f64": (_c_i32, [_vp, _c_i64, _c_f64, _c_f64, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _vp,
                                        _vp, _c_size, _vp]),

@@ -332,8 +332,8 @@ def fit_per_patient_moments(mom: torch.Tensor, u: torch.Tensor, arm: torch.Tenso
 SEGMENT_FD_KINDS = {"order1": _lib.FD_ORDER1, "smoothed1": _lib.FD_SMOOTHED1}
 
 
-def _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layout, stlsq_args=None):
-    """Validate the F4 (treatment-segment) discovery inputs and pack the C arguments."""
+def _check_segments(x, arm, seq_len, u, lib, n_arms, fd, layout):
+    """Validate the F4 (treatment-segment) discovery inputs; returns (N, n_steps)."""
     if layout not in LAYOUTS:
         raise ValueError(f"layout must be one of {sorted(LAYOUTS)}")
     if fd not in SEGMENT_FD_KINDS:
@@ -358,6 +358,12 @@ def _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layo
         _dev("u", u, torch.float64, 2)
         if u.size(0) != N or u.size(1) != lib.n_statics or u.stride(0) != lib.n_statics:
             raise ValueError("u must be a contiguous [N, n_statics] tensor")
+    return N, n_steps
+
+
+def _prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layout, stlsq_args=None):
+    """Validate the F4 (treatment-segment) discovery inputs and pack the C arguments."""
+    N, n_steps = _check_segments(x, arm, seq_len, u, lib, n_arms, fd, layout)
     L = _lib.load()
     F = lib.n_terms
     dev = x.device
@@ -406,6 +412,28 @@ def sindy_fit_segments(x: torch.Tensor, arm: torch.Tensor, seq_len: torch.Tensor
     Returns (coef[A,F], mask[A,F], iters[A], G[A,F,F], b[A,F])."""
     return _run(_prep_segments(x, arm, seq_len, u, dt, lib, n_arms, fd, workspace, out, layout,
                                (threshold, alpha, max_iter, unbias)))
+
+
+def gen_gram_segments(x: torch.Tensor, arm: torch.Tensor, seq_len: torch.Tensor, u: torch.Tensor, dt: float,
+                      lib: PolyLibrary, n_arms: int = 4, fd: str = "order1", workspace: Workspace | None = None,
+                      out: tuple | None = None, layout: str = "patient"):
+    """Per-arm Gram of the treatment-segment regression with a GENERAL library (state exponents <= 4: the
+    degree-4 ablation on cancer_sim / EQ_5, sindy.py:185-186; insite_gen_gram_segments_f64).  Arrays as
+    ``gram_segments``.  Returns (G [A, F, F], b [A, F])."""
+    N, n_steps = _check_segments(x, arm, seq_len, u, lib, n_arms, fd, layout)
+    L = _lib.load()
+    F = lib.n_terms
+    dev = x.device
+    ws = _ws(workspace, dev, "scratch").get(L.insite_gen_gram_segments_workspace_bytes(N, n_arms, F), dev)
+    if out is None:
+        out = (torch.empty((n_arms, F, F), dtype=torch.float64, device=dev),
+               torch.empty((n_arms, F), dtype=torch.float64, device=dev))
+    G, b = out
+    tab = lib.ctypes_table()
+    args = (_p(x), x.stride(0), _p(arm), arm.stride(0), LAYOUTS[layout], n_steps, _p(seq_len),
+            _p(u) if lib.n_statics else ctypes.c_void_p(0), lib.n_statics, N, n_arms,
+            tab.ctypes.data_as(ctypes.c_void_p), F, SEGMENT_FD_KINDS[fd], float(dt), _p(G), _p(b), _p(ws), ws.numel())
+    return _run(("insite_gen_gram_segments_f64", args, dev, out))
 
 
 def plan_gram_segments(x, arm, seq_len, u, dt, lib, n_arms=4, fd="order1", workspace=None, out=None,

@@ -27,9 +27,9 @@ interaction_only=False), sindy.py:185-186; EQ_4) and ``joint_model`` (one regres
 treatment(s) as library inputs, pkpd/utils.py:486-497, 639-672; sindy.py:283-288, 313-322), whose RHS
 is folded per treatment combination into the per-arm rollout; with ``insite: true`` both refine on the
 GPU (``insite_refine_general_f64``: the joint model's coefficients act on the treatment combinations their
-inputs switch on; the degree-4 library runs the state-polynomial refinement kernels).  Not on the MI355X
-path (raise ``NotImplementedError``): weak SINDy and the degree-4 library on the treatment-segment
-datasets.
+inputs switch on; the degree-4 library runs the state-polynomial refinement kernels).  The degree-4 library
+on the treatment-segment datasets runs ``insite_gen_gram_segments_f64`` (per-arm power moments of the
+segment rows).  Not on the MI355X path (raises ``NotImplementedError``): weak SINDy.
 """
 from __future__ import annotations
 
@@ -172,9 +172,6 @@ class SINDY:
                                       "the treatment-segment datasets (cancer_sim, EQ_5_*)")
         if self.wsindy:
             raise NotImplementedError("weak SINDy (wsindy: true) is not on the MI355X path")
-        if self.ablation_more_complex_basis_functions and self.segment_mode and not self.joint_model:
-            raise NotImplementedError("the degree-4 library on the treatment-segment datasets (cancer_sim / EQ_5) "
-                                      "is not on the MI355X path")
         if self.integrator not in ops.METHODS:
             raise ValueError(f"integrator must be one of {sorted(ops.METHODS)}")
 
@@ -231,6 +228,10 @@ class SINDY:
         the reduction launch (insite_sindy_fit_segments_f64)."""
         x, u, arm, sl = self.de_format_segments(train_f)
         fd = "smoothed1" if self.use_smoothed_finite_difference else "order1"
+        if self.library.state_degree > 1:   # the degree-4 ablation library: per-arm power moments (insite_gen.hip)
+            G, b = ops.gen_gram_segments(x, arm, sl, u, self.dt, self.library, n_arms=self.dim_treatments, fd=fd)
+            coef, mask, iters = ops.stlsq(G, b, self.sindy_threshold, self.sindy_alpha, 100, True)
+            return coef, mask, iters, G, b
         return ops.sindy_fit_segments(x, arm, sl, u, self.dt, self.library, self.sindy_threshold, self.sindy_alpha,
                                       max_iter=100, unbias=True, n_arms=self.dim_treatments, fd=fd)
 

@@ -145,10 +145,10 @@ def build_rows(X_list, U_list, dt, fd="order1"):
 
 
 def sindy_fit_segments(x, u, arm_steps, seq_len, dt, threshold=1e-3, alpha=0.5, max_iter=100, fd="order1",
-                       n_arms=4):
+                       n_arms=4, degree=2, interaction_only=True):
     """Row-form restatement (what the four pysindy fits compute): returns coef[A, F], ind[A, F],
     iters[A], exps.  An arm without segments raises (pysindy cannot fit an empty list)."""
-    exps = R.poly_library(1 + u.shape[1], 2, True)
+    exps = R.poly_library(1 + u.shape[1], degree, interaction_only)    # degree 4: sindy.py:185-186
     X, Ul = de_segments(x, u, arm_steps, seq_len, n_arms)
     F = exps.shape[0]
     coef = np.zeros((n_arms, F))

@@ -1,0 +1,79 @@
+"""The degree-4 library on the treatment-segment datasets (ABLATION_MORE_COMPLEX_BASIS_FUNCTIONS over
+cancer_sim / EQ_5: PolynomialLibrary(degree=4, interaction_only=False), sindy.py:185-186; run.py:96-104,
+208) through insite_gen_gram_segments_f64 (per-arm power moments of the segment rows, insite_gen.hip)
+against oracle/segments_ref.py (explicit Theta over the literal segment walk), on the reference's own
+cancer_sim cohort (oracle/cancer_sim_ref.py, seed 1): per-arm Gram/moments to rtol 1e-9 (x reaches 1150,
+so G spans x^8 ~ 1e24), both layouts and both derivative methods; the plugin end to end (fit -> 4-arm
+polynomial rollout) against the oracle rollout of the fitted model."""
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import cancer_sim_ref as CS
+from oracle import insite_ref as R
+from oracle import segments_ref as S
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cohort():
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        coll = CS.make_collection(1, {"train": 400, "val": 20, "test": 10}, with_tests=False)
+    tr = coll["train"]
+    return coll, CS.de_format_segments(tr.data, tr.scaling_params)
+
+
+@pytest.mark.parametrize("layout", ["patient", "time"])
+@pytest.mark.parametrize("fd", ["order1", "smoothed1"])
+def test_gen_gram_segments_matches_oracle(dev, cohort, layout, fd):
+    from insite_amd import ops
+    from insite_amd.library import polynomial_library
+    _, (x, u, arm, sl) = cohort
+    lib = polynomial_library(1, 4, False)
+    G_ref, b_ref, _ = S.gram_segments(x, u, arm, sl, R.STANDARD_DT, lib.exps.astype(np.int64), fd=fd)
+    if layout == "patient":
+        xd, ad = torch.tensor(x, device=dev), torch.tensor(arm.astype(np.int8), device=dev)
+    else:
+        xd = torch.tensor(np.ascontiguousarray(x.T), device=dev)
+        ad = torch.tensor(np.ascontiguousarray(arm.T.astype(np.int8)), device=dev)
+    G, b = ops.gen_gram_segments(xd, ad, torch.tensor(sl.astype(np.int32), device=dev),
+                                 torch.tensor(np.ascontiguousarray(u), device=dev), R.STANDARD_DT, lib, fd=fd,
+                                 layout=layout)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(G.cpu().numpy(), G_ref, rtol=1e-9, atol=0)
+    np.testing.assert_allclose(b.cpu().numpy(), b_ref, rtol=1e-9, atol=1e-9 * np.abs(b_ref).max())
+
+
+def test_plugin_degree4_segments_end_to_end(dev, cohort):
+    from insite_amd import config as C
+    from insite_amd.sindy import SINDY
+    coll, (x, u, arm, sl) = cohort
+    a = C.compose(["+backbone=sindy", "+dataset=pkpd_sim", "model.sindy_threshold=0.001", "model.sindy_alpha=0.5",
+                   "model.lam=10.0", "model.ablation_more_complex_basis_functions=true"])
+    a["model"].update({"dataset_name": "cancer_sim", "dim_treatments": 4, "dim_static_features": 1, "dim_outcomes": 1})
+    m = SINDY(a, device=dev)
+    m.fit(coll["train"], coll["val"])
+    assert m.library.n_terms == 15 and m.joint_coefs.shape == (4, 15)
+    assert m.global_equation_string.count("Treatment ") == 4
+    # discovery: the GPU's STLSQ on the GPU Gram equals the oracle's Gram-form STLSQ on the oracle Gram
+    ex = m.library.exps.astype(np.int64)
+    G_ref, b_ref, _ = S.gram_segments(x, u, arm, sl, R.STANDARD_DT, ex)
+    for k in range(4):
+        c_ref, ind_ref, _ = R.stlsq_gram(G_ref[k], b_ref[k], 1e-3, 0.5)
+        assert np.array_equal(m.joint_coefs[k] != 0, ind_ref), k
+        assert np.max(np.abs(m.joint_coefs[k] - c_ref)) <= 1e-6 * max(1.0, np.abs(c_ref).max()), k
+    # rollout: the 4-arm polynomial RHS of the fitted model, Euler-5, against the oracle's literal RHS
+    val = coll["val"]
+    p = m.get_predictions(val)[..., 0]
+    prev, st = R.unscale_inputs(val.data, val.scaling_params, 1, 1)
+    y_ref = R.rollout(prev[:, 0], st, np.argmax(val.data["current_treatments"], axis=-1), m.joint_coefs, ex,
+                      R.STANDARD_DT, "euler5")
+    sp = val.scaling_params
+    got = p * sp["output_stds"] + sp["output_means"]
+    fin = np.isfinite(y_ref)
+    assert np.array_equal(np.isfinite(got), fin)
+    np.testing.assert_allclose(got[fin], y_ref[fin], rtol=1e-9, atol=1e-9)

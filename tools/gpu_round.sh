@@ -2,8 +2,9 @@
 # One GPU call: selected parity tests, then bench lines.  Every GPU step has its own time limit and the first
 # failure (test failure, crash, timeout) ends the call.
 #   OUT=r03_x TESTS="tests/test_gpu_foo.py" BENCH="--config c5;--config c4 --T 60" bash tools/gpu_round.sh
-# TESTS="all" runs the whole -m gpu suite; empty skips tests.  BENCH is a ';'-separated list of bench.py
-# argument strings ("default" = the driver's default line).
+# TESTS="all" runs the whole -m gpu suite; empty skips tests; KSEL is an optional pytest -k expression.
+# POST is an optional command run (under its own time limit) after the tests.  BENCH is a ';'-separated list
+# of bench.py argument strings ("default" = the driver's default line).
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/${OUT:-round}
@@ -11,8 +12,12 @@ mkdir -p "$O"
 if [ -n "$TESTS" ]; then
   sel="$TESTS"; [ "$TESTS" = "all" ] && sel="tests"
   timeout -k 10 ${TEST_LIMIT:-600} python -u -m pytest $sel -m gpu -x -v --timeout 300 --timeout-method thread \
-    -p no:cacheprovider > "$O/tests.log" 2>&1 || { grep -E "PASSED|FAILED|ERROR" "$O/tests.log" | tail -15; tail -40 "$O/tests.log"; exit 1; }
+    -p no:cacheprovider ${KSEL:+-k "$KSEL"} > "$O/tests.log" 2>&1 || { grep -E "PASSED|FAILED|ERROR" "$O/tests.log" | tail -15; tail -40 "$O/tests.log"; exit 1; }
   grep -cE "PASSED" "$O/tests.log"; tail -2 "$O/tests.log"
+fi
+if [ -n "$POST" ]; then
+  timeout -k 10 ${POST_LIMIT:-600} bash -c "$POST" > "$O/post.log" 2>&1 || { echo "post failed"; tail -30 "$O/post.log"; exit 1; }
+  tail -${POST_TAIL:-10} "$O/post.log"
 fi
 i=0
 IFS=';' read -ra LINES <<< "$BENCH"
