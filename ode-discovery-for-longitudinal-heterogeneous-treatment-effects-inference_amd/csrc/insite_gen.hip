@@ -432,7 +432,33 @@ gen_stlsq_wave_kernel(const double* __restrict__ G, const double* __restrict__ B
     prev = pattern;
   }
   const u64 sup = __ballot(lane < F && fabs(c[lane]) > 1e-14);
-  if (sp.unbias && sup) ok &= gen_wave_chol_solve(Gs, bs, F, sup, 0.0, M, v, c, lane);
+  if (sp.unbias && sup) {
+    // minimum-norm unbias over exactly duplicated columns (lstsq's solution; see stlsq_solve in insite_hip.hip):
+    // lane k finds the first earlier active column equal to its own, one representative per group is solved
+    // and its coefficient split equally
+    int rep = lane;
+    if (lane < F && ((sup >> lane) & 1ull)) {
+      const double gkk = Gs[(int64_t)lane * F + lane], bk = bs[lane];
+      for (int i = 0; i < lane; ++i)
+        if (((sup >> i) & 1ull) && Gs[(int64_t)i * F + i] == gkk && Gs[(int64_t)lane * F + i] == gkk && bs[i] == bk) {
+          rep = i;
+          break;
+        }
+    }
+    const u64 solve = sup & ~__ballot(rep != lane);
+    ok &= gen_wave_chol_solve(Gs, bs, F, solve, 0.0, M, v, c, lane);
+    wave_lds_sync();
+    if (solve != sup) {
+      // a representative is its own first equal column, so rep chains have length one
+      int cnt = 0;
+      for (int k = 0; k < F; ++k) cnt += __shfl(rep, k) == lane && ((sup >> k) & 1ull) ? 1 : 0;
+      const double ci = lane < F ? c[lane] : 0.0;
+      wave_lds_sync();
+      if (lane < F && cnt > 1) c[lane] = ci / (double)cnt;
+      wave_lds_sync();
+      if (lane < F && rep != lane) c[lane] = c[rep];
+    }
+  }
   wave_lds_sync();
   if (lane < F) {
     coef[(int64_t)s * F + lane] = c[lane];

@@ -942,7 +942,40 @@ __device__ int stlsq_solve(const double (&g)[F][F], const double (&rhs)[F], doub
 #pragma unroll
   for (int i = 0; i < F; ++i)
     if (fabs(c[i]) > 1e-14) sup |= 1u << i;
-  if (unbias && sup) ok &= masked_cholesky_solve<F>(g, rhs, sup, 0.0, c);
+  if (unbias && sup) {
+    // pysindy's unbias is an unregularised lstsq on the support, i.e. its MINIMUM-NORM solution when the
+    // support holds exactly duplicated columns (a static that is the same for every patient, e.g. EQ_5_A/B's
+    // single patient type u0 == 1: columns {1, u0} and {x0, x0 u0} coincide, G singular).  Column k equals
+    // an earlier active column i iff ||theta_i - theta_k||^2 = G_ii + G_kk - 2 G_ik = 0 with b_i = b_k:
+    // solve on one representative per group, then split its coefficient equally (the minimum-norm split).
+    int rep[F];
+    unsigned solve = sup;
+#pragma unroll
+    for (int k = 0; k < F; ++k) {
+      rep[k] = k;
+#pragma unroll
+      for (int i = 0; i < k; ++i)
+        if (rep[k] == k && rep[i] == i && ((sup >> i) & 1u) && ((sup >> k) & 1u) && g[i][i] == g[k][k] &&
+            g[k][i] == g[i][i] && rhs[i] == rhs[k])
+          rep[k] = i;
+      if (rep[k] != k) solve &= ~(1u << k);
+    }
+    ok &= masked_cholesky_solve<F>(g, rhs, solve, 0.0, c);
+    if (solve != sup) {
+#pragma unroll
+      for (int i = 0; i < F; ++i) {
+        int cnt = 0;
+#pragma unroll
+        for (int k = 0; k < F; ++k) cnt += (((sup >> k) & 1u) && rep[k] == i) ? 1 : 0;
+        if (cnt > 1) c[i] /= (double)cnt;
+      }
+#pragma unroll
+      for (int k = 0; k < F; ++k)
+#pragma unroll
+        for (int i = 0; i < k; ++i)
+          if (rep[k] == i) c[k] = c[i];
+    }
+  }
   return ok ? it : -1;
 }
 

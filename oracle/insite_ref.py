@@ -657,9 +657,24 @@ def stlsq_gram(G, b, threshold, alpha, max_iter=100, unbias=True):
         prev_pattern = pattern
     ind = np.abs(coef) > SUPPORT_EPS
     if unbias and ind.any():
-        S = np.nonzero(ind)[0]
+        # the unbias is lstsq's minimum-norm solution: exactly duplicated support columns (||theta_i -
+        # theta_k||^2 = G_ii + G_kk - 2 G_ik = 0, b_i = b_k; e.g. a static equal to 1 for every patient,
+        # EQ_5_A/B) are solved once and their coefficient split equally (the GPU solvers do the same)
+        S = list(np.nonzero(ind)[0])
+        rep = {}
+        for k in S:
+            for i in S:
+                if i >= k:
+                    break
+                if rep.get(i, i) == i and G[i, i] == G[k, k] and G[k, i] == G[i, i] and b[i] == b[k]:
+                    rep[k] = i
+                    break
+        R_ = [k for k in S if rep.get(k, k) == k]
         out = np.zeros(F)
-        out[S] = np.linalg.solve(G[np.ix_(S, S)], b[S])
+        out[R_] = np.linalg.solve(G[np.ix_(R_, R_)], b[R_])
+        for i in R_:
+            grp = [k for k in S if rep.get(k, k) == i]
+            out[grp] = out[i] / len(grp)
         coef = out
     return coef, ind, it
 

@@ -2,7 +2,8 @@
 # One GPU call: selected parity tests, then bench lines.  Every GPU step has its own time limit and the first
 # failure (test failure, crash, timeout) ends the call.
 #   OUT=r03_x TESTS="tests/test_gpu_foo.py" BENCH="--config c5;--config c4 --T 60" bash tools/gpu_round.sh
-# TESTS="all" runs the whole -m gpu suite; empty skips tests; KSEL is an optional pytest -k expression.
+# TESTS="all" runs the whole -m gpu suite; empty skips tests; KSEL is an optional pytest -k expression;
+# XFLAG="" runs past the first failure (default -x); CONT=1 goes on to POST / BENCH after test failures.
 # POST is an optional command run (under its own time limit) after the tests.  BENCH is a ';'-separated list
 # of bench.py argument strings ("default" = the driver's default line).
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -11,9 +12,12 @@ O=gpurun_out/${OUT:-round}
 mkdir -p "$O"
 if [ -n "$TESTS" ]; then
   sel="$TESTS"; [ "$TESTS" = "all" ] && sel="tests"
-  timeout -k 10 ${TEST_LIMIT:-600} python -u -m pytest $sel -m gpu -x -v --timeout 300 --timeout-method thread \
-    -p no:cacheprovider ${KSEL:+-k "$KSEL"} > "$O/tests.log" 2>&1 || { grep -E "PASSED|FAILED|ERROR" "$O/tests.log" | tail -15; tail -40 "$O/tests.log"; exit 1; }
-  grep -cE "PASSED" "$O/tests.log"; tail -2 "$O/tests.log"
+  timeout -k 10 ${TEST_LIMIT:-600} python -u -m pytest $sel -m gpu ${XFLAG--x} -v --timeout 300 --timeout-method thread \
+    -p no:cacheprovider ${KSEL:+-k "$KSEL"} > "$O/tests.log" 2>&1
+  rc=$?
+  grep -cE "PASSED" "$O/tests.log"; grep -E "^(FAILED|ERROR)" "$O/tests.log" | head -20; tail -2 "$O/tests.log"
+  # CONT=1: test failures (rc 1) do not stop the call; crashes, timeouts and collection errors do
+  if [ $rc -ne 0 ] && ! { [ "$CONT" = 1 ] && [ $rc -eq 1 ]; }; then tail -40 "$O/tests.log"; exit 1; fi
 fi
 if [ -n "$POST" ]; then
   timeout -k 10 ${POST_LIMIT:-600} bash -c "$POST" > "$O/post.log" 2>&1 || { echo "post failed"; tail -30 "$O/post.log"; exit 1; }
