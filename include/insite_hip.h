@@ -470,6 +470,15 @@ int32_t insite_rollout_ms_sparse_f32(const float* y0, int64_t ld_y0, const uint3
                                      int32_t n_states, int64_t n_rows, int32_t T, double dt, int32_t method,
                                      int32_t substeps, double drop_below, float* y_out, int64_t ld_y, void* stream);
 
+/* Counter-based random words of the on-device PK/PD cohort generator (csrc/insite_rng.hip; SURVEY.md §8
+ * F3).  Replaces the words under every jax.random draw the reference makes for a cohort
+ * (libs_m/ct/src/data/pkpd/dataset.py:52-54 PRNGKey(seed) per subset; pkpd_simulation.py:117-197,
+ * 233-236, 290-291 split / normal / uniform / permutation): out[0 .. n_words) = jax.prng.threefry_2x32
+ * ((key0, key1), iota(n_words)) -- Threefry-2x32-20 over the pairs (j, j + ceil(n/2)), the odd count
+ * padded with one zero, output halves concatenated.  The uniform / normal / permutation transforms run
+ * on these words in insite_amd/threefry.py.  out: device uint32 [n_words], 0 <= n_words < 2^32 - 1. */
+int32_t insite_threefry2x32_iota_u32(uint32_t key0, uint32_t key1, int64_t n_words, uint32_t* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

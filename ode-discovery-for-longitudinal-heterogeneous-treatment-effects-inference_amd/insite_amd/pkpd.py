@@ -10,9 +10,22 @@ Cohorts are generated with torch on the requested device (the MI355X by default)
 the model in the reference's layout: ``dataset.data`` is a dict of numpy arrays
 (``prev_outputs [N,T-1,1]``, ``current_treatments [N,T-1,2]`` one-hot, ``static_features [N,2]``,
 ``outputs``/``unscaled_outputs``/``active_entries [N,T-1,1]``, ``sequence_lengths [N]``, ...),
-``dataset.scaling_params`` and ``dataset.norm_const = 50``.  The reference draws with JAX
-threefry keys, which are not reproducible without jax; this module uses torch's generator with the
-same distributions ("Deviations").
+``dataset.scaling_params`` and ``dataset.norm_const = 50``.
+
+Random draws (``rng=``):
+
+* ``"threefry"`` (default): the reference's own key schedule and draws -- ``PRNGKey(seed)`` per
+  subset, ``key, subkey = split(key)`` before every draw, jax's uniform / normal / permutation /
+  choice transforms -- with the Threefry-2x32 words produced on the device by
+  ``insite_threefry2x32_iota_u32`` (insite_amd/threefry.py).  The reference's cohorts are
+  reproduced (tests/test_gpu_threefry.py), so ``run.py`` reproduces its logged rows.  Needs the
+  HIP library and a GPU device.
+* ``"torch"``: torch's generator with the same distributions and time grids, seeded per
+  (seed, subset); host-side tests on CPU tensors.
+
+The time grids are the reference's: ``arange(0, 10, dt)`` for the factual and one-step
+simulators, ``arange(T + 1) * dt`` with accumulated ``+ dt`` windows for the tau-step one, each
+interval integrated by 5 Euler sub-steps of ``(t1 - t0) / 5`` (utils.py:68-94).
 """
 from __future__ import annotations
 
@@ -32,8 +45,9 @@ def _noisy(equation: str) -> bool:
     return equation.split("_")[-1] in ("B", "C", "D")
 
 
-class _Rng:
-    """Device generator for one subset (seeded from (seed, subset))."""
+class _TorchRng:
+    """torch's generator on ``device``, one per (seed, subset); same interface as ``_ThreefryRng``
+    (the key-schedule hooks are no-ops)."""
 
     def __init__(self, seed: int, subset: str, device):
         self.dev = torch.device(device)
@@ -43,11 +57,78 @@ class _Rng:
     def normal(self, *shape):
         return torch.randn(shape, generator=self.g, device=self.dev, dtype=torch.float64)
 
-    def uniform(self, *shape):
-        return torch.rand(shape, generator=self.g, device=self.dev, dtype=torch.float64)
+    def uniform(self, *shape, lo: float = 0.0, hi: float = 1.0):
+        u = torch.rand(shape, generator=self.g, device=self.dev, dtype=torch.float64)
+        return u if (lo, hi) == (0.0, 1.0) else u * (hi - lo) + lo
+
+    def permutation(self, n: int):
+        return torch.randperm(int(n), generator=self.g, device=self.dev)
+
+    def choice2(self, n: int, values):
+        return torch.where(self.uniform(n) < 0.5, values[0], values[1])
+
+    def skip(self):
+        pass
+
+    def split_first(self, num: int):
+        pass
 
 
-def draw_params(n: int, equation: str, rng: _Rng) -> dict:
+class _ThreefryRng:
+    """The reference's jax.random key threading for one key (``key, subkey = split(key)`` before
+    every draw), words from the device Threefry kernel (insite_amd/threefry.py)."""
+
+    def __init__(self, key, device):
+        from . import threefry
+        self._tf = threefry
+        self.s = threefry.Stream(key, device)
+        self.dev = self.s.dev
+
+    def normal(self, *shape):
+        return self.s.normal(*shape)
+
+    def uniform(self, *shape, lo: float = 0.0, hi: float = 1.0):
+        return self.s.uniform(*shape, lo=lo, hi=hi)
+
+    def permutation(self, n: int):
+        return self.s.permutation(n)
+
+    def choice2(self, n: int, values):
+        """``jax.random.choice(key, [v0, v1], (n,))`` = ``a[randint(key, (n,), 0, 2)]``; randint over a
+        span of 2 with 64-bit draws (multiplier 2^32 mod 2 = 0) keeps ``lower_bits mod 2`` of the second
+        split subkey's bits (jax 0.4.x random.py ``_randint``).  Parity unpinned: no logged EQ_4_M run."""
+        sub = self.s._sub()
+        _, k2 = self._tf.split(sub, 2, self.dev)
+        lower = self._tf.random_bits(k2, 64, (int(n),), self.dev)
+        return torch.where((lower & 1) == 0, values[0], values[1])
+
+    def skip(self):
+        """A ``key, subkey = split(key)`` whose draw the simulator never reads (recovery rvs)."""
+        self.s._sub()
+
+    def split_first(self, num: int):
+        self.s.split_first(num)
+
+
+def subset_rngs(kind: str, seed: int, subset: str, device):
+    """(params rng, simulator rng) for one subset.  threefry: ``key = PRNGKey(seed)``, then
+    ``key, k_params = split(key)``; ``key, k_sim = split(key)`` (pkpd/dataset.py:52-54, 64-71) -- every
+    subset restarts from the same seed, as the reference does (dataset.py:594-603)."""
+    if kind == "threefry":
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise RuntimeError("rng='threefry' draws on the device (HIP kernel); pass a cuda device "
+                               "(rng='torch' is the host-side generator)")
+        from . import threefry
+        kp, ks = threefry.subset_streams(seed, dev)
+        return _ThreefryRng(kp.key, dev), _ThreefryRng(ks.key, dev)
+    if kind == "torch":
+        r = _TorchRng(seed, subset, device)
+        return r, r
+    raise ValueError(f"rng {kind!r}: 'threefry' or 'torch'")
+
+
+def draw_params(n: int, equation: str, rng) -> dict:
     """Patient parameters (get_standard_params, pkpd_simulation.py:96-203)."""
     if equation not in EQUATIONS:
         raise NotImplementedError(f"equation {equation!r} (PK/PD EQ_4 family only)")
@@ -59,25 +140,28 @@ def draw_params(n: int, equation: str, rng: _Rng) -> dict:
         C_0 = c_0 + 0.1 * scale
         C_1 = c_1 + 0.3 * scale
         if equation == "EQ_4_D":                                      # :152-158, one shift per arm
-            C_0 = C_0 + rng.normal(1) * (0.5 * scale)
-            C_1 = C_1 + rng.normal(1) * (0.5 * scale)
+            C_0 = rng.normal() * (0.5 * scale) + C_0
+            C_1 = rng.normal() * (0.5 * scale) + C_1
     elif equation == "EQ_4_M":                                        # :159-165 bimodal
-        C_0 = c_0 + torch.where(rng.uniform(n) < 0.5, 0.1 * scale, 0.3 * scale)
-        C_1 = c_1 + torch.where(rng.uniform(n) < 0.5, 0.1 * scale, 0.3 * scale)
-    x0 = rng.uniform(n) * (MAX_VALUE - 1.0) + 1.0                     # :182
-    perm = torch.randperm(n, generator=rng.g, device=rng.dev)         # :196-201
+        C_0 = c_0 + rng.choice2(n, (0.1 * scale, 0.3 * scale))
+        C_1 = c_1 + rng.choice2(n, (0.1 * scale, 0.3 * scale))
+    x0 = rng.uniform(n, lo=1.0, hi=MAX_VALUE)                         # :181-182
+    perm = rng.permutation(n)                                         # :195-201
     return {"initial_volumes": x0[perm], "hidden_C_0": C_0[perm], "hidden_C_1": C_1[perm],
             "observed_static_c_0": c_0[perm], "observed_static_c_1": c_1[perm]}
 
 
 def _assign(x0, rv, conf_coeff):
-    """Bernoulli(sigmoid(gamma/50 (x0 - 25))) (pkpd_simulation.py:76-94, 255-259)."""
-    return (rv < torch.sigmoid((conf_coeff / MAX_VALUE) * (x0 - MAX_VALUE / 2.0))).to(torch.int64)
+    """``rv < 1 / (1 + exp(-gamma (x0 - 25)))``, gamma = coeff / 50 (pkpd_simulation.py:76-94, 255-259)."""
+    gamma = conf_coeff / MAX_VALUE
+    prob = 1.0 / (1.0 + torch.exp(-gamma * (x0 - MAX_VALUE / 2.0)))
+    return (rv < prob).to(torch.int64)
 
 
-def _decay(v, C, dt):
-    """One observation interval of dy/dt = -C y with the reference Euler-5 (utils.py:68-79)."""
-    h = dt / STEPS_FOR_DT
+def _interval(v, C, t0: float, t1: float):
+    """``odeint(dy_dt, v, [t0, t1])[1]`` of dy/dt = -C y: HMAX < t1 - t0, so 5 Euler sub-steps of
+    (t1 - t0) / 5 (utils.py:68-94; pkpd_simulation.py:69-73)."""
+    h = (t1 - t0) / STEPS_FOR_DT
     for _ in range(STEPS_FOR_DT):
         v = v + (-C * v) * h
     return v
@@ -90,18 +174,18 @@ def _first_true(mask):
     return anyv, first
 
 
-def simulate_factual(p: dict, T: int, rng: _Rng, equation: str, conf_coeff: float) -> dict:
+def simulate_factual(p: dict, T: int, rng, equation: str, conf_coeff: float) -> dict:
     """Factual cohort (pkpd_simulation.py:205-309)."""
-    dt = MAX_TIME_HORIZON / T
+    t_grid = np.arange(0, MAX_TIME_HORIZON, MAX_TIME_HORIZON / T)     # :261
     x0 = p["initial_volumes"]
     n = x0.numel()
-    rec_rv = rng.uniform(n, T)                                        # :250
-    a = _assign(x0, rng.uniform(n), conf_coeff)                       # :252-259
+    rec_rv = rng.uniform(n, T)                                        # :233-234
+    a = _assign(x0, rng.uniform(n), conf_coeff)                       # :235-236, 255-259
     C = torch.where(a == 0, p["hidden_C_0"], p["hidden_C_1"])
     V = torch.empty((n, T), dtype=torch.float64, device=x0.device)
     V[:, 0] = x0
     for k in range(1, T):                                             # :262
-        V[:, k] = _decay(V[:, k - 1], C, dt)
+        V[:, k] = _interval(V[:, k - 1], C, float(t_grid[k - 1]), float(t_grid[k]))
     seq = torch.full((n,), T - 1, dtype=torch.int64, device=x0.device)  # :254
     t = torch.arange(T, device=x0.device)[None, :]
     rec_any, rec_first = _first_true(rec_rv < torch.exp(-V * RECOVERY_MULTIPLIER))   # :264-265
@@ -118,22 +202,23 @@ def simulate_factual(p: dict, T: int, rng: _Rng, equation: str, conf_coeff: floa
             "observed_static_c_0": p["observed_static_c_0"], "observed_static_c_1": p["observed_static_c_1"]}
 
 
-def simulate_counterfactual_1_step(p: dict, T: int, rng: _Rng, equation: str, conf_coeff: float) -> dict:
+def simulate_counterfactual_1_step(p: dict, T: int, rng, equation: str, conf_coeff: float) -> dict:
     """Every one-step-ahead counterfactual (pkpd_simulation.py:341-471): per patient and step i,
     a factual row and a row whose treatment flips at step i; 2(T-1) rows per patient."""
-    dt = MAX_TIME_HORIZON / T
+    t_grid = np.arange(0, MAX_TIME_HORIZON, MAX_TIME_HORIZON / T)     # :394-395
     x0 = p["initial_volumes"]
     n, dev = x0.numel(), x0.device
-    rng.uniform(n, T - 1)                                             # recovery rvs (:375), unused
-    a = _assign(x0, rng.uniform(n), conf_coeff)                       # :377
+    rng.skip()                                                        # recovery rvs (:380-381), unused
+    a = _assign(x0, rng.uniform(n), conf_coeff)                       # :382-383
     C = torch.where(a == 0, p["hidden_C_0"], p["hidden_C_1"])
     Ccf = torch.where(a == 0, p["hidden_C_1"], p["hidden_C_0"])
     V = torch.empty((n, T), dtype=torch.float64, device=dev)
     V[:, 0] = x0
     cf = torch.empty((n, T - 1), dtype=torch.float64, device=dev)
     for k in range(T - 1):                                            # :344-350
-        cf[:, k] = _decay(V[:, k], Ccf, dt)
-        V[:, k + 1] = _decay(V[:, k], C, dt)
+        t0, t1 = float(t_grid[k]), float(t_grid[k + 1])
+        cf[:, k] = _interval(V[:, k], Ccf, t0, t1)
+        V[:, k + 1] = _interval(V[:, k], C, t0, t1)
     i = torch.arange(T - 1, device=dev)[:, None]                      # row pair index
     t = torch.arange(T, device=dev)[None, :]
     fact = torch.where(t < i + 2, V[:, None, :], 0.0)                 # [n, T-1, T]
@@ -145,7 +230,7 @@ def simulate_counterfactual_1_step(p: dict, T: int, rng: _Rng, equation: str, co
     trt_c = torch.where(tt < i, af, 0.0) + torch.where(tt == i, 1.0 - af, 0.0)
     trt = torch.stack([trt_f, trt_c], dim=2).reshape(n, 2 * (T - 1), T - 1)
     sl = (torch.arange(T - 1, device=dev) + 1).repeat_interleave(2)[None, :].expand(n, -1)
-    if _noisy(equation):                                              # :438-440
+    if _noisy(equation):                                              # :438-444
         vol = vol + OBSERVATION_NOISE * rng.normal(*vol.shape)
     rows = n * 2 * (T - 1)
     treat = torch.zeros((rows, T), dtype=torch.float64, device=dev)
@@ -157,31 +242,34 @@ def simulate_counterfactual_1_step(p: dict, T: int, rng: _Rng, equation: str, co
             "observed_static_c_1": p["observed_static_c_1"].repeat_interleave(reps)}
 
 
-def simulate_counterfactuals_treatment_seq(p: dict, T: int, tau: int, rng: _Rng, equation: str,
+def simulate_counterfactuals_treatment_seq(p: dict, T: int, tau: int, rng, equation: str,
                                            conf_coeff: float) -> dict:
     """tau-step sliding-treatment counterfactuals (pkpd_simulation.py:474-487, 516-667): per
     patient and step i, 2*tau treatment plans (one-hot and inverted one-hot over tau steps)."""
     dt = MAX_TIME_HORIZON / T
+    t_grid = np.arange(0, T + 1).astype(np.float64) * dt              # :537
     x0 = p["initial_volumes"]
     n, dev = x0.numel(), x0.device
-    rng.uniform(n, T + tau - 1)                                       # recovery rvs (:571), unused
-    a = _assign(x0, rng.uniform(n), conf_coeff)                       # :573
+    rng.skip()                                                        # recovery rvs (:555-556), unused
+    a = _assign(x0, rng.uniform(n), conf_coeff)                       # :557-558
     C0, C1 = p["hidden_C_0"], p["hidden_C_1"]
     C = torch.where(a == 0, C0, C1)
     eye = torch.eye(tau, dtype=torch.int64, device=dev)
-    plans = torch.cat([eye, 1 - eye], dim=0)                          # [2tau, tau] (:489)
+    plans = torch.cat([eye, 1 - eye], dim=0)                          # [2tau, tau] (:476-489)
     V = torch.empty((n, T + 1), dtype=torch.float64, device=dev)
     V[:, 0] = x0
-    V[:, 1] = _decay(x0, C, dt)                                       # :593
+    V[:, 1] = _interval(x0, C, float(t_grid[0]), float(t_grid[1]))   # :574
     P = 2 * tau
     cfv = torch.empty((n, T - 1, P, tau), dtype=torch.float64, device=dev)
     Cp = torch.where(plans[None] == 0, C0[:, None, None], C1[:, None, None])   # [n, P, tau]
-    for i in range(T - 1):                                            # :600
+    for i in range(T - 1):                                            # t_tuples (t[i+1], t[i+2]) :571-600
+        ts, te = float(t_grid[i + 1]), float(t_grid[i + 2])
         v = V[:, i + 1][:, None].expand(n, P)
-        for j in range(tau):
-            v = _decay(v, Cp[:, :, j], dt)
+        for j in range(tau):                                          # windows advance by += dt (:478-486)
+            v = _interval(v, Cp[:, :, j], ts, te)
+            ts, te = ts + dt, te + dt
             cfv[:, i, :, j] = v
-        V[:, i + 2] = _decay(V[:, i + 1], C, dt)
+        V[:, i + 2] = _interval(V[:, i + 1], C, float(t_grid[i + 1]), float(t_grid[i + 2]))   # :513
     L = T + tau
     i = torch.arange(T - 1, device=dev)[:, None, None]                # [T-1, 1, 1]
     t = torch.arange(L, device=dev)[None, None, :]                    # [1, 1, L]
@@ -201,7 +289,8 @@ def simulate_counterfactuals_treatment_seq(p: dict, T: int, tau: int, rng: _Rng,
     trt = torch.where(tt < i + 1, af, 0.0) + torch.where(inw_t, plan_v, 0.0)[None]
     nr = (T - 1) * P
     sl = (torch.arange(T - 1, device=dev) + 1 + tau).repeat_interleave(P)[None, :].expand(n, -1)
-    if _noisy(equation):                                              # :644-646
+    rng.split_first(n + 1)                                            # :616 key, *subkeys = split(key, n + 1)
+    if _noisy(equation):                                              # :639-646
         vol = vol + OBSERVATION_NOISE * rng.normal(*vol.shape)
     rows = n * nr
     treat = torch.zeros((rows, L), dtype=torch.float64, device=dev)
@@ -302,7 +391,8 @@ class SyntheticPkpdDatasetCollection:
     and builds the tau-step targets (dataset_collection.py:74-86)."""
 
     def __init__(self, conf_coeff: float, num_patients: dict, equation_str: str, seed: int,
-                 max_seq_length: int = 60, projection_horizon: int = 5, device=None, **kwargs):
+                 max_seq_length: int = 60, projection_horizon: int = 5, device=None, rng: str = "threefry",
+                 **kwargs):
         dev = torch.device(device) if device is not None else (
             torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
         T = int(max_seq_length)
@@ -312,16 +402,17 @@ class SyntheticPkpdDatasetCollection:
         self.autoregressive = True
         self.has_vitals = False
         self.processed_data_multi = False
+        self.rng = rng
         subsets = {}
         for name, n in (("train", num_patients["train"]), ("val", num_patients["val"])):
-            rng = _Rng(seed, name, dev)
-            subsets[name] = simulate_factual(draw_params(int(n), equation_str, rng), T, rng, equation_str, conf_coeff)
-        rng = _Rng(seed, "test_cf_one_step", dev)
-        one = simulate_counterfactual_1_step(draw_params(int(num_patients["test"]), equation_str, rng), T, rng,
+            rp, rs = subset_rngs(rng, seed, name, dev)
+            subsets[name] = simulate_factual(draw_params(int(n), equation_str, rp), T, rs, equation_str, conf_coeff)
+        rp, rs = subset_rngs(rng, seed, "test_cf_one_step", dev)
+        one = simulate_counterfactual_1_step(draw_params(int(num_patients["test"]), equation_str, rp), T, rs,
                                              equation_str, conf_coeff)
-        rng = _Rng(seed, "test_cf_treatment_seq", dev)
-        seqs = simulate_counterfactuals_treatment_seq(draw_params(int(num_patients["test"]), equation_str, rng), T,
-                                                      self.projection_horizon, rng, equation_str, conf_coeff)
+        rp, rs = subset_rngs(rng, seed, "test_cf_treatment_seq", dev)
+        seqs = simulate_counterfactuals_treatment_seq(draw_params(int(num_patients["test"]), equation_str, rp), T,
+                                                      self.projection_horizon, rs, equation_str, conf_coeff)
         self.train_f = SyntheticPkpdDataset("train", subsets["train"])
         self.val_f = SyntheticPkpdDataset("val", subsets["val"])
         self.test_cf_one_step = SyntheticPkpdDataset("test", one)
@@ -339,10 +430,10 @@ class SyntheticPkpdDatasetCollection:
 
 
 def dataset_collection(equation: str, num_patients: dict, seed: int, conf_coeff: float = 2.0,
-                       max_seq_length: int = 60, projection_horizon: int = 5, device=None):
+                       max_seq_length: int = 60, projection_horizon: int = 5, device=None, rng: str = "threefry"):
     """Build and process a collection in one call (``get_dataset`` + ``process_data_multi``)."""
     c = SyntheticPkpdDatasetCollection(conf_coeff, num_patients, equation, seed, max_seq_length, projection_horizon,
-                                       device=device)
+                                       device=device, rng=rng)
     c.process_data_multi()
     return c
 

@@ -46,7 +46,7 @@ def train_sindy_main(args: dict, dataset_name: str = "", device=None) -> dict:
                                                equation_str=ds["equation_str"], seed=int(ds["seed"]),
                                                max_seq_length=int(ds.get("max_seq_length", 60)),
                                                projection_horizon=int(ds.get("projection_horizon", 5)),
-                                               device=device)
+                                               device=device, rng=str(ds.get("rng", "threefry")))
     coll.process_data_multi()
     tr = coll.train_f.data
     C.set_path(args, "model.dim_outcomes", tr["outputs"].shape[-1])

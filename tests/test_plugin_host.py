@@ -114,7 +114,7 @@ def test_tau_slice_matches_oracle():
 
 def test_pkpd_collection_layout_matches_reference_format():
     from insite_amd import pkpd
-    c = pkpd.dataset_collection("EQ_4_C", {"train": 40, "val": 5, "test": 4}, seed=0, device="cpu")
+    c = pkpd.dataset_collection("EQ_4_C", {"train": 40, "val": 5, "test": 4}, seed=0, device="cpu", rng="torch")
     o = R.make_collection("EQ_4_C", {"train": 40, "val": 5, "test": 4}, seq_length=60, seed=0)
     for mine, ref in ((c.train_f, o["train"]), (c.val_f, o["val"]), (c.test_cf_one_step, o["test_cf_one_step"]),
                       (c.test_cf_treatment_seq, o["test_cf_treatment_seq"])):
@@ -136,7 +136,7 @@ def test_pkpd_counterfactual_structure():
     from insite_amd import pkpd
     T, tau = 12, 3
     c = pkpd.SyntheticPkpdDatasetCollection(2.0, {"train": 6, "val": 2, "test": 3}, "EQ_4_A", seed=4,
-                                            max_seq_length=T, projection_horizon=tau, device="cpu")
+                                            max_seq_length=T, projection_horizon=tau, device="cpu", rng="torch")
     one = {k: v.numpy() for k, v in c.test_cf_one_step.sim.items()}
     V, trt, sl = one["cancer_volume"], one["treatment_application"], one["sequence_lengths"]
     for p in range(3):
@@ -159,7 +159,7 @@ def test_pkpd_counterfactual_structure():
 def test_pkpd_noise_free_trajectory_is_euler5_decay():
     from insite_amd import pkpd
     c = pkpd.SyntheticPkpdDatasetCollection(2.0, {"train": 20, "val": 2, "test": 2}, "EQ_4_A", seed=5,
-                                            max_seq_length=30, device="cpu")
+                                            max_seq_length=30, device="cpu", rng="torch")
     s = {k: v.numpy() for k, v in c.train_f.sim.items()}
     V, a = s["cancer_volume"], s["treatment_application"][:, 0]
     dt = 10.0 / 30
@@ -171,11 +171,21 @@ def test_pkpd_noise_free_trajectory_is_euler5_decay():
 
 def test_pkpd_is_deterministic_per_seed():
     from insite_amd import pkpd
-    a = pkpd.dataset_collection("EQ_4_D", {"train": 10, "val": 2, "test": 2}, seed=9, device="cpu")
-    b = pkpd.dataset_collection("EQ_4_D", {"train": 10, "val": 2, "test": 2}, seed=9, device="cpu")
+    a = pkpd.dataset_collection("EQ_4_D", {"train": 10, "val": 2, "test": 2}, seed=9, device="cpu", rng="torch")
+    b = pkpd.dataset_collection("EQ_4_D", {"train": 10, "val": 2, "test": 2}, seed=9, device="cpu", rng="torch")
     np.testing.assert_array_equal(a.train_f.data["outputs"], b.train_f.data["outputs"])
-    c = pkpd.dataset_collection("EQ_4_D", {"train": 10, "val": 2, "test": 2}, seed=10, device="cpu")
+    c = pkpd.dataset_collection("EQ_4_D", {"train": 10, "val": 2, "test": 2}, seed=10, device="cpu", rng="torch")
     assert not np.array_equal(a.train_f.data["outputs"], c.train_f.data["outputs"])
+
+
+def test_pkpd_threefry_needs_the_device():
+    """rng='threefry' (the default, the reference's draws) runs on the HIP kernel: a CPU device is refused
+    loudly rather than served by a host generator."""
+    from insite_amd import pkpd
+    with pytest.raises(RuntimeError, match="threefry"):
+        pkpd.dataset_collection("EQ_4_A", {"train": 4, "val": 2, "test": 2}, seed=1, device="cpu")
+    with pytest.raises(ValueError):
+        pkpd.subset_rngs("pcg", 1, "train", "cpu")
 
 
 def test_savgol_rows_matches_scipy():
@@ -230,3 +240,35 @@ def test_refine_terms_fold_matches_the_oracle():
         assert mask.tolist() == [t[0] for t in ref]
         assert qexps[:, 0].tolist() == [t[1] for t in ref]
         assert [tuple(r) for r in qexps[:, 1:].tolist()] == [t[2] for t in ref]
+
+
+@pytest.mark.parametrize("eq", ["EQ_4_B", "EQ_4_D"])
+def test_pkpd_threefry_key_schedule_host_logic(monkeypatch, eq):
+    """The host side of rng='threefry' (key threading, transforms, time grids, simulators) on CPU tensors,
+    with the device word kernel stood in by the numpy restatement of jax's threefry_2x32 (test-only; the
+    kernel itself is pinned in tests/test_gpu_threefry.py): the reference's cohorts come out."""
+    from insite_amd import pkpd, threefry
+    from oracle import jax_prng as J
+    from oracle import ref_cohort as RC
+
+    def words(key, n, device):
+        w = J.threefry_2x32(np.array(key, np.uint32), np.arange(n, dtype=np.uint32)).astype(np.int64)
+        return torch.from_numpy(w)
+
+    monkeypatch.setattr(threefry, "_words", words)
+
+    def rngs(kind, seed, subset, device):
+        kp, ks = threefry.subset_streams(seed, "cpu")
+        return pkpd._ThreefryRng(kp.key, "cpu"), pkpd._ThreefryRng(ks.key, "cpu")
+
+    monkeypatch.setattr(pkpd, "subset_rngs", rngs)
+    n = {"train": 30, "val": 5, "test": 4}
+    c = pkpd.dataset_collection(eq, n, seed=1, max_seq_length=20, projection_horizon=3, device="cpu")
+    ref = RC.make_collection(eq, n, seq_length=20, projection_horizon=3, seed=1)
+    for mine, name in ((c.train_f, "train"), (c.val_f, "val"), (c.test_cf_one_step, "test_cf_one_step"),
+                       (c.test_cf_treatment_seq, "test_cf_treatment_seq")):
+        r = ref[name].data
+        for k in ("sequence_lengths", "current_treatments", "active_entries"):
+            assert np.array_equal(mine.data[k], r[k]), (name, k)
+        for k in ("prev_outputs", "outputs", "static_features", "unscaled_outputs"):
+            np.testing.assert_allclose(mine.data[k], r[k], rtol=0, atol=1e-11, err_msg=f"{name}/{k}")
