@@ -69,6 +69,13 @@ def parse():
                          "library's default split)")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="C2 at N = 1: join a single-rank RCCL process group and run the N > 1 pipeline's data path "
+                         "(gram, one bucketed all_reduce per batch, STLSQ) so the collective and the process "
+                         "group's stream synchronisation sit in the timed region")
+    ap.add_argument("--no-rotate", action="store_true",
+                    help="C2 fused: one cohort re-read every step (default: two cohorts alternate, so no step "
+                         "re-reads data the 256 MB Infinity Cache still holds)")
     ap.add_argument("--isolated", action="store_true",
                     help="also time each C2 kernel in isolation (back-to-back launches on one stream)")
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "insite", "f4"],
@@ -433,7 +440,8 @@ def c5_main(args):
     lib = polynomial_library(2, 2, True)
     coef = torch.zeros((2, lib.n_terms), dtype=torch.float64, device=dev)
     coef[0, 4], coef[1, 1], coef[1, 5] = C5_COEF
-    y = torch.empty((N, Tm), dtype=torch.float64, device=dev)
+    # rows padded to whole 64-B sectors (ld 64): the kernel stages each lane's outputs per sector
+    y = torch.empty((N, (Tm + 7) // 8 * 8), dtype=torch.float64, device=dev)[:, :Tm]
     steps = torch.empty((N,), dtype=torch.int32, device=dev)
 
     order = not args.rk45_identity_order
@@ -899,16 +907,22 @@ def launch_ranks(args):
         sys.exit(2)
 
 
-def dist_setup():
-    """(world, rank, device) of this process; joins the process group when world > 1.  Rehearsal knobs
-    for a one-GPU box (never set by the driver): INSITE_REHEARSE_ONE_GPU puts every rank on cuda:0 and
-    INSITE_DIST_BACKEND=gloo swaps RCCL for gloo."""
+def dist_setup(force_group: bool = False):
+    """(world, rank, device) of this process; joins the process group when world > 1 (or, with
+    ``force_group``, as a single-rank RCCL group: --force-collective).  Rehearsal knobs for a one-GPU box
+    (never set by the driver): INSITE_REHEARSE_ONE_GPU puts every rank on cuda:0 and INSITE_DIST_BACKEND=gloo
+    swaps RCCL for gloo."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if os.environ.get("INSITE_REHEARSE_ONE_GPU") else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or force_group:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         backend = os.environ.get("INSITE_DIST_BACKEND", "nccl")
         dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
     return world, rank, dev
@@ -928,27 +942,38 @@ def step_traffic(args):
     return None
 
 
-def fused_run(args, dev, coh, arm_cf):
+def fused_run(args, dev, coh, arm_cf, coh2=None, arm_cf2=None):
     """Time the fused step (insite_fit_rollout_f64: step_kernel) on the C2 cohort.  One launch per step runs
     the discovery of step i (gram + in-launch reduction + the F = 7 STLSQ in its last block) and, on the
     other blocks of the same resident round, the rollout of step i-1 with the coefficients discovery i-1
-    wrote (two coefficient buffers, ping-pong).  K timed launches = K discoveries + K rollouts."""
+    wrote (two coefficient buffers, ping-pong).  K timed launches = K discoveries + K rollouts.
+    With a second cohort (coh2, the default: --no-rotate turns it off) the steps alternate between the two:
+    step i discovers cohort i % 2 and rolls cohort (i - 1) % 2 out into that cohort's own y, so consecutive
+    reads of one cohort's x are 480 MB of other traffic apart -- more than the 256 MB Infinity Cache, whose
+    hits the PMC byte counters count (MI355X_MICROARCH.md) -- and no step re-reads resident data."""
     from insite_amd import ops
     N, T = args.patients, args.T
     lib = coh.lib
     F = lib.n_terms
     f64 = torch.float64
+    cohs = [coh, coh2 if coh2 is not None else coh]
+    arms = [arm_cf, arm_cf2 if coh2 is not None else arm_cf]
     coefs = [torch.zeros((2, F), dtype=f64, device=dev) for _ in range(2)]
     masks = [torch.zeros((2, F), dtype=torch.int8, device=dev) for _ in range(2)]
     iters = [torch.zeros((2,), dtype=torch.int32, device=dev) for _ in range(2)]
     Gs = [torch.zeros((2, F, F), dtype=f64, device=dev) for _ in range(2)]
     bs = [torch.zeros((2, F), dtype=f64, device=dev) for _ in range(2)]
-    y = torch.empty((T, N), dtype=f64, device=dev)
-    # step -1: a plain discovery gives the first rollout its model
-    ops.sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, out=(coefs[1], masks[1], iters[1], Gs[1],
-                                                                              bs[1]), layout="time")
-    plans = [ops.plan_fit_rollout(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, coh.y0, coh.u, arm_cf,
-                                  coefs[1 - j], coh.dt, method=args.method, T=T, y_out=y,
+    y1 = torch.empty((T, N), dtype=f64, device=dev)
+    ys = [y1, torch.empty((T, N), dtype=f64, device=dev) if coh2 is not None else y1]
+    y = ys[0]
+    # step -1: a plain discovery of the cohort step 0 rolls out gives the first rollout its model
+    c1 = cohs[1]
+    ops.sindy_fit(c1.x, c1.u, c1.arm, c1.rows, c1.dt, lib, 0.1, 0.5, out=(coefs[1], masks[1], iters[1], Gs[1],
+                                                                          bs[1]), layout="time")
+    # plan j: discovery of cohort j into coefs[j] | rollout of cohort 1 - j with coefs[1 - j] into its y
+    plans = [ops.plan_fit_rollout(cohs[j].x, cohs[j].u, cohs[j].arm, cohs[j].rows, cohs[j].dt, lib, 0.1, 0.5,
+                                  cohs[1 - j].y0, cohs[1 - j].u, arms[1 - j], coefs[1 - j], cohs[1 - j].dt,
+                                  method=args.method, T=T, y_out=ys[1 - j],
                                   out=(coefs[j], masks[j], iters[j], Gs[j], bs[j]), gram_blocks=args.gram_blocks)
              for j in range(2)]
     st = torch.cuda.current_stream(dev)
@@ -991,17 +1016,22 @@ def fused_run(args, dev, coh, arm_cf):
     step_ms = float(np.mean([hip.elapsed_ms(e0, e1) for e0, e1 in tevs])) / KB
     rb, gb = rollout_bytes(N, T, arm_bits=1), gram_bytes(N, T)
     return {"ms_step": ms_step, "host_ms": host_ms, "step_ms": step_ms, "KB": KB, "NBAT": NBAT,
-            "coef": coefs[last], "mask": masks[last], "y": y, "rb": rb, "gb": gb,
+            "coef": coefs[last], "mask": masks[last], "y": ys[last], "rb": rb, "gb": gb, "rotated": coh2 is not None,
             "frac": (rb + gb) / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
 
 
 def c2_fused(args, dev, coh, arm_cf, cpu):
-    """C2 at N = 1 with one step_kernel launch per step (--mode fused); see fused_run."""
-    from insite_amd import ops
+    """C2 at N = 1 with one step_kernel launch per step (--mode fused); see fused_run.  Two cohorts rotate
+    (a second seed) unless --no-rotate."""
+    from insite_amd import ops, cohort
     N, T = args.patients, args.T
     lib = coh.lib
     F = lib.n_terms
-    fr = fused_run(args, dev, coh, arm_cf)
+    coh2 = arm_cf2 = None
+    if not args.no_rotate:
+        coh2 = cohort.synthetic_pkpd(N, T, seed=args.seed * 1000 + 500, device=dev, equation="EQ_4_C", layout="time")
+        arm_cf2 = cohort.counterfactual_arms(coh2.arm, T, seed=args.seed * 1000 + 500, layout="time_bits")
+    fr = fused_run(args, dev, coh, arm_cf, coh2, arm_cf2)
     ms_step, host_ms, step_ms, KB, NBAT = fr["ms_step"], fr["host_ms"], fr["step_ms"], fr["KB"], fr["NBAT"]
     y = fr["y"]
     st = torch.cuda.current_stream(dev)
@@ -1044,6 +1074,7 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
             "patients_per_gpu": N, "T": T, "rows_per_patient": T - 2, "library_terms": F,
             "parallelism": "patient-shard x1", "mode": "fused", "gram_blocks": args.gram_blocks or "default",
             "discovered_support": sup.tolist(), "finite": ok,
+            "cohorts_rotated": 2 if fr["rotated"] else 1,
         },
         "host_submit_ms_per_step": host_ms,
         "roofline": {
@@ -1132,7 +1163,10 @@ def main():
     cpu = None
     if os.environ.get("WORLD_SIZE", "1") == "1" and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_sample, args.T, args.method, args.seed)
-    world, rank, dev = dist_setup()
+    world, rank, dev = dist_setup(force_group=args.force_collective)
+    if args.force_collective:
+        args.mode = "pipeline"
+    collective = world > 1 or args.force_collective   # the pipeline's data path all-reduces G|b
 
     from insite_amd import ops, cohort
     from insite_amd import dist as idist
@@ -1216,13 +1250,13 @@ def main():
     g_fast = [p.bind(s_g) for p in gram_plans]
     c_fast = [p.bind(s_g) for p in stlsq_plans]
     r_fast = [p.bind(s_rs[(j // K) % RS]) for j, p in enumerate(roll_plans)]
-    stl_roll = world == 1 and mode == "pipeline" and args.stlsq_stream == "rollout"
+    stl_roll = not collective and mode == "pipeline" and args.stlsq_stream == "rollout"
     c_roll = [p.bind(s_rs[(j // K) % RS]) for j, p in enumerate(stlsq_plans)] if stl_roll else None
 
     def discover(i, st):
         """Discovery of step i on stream st (used by seq / graph and the roofline pass)."""
         j = i % NB
-        if world == 1:
+        if not collective:
             fused[j](st)
         else:
             gram_plans[j](st)
@@ -1259,7 +1293,7 @@ def main():
             hip.record(tev[0], hs_g)
         if stl_roll:
             g_fast[j]()                             # gram + in-launch reduction (STLSQ: rollout stream)
-        elif world == 1:
+        elif not collective:
             f_fast[j]()                             # gram + in-launch reduction, STLSQ
         else:
             g_fast[j]()                             # gram; the batch's all-reduce + STLSQs in flush()
@@ -1272,9 +1306,9 @@ def main():
         if not pending:
             return
         b = pending[0] // K
-        if world > 1:                               # the batch's K systems: one collective, then K STLSQs
+        if collective:                              # the batch's K systems: one collective, then K STLSQs
             with torch.cuda.stream(s_g):
-                idist.reduce_bucket(buckets[(pending[0] % NB) // K])   # the only data-path collective
+                idist.reduce_bucket(buckets[(pending[0] % NB) // K], force=args.force_collective)  # the only collective
             for k in pending:
                 c_fast[k % NB]()
         if tev:
@@ -1400,7 +1434,9 @@ def main():
                 "workload": f"C2: PK/PD {N // 1000}k patients/GPU x {T} steps fp64 - discovery (savgol+FD4+poly2 "
                             f"library+Gram, RCCL all-reduce when N>1, STLSQ) + {args.method.upper()} counterfactual rollout",
                 "patients_per_gpu": N, "T": T, "rows_per_patient": T - 2, "library_terms": F,
-                "parallelism": f"patient-shard x{world}", "mode": mode, "stlsq_stream": "rollout" if stl_roll else "discovery",
+                "parallelism": f"patient-shard x{world}" + (" (single-rank RCCL group: --force-collective)"
+                                                             if args.force_collective and world == 1 else ""),
+                "mode": mode, "stlsq_stream": "rollout" if stl_roll else "discovery",
                 "discovered_support": sup.tolist(), "finite": ok,
             },
             "host_submit_ms_per_step": host_ms,
@@ -1444,6 +1480,27 @@ def main():
                                "achieved_GBps": (rb + gram_bytes(N, T)) / (ms_step * 1e-3) / 1e9,
                                "frac": (rb + gram_bytes(N, T)) / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS},
         }
+        if collective:
+            # the bucketed all-reduce alone: back-to-back collectives on the discovery stream, HIP events around
+            # the batch (per-collective device time incl. the process group's stream handshakes)
+            fb = buckets[0].flat
+            nc = 200
+            with torch.cuda.stream(s_g):
+                for _ in range(10):
+                    idist.reduce_bucket(buckets[0], force=args.force_collective)
+                torch.cuda.synchronize(dev)
+                e0, e1 = hip.create(timing=True), hip.create(timing=True)
+                t1 = time.perf_counter()
+                hip.record(e0, hs_g)
+                for _ in range(nc):
+                    idist.reduce_bucket(buckets[0], force=args.force_collective)
+                hip.record(e1, hs_g)
+                torch.cuda.synchronize(dev)
+                host_us = (time.perf_counter() - t1) / nc * 1e6
+            out["collective"] = {"op": "all_reduce(SUM) of one batch bucket (RCCL)", "bytes": fb.numel() * 8,
+                                 "systems_per_collective": K, "ranks": world,
+                                 "avg_device_us": hip.elapsed_ms(e0, e1) / nc * 1e3, "avg_host_us": host_us,
+                                 "per_step_us": hip.elapsed_ms(e0, e1) / nc * 1e3 / K}
         if iso is not None:
             out["isolated"] = dict(iso, rollout_frac=rb / (iso["rollout_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                                    gram_frac=gram_bytes(N, T) / (iso["gram_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS)
@@ -1476,7 +1533,7 @@ def main():
         out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out))
-    if world > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

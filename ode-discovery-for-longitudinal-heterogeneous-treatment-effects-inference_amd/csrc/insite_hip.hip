@@ -192,6 +192,9 @@ __device__ __forceinline__ void tele_lo(const GramW& w, double vm2, double vm1, 
 // of each counter resets it (all its arrivals are in), so a call leaves them zero; the workspace header
 // must be zero before its first use (insite_gram_workspace_bytes).  The launcher's alternative, a memset
 // node per call (-DINSITE_GRAM_MEMSET), puts a ~20 us gap in the stream on ROCm 7.2 (profiles/).
+#ifndef INSITE_TAIL_RELEASE_FENCE
+#define INSITE_TAIL_RELEASE_FENCE 0
+#endif
 constexpr int kTailGroup = 16;
 constexpr int kTailMaxEnt = INSITE_MAX_ARMS * (INSITE_MAX_TERMS * (INSITE_MAX_TERMS + 1) / 2 + INSITE_MAX_TERMS);
 struct GramOut {
@@ -230,9 +233,18 @@ __device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
     if (threadIdx.x == 0) {
-      // release at agent scope before the ticket (the HIP memory model's guarantee that the block's
-      // partial stores are visible to the last arriver on another XCD, not only the sc1 write-through)
+      // No release fence before the ticket (A/B knob INSITE_TAIL_RELEASE_FENCE).  On gfx950 an agent-scope
+      // release compiles to `buffer_wbl2 sc1; s_waitcnt vmcnt(0)`: a write-back of every dirty line in this
+      // XCD's L2 -- in the fused step kernel the rollout role's y stores -- at every block's arrival, which
+      // measured 0.0622 -> 0.0732 ms per C2 step (profiles/r03/).  What the fence would order is already
+      // ordered: every partial is written by an agent-scope atomic store, which gfx950 issues write-through
+      // (`global_store ... sc1`: it never sits dirty in the L2), each storing wave has drained its stores
+      // (s_waitcnt vmcnt(0): completion is acknowledged from the device coherence point) before the
+      // __syncthreads that precedes this ticket, the ticket is an agent-scope atomic performed at that point,
+      // and the last arriver reads only after its acquire fence (buffer_inv sc1).
+#if INSITE_TAIL_RELEASE_FENCE
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
       const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = t == arrivals - 1u;
       if (last) {
@@ -2252,19 +2264,32 @@ rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
 #ifndef INSITE_RK45_PM_NT
 #define INSITE_RK45_PM_NT 0
 #endif
+// PM output staging: a lane's y elements go to an 8-slot LDS ring indexed by their address within a 64-B
+// sector and are stored as one 64-B run (4 x 16 B) when the sector's last element arrives (partial sectors at
+// a row's ends element by element).  With one 8-B store per close the lane's sectors were written back
+// piecewise: L2 evicted a partly written line between two closes of the same lane (1M lanes x 480 B rows),
+// PMC WRITE_SIZE 1.35 GB per launch against 312 MB of y (profiles/r02_c5_pmc/).
+#ifndef INSITE_RK45_STAGE
+#define INSITE_RK45_STAGE 1
+#endif
 constexpr int kRkWin = INSITE_RK45_WIN;
+constexpr int kRkStage = INSITE_RK45_STAGE ? 8 : 1;
 template <int NARM, bool PERROW, bool PM>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_RK45_WPE)))
 rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
   constexpr double q2 = 1.0 / 2.0, q3 = 1.0 / 6.0, q4 = 1.0 / 24.0, q5 = 1.0 / 120.0, q6 = 1.0 / 600.0;
   constexpr double p0 = 97.0 / 120000.0, p1 = -13.0 / 40000.0, p2 = 1.0 / 24000.0;
   __shared__ double t_win[kWavesPerBlock * kRkWin * kWave];
+  __shared__ double y_ring[kWavesPerBlock * kRkStage * kWave];  // PM staging ring [slot][lane]
   const int64_t lane_id = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool act = lane_id < ra.N;
   int64_t p = act ? (ra.order ? (int64_t)ra.order[lane_id] : lane_id) : ra.N - 1;  // this lane's row
   p = p < 0 ? 0 : p >= ra.N ? ra.N - 1 : p;  // memory-safe on a malformed order (documented: a permutation)
   const int64_t pc = p;
   double* tw = t_win + (threadIdx.x / kWave) * (kRkWin * kWave) + (threadIdx.x & (kWave - 1));
+  double* yr = y_ring + (threadIdx.x / kWave) * (kRkStage * kWave) + (threadIdx.x & (kWave - 1));
+  constexpr bool kStage = PM && INSITE_RK45_STAGE && !INSITE_RK45_PM_NT;
+  int slot_lo = -1;  // kStage: first slot of the current sector holding a staged element (-1: none)
   double uu[INSITE_MAX_STATICS];
 #pragma unroll
   for (int t = 0; t < INSITE_MAX_STATICS; ++t) {
@@ -2401,8 +2426,32 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
         f = f_new;
       }
       if (close) {  // store y at t_{k+1} (row k), open interval k + 1 from the window
-        if (PM && !INSITE_RK45_PM_NT) *yp = y;  // PM: cached store, the lane's own line fills in L2
-        else __builtin_nontemporal_store(y, yp);
+        if constexpr (kStage) {
+          // element slot within its 64-B sector; the sector goes out when its last slot arrives or the row ends
+          const int slot = (int)(((uintptr_t)yp >> 3) & 7u);
+          yr[slot * kWave] = y;
+          if (slot_lo < 0) slot_lo = slot;
+          if (slot == 7 || !(k + 2 < n)) {
+            double* sec = yp - slot;
+            if (slot_lo == 0 && slot == 7) {
+              double v[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] = yr[j * kWave];
+#pragma unroll
+              for (int j = 0; j < 8; j += 2) {
+                typedef double d2 __attribute__((ext_vector_type(2)));
+                *reinterpret_cast<d2*>(sec + j) = d2{v[j], v[j + 1]};
+              }
+            } else {
+              for (int j = slot_lo; j <= slot; ++j) sec[j] = yr[j * kWave];
+            }
+            slot_lo = -1;
+          }
+        } else if (PM && !INSITE_RK45_PM_NT) {
+          *yp = y;  // PM: cached store, the lane's own line fills in L2
+        } else {
+          __builtin_nontemporal_store(y, yp);
+        }
         yp += ystep;
         t = t1;
         ++k;

@@ -46,9 +46,10 @@ class MomentBucket:
             self.bufs.append(b)
 
 
-def reduce_bucket(bucket: MomentBucket, group=None, deterministic: bool = False) -> MomentBucket:
-    """Sum every partial system of the bucket over all ranks in place, in one collective."""
-    if _world(group) > 1:
+def reduce_bucket(bucket: MomentBucket, group=None, deterministic: bool = False, force: bool = False) -> MomentBucket:
+    """Sum every partial system of the bucket over all ranks in place, in one collective (``force``: issue it
+    on a single-rank group too -- the bench's --force-collective measurement of the collective's cost)."""
+    if _world(group) > 1 or (force and dist.is_available() and dist.is_initialized()):
         if deterministic:
             fixed_order_sum(bucket.flat, group)
         else:

