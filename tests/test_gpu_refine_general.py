@@ -44,7 +44,9 @@ def _check(dev, V, arms, u, sl, c0, lib, tau, n_inputs=0):
             agree += 1
         fin = np.isfinite(rp)                                   # a refined model may leave the window unstable
         assert np.array_equal(np.isfinite(preds[p]), fin), p
-        assert np.sqrt(np.mean((preds[p][fin] - rp[fin]) ** 2)) <= 1e-6, p
+        # a refined polynomial model may blow up late in the window (x^3 terms): relative beyond unit scale
+        err = np.abs(preds[p][fin] - rp[fin]) / np.maximum(1.0, np.abs(rp[fin]))
+        assert np.sqrt(np.mean(err ** 2)) <= 1e-6, p
     assert agree == V.shape[0]
     assert (status[sl <= tau] == -1).all() and (iters[sl > tau] > 0).all()
     return status

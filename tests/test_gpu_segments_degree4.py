@@ -74,7 +74,13 @@ def test_plugin_degree4_segments_end_to_end(dev):
     for k in range(4):
         c_ref, ind_ref, _ = R.stlsq_gram(G_ref[k], b_ref[k], 1e-3, 0.5)
         assert np.array_equal(m.joint_coefs[k] != 0, ind_ref), k
-        assert np.max(np.abs(m.joint_coefs[k] - c_ref)) <= 1e-6 * max(1.0, np.abs(c_ref).max()), k
+        # the degree-4 normal equations are ill-conditioned (cond 1e11..3e13 on this cohort): coefficient
+        # agreement is bounded by cond x eps x |c| (up to ~1e-1 here), so the GPU solution is checked as what it
+        # is -- the unbiased least-squares minimiser on the support: the same objective to 1e-9 relative (a
+        # wrong support or solve moves it by O(1)), evaluated on the oracle's Gram
+        c = m.joint_coefs[k]
+        obj = lambda v: v @ G_ref[k] @ v - 2.0 * b_ref[k] @ v
+        assert abs(obj(c) - obj(c_ref)) <= 1e-9 * max(1.0, abs(obj(c_ref))), k
     p = m.get_predictions(ds)[..., 0]
     y_ref = R.rollout(x[:, 0], u, arm, m.joint_coefs, ex, 1 / 6, "euler5")
     fin = np.isfinite(y_ref)
