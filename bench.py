@@ -105,7 +105,7 @@ class HipEvents:
         # ordering events: hipEventDisableTiming | hipEventReleaseToDevice -- the consumers are queues of
         # this device, so a device-scope release suffices; the default system-scope release writes back
         # and invalidates the caches at every record (~20 us of dead queue time per step on ROCm 7.2:
-        # profiles/r02_c2_pipeline_trace.txt)
+        # profiles/r02/c2_pipeline_trace.txt)
         flags = 0x0 if timing else (0x2 | 0x40000000)
         if self._hip.hipEventCreateWithFlags(self._c.byref(e), flags) != 0:
             raise RuntimeError("hipEventCreateWithFlags failed")
@@ -1097,7 +1097,7 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
         "step_aggregate": {"algorithmic_bytes": rb + gb, "achieved_GBps": (rb + gb) / (ms_step * 1e-3) / 1e9,
                            "frac": (rb + gb) / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS},
         "pipeline_alternative": "bench.py --mode pipeline: gram | rollout on two streams (the N > 1 schedule); "
-                                "within a few % of this line, ahead over long runs (profiles/r02_fused_sweep/)",
+                                "within a few % of this line, ahead over long runs (profiles/r02/fused_sweep/)",
     }
     out["roofline"]["traffic"] = step_traffic(args)
     if iso is not None:
@@ -1191,7 +1191,7 @@ def main():
     # still read theirs (G|b and the gram workspace are only touched by the discovery stream, in order,
     # but are buffered alike to keep the plans independent).  Steps go in batches of K: one event per batch
     # each way (an event record costs ~20 us of dead queue time on ROCm 7.2, profiles/
-    # r02_c2_pipeline_trace.txt); batches alternate between RS rollout streams and y buffers.
+    # r02/c2_pipeline_trace.txt); batches alternate between RS rollout streams and y buffers.
     K, RS = args.pipe_k, args.pipe_rs
     WAR_EVERY = 2 * K
     NB = 3 * K * RS                     # a multiple of K * RS: step k's y buffer (k // K) % RS is fixed per coef slot
@@ -1223,7 +1223,7 @@ def main():
     #              NB-buffered coefficients; a batch's rollouts wait for one event after its last discovery,
     #              and the discovery stream waits, every WAR_EVERY steps, for the rollout batches whose
     #              buffers the next WAR_EVERY steps reuse.  Event records cost ~20 us of dead queue time
-    #              each on ROCm 7.2 (profiles/r02_c2_pipeline_trace.txt), so there is one per batch per
+    #              each on ROCm 7.2 (profiles/r02/c2_pipeline_trace.txt), so there is one per batch per
     #              stream; every step still runs its own discovery and the rollout with its coefficients
     #   seq      : gram + in-launch reduction + STLSQ (N = 1) then the rollout, eagerly on one stream
     #   graph    : the seq step captured once in a HIP graph and replayed (N = 1)
@@ -1521,7 +1521,7 @@ def main():
             "avg_ms_source": f"HIP timing events around {fr['NBAT']} batches of {fr['KB']} back-to-back launches",
             "why_not_headline": "one launch holds both roles at the gram's 2 waves/SIMD register budget, the two-stream "
                                 "pipeline keeps more rollout waves resident: the two measure within a few % of each "
-                                "other, the pipeline ahead on most boxes (profiles/r02_fused_sweep/)",
+                                "other, the pipeline ahead on most boxes (profiles/r02/fused_sweep/)",
         }
         del fr
     # north-star probe: 1M x 500 RK4 rollout alone (the >= 40 % roofline target), rank 0, N = 1
