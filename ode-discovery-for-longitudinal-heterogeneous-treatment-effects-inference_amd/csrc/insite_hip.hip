@@ -2268,7 +2268,7 @@ rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
 // sector and are stored as one 64-B run (4 x 16 B) when the sector's last element arrives (partial sectors at
 // a row's ends element by element).  With one 8-B store per close the lane's sectors were written back
 // piecewise: L2 evicted a partly written line between two closes of the same lane (1M lanes x 480 B rows),
-// PMC WRITE_SIZE 1.35 GB per launch against 312 MB of y (profiles/r02_c5_pmc/).
+// PMC WRITE_SIZE 1.35 GB per launch against 312 MB of y (profiles/r02/c5_pmc/).
 #ifndef INSITE_RK45_STAGE
 #define INSITE_RK45_STAGE 1
 #endif
@@ -2465,7 +2465,7 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
       if (rejected) factor = fmin(1.0, factor);
       const double h_next = close ? init_h(r5) : acc ? h_abs * factor : h_abs * fmax(0.2, 0.9 * r5);
       // a new step starts after an accept or a close (gating the bit-exact min_step on a wave ballot of the
-      // steps it could raise measured slower: 0.93 -> 0.98 ms, profiles/r02_c5_minstep/)
+      // steps it could raise measured slower: 0.93 -> 0.98 ms, profiles/r02/c5_minstep/)
       h_abs = acc ? fmax(h_next, min_step()) : h_next;
       rejected = !acc;
     }
@@ -3487,7 +3487,7 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
     // one patient per lane: with the interval propagator the time loop is store-bound, more chains per
     // lane buy nothing; since the prologue loads its coefficient row in one burst (affine_rates), two
     // patients per lane (16-B stores) is slower too: F4's 1M x 60 4-arm int8 rollout 0.117 ms at PPL 2,
-    // 0.094 ms at PPL 1, 0.168 ms at PPL 4 (profiles/r02_ppl/); INSITE_FORCE_PPL keeps the others
+    // 0.094 ms at PPL 1, 0.168 ms at PPL 4 (profiles/r02/ppl/); INSITE_FORCE_PPL keeps the others
 #endif
     if (ppl >= 2 && !(y16 && aw4 && n_rows % ppl == 0)) ppl = 1;
     const int64_t per_block = (int64_t)kBlock * ppl;

@@ -786,7 +786,7 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
     runs.  ``binned``: lanes take the rows sorted by seq_len (insite_rk45_order_i32 on the
     device), so a wave's objective scans have similar lengths; scheduling only, the outputs are bitwise the
     same.  Off by default: on the time-major V the binned lanes' scattered loads cost more than the shorter
-    scans save (1M rows, seq_len U{1..59}: 10.7 vs 9.5 ms, profiles/r02_v10_insite_bench.log).
+    scans save (1M rows, seq_len U{1..59}: 10.7 vs 9.5 ms, profiles/r02/v10_insite_bench.log).
     Returns (preds [N, T], coef [N, A, F], status [N], iterations [N])."""
     _dev("V", V, torch.float64, 2)
     _dev("arm", arm, torch.int8, 2)

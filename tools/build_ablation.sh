@@ -4,7 +4,7 @@ set -e
 R="$(cd "$(dirname "$0")/.." && pwd)"
 P="$R/ode-discovery-for-longitudinal-heterogeneous-treatment-effects-inference_amd"
 rm -rf "$P/lib/ablate"; mkdir -p "$P/lib/ablate"
-build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC "$@" -I "$R/include" -o "$P/lib/ablate/libinsite_hip_$NAME.so" "$P/csrc/insite_hip.hip" "$P/csrc/insite_ms.hip" "$P/csrc/insite_gen.hip" "$P/csrc/insite_refine.hip" -lhiprtc & }
+build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC "$@" -I "$R/include" -o "$P/lib/ablate/libinsite_hip_$NAME.so" "$P/csrc/insite_hip.hip" "$P/csrc/insite_ms.hip" "$P/csrc/insite_gen.hip" "$P/csrc/insite_refine.hip" "$P/csrc/insite_rng.hip" -lhiprtc & }
 for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
   case $v in
     NOSTORE) NAME=$v build -DINSITE_ABLATE_NOSTORE ;;
