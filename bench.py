@@ -1046,10 +1046,16 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
             e1.record(st)
             torch.cuda.synchronize(dev)
             return e0.elapsed_time(e1) / n
-        gp = ops.plan_sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, layout="time").bind(st)
-        rp = ops.plan_rollout(coh.y0, coh.u, arm_cf, fr["coef"], lib, coh.dt, method=args.method, T=T, out=y,
-                              layout="time_bits").bind(st)
-        iso = {"discovery_avg_launch_ms": timed(gp, 20), "rollout_avg_launch_ms": timed(rp, 20)}
+        # with rotation on, the isolated launches alternate between the two cohorts (and their y) as well
+        cs = [(coh, arm_cf), (coh2, arm_cf2)] if coh2 is not None else [(coh, arm_cf)]
+        y2 = torch.empty_like(y) if coh2 is not None else y
+        gps = [ops.plan_sindy_fit(c.x, c.u, c.arm, c.rows, c.dt, lib, 0.1, 0.5, layout="time").bind(st) for c, _ in cs]
+        rps = [ops.plan_rollout(c.y0, c.u, a, fr["coef"], lib, c.dt, method=args.method, T=T, out=yy,
+                                layout="time_bits").bind(st) for (c, a), yy in zip(cs, (y, y2))]
+        gi, ri = iter(range(10 ** 9)), iter(range(10 ** 9))
+        iso = {"discovery_avg_launch_ms": timed(lambda: gps[next(gi) % len(gps)](), 20),
+               "rollout_avg_launch_ms": timed(lambda: rps[next(ri) % len(rps)](), 20),
+               "rotated": coh2 is not None}
 
     sup = fr["mask"].cpu().numpy()
     ok = bool(torch.isfinite(y).all().item())

@@ -231,6 +231,24 @@ int32_t insite_fit_per_patient_moments_f64(const double* mom, const double* u, c
                                            double threshold, double alpha, int32_t max_iter, int32_t unbias,
                                            double* coef_out, int8_t* mask_out, int32_t* iters_out, void* stream);
 
+/* The per-patient refit of insite_fit_per_patient_moments_f64 folded into the rollout that uses it (C4; ABI
+ * 5): one launch, wave = 64 patients, whose prologue refits each lane's factual-arm row (arm[p]) from its
+ * moments mom [n_patients, 5] -- the same STLSQ from the global support, the ridge iterations in closed form
+ * (rank-2 Gram: a 2 x 2 solve per iteration) and the same unbias -- and whose time loop is insite_rollout_f64's
+ * (TIME_MAJOR_BITS arms arm_bits [T, ld_bits], y_out [T, ld_y]; the other arm keeps global_coef).  Replaces
+ * predict_with_reduced_coefs over the LSQIntialMask refits (pkpd_simulation.py:791-800, sindy.py:767-778)
+ * without the per-patient coefficient rows' HBM round trip.  coef_out [n_patients, n_arms, F] / mask_out
+ * [n_patients, F] / iters_out [n_patients] as insite_fit_per_patient_moments_f64, each may be NULL.
+ * Restrictions (else INSITE_E_UNSUPPORTED; use the two calls): n_arms <= 2, alpha > 0, state degree <= 1. */
+int32_t insite_refit_rollout_moments_f64(const double* mom, const int8_t* arm, const int32_t* rows, int64_t n_patients,
+                                         int32_t n_steps, int32_t n_statics, int32_t n_arms, const int8_t* exps,
+                                         int32_t n_terms, const double* global_coef, double threshold, double alpha,
+                                         int32_t max_iter, int32_t unbias, const double* y0, const double* u,
+                                         const uint32_t* arm_bits, int64_t ld_bits, int32_t T, double dt,
+                                         int32_t method, int32_t substeps, double drop_below, double* y_out,
+                                         int64_t ld_y, double* coef_out, int8_t* mask_out, int32_t* iters_out,
+                                         void* stream);
+
 /* Batched sequentially-thresholded least squares on Gram systems (one system per thread):
  * STLSQ._reduce semantics (all-ones initial support; ridge (G_SS + alpha I) c = b_S by
  * Cholesky; zero |c| < threshold; stop when nothing was removed in the first pass or the

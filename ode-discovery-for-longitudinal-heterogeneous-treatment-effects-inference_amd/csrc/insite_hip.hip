@@ -1326,6 +1326,161 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
 #ifndef INSITE_PP_WPE
 #define INSITE_PP_WPE 2  // waves per SIMD the per-patient fit's register budget is sized for
 #endif
+// The ridge iterations of that STLSQ in closed form.  On the support S the system is
+// (G_SS + alpha I) c = b_S with G = V W V^T, b = V s: V [j, e] = m_j [e_j == e] (two disjoint column
+// groups, state exponent 0 / 1), W = [[M0, M1], [M1, M2]], s = (Sd, Sdx).  Its unique solution (alpha > 0)
+// lies in span(V): c = V z with (W N + alpha I) z = s, N = V^T V = diag(n0, n1), n_e = sum_{j in S, e_j = e}
+// m_j^2 -- a 2 x 2 solve per iteration instead of a 7 x 7 Cholesky (and ~20 registers instead of ~180), so
+// the fit fits in the rollout's prologue (rollout_bits_range PR = 2).  Mathematically the masked solve of
+// stlsq_solve (its rounding differs at the last bits).  Stop rules, support and iteration count are
+// stlsq_solve's with init = the global support.  Returns the iteration count, or -3 if alpha <= 0 (the
+// caller then runs stlsq_solve, whose Cholesky reports a singular ridge system).
+__device__ __forceinline__ int refit_rank2(const double (&m)[INSITE_MAX_TERMS], const int (&e)[INSITE_MAX_TERMS], int F,
+                                           const double (&M)[3], double Sd, double Sdx, double thr, double alpha,
+                                           int max_iter, unsigned init, double (&c)[INSITE_MAX_TERMS], unsigned& sup) {
+  if (!(alpha > 0.0)) return -3;
+  const unsigned all = (1u << F) - 1u;
+  unsigned ind = init, prev = all;
+  int it = 0;
+#pragma unroll
+  for (int j = 0; j < INSITE_MAX_TERMS; ++j) c[j] = 0.0;
+  for (int k = 0; k < max_iter; ++k) {
+    it = k + 1;
+    if (ind == 0u) {
+#pragma unroll
+      for (int j = 0; j < INSITE_MAX_TERMS; ++j) c[j] = 0.0;
+      break;
+    }
+    double n0 = 0.0, n1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < INSITE_MAX_TERMS; ++j) {
+      const double q = ((ind >> j) & 1u) ? m[j] * m[j] : 0.0;
+      if (e[j]) n1 += q;
+      else n0 += q;
+    }
+    const double a11 = fma(M[0], n0, alpha), a12 = M[1] * n1, a21 = M[1] * n0, a22 = fma(M[2], n1, alpha);
+    const double det = a11 * a22 - a12 * a21;
+    const double z0 = (Sd * a22 - a12 * Sdx) / det, z1 = (a11 * Sdx - a21 * Sd) / det;
+    unsigned big = 0u;
+#pragma unroll
+    for (int j = 0; j < INSITE_MAX_TERMS; ++j) {
+      double cj = ((ind >> j) & 1u) ? m[j] * (e[j] ? z1 : z0) : 0.0;
+      if (fabs(cj) >= thr) big |= 1u << j;
+      else cj = 0.0;
+      c[j] = cj;
+    }
+    ind = big;
+    unsigned pattern = 0u;
+#pragma unroll
+    for (int j = 0; j < INSITE_MAX_TERMS; ++j)
+      if (c[j] != 0.0) pattern |= 1u << j;
+    if (ind == init || pattern == prev) break;
+    prev = pattern;
+  }
+  sup = 0u;
+#pragma unroll
+  for (int j = 0; j < INSITE_MAX_TERMS; ++j)
+    if (fabs(c[j]) > 1e-14) sup |= 1u << j;
+  return it;
+}
+
+// The per-patient unbias (minimum-norm lstsq on the support, closed form -- see patient_fit_kernel) and the
+// reference's sum |c| > 10 fallback; c holds the last ridge iterate on entry.
+__device__ __forceinline__ void refit_unbias(const double (&m)[INSITE_MAX_TERMS], const int (&e)[INSITE_MAX_TERMS],
+                                             const double (&M)[3], double Sd, double Sdx, unsigned sup,
+                                             double (&c)[INSITE_MAX_TERMS]) {
+  double n0 = 0.0, n1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < INSITE_MAX_TERMS; ++j)
+    if ((sup >> j) & 1u) {
+      if (e[j]) n1 += m[j] * m[j];
+      else n0 += m[j] * m[j];
+    }
+  const bool h0 = n0 > 0.0, h1 = n1 > 0.0;
+  double al = 0.0, be = 0.0, cu[INSITE_MAX_TERMS];
+  bool rank1 = false;
+  if (h0 && h1) {
+    const double det = M[0] * M[2] - M[1] * M[1];
+    if (det > 1e-13 * M[0] * M[2]) {
+      al = (Sd * M[2] - M[1] * Sdx) / det;
+      be = (M[0] * Sdx - M[1] * Sd) / det;
+    } else {
+      rank1 = true;  // x constant: every support column ~ m_j x0^{e_j}
+    }
+  } else if (h0) {
+    al = Sd / M[0];
+  } else if (h1 && M[2] > 0.0) {
+    be = Sdx / M[2];
+  }
+  double s1 = 0.0;
+  if (rank1) {
+    const double x0 = M[1] / M[0];
+    double vv = 0.0;
+#pragma unroll
+    for (int j = 0; j < INSITE_MAX_TERMS; ++j)
+      if ((sup >> j) & 1u) vv += (m[j] * (e[j] ? x0 : 1.0)) * (m[j] * (e[j] ? x0 : 1.0));
+    const double tq = vv > 0.0 ? Sd / (M[0] * vv) : 0.0;
+#pragma unroll
+    for (int j = 0; j < INSITE_MAX_TERMS; ++j) {
+      cu[j] = ((sup >> j) & 1u) ? m[j] * (e[j] ? x0 : 1.0) * tq : 0.0;
+      s1 += fabs(cu[j]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < INSITE_MAX_TERMS; ++j) {
+      cu[j] = ((sup >> j) & 1u) ? (e[j] ? (h1 ? m[j] * be / n1 : 0.0) : (h0 ? m[j] * al / n0 : 0.0)) : 0.0;
+      s1 += fabs(cu[j]);
+    }
+  }
+  if (s1 <= 10.0) {
+#pragma unroll
+    for (int j = 0; j < INSITE_MAX_TERMS; ++j) c[j] = cu[j];
+  }
+}
+
+// One patient's refit from its five moments (the patient_fit_kernel semantics): c[] = the refitted row of
+// arm a (global coefficients outside the refit), returns the STLSQ iteration count (0: < 5 rows, the global
+// model kept; -1: a non-positive-definite ridge system).
+template <int F, bool FALLBACK = true>
+__device__ __forceinline__ int patient_refit(const LibDesc& lib, const double* uu, const double (&M)[3], double Sd,
+                                             double Sdx, int L, const double* gca, const StlsqParams& sp,
+                                             double (&c)[INSITE_MAX_TERMS], unsigned& init_out) {
+  const int Fr = lib.F;  // == F in patient_fit_kernel; the fold (F = INSITE_MAX_TERMS) runs any library
+  unsigned init = 0u;
+#pragma unroll
+  for (int j = 0; j < INSITE_MAX_TERMS; ++j) {
+    c[j] = j < Fr ? gca[j] : 0.0;
+    if (j < Fr && fabs(c[j]) > 1e-14) init |= 1u << j;
+  }
+  init_out = init;
+  if (L < 5) return 0;
+  double m[INSITE_MAX_TERMS];
+  int e[INSITE_MAX_TERMS];
+#pragma unroll
+  for (int j = 0; j < INSITE_MAX_TERMS; ++j) {
+    m[j] = j < Fr ? monomial(lib, j, uu) : 0.0;
+    e[j] = j < Fr ? col_ex(lib, j) : 0;
+  }
+  unsigned sup = 0u;
+  int it = refit_rank2(m, e, Fr, M, Sd, Sdx, sp.thr, sp.alpha, sp.max_iter, init, c, sup);
+  if constexpr (!FALLBACK) {
+    if (it == -3) return -3;  // the caller guarantees alpha > 0
+  } else if (it == -3) {  // alpha <= 0: the generic masked-Cholesky STLSQ
+    double g[F][F], rhs[F], cf[F];
+#pragma unroll
+    for (int i = 0; i < F; ++i) {
+      rhs[i] = m[i] * (e[i] ? Sdx : Sd);
+#pragma unroll
+      for (int j = 0; j <= i; ++j) g[i][j] = m[i] * m[j] * M[e[i] + e[j]];
+    }
+    it = stlsq_solve<F>(g, rhs, sp.thr, sp.alpha, sp.max_iter, 0, cf, sup, init);
+#pragma unroll
+    for (int j = 0; j < INSITE_MAX_TERMS; ++j) c[j] = j < F ? cf[j] : 0.0;
+  }
+  if (sp.unbias && sup) refit_unbias(m, e, M, Sd, Sdx, sup, c);
+  return it;
+}
+
 template <int F>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_PP_WPE)))
 patient_fit_kernel(const double* __restrict__ mom, const double* __restrict__ u, const int8_t* __restrict__ arm,
@@ -1344,6 +1499,27 @@ patient_fit_kernel(const double* __restrict__ mom, const double* __restrict__ u,
     if (iters) iters[p] = -2;
     return;
   }
+#ifndef INSITE_PP_CHOLESKY
+  double uu[INSITE_MAX_STATICS];
+#pragma unroll
+  for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < lib.U ? u[p * lib.U + t] : 0.0;
+  const double M[3] = {mom[p * 5 + 0], mom[p * 5 + 1], mom[p * 5 + 2]};
+  double c[INSITE_MAX_TERMS];
+  unsigned init = 0u;
+  const int it = patient_refit<F>(lib, uu, M, mom[p * 5 + 3], mom[p * 5 + 4], L, gcoef + a * F, sp, c, init);
+  unsigned fin = 0u;
+#pragma unroll
+  for (int j = 0; j < F; ++j) {
+    coef[(p * n_arms + a) * F + j] = c[j];
+    if (fabs(c[j]) > 1e-14) fin |= 1u << j;
+  }
+  if (L < 5) fin = init;
+  if (mask) {
+#pragma unroll
+    for (int j = 0; j < F; ++j) mask[p * F + j] = (int8_t)((fin >> j) & 1u);
+  }
+  if (iters) iters[p] = it;
+#else  // A/B: the 7 x 7 masked-Cholesky STLSQ of round 2
   unsigned init = 0u;
 #pragma unroll
   for (int j = 0; j < F; ++j)
@@ -1436,6 +1612,7 @@ patient_fit_kernel(const double* __restrict__ mom, const double* __restrict__ u,
     for (int j = 0; j < F; ++j) mask[p * F + j] = (int8_t)((fin >> j) & 1u);
   }
   if (iters) iters[p] = it;
+#endif
 }
 
 // =============================================================================================
@@ -1453,6 +1630,21 @@ struct RolloutArgs {
   double dt, drop;
 };
 
+// The per-patient refit folded into a rollout prologue (rollout_bits_range PR = 2; C4): the factual arm's
+// row is refitted from the patient's moments (patient_refit, closed-form ridge), the other arms keep the
+// global model; optional per-patient outputs as insite_fit_per_patient_moments_f64.
+struct RefitArgs {
+  const double* mom;      // [N, 5]
+  const int8_t* farm;     // [N] factual arm
+  const int32_t* rows;    // [N] regression rows
+  const double* gcoef;    // [A, F] global model
+  double* coef_out;       // [N, A, F] or null
+  int8_t* mask_out;       // [N, F] or null
+  int32_t* iters_out;     // [N] or null
+  StlsqParams sp;
+  int32_t n_steps;
+};
+
 
 // Per-patient affine rates of every arm, f_a(y) = alpha_a + beta_a y: columns with x-exponent 0 feed alpha,
 // exponent 1 beta (terms with |c| <= drop dropped, sindy.py:388).  The lane's A x F coefficients are loaded
@@ -1461,9 +1653,11 @@ struct RolloutArgs {
 // C4 sizes: 14 dependent HBM round trips before the first step); the column codes are dword scalar loads.
 // Accumulation order (j ascending per arm) is that of the reference's term sum.
 template <int NARM>
-__device__ __forceinline__ void affine_rates(const LibDesc& lib, const double* cbase, int A, double drop,
-                                             const double* uu, double* alpha, double* beta) {
-  double cv[NARM][INSITE_MAX_TERMS];
+__device__ __forceinline__ void affine_rates_regs(const LibDesc& lib, const double (&cv)[NARM][INSITE_MAX_TERMS], int A,
+                                                  double drop, const double* uu, double* alpha, double* beta);
+template <int NARM>
+__device__ __forceinline__ void load_coef_rows(const LibDesc& lib, const double* cbase, int A,
+                                               double (&cv)[NARM][INSITE_MAX_TERMS]) {
 #pragma unroll
   for (int a = 0; a < NARM; ++a)
 #pragma unroll
@@ -1471,6 +1665,17 @@ __device__ __forceinline__ void affine_rates(const LibDesc& lib, const double* c
       const int aa = a < A ? a : 0, jj = j < lib.F ? j : 0;
       cv[a][j] = cbase[aa * lib.F + jj];
     }
+}
+template <int NARM>
+__device__ __forceinline__ void affine_rates(const LibDesc& lib, const double* cbase, int A, double drop,
+                                             const double* uu, double* alpha, double* beta) {
+  double cv[NARM][INSITE_MAX_TERMS];
+  load_coef_rows<NARM>(lib, cbase, A, cv);
+  affine_rates_regs<NARM>(lib, cv, A, drop, uu, alpha, beta);
+}
+template <int NARM>
+__device__ __forceinline__ void affine_rates_regs(const LibDesc& lib, const double (&cv)[NARM][INSITE_MAX_TERMS], int A,
+                                                  double drop, const double* uu, double* alpha, double* beta) {
 #pragma unroll
   for (int a = 0; a < NARM; ++a) alpha[a] = beta[a] = 0.0;
 #pragma unroll
@@ -1718,9 +1923,14 @@ constexpr int kArmByte = 0, kArmDword = 1, kArmBits = 2;
 // groups before it without storing them -- the same FMA sequence from y0, so the stored states are
 // bitwise those of a whole-trajectory pass (32 FMAs per skipped group against 32 x 512 B of stores).
 constexpr int kRollGS = 32;  // steps per arm group
-template <int METHOD, int NARM, bool PERROW>
+// PR: 0 = one global model (ra.coef [A, F]), 1 = per-patient rows (ra.coef + p * coef_stride), 2 = the
+// factual arm's row refitted in the prologue from the patient's moments (RefitArgs rf; C4's fit folded into
+// its rollout: no per-patient coefficient round trip through HBM, one launch less).
+template <int METHOD, int NARM, int PR>
 __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const LibDesc& lib, const int lane,
-                                                   const int64_t tile, const int g_begin, const int g_end) {
+                                                   const int64_t tile, const int g_begin, const int g_end,
+                                                   const RefitArgs* rf = nullptr) {
+  constexpr bool PERROW = PR == 1;
   const int64_t p0 = tile * kWave;
   const int64_t p = p0 + lane;
   const bool act = p < ra.N;
@@ -1734,7 +1944,36 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
       uu[t] = (act && t < lib.U) ? v : 0.0;
     }
     double al[NARM], be[NARM];
-    affine_rates<NARM>(lib, ra.coef + (PERROW ? pc * ra.coef_stride : 0), ra.A, ra.drop, uu, al, be);
+    if constexpr (PR == 2) {
+      double cv[NARM][INSITE_MAX_TERMS];
+      load_coef_rows<NARM>(lib, rf->gcoef, ra.A, cv);
+      const int af = rf->farm[pc];
+      int L = rf->rows[pc];
+      if (L > rf->n_steps) L = rf->n_steps;
+      const bool fit = act && af >= 0 && af < ra.A;
+      const double M[3] = {rf->mom[pc * 5 + 0], rf->mom[pc * 5 + 1], rf->mom[pc * 5 + 2]};
+      const double Sd = rf->mom[pc * 5 + 3], Sdx = rf->mom[pc * 5 + 4];
+      double c[INSITE_MAX_TERMS];
+      unsigned init = 0u;
+      const int it = patient_refit<INSITE_MAX_TERMS, false>(lib, uu, M, Sd, Sdx, L, rf->gcoef + (fit ? af : 0) * lib.F,
+                                                             rf->sp, c, init);
+#pragma unroll
+      for (int a = 0; a < NARM; ++a)
+#pragma unroll
+        for (int j = 0; j < INSITE_MAX_TERMS; ++j) cv[a][j] = (fit && a == af) ? c[j] : cv[a][j];
+      if (act && rf->coef_out) {
+        for (int a = 0; a < ra.A; ++a)
+          for (int j = 0; j < lib.F; ++j) rf->coef_out[(p * ra.A + a) * lib.F + j] = (fit && a == af) ? c[j] : rf->gcoef[a * lib.F + j];
+      }
+      if (act && fit && rf->mask_out) {
+        for (int j = 0; j < lib.F; ++j)
+          rf->mask_out[p * lib.F + j] = (int8_t)(L < 5 ? (init >> j) & 1u : (fabs(c[j]) > 1e-14 ? 1u : 0u));
+      }
+      if (act && rf->iters_out) rf->iters_out[p] = fit ? it : -2;
+      affine_rates_regs<NARM>(lib, cv, ra.A, ra.drop, uu, al, be);
+    } else {
+      affine_rates<NARM>(lib, ra.coef + (PERROW ? pc * ra.coef_stride : 0), ra.A, ra.drop, uu, al, be);
+    }
     const double h = ra.dt / (double)ra.substeps;
 #ifndef INSITE_ROLLOUT_STAGEWISE
 #pragma unroll
@@ -1994,6 +2233,19 @@ __global__ void __launch_bounds__(kBlock) rollout_tm_kernel(RolloutArgs ra, LibD
 #endif
     }
   }
+}
+
+// Per-patient refit + rollout in one launch (C4; insite_refit_rollout_moments_f64): wave = 64-patient tile,
+// the prologue refits the lane's factual-arm row from its moments (patient_refit, closed-form ridge) and
+// the time loop is rollout_bits_range's.  Replaces patient_fit_kernel + the per-row rollout: the
+// per-patient coefficient rows (N x A x F doubles written, then read) never touch HBM.
+template <int METHOD, int NARM>
+__global__ void __launch_bounds__(kBlock) refit_rollout_kernel(RolloutArgs ra, LibDesc lib, RefitArgs rf) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  if (tile * kWave >= ra.N) return;
+  rollout_bits_range<METHOD, NARM, 2>(ra, lib, lane, tile, 0, (ra.T + kRollGS - 1) / kRollGS, &rf);
 }
 
 // =============================================================================================
@@ -3319,6 +3571,61 @@ int32_t insite_fit_per_patient_moments_f64(const double* mom, const double* u, c
   return launch_patient_fit(mom, u, arm, rows, n_patients, n_steps, n_arms, lib, global_coef,
                             StlsqParams{threshold, alpha, max_iter, unbias, 1}, coef_out, mask_out, iters_out,
                             reinterpret_cast<hipStream_t>(stream));
+}
+
+int32_t insite_refit_rollout_moments_f64(const double* mom, const int8_t* arm, const int32_t* rows, int64_t n_patients,
+                                         int32_t n_steps, int32_t n_statics, int32_t n_arms, const int8_t* exps,
+                                         int32_t n_terms, const double* global_coef, double threshold, double alpha,
+                                         int32_t max_iter, int32_t unbias, const double* y0, const double* u,
+                                         const uint32_t* arm_bits, int64_t ld_bits, int32_t T, double dt,
+                                         int32_t method, int32_t substeps, double drop_below, double* y_out,
+                                         int64_t ld_y, double* coef_out, int8_t* mask_out, int32_t* iters_out,
+                                         void* stream) {
+  if (n_patients < 0 || n_arms < 1 || n_arms > 2 || n_steps < 0 || max_iter < 0 || !(threshold >= 0.0) ||
+      !(alpha >= 0.0) || T < 0 || substeps < 1 || !(dt >= 0.0) || ld_bits < (n_patients + 31) / 32 ||
+      ld_y < n_patients)
+    return INSITE_E_INVALID_ARG;
+  if (method != INSITE_METHOD_EULER && method != INSITE_METHOD_RK4) return INSITE_E_UNSUPPORTED;
+  if (!(alpha > 0.0)) return INSITE_E_UNSUPPORTED;  // the closed-form refit needs a ridge: use the two calls
+  LibDesc lib;
+  int32_t st = build_lib(exps, n_terms, n_statics, &lib);
+  if (st != INSITE_OK) return st;
+  for (int j = 0; j < n_terms; ++j)
+    if (exps[j * (1 + n_statics)] > 1) return INSITE_E_UNSUPPORTED;  // state degree <= 1 (the moments' model)
+  if (n_patients == 0 || T == 0) return INSITE_OK;
+  if (!mom || !arm || !rows || !global_coef || !y0 || !arm_bits || !y_out || (n_statics > 0 && !u))
+    return INSITE_E_INVALID_ARG;
+  if ((reinterpret_cast<uintptr_t>(arm_bits) & 3u) != 0) return INSITE_E_INVALID_ARG;
+  if (ld_bits * 4 > kTmMaxLd || ld_y > kTmMaxLd) return INSITE_E_UNSUPPORTED;
+  RolloutArgs ra;
+  ra.y0 = y0;
+  ra.u = n_statics == 0 ? y0 : u;
+  ra.arm = reinterpret_cast<const int8_t*>(arm_bits);
+  ra.coef = global_coef;
+  ra.y = y_out;
+  ra.lda = ld_bits;
+  ra.ldy = ld_y;
+  ra.coef_stride = 0;
+  ra.N = n_patients;
+  ra.T = T;
+  ra.substeps = substeps;
+  ra.A = n_arms;
+  ra.dt = dt;
+  ra.drop = drop_below;
+  RefitArgs rf{mom, arm, rows, global_coef, coef_out, mask_out, iters_out,
+               StlsqParams{threshold, alpha, max_iter, unbias, 1}, n_steps};
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  const int64_t tiles = (n_patients + kWave - 1) / kWave;
+  const dim3 grid((unsigned)((tiles + kWavesPerBlock - 1) / kWavesPerBlock));
+  const int na = narm_pad(n_arms);
+  if (method == INSITE_METHOD_EULER) {
+    if (na == 1) refit_rollout_kernel<INSITE_METHOD_EULER, 1><<<grid, kBlock, 0, hs>>>(ra, lib, rf);
+    else refit_rollout_kernel<INSITE_METHOD_EULER, 2><<<grid, kBlock, 0, hs>>>(ra, lib, rf);
+  } else {
+    if (na == 1) refit_rollout_kernel<INSITE_METHOD_RK4, 1><<<grid, kBlock, 0, hs>>>(ra, lib, rf);
+    else refit_rollout_kernel<INSITE_METHOD_RK4, 2><<<grid, kBlock, 0, hs>>>(ra, lib, rf);
+  }
+  return launch_status();
 }
 
 size_t insite_gram_segments_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms) {

@@ -67,6 +67,7 @@ EXPORTS = (
     "insite_stlsq_wave64_f64",
     "insite_rollout_poly_f64",
     "insite_threefry2x32_iota_u32",
+    "insite_refit_rollout_moments_f64",
 )
 
 
@@ -135,6 +136,9 @@ _SIGNATURES = {
     "insite_gen_gram_segments_workspace_bytes": (_c_size, [_c_i64, _c_i32, _c_i32]),
     "insite_gen_gram_segments_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i32, _c_i64,
                                               _c_i32, _vp, _c_i32, _c_i32, _c_f64, _vp, _vp, _vp, _c_size, _vp]),
+    "insite_refit_rollout_moments_f64": (_c_i32, [_vp, _vp, _vp, _c_i64, _c_i32, _c_i32, _c_i32, _vp, _c_i32, _vp,
+                                                  _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i64, _c_i32,
+                                                  _c_f64, _c_i32, _c_i32, _c_f64, _vp, _c_i64, _vp, _vp, _vp, _vp]),
     "insite_threefry2x32_iota_u32": (_c_i32, [ctypes.c_uint32, ctypes.c_uint32, _c_i64, _vp, _vp]),
     "insite_masked_sse_workspace_bytes": (_c_size, [_c_i64, _c_i32]),
     "insite_masked_sse_f64": (_c_i32, [_vp, _c_i64, _c_f64, _c_f64, _vp, _vp, _c_i64, _c_i32, _vp, _vp, _vp,

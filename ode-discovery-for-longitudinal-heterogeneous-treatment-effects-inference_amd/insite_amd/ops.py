@@ -329,6 +329,61 @@ def fit_per_patient_moments(mom: torch.Tensor, u: torch.Tensor, arm: torch.Tenso
     return _run(("insite_fit_per_patient_moments_f64", args, dev, out))
 
 
+def _prep_refit_rollout(mom, u, arm, rows, n_steps, lib, global_coef, threshold, alpha, y0, arm_bits, dt, T, method,
+                        max_iter, unbias, drop_below, out, fits):
+    _dev("mom", mom, torch.float64, 2)
+    N = mom.size(0)
+    _dev("global_coef", global_coef, torch.float64, 2)
+    A, F = global_coef.shape
+    if mom.size(1) != 5 or not mom.is_contiguous() or F != lib.n_terms or not global_coef.is_contiguous():
+        raise ValueError("mom must be contiguous [N, 5]; global_coef a contiguous [n_arms, F] tensor")
+    if arm.numel() != N or rows.numel() != N or y0.numel() != N:
+        raise ValueError("arm/rows/y0 must have one entry per patient")
+    _dev("arm_bits", arm_bits, torch.int32, 2)
+    if arm_bits.size(0) < T or arm_bits.size(1) < (N + 31) // 32:
+        raise ValueError("arm_bits must be [T, >= ceil(N / 32)] int32 words")
+    if method not in METHODS:
+        raise ValueError(f"method must be one of {sorted(METHODS)}")
+    meth, sub = METHODS[method]
+    dev = mom.device
+    if out is None:
+        out = torch.empty((T, N), dtype=torch.float64, device=dev)
+    _dev("out", out, torch.float64, 2)
+    if out.size(0) < T or out.size(1) < N:
+        raise ValueError("out must be [T, >= N]")
+    fc, fm, fi = fits if fits is not None else (None, None, None)
+    tab = lib.ctypes_table()
+    nul = ctypes.c_void_p(0)
+    args = (_p(mom), _p(arm), _p(rows), N, int(n_steps), lib.n_statics, A, tab.ctypes.data_as(ctypes.c_void_p), F,
+            _p(global_coef), float(threshold), float(alpha), int(max_iter), int(bool(unbias)), _p(y0),
+            _p(u) if lib.n_statics else nul, _p(arm_bits), arm_bits.stride(0), int(T), float(dt), meth, sub,
+            float(drop_below), _p(out), out.stride(0), _p(fc), _p(fm), _p(fi))
+    keep = (mom, u, arm, rows, global_coef, y0, arm_bits, out, fc, fm, fi, tab)
+    return "insite_refit_rollout_moments_f64", args, dev, out, keep
+
+
+def refit_rollout_moments(mom: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, rows: torch.Tensor, n_steps: int,
+                          lib: PolyLibrary, global_coef: torch.Tensor, threshold: float, alpha: float,
+                          y0: torch.Tensor, arm_bits: torch.Tensor, dt: float, T: int, method: str = "euler5",
+                          max_iter: int = 100, unbias: bool = True, drop_below: float = 1e-3,
+                          out: torch.Tensor | None = None, fits: tuple | None = None):
+    """``fit_per_patient_moments`` + the per-patient-coefficient ``rollout`` (TIME_MAJOR_BITS arms) in ONE launch
+    (insite_refit_rollout_moments_f64): each lane refits its factual arm's row from its moments in the rollout's
+    prologue, so the per-patient coefficient rows never reach HBM.  ``fits`` = (coef[N, A, F], mask[N, F],
+    iters[N]) to also receive the refits (any entry None).  Returns y [T, N]."""
+    return _run(_prep_refit_rollout(mom, u, arm, rows, n_steps, lib, global_coef, threshold, alpha, y0, arm_bits, dt,
+                                    T, method, max_iter, unbias, drop_below, out, fits))
+
+
+def plan_refit_rollout_moments(mom, u, arm, rows, n_steps, lib, global_coef, threshold, alpha, y0, arm_bits, dt, T,
+                               method="euler5", max_iter=100, unbias=True, drop_below=1e-3, out=None, fits=None):
+    """``refit_rollout_moments`` prepared once (a ``Plan``)."""
+    name, args, dev, out, keep = _prep_refit_rollout(mom, u, arm, rows, n_steps, lib, global_coef, threshold, alpha,
+                                                     y0, arm_bits, dt, T, method, max_iter, unbias, drop_below, out,
+                                                     fits)
+    return Plan(name, args, dev, out, keep)
+
+
 SEGMENT_FD_KINDS = {"order1": _lib.FD_ORDER1, "smoothed1": _lib.FD_SMOOTHED1}
 
 
