@@ -356,7 +356,7 @@ def c3_main(args):
                    "support_equals_truth": bool(torch.equal(mask != 0, truth != 0))},
         "roofline": {"kernel": "gram_ms4_kernel", "bound": "mfma", "achieved": gflop / (gram_ms_t * 1e-3) / 1e12,
                      "peak": 78.6, "unit": "TFLOP/s", "frac": gflop / (gram_ms_t * 1e-3) / 1e12 / 78.6,
-                     "traffic": None, "avg_launch_ms": gram_ms_t,
+                     "traffic": traffic_for("c3", "gram_ms4_kernel"), "avg_launch_ms": gram_ms_t,
                      "issued_mfma_TFLOPs": mfma_flop / (gram_ms_t * 1e-3) / 1e12,
                      "hbm_GBps": gram_bytes / (gram_ms_t * 1e-3) / 1e9},
         "rollout": {"kernel": "ms_rollout_sparse (hipRTC, support-specialised; rk4, fp32)", "bound": "hbm",
@@ -487,7 +487,8 @@ def c5_main(args):
                    "mean_intervals": float(intervals.mean()), "parallelism": f"patient-shard x{world}"},
         "roofline": {"kernel": "rollout_rk45_kernel", "bound": "valu-f64", "unit": "TFLOP/s",
                      "achieved": flop / (launch_ms * 1e-3) / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
-                     "frac": flop / (launch_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS, "traffic": None,
+                     "frac": flop / (launch_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
+                     "traffic": traffic_for("c5", "rollout_rk45_flat_kernel"),
                      "avg_launch_ms": launch_ms, "flop_per_attempt": RK45_FLOP_PER_ATTEMPT,
                      "issued_incl_divergence_TFLOPs": issued / (launch_ms * 1e-3) / 1e12,
                      "algorithmic_bytes": N * (8 * 3 + 4) + N * Tm * 8 * 2 + N * ((Tm + 30) // 32) * 4,
@@ -606,6 +607,36 @@ def insite_main(args):
     ms_step, (preds, coef, status, iters) = timed(False)
     st = status.cpu().numpy()
     it = iters.cpu().numpy()
+    # roofline: the refinement kernel alone on the time-major layout (no per-call transposes), HIP events on its
+    # stream; its work = every objective/gradient evaluation (nfev per row, counted by the kernel on one
+    # untimed launch through insite_refine_general_f64) x the row's K-step window x flops per sensitivity step
+    Vt = V.t().contiguous()
+    bits = ops.pack_arm_bits(arm.t().contiguous(), N)
+    kst = torch.cuda.current_stream(dev)
+
+    def kern():
+        return ops.insite_refine_tm(Vt, bits, coh.u, sl, c0, coh.lib, dt, 10.0, 5)
+
+    for _ in range(2):
+        kern()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(kst)
+    for _ in range(args.steps):
+        kern()
+    e1.record(kst)
+    torch.cuda.synchronize(dev)
+    kern_ms = e0.elapsed_time(e1) / args.steps
+    nf = torch.empty((N,), dtype=torch.int32, device=dev)
+    p2, _, s2, i2 = ops.insite_refine_tm(Vt, bits, coh.u, sl, c0, coh.lib, dt, 10.0, 5, nfev=nf)
+    torch.cuda.synchronize(dev)
+    same = bool(torch.equal(s2, status) and torch.equal(i2, iters) and torch.equal(p2.t(), preds))
+    K = torch.clamp(sl.to(torch.int64) - 5, min=0, max=T - 1)
+    A_, SUB = 2, 5
+    per_step = SUB * (4 * A_ + 7) + 4 * A_ + 5     # Euler sub-steps with the A x 2 sensitivities + residual/gradient
+    refine_flop = float((nf.to(torch.int64) * K).sum().item()) * per_step
+    final_flop = float(N) * T * SUB * 4            # the refined model's final Euler scan over the whole row
+    flop = refine_flop + final_flop
+    kbytes = N * T * (8 + 8) + T * ((N + 31) // 32) * 4 + N * (8 * 2 + 4) + N * (2 * coh.lib.n_terms * 8 + 8)
     out = {
         "metric": METRIC, "value": N / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
@@ -618,7 +649,20 @@ def insite_main(args):
                    "lane_order": "identity (lane = row: coalesced time-major V)",
                    "binned_by_seq_len_ms_per_step": ms_binned,
                    "reference_wall_time_s": "88.96 s per INSITE EQ_4_A run incl. 59,000 + 11,800 refinements "
-                                            "(results/2_main_table/final_with_insite.txt:2346; SURVEY.md §6)"},
+                                            "(results/2_main_table/final_with_insite.txt:2346; SURVEY.md §6)",
+                   "mean_evaluations_per_refined_row": float(nf.to(torch.float64)[status >= 0].mean().item()),
+                   "evaluation_count_route_matches": same},
+        "roofline": {"kernel": "insite_refine_kernel<4, 2, 1> (per-row BFGS + final Euler-5 scan)", "bound": "valu-f64",
+                     "unit": "TFLOP/s", "achieved": flop / (kern_ms * 1e-3) / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
+                     "frac": flop / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
+                     "traffic": traffic_for("insite", "insite_refine_kernel"), "avg_launch_ms": kern_ms,
+                     "algorithmic_flop": flop, "flop_per_sensitivity_step": per_step,
+                     "flop_method": "sum over refined rows of nfev_r x K_r (K_r = min(seq_len - tau, T - 1)) x "
+                                    "(5 Euler sub-steps x (4A + 7) + 4A + 5) with A = 2 arms, + N x T x 5 x 4 for "
+                                    "the final scan; nfev from the kernel's own count (insite_refine_general_f64)",
+                     "algorithmic_bytes": kbytes, "achieved_GBps": kbytes / (kern_ms * 1e-3) / 1e9,
+                     "avg_ms_source": "HIP events on the launch stream around args.steps back-to-back launches of "
+                                      "the time-major entry (the step's transposes excluded)"},
     }
     if cpu is not None:
         out["cpu_baseline"] = cpu
@@ -704,7 +748,8 @@ def f4_main(args):
                    "max_abs_coef_error_vs_planted": float(np.max(np.abs(out[0].cpu().numpy() - np.array(F4_COEF))))},
         "roofline": {"kernel": "gram_seg_kernel (order1, 4 arms) + discovery_finalize<0>", "bound": "hbm",
                      "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
-                     "traffic": None, "algorithmic_bytes_per_launch": gb, "avg_launch_ms": gram_ms},
+                     "traffic": traffic_for("f4", "gram_seg_kernel"), "algorithmic_bytes_per_launch": gb,
+                     "avg_launch_ms": gram_ms},
         "rollout": {"kernel": "rollout_tm_kernel (euler5, 4 arms, int8 arms)", "avg_launch_ms": roll_ms,
                     "algorithmic_bytes": rb, "achieved_GBps": rb / (roll_ms * 1e-3) / 1e9,
                     "frac": rb / (roll_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS},
@@ -793,10 +838,15 @@ def c4_main(args):
     def per_patient():
         ops.fit_per_patient_moments(mom, coh.u, coh.arm, coh.rows, T, lib, gout[0], 0.1, 0.5, out=pout)
 
+    # the per-patient refit folded into the rollout (insite_refit_rollout_moments_f64): one launch, the
+    # per-patient coefficient rows never reach HBM; the two-call form (fit, then per-row rollout) is timed
+    # beside it as "two_call_alternative"
+    fold = ops.plan_refit_rollout_moments(mom, coh.u, coh.arm, coh.rows, T, lib, gout[0], 0.1, 0.5, coh.y0, arm_cf,
+                                          coh.dt, T, method="euler5", out=y)
+
     def step():
         discover()
-        per_patient()
-        ops.rollout(coh.y0, coh.u, arm_cf, pout[0], lib, coh.dt, method="euler5", T=T, out=y, layout="time_bits")
+        fold()
 
     for _ in range(args.warmup):
         step()
@@ -825,12 +875,17 @@ def c4_main(args):
 
     n_roof = max(args.steps, 5)
     disc_ms = timed(discover, n_roof)
+    fold_ms = timed(fold, n_roof)
     pp_ms = timed(per_patient, n_roof)
     roll_ms = timed(lambda: ops.rollout(coh.y0, coh.u, arm_cf, pout[0], lib, coh.dt, method="euler5", T=T, out=y,
                                         layout="time_bits"), n_roof)
+    # the refits themselves (iterations, supports): one untimed launch with the optional outputs
+    ops.refit_rollout_moments(mom, coh.u, coh.arm, coh.rows, T, lib, gout[0], 0.1, 0.5, coh.y0, arm_cf, coh.dt, T,
+                              out=y, fits=pout)
     it = pout[2].to(torch.float64)
     if rank == 0:
-        rb = rollout_bytes(N, T, arm_bits=1) + N * 2 * F * 8          # + the per-patient coefficient rows
+        fb = rollout_bytes(N, T, arm_bits=1) + N * (5 * 8 + 1 + 4)      # + moments / factual arm / rows read
+        rb = rollout_bytes(N, T, arm_bits=1) + N * 2 * F * 8            # two-call: + the per-patient coefficient rows
         db = N * T * 8 + N * (2 * 8 + 1 + 4) + N * 5 * 8                # x + statics/arm/rows in, moments out
         pb = N * 5 * 8 + N * (2 * 8 + 1 + 4) + N * (2 * F * 8 + F + 4)  # moments + statics/arm/rows in, fits out
         res = {
@@ -840,19 +895,23 @@ def c4_main(args):
             "data": "synthetic: on-device EQ_4_C PK/PD cohort (reference distributions, Euler-5 truth + 0.01 noise)",
             "config": {"workload": f"C4: PK/PD {N_total // 1000}k patients x {T} steps: global discovery and every "
                                    f"patient's moments in one pass (+ RCCL all-reduce when N>1) + per-patient STLSQ "
-                                   f"+ per-patient-coefficient Euler-5 rollout", "patients_total": N_total, "patients_per_gpu": N, "T": T,
+                                   f"folded into the per-patient-coefficient Euler-5 rollout", "patients_total": N_total, "patients_per_gpu": N, "T": T,
                        "parallelism": f"patient-shard x{world}",
                        "global_support": (gout[1].cpu().numpy() != 0).astype(int).tolist(),
                        "mean_per_patient_iterations": float(it.mean())},
-            "roofline": {"kernel": "rollout_tm_kernel (euler5, per-patient coef, bit arms)", "bound": "hbm",
-                         "achieved": rb / (roll_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": rb / (roll_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": None,
-                         "algorithmic_bytes_per_launch": rb, "avg_launch_ms": roll_ms},
+            "roofline": {"kernel": "refit_rollout_kernel (per-patient refit from the moments in the prologue + "
+                                   "euler5 bit-arm rollout)", "bound": "hbm",
+                         "achieved": fb / (fold_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": fb / (fold_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": traffic_for("c4", "refit_rollout_kernel"),
+                         "algorithmic_bytes_per_launch": fb, "avg_launch_ms": fold_ms},
             "discovery": {"kernels": "gram_kernel<MOM=2> (Gram + in-launch reduction + STLSQ + every patient's "
                                      "moments, one pass over x)" + (" + RCCL all-reduce + stlsq_kernel" if world > 1 else ""),
                           "avg_ms": disc_ms, "algorithmic_bytes": db, "achieved_GBps": db / (disc_ms * 1e-3) / 1e9},
-            "per_patient_fit": {"kernels": "patient_fit_kernel<7> (from the moments)", "avg_ms": pp_ms,
-                                "algorithmic_bytes": pb, "achieved_GBps": pb / (pp_ms * 1e-3) / 1e9},
+            "two_call_alternative": {
+                "kernels": "patient_fit_kernel<7> (from the moments) + rollout_tm_kernel (per-patient coefficient rows)",
+                "per_patient_fit_ms": pp_ms, "per_patient_fit_bytes": pb,
+                "per_patient_fit_GBps": pb / (pp_ms * 1e-3) / 1e9, "rollout_ms": roll_ms, "rollout_bytes": rb,
+                "rollout_GBps": rb / (roll_ms * 1e-3) / 1e9, "sum_ms": pp_ms + roll_ms},
         }
         if world == 1 and not args.no_cpu_baseline:
             sys.path.insert(0, ROOT)
@@ -926,6 +985,27 @@ def dist_setup(force_group: bool = False):
         backend = os.environ.get("INSITE_DIST_BACKEND", "nccl")
         dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
     return world, rank, dev
+
+
+TRAFFIC_R03 = os.path.join(ROOT, "profiles", "traffic_r03.json")
+
+
+def traffic_for(config, kernel, grid=None):
+    """HBM bytes per launch of `kernel` (symbol prefix) in the bench line `config`, from the committed PMC passes
+    (profiles/traffic_r03.json, tools/g_traffic.sh + tools/traffic_summary.py: FETCH_SIZE x 2 calibration +
+    WRITE_SIZE, median per dispatch), or None when that table has no such entry.  `grid`: the launch's total
+    threads when a config launches the kernel at several sizes."""
+    try:
+        with open(TRAFFIC_R03) as f:
+            tab = json.load(f).get(config, {})
+    except Exception:
+        return None
+    hits = [v for v in tab.values() if v.get("kernel", "").startswith(kernel)
+            and (grid is None or str(v.get("grid_size")) == str(grid))]
+    if not hits:
+        return None
+    best = max(hits, key=lambda v: v.get("dispatches") or 0)
+    return best.get("hbm_bytes")
 
 
 def step_traffic(args):
@@ -1105,7 +1185,8 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
         "pipeline_alternative": "bench.py --mode pipeline: gram | rollout on two streams (the N > 1 schedule); "
                                 "within a few % of this line, ahead over long runs (profiles/r02/fused_sweep/)",
     }
-    out["roofline"]["traffic"] = step_traffic(args)
+    t3 = traffic_for("c2", "step_kernel") if fr["rotated"] and args.patients == 100_000 and args.T == 200 else None
+    out["roofline"]["traffic"] = t3 if t3 is not None else step_traffic(args)
     if iso is not None:
         out["isolated"] = dict(iso, discovery_frac=gb / (iso["discovery_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                                rollout_frac=rb / (iso["rollout_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS)

@@ -371,14 +371,16 @@ int32_t insite_gen_gram_segments_f64(const double* x, int64_t ldx, const int8_t*
  * non-zero coefficient of exponent >= 2 runs the state-polynomial kernels).  Objective, BFGS, status and
  * outputs as insite_refine_f64; coef_out [n_rows, n_coef].
  *   arm_bits TIME_MAJOR_BITS [T, ld_arm] (n_arms <= 2)  XOR  arm [T, ld_arm] int8 (n_arms <= 4)
- *   coef0 / coef_arm_mask [n_coef] / coef_exps [n_coef][1 + n_statics]: HOST arrays, n_coef <= 72  */
+ *   coef0 / coef_arm_mask [n_coef] / coef_exps [n_coef][1 + n_statics]: HOST arrays, n_coef <= 72   * nfev_out [n_rows] int32 (may be NULL): evaluations of the objective and its gradient per row (each one
+ * Euler scan of the row's K-step window with its sensitivities) -- the refinement's work count (bench.py's
+ * INSITE roofline: flops = sum_r nfev_r K_r x flops per sensitivity step). */
 int32_t insite_refine_general_f64(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits,
                                   const int8_t* arm, int64_t ld_arm, const double* u, const int32_t* seq_len,
                                   int64_t n_rows, int32_t n_statics, int32_t n_coef, const double* coef0,
                                   const int32_t* coef_arm_mask, const int8_t* coef_exps, int32_t n_arms, double dt,
                                   double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail,
                                   double* preds, int64_t ld_p, double* coef_out, int32_t* status_out,
-                                  int32_t* iters_out, const int32_t* row_order, void* stream);
+                                  int32_t* iters_out, int32_t* nfev_out, const int32_t* row_order, void* stream);
 
 /* General one-state discovery (insite_gen.hip): libraries with state exponents up to 4 and/or per-step
  * binary treatment INPUTS — the reference's degree-4 ablation (PolynomialLibrary(degree=4,

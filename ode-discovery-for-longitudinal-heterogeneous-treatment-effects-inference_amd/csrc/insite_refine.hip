@@ -52,6 +52,7 @@ struct RefineArgs {
   double* coef_out;     // [N, n_coef] or NULL
   int32_t* status;      // [N] or NULL (-1 skipped, else the BFGS status)
   int32_t* iters;       // [N] or NULL
+  int32_t* nfev;        // [N] or NULL: objective + gradient evaluations (the roofline's flop count)
   const int32_t* order; // [N] lane -> row (rows binned by seq_len), NULL = identity
   int64_t ldv, lda, ldp, N;
   int32_t T, tau, sub, U, A, m, n_coef;
@@ -107,7 +108,9 @@ struct RefineLane {
     else return (int)ra.arm8[(int64_t)k * ra.lda + p];
   }
   // f and gradient at c (active coordinates)
+  mutable int nev = 0;  // evaluations of f and its gradient (each one scan of the K-step window)
   __device__ double fg(const double (&c)[M], double (&g)[M]) const {
+    ++nev;
     double gam[NA][D + 1];
 #pragma unroll
     for (int a = 0; a < NA; ++a)
@@ -543,6 +546,7 @@ insite_refine_kernel(RefineArgs ra) {
     for (int q = 0; q < ra.n_coef; ++q) ra.coef_out[p * ra.n_coef + q] = coef_at(q);
   if (ra.status) ra.status[p] = status;
   if (ra.iters) ra.iters[p] = nit;
+  if (ra.nfev) ra.nfev[p] = ln.nev;
 }
 
 template <int NA, int D>
@@ -567,7 +571,7 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
                       int32_t n_coef, const double* coef0, const int32_t* mask, const int8_t* exps, int32_t n_arms,
                       double dt, double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail,
                       double* preds, int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out,
-                      const int32_t* row_order, void* stream) {
+                      const int32_t* row_order, void* stream, int32_t* nfev_out = nullptr) {
   const bool bits = arm8 == nullptr;
   if (n_rows < 0 || T < 1 || n_arms < 1 || n_arms > (bits ? 2 : 4) || substeps < 1 || !(dt > 0.0) ||
       !(lam >= 0.0) || tau < 0 || ld_v < n_rows || ld_p < n_rows || n_statics < 0 ||
@@ -611,6 +615,7 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
   ra.coef_out = coef_out;
   ra.status = status_out;
   ra.iters = iters_out;
+  ra.nfev = nfev_out;
   ra.order = row_order;
   ra.ldv = ld_v;
   ra.lda = ld_arm;
@@ -695,10 +700,10 @@ int32_t insite_refine_general_f64(const double* V, int64_t ld_v, int32_t T, cons
                                   const int32_t* coef_arm_mask, const int8_t* coef_exps, int32_t n_arms, double dt,
                                   double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail,
                                   double* preds, int64_t ld_p, double* coef_out, int32_t* status_out,
-                                  int32_t* iters_out, const int32_t* row_order, void* stream) {
+                                  int32_t* iters_out, int32_t* nfev_out, const int32_t* row_order, void* stream) {
   if ((arm_bits == nullptr) == (arm == nullptr) && n_rows > 0) return INSITE_E_INVALID_ARG;
   static const int8_t kNoArms = 0;  // non-null marker for the int8 format when n_rows == 0
   return refine_launch(V, ld_v, T, arm_bits, arm_bits ? nullptr : (arm ? arm : &kNoArms), ld_arm, u, seq_len, n_rows, n_statics, n_coef,
                        coef0, coef_arm_mask, coef_exps, n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds,
-                       ld_p, coef_out, status_out, iters_out, row_order, stream);
+                       ld_p, coef_out, status_out, iters_out, row_order, stream, nfev_out);
 }

@@ -828,7 +828,7 @@ def refine_terms(lib: PolyLibrary, n_coef_rows: int):
 
 def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: torch.Tensor, coef0: np.ndarray,
                   lib: PolyLibrary, dt: float, lam: float, tau: int, substeps: int = 5,
-                  revert_on_zoom_fail: bool = False, binned: bool = False):
+                  revert_on_zoom_fail: bool = False, binned: bool = False, nfev: torch.Tensor | None = None):
     """INSITE per-patient refinement (reference sindy.py:433-715).  V [N, T] f64 unscaled observations
     and arm [N, T] int8 per-step arms in the reference's patient-major layout (transposed to the
     kernel's time-major layout here), u [N, U], seq_len [N], coef0 the HOST global model [A, F].
@@ -842,6 +842,9 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
     device), so a wave's objective scans have similar lengths; scheduling only, the outputs are bitwise the
     same.  Off by default: on the time-major V the binned lanes' scattered loads cost more than the shorter
     scans save (1M rows, seq_len U{1..59}: 10.7 vs 9.5 ms, profiles/r02/v10_insite_bench.log).
+    ``nfev``: an int32 [N] device tensor receiving each row's objective/gradient evaluation count (the work
+    count behind bench.py's INSITE roofline); it routes every model through insite_refine_general_f64 (the
+    same kernels and arithmetic as the per-arm entry points).
     Returns (preds [N, T], coef [N, A, F], status [N], iterations [N])."""
     _dev("V", V, torch.float64, 2)
     _dev("arm", arm, torch.int8, 2)
@@ -862,21 +865,63 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
     Vt = V.t().contiguous()
     arm_t = arm.t().contiguous()
     arms = pack_arm_bits(arm_t, N) if A <= 2 else arm_t
-    dev = V.device
+    order = rk45_order(seq_len, T) if (binned and N > 64) else None
+    preds, coef, status, iters = insite_refine_tm(Vt, arms, u, seq_len, c0, lib, dt, lam, tau, substeps,
+                                                  revert_on_zoom_fail, order=order, nfev=nfev)
+    return preds.t(), coef, status, iters
+
+
+def insite_refine_tm(Vt: torch.Tensor, arms: torch.Tensor, u: torch.Tensor, seq_len: torch.Tensor, coef0,
+                     lib: PolyLibrary, dt: float, lam: float, tau: int, substeps: int = 5,
+                     revert_on_zoom_fail: bool = False, order: torch.Tensor | None = None,
+                     nfev: torch.Tensor | None = None):
+    """``insite_refine`` on the kernels' own time-major layout (no per-call transposes): Vt [T, >= N] f64, arms
+    the per-step arms as the bit mask int32 [T, >= ceil(N / 32)] (A <= 2, ``pack_arm_bits``) or int8 [T, >= N]
+    (A <= 4); ``order`` an optional lane -> row permutation (``rk45_order``).  Returns (preds [T, N] time-major,
+    coef [N, A, F], status [N], iterations [N])."""
+    _dev("Vt", Vt, torch.float64, 2)
+    _dev("seq_len", seq_len, torch.int32, 1)
+    N = seq_len.numel()
+    T = Vt.size(0)
+    if Vt.size(1) < N:
+        raise ValueError("Vt must be [T, >= N]")
+    c0 = np.ascontiguousarray(coef0, dtype=np.float64)
+    if c0.ndim != 2 or c0.shape[1] != lib.n_terms:
+        raise ValueError("coef0 must be a host [A, F] array")
+    mask, qexps, A = refine_terms(lib, c0.shape[0])
+    if A > 4:
+        raise ValueError("at most 4 treatment arms (joint model: 2 binary treatment inputs)")
+    if A <= 2:
+        _dev("arms", arms, torch.int32, 2)
+        if arms.size(0) < T or arms.size(1) < (N + 31) // 32:
+            raise ValueError("bit-packed arms must be [T, >= ceil(N / 32)] int32")
+    else:
+        _dev("arms", arms, torch.int8, 2)
+        if arms.size(0) < T or arms.size(1) < N:
+            raise ValueError("int8 arms must be [T, >= N]")
+    if lib.n_statics:
+        _dev("u", u, torch.float64, 2)
+        if u.size(0) != N or u.size(1) != lib.n_statics or u.stride(0) != lib.n_statics:
+            raise ValueError("u must be a contiguous [N, n_statics] tensor")
+    if nfev is not None:
+        _dev("nfev", nfev, torch.int32, 1)
+        if nfev.numel() != N:
+            raise ValueError("nfev must have one entry per row")
+    dev = Vt.device
     preds = torch.empty((T, N), dtype=torch.float64, device=dev)
     coef = torch.empty((N,) + c0.shape, dtype=torch.float64, device=dev)
     status = torch.empty((N,), dtype=torch.int32, device=dev)
     iters = torch.empty((N,), dtype=torch.int32, device=dev)
     nul = ctypes.c_void_p(0)
     ustat = _p(u) if lib.n_statics else nul
-    order = rk45_order(seq_len, T) if (binned and N > 64) else None
     tail = (c0.ctypes.data_as(ctypes.c_void_p),)
     common = (float(dt), float(lam), int(tau), int(substeps), int(bool(revert_on_zoom_fail)), _p(preds),
               preds.stride(0), _p(coef), _p(status), _p(iters), _p(order) if order is not None else nul)
-    if lib.n_inputs:
+    if lib.n_inputs or nfev is not None:
+        gcommon = common[:-1] + (_p(nfev), common[-1])
         args = (_p(Vt), Vt.stride(0), T, _p(arms) if A <= 2 else nul, _p(arms) if A > 2 else nul, arms.stride(0),
                 ustat, _p(seq_len), N, lib.n_statics, c0.size, *tail, mask.ctypes.data_as(ctypes.c_void_p),
-                qexps.ctypes.data_as(ctypes.c_void_p), A) + common
+                qexps.ctypes.data_as(ctypes.c_void_p), A) + gcommon
         _run(("insite_refine_general_f64", args, dev, None))
     else:
         tab = lib.ctypes_table()
@@ -884,7 +929,7 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
         args = (_p(Vt), Vt.stride(0), T, _p(arms), arms.stride(0), ustat, _p(seq_len), N, lib.n_statics,
                 tab.ctypes.data_as(ctypes.c_void_p), lib.n_terms, *tail, A) + common
         _run((name, args, dev, None))
-    return preds.t(), coef, status, iters
+    return preds, coef, status, iters
 
 
 def masked_sse(pred: torch.Tensor, target: torch.Tensor, active: torch.Tensor, scale: float = 1.0,
