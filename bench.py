@@ -745,8 +745,17 @@ def f4_main(args):
                    "planted_support": (np.array(F4_COEF) != 0).astype(int).tolist(),
                    "support_equals_planted": bool(np.array_equal(out[1].cpu().numpy() != 0, np.array(F4_COEF) != 0)),
                    "planted_terms_recovered": bool(np.all((out[1].cpu().numpy() != 0)[np.array(F4_COEF) != 0])),
-                   "max_abs_coef_error_vs_planted": float(np.max(np.abs(out[0].cpu().numpy() - np.array(F4_COEF))))},
-        "roofline": {"kernel": "gram_seg_kernel (order1, 4 arms) + discovery_finalize<0>", "bound": "hbm",
+                   "max_abs_coef_error_vs_planted": float(np.max(np.abs(out[0].cpu().numpy() - np.array(F4_COEF)))),
+                   "max_abs_spurious_coef": float(np.max(np.abs(np.where(np.array(F4_COEF) != 0, 0.0,
+                                                                         out[0].cpu().numpy())))),
+                   "support_note": "exact planted-support recovery is not expected at the reference's threshold "
+                                   "(0.001): with FiniteDifference(order=1) per treatment segment the backward "
+                                   "difference closing a segment is a different affine relation in x than the "
+                                   "interior forward differences, so the least-squares fit blends them into small "
+                                   "spurious terms even on noise-free data (the reference algorithm's own output: "
+                                   "tests/test_gpu_segments.py pins the GPU support to the oracle restatement)"},
+        "roofline": {"kernel": "gram_seg_kernel (order1, 4 arms; in-launch fixed-order reduction, G|b written by the "
+                               "last block)", "bound": "hbm",
                      "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic_for("f4", "gram_seg_kernel"), "algorithmic_bytes_per_launch": gb,
                      "avg_launch_ms": gram_ms},

@@ -196,6 +196,7 @@ __device__ __forceinline__ void tele_lo(const GramW& w, double vm2, double vm1, 
 #define INSITE_TAIL_RELEASE_FENCE 0
 #endif
 constexpr int kTailGroup = 16;
+constexpr int kTailMaxGroups = 64;  // group partials summed by the last reducer (counters cnt[1 .. 64])
 constexpr int kTailMaxEnt = INSITE_MAX_ARMS * (INSITE_MAX_TERMS * (INSITE_MAX_TERMS + 1) / 2 + INSITE_MAX_TERMS);
 struct GramOut {
   double* G;
@@ -224,10 +225,15 @@ __device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double
                                           unsigned* __restrict__ cnt, const LibDesc& lib, const GramOut& o,
                                           double* red) {
   int* flag = reinterpret_cast<int*>(red + kTailMaxEnt);  // "I am last", through the kernel's LDS array
-  const int ng = (nblk + kTailGroup - 1) / kTailGroup;
-  const int g = vblk / kTailGroup;
-  const int g0 = g * kTailGroup;
-  const int gs = nblk - g0 < kTailGroup ? nblk - g0 : kTailGroup;
+  // group size: kTailGroup blocks, or a multiple of it so that at most kTailMaxGroups groups remain (the
+  // segment kernel's one-tile-per-wave grids reach 8192 blocks); the group sums run in block order either way
+  const int tg = nblk <= kTailGroup * kTailMaxGroups
+                     ? kTailGroup
+                     : ((nblk + kTailMaxGroups - 1) / kTailMaxGroups + kTailGroup - 1) / kTailGroup * kTailGroup;
+  const int ng = (nblk + tg - 1) / tg;
+  const int g = vblk / tg;
+  const int g0 = g * tg;
+  const int gs = nblk - g0 < tg ? nblk - g0 : tg;
   double* gpart = part + (int64_t)nblk * n_ent;
   auto publish = [&](unsigned* counter, unsigned arrivals) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
@@ -259,12 +265,14 @@ __device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double
   };
   if (!publish(&cnt[1 + g], (unsigned)gs)) return;
   for (int q = threadIdx.x; q < n_ent; q += kBlock) {  // the group's partials, block-index order
-    double v[kTailGroup];
+    double acc = 0.0;
+    for (int j0 = 0; j0 < gs; j0 += kTailGroup) {  // kTailGroup loads in flight per round
+      double v[kTailGroup];
 #pragma unroll
-    for (int j = 0; j < kTailGroup; ++j) v[j] = part[(int64_t)(g0 + (j < gs ? j : 0)) * n_ent + q];
-    double acc = v[0];
+      for (int j = 0; j < kTailGroup; ++j) v[j] = part[(int64_t)(g0 + (j0 + j < gs ? j0 + j : 0)) * n_ent + q];
 #pragma unroll
-    for (int j = 1; j < kTailGroup; ++j) acc += j < gs ? v[j] : 0.0;
+      for (int j = 0; j < kTailGroup; ++j) acc += j0 + j < gs ? v[j] : 0.0;  // 0 + v[0] = v[0]: the old order
+    }
     tail_store(gpart + (int64_t)g * n_ent + q, acc);
   }
   if (!publish(&cnt[0], (unsigned)ng)) return;
@@ -1017,84 +1025,6 @@ stlsq_kernel(const double* __restrict__ G, const double* __restrict__ b, int64_t
 
 
 
-// Fixed-order reduction of the per-block Gram partials: one block per (arm, entry) — threads
-// strided over the partial blocks, then an LDS tree — G/b written out.  With F > 0 the block
-// that arrives last (agent-scope release/acquire around a ticket, MI355X_MICROARCH.md
-// "Workgroup dispatch ... visibility") runs one STLSQ fit per arm in the same launch
-// (SINDy.fit: reference sindy.py:190-192).  The ticket is zeroed by the preceding gram launch.
-template <int F>
-__global__ void __launch_bounds__(kBlock)
-discovery_finalize(const double* __restrict__ partial, int nblk, int narm_pad, int n_arms, LibDesc lib,
-                   double* __restrict__ G, double* __restrict__ b, StlsqParams sp,
-                   double* __restrict__ coef, int8_t* __restrict__ mask, int32_t* __restrict__ iters,
-                   unsigned* __restrict__ ticket) {
-  __shared__ double red[kBlock];
-  __shared__ int last;
-  const int a = blockIdx.x / lib.nE;
-  const int e = blockIdx.x % lib.nE;
-  INSITE_TSTAMP(49152 + blockIdx.x, 0);
-  INSITE_TREAL(49152 + blockIdx.x, 8);
-  double s = 0.0;
-  if (lib.mfma) {
-    const int off = (a * lib.F + lib.ei[e]) * 16 + lib.qcol[e];
-    for (int g = threadIdx.x; g < nblk; g += kBlock) s += partial[(int64_t)g * 256 + off];
-  } else {
-    for (int g = threadIdx.x; g < nblk; g += kBlock) s += partial[((int64_t)g * narm_pad + a) * kWave + e];
-  }
-  red[threadIdx.x] = s;
-  __syncthreads();
-#pragma unroll
-  for (int off = kBlock / 2; off > 0; off >>= 1) {
-    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
-    __syncthreads();
-  }
-  INSITE_TSTAMP(49152 + blockIdx.x, 1);
-  if (threadIdx.x == 0) {
-    const int i = lib.ei[e], k = lib.ek[e];
-    if (k >= 0) {
-      G[((int64_t)a * lib.F + i) * lib.F + k] = red[0];
-      G[((int64_t)a * lib.F + k) * lib.F + i] = red[0];
-    } else {
-      b[(int64_t)a * lib.F + i] = red[0];
-    }
-  }
-  if constexpr (F > 0) {
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = (t == gridDim.x - 1u);
-      if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    __syncthreads();
-    INSITE_TSTAMP(49152 + blockIdx.x, 2);
-    INSITE_TREAL(49152 + blockIdx.x, 9);
-    if (!last) return;
-    if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // header stays zero
-    const int arm_i = threadIdx.x;
-    if (arm_i < n_arms) {
-      double g[F][F], rhs[F], c[F];
-#pragma unroll
-      for (int ii = 0; ii < F; ++ii) {
-        rhs[ii] = __hip_atomic_load(&b[arm_i * F + ii], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int jj = 0; jj <= ii; ++jj)
-          g[ii][jj] = __hip_atomic_load(&G[(arm_i * F + ii) * F + jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      unsigned sup = 0u;
-      const int it = stlsq_solve<F>(g, rhs, sp.thr, sp.alpha, sp.max_iter, sp.unbias, c, sup);
-#pragma unroll
-      for (int i = 0; i < F; ++i) {
-        coef[arm_i * F + i] = c[i];
-        if (mask) mask[arm_i * F + i] = (int8_t)((sup >> i) & 1u);
-      }
-      if (iters) iters[arm_i] = it;
-    }
-    INSITE_TSTAMP(49152 + blockIdx.x, 3);
-    INSITE_TREAL(49152 + blockIdx.x, 9);
-  }
-}
-
 // =============================================================================================
 // Treatment-segment discovery (cancer_sim / EQ_5)
 // =============================================================================================
@@ -1112,8 +1042,8 @@ discovery_finalize(const double* __restrict__ partial, int nblk, int narm_pad, i
 // Smoothed: inside a segment xs_i = (x_i + x_{i+1}) / 2 except at its first and last sample (raw);
 // the derivative uses xs, the library the raw samples (pysindy smooths only for x_dot).
 // Per 64-patient tile the per-(patient, arm) moments are contracted to Gram entries (one entry per
-// lane, patients staged through LDS in two halves); block partials in the gram_kernel scalar layout
-// feed discovery_finalize.
+// lane, patients staged through LDS in two halves); the block partials go through the in-launch tail of
+// gram_kernel (gram_tail: fixed-order group sums, G / b and the per-arm STLSQ in the last block).
 #ifndef INSITE_SEG_KC
 #define INSITE_SEG_KC 4
 #endif
@@ -1129,16 +1059,15 @@ constexpr int kSegRS = kSegMono + 5 * INSITE_MAX_ARMS;  // LDS row: F monomials 
 #ifndef INSITE_SEG_WPE
 #define INSITE_SEG_WPE 4  // waves per SIMD the register budget is sized for (4: <= 128 VGPRs)
 #endif
-template <int NARM, bool SMOOTH1>
+template <int NARM, bool SMOOTH1, int STF>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_SEG_WPE)))
 gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const int8_t* __restrict__ arm, int64_t asp,
                 int64_t ask, const int32_t* __restrict__ seq_len, int n_steps, const double* __restrict__ u, int64_t N,
-                double inv_dt, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ ticket) {
+                double inv_dt, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ cnt, GramOut out) {
   __shared__ double smem[kWavesPerBlock * 32 * kSegRS];
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   double* ps = smem + wid * (32 * kSegRS);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0u;  // consumed by discovery_finalize (next launch)
   double acc[NARM];
 #pragma unroll
   for (int a = 0; a < NARM; ++a) acc[a] = 0.0;
@@ -1297,21 +1226,23 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
     }
     wave_lds_sync();
   }
-  // ---- block reduction (fixed order) -> partial[block][arm][entry] (gram_kernel scalar layout) ----
+  // ---- block reduction (fixed order) -> compact partial[block][a * nE + e] -> in-launch tail ----
+  // (gram_tail: group partials, then G / b and, STF > 0, the per-arm STLSQ fits in the last arriving block;
+  // replaces round 2's separate discovery_finalize launch)
   __syncthreads();
   double* red = smem;
 #pragma unroll
   for (int a = 0; a < NARM; ++a) red[(wid * NARM + a) * kWave + lane] = acc[a];
   __syncthreads();
-  if (wid == 0 && lane < lib.nE) {  // entry `lane`: fixed-order sum over waves and lane groups
-#pragma unroll
-    for (int a = 0; a < NARM; ++a) {
-      double s = 0.0;
-      for (int ww = 0; ww < kWavesPerBlock; ++ww)
-        for (int g = 0; g < ng; ++g) s += red[(ww * NARM + a) * kWave + g * lib.nE + lane];
-      partial[((int64_t)blockIdx.x * NARM + a) * kWave + lane] = s;
-    }
+  const int n_ent = out.n_arms * lib.nE;
+  for (int idx = threadIdx.x; idx < n_ent; idx += kBlock) {  // entry: fixed-order sum over waves and lane groups
+    const int a = idx / lib.nE, e = idx - a * lib.nE;
+    double sum = 0.0;
+    for (int ww = 0; ww < kWavesPerBlock; ++ww)
+      for (int g = 0; g < ng; ++g) sum += red[(ww * NARM + a) * kWave + g * lib.nE + e];
+    tail_store(partial + (int64_t)blockIdx.x * n_ent + idx, sum);
   }
+  gram_tail<STF>((int)blockIdx.x, (int)gridDim.x, partial, n_ent, cnt, lib, out, smem);
 }
 
 // Per-patient refit (LSQIntialMask per patient, pkpd_simulation.py:791-800):
@@ -1481,7 +1412,9 @@ __device__ __forceinline__ int patient_refit(const LibDesc& lib, const double* u
   return it;
 }
 
-template <int F>
+// CHOL: the masked-Cholesky STLSQ (alpha <= 0, where the closed form does not apply; also the round-2 path);
+// otherwise the closed-form refit, without the Cholesky code's registers
+template <int F, bool CHOL>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_PP_WPE)))
 patient_fit_kernel(const double* __restrict__ mom, const double* __restrict__ u, const int8_t* __restrict__ arm,
                    const int32_t* __restrict__ rows, int64_t N, int n_steps, int n_arms, LibDesc lib,
@@ -1499,14 +1432,14 @@ patient_fit_kernel(const double* __restrict__ mom, const double* __restrict__ u,
     if (iters) iters[p] = -2;
     return;
   }
-#ifndef INSITE_PP_CHOLESKY
+  if constexpr (!CHOL) {
   double uu[INSITE_MAX_STATICS];
 #pragma unroll
   for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < lib.U ? u[p * lib.U + t] : 0.0;
   const double M[3] = {mom[p * 5 + 0], mom[p * 5 + 1], mom[p * 5 + 2]};
   double c[INSITE_MAX_TERMS];
   unsigned init = 0u;
-  const int it = patient_refit<F>(lib, uu, M, mom[p * 5 + 3], mom[p * 5 + 4], L, gcoef + a * F, sp, c, init);
+  const int it = patient_refit<F, false>(lib, uu, M, mom[p * 5 + 3], mom[p * 5 + 4], L, gcoef + a * F, sp, c, init);
   unsigned fin = 0u;
 #pragma unroll
   for (int j = 0; j < F; ++j) {
@@ -1519,7 +1452,7 @@ patient_fit_kernel(const double* __restrict__ mom, const double* __restrict__ u,
     for (int j = 0; j < F; ++j) mask[p * F + j] = (int8_t)((fin >> j) & 1u);
   }
   if (iters) iters[p] = it;
-#else  // A/B: the 7 x 7 masked-Cholesky STLSQ of round 2
+  } else {
   unsigned init = 0u;
 #pragma unroll
   for (int j = 0; j < F; ++j)
@@ -1612,7 +1545,7 @@ patient_fit_kernel(const double* __restrict__ mom, const double* __restrict__ u,
     for (int j = 0; j < F; ++j) mask[p * F + j] = (int8_t)((fin >> j) & 1u);
   }
   if (iters) iters[p] = it;
-#endif
+  }
 }
 
 // =============================================================================================
@@ -1929,7 +1862,8 @@ constexpr int kRollGS = 32;  // steps per arm group
 template <int METHOD, int NARM, int PR>
 __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const LibDesc& lib, const int lane,
                                                    const int64_t tile, const int g_begin, const int g_end,
-                                                   const RefitArgs* rf = nullptr) {
+                                                   const RefitArgs rf = RefitArgs{}) {
+  // rf by value: the address of the kernel's by-value argument would put a copy of it in scratch
   constexpr bool PERROW = PR == 1;
   const int64_t p0 = tile * kWave;
   const int64_t p = p0 + lane;
@@ -1946,30 +1880,37 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
     double al[NARM], be[NARM];
     if constexpr (PR == 2) {
       double cv[NARM][INSITE_MAX_TERMS];
-      load_coef_rows<NARM>(lib, rf->gcoef, ra.A, cv);
-      const int af = rf->farm[pc];
-      int L = rf->rows[pc];
-      if (L > rf->n_steps) L = rf->n_steps;
+      load_coef_rows<NARM>(lib, rf.gcoef, ra.A, cv);
+      const int af = rf.farm[pc];
+      int L = rf.rows[pc];
+      if (L > rf.n_steps) L = rf.n_steps;
       const bool fit = act && af >= 0 && af < ra.A;
-      const double M[3] = {rf->mom[pc * 5 + 0], rf->mom[pc * 5 + 1], rf->mom[pc * 5 + 2]};
-      const double Sd = rf->mom[pc * 5 + 3], Sdx = rf->mom[pc * 5 + 4];
+      const double M[3] = {rf.mom[pc * 5 + 0], rf.mom[pc * 5 + 1], rf.mom[pc * 5 + 2]};
+      const double Sd = rf.mom[pc * 5 + 3], Sdx = rf.mom[pc * 5 + 4];
       double c[INSITE_MAX_TERMS];
       unsigned init = 0u;
-      const int it = patient_refit<INSITE_MAX_TERMS, false>(lib, uu, M, Sd, Sdx, L, rf->gcoef + (fit ? af : 0) * lib.F,
-                                                             rf->sp, c, init);
+      const int it = patient_refit<INSITE_MAX_TERMS, false>(lib, uu, M, Sd, Sdx, L, rf.gcoef + (fit ? af : 0) * lib.F,
+                                                             rf.sp, c, init);
 #pragma unroll
       for (int a = 0; a < NARM; ++a)
 #pragma unroll
         for (int j = 0; j < INSITE_MAX_TERMS; ++j) cv[a][j] = (fit && a == af) ? c[j] : cv[a][j];
-      if (act && rf->coef_out) {
-        for (int a = 0; a < ra.A; ++a)
-          for (int j = 0; j < lib.F; ++j) rf->coef_out[(p * ra.A + a) * lib.F + j] = (fit && a == af) ? c[j] : rf->gcoef[a * lib.F + j];
+      // (compile-time column loops: a run-time index into c[] would move it to scratch)
+      if (act && rf.coef_out) {
+#pragma unroll
+        for (int a = 0; a < NARM; ++a)
+#pragma unroll
+          for (int j = 0; j < INSITE_MAX_TERMS; ++j)
+            if (a < ra.A && j < lib.F)
+              rf.coef_out[(p * ra.A + a) * lib.F + j] = (fit && a == af) ? c[j] : rf.gcoef[a * lib.F + j];
       }
-      if (act && fit && rf->mask_out) {
-        for (int j = 0; j < lib.F; ++j)
-          rf->mask_out[p * lib.F + j] = (int8_t)(L < 5 ? (init >> j) & 1u : (fabs(c[j]) > 1e-14 ? 1u : 0u));
+      if (act && fit && rf.mask_out) {
+#pragma unroll
+        for (int j = 0; j < INSITE_MAX_TERMS; ++j)
+          if (j < lib.F)
+            rf.mask_out[p * lib.F + j] = (int8_t)(L < 5 ? (init >> j) & 1u : (fabs(c[j]) > 1e-14 ? 1u : 0u));
       }
-      if (act && rf->iters_out) rf->iters_out[p] = fit ? it : -2;
+      if (act && rf.iters_out) rf.iters_out[p] = fit ? it : -2;
       affine_rates_regs<NARM>(lib, cv, ra.A, ra.drop, uu, al, be);
     } else {
       affine_rates<NARM>(lib, ra.coef + (PERROW ? pc * ra.coef_stride : 0), ra.A, ra.drop, uu, al, be);
@@ -2245,7 +2186,7 @@ __global__ void __launch_bounds__(kBlock) refit_rollout_kernel(RolloutArgs ra, L
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid;
   if (tile * kWave >= ra.N) return;
-  rollout_bits_range<METHOD, NARM, 2>(ra, lib, lane, tile, 0, (ra.T + kRollGS - 1) / kRollGS, &rf);
+  rollout_bits_range<METHOD, NARM, 2>(ra, lib, lane, tile, 0, (ra.T + kRollGS - 1) / kRollGS, rf);
 }
 
 // =============================================================================================
@@ -3186,16 +3127,16 @@ inline int64_t seg_grid(int64_t N) {
   return g < 1 ? 1 : g;
 }
 
-template <int NARM, bool SMOOTH1>
+template <int NARM, bool SMOOTH1, int STF>
 int launch_gram_seg(hipStream_t st, const double* x, int64_t xsp, int64_t xsk, const int8_t* arm, int64_t asp,
                     int64_t ask, const int32_t* seq_len, int n_steps, const double* u, int64_t N, double inv_dt,
-                    const LibDesc& lib, double* part, unsigned* ticket) {
-  auto kern = gram_seg_kernel<NARM, SMOOTH1>;
+                    const LibDesc& lib, double* part, unsigned* cnt, const GramOut& out) {
+  auto kern = gram_seg_kernel<NARM, SMOOTH1, STF>;
   // one 64-patient tile per wave up to kSegMaxBlocks blocks: the dispatcher hands freed slots to the
   // next block, which balances the tail better than a resident grid striding over 5-6 tiles per wave
   const int64_t g = seg_grid(N);
   kern<<<dim3((unsigned)g), kBlock, 0, st>>>(x, xsp, xsk, arm, asp, ask, seq_len, n_steps, u, N, inv_dt, lib, part,
-                                             ticket);
+                                             cnt, out);
   return (int)g;
 }
 
@@ -3240,44 +3181,29 @@ int32_t run_segment_discovery(const double* x, int64_t ldx, const int8_t* arm, i
   const int64_t asp = tm ? 1 : ld_arm, ask = tm ? ld_arm : 1;
   const double inv_dt = 1.0 / dt;
   const bool sm = fd_kind == INSITE_FD_SMOOTHED1;
-  int grid;
-#define INSITE_SEG_LAUNCH(NA)                                                                                    \
-  grid = sm ? launch_gram_seg<NA, true>(hs, x, xsp, xsk, arm, asp, ask, seq_len, n_steps, u, n_patients, inv_dt, \
-                                        lib, part, ticket)                                                       \
-            : launch_gram_seg<NA, false>(hs, x, xsp, xsk, arm, asp, ask, seq_len, n_steps, u, n_patients, inv_dt, \
-                                         lib, part, ticket)
-  if (na == 1) INSITE_SEG_LAUNCH(1);
-  else if (na == 2) INSITE_SEG_LAUNCH(2);
-  else INSITE_SEG_LAUNCH(4);
+  // STLSQ fused into the tail for the cancer_sim / EQ_5 library (F = 4); other libraries: the tail writes G|b and
+  // one stlsq_kernel launch fits the arms
+  const bool fuse = sp.enabled && n_terms == 4;
+  const GramOut go{G_out, b_out, n_arms, coef_out, mask_out, iters_out, sp, nullptr};
+#define INSITE_SEG_LAUNCH(NA, SF)                                                                                      \
+  sm ? launch_gram_seg<NA, true, SF>(hs, x, xsp, xsk, arm, asp, ask, seq_len, n_steps, u, n_patients, inv_dt, lib, part, \
+                                     ticket, go)                                                                       \
+     : launch_gram_seg<NA, false, SF>(hs, x, xsp, xsk, arm, asp, ask, seq_len, n_steps, u, n_patients, inv_dt, lib,    \
+                                      part, ticket, go)
+  if (fuse) {
+    if (na == 1) INSITE_SEG_LAUNCH(1, 4);
+    else if (na == 2) INSITE_SEG_LAUNCH(2, 4);
+    else INSITE_SEG_LAUNCH(4, 4);
+  } else {
+    if (na == 1) INSITE_SEG_LAUNCH(1, 0);
+    else if (na == 2) INSITE_SEG_LAUNCH(2, 0);
+    else INSITE_SEG_LAUNCH(4, 0);
+  }
 #undef INSITE_SEG_LAUNCH
   st = launch_status();
-  if (st != INSITE_OK) return st;
-  const dim3 fg(n_arms * lib.nE);
-  if (!sp.enabled) {
-    discovery_finalize<0><<<fg, kBlock, 0, hs>>>(part, grid, na, n_arms, lib, G_out, b_out, sp, nullptr, nullptr,
-                                                 nullptr, ticket);
-    return launch_status();
-  }
-  switch (n_terms) {
-#define INSITE_FIN_CASE(FF)                                                                                    \
-  case FF:                                                                                                     \
-    discovery_finalize<FF><<<fg, kBlock, 0, hs>>>(part, grid, na, n_arms, lib, G_out, b_out, sp, coef_out,     \
-                                                  mask_out, iters_out, ticket);                                \
-    break;
-    INSITE_FIN_CASE(1)
-    INSITE_FIN_CASE(2)
-    INSITE_FIN_CASE(3)
-    INSITE_FIN_CASE(4)
-    INSITE_FIN_CASE(5)
-    INSITE_FIN_CASE(6)
-    INSITE_FIN_CASE(7)
-    INSITE_FIN_CASE(8)
-    INSITE_FIN_CASE(9)
-#undef INSITE_FIN_CASE
-    default:
-      return INSITE_E_UNSUPPORTED;
-  }
-  return launch_status();
+  if (st != INSITE_OK || !sp.enabled || fuse) return st;
+  return insite_stlsq_f64(G_out, b_out, n_arms, n_terms, sp.thr, sp.alpha, sp.max_iter, sp.unbias, coef_out, mask_out,
+                          iters_out, stream);
 }
 
 template <int METHOD, int NARM, bool PERROW>
@@ -3348,8 +3274,12 @@ int32_t launch_patient_fit(const double* mom, const double* u, const int8_t* arm
   switch (lib.F) {
 #define INSITE_PP_CASE(FF)                                                                                      \
   case FF:                                                                                                     \
-    patient_fit_kernel<FF><<<grid, kBlock, 0, hs>>>(mom, u, arm, rows, n_patients, n_steps, n_arms, lib,        \
-                                                    global_coef, sp, coef_out, mask_out, iters_out);           \
+    if (sp.alpha > 0.0)                                                                                        \
+      patient_fit_kernel<FF, false><<<grid, kBlock, 0, hs>>>(mom, u, arm, rows, n_patients, n_steps, n_arms, lib, \
+                                                             global_coef, sp, coef_out, mask_out, iters_out);  \
+    else                                                                                                       \
+      patient_fit_kernel<FF, true><<<grid, kBlock, 0, hs>>>(mom, u, arm, rows, n_patients, n_steps, n_arms, lib,  \
+                                                            global_coef, sp, coef_out, mask_out, iters_out);   \
     break;
     INSITE_PP_CASE(1)
     INSITE_PP_CASE(2)
@@ -3631,7 +3561,9 @@ int32_t insite_refit_rollout_moments_f64(const double* mom, const int8_t* arm, c
 size_t insite_gram_segments_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms) {
   (void)n_terms;
   if (n_patients < 0 || n_arms < 1 || n_arms > INSITE_MAX_ARMS) return 0;
-  return kGramWsHeader + (size_t)seg_grid(n_patients) * narm_pad(n_arms) * kWave * sizeof(double);
+  // block partials [grid][n_arms * nE] and <= kTailMaxGroups group partials (gram_tail), nE <= 54
+  const size_t ent = (size_t)n_arms * (INSITE_MAX_TERMS * (INSITE_MAX_TERMS + 1) / 2 + INSITE_MAX_TERMS);
+  return kGramWsHeader + ((size_t)seg_grid(n_patients) + kTailMaxGroups) * ent * sizeof(double);
 }
 
 int32_t insite_gram_segments_f64(const double* x, int64_t ldx, const int8_t* arm, int64_t ld_arm, int32_t layout,

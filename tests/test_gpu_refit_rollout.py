@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 
 def _two_call(ops, mom, u, arm, rows, T_fit, lib, coef, y0, bits, dt, T):
     pc, pm, pi = ops.fit_per_patient_moments(mom, u, arm, rows, T_fit, lib, coef, 0.1, 0.5)
-    y = ops.rollout(y0, u, bits, pc.reshape(pc.size(0), -1), lib, dt, method="euler5", T=T, layout="time_bits")
+    y = ops.rollout(y0, u, bits, pc, lib, dt, method="euler5", T=T, layout="time_bits")
     return pc, pm, pi, y
 
 
