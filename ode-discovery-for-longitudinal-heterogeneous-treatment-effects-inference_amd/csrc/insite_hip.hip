@@ -2257,6 +2257,7 @@ struct Rk45Args {
   int64_t lda, ldt, ldy, coef_stride, N;
   int32_t Tmax, A;
   double rtol, atol, drop;
+  int32_t ybuf;         // PM staging: y's byte offsets fit a buffer descriptor (< 2^31): branch-free flushes
 };
 
 // e^(-1/5) for the RK45 step-size rules (scipy rk.py: `error_norm ** error_exponent`, exponent -1/5, once
@@ -2270,7 +2271,11 @@ struct Rk45Args {
 // the fp64 range's comfort zone / the fp32 estimate would flush) take the exactly range-reduced form
 // e = m 2^(5q), m in [1, 64), on a branch no realistic controller error reaches; zero, infinite and NaN
 // inputs get pow's values (inf, 0, NaN) by select, so no pow body is inlined into the loop's registers.
+#ifndef INSITE_RK45_ROOT_BRANCH
+#define INSITE_RK45_ROOT_BRANCH 0
+#endif
 __device__ __forceinline__ double rk45_inv_root5(double e) {
+#if INSITE_RK45_ROOT_BRANCH  // A/B: round 2's exact range reduction on a (never taken) branch
   double m = e;
   int q = 0;
   if (!(e >= 0x1p-120 && e <= 0x1p120)) {
@@ -2279,6 +2284,15 @@ __device__ __forceinline__ double rk45_inv_root5(double e) {
     q = (k >= 0 ? k : k - 4) / 5;  // floor(k / 5)
     m = ldexp(e, -5 * q);
   }
+#else
+  // Branch-free: the argument is clamped to [2^-120, 2^120].  Every use of the root is bounded by its callers
+  // where the clamp bites: the step factor min(10, 0.9 x) is 10 for any e < 2^-120 (x > 2^24) and
+  // max(0.2, 0.9 x) is 0.2 for any e > 2^120, and select_initial_step's min(100 h0, x, span) keeps 100 h0
+  // (d1 > 1e34 makes h0 <= 1e-36 |y| / scale); NaN stays NaN (pow's value).  The branch cost ~10 scalar
+  // and branch instructions per attempt for every wave (round 2's SQ_INSTS_SALU / _BRANCH, profiles/r02/c5_pmc/).
+  const double m = fmin(fmax(e, 0x1p-120), 0x1p120);
+  constexpr int q = 0;
+#endif
   double x = (double)__builtin_amdgcn_exp2f(-0.2f * __builtin_amdgcn_logf((float)m));
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -2286,7 +2300,12 @@ __device__ __forceinline__ double rk45_inv_root5(double e) {
     const double r = fma(x2 * x2 * x, m, -1.0);
     x = fma(-0.2 * x, r, x);
   }
+#if INSITE_RK45_ROOT_BRANCH
   return q == 0 ? x : ldexp(x, -q);
+#else
+  (void)q;
+  return e == e ? x : e;
+#endif
 }
 
 // 1 / b for the controller's norms (b a positive normal double: atol + |y| rtol, |f| > 0): the hardware
@@ -2465,6 +2484,9 @@ rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
 #ifndef INSITE_RK45_STAGE
 #define INSITE_RK45_STAGE 1
 #endif
+#ifndef INSITE_RK45_CLOSE_BRANCH
+#define INSITE_RK45_CLOSE_BRANCH 0  // 1: round 2's close block under `if (close)` (A/B)
+#endif
 constexpr int kRkWin = INSITE_RK45_WIN;
 constexpr int kRkStage = INSITE_RK45_STAGE ? 8 : 1;
 template <int NARM, bool PERROW, bool PM>
@@ -2618,7 +2640,48 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
         y = y_new;
         f = f_new;
       }
+#if INSITE_RK45_CLOSE_BRANCH
       if (close) {  // store y at t_{k+1} (row k), open interval k + 1 from the window
+#else
+      // The interval close, branch-free except for the store: nearly every iteration some lane of the wave
+      // closes an interval, so the close work is issued for the whole wave anyway; computing the next
+      // interval's values for every lane and selecting them drops the exec-mask and branch instructions
+      // around it.  Only the output store (and its LDS staging) stays under `close`.
+      {
+        const int kn = k + (close ? 1 : 0);
+        const double t1n = tw[(kn + 1 - base) * kWave];  // k + 1 - base when not closing: the current t1 slot
+        double aln = al, ben = be;
+        if (NARM > 1) {
+          if (amask_ok) {  // uniform
+            const int an = (int)((amask >> kn) & 1ull);
+            aln = alpha[0];
+            ben = beta[0];
+#pragma unroll
+            for (int aa = 1; aa < NARM; ++aa) {
+              aln = (an == aa) ? alpha[aa] : aln;
+              ben = (an == aa) ? beta[aa] : ben;
+            }
+          } else if (close) {
+            const int kk = k;
+            k = kn;
+            rates();
+            aln = al;
+            ben = be;
+            k = kk;
+          }
+        }
+        // select_initial_step of interval kn from (t1, y): the front half, every lane
+        const double fi = fma(ben, y, aln);
+        const double spani = t1n - t1;
+        const double scale_i = atol + fabs(y) * rtol;
+        const double d1 = fabs(fi) * rk45_rcp(scale_i);
+        const bool tiny = fabs(y) < 1e-5 * scale_i || d1 < 1e-5;
+        const double h0i = fmin(tiny ? 1e-6 : 0.01 * fabs(y) * rk45_rcp(fabs(fi)), spani);
+        const double d2 = fabs(ben) * d1;
+        const bool smalli = d1 <= 1e-15 && d2 <= 1e-15;
+        const double argi = smalli ? 1.0 : fmax(d1, d2) * 100.0;
+        if (close) {
+#endif
         if constexpr (kStage) {
           // element slot within its 64-B sector; the sector goes out when its last slot arrives or the row ends
           const int slot = (int)(((uintptr_t)yp >> 3) & 7u);
@@ -2626,7 +2689,19 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
           if (slot_lo < 0) slot_lo = slot;
           if (slot == 7 || !(k + 2 < n)) {
             double* sec = yp - slot;
-            if (slot_lo == 0 && slot == 7) {
+            if (ra.ybuf) {  // uniform: the sector's staged elements [slot_lo, slot] as 8-B buffer stores, the
+                            // others to an offset the hardware drops (no per-element exec-mask branches)
+              const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+                  (void*)ra.y, (short)0, (int)(ra.N * ra.ldy * 8), 0x00020000);
+              const unsigned sb = (unsigned)((sec - ra.y) * 8);
+              double v[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] = yr[j * kWave];
+#pragma unroll
+              for (int j = 0; j < 8; ++j)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v[j]), yrs,
+                                                      (j >= slot_lo && j <= slot) ? sb + 8u * j : kOOB, 0, 0);
+            } else if (slot_lo == 0 && slot == 7) {
               double v[8];
 #pragma unroll
               for (int j = 0; j < 8; ++j) v[j] = yr[j * kWave];
@@ -2645,6 +2720,7 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
         } else {
           __builtin_nontemporal_store(y, yp);
         }
+#if INSITE_RK45_CLOSE_BRANCH
         yp += ystep;
         t = t1;
         ++k;
@@ -2653,6 +2729,22 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
         live = k + 1 < n;
         rarg = init_front();
       }
+#else
+        }
+        yp = close ? yp + ystep : yp;
+        t = close ? t1 : t;
+        k = kn;
+        t1 = close ? t1n : t1;
+        al = close ? aln : al;
+        be = close ? ben : be;
+        f = close ? fi : f;
+        span = close ? spani : span;
+        h0 = close ? h0i : h0;
+        small = close ? smalli : small;
+        rarg = close ? argi : rarg;
+        live = k + 1 < n;
+      }
+#endif
       const double r5 = rk45_inv_root5(rarg);
       double factor = err == 0.0 ? 10.0 : fmin(10.0, 0.9 * r5);
       if (rejected) factor = fmin(1.0, factor);
@@ -3782,7 +3874,8 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
   if (st != INSITE_OK) return st;
   if (coef_row_stride != 0 && coef_row_stride < (int64_t)n_arms * n_terms) return INSITE_E_INVALID_ARG;
   Rk45Args ra{y0, n_statics > 0 ? u : y0, arm_bits, t_obs, n_obs, coef, y_out, steps_out, row_order, ld_arm, ld_t, ld_y,
-              coef_row_stride, n_rows, T_max, n_arms, rtol, atol, drop_below};
+              coef_row_stride, n_rows, T_max, n_arms, rtol, atol, drop_below,
+              (pm && n_rows * ld_y * 8 < ((int64_t)1 << 31) - 64) ? 1 : 0};
   const int64_t waves = (n_rows + kWave - 1) / kWave;
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);

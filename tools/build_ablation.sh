@@ -36,6 +36,8 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     RKW8W8) NAME=$v build -DINSITE_RK45_WIN=8 -DINSITE_RK45_WPE=8 ;;
     RKW16W5) NAME=$v build -DINSITE_RK45_WIN=16 -DINSITE_RK45_WPE=5 ;;
     RKNOSTAGE) NAME=$v build -DINSITE_RK45_STAGE=0 ;;
+    RKR02) NAME=$v build -DINSITE_RK45_CLOSE_BRANCH=1 -DINSITE_RK45_ROOT_BRANCH=1 ;;
+    RKROOTBR) NAME=$v build -DINSITE_RK45_ROOT_BRANCH=1 ;;
     RKW12) NAME=$v build -DINSITE_RK45_WIN=12 ;;
     SEGKC8) NAME=$v build -DINSITE_SEG_KC=8 -DINSITE_SEG_WPE=3 ;;
     SEGKC4) NAME=$v build -DINSITE_SEG_KC=4 -DINSITE_SEG_WPE=4 ;;

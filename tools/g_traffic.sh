@@ -5,7 +5,9 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/${OUT:-traffic}
 mkdir -p $O
-for spec in ${CONFIGS:-"c2:--no-north-star" "c4:--config c4 --T 60" "c5:--config c5" "c3:--config c3" "f4:--config f4" "insite:--config insite"}; do
+# CONFIGS: ';'-separated name:bench-arguments specs
+IFS=';' read -ra SPECS <<< "${CONFIGS:-c2:--no-north-star;c4:--config c4 --T 60;c5:--config c5;c3:--config c3;f4:--config f4;insite:--config insite}"
+for spec in "${SPECS[@]}"; do
   name=${spec%%:*}; argsx=${spec#*:}
   for C in FETCH_SIZE WRITE_SIZE; do
     d=$O/pmc/$name/$( [ $C = FETCH_SIZE ] && echo fetch || echo write )
