@@ -235,6 +235,15 @@ __device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double
   const int g0 = g * tg;
   const int gs = nblk - g0 < tg ? nblk - g0 : tg;
   double* gpart = part + (int64_t)nblk * n_ent;
+#ifdef INSITE_TIMING  // the final reducer's tail phases -> g_tstamp wave 49152 (slot 0 entry, 1..6 phases, 8/9 real)
+  unsigned long long tt[7] = {__builtin_amdgcn_s_memtime(), 0, 0, 0, 0, 0, 0};
+  const unsigned long long tr0 = __builtin_amdgcn_s_memrealtime();
+#define INSITE_TT(k) tt[k] = __builtin_amdgcn_s_memtime()
+#else
+#define INSITE_TT(k) \
+  do {               \
+  } while (0)
+#endif
   auto publish = [&](unsigned* counter, unsigned arrivals) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
@@ -264,6 +273,7 @@ __device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double
     return *flag != 0;
   };
   if (!publish(&cnt[1 + g], (unsigned)gs)) return;
+  INSITE_TT(1);
   for (int q = threadIdx.x; q < n_ent; q += kBlock) {  // the group's partials, block-index order
     double acc = 0.0;
     for (int j0 = 0; j0 < gs; j0 += kTailGroup) {  // kTailGroup loads in flight per round
@@ -275,7 +285,9 @@ __device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double
     }
     tail_store(gpart + (int64_t)g * n_ent + q, acc);
   }
+  INSITE_TT(2);
   if (!publish(&cnt[0], (unsigned)ng)) return;
+  INSITE_TT(3);
   for (int q = threadIdx.x; q < n_ent; q += kBlock) {  // the group partials, group order (ng <= 64)
     double acc = 0.0;
 #pragma unroll 16
@@ -283,6 +295,7 @@ __device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double
     red[q] = acc;
   }
   __syncthreads();
+  INSITE_TT(4);
   const int64_t F = lib.F;
   double* dense = red + kTailMaxEnt + 8;  // STF: [a][F x F | F] copy in LDS for the fused STLSQ
   constexpr int kDense = STF * STF + STF;
@@ -304,6 +317,7 @@ __device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double
   }
   if constexpr (STF > 0) {  // one thread per arm, register-resident STLSQ (reference sindy.py:190-192)
     __syncthreads();
+    INSITE_TT(5);
     const int a = (int)threadIdx.x;
     if (a < o.n_arms) {
       const double* d = dense + a * kDense;
@@ -324,6 +338,16 @@ __device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double
       if (o.iters) o.iters[a] = it;
     }
   }
+#ifdef INSITE_TIMING
+  INSITE_TT(6);
+  if (threadIdx.x == 0) {
+    unsigned long long* d = g_tstamp + (int64_t)49152 * kTsSlots;
+    for (int k = 0; k < 7; ++k) d[k] = tt[k];
+    d[8] = tr0;
+    d[9] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
+#undef INSITE_TT
 }
 static_assert(kTailMaxEnt + 8 + INSITE_MAX_ARMS * (INSITE_MAX_TERMS * INSITE_MAX_TERMS + INSITE_MAX_TERMS) <=
                   kWavesPerBlock * kWave * kGSlot,
@@ -349,6 +373,18 @@ static_assert(kTailMaxEnt + 8 + INSITE_MAX_ARMS * (INSITE_MAX_TERMS * INSITE_MAX
 // The body is a device function of a virtual block index / grid size (vblk, vgrid) and the block's LDS,
 // so the fused step kernel (step_kernel) can run it on a subset of its blocks.
 constexpr int kGramSmem = kWavesPerBlock * kWave * kGSlot;  // doubles of LDS per block
+// Work item -> (64-patient tile, time segment).  0: tile-major (the segments of one tile are consecutive
+// items); 1 (A/B knob): segment-major (consecutive items are adjacent tiles of one segment, so the waves
+// resident together read neighbouring columns of the same steps).
+#ifndef INSITE_GRAM_ORDER
+#define INSITE_GRAM_ORDER 0
+#endif
+__device__ __forceinline__ int64_t gram_item_tile(int64_t item, int n_seg, int64_t n_tiles) {
+  return INSITE_GRAM_ORDER ? item % n_tiles : item / n_seg;
+}
+__device__ __forceinline__ int gram_item_seg(int64_t item, int n_seg, int64_t n_tiles) {
+  return INSITE_GRAM_ORDER ? (int)(item / n_tiles) : (int)(item - (item / n_seg) * n_seg);
+}
 template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, int MOM, int STF = 0>
 __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, double* __restrict__ smem,
             const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
@@ -388,7 +424,38 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
   const int cl = (lane % LPR) * VEC;
 
   const int64_t n_tiles = (N + kWave - 1) / kWave;
-  const int64_t n_items = n_tiles * n_seg;
+  // Work pieces (tile, owned steps [s0, sE)).  n_seg > 0: items (tile, segment) of `seg` steps, strided over the
+  // waves.  n_seg == 0 (range mode): the (tile, kGT-step group) units, tile-major, cut into one equal contiguous
+  // range per wave (as the rollout role cuts its work), a piece being the part of the range inside one tile --
+  // every wave streams the same number of steps whatever the cohort size, where items leave the waves with
+  // one item more than the others setting the end (C2 at 1,228 waves: 3,126 items = 2.55 per wave).
+  const bool ranged = n_seg == 0;
+  const int ng = (n_steps + kGT - 1) / kGT;
+  const int64_t nW = (int64_t)vgrid * kWavesPerBlock;
+  const int64_t wv = (int64_t)vblk * kWavesPerBlock + wid;
+  const int64_t units = ranged ? n_tiles * ng : n_tiles * n_seg;
+  const int64_t c_end = ranged ? (wv + 1) * units / nW : units;
+  struct Piece {
+    int64_t tile, next;
+    int s0, sE;
+  };
+  auto piece_of = [&](int64_t c) -> Piece {
+    Piece pc;
+    if (ranged) {
+      pc.tile = c / ng;
+      const int g0 = (int)(c - pc.tile * ng);
+      const int g1 = (int)min((int64_t)ng, (int64_t)g0 + (c_end - c));
+      pc.s0 = g0 * kGT;
+      pc.sE = g1 * kGT;
+      pc.next = c + (g1 - g0);
+    } else {
+      pc.tile = gram_item_tile(c, n_seg, n_tiles);
+      pc.s0 = gram_item_seg(c, n_seg, n_tiles) * seg;
+      pc.sE = pc.s0 + seg;
+      pc.next = c + nW;
+    }
+    return pc;
+  };
   // time-major register ring, live across work items: a wave with several items requests the next item's
   // first tiles as soon as the current item's last tile is consumed, so they stream in under the current
   // item's tail rows and Gram contraction (per-item start-up latency hidden; C4: ~8 items per wave)
@@ -406,22 +473,23 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
     for (int i = 0; i < kGT; ++i)
       v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, qoff + (unsigned)(i * ldx * 8), 0, 0));
   };
-  for (int64_t item = (int64_t)vblk * kWavesPerBlock + wid; item < n_items;
-       item += (int64_t)vgrid * kWavesPerBlock) {
-    const int64_t tile = item / n_seg;
-    const int sidx = (int)(item - tile * n_seg);
+  for (int64_t cur = ranged ? wv * units / nW : wv; cur < c_end;) {
+    const Piece pc = piece_of(cur);
+    cur = pc.next;
+    const int64_t tile = pc.tile;
     const int64_t p0 = tile * kWave;
     const int64_t p = p0 + lane;
     // time-major: the first kTmDepth tiles are requested before the per-patient scalars (their
     // range is clipped at the stored steps, not at this wave's longest row, which is not known yet)
-    const int s0 = sidx * seg;  // first step owned by this segment
-    const int tb = (sidx == 0) ? 0 : s0 - kWarm;
+    const int s0 = pc.s0;       // first step owned by this piece
+    const bool first = s0 == 0;  // the piece holding the head rows (and the row count) of its tile
+    const int tb = first ? 0 : s0 - kWarm;
     const int tm_valid = (int)(N - p0 < kWave ? N - p0 : kWave);
     const unsigned tm_off = p < N ? (unsigned)lane * 8u : kOOB;
     auto tm_load = [&](TmTile& v, int t0, int lim) { tm_load_for(v, t0, lim, p0, tm_valid, tm_off); };
 #ifndef INSITE_GRAM_LATE_ISSUE
     if constexpr (TM) {
-      const int s1p = min(s0 + seg, n_steps);
+      const int s1p = min(pc.sE, n_steps);
       if (!prefetched) {
 #pragma unroll
         for (int d = 0; d < kTmDepth; ++d)
@@ -451,9 +519,9 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
     }
     const int Lm = L >= kMinMain ? L : 0;  // length on the streaming path
     const int Lmax = wave_max_i(Lm);
-    const int s1 = min(s0 + seg, Lmax);      // one past the last step processed
+    const int s1 = min(pc.sE, Lmax);         // one past the last step processed
     INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 1);
-    const int e = min(Lm, s0 + seg);         // per-lane end of owned steps
+    const int e = min(Lm, pc.sE);            // per-lane end of owned steps
     const int Lmin = wave_min_i(e);
     const int bstart = max(2 * kLag, s0);    // first body step of the segment
     const bool has_body = e > bstart;        // at least one body row owned
@@ -554,7 +622,7 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
           if constexpr (SMOOTH) {
             if (i >= 4) sr[(i - 2) & 7] = sg_int(w, xr[(i - 4) & 7], xr[(i - 3) & 7], xr[(i - 2) & 7], xr[(i - 1) & 7], xr[i & 7]);
             if (i == 7) {
-              if (sidx == 0) {  // head rows kd = 0..3 from x[0..7], xs[2..5]
+              if (first) {  // head rows kd = 0..3 from x[0..7], xs[2..5]
                 const double xs0 = sg_pos0(xr[0], xr[1], xr[2], xr[3], xr[4]);
                 const double xs1 = sg_pos1(xr[0], xr[1], xr[2], xr[3], xr[4]);
                 const double d0 = fd_pos0(xs0, xs1, sr[2], sr[3], sr[4]) * w.inv_dt;
@@ -579,7 +647,7 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
             }
           } else {
             if (i == 3) tele_lo(w, xr[0], xr[1], xr[2], xr[3], loSd, loSdx);  // x[a-2..a+1], a = tb + 2
-            if (i == 4 && sidx == 0) {  // head rows kd = 0, 1 from x[0..4]
+            if (i == 4 && first) {  // head rows kd = 0, 1 from x[0..4]
               const double d0 = fd_pos0(xr[0], xr[1], xr[2], xr[3], xr[4]) * w.inv_dt;
               const double d1 = fd_pos1(xr[0], xr[1], xr[2], xr[3], xr[4]) * w.inv_dt;
               const bool on = Lm > 0;
@@ -654,14 +722,11 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
         }
 #ifndef INSITE_GRAM_NO_XPREFETCH
         {  // every tile of this item consumed: request the wave's next item's first tiles
-          const int64_t nitem = item + (int64_t)vgrid * kWavesPerBlock;
-          if (nitem < n_items) {  // uniform
-            const int64_t ntile = nitem / n_seg;
-            const int nsidx = (int)(nitem - ntile * n_seg);
-            const int64_t np0 = ntile * kWave;
-            const int ns0 = nsidx * seg;
-            const int ntb = nsidx == 0 ? 0 : ns0 - kWarm;
-            const int ns1p = min(ns0 + seg, n_steps);
+          if (cur < c_end) {  // uniform
+            const Piece np = piece_of(cur);
+            const int64_t np0 = np.tile * kWave;
+            const int ntb = np.s0 == 0 ? 0 : np.s0 - kWarm;
+            const int ns1p = min(np.sE, n_steps);
             const int nvalid = (int)(N - np0 < kWave ? N - np0 : kWave);
             const unsigned noff = np0 + lane < N ? (unsigned)lane * 8u : kOOB;
 #pragma unroll
@@ -727,7 +792,7 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
       }
     }
     if constexpr (SMOOTH) {
-      if (sidx == 0 && L > 0 && L < kMinMain) {
+      if (first && L > 0 && L < kMinMain) {
         const double* xrow = TM ? x + p : x + p * ldx;
         const int64_t st = TM ? ldx : 1;
         if (L == 5) small_trajectory<5>(xrow, st, w, Sx, Sxx, Sd, Sdx);
@@ -735,7 +800,7 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
         else small_trajectory<7>(xrow, st, w, Sx, Sxx, Sd, Sdx);
       }
     }
-    if (s0 >= Lmax && !(SMOOTH && sidx == 0)) continue;  // nothing owned by this work item (uniform)
+    if (s0 >= Lmax && !(SMOOTH && first)) continue;  // nothing owned by this work piece (uniform)
     if constexpr (MOM != 0) {  // 1: moments only (partial = the [N, 5] moments); 2: moments to out.mom + the Gram
       if (p < N) {
         double* mrow = (MOM == 1 ? partial : out.mom) + p * 5;
@@ -754,7 +819,7 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
 
     INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 4);
     // ---- per-patient Gram block A(u) M A(u)^T ----
-    const double M0 = (sidx == 0) ? (double)L : 0.0;  // row count, counted once per patient
+    const double M0 = first ? (double)L : 0.0;  // row count, counted once per patient
     const int my_arm = (L > 0) ? arm_p : -1;
     double* ps = xt;  // reuse the x tile
     if constexpr (MFMA) {
@@ -2222,6 +2287,7 @@ step_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int64_t RW = (int64_t)(gridDim.x - gblocks) * kWavesPerBlock;
   const int64_t rw = (int64_t)((int)blockIdx.x - gblocks) * kWavesPerBlock + wid;
+  INSITE_TREAL(32768 + rw, 8);
   const int ng = (ra.T + kRollGS - 1) / kRollGS;
   const int64_t units = (ra.N + kWave - 1) / kWave * ng;  // (tile, arm group) pairs, tile-major
   int64_t q = rw * units / RW;
@@ -2233,6 +2299,8 @@ step_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
     rollout_bits_range<METHOD, 2, false>(ra, lib, lane, tile, gb, ge);
     q += ge - gb;
   }
+  INSITE_TSTAMP(32768 + rw, 0);
+  INSITE_TREAL(32768 + rw, 9);
 }
 
 // =============================================================================================
@@ -2971,8 +3039,16 @@ inline int narm_pad(int n_arms) { return n_arms <= 1 ? 1 : (n_arms <= 2 ? 2 : 4)
 // gram's time segments are chosen so its (tile, segment) items spread evenly over the gram waves
 // (a wave that takes one item more than the others sets the gram's end): the segment count with the
 // smallest max/mean items per wave, a small charge per extra segment for its warm-up and contraction.
+// Range mode (INSITE_STEP_RANGED, default): the gram role cuts its (tile, 16-step group) units into one equal
+// contiguous range per wave (gram_body, n_seg = 0), so its waves end together at any block count, and the
+// default split is half the resident blocks: blocks b and b + resident/2 share a CU under the dispatcher's
+// round-robin placement, so every CU holds one gram block and one rollout block (one HBM read stream and one
+// write stream per CU; profiles/r03/ timelines).  Item mode (0, round 2) keeps the segment search below.
+#ifndef INSITE_STEP_RANGED
+#define INSITE_STEP_RANGED 1
+#endif
 #ifndef INSITE_STEP_GSHARE
-#define INSITE_STEP_GSHARE 600
+#define INSITE_STEP_GSHARE (INSITE_STEP_RANGED ? 500 : 600)
 #endif
 struct StepPlan {
   int grid, gblocks, seg, n_seg;
@@ -2986,6 +3062,11 @@ inline StepPlan step_plan(int64_t N, int64_t n_steps, int resident, int gram_blo
   if (gb > kGramMaxBlocks) gb = kGramMaxBlocks;
   pl.gblocks = gb;
   pl.grid = resident;
+  if (INSITE_STEP_RANGED) {
+    pl.seg = 0;
+    pl.n_seg = 0;
+    return pl;
+  }
   const int64_t tiles = (N + kWave - 1) / kWave;
   const int64_t T = n_steps > 0 ? n_steps : 1;
   const int64_t gw = (int64_t)gb * kWavesPerBlock;
@@ -3085,6 +3166,12 @@ struct GramLaunch {
   GramOut out;
 };
 
+// INSITE_GRAM_RANGED: the standalone time-major gram in range mode (gram_body, n_seg = 0) over one resident
+// round instead of the (tile, segment) items of gram_plan (0 = items: C2 cold gram 50.4 vs 47.6 us ranged,
+// profiles/r03/).
+#ifndef INSITE_GRAM_RANGED
+#define INSITE_GRAM_RANGED 1
+#endif
 template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, int MOM = 0, int STF = 0>
 int launch_gram4(hipStream_t st, const GramLaunch& g) {
   auto kern = gram_kernel<VEC, NARM, SMOOTH, MFMA, TM, MOM, STF>;
@@ -3098,6 +3185,14 @@ int launch_gram4(hipStream_t st, const GramLaunch& g) {
     pl.n_seg = 1;
     pl.seg = (int)((g.n_steps + kGT - 1) / kGT * kGT);
     if (pl.seg < kGT) pl.seg = kGT;
+  } else if (INSITE_GRAM_RANGED && TM) {  // equal contiguous (tile, 16-step group) ranges over one resident round
+    const int64_t units = (g.N + kWave - 1) / kWave * ((g.n_steps + kGT - 1) / kGT);
+    int64_t gb = resident_waves(kern) / kWavesPerBlock;
+    if (gb > (units + kWavesPerBlock - 1) / kWavesPerBlock) gb = (units + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (gb > kGramMaxBlocks) gb = kGramMaxBlocks;
+    pl.grid = (int)(gb < 1 ? 1 : gb);
+    pl.seg = 0;
+    pl.n_seg = 0;
   }
   kern<<<dim3(pl.grid), kBlock, 0, st>>>(g.x, g.ldx, g.n_steps, g.u, g.arm, g.rows, g.N, pl.seg, pl.n_seg, g.w,
                                           g.lib, g.part, g.cnt, g.out);

@@ -23,6 +23,13 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     MS4NC1) NAME=$v build -DINSITE_MS4_NCHUNK=1 ;;
     STLSEP) NAME=$v build -DINSITE_STLSQ_SEPARATE ;;
     STEPDEPTH3) NAME=$v build -DINSITE_TM_DEPTH=3 ;;
+    GORD1) NAME=$v build -DINSITE_GRAM_ORDER=1 ;;
+    STEPITEM) NAME=$v build -DINSITE_STEP_RANGED=0 ;;
+    GSH450) NAME=$v build -DINSITE_STEP_GSHARE=450 ;;
+    GSH550) NAME=$v build -DINSITE_STEP_GSHARE=550 ;;
+    GSH600) NAME=$v build -DINSITE_STEP_GSHARE=600 ;;
+    GRANGED) NAME=$v build -DINSITE_GRAM_RANGED=1 ;;
+    GORD1D3) NAME=$v build -DINSITE_GRAM_ORDER=1 -DINSITE_TM_DEPTH=3 ;;
     GT8D4) NAME=$v build -DINSITE_GT=8 -DINSITE_TM_DEPTH=4 ;;
     GNOCOMP) NAME=$v build -DINSITE_ABLATE_GRAM_NOCOMPUTE ;;
     STAGEWISE) NAME=$v build -DINSITE_ROLLOUT_STAGEWISE ;;
