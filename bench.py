@@ -48,9 +48,10 @@ def parse():
     ap.add_argument("--arm-format", default="bits", choices=["bits", "int8"],
                     help="per-step arms of the time-major rollout: 1-bit mask (A <= 2) or int8")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", default=None, choices=["fused", "graph", "seq", "pipeline"],
-                    help="fused (default at N = 1): ONE step_kernel launch per step -- the discovery of step i and "
-                         "the rollout of step i-1 in the same launch; pipeline (default at N > 1, where the RCCL "
+    ap.add_argument("--mode", default=None, choices=["deferred", "fused", "graph", "seq", "pipeline"],
+                    help="deferred (default at N = 1) / fused: ONE launch per step -- the discovery of step i and "
+                         "the rollout of step i-1 in the same launch; deferred: the same with the discovery's "
+                         "reduction + STLSQ moved into the next launch (step_deferred_kernel); pipeline (default at N > 1, where the RCCL "
                          "all-reduce sits between the gram and STLSQ): discovery | rollout on two streams, "
                          "consecutive steps overlapped; seq: eager launches on one stream; graph: the seq step in a "
                          "HIP graph")
@@ -1109,6 +1110,70 @@ def fused_run(args, dev, coh, arm_cf, coh2=None, arm_cf2=None):
             "frac": (rb + gb) / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
 
 
+def deferred_run(args, dev, coh, arm_cf, coh2=None, arm_cf2=None):
+    """Time the deferred fused step (insite_fit_rollout_deferred_f64: step_deferred_kernel).  One launch per
+    step: the gram streaming of cohort k % 2 into partial slot k % 2, the finalisation (reduction + STLSQ) of
+    the previous step's cohort by one block, and the rollout of cohort k % 2 with the coefficients finalised
+    in step k - 1 (its discovery two steps earlier: three coefficient buffers, k % 3).  K timed launches = K
+    gram passes + K finalisations + K rollouts; nothing in a launch waits on anything else in it.  Two cohorts
+    alternate (coh2; --no-rotate: one), so consecutive reads of one cohort's x are 320 MB of traffic apart."""
+    from insite_amd import ops
+    N, T = args.patients, args.T
+    lib = coh.lib
+    F = lib.n_terms
+    f64 = torch.float64
+    cohs = [coh, coh2 if coh2 is not None else coh]
+    arms = [arm_cf, arm_cf2 if coh2 is not None else arm_cf]
+    outs = [(torch.zeros((2, F), dtype=f64, device=dev), torch.zeros((2, F), dtype=torch.int8, device=dev),
+             torch.zeros((2,), dtype=torch.int32, device=dev), torch.zeros((2, F, F), dtype=f64, device=dev),
+             torch.zeros((2, F), dtype=f64, device=dev)) for _ in range(3)]
+    y1 = torch.empty((T, N), dtype=f64, device=dev)
+    ys = [y1, torch.empty((T, N), dtype=f64, device=dev) if coh2 is not None else y1]
+    # steps 0 and 1 roll cohorts 0 and 1 out with coefficients from before the stream: plain discoveries
+    for j, c in ((1, cohs[0]), (2, cohs[1])):
+        ops.sindy_fit(c.x, c.u, c.arm, c.rows, c.dt, lib, 0.1, 0.5, out=outs[j], layout="time")
+    ws = ops.Workspace()
+
+    def plan(k, finalize):   # step k: gram of cohort k % 2 -> slot k % 2; finalise -> outs[(k-1) % 3]; roll k % 2
+        c, r = cohs[k % 2], cohs[k % 2]
+        return ops.plan_fit_rollout_deferred(c.x, c.u, c.arm, c.rows, c.dt, lib, 0.1, 0.5, r.y0, r.u, arms[k % 2],
+                                             outs[(k - 2) % 3][0], r.dt, k % 2, finalize, ws, method=args.method,
+                                             T=T, y_out=ys[k % 2], out=outs[(k - 1) % 3],
+                                             gram_blocks=args.gram_blocks)
+    st = torch.cuda.current_stream(dev)
+    plan(0, False)(st)                         # the stream's first call has nothing to finalise
+    fast = [plan(k, True).bind(st) for k in range(6)]   # then a cycle of 6 (slot k % 2, buffers k % 3)
+    pos = [1]
+
+    def run_steps(n):
+        for _ in range(n):
+            fast[pos[0] % 6]()
+            pos[0] += 1
+
+    run_steps(args.warmup)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run_steps(args.steps)
+    host_ms = (time.perf_counter() - t0) / args.steps * 1e3
+    torch.cuda.synchronize(dev)
+    ms_step = (time.perf_counter() - t0) / args.steps * 1e3
+    last = pos[0] - 1                          # the last step finalised cohort (last - 1) % 2 into outs[(last-1) % 3]
+    hip = HipEvents()
+    KB, NBAT = max(args.steps, 10), 3
+    tevs = [(hip.create(timing=True), hip.create(timing=True)) for _ in range(NBAT)]
+    for e0, e1 in tevs:
+        hip.record(e0, st.cuda_stream)
+        run_steps(KB)
+        hip.record(e1, st.cuda_stream)
+    torch.cuda.synchronize(dev)
+    step_ms = float(np.mean([hip.elapsed_ms(e0, e1) for e0, e1 in tevs])) / KB
+    rb, gb = rollout_bytes(N, T, arm_bits=1), gram_bytes(N, T)
+    fin = outs[(last - 1) % 3]
+    return {"ms_step": ms_step, "host_ms": host_ms, "step_ms": step_ms, "KB": KB, "NBAT": NBAT,
+            "coef": fin[0], "mask": fin[1], "y": ys[last % 2], "rb": rb, "gb": gb, "rotated": coh2 is not None,
+            "frac": (rb + gb) / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+
+
 def c2_fused(args, dev, coh, arm_cf, cpu):
     """C2 at N = 1 with one step_kernel launch per step (--mode fused); see fused_run.  Two cohorts rotate
     (a second seed) unless --no-rotate."""
@@ -1120,7 +1185,8 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
     if not args.no_rotate:
         coh2 = cohort.synthetic_pkpd(N, T, seed=args.seed * 1000 + 500, device=dev, equation="EQ_4_C", layout="time")
         arm_cf2 = cohort.counterfactual_arms(coh2.arm, T, seed=args.seed * 1000 + 500, layout="time_bits")
-    fr = fused_run(args, dev, coh, arm_cf, coh2, arm_cf2)
+    deferred = args.mode == "deferred"
+    fr = (deferred_run if deferred else fused_run)(args, dev, coh, arm_cf, coh2, arm_cf2)
     ms_step, host_ms, step_ms, KB, NBAT = fr["ms_step"], fr["host_ms"], fr["step_ms"], fr["KB"], fr["NBAT"]
     y = fr["y"]
     st = torch.cuda.current_stream(dev)
@@ -1167,13 +1233,15 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
             "workload": f"C2: PK/PD {N // 1000}k patients/GPU x {T} steps fp64 - discovery (savgol+FD4+poly2 "
                         f"library+Gram, STLSQ) + {args.method.upper()} counterfactual rollout",
             "patients_per_gpu": N, "T": T, "rows_per_patient": T - 2, "library_terms": F,
-            "parallelism": "patient-shard x1", "mode": "fused", "gram_blocks": args.gram_blocks or "default",
+            "parallelism": "patient-shard x1", "mode": args.mode, "gram_blocks": args.gram_blocks or "default",
             "discovered_support": sup.tolist(), "finite": ok,
             "cohorts_rotated": 2 if fr["rotated"] else 1,
         },
         "host_submit_ms_per_step": host_ms,
         "roofline": {
-            "kernel": f"step_kernel (discovery: gram + in-launch reduction + STLSQ | {args.method} bit-arm rollout)",
+            "kernel": (f"step_deferred_kernel (gram streaming | finalisation of the previous step's gram: reduction + "
+                       f"STLSQ | {args.method} bit-arm rollout)") if deferred else
+                      f"step_kernel (discovery: gram + in-launch reduction + STLSQ | {args.method} bit-arm rollout)",
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
@@ -1184,11 +1252,15 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
             "algorithmic_bytes_split": {"discovery_x_read": gb, "rollout_y_written": rb},
             "avg_launch_ms": step_ms,
             "avg_ms_source": f"HIP timing events on the launch stream around {NBAT} batches of {KB} back-to-back "
-                             "step_kernel launches, divided by the batch size (one launch = one step)",
+                             f"{'step_deferred_kernel' if deferred else 'step_kernel'} launches, divided by the batch "
+                             "size (one launch = one step)",
             "layout": "time-major x[T,N] read, 1-bit arm mask [T,N/32], y[T,N] written",
         },
-        "timed_region": "one step_kernel launch per step on one stream: discovery of step i | rollout of step i-1 "
-                        "(two coefficient buffers); no events or cross-stream waits inside the timed region",
+        "timed_region": ("one step_deferred_kernel launch per step on one stream: gram of cohort i | finalisation "
+                         "(block reduction + STLSQ) of cohort i-1 | rollout with the coefficients of cohort i-2 (three "
+                         "coefficient buffers); no events or cross-stream waits inside the timed region") if deferred
+                        else "one step_kernel launch per step on one stream: discovery of step i | rollout of step "
+                             "i-1 (two coefficient buffers); no events or cross-stream waits inside the timed region",
         "step_aggregate": {"algorithmic_bytes": rb + gb, "achieved_GBps": (rb + gb) / (ms_step * 1e-3) / 1e9,
                            "frac": (rb + gb) / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS},
         "pipeline_alternative": "bench.py --mode pipeline: gram | rollout on two streams (the N > 1 schedule); "
@@ -1276,12 +1348,12 @@ def main():
     lib = coh.lib
     F = lib.n_terms
     y0 = coh.y0
-    if args.mode is None:   # N = 1: one fused launch per step; N > 1: the all-reduce splits the step -> pipeline
-        args.mode = "fused" if world == 1 else "pipeline"
-    if args.mode == "fused" and world > 1:
-        raise SystemExit("--mode fused is single-GPU (the all-reduce sits between the gram and STLSQ): "
+    if args.mode is None:   # N = 1: one deferred fused launch per step; N > 1: the all-reduce splits the step
+        args.mode = "deferred" if world == 1 else "pipeline"
+    if args.mode in ("fused", "deferred") and world > 1:
+        raise SystemExit(f"--mode {args.mode} is single-GPU (the all-reduce sits between the gram and STLSQ): "
                          "use --mode pipeline at N > 1")
-    if args.mode == "fused":
+    if args.mode in ("fused", "deferred"):
         return c2_fused(args, dev, coh, arm_cf, cpu)
     # per-step state in NB buffers: the discovery of step i writes coefs[i % NB] while older rollouts may
     # still read theirs (G|b and the gram workspace are only touched by the discovery stream, in order,

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define INSITE_ABI_VERSION 5
+#define INSITE_ABI_VERSION 6
 
 /* status codes */
 #define INSITE_OK 0
@@ -159,6 +159,31 @@ int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, co
                                int64_t n_rows, int32_t T, double rdt, int32_t method, int32_t substeps,
                                double drop_below, double* y_out, int64_t ld_y, int32_t gram_blocks, void* workspace,
                                size_t workspace_bytes, void* stream);
+
+/* The fused step with the discovery's finalisation deferred by one call (ABI 6; the C2 bench's N = 1 schedule).
+ * In insite_fit_rollout_f64 the discovery's last block reduces every block's partial and solves the STLSQ after
+ * all other blocks have streamed -- a serial tail the launch cannot end before.  Here call k streams cohort k's
+ * Gram into workspace partial slot `slot` (0 or 1) only; with finalize_prev = 1 one block of the same launch
+ * reduces the partials the previous call left in slot 1 - slot and writes THAT cohort's G_out, b_out, coef_out,
+ * mask_out, iters_out (insite_sindy_fit_f64 semantics, the same fixed-order sums as insite_fit_rollout_f64 with
+ * the same gram_blocks); the rollout half is that of insite_fit_rollout_f64 (y_out bitwise).  A stream: call k
+ * uses slot k % 2, finalize_prev = (k > 0), and rolls out with the coefficients call k - 1 produced (cohort
+ * k - 2); a last call with n_patients = 0, n_rows = 0 and finalize_prev = 1 finalises the stream's last
+ * cohort.  Consecutive calls on one workspace must pass the same gram_blocks (0 = the default split).  Same
+ * shape restrictions as insite_fit_rollout_f64.  Workspace: insite_fit_rollout_deferred_workspace_bytes (two
+ * slots; the header need not be zero: this entry uses no counters). */
+size_t insite_fit_rollout_deferred_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms);
+int32_t insite_fit_rollout_deferred_f64(const double* x, int64_t ldx, int32_t n_steps, const double* u,
+                                        const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics,
+                                        int32_t n_arms, const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
+                                        double threshold, double alpha, int32_t max_iter, int32_t unbias,
+                                        double* G_out, double* b_out, double* coef_out, int8_t* mask_out,
+                                        int32_t* iters_out, const double* y0, const double* ru,
+                                        const uint32_t* arm_bits, int64_t ld_arm, const double* coef_in,
+                                        int64_t n_rows, int32_t T, double rdt, int32_t method, int32_t substeps,
+                                        double drop_below, double* y_out, int64_t ld_y, int32_t gram_blocks,
+                                        int32_t slot, int32_t finalize_prev, void* workspace, size_t workspace_bytes,
+                                        void* stream);
 
 /* Treatment-segment discovery for the cancer_sim / EQ_5 datasets, replacing
  * process_sindy_training_data's segment split (libs_m/ct/src/data/pkpd/utils.py:433-462, 607-637)

@@ -220,6 +220,53 @@ __device__ __forceinline__ void tail_store(double* p, double v) {  // sc1 (write
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The tail's last stage, shared by gram_tail and the deferred finalisation (deferred_finalize): red[0, n_ent)
+// holds the reduced Gram entries; write G (both triangles) and b, and with STF > 0 solve the n_arms STLSQ fits.
+template <int STF>
+__device__ __forceinline__ void tail_finish(double* red, int n_ent, const LibDesc& lib, const GramOut& o) {
+  const int64_t F = lib.F;
+  double* dense = red + kTailMaxEnt + 8;  // STF: [a][F x F | F] copy in LDS for the fused STLSQ
+  constexpr int kDense = STF * STF + STF;
+  for (int idx = threadIdx.x; idx < n_ent; idx += kBlock) {
+    const int a = idx / lib.nE, e = idx - a * lib.nE;
+    const int i = lib.ei[e], k = lib.ek[e];
+    const double v = red[idx];
+    if (k >= 0) {
+      o.G[(a * F + i) * F + k] = v;
+      o.G[(a * F + k) * F + i] = v;
+      if constexpr (STF > 0) {
+        dense[a * kDense + i * STF + k] = v;
+        dense[a * kDense + k * STF + i] = v;
+      }
+    } else {
+      o.b[a * F + i] = v;
+      if constexpr (STF > 0) dense[a * kDense + STF * STF + i] = v;
+    }
+  }
+  if constexpr (STF > 0) {  // one thread per arm, register-resident STLSQ (reference sindy.py:190-192)
+    __syncthreads();
+    const int a = (int)threadIdx.x;
+    if (a < o.n_arms) {
+      const double* d = dense + a * kDense;
+      double g[STF][STF], rhs[STF], c[STF];
+#pragma unroll
+      for (int i = 0; i < STF; ++i) {
+        rhs[i] = d[STF * STF + i];
+#pragma unroll
+        for (int j = 0; j <= i; ++j) g[i][j] = d[i * STF + j];
+      }
+      unsigned sup = 0u;
+      const int it = stlsq_solve<STF>(g, rhs, o.sp.thr, o.sp.alpha, o.sp.max_iter, o.sp.unbias, c, sup);
+#pragma unroll
+      for (int i = 0; i < STF; ++i) {
+        o.coef[a * STF + i] = c[i];
+        if (o.mask) o.mask[a * STF + i] = (int8_t)((sup >> i) & 1u);
+      }
+      if (o.iters) o.iters[a] = it;
+    }
+  }
+}
+
 template <int STF>
 __device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double* __restrict__ part, int n_ent,
                                           unsigned* __restrict__ cnt, const LibDesc& lib, const GramOut& o,
@@ -296,48 +343,7 @@ __device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double
   }
   __syncthreads();
   INSITE_TT(4);
-  const int64_t F = lib.F;
-  double* dense = red + kTailMaxEnt + 8;  // STF: [a][F x F | F] copy in LDS for the fused STLSQ
-  constexpr int kDense = STF * STF + STF;
-  for (int idx = threadIdx.x; idx < n_ent; idx += kBlock) {
-    const int a = idx / lib.nE, e = idx - a * lib.nE;
-    const int i = lib.ei[e], k = lib.ek[e];
-    const double v = red[idx];
-    if (k >= 0) {
-      o.G[(a * F + i) * F + k] = v;
-      o.G[(a * F + k) * F + i] = v;
-      if constexpr (STF > 0) {
-        dense[a * kDense + i * STF + k] = v;
-        dense[a * kDense + k * STF + i] = v;
-      }
-    } else {
-      o.b[a * F + i] = v;
-      if constexpr (STF > 0) dense[a * kDense + STF * STF + i] = v;
-    }
-  }
-  if constexpr (STF > 0) {  // one thread per arm, register-resident STLSQ (reference sindy.py:190-192)
-    __syncthreads();
-    INSITE_TT(5);
-    const int a = (int)threadIdx.x;
-    if (a < o.n_arms) {
-      const double* d = dense + a * kDense;
-      double g[STF][STF], rhs[STF], c[STF];
-#pragma unroll
-      for (int i = 0; i < STF; ++i) {
-        rhs[i] = d[STF * STF + i];
-#pragma unroll
-        for (int j = 0; j <= i; ++j) g[i][j] = d[i * STF + j];
-      }
-      unsigned sup = 0u;
-      const int it = stlsq_solve<STF>(g, rhs, o.sp.thr, o.sp.alpha, o.sp.max_iter, o.sp.unbias, c, sup);
-#pragma unroll
-      for (int i = 0; i < STF; ++i) {
-        o.coef[a * STF + i] = c[i];
-        if (o.mask) o.mask[a * STF + i] = (int8_t)((sup >> i) & 1u);
-      }
-      if (o.iters) o.iters[a] = it;
-    }
-  }
+  tail_finish<STF>(red, n_ent, lib, o);
 #ifdef INSITE_TIMING
   INSITE_TT(6);
   if (threadIdx.x == 0) {
@@ -349,6 +355,46 @@ __device__ __forceinline__ void gram_tail(const int vblk, const int nblk, double
 #endif
 #undef INSITE_TT
 }
+// Deferred finalisation (step_deferred_kernel): one block reduces the nblk block partials a PREVIOUS launch
+// left in `part` and finishes them (G|b, STLSQ) with tail_finish.  Same association as gram_tail (each group of
+// tg blocks summed in block order from 0, then the groups in order), so G|b are bitwise those of the in-launch
+// tail over the same partials; the (group, entry) sums run on all the block's threads, kTailGroup loads in
+// flight each.  The partials were written by the previous kernel on this stream: visible after its end.
+template <int STF>
+__device__ void deferred_finalize(const double* __restrict__ part, const int nblk, const int n_ent, const LibDesc& lib,
+                                  const GramOut& o, double* red) {
+  constexpr int kOff = kTailMaxEnt + 8 + INSITE_MAX_ARMS * (INSITE_MAX_TERMS * INSITE_MAX_TERMS + INSITE_MAX_TERMS);
+  // groups of kTailGroup blocks as in gram_tail, coarser (a multiple of it) when their sums would not fit the LDS
+  const int maxg = min(kTailMaxGroups, (kWavesPerBlock * kWave * kGSlot - kOff) / (n_ent > 0 ? n_ent : 1));
+  const int tg = nblk <= kTailGroup * maxg ? kTailGroup
+                                           : ((nblk + maxg - 1) / maxg + kTailGroup - 1) / kTailGroup * kTailGroup;
+  const int ng = (nblk + tg - 1) / tg;
+  double* gsum = red + kOff;  // [ng][n_ent] group sums, after tail_finish's scratch
+  for (int pi = threadIdx.x; pi < ng * n_ent; pi += kBlock) {
+    const int g = pi / n_ent, q = pi - g * n_ent;
+    const int g0 = g * tg, gs = nblk - g0 < tg ? nblk - g0 : tg;
+    double acc = 0.0;
+    for (int j0 = 0; j0 < gs; j0 += kTailGroup) {
+      double v[kTailGroup];
+#pragma unroll
+      for (int j = 0; j < kTailGroup; ++j) v[j] = part[(int64_t)(g0 + (j0 + j < gs ? j0 + j : 0)) * n_ent + q];
+#pragma unroll
+      for (int j = 0; j < kTailGroup; ++j) acc += j0 + j < gs ? v[j] : 0.0;
+    }
+    gsum[pi] = acc;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < n_ent; q += kBlock) {
+    double acc = 0.0;
+    for (int g = 0; g < ng; ++g) acc += gsum[g * n_ent + q];
+    red[q] = acc;
+  }
+  __syncthreads();
+  tail_finish<STF>(red, n_ent, lib, o);
+}
+static_assert(kTailMaxEnt + 8 + INSITE_MAX_ARMS * (INSITE_MAX_TERMS * INSITE_MAX_TERMS + INSITE_MAX_TERMS) +
+                      kTailMaxEnt <= kWavesPerBlock * kWave * kGSlot,
+              "deferred_finalize holds at least one group's sums in the gram kernel's LDS array");
 static_assert(kTailMaxEnt + 8 + INSITE_MAX_ARMS * (INSITE_MAX_TERMS * INSITE_MAX_TERMS + INSITE_MAX_TERMS) <=
                   kWavesPerBlock * kWave * kGSlot,
               "tail scratch fits the gram kernel's LDS array");
@@ -909,7 +955,7 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
     tail_store(partial + (int64_t)vblk * n_ent + idx, v);
   }
   INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 6);
-  gram_tail<STF>(vblk, vgrid, partial, n_ent, cnt, lib, out, smem);
+  if (cnt) gram_tail<STF>(vblk, vgrid, partial, n_ent, cnt, lib, out, smem);  // null: the deferred step's partials
   INSITE_TREAL(blockIdx.x * kWavesPerBlock + wid, 9);
 }
 
@@ -2268,6 +2314,24 @@ __global__ void __launch_bounds__(kBlock) refit_rollout_kernel(RolloutArgs ra, L
 // so every stored state is bitwise that of the standalone rollout.  Results do not depend on gblocks
 // except through the gram's block count (the fixed-order reduction's association, as for gram_kernel's
 // grid).  Replaces, per step, the gram + rollout launch pair on two streams and the events between them.
+//
+// Serial mode (gblocks == gridDim.x; INSITE_STEP_SERIAL, default): EVERY wave runs its gram range first and
+// then rollout work, so the chip reads x with all its waves, then writes y with all of them (no read/write
+// mix inside the HBM stream), and the gram's serial tail -- the last block's reduction and STLSQ, ~15 us
+// after the last gram wave in the split schedule (profiles/r03/ timelines) -- overlaps the other waves'
+// rollout.  The rollout work is a static part (the first INSITE_STEP_DYN_STATIC per mille of the units,
+// equal contiguous ranges per wave) and a dynamic remainder of INSITE_STEP_DYN_CHUNK-unit chunks claimed
+// with an agent-scope counter, so waves that leave the gram late (the tail block, slow CUs) take fewer
+// chunks.  The claim order does not reach the results: every chunk is a rollout_bits_range (bitwise the
+// standalone rollout).  Counters rc[0] (claims) / rc[1] (waves done claiming) sit in the workspace header;
+// the last wave done resets both, so a launch leaves them zero (the header invariant).
+#ifndef INSITE_STEP_DYN_STATIC
+#define INSITE_STEP_DYN_STATIC 500
+#endif
+#ifndef INSITE_STEP_DYN_CHUNK
+#define INSITE_STEP_DYN_CHUNK 2
+#endif
+constexpr int kStepRcnt = 96;  // rc = cnt + kStepRcnt (the gram tail uses cnt[0 .. 64])
 #ifndef INSITE_STEP_WPE
 #define INSITE_STEP_WPE 2  // waves per SIMD the step kernel's register budget is sized for
 #endif
@@ -2278,6 +2342,53 @@ step_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
             GramW w, LibDesc lib, double* __restrict__ partial, unsigned* __restrict__ cnt, GramOut out,
             RolloutArgs ra, int gblocks) {
   __shared__ double smem[kGramSmem];
+  if (gblocks == (int)gridDim.x) {  // serial mode: gram range, then rollout (static part + claimed chunks)
+    gram_body<1, 2, SMOOTH, true, true, 0, 7>((int)blockIdx.x, gblocks, smem, x, ldx, n_steps, u, arm, rows, N,
+                                                 seg, n_seg, w, lib, partial, cnt, out);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t RW = (int64_t)gridDim.x * kWavesPerBlock;
+    const int64_t rw = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+    INSITE_TREAL(32768 + rw, 8);
+    const int ng = (ra.T + kRollGS - 1) / kRollGS;
+    const int64_t units = (ra.N + kWave - 1) / kWave * ng;  // (tile, arm group) pairs, tile-major
+    auto run_units = [&](int64_t q, const int64_t q1) {
+      while (q < q1) {
+        const int64_t tile = q / ng;
+        const int gb = (int)(q - tile * ng);
+        const int ge = q1 - q < (int64_t)(ng - gb) ? gb + (int)(q1 - q) : ng;
+        rollout_bits_range<METHOD, 2, false>(ra, lib, lane, tile, gb, ge);
+        q += ge - gb;
+      }
+    };
+    const int64_t S = units * INSITE_STEP_DYN_STATIC / 1000;
+    run_units(rw * S / RW, (rw + 1) * S / RW);
+    unsigned* rc = cnt + kStepRcnt;
+    const int64_t n_chunks = (units - S + INSITE_STEP_DYN_CHUNK - 1) / INSITE_STEP_DYN_CHUNK;
+    auto claim = [&]() -> unsigned {  // lane 0 holds the claimed chunk index (read when it is needed)
+      unsigned v = 0u;
+      if (lane == 0) v = __hip_atomic_fetch_add(rc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return v;
+    };
+    unsigned nxt = claim();
+    for (;;) {
+      const int64_t c = (int64_t)__builtin_amdgcn_readfirstlane(nxt);
+      if (c >= n_chunks) break;
+      nxt = claim();  // in flight while this chunk is stored
+      const int64_t q = S + c * INSITE_STEP_DYN_CHUNK;
+      run_units(q, q + INSITE_STEP_DYN_CHUNK < units ? q + INSITE_STEP_DYN_CHUNK : units);
+    }
+    if (lane == 0) {  // done claiming; the last wave resets both counters for the next launch
+      const unsigned t = __hip_atomic_fetch_add(rc + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == (unsigned)RW - 1u) {
+        __hip_atomic_store(rc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(rc + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    INSITE_TSTAMP(32768 + rw, 0);
+    INSITE_TREAL(32768 + rw, 9);
+    return;
+  }
   if ((int)blockIdx.x < gblocks) {
     gram_body<1, 2, SMOOTH, true, true, 0, 7>((int)blockIdx.x, gblocks, smem, x, ldx, n_steps, u, arm, rows, N,
                                                  seg, n_seg, w, lib, partial, cnt, out);
@@ -2287,6 +2398,54 @@ step_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int64_t RW = (int64_t)(gridDim.x - gblocks) * kWavesPerBlock;
   const int64_t rw = (int64_t)((int)blockIdx.x - gblocks) * kWavesPerBlock + wid;
+  INSITE_TREAL(32768 + rw, 8);
+  const int ng = (ra.T + kRollGS - 1) / kRollGS;
+  const int64_t units = (ra.N + kWave - 1) / kWave * ng;  // (tile, arm group) pairs, tile-major
+  int64_t q = rw * units / RW;
+  const int64_t q1 = (rw + 1) * units / RW;
+  while (q < q1) {
+    const int64_t tile = q / ng;
+    const int gb = (int)(q - tile * ng);
+    const int ge = q1 - q < (int64_t)(ng - gb) ? gb + (int)(q1 - q) : ng;
+    rollout_bits_range<METHOD, 2, false>(ra, lib, lane, tile, gb, ge);
+    q += ge - gb;
+  }
+  INSITE_TSTAMP(32768 + rw, 0);
+  INSITE_TREAL(32768 + rw, 9);
+}
+
+// The fused step with the discovery's finalisation deferred to the next launch (insite_fit_rollout_deferred_f64).
+// In step_kernel the last gram block's reduction and STLSQ run after every other gram wave has ended (14 us of a
+// 75 us C2 step in the phase timelines, profiles/r03/): the launch cannot end before that serial tail.  Here the
+// gram blocks [0, gblocks) only stream cohort k and leave their compact partials in `part_cur`; block gblocks
+// reduces the partials the PREVIOUS launch left in `part_prev` (cohort k-1: G|b, STLSQ -> coefficients) while
+// the others stream; the remaining blocks roll out a cohort with coefficients finalised one launch earlier
+// still (cohort k-2 in a stream).  Nothing in the launch waits on anything else in it: no counters, no tail.
+template <bool SMOOTH, int METHOD>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_STEP_WPE)))
+step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
+                     const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, GramW w, LibDesc lib,
+                     double* __restrict__ part_cur, const double* __restrict__ part_prev, GramOut out, RolloutArgs ra,
+                     int gblocks) {
+  __shared__ double smem[kGramSmem];
+  if ((int)blockIdx.x < gblocks) {
+    gram_body<1, 2, SMOOTH, true, true, 0, 7>((int)blockIdx.x, gblocks, smem, x, ldx, n_steps, u, arm, rows, N, 0, 0,
+                                                 w, lib, part_cur, nullptr, out);
+    return;
+  }
+  if ((int)blockIdx.x == gblocks) {
+    if (part_prev) {
+      INSITE_TREAL(49152, 8);
+      deferred_finalize<7>(part_prev, gblocks, out.n_arms * lib.nE, lib, out, smem);
+      INSITE_TREAL(49152, 9);
+      INSITE_TSTAMP(49152, 0);
+    }
+    return;
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t RW = (int64_t)(gridDim.x - gblocks - 1) * kWavesPerBlock;
+  const int64_t rw = (int64_t)((int)blockIdx.x - gblocks - 1) * kWavesPerBlock + wid;
   INSITE_TREAL(32768 + rw, 8);
   const int ng = (ra.T + kRollGS - 1) / kRollGS;
   const int64_t units = (ra.N + kWave - 1) / kWave * ng;  // (tile, arm group) pairs, tile-major
@@ -3047,6 +3206,9 @@ inline int narm_pad(int n_arms) { return n_arms <= 1 ? 1 : (n_arms <= 2 ? 2 : 4)
 #ifndef INSITE_STEP_RANGED
 #define INSITE_STEP_RANGED 1
 #endif
+#ifndef INSITE_STEP_SERIAL
+#define INSITE_STEP_SERIAL 0  // 1: every block runs its gram range, then rollout work (step_kernel serial mode)
+#endif
 #ifndef INSITE_STEP_GSHARE
 #define INSITE_STEP_GSHARE (INSITE_STEP_RANGED ? 500 : 600)
 #endif
@@ -3065,6 +3227,7 @@ inline StepPlan step_plan(int64_t N, int64_t n_steps, int resident, int gram_blo
   if (INSITE_STEP_RANGED) {
     pl.seg = 0;
     pl.n_seg = 0;
+    if (INSITE_STEP_SERIAL && gram_blocks <= 0 && resident <= kGramMaxBlocks) pl.gblocks = pl.grid;  // serial mode
     return pl;
   }
   const int64_t tiles = (N + kWave - 1) / kWave;
@@ -3142,6 +3305,8 @@ inline GramPlan gram_plan(int64_t N, int64_t n_steps, int resident) {
 
 constexpr size_t kGramWsHeader = 512;  // counters: gram_tail cnt[0..64] / finalize ticket (+ padding; one memset block)
 static_assert((1 + (kGramMaxBlocks + kTailGroup - 1) / kTailGroup) * sizeof(unsigned) <= kGramWsHeader, "counters");
+static_assert(1 + (kGramMaxBlocks + kTailGroup - 1) / kTailGroup <= kStepRcnt && (kStepRcnt + 2) * sizeof(unsigned) <= kGramWsHeader,
+              "step kernel claim counters sit in the header, clear of the gram tail's");
 
 inline int sse_grid(int64_t n_rows) {
   int64_t g = (n_rows + 63) / 64;
@@ -3574,7 +3739,9 @@ int32_t insite_gram_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_
                        dt, G_out, b_out, workspace, workspace_bytes, stream, sp, nullptr, nullptr, nullptr);
 }
 
-int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, const double* u, const int8_t* arm,
+// insite_fit_rollout_f64 (deferred = 0) and insite_fit_rollout_deferred_f64 (deferred = 1: partial slot `slot`,
+// finalise the other slot when finalize_prev).
+static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, const double* u, const int8_t* arm,
                                const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
                                const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt, double threshold,
                                double alpha, int32_t max_iter, int32_t unbias, double* G_out, double* b_out,
@@ -3582,7 +3749,7 @@ int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, co
                                const double* ru, const uint32_t* arm_bits, int64_t ld_arm, const double* coef_in,
                                int64_t n_rows, int32_t T, double rdt, int32_t method, int32_t substeps,
                                double drop_below, double* y_out, int64_t ld_y, int32_t gram_blocks, void* workspace,
-                               size_t workspace_bytes, void* stream) {
+                               size_t workspace_bytes, void* stream, int deferred, int32_t slot, int32_t finalize_prev) {
   // ---- discovery half: insite_sindy_fit_f64's checks, restricted to the fused kernel's shape ----
   if (n_patients < 0 || !G_out || !b_out || !coef_out || n_arms != 2 || ldx < 1 || !(dt > 0.0) || n_steps < 0 ||
       ldx < n_patients || max_iter < 0 || !(threshold >= 0.0) || !(alpha >= 0.0))
@@ -3598,8 +3765,9 @@ int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, co
     for (int j = 0; j < n_terms; ++j)
       if (exps[j * (1 + n_statics)] > INSITE_MAX_STATE_DEGREE) return INSITE_E_UNSUPPORTED;
   }
-  if (!workspace || workspace_bytes < insite_gram_workspace_bytes(n_patients, n_arms, n_terms))
-    return INSITE_E_WORKSPACE;
+  const size_t ws_one = insite_gram_workspace_bytes(n_patients, n_arms, n_terms);
+  if (!workspace || workspace_bytes < (deferred ? 2 : 1) * ws_one) return INSITE_E_WORKSPACE;
+  if (deferred && (slot < 0 || slot > 1 || finalize_prev < 0 || finalize_prev > 1)) return INSITE_E_INVALID_ARG;
   if (ldx > ((int64_t)1 << 31) / (8 * kGT)) return INSITE_E_UNSUPPORTED;
   // ---- rollout half: insite_rollout_f64's checks for TIME_MAJOR_BITS, shared library ----
   if (n_rows < 0 || T < 0 || substeps < 1 || !(rdt >= 0.0) || ld_arm < (n_rows + 31) / 32 || ld_y < n_rows)
@@ -3631,11 +3799,36 @@ int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, co
   unsigned* cnt = static_cast<unsigned*>(workspace);
   double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + kGramWsHeader);
   const bool smooth = fd_kind == INSITE_FD_SMOOTHED4;
+  if (n_statics == 0) u = x ? x : G_out;
+  if (deferred) {
+    auto kd = smooth ? (method == INSITE_METHOD_RK4 ? step_deferred_kernel<true, INSITE_METHOD_RK4>
+                                                    : step_deferred_kernel<true, INSITE_METHOD_EULER>)
+                     : (method == INSITE_METHOD_RK4 ? step_deferred_kernel<false, INSITE_METHOD_RK4>
+                                                    : step_deferred_kernel<false, INSITE_METHOD_EULER>);
+    int grid = resident_waves(kd) / kWavesPerBlock;
+    if (grid < 3) grid = 3;
+    // half the resident blocks stream the gram (blocks b and b + grid/2 share a CU), one finalises, the rest roll out
+    int gb = gram_blocks > 0 ? gram_blocks : grid / 2;
+    if (gb > grid - 2) gb = grid - 2;
+    if (gb > kGramMaxBlocks) gb = kGramMaxBlocks;
+    char* wsb = static_cast<char*>(workspace);
+    double* part_cur = reinterpret_cast<double*>(wsb + (size_t)slot * ws_one + kGramWsHeader);
+    const double* part_prev =
+        finalize_prev ? reinterpret_cast<const double*>(wsb + (size_t)(1 - slot) * ws_one + kGramWsHeader) : nullptr;
+    if (n_patients == 0) {  // the gram blocks leave zero partials
+      x = G_out;
+      arm = reinterpret_cast<const int8_t*>(G_out);
+      rows = reinterpret_cast<const int32_t*>(G_out);
+      u = G_out;
+    }
+    kd<<<dim3(grid), kBlock, 0, hs>>>(x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, part_cur,
+                                      part_prev, go, ra, gb);
+    return launch_status();
+  }
   // (a two-patients-per-lane rollout role with 16-B stores measured slower: 46 vs 37 us rollout-only)
   auto kern = smooth ? (method == INSITE_METHOD_RK4 ? step_kernel<true, INSITE_METHOD_RK4> : step_kernel<true, INSITE_METHOD_EULER>)
                      : (method == INSITE_METHOD_RK4 ? step_kernel<false, INSITE_METHOD_RK4> : step_kernel<false, INSITE_METHOD_EULER>);
   const StepPlan pl = step_plan(n_patients, n_steps, resident_waves(kern) / kWavesPerBlock, gram_blocks);
-  if (n_statics == 0) u = x ? x : G_out;
   if (n_patients == 0) {  // G = b = 0 and the fit of the zero system, through the same tail
     x = G_out;
     arm = reinterpret_cast<const int8_t*>(G_out);
@@ -3645,6 +3838,43 @@ int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, co
   kern<<<dim3(pl.grid), kBlock, 0, hs>>>(x, ldx, n_steps, u, arm, rows, n_patients, pl.seg, pl.n_seg,
                                         make_gram_w(dt), lib, part, cnt, go, ra, pl.gblocks);
   return launch_status();
+}
+
+int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, const double* u, const int8_t* arm,
+                               const int32_t* rows, int64_t n_patients, int32_t n_statics, int32_t n_arms,
+                               const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt, double threshold,
+                               double alpha, int32_t max_iter, int32_t unbias, double* G_out, double* b_out,
+                               double* coef_out, int8_t* mask_out, int32_t* iters_out, const double* y0,
+                               const double* ru, const uint32_t* arm_bits, int64_t ld_arm, const double* coef_in,
+                               int64_t n_rows, int32_t T, double rdt, int32_t method, int32_t substeps,
+                               double drop_below, double* y_out, int64_t ld_y, int32_t gram_blocks, void* workspace,
+                               size_t workspace_bytes, void* stream) {
+  return run_fit_rollout(x, ldx, n_steps, u, arm, rows, n_patients, n_statics, n_arms, exps, n_terms, fd_kind, dt,
+                         threshold, alpha, max_iter, unbias, G_out, b_out, coef_out, mask_out, iters_out, y0, ru,
+                         arm_bits, ld_arm, coef_in, n_rows, T, rdt, method, substeps, drop_below, y_out, ld_y,
+                         gram_blocks, workspace, workspace_bytes, stream, 0, 0, 0);
+}
+
+size_t insite_fit_rollout_deferred_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms) {
+  const size_t one = insite_gram_workspace_bytes(n_patients, n_arms, n_terms);
+  return one ? 2 * one : 0;
+}
+
+int32_t insite_fit_rollout_deferred_f64(const double* x, int64_t ldx, int32_t n_steps, const double* u,
+                                        const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics,
+                                        int32_t n_arms, const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
+                                        double threshold, double alpha, int32_t max_iter, int32_t unbias,
+                                        double* G_out, double* b_out, double* coef_out, int8_t* mask_out,
+                                        int32_t* iters_out, const double* y0, const double* ru,
+                                        const uint32_t* arm_bits, int64_t ld_arm, const double* coef_in,
+                                        int64_t n_rows, int32_t T, double rdt, int32_t method, int32_t substeps,
+                                        double drop_below, double* y_out, int64_t ld_y, int32_t gram_blocks,
+                                        int32_t slot, int32_t finalize_prev, void* workspace, size_t workspace_bytes,
+                                        void* stream) {
+  return run_fit_rollout(x, ldx, n_steps, u, arm, rows, n_patients, n_statics, n_arms, exps, n_terms, fd_kind, dt,
+                         threshold, alpha, max_iter, unbias, G_out, b_out, coef_out, mask_out, iters_out, y0, ru,
+                         arm_bits, ld_arm, coef_in, n_rows, T, rdt, method, substeps, drop_below, y_out, ld_y,
+                         gram_blocks, workspace, workspace_bytes, stream, 1, slot, finalize_prev);
 }
 
 int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,

@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(LIB_DIR, "libinsite_hip.so")
 if os.environ.get("INSITE_LIB_OVERRIDE"):
     LIB_PATH = os.environ["INSITE_LIB_OVERRIDE"]
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # status codes / enums (insite_hip.h)
 INSITE_OK = 0
@@ -38,6 +38,8 @@ EXPORTS = (
     "insite_gram_f64",
     "insite_sindy_fit_f64",
     "insite_fit_rollout_f64",
+    "insite_fit_rollout_deferred_workspace_bytes",
+    "insite_fit_rollout_deferred_f64",
     "insite_gram_segments_workspace_bytes",
     "insite_gram_segments_f64",
     "insite_sindy_fit_segments_f64",
@@ -101,6 +103,12 @@ _SIGNATURES = {
                                         _c_i32, _c_f64, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp,
                                         _vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_f64, _c_i32, _c_i32, _c_f64,
                                         _vp, _c_i64, _c_i32, _vp, _c_size, _vp]),
+    "insite_fit_rollout_deferred_workspace_bytes": (_c_size, [_c_i64, _c_i32, _c_i32]),
+    "insite_fit_rollout_deferred_f64": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp,
+                                                 _c_i32, _c_i32, _c_f64, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp,
+                                                 _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_f64, _c_i32,
+                                                 _c_i32, _c_f64, _vp, _c_i64, _c_i32, _c_i32, _c_i32, _vp, _c_size,
+                                                 _vp]),
     "insite_gram_segments_workspace_bytes": (_c_size, [_c_i64, _c_i32, _c_i32]),
     "insite_gram_segments_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i64, _c_i32, _c_i32,
                                           _vp, _c_i32, _c_i32, _c_f64, _vp, _vp, _vp, _c_size, _vp]),

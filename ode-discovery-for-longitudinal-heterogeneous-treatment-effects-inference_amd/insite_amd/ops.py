@@ -719,6 +719,45 @@ def plan_fit_rollout(x, u, arm, rows, dt, lib, threshold, alpha, y0, ru, arm_bit
     return Plan(name, args, dev, out, keep)
 
 
+def _prep_fit_rollout_deferred(x, u, arm, rows, dt, lib, threshold, alpha, max_iter, unbias, fd, workspace, out,
+                               y0, ru, arm_bits, coef_in, rdt, method, substeps, drop_below, T, y_out, gram_blocks,
+                               slot, finalize_prev):
+    if workspace is None:
+        raise ValueError("the deferred step keeps its partial slots between calls: pass the stream's Workspace")
+    if slot not in (0, 1):
+        raise ValueError("slot must be 0 or 1")
+    name, args, dev, outs, keep = _prep_fit_rollout(x, u, arm, rows, dt, lib, threshold, alpha, max_iter, unbias, fd,
+                                                    None, out, y0, ru, arm_bits, coef_in, rdt, method, substeps,
+                                                    drop_below, T, y_out, gram_blocks)
+    nbytes = _lib.load().insite_fit_rollout_deferred_workspace_bytes(int(args[6]), 2, lib.n_terms)
+    ws = workspace.claim("deferred").get(nbytes, dev)
+    args = args[:-2] + (int(slot), int(bool(finalize_prev)), _p(ws), ws.numel())
+    return "insite_fit_rollout_deferred_f64", args, dev, outs, keep + (ws,)
+
+
+def fit_rollout_deferred(x, u, arm, rows, dt, lib, threshold, alpha, y0, ru, arm_bits, coef_in, rdt, slot,
+                         finalize_prev, workspace, method="rk4", max_iter=100, unbias=True, fd="smoothed4",
+                         substeps=None, drop_below=1e-3, T=None, out=None, y_out=None, gram_blocks=0):
+    """The fused step with the discovery's finalisation deferred by one call (insite_fit_rollout_deferred_f64):
+    streams the Gram of cohort (x, u, arm, rows) into partial slot ``slot`` of ``workspace`` (a Workspace kept
+    for the whole stream of calls), and -- with ``finalize_prev`` -- reduces the other slot (the previous
+    call's cohort) into ``out`` = (coef, mask, iters, G, b), all in the launch that rolls out (y0, ru,
+    arm_bits) with coef_in.  Returns ((coef, mask, iters, G, b), y); the first tuple holds the PREVIOUS
+    call's cohort (untouched without ``finalize_prev``)."""
+    return _run(_prep_fit_rollout_deferred(x, u, arm, rows, dt, lib, threshold, alpha, max_iter, unbias, fd,
+                                           workspace, out, y0, ru, arm_bits, coef_in, rdt, method, substeps,
+                                           drop_below, T, y_out, gram_blocks, slot, finalize_prev))
+
+
+def plan_fit_rollout_deferred(x, u, arm, rows, dt, lib, threshold, alpha, y0, ru, arm_bits, coef_in, rdt, slot,
+                              finalize_prev, workspace, method="rk4", max_iter=100, unbias=True, fd="smoothed4",
+                              substeps=None, drop_below=1e-3, T=None, out=None, y_out=None, gram_blocks=0) -> Plan:
+    """``fit_rollout_deferred`` as a prepared launch."""
+    return Plan(*_prep_fit_rollout_deferred(x, u, arm, rows, dt, lib, threshold, alpha, max_iter, unbias, fd,
+                                            workspace, out, y0, ru, arm_bits, coef_in, rdt, method, substeps,
+                                            drop_below, T, y_out, gram_blocks, slot, finalize_prev))
+
+
 def rk45_order(n_obs: torch.Tensor, T_max: int, out: torch.Tensor | None = None) -> torch.Tensor:
     """Lane order for ``rollout_rk45``: rows sorted by n_obs, descending (insite_rk45_order_i32, a
     counting sort on the device).  Scheduling only: the rollout's outputs do not depend on it."""

@@ -124,3 +124,66 @@ def test_fused_refuses_unsupported_shapes(dev):
     with pytest.raises(_lib.InsiteError):
         ops.fit_rollout(disc.x, u1, disc.arm, disc.rows, disc.dt, lib1, 0.1, 0.5, rc.y0, rc.u[:, :1].contiguous(),
                         bits, torch.zeros((2, lib1.n_terms), dtype=torch.float64, device=dev), rc.dt)
+
+
+@pytest.mark.parametrize("N,T,Nr,Tr,gblocks", [
+    (100_000, 200, 100_000, 200, 0),
+    (3_001, 60, 5_003, 37, 0),
+    (64, 20, 65, 33, 7),
+])
+def test_deferred_stream_matches_separate_calls(dev, N, T, Nr, Tr, gblocks):
+    """insite_fit_rollout_deferred_f64 over a stream of three cohorts plus the flush call: call k streams cohort
+    k's Gram into slot k % 2 and finalises cohort k - 1 (coef / mask / iters / G / b equal to insite_sindy_fit_f64
+    -- G|b bitwise those of insite_fit_rollout_f64 with the same gram_blocks, whose tail sums the same partials in
+    the same order); every call's y bitwise insite_rollout_f64's.  The oracle checks the small cohorts' fits."""
+    from insite_amd import cohort, ops
+    lib = None
+    discs = []
+    for k in range(3):
+        d = cohort.synthetic_pkpd(N, T, seed=11 + k, device=dev, equation="EQ_4_C", layout="time")
+        if N <= 5_000:
+            g = torch.Generator(device=dev)
+            g.manual_seed(N + k)
+            d.rows = torch.randint(0, T - 1, (N,), generator=g, device=dev, dtype=torch.int32)
+        discs.append(d)
+        lib = d.lib
+    _, rc, bits = _cohorts(dev, 64, T, Nr, Tr, seed=21)
+    F = lib.n_terms
+    cin = _coef_in(dev, F)
+    ws = ops.Workspace()
+    f64 = torch.float64
+    outs = [(torch.zeros((2, F), dtype=f64, device=dev), torch.zeros((2, F), dtype=torch.int8, device=dev),
+             torch.zeros((2,), dtype=torch.int32, device=dev), torch.zeros((2, F, F), dtype=f64, device=dev),
+             torch.zeros((2, F), dtype=f64, device=dev)) for _ in range(3)]
+    y_ref = ops.rollout(rc.y0, rc.u, bits, cin, lib, rc.dt, method="rk4", T=Tr, layout="time_bits")
+    for k in range(4):   # k = 3: the flush (no cohort streamed, no rollout), finalising cohort 2
+        d = discs[min(k, 2)]
+        n = N if k < 3 else 0
+        (_, _, _, _, _), y = ops.fit_rollout_deferred(
+            d.x[:, :n] if n else d.x[:, :0], d.u[:n], d.arm[:n], d.rows[:n], d.dt, lib, 0.1, 0.5,
+            rc.y0 if k < 3 else rc.y0[:0], rc.u if k < 3 else rc.u[:0], bits, cin, rc.dt, k % 2, k > 0, ws,
+            method="rk4", T=Tr, out=outs[k - 1] if k > 0 else outs[2], gram_blocks=gblocks)
+        if k < 3:
+            torch.cuda.synchronize()
+            assert torch.equal(y, y_ref), f"call {k}: deferred rollout differs from insite_rollout_f64"
+    torch.cuda.synchronize()
+    for k in range(3):
+        d = discs[k]
+        coef, mask, iters, G, b = outs[k]
+        (c1, m1, _, G1, b1), _ = ops.fit_rollout(d.x, d.u, d.arm, d.rows, d.dt, lib, 0.1, 0.5, rc.y0, rc.u, bits,
+                                                 cin, rc.dt, method="rk4", gram_blocks=gblocks, T=Tr)
+        c2, m2, _, G2, b2 = ops.sindy_fit(d.x, d.u, d.arm, d.rows, d.dt, lib, 0.1, 0.5, layout="time")
+        torch.cuda.synchronize()
+        assert torch.equal(G, G1) and torch.equal(b, b1), f"cohort {k}: deferred G|b differ from the in-launch tail"
+        assert torch.equal(coef, c1) and torch.equal(mask, m1)
+        np.testing.assert_allclose(G.cpu().numpy(), G2.cpu().numpy(), rtol=1e-12, atol=1e-9)
+        assert torch.equal(mask, m2)
+        assert (coef - c2).abs().max().item() < 1e-10
+        if N <= 5_000:
+            x = d.x[:, :N].t().contiguous().cpu().numpy()
+            Gr, br = R.gram_moments(x, d.u.cpu().numpy(), d.arm.cpu().numpy().astype(np.int64),
+                                    d.rows.cpu().numpy(), d.dt, lib.exps.astype(np.int64))
+            np.testing.assert_allclose(G.cpu().numpy(), Gr, rtol=1e-10, atol=1e-8)
+            cr = np.stack([R.stlsq_gram(Gr[a], br[a], 0.1, 0.5)[0] for a in range(2)])
+            assert np.array_equal(mask.cpu().numpy() != 0, cr != 0)
+            assert np.max(np.abs(coef.cpu().numpy() - cr)) < 1e-8

@@ -25,6 +25,13 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     STEPDEPTH3) NAME=$v build -DINSITE_TM_DEPTH=3 ;;
     GORD1) NAME=$v build -DINSITE_GRAM_ORDER=1 ;;
     STEPITEM) NAME=$v build -DINSITE_STEP_RANGED=0 ;;
+    STEPSPLIT) NAME=$v build -DINSITE_STEP_SERIAL=0 ;;
+    DYN0) NAME=$v build -DINSITE_STEP_DYN_STATIC=0 ;;
+    DYN250) NAME=$v build -DINSITE_STEP_DYN_STATIC=250 ;;
+    DYN750) NAME=$v build -DINSITE_STEP_DYN_STATIC=750 ;;
+    DYN1000) NAME=$v build -DINSITE_STEP_DYN_STATIC=1000 ;;
+    DCH1) NAME=$v build -DINSITE_STEP_DYN_CHUNK=1 ;;
+    DCH4) NAME=$v build -DINSITE_STEP_DYN_CHUNK=4 ;;
     GSH450) NAME=$v build -DINSITE_STEP_GSHARE=450 ;;
     GSH550) NAME=$v build -DINSITE_STEP_GSHARE=550 ;;
     GSH600) NAME=$v build -DINSITE_STEP_GSHARE=600 ;;

@@ -9,7 +9,8 @@ import torch
 from insite_amd import ops, cohort
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--op", default="gram", choices=["gram", "sindy_fit", "rollout", "stlsq", "step", "gram_seg", "fused"])
+ap.add_argument("--op", default="gram", choices=["gram", "sindy_fit", "rollout", "stlsq", "step", "gram_seg", "fused",
+                                                "deferred"])
 ap.add_argument("--patients", type=int, default=100_000)
 ap.add_argument("--T", type=int, default=200)
 ap.add_argument("--iters", type=int, default=50)
@@ -43,9 +44,19 @@ if a.op == "gram_seg":   # F4: 4-arm treatment-segment Gram, time-major (bench.p
 if a.op == "fused":   # the fused step kernel (insite_fit_rollout_f64): discovery of coh | bit-arm rollout of coh
     fplan = ops.plan_fit_rollout(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, coh.y0, coh.u, arm_cf, coef,
                                  coh.dt, method=a.method, T=a.T, y_out=y, out=step_out, workspace=ws)
+if a.op == "deferred":   # the deferred fused step (insite_fit_rollout_deferred_f64), slots alternating
+    dws = ops.Workspace()
+    dplans = [ops.plan_fit_rollout_deferred(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, coh.y0, coh.u,
+                                            arm_cf, coef, coh.dt, j, True, dws, method=a.method, T=a.T, y_out=y,
+                                            out=step_out) for j in range(2)]
+    dpos = [0]
 def run():
     if a.op == "fused":
         fplan()
+        return
+    if a.op == "deferred":
+        dplans[dpos[0] % 2]()
+        dpos[0] += 1
         return
     if a.op == "gram_seg":
         ops.gram_segments(seg.x, seg.arm, seg.seq_len, seg.u, seg.dt, seg.lib, 4, "order1", ws, layout="time")
