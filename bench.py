@@ -1266,8 +1266,9 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
         "pipeline_alternative": "bench.py --mode pipeline: gram | rollout on two streams (the N > 1 schedule); "
                                 "within a few % of this line, ahead over long runs (profiles/r02/fused_sweep/)",
     }
-    t3 = traffic_for("c2", "step_kernel") if fr["rotated"] and args.patients == 100_000 and args.T == 200 else None
-    out["roofline"]["traffic"] = t3 if t3 is not None else step_traffic(args)
+    t3 = (traffic_for("c2", "step_deferred_kernel" if deferred else "step_kernel")
+          if fr["rotated"] and args.patients == 100_000 and args.T == 200 else None)
+    out["roofline"]["traffic"] = t3 if (t3 is not None or deferred) else step_traffic(args)
     if iso is not None:
         out["isolated"] = dict(iso, discovery_frac=gb / (iso["discovery_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                                rollout_frac=rb / (iso["rollout_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS)
