@@ -59,6 +59,8 @@ def parse():
                     help="pipeline mode, N = 1: run each step's STLSQ in the gram's last block on the discovery "
                          "stream (default) or as its own launch on the rollout stream ahead of that step's rollout "
                          "(off the discovery stream's critical path)")
+    ap.add_argument("--dstreams", type=int, default=1,
+                    help="deferred mode: independent streams of cohorts, launch k on stream k %% S (1 = one stream)")
     ap.add_argument("--pipe-k", type=int, default=4, help="pipeline: steps per batch (one event per batch per stream)")
     ap.add_argument("--pipe-rs", type=int, default=2, help="pipeline: rollout streams taking alternate batches")
     ap.add_argument("--fused-graph", action="store_true",
@@ -1112,43 +1114,61 @@ def fused_run(args, dev, coh, arm_cf, coh2=None, arm_cf2=None):
 
 def deferred_run(args, dev, coh, arm_cf, coh2=None, arm_cf2=None):
     """Time the deferred fused step (insite_fit_rollout_deferred_f64: step_deferred_kernel).  One launch per
-    step: the gram streaming of cohort k % 2 into partial slot k % 2, the finalisation (reduction + STLSQ) of
-    the previous step's cohort by one block, and the rollout of cohort k % 2 with the coefficients finalised
-    in step k - 1 (its discovery two steps earlier: three coefficient buffers, k % 3).  K timed launches = K
-    gram passes + K finalisations + K rollouts; nothing in a launch waits on anything else in it.  Two cohorts
-    alternate (coh2; --no-rotate: one), so consecutive reads of one cohort's x are 320 MB of traffic apart."""
-    from insite_amd import ops
+    step: the gram streaming of a cohort into a partial slot, the finalisation (reduction + STLSQ) of the
+    previous launch's cohort by one block, and the rollout of a cohort with coefficients finalised one launch
+    earlier still (three coefficient buffers); nothing in a launch waits on anything else in it.
+    --dstreams S (default 1): S independent deferred streams of cohorts, launch k on stream k % S, each with
+    its own workspace, slots and buffers -- a launch depends only on the previous launch of its own stream, so
+    the next stream's launch fills the CU slots the current one's last waves leave idle (the end of every
+    launch is a 48-73 us spread of wave finish times, profiles/r03/v16_timing_deferred.jsonl).  Two cohorts
+    per stream alternate (one per stream with --no-rotate), so no launch re-reads x that is still resident."""
+    from insite_amd import ops, cohort
     N, T = args.patients, args.T
     lib = coh.lib
     F = lib.n_terms
     f64 = torch.float64
-    cohs = [coh, coh2 if coh2 is not None else coh]
-    arms = [arm_cf, arm_cf2 if coh2 is not None else arm_cf]
-    outs = [(torch.zeros((2, F), dtype=f64, device=dev), torch.zeros((2, F), dtype=torch.int8, device=dev),
-             torch.zeros((2,), dtype=torch.int32, device=dev), torch.zeros((2, F, F), dtype=f64, device=dev),
-             torch.zeros((2, F), dtype=f64, device=dev)) for _ in range(3)]
-    y1 = torch.empty((T, N), dtype=f64, device=dev)
-    ys = [y1, torch.empty((T, N), dtype=f64, device=dev) if coh2 is not None else y1]
-    # steps 0 and 1 roll cohorts 0 and 1 out with coefficients from before the stream: plain discoveries
-    for j, c in ((1, cohs[0]), (2, cohs[1])):
-        ops.sindy_fit(c.x, c.u, c.arm, c.rows, c.dt, lib, 0.1, 0.5, out=outs[j], layout="time")
-    ws = ops.Workspace()
+    S = max(1, args.dstreams)
+    pool = [(coh, arm_cf)] + ([(coh2, arm_cf2)] if coh2 is not None else [])
+    need = 2 * S if coh2 is not None else S
+    while len(pool) < need:   # more cohorts for the extra streams (distinct seeds)
+        sd = args.seed * 1000 + 700 + len(pool)
+        c = cohort.synthetic_pkpd(N, T, seed=sd, device=dev, equation="EQ_4_C", layout="time")
+        pool.append((c, cohort.counterfactual_arms(c.arm, T, seed=sd, layout="time_bits")))
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    lanes = []   # per stream: (its cohorts, outs ring, ys, workspace)
+    for si in range(S):
+        mine = pool[si::S]
+        outs = [(torch.zeros((2, F), dtype=f64, device=dev), torch.zeros((2, F), dtype=torch.int8, device=dev),
+                 torch.zeros((2,), dtype=torch.int32, device=dev), torch.zeros((2, F, F), dtype=f64, device=dev),
+                 torch.zeros((2, F), dtype=f64, device=dev)) for _ in range(3)]
+        ys = [torch.empty((T, N), dtype=f64, device=dev) for _ in mine]
+        # the stream's steps 0 and 1 roll out with coefficients from before the stream: plain discoveries
+        for j in (1, 2):
+            c = mine[(j - 1) % len(mine)][0]
+            ops.sindy_fit(c.x, c.u, c.arm, c.rows, c.dt, lib, 0.1, 0.5, out=outs[j], layout="time")
+        lanes.append((mine, outs, ys, ops.Workspace()))
+    torch.cuda.synchronize(dev)
 
-    def plan(k, finalize):   # step k: gram of cohort k % 2 -> slot k % 2; finalise -> outs[(k-1) % 3]; roll k % 2
-        c, r = cohs[k % 2], cohs[k % 2]
-        return ops.plan_fit_rollout_deferred(c.x, c.u, c.arm, c.rows, c.dt, lib, 0.1, 0.5, r.y0, r.u, arms[k % 2],
-                                             outs[(k - 2) % 3][0], r.dt, k % 2, finalize, ws, method=args.method,
-                                             T=T, y_out=ys[k % 2], out=outs[(k - 1) % 3],
+    def plan(si, k, finalize):   # stream si's step k: gram of its cohort k % m -> slot k % 2; finalise the
+        mine, outs, ys, ws = lanes[si]   # previous step's cohort -> outs[(k-1) % 3]; roll cohort k % m out
+        m = len(mine)
+        c, a = mine[k % m]
+        return ops.plan_fit_rollout_deferred(c.x, c.u, c.arm, c.rows, c.dt, lib, 0.1, 0.5, c.y0, c.u, a,
+                                             outs[(k - 2) % 3][0], c.dt, k % 2, finalize, ws, method=args.method,
+                                             T=T, y_out=ys[k % m], out=outs[(k - 1) % 3],
                                              gram_blocks=args.gram_blocks)
-    st = torch.cuda.current_stream(dev)
-    plan(0, False)(st)                         # the stream's first call has nothing to finalise
-    fast = [plan(k, True).bind(st) for k in range(6)]   # then a cycle of 6 (slot k % 2, buffers k % 3)
-    pos = [1]
+    for si in range(S):          # each stream's first call has nothing to finalise
+        plan(si, 0, False)(streams[si])
+    fast = [[plan(si, k, True).bind(streams[si]) for k in range(6)] for si in range(S)]  # cycle: slot k%2, bufs k%3
+    pos = [1] * S
+    turn = [0]
 
-    def run_steps(n):
+    def run_steps(n):            # step i on stream i % S
         for _ in range(n):
-            fast[pos[0] % 6]()
-            pos[0] += 1
+            si = turn[0] % S
+            fast[si][pos[si] % 6]()
+            pos[si] += 1
+            turn[0] += 1
 
     run_steps(args.warmup)
     torch.cuda.synchronize(dev)
@@ -1157,21 +1177,32 @@ def deferred_run(args, dev, coh, arm_cf, coh2=None, arm_cf2=None):
     host_ms = (time.perf_counter() - t0) / args.steps * 1e3
     torch.cuda.synchronize(dev)
     ms_step = (time.perf_counter() - t0) / args.steps * 1e3
-    last = pos[0] - 1                          # the last step finalised cohort (last - 1) % 2 into outs[(last-1) % 3]
+    # instrumented pass: timing events on stream 0 around batches of KB steps; the other streams' last launches
+    # are joined into stream 0 before the closing event (one ordering event per stream per batch)
     hip = HipEvents()
     KB, NBAT = max(args.steps, 10), 3
     tevs = [(hip.create(timing=True), hip.create(timing=True)) for _ in range(NBAT)]
+    joins = [hip.create() for _ in range(S)]
+    st0 = streams[0].cuda_stream
     for e0, e1 in tevs:
-        hip.record(e0, st.cuda_stream)
+        torch.cuda.synchronize(dev)
+        hip.record(e0, st0)
+        for si in range(1, S):
+            hip.wait(streams[si].cuda_stream, e0)
         run_steps(KB)
-        hip.record(e1, st.cuda_stream)
+        for si in range(1, S):
+            hip.record(joins[si], streams[si].cuda_stream)
+            hip.wait(st0, joins[si])
+        hip.record(e1, st0)
     torch.cuda.synchronize(dev)
     step_ms = float(np.mean([hip.elapsed_ms(e0, e1) for e0, e1 in tevs])) / KB
     rb, gb = rollout_bytes(N, T, arm_bits=1), gram_bytes(N, T)
+    mine, outs, ys, _ = lanes[(turn[0] - 1) % S]
+    last = pos[(turn[0] - 1) % S] - 1
     fin = outs[(last - 1) % 3]
     return {"ms_step": ms_step, "host_ms": host_ms, "step_ms": step_ms, "KB": KB, "NBAT": NBAT,
-            "coef": fin[0], "mask": fin[1], "y": ys[last % 2], "rb": rb, "gb": gb, "rotated": coh2 is not None,
-            "frac": (rb + gb) / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+            "coef": fin[0], "mask": fin[1], "y": ys[last % len(mine)], "rb": rb, "gb": gb, "rotated": coh2 is not None,
+            "streams": S, "frac": (rb + gb) / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
 
 
 def c2_fused(args, dev, coh, arm_cf, cpu):
@@ -1235,7 +1266,8 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
             "patients_per_gpu": N, "T": T, "rows_per_patient": T - 2, "library_terms": F,
             "parallelism": "patient-shard x1", "mode": args.mode, "gram_blocks": args.gram_blocks or "default",
             "discovered_support": sup.tolist(), "finite": ok,
-            "cohorts_rotated": 2 if fr["rotated"] else 1,
+            "cohorts_rotated": (2 if fr["rotated"] else 1) * fr.get("streams", 1),
+            **({"deferred_streams": fr["streams"]} if deferred else {}),
         },
         "host_submit_ms_per_step": host_ms,
         "roofline": {
