@@ -145,3 +145,34 @@ def test_insite_plugin_segment_metrics(dev, case):
     print(eq, "log rel diff", {k: f"{got[k] / anchor[k] - 1:+.2e}" for k in METRICS})
     bad = {k: (got[k], ref[k]) for k in METRICS if got[k] != pytest.approx(ref[k], rel=1e-9)}
     assert not bad, bad
+
+
+def test_plugin_joint_one_ode_reproduces_log(dev):
+    """The one-ODE ablation (run.py:198-201, joint_model + multilabel treatments) through the plugin on the GPU
+    (general one-state Gram + STLSQ, folded per-combination rollout) on the logged cohort (np.random.seed(10),
+    tests/test_cancer_sim_reference.py::test_one_ode_joint_model_equals_log): the 16-digit equation of
+    results/ablation/one_ode/build_tables/...one_big_ode.txt:10 to 1e-10 relative and every metric to 1e-9."""
+    from insite_amd import config as C
+    from insite_amd.sindy import SINDY
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        coll = CS.make_collection(10, treatment_mode="multilabel")
+    a = C.compose(["+backbone=sindy", "+dataset=pkpd_sim", "model.sindy_threshold=0.001", "model.sindy_alpha=0.5",
+                   "model.joint_model=true", "dataset.treatment_mode=multilabel"])
+    a["model"].update({"dataset_name": "cancer_sim", "dim_treatments": 2, "dim_static_features": 1,
+                       "dim_outcomes": 1})
+    m = SINDY(a, device=dev)
+    m.fit(coll["train"], coll["val"])
+    anchor = ANCHORS["ABLATION_ONE_ODE/cancer_sim/sindy/1"]
+    names = ["1", "x0", "u0", "u1", "u2", "x0 u0", "x0 u1", "x0 u2", "u0 u1", "u0 u2", "u1 u2"]
+    parts = anchor["global_equation_string"].split("= ", 1)[1].split("+")[1:]
+    ref = np.zeros(len(names))
+    for term in parts:
+        c, name = term.split("*", 1)
+        ref[names.index(name.replace("*", " "))] = float(c)
+    got = np.asarray(m.joint_coefs)[0]
+    assert np.array_equal(got != 0, ref != 0)
+    assert np.max(np.abs(got - ref) / np.maximum(1.0, np.abs(ref))) < 1e-10
+    res = _metrics(m, coll)
+    for k in METRICS:
+        assert res[k] == pytest.approx(anchor[k], rel=1e-9), k
