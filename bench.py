@@ -359,7 +359,7 @@ def c3_main(args):
                    "support_equals_truth": bool(torch.equal(mask != 0, truth != 0))},
         "roofline": {"kernel": "gram_ms4_kernel", "bound": "mfma", "achieved": gflop / (gram_ms_t * 1e-3) / 1e12,
                      "peak": 78.6, "unit": "TFLOP/s", "frac": gflop / (gram_ms_t * 1e-3) / 1e12 / 78.6,
-                     "traffic": traffic_for("c3", "gram_ms4_kernel"), "avg_launch_ms": gram_ms_t,
+                     "traffic": traffic_for("c3", "gram_ms4_kernel", args=args), "avg_launch_ms": gram_ms_t,
                      "issued_mfma_TFLOPs": mfma_flop / (gram_ms_t * 1e-3) / 1e12,
                      "hbm_GBps": gram_bytes / (gram_ms_t * 1e-3) / 1e9},
         "rollout": {"kernel": "ms_rollout_sparse (hipRTC, support-specialised; rk4, fp32)", "bound": "hbm",
@@ -491,7 +491,7 @@ def c5_main(args):
         "roofline": {"kernel": "rollout_rk45_kernel", "bound": "valu-f64", "unit": "TFLOP/s",
                      "achieved": flop / (launch_ms * 1e-3) / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
                      "frac": flop / (launch_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
-                     "traffic": traffic_for("c5", "rollout_rk45_flat_kernel"),
+                     "traffic": traffic_for("c5", "rollout_rk45_flat_kernel", args=args),
                      "avg_launch_ms": launch_ms, "flop_per_attempt": RK45_FLOP_PER_ATTEMPT,
                      "issued_incl_divergence_TFLOPs": issued / (launch_ms * 1e-3) / 1e12,
                      "algorithmic_bytes": N * (8 * 3 + 4) + N * Tm * 8 * 2 + N * ((Tm + 30) // 32) * 4,
@@ -658,7 +658,7 @@ def insite_main(args):
         "roofline": {"kernel": "insite_refine_kernel<4, 2, 1> (per-row BFGS + final Euler-5 scan)", "bound": "valu-f64",
                      "unit": "TFLOP/s", "achieved": flop / (kern_ms * 1e-3) / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
                      "frac": flop / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
-                     "traffic": traffic_for("insite", "insite_refine_kernel"), "avg_launch_ms": kern_ms,
+                     "traffic": traffic_for("insite", "insite_refine_kernel", args=args), "avg_launch_ms": kern_ms,
                      "algorithmic_flop": flop, "flop_per_sensitivity_step": per_step,
                      "flop_method": "sum over refined rows of nfev_r x K_r (K_r = min(seq_len - tau, T - 1)) x "
                                     "(5 Euler sub-steps x (4A + 7) + 4A + 5) with A = 2 arms, + N x T x 5 x 4 for "
@@ -760,7 +760,7 @@ def f4_main(args):
         "roofline": {"kernel": "gram_seg_kernel (order1, 4 arms; in-launch fixed-order reduction, G|b written by the "
                                "last block)", "bound": "hbm",
                      "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
-                     "traffic": traffic_for("f4", "gram_seg_kernel"), "algorithmic_bytes_per_launch": gb,
+                     "traffic": traffic_for("f4", "gram_seg_kernel", args=args), "algorithmic_bytes_per_launch": gb,
                      "avg_launch_ms": gram_ms},
         "rollout": {"kernel": "rollout_tm_kernel (euler5, 4 arms, int8 arms)", "avg_launch_ms": roll_ms,
                     "algorithmic_bytes": rb, "achieved_GBps": rb / (roll_ms * 1e-3) / 1e9,
@@ -914,7 +914,7 @@ def c4_main(args):
             "roofline": {"kernel": "refit_rollout_kernel (per-patient refit from the moments in the prologue + "
                                    "euler5 bit-arm rollout)", "bound": "hbm",
                          "achieved": fb / (fold_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": fb / (fold_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": traffic_for("c4", "refit_rollout_kernel"),
+                         "frac": fb / (fold_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, "traffic": traffic_for("c4", "refit_rollout_kernel", args=args),
                          "algorithmic_bytes_per_launch": fb, "avg_launch_ms": fold_ms},
             "discovery": {"kernels": "gram_kernel<MOM=2> (Gram + in-launch reduction + STLSQ + every patient's "
                                      "moments, one pass over x)" + (" + RCCL all-reduce + stlsq_kernel" if world > 1 else ""),
@@ -1002,11 +1002,15 @@ def dist_setup(force_group: bool = False):
 TRAFFIC_R03 = os.path.join(ROOT, "profiles", "traffic_r03.json")
 
 
-def traffic_for(config, kernel, grid=None):
+def traffic_for(config, kernel, grid=None, args=None):
     """HBM bytes per launch of `kernel` (symbol prefix) in the bench line `config`, from the committed PMC passes
     (profiles/traffic_r03.json, tools/g_traffic.sh + tools/traffic_summary.py: FETCH_SIZE x 2 calibration +
     WRITE_SIZE, median per dispatch), or None when that table has no such entry.  `grid`: the launch's total
-    threads when a config launches the kernel at several sizes."""
+    threads when a config launches the kernel at several sizes.  `args`: the table was taken on each config's
+    DEFAULT workload at N = 1 (tools/g_traffic.sh), so a line with other sizes gets None."""
+    if args is not None and (args.patients != 100_000 or args.T not in (200, 60 if config == "c4" else 200)
+                             or int(os.environ.get("WORLD_SIZE", "1")) != 1):
+        return None
     try:
         with open(TRAFFIC_R03) as f:
             tab = json.load(f).get(config, {})
