@@ -52,7 +52,17 @@ __device__ unsigned long long g_tstamp[kTsWaves * kTsSlots];
     const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                 \
     if ((threadIdx.x & 63) == 0 && (wave) < kTsWaves) g_tstamp[(int64_t)(wave) * kTsSlots + (slot)] = t_; \
   } while (0)
+// slot 7: where the wave runs -- HW_ID (gfx9 layout: CU 11:8, SH 12, SE 14:13) | XCC_ID << 32
+#define INSITE_THWID(wave)                                                                                     \
+  do {                                                                                                         \
+    const unsigned long long h_ = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |             \
+                                  ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32);      \
+    if ((threadIdx.x & 63) == 0 && (wave) < kTsWaves) g_tstamp[(int64_t)(wave) * kTsSlots + 7] = h_;         \
+  } while (0)
 #else
+#define INSITE_THWID(wave) \
+  do {                     \
+  } while (0)
 #define INSITE_TSTAMP(wave, slot) \
   do {                            \
   } while (0)
@@ -449,6 +459,7 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
   static_assert(!TM || (VEC == 1 && NLD == kGT), "time-major tiles hold the lane's own kGT samples");
   INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 0);
   INSITE_TREAL(blockIdx.x * kWavesPerBlock + wid, 8);
+  INSITE_THWID(blockIdx.x * kWavesPerBlock + wid);
 
   // G-phase accumulators
   dbl4 cacc = {0.0, 0.0, 0.0, 0.0};  // MFMA path: C[(lane>>4) + 4j][lane & 15]
@@ -2328,6 +2339,47 @@ __global__ void __launch_bounds__(kBlock) refit_rollout_kernel(RolloutArgs ra, L
 #ifndef INSITE_STEP_DYN_STATIC
 #define INSITE_STEP_DYN_STATIC 500
 #endif
+// The bit-arm rollout of the (tile, arm group) units [q, q1) (tile-major), one rollout_bits_range per tile.
+template <int METHOD>
+__device__ __forceinline__ void rollout_units(const RolloutArgs& ra, const LibDesc& lib, const int lane, int64_t q,
+                                              const int64_t q1, const int ng) {
+  while (q < q1) {
+    const int64_t tile = q / ng;
+    const int gb = (int)(q - tile * ng);
+    const int ge = q1 - q < (int64_t)(ng - gb) ? gb + (int)(q1 - q) : ng;
+    rollout_bits_range<METHOD, 2, false>(ra, lib, lane, tile, gb, ge);
+    q += ge - gb;
+  }
+}
+// Units [S, units) in chunks of `chunk` units claimed with the agent-scope counter rc[0] (the next claim in flight
+// while a chunk is stored); rc[1] counts the waves done claiming, and the last of the `waves` participants resets
+// both.  Which wave stores a chunk never reaches y (every chunk is a rollout_bits_range).
+template <int METHOD>
+__device__ __forceinline__ void rollout_claimed(const RolloutArgs& ra, const LibDesc& lib, const int lane, const int64_t S,
+                                                const int64_t units, const int ng, const int chunk,
+                                                unsigned* __restrict__ rc, const int64_t waves) {
+  const int64_t n_chunks = (units - S + chunk - 1) / chunk;
+  auto claim = [&]() -> unsigned {  // lane 0 holds the claimed chunk index (read when it is needed)
+    unsigned v = 0u;
+    if (lane == 0) v = __hip_atomic_fetch_add(rc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+  };
+  unsigned nxt = claim();
+  for (;;) {
+    const int64_t c = (int64_t)__builtin_amdgcn_readfirstlane(nxt);
+    if (c >= n_chunks) break;
+    nxt = claim();
+    const int64_t q = S + c * chunk;
+    rollout_units<METHOD>(ra, lib, lane, q, q + chunk < units ? q + chunk : units, ng);
+  }
+  if (lane == 0) {
+    const unsigned t = __hip_atomic_fetch_add(rc + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == (unsigned)waves - 1u) {
+      __hip_atomic_store(rc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(rc + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 #ifndef INSITE_STEP_DYN_CHUNK
 #define INSITE_STEP_DYN_CHUNK 2
 #endif
@@ -2352,39 +2404,9 @@ step_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
     INSITE_TREAL(32768 + rw, 8);
     const int ng = (ra.T + kRollGS - 1) / kRollGS;
     const int64_t units = (ra.N + kWave - 1) / kWave * ng;  // (tile, arm group) pairs, tile-major
-    auto run_units = [&](int64_t q, const int64_t q1) {
-      while (q < q1) {
-        const int64_t tile = q / ng;
-        const int gb = (int)(q - tile * ng);
-        const int ge = q1 - q < (int64_t)(ng - gb) ? gb + (int)(q1 - q) : ng;
-        rollout_bits_range<METHOD, 2, false>(ra, lib, lane, tile, gb, ge);
-        q += ge - gb;
-      }
-    };
     const int64_t S = units * INSITE_STEP_DYN_STATIC / 1000;
-    run_units(rw * S / RW, (rw + 1) * S / RW);
-    unsigned* rc = cnt + kStepRcnt;
-    const int64_t n_chunks = (units - S + INSITE_STEP_DYN_CHUNK - 1) / INSITE_STEP_DYN_CHUNK;
-    auto claim = [&]() -> unsigned {  // lane 0 holds the claimed chunk index (read when it is needed)
-      unsigned v = 0u;
-      if (lane == 0) v = __hip_atomic_fetch_add(rc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return v;
-    };
-    unsigned nxt = claim();
-    for (;;) {
-      const int64_t c = (int64_t)__builtin_amdgcn_readfirstlane(nxt);
-      if (c >= n_chunks) break;
-      nxt = claim();  // in flight while this chunk is stored
-      const int64_t q = S + c * INSITE_STEP_DYN_CHUNK;
-      run_units(q, q + INSITE_STEP_DYN_CHUNK < units ? q + INSITE_STEP_DYN_CHUNK : units);
-    }
-    if (lane == 0) {  // done claiming; the last wave resets both counters for the next launch
-      const unsigned t = __hip_atomic_fetch_add(rc + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == (unsigned)RW - 1u) {
-        __hip_atomic_store(rc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(rc + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    rollout_units<METHOD>(ra, lib, lane, rw * S / RW, (rw + 1) * S / RW, ng);
+    rollout_claimed<METHOD>(ra, lib, lane, S, units, ng, INSITE_STEP_DYN_CHUNK, cnt + kStepRcnt, RW);
     INSITE_TSTAMP(32768 + rw, 0);
     INSITE_TREAL(32768 + rw, 9);
     return;
@@ -2421,14 +2443,27 @@ step_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
 // reduces the partials the PREVIOUS launch left in `part_prev` (cohort k-1: G|b, STLSQ -> coefficients) while
 // the others stream; the remaining blocks roll out a cohort with coefficients finalised one launch earlier
 // still (cohort k-2 in a stream).  Nothing in the launch waits on anything else in it: no counters, no tail.
+// A/B knobs: INSITE_DEF_RSTATIC (per mille of the rollout units split statically; below 1000 the rest is claimed
+// in INSITE_DEF_RCHUNK-unit chunks through the counters in the workspace header), INSITE_DEF_GPRIO (s_setprio of
+// the gram waves).
+#ifndef INSITE_DEF_RSTATIC
+#define INSITE_DEF_RSTATIC 1000
+#endif
+#ifndef INSITE_DEF_RCHUNK
+#define INSITE_DEF_RCHUNK 1
+#endif
+#ifndef INSITE_DEF_GPRIO
+#define INSITE_DEF_GPRIO 0
+#endif
 template <bool SMOOTH, int METHOD>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_STEP_WPE)))
 step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
                      const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, GramW w, LibDesc lib,
                      double* __restrict__ part_cur, const double* __restrict__ part_prev, GramOut out, RolloutArgs ra,
-                     int gblocks) {
+                     int gblocks, unsigned* __restrict__ rc) {
   __shared__ double smem[kGramSmem];
   if ((int)blockIdx.x < gblocks) {
+    if (INSITE_DEF_GPRIO) __builtin_amdgcn_s_setprio(INSITE_DEF_GPRIO);
     gram_body<1, 2, SMOOTH, true, true, 0, 7>((int)blockIdx.x, gblocks, smem, x, ldx, n_steps, u, arm, rows, N, 0, 0,
                                                  w, lib, part_cur, nullptr, out);
     return;
@@ -2447,17 +2482,12 @@ step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, con
   const int64_t RW = (int64_t)(gridDim.x - gblocks - 1) * kWavesPerBlock;
   const int64_t rw = (int64_t)((int)blockIdx.x - gblocks - 1) * kWavesPerBlock + wid;
   INSITE_TREAL(32768 + rw, 8);
+  INSITE_THWID(32768 + rw);
   const int ng = (ra.T + kRollGS - 1) / kRollGS;
   const int64_t units = (ra.N + kWave - 1) / kWave * ng;  // (tile, arm group) pairs, tile-major
-  int64_t q = rw * units / RW;
-  const int64_t q1 = (rw + 1) * units / RW;
-  while (q < q1) {
-    const int64_t tile = q / ng;
-    const int gb = (int)(q - tile * ng);
-    const int ge = q1 - q < (int64_t)(ng - gb) ? gb + (int)(q1 - q) : ng;
-    rollout_bits_range<METHOD, 2, false>(ra, lib, lane, tile, gb, ge);
-    q += ge - gb;
-  }
+  const int64_t S = rc ? units * INSITE_DEF_RSTATIC / 1000 : units;
+  rollout_units<METHOD>(ra, lib, lane, rw * S / RW, (rw + 1) * S / RW, ng);
+  if (rc) rollout_claimed<METHOD>(ra, lib, lane, S, units, ng, INSITE_DEF_RCHUNK, rc, RW);
   INSITE_TSTAMP(32768 + rw, 0);
   INSITE_TREAL(32768 + rw, 9);
 }
@@ -3821,8 +3851,9 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
       rows = reinterpret_cast<const int32_t*>(G_out);
       u = G_out;
     }
+    unsigned* rc = INSITE_DEF_RSTATIC < 1000 ? static_cast<unsigned*>(workspace) : nullptr;  // slot 0's header
     kd<<<dim3(grid), kBlock, 0, hs>>>(x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, part_cur,
-                                      part_prev, go, ra, gb);
+                                      part_prev, go, ra, gb, rc);
     return launch_status();
   }
   // (a two-patients-per-lane rollout role with 16-B stores measured slower: 46 vs 37 us rollout-only)

@@ -26,6 +26,11 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     GORD1) NAME=$v build -DINSITE_GRAM_ORDER=1 ;;
     STEPITEM) NAME=$v build -DINSITE_STEP_RANGED=0 ;;
     STEPSPLIT) NAME=$v build -DINSITE_STEP_SERIAL=0 ;;
+    DR600) NAME=$v build -DINSITE_DEF_RSTATIC=600 ;;
+    DR800) NAME=$v build -DINSITE_DEF_RSTATIC=800 ;;
+    DR800C2) NAME=$v build -DINSITE_DEF_RSTATIC=800 -DINSITE_DEF_RCHUNK=2 ;;
+    DGPRIO) NAME=$v build -DINSITE_DEF_GPRIO=2 ;;
+    DGPRIO800) NAME=$v build -DINSITE_DEF_GPRIO=2 -DINSITE_DEF_RSTATIC=800 ;;
     DYN0) NAME=$v build -DINSITE_STEP_DYN_STATIC=0 ;;
     DYN250) NAME=$v build -DINSITE_STEP_DYN_STATIC=250 ;;
     DYN750) NAME=$v build -DINSITE_STEP_DYN_STATIC=750 ;;

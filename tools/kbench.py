@@ -21,6 +21,7 @@ ap.add_argument("--cold", action="store_true",
 ap.add_argument("--flush", default="read", choices=["read", "write"],
                 help="cold eviction by reading 512 MB (clean cache) or writing it (dirty lines left behind)")
 ap.add_argument("--timing", action="store_true", help="phase timestamps (needs an INSITE_TIMING build)")
+ap.add_argument("--hwid", action="store_true", help="with --timing: wave end times by XCC / SE / CU")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 xlay = "time" if a.layout == "time_bits" else a.layout
@@ -116,7 +117,20 @@ if a.timing:
         if not len(t):
             continue
         out = {"kernel": part, "waves": len(t)}
-        for j in range(1, 8):
+        if a.hwid and part in ("gram", "rollout"):   # end time by where the wave ran (slot 7: HW_ID | XCC_ID << 32)
+            hw = t[:, 7].astype(np.uint64)
+            xcc = (hw >> np.uint64(32)).astype(np.int64) & 15
+            cu = (hw >> np.uint64(8)).astype(np.int64) & 15
+            se = (hw >> np.uint64(13)).astype(np.int64) & 7
+            endt = (t[:, 9] - t[:, 8]) / 100.0
+            out["end_by_xcc_us"] = {int(x): round(float(endt[xcc == x].mean()), 2) for x in np.unique(xcc)}
+            out["end_by_se_us"] = {int(x): round(float(endt[se == x].mean()), 2) for x in np.unique(se)}
+            cuid = xcc * 1000 + se * 100 + cu
+            per_cu = np.array([endt[cuid == c].mean() for c in np.unique(cuid)])
+            out["cu_mean_end_pcts"] = [round(float(np.percentile(per_cu, q)), 2) for q in (0, 10, 50, 90, 100)]
+            out["within_cu_spread_us_mean"] = round(float(np.mean([endt[cuid == c].max() - endt[cuid == c].min()
+                                                                   for c in np.unique(cuid)])), 2)
+        for j in range(1, 7):
             ok = t[:, j] > 0
             if ok.any():
                 out[f"slot{j}_cyc"] = round(float((t[ok, j] - t[ok, 0]).mean()))
