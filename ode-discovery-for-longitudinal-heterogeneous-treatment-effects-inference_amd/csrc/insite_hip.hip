@@ -2725,7 +2725,7 @@ rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
 // fastest lane), not once per iteration.  (vmcnt is per wave: with a load issued at every close, and some
 // lane closing in nearly every iteration, a register queue waits on the previous iteration's load.)
 #ifndef INSITE_RK45_WIN
-#define INSITE_RK45_WIN 16
+#define INSITE_RK45_WIN 8  // 8: 32 KB of LDS per block with the output staging -> 5 blocks per CU (16: 3; 0.94 -> 0.88 ms, profiles/r03/v23)
 #endif
 // PM: patient-major t / y / arm bits (INSITE_LAYOUT_PATIENT_MAJOR_BITS): a lane's window refill reads one
 // contiguous run and its y elements share lines that only this lane writes, whatever rows the lanes hold

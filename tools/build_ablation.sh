@@ -58,6 +58,9 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     RKR02) NAME=$v build -DINSITE_RK45_CLOSE_BRANCH=1 -DINSITE_RK45_ROOT_BRANCH=1 ;;
     RKROOTBR) NAME=$v build -DINSITE_RK45_ROOT_BRANCH=1 ;;
     RKW12) NAME=$v build -DINSITE_RK45_WIN=12 ;;
+    RKW8) NAME=$v build -DINSITE_RK45_WIN=8 ;;
+    RKW8W5) NAME=$v build -DINSITE_RK45_WIN=8 -DINSITE_RK45_WPE=5 ;;
+    RKW4W5) NAME=$v build -DINSITE_RK45_WIN=4 -DINSITE_RK45_WPE=5 ;;
     SEGKC8) NAME=$v build -DINSITE_SEG_KC=8 -DINSITE_SEG_WPE=3 ;;
     SEGKC4) NAME=$v build -DINSITE_SEG_KC=4 -DINSITE_SEG_WPE=4 ;;
     SEGKC16) NAME=$v build -DINSITE_SEG_KC=16 -DINSITE_SEG_WPE=2 ;;
