@@ -469,7 +469,13 @@ constexpr int kMs4Stride = 29;   // LDS row stride (doubles): odd, stores confli
 #ifndef INSITE_MS4_RING
 #define INSITE_MS4_RING 12
 #endif
-constexpr int kMs4Ring = INSITE_MS4_RING;  // raw-sample ring slots (interior): x[t-8 .. t] + kMs4Ring - 9 prefetched
+constexpr int kMs4Ring = INSITE_MS4_RING;
+// INSITE_MS4_BUFLD (default 1): interior samples through a per-step buffer descriptor (SGPR address math) instead
+// of per-lane 64-bit addresses -- with those the 256-VGPR kernel spilled its step index and reloaded it from
+// scratch before every prefetch, and each reload's s_waitcnt vmcnt(0) drained the whole prefetch ring
+#ifndef INSITE_MS4_BUFLD
+#define INSITE_MS4_BUFLD 1
+#endif  // raw-sample ring slots (interior): x[t-8 .. t] + kMs4Ring - 9 prefetched
 constexpr double kMsC1 = 37.0 / 105.0, kMsC2 = 79.0 / 420.0, kMsC3 = -3.0 / 35.0, kMsC4 = 1.0 / 140.0;
 
 // The library row is formed column by column straight into LDS (Theta_j = z_i z_k, pysindy order), so the
@@ -580,11 +586,26 @@ struct Ms4Z {
 };
 
 // Per-lane LDS read pointers of the staged-factor form (row R0(lane) of pass 0; pass r adds r rows).
+// INSITE_MS4Z_PACK (default): the product groups' factor positions (< 256) packed 4 to a register and unpacked
+// at each read (one bit-field extract), where 2 QG + 1 separate pointers pushed the 256-VGPR kernel into
+// scratch reloads inside the MFMA passes (C3: 6 reloads per pass; -Rpass-analysis 84 B/lane).
+#ifndef INSITE_MS4Z_PACK
+#define INSITE_MS4Z_PACK 1
+#endif
 template <int QG>
 struct Ms4ZPtr {
   const double* pure;    // &P[R0][i]
+#if INSITE_MS4Z_PACK
+  const double* row;                            // &P[R0][0]
+  unsigned pa[(QG + 3) / 4], pb[(QG + 3) / 4];  // pos_a / pos_b of product group g in byte g % 4 of word g / 4
+  __device__ const double* at_a(int g) const { return row + ((pa[g >> 2] >> (8 * (g & 3))) & 0xffu); }
+  __device__ const double* at_b(int g) const { return row + ((pb[g >> 2] >> (8 * (g & 3))) & 0xffu); }
+#else
   const double* qa[QG];  // &P[R0][pos_a(g, i)]
   const double* qb[QG];
+  __device__ const double* at_a(int g) const { return qa[g]; }
+  __device__ const double* at_b(int g) const { return qb[g]; }
+#endif
 };
 
 template <int S, int NZ, bool INTER>
@@ -596,6 +617,11 @@ __device__ __forceinline__ Ms4ZPtr<Ms4Z<S, NZ, INTER>::QG> ms4z_ptrs(const doubl
   const double* row = wbase + r0 * LZ::STRIDE;
   Ms4ZPtr<LZ::QG> p;
   p.pure = row + i;
+#if INSITE_MS4Z_PACK
+  p.row = row;
+#pragma unroll
+  for (int q = 0; q < (LZ::QG + 3) / 4; ++q) p.pa[q] = p.pb[q] = 0u;
+#endif
 #pragma unroll
   for (int g = 0; g < LZ::QG; ++g) {
     int a = lz.pos_a[LZ::PY + g][0], bb = lz.pos_b[LZ::PY + g][0];
@@ -606,8 +632,14 @@ __device__ __forceinline__ Ms4ZPtr<Ms4Z<S, NZ, INTER>::QG> ms4z_ptrs(const doubl
         bb = lz.pos_b[LZ::PY + g][ii];
       }
     }
+#if INSITE_MS4Z_PACK
+    static_assert(4 * LZ::PG < 256, "factor positions fit a byte");
+    p.pa[g >> 2] |= (unsigned)a << (8 * (g & 3));
+    p.pb[g >> 2] |= (unsigned)bb << (8 * (g & 3));
+#else
     p.qa[g] = row + a;
     p.qb[g] = row + bb;
+#endif
   }
   return p;
 }
@@ -664,8 +696,8 @@ __device__ __forceinline__ void ms4z_passes(const Ms4ZPtr<Ms4Z<S, NZ, INTER>::QG
 #pragma unroll
     for (int g = 0; g < LZ::CG; ++g) {
       if (g >= LZ::PY && g < LZ::PY + LZ::QG) {
-        ra[slot][g] = pp.qa[g - LZ::PY][r * LZ::STRIDE];
-        rb[slot][g - LZ::PY] = pp.qb[g - LZ::PY][r * LZ::STRIDE];
+        ra[slot][g] = pp.at_a(g - LZ::PY)[r * LZ::STRIDE];
+        rb[slot][g - LZ::PY] = pp.at_b(g - LZ::PY)[r * LZ::STRIDE];
       } else {
         const int pgi = g < LZ::PY ? g : g - LZ::QG;
         ra[slot][g] = pp.pure[4 * pgi + r * LZ::STRIDE];
@@ -780,6 +812,19 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
     const int tzc = tz > ea ? tz : ea;  // a lane already past its end zeroes its (stale) row at the first emit
     if (Lmax >= 9 && eb > ea) {
       float xr[kMs4Ring][S];
+#if INSITE_MS4_BUFLD
+      // the S state rows of step k through one wave-uniform descriptor based at (k, state 0, column p0):
+      // SGPR address math per step, lanes past N read 0 (their rows are never emitted)
+      const int tval = (int)(N - p0 < kWave ? N - p0 : kWave);
+      const unsigned loff = p < N ? (unsigned)lane * 4u : kOOB;
+      auto ld_step = [&](float (&dst)[S], int k) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(x + (int64_t)k * kstride + p0), (short)0, (int)(((int64_t)(S - 1) * sstride + tval) * 4), 0x00020000);
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          dst[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, loff, (int)(s * sstride * 4), 0));
+      };
+#endif
       auto word = [&](int g) -> unsigned {  // treatment bits of rows [32 g, 32 g + 32), half-wave transpose
         if (!abits) return 0u;
         const int k = 32 * g + (lane & 31);
@@ -789,9 +834,14 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
         return bit_transpose32(v, lane);
       };
 #pragma unroll
-      for (int t = 0; t < kMs4Ring - 9; ++t)
+      for (int t = 0; t < kMs4Ring - 9; ++t) {
+#if INSITE_MS4_BUFLD
+        ld_step(xr[t], ts + t);
+#else
 #pragma unroll
         for (int s = 0; s < S; ++s) xr[t][s] = xp[(int64_t)(ts + t) * kstride + s * sstride];
+#endif
+      }
       unsigned wcur = word((ea - 4) >> 5);
       for (int t0 = ts; t0 < eb; t0 += kMs4Ring) {
 #pragma unroll
@@ -801,8 +851,12 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
             // x[t + PF] into the slot of x[t - 9 + ...] (no longer needed): its wait falls PF steps later
             constexpr int PF = kMs4Ring - 9;
             const int tn = t + PF < n_steps ? t + PF : n_steps - 1;
+#if INSITE_MS4_BUFLD
+            ld_step(xr[(i + PF) % kMs4Ring], tn);
+#else
 #pragma unroll
             for (int s = 0; s < S; ++s) xr[(i + PF) % kMs4Ring][s] = xp[(int64_t)tn * kstride + s * sstride];
+#endif
             if (t >= ea) {  // row r = t - 4: raw x[r], xdot from x[r-4 .. r+4] (slots i-8 .. i)
               const int r = t - 4;
               if ((r & 31) == 0) wcur = word(r >> 5);

@@ -21,6 +21,8 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     MS4MASKSEL) NAME=$v build -DINSITE_MS4Z_MASKSEL=1 ;;
     MS4PRIO) NAME=$v build -DINSITE_MS4_PRIO=1 ;;
     MS4NC1) NAME=$v build -DINSITE_MS4_NCHUNK=1 ;;
+    MS4NOBUF) NAME=$v build -DINSITE_MS4_BUFLD=0 ;;
+    MS4NOPACK) NAME=$v build -DINSITE_MS4Z_PACK=0 ;;
     STLSEP) NAME=$v build -DINSITE_STLSQ_SEPARATE ;;
     STEPDEPTH3) NAME=$v build -DINSITE_TM_DEPTH=3 ;;
     GORD1) NAME=$v build -DINSITE_GRAM_ORDER=1 ;;
