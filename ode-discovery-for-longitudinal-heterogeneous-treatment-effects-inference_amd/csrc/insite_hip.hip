@@ -1181,6 +1181,9 @@ constexpr int kSegRS = kSegMono + 5 * INSITE_MAX_ARMS;  // LDS row: F monomials 
 #ifndef INSITE_SEG_WPE
 #define INSITE_SEG_WPE 4  // waves per SIMD the register budget is sized for (4: <= 128 VGPRs)
 #endif
+#ifndef INSITE_SEG_RANGED
+#define INSITE_SEG_RANGED 1
+#endif
 template <int NARM, bool SMOOTH1, int STF>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_SEG_WPE)))
 gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const int8_t* __restrict__ arm, int64_t asp,
@@ -1204,14 +1207,36 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
   const int moff = kSegMono + (my_k >= 0 ? lib.ex[my_i] + lib.ex[my_k] : 3 + lib.ex[my_i]);
 
   const int64_t n_tiles = (N + kWave - 1) / kWave;
-  for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid; tile < n_tiles;
-       tile += (int64_t)gridDim.x * kWavesPerBlock) {
+  // Work pieces (tile, steps [kbeg, kend)).  INSITE_SEG_RANGED (default): the (tile, kSegKC-step chunk) units,
+  // tile-major, cut into one equal contiguous range per wave of a resident grid, a piece being the part of a
+  // range inside one tile (it starts from sample kbeg with the segment state of that step: the arms of samples
+  // kbeg - 1 and kbeg); moments are additive over a patient's pieces, so each piece is contracted on its own.
+  // Otherwise one whole tile per wave (round 2; grid = one wave per tile).
+  const int ngc = n_steps > 1 ? (n_steps - 1 + kSegKC - 1) / kSegKC : 1;
+  const int64_t nW = (int64_t)gridDim.x * kWavesPerBlock, wv = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  const int64_t c_end = INSITE_SEG_RANGED ? (wv + 1) * (n_tiles * ngc) / nW : n_tiles;
+  for (int64_t cur = INSITE_SEG_RANGED ? wv * (n_tiles * ngc) / nW : wv; cur < c_end;) {
+    int64_t tile;
+    int kbeg, kend;
+    if (INSITE_SEG_RANGED) {
+      tile = cur / ngc;
+      const int g0 = (int)(cur - tile * ngc);
+      const int g1 = (int)min((int64_t)ngc, (int64_t)g0 + (c_end - cur));
+      kbeg = g0 * kSegKC;
+      kend = g1 * kSegKC;
+      cur += g1 - g0;
+    } else {
+      tile = cur;
+      kbeg = 0;
+      kend = n_steps;
+      cur += nW;
+    }
     const int64_t p = tile * kWave + lane;
     const bool valid = p < N;
     int L = valid ? seq_len[p] : 0;
     if (L > n_steps - 1) L = n_steps - 1;
     if (L < 0) L = 0;
-    const int Lw = wave_max_i(L);
+    const int Lw = min(wave_max_i(L), kend);  // one past the last step this piece processes
     double mo[NARM][5];
 #pragma unroll
     for (int a = 0; a < NARM; ++a)
@@ -1241,16 +1266,21 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
                                                bytes, 0x00020000);
     };
     const unsigned xstep = (unsigned)(xsk * 8), astep = (unsigned)ask;
-    if (Lw > 0) {
+    if (kbeg < Lw) {
       double xj;
       int aj;
-      {
-        const __amdgpu_buffer_rsrc_t rx = x_rsrc(0), ra = a_rsrc(0);
-        xj = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, xvo, 0, 0));
-        const int a0 = (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(ra, avo, 0, 0);
-        aj = 0 < L ? a0 : -1;
-      }
       int aprev = -1;  // arm of sample j-1 (SMOOTH1: segment-start test)
+      {
+        const __amdgpu_buffer_rsrc_t rx = x_rsrc(kbeg), ra = a_rsrc(kbeg);
+        const double x0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, xvo, 0, 0));
+        xj = kbeg <= L ? x0 : 0.0;  // past the lane's samples (padding may be NaN): zero, as the chunk masks do
+        const int a0 = (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(ra, avo, 0, 0);
+        aj = kbeg < L ? a0 : -1;
+        if (SMOOTH1 && kbeg > 0) {  // uniform
+          const int am = (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(a_rsrc(kbeg - 1), avo, 0, 0);
+          aprev = kbeg - 1 < L ? am : -1;
+        }
+      }
       constexpr int NX = kSegKC + (SMOOTH1 ? 1 : 0);
       // raw chunk registers; the masks (k <= L, k < L) are applied at the use, so a prefetched chunk
       // is not waited for when it is issued
@@ -1304,8 +1334,8 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
       int aA[kSegKC], aB[kSegKC];
       if constexpr (kSegPF) {
         // two chunks in flight: chunk c + 1 is requested before chunk c is consumed (buffers alternate)
-        load(xA, aA, 0);
-        for (int k0 = 0; k0 < Lw;) {
+        load(xA, aA, kbeg);
+        for (int k0 = kbeg; k0 < Lw;) {
           if (k0 + kSegKC < Lw) load(xB, aB, k0 + kSegKC);
           process(xA, aA, k0);
           k0 += kSegKC;
@@ -1315,7 +1345,7 @@ gram_seg_kernel(const double* __restrict__ x, int64_t xsp, int64_t xsk, const in
           k0 += kSegKC;
         }
       } else {
-        for (int k0 = 0; k0 < Lw; k0 += kSegKC) {
+        for (int k0 = kbeg; k0 < Lw; k0 += kSegKC) {
           load(xA, aA, k0);
           process(xA, aA, k0);
         }
@@ -3514,9 +3544,16 @@ int launch_gram_seg(hipStream_t st, const double* x, int64_t xsp, int64_t xsk, c
                     int64_t ask, const int32_t* seq_len, int n_steps, const double* u, int64_t N, double inv_dt,
                     const LibDesc& lib, double* part, unsigned* cnt, const GramOut& out) {
   auto kern = gram_seg_kernel<NARM, SMOOTH1, STF>;
-  // one 64-patient tile per wave up to kSegMaxBlocks blocks: the dispatcher hands freed slots to the
-  // next block, which balances the tail better than a resident grid striding over 5-6 tiles per wave
-  const int64_t g = seg_grid(N);
+  // ranged: one resident round of waves, each with an equal contiguous range of (tile, chunk) units;
+  // otherwise one 64-patient tile per wave up to kSegMaxBlocks blocks (the dispatcher hands freed slots to the
+  // next block, which balanced the tail better than a resident grid striding over 5-6 whole tiles per wave)
+  int64_t g = seg_grid(N);
+  if (INSITE_SEG_RANGED) {
+    const int64_t units = (N + kWave - 1) / kWave * (((n_steps > 1 ? n_steps - 1 : 1) + kSegKC - 1) / kSegKC);
+    int64_t r = resident_waves(kern) / kWavesPerBlock;
+    if (r > (units + kWavesPerBlock - 1) / kWavesPerBlock) r = (units + kWavesPerBlock - 1) / kWavesPerBlock;
+    g = r < 1 ? 1 : (r > kSegMaxBlocks ? kSegMaxBlocks : r);
+  }
   kern<<<dim3((unsigned)g), kBlock, 0, st>>>(x, xsp, xsk, arm, asp, ask, seq_len, n_steps, u, N, inv_dt, lib, part,
                                              cnt, out);
   return (int)g;

@@ -64,6 +64,8 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     RKW8W5) NAME=$v build -DINSITE_RK45_WIN=8 -DINSITE_RK45_WPE=5 ;;
     RKW4W5) NAME=$v build -DINSITE_RK45_WIN=4 -DINSITE_RK45_WPE=5 ;;
     SEGKC8) NAME=$v build -DINSITE_SEG_KC=8 -DINSITE_SEG_WPE=3 ;;
+    SEGTILE) NAME=$v build -DINSITE_SEG_RANGED=0 ;;
+    SEGKC8R) NAME=$v build -DINSITE_SEG_KC=8 ;;
     SEGKC4) NAME=$v build -DINSITE_SEG_KC=4 -DINSITE_SEG_WPE=4 ;;
     SEGKC16) NAME=$v build -DINSITE_SEG_KC=16 -DINSITE_SEG_WPE=2 ;;
     SEGNOPF) NAME=$v build -DINSITE_SEG_PF=0 -DINSITE_SEG_WPE=4 ;;
