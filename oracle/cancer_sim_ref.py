@@ -205,16 +205,20 @@ def get_scaling_params(sim):
     return means, stds
 
 
-def process_data(sim, scaling, treatment_mode="multiclass", equation=None):
+def process_data(sim, scaling, treatment_mode="multiclass", equation=None, include_continuous_treatment=False):
     """SyntheticCancerDataset.process_data (dataset.py:96-185) for one-step-ahead data (continuous
-    dataset.py:96-200: EQ_5_A / B set the patient-type std to 1, their single type has std 0)."""
+    dataset.py:96-200: EQ_5_A / B set the patient-type std to 1, their single type has std 0).
+    ``include_continuous_treatment`` (what train_sindy.py:41-42 passes for every EQ_5 dataset): the scaled
+    chemo dosage is a third covariate channel, so static_features = [patient type, chemo dosage at t = 0]
+    and the model's dim_static_features becomes 2 (train_sindy.py:48)."""
     mean, std = dict(scaling[0]), dict(scaling[1])
     if equation in ("EQ_5_A", "EQ_5_B"):
         std["patient_types"] = 1
     offset = horizon = 1
     for k in ("chemo_application", "radio_application"):
         mean[k], std[k] = 0, 1
-    keys = ("cancer_volume", "patient_types", "chemo_application", "radio_application")
+    keys = ("cancer_volume", "patient_types") + (("chemo_dosage",) if include_continuous_treatment else ()) + \
+        ("chemo_application", "radio_application")
     input_means = np.array([mean[k] for k in keys], dtype=np.float64)
     input_stds = np.array([std[k] for k in keys], dtype=np.float64)
     data = dict(sim)
@@ -234,7 +238,11 @@ def process_data(sim, scaling, treatment_mode="multiclass", equation=None):
         data["current_treatments"] = treatments
     else:
         raise ValueError(treatment_mode)
-    cov = np.concatenate([cv[:, :-offset, None], pt[:, :-offset, None]], axis=-1)
+    cov = [cv[:, :-offset, None], pt[:, :-offset, None]]
+    if include_continuous_treatment:
+        cd = (sim["chemo_dosage"] - mean["chemo_dosage"]) / std["chemo_dosage"]
+        cov.append(cd[:, :-offset, None])
+    cov = np.concatenate(cov, axis=-1)
     outputs = cv[:, horizon:, None]
     active = np.zeros(outputs.shape)
     for i in range(sim["sequence_lengths"].shape[0]):
@@ -265,12 +273,13 @@ def make_train(seed=1, num_patients=1000, coeff=2.0, window_size=15, lag=0, seq_
 
 def de_format_segments(data, sp):
     """The device-side arrays the product's ``SINDY.de_format_segments`` builds (pkpd/utils.py:607-637):
-    x [N, T] = prev_outputs[:, 0] ++ unscaled_outputs (unscaled), u [N, 1] unscaled patient types,
+    x [N, T] = prev_outputs[:, 0] ++ unscaled_outputs (unscaled), u [N, U] unscaled statics (patient type; EQ_5 also the t = 0 chemo dosage),
     arm [N, T-1] = argmax(current_treatments), seq_len [N]."""
     std, mean = float(sp["output_stds"]), float(sp["output_means"])
     prev = data["prev_outputs"][..., 0] * std + mean
     x = np.concatenate([prev[:, :1], data["unscaled_outputs"][..., 0]], axis=1)
-    u = data["static_features"] * sp["inputs_stds"][1:2] + sp["input_means"][1:2]
+    U = data["static_features"].shape[-1]
+    u = data["static_features"] * sp["inputs_stds"][1:1 + U] + sp["input_means"][1:1 + U]
     arm = np.argmax(data["current_treatments"], axis=-1).astype(np.int64)
     return x, u, arm, data["sequence_lengths"].astype(np.int64)
 
@@ -286,6 +295,7 @@ def simulate_counterfactual_1_step(p, seq_length, rs):
     V = np.zeros((n_pts, seq_length))
     chemo_a = np.zeros((n_pts, seq_length))
     radio_a = np.zeros((n_pts, seq_length))
+    chemo_dose = np.zeros((n_pts, seq_length))
     sl = np.zeros(n_pts)
     ptypes = np.zeros(n_pts)
     idx = 0
@@ -320,6 +330,7 @@ def simulate_counterfactual_1_step(p, seq_length, rs):
             V[idx] = fV
             chemo_a[idx] = fchemo_a
             radio_a[idx] = fradio_a
+            chemo_dose[idx] = fchemo_d
             ptypes[idx] = p["patient_types"][i]
             sl[idx] = int(t) + 1
             idx += 1
@@ -334,6 +345,7 @@ def simulate_counterfactual_1_step(p, seq_length, rs):
                 V[idx][:t + 2] = np.append(fV[:t + 1], [cf_V])
                 chemo_a[idx][:t + 1] = np.append(fchemo_a[:t], [opt[0]])
                 radio_a[idx][:t + 1] = np.append(fradio_a[:t], [opt[1]])
+                chemo_dose[idx][:t + 1] = np.append(fchemo_d[:t], [cf_chemo_d])
                 ptypes[idx] = p["patient_types"][i]
                 sl[idx] = int(t) + 1
                 idx += 1
@@ -341,7 +353,7 @@ def simulate_counterfactual_1_step(p, seq_length, rs):
                 break
     V = _observation_noise(V, p, rs)[:idx]          # drawn over the whole preallocated array
     return {"cancer_volume": V, "chemo_application": chemo_a[:idx], "radio_application": radio_a[:idx],
-            "sequence_lengths": sl[:idx], "patient_types": ptypes[:idx]}
+            "chemo_dosage": chemo_dose[:idx], "sequence_lengths": sl[:idx], "patient_types": ptypes[:idx]}
 
 
 def simulate_counterfactuals_treatment_seq(p, seq_length, projection_horizon, rs, cf_seq_mode="sliding_treatment"):
@@ -360,6 +372,7 @@ def simulate_counterfactuals_treatment_seq(p, seq_length, projection_horizon, rs
     V = np.zeros((n_pts, seq_length + tau))
     chemo_a = np.zeros((n_pts, seq_length + tau))
     radio_a = np.zeros((n_pts, seq_length + tau))
+    chemo_dose = np.zeros((n_pts, seq_length + tau))
     sl = np.zeros(n_pts)
     ptypes = np.zeros(n_pts)
     pids = np.zeros(n_pts)
@@ -423,6 +436,7 @@ def simulate_counterfactuals_treatment_seq(p, seq_length, projection_horizon, rs
                 V[idx][:t + 1 + tau + 1] = cV
                 chemo_a[idx][:t + 1 + tau] = cchemo_a
                 radio_a[idx][:t + 1 + tau] = cradio_a
+                chemo_dose[idx][:t + 1 + tau] = cchemo_d
                 ptypes[idx] = p["patient_types"][i]
                 pids[idx] = i
                 pcur[idx] = t
@@ -432,7 +446,8 @@ def simulate_counterfactuals_treatment_seq(p, seq_length, projection_horizon, rs
                 break
     V = _observation_noise(V, p, rs)[:idx]          # drawn over the whole preallocated array
     return {"cancer_volume": V, "chemo_application": chemo_a[:idx], "radio_application": radio_a[:idx],
-            "sequence_lengths": sl[:idx], "patient_types": ptypes[:idx], "patient_ids_all_trajectories": pids[:idx],
+            "chemo_dosage": chemo_dose[:idx], "sequence_lengths": sl[:idx], "patient_types": ptypes[:idx],
+            "patient_ids_all_trajectories": pids[:idx],
             "patient_current_t": pcur[:idx]}
 
 
@@ -469,7 +484,7 @@ def make_collection(seed=1, num_patients=None, coeff=2.0, window_size=15, lag=0,
     scaling = get_scaling_params(sims["train"])
     out = {}
     for name, sim in sims.items():
-        data, sp = process_data(sim, scaling, treatment_mode, equation)
+        data, sp = process_data(sim, scaling, treatment_mode, equation, include_continuous_treatment=equation is not None)
         seq = R.process_sequential_test(data, sp, projection_horizon) if name == "test_cf_treatment_seq" else None
         out[name] = R.Subset(name, data, sp, seq, TUMOUR_DEATH_THRESHOLD)
     return out
@@ -484,10 +499,13 @@ def sindy_pipeline(coll, threshold=1e-3, alpha=0.5, dt=None, fd="order1"):
     tr = coll["train"]
     x, u, arm, sl = de_format_segments(tr.data, tr.scaling_params)
     joint, _, _, exps = S.sindy_fit_segments(x, u, arm, sl, dt, threshold, alpha, fd=fd)
-    res = {"joint_coefs": joint, "global_equation_string": S.global_equation_string(joint, ["1", "x0", "u0", "x0 u0"])}
+    U = u.shape[1]
+    names = R.library_names(exps, ["x0"] + [f"u{i}" for i in range(U)])
+    res = {"joint_coefs": joint, "exps": exps, "names": names,
+           "global_equation_string": S.global_equation_string(joint, names)}
 
     def predict(sub):
-        prev, st = R.unscale_inputs(sub.data, sub.scaling_params, 1, 1)
+        prev, st = R.unscale_inputs(sub.data, sub.scaling_params, 1, U)
         return R.rollout(prev[:, 0], st, np.argmax(sub.data["current_treatments"], axis=-1), joint, exps, dt, "euler5")
 
     norm = TUMOUR_DEATH_THRESHOLD

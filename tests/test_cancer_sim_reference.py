@@ -6,6 +6,12 @@ rollout, the reference's metrics) must reproduce the published runs
 ``results/2_main_table/final_with_insite.txt:6`` (cancer_sim), ``:54, :78, :102`` (EQ_5_B..D):
 16-digit equations to 1e-10 and every RMSE metric to 1e-11 relative.
 
+EQ_5 runs go through ``process_data_multi(include_continuous_treatment=True)`` (train_sindy.py:41-42): the
+chemo dosage is a third covariate, so the statics are [patient type, chemo dosage at t = 0] and the library
+over (x0, u0, u1) has 7 columns; the factual dosage at t = 0 is 0, the u1 columns are zero and their
+coefficients exactly 0 -- the logged strings omit |c| <= 1e-3 terms (pkpd/utils.py:387-391), so the log
+shows 4 terms per arm.
+
 EQ_5_A (``:30``): its single patient type makes the static column u0 == 1, so the library columns
 {1, u0} and {x0, x0 u0} coincide and pysindy's unbias lstsq is singular.  Arms 1 and 2 reproduce the log
 (where the logged solve landed on the minimum-norm split, equal halves, as here); arms 0 and 3 are logged
@@ -50,13 +56,15 @@ def pipeline(request):
 def test_segment_equation_and_metrics_equal_log(pipeline):
     eq, _, res = pipeline
     anchor = ANCHORS[f"{eq}/sindy"]
-    ref = logged_coefs(anchor["global_equation_string"])
+    names = res["names"]
+    ref = logged_coefs(anchor["global_equation_string"], names)
     got = res["joint_coefs"]
     arms = [1, 2] if eq == "EQ_5_A" else [0, 1, 2, 3]
     assert np.array_equal(got[arms] != 0, ref[arms] != 0)
     assert np.max(np.abs(got[arms] - ref[arms]) / np.maximum(1.0, np.abs(ref[arms]))) < 1e-10
     if eq == "EQ_5_A":       # the singular arms 0 / 3: the duplicated columns' halves are equal here
-        np.testing.assert_allclose(got[[0, 3]][:, [0, 1]], got[[0, 3]][:, [2, 3]], rtol=1e-9)
+        pair = [names.index("u0"), names.index("x0 u0")]
+        np.testing.assert_allclose(got[[0, 3]][:, [0, 1]], got[[0, 3]][:, pair], rtol=1e-9)
         return
     for k in METRICS:
         assert res[k] == pytest.approx(anchor[k], rel=1e-11), k
@@ -72,6 +80,13 @@ def test_cohort_layout(pipeline):
     assert coll["test_cf_treatment_seq"].data_processed_seq["outputs"].shape[1:] == (5, 1)
     assert coll["val"].scaling_params["output_means"] == tr.scaling_params["output_means"]
     assert tr.norm_const == pytest.approx(CS.calc_volume(13))
+    # EQ_5: statics [patient type, chemo dosage at t = 0] (continuous/dataset.py:112-117, 160-163, 191)
+    U = 1 if eq == "cancer_sim" else 2
+    assert tr.data["static_features"].shape == (1000, U)
+    assert len(tr.scaling_params["input_means"]) == 3 + U
+    if U == 2:
+        u = CS.de_format_segments(tr.data, tr.scaling_params)[1]
+        assert np.all(u[:, 1] == 0.0)           # the factual simulation doses from t = 1 (continuous.py:308)
 
 
 def test_one_ode_joint_model_equals_log():
