@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define INSITE_ABI_VERSION 6
+#define INSITE_ABI_VERSION 7
 
 /* status codes */
 #define INSITE_OK 0
@@ -384,6 +384,18 @@ int32_t insite_gen_gram_segments_f64(const double* x, int64_t ldx, const int8_t*
                                      int64_t n_patients, int32_t n_arms, const int8_t* exps, int32_t n_terms,
                                      int32_t fd_kind, double dt, double* G_out, double* b_out, void* workspace,
                                      size_t workspace_bytes, void* stream);
+
+/*
+ * INSITE layout preparation (ABI 7): the reference hands the refinement patient-major prev_outputs and
+ * per-step arms (sindy.py:555-566); the refinement kernels read time-major.  One pass writes
+ * Vt [T, ld_vt] from V [n_rows, ld_v] and, when arm [n_rows, ld_arm] is given, either the bit-packed
+ * arms arm_bits [T, ld_bits >= ceil(n_rows / 32)] (bit r & 31 of word r >> 5: arm != 0; the per-arm
+ * two-arm and joint two-input entries) or int8 arm_t [T, ld_armt] (exactly one of the two).  Replaces
+ * three torch copies and an int64 bit-pack of the reference-side transposes.
+ */
+int32_t insite_refine_prepare_f64(const double* V, int64_t ld_v, const int8_t* arm, int64_t ld_arm, int64_t n_rows,
+                                  int32_t T, double* Vt, int64_t ld_vt, uint32_t* arm_bits, int64_t ld_bits,
+                                  int8_t* arm_t, int64_t ld_armt, void* stream);
 
 /* INSITE refinement of ANY global model of the reference (ABI 5, csrc/insite_refine.hip): the joint
  * "one ODE" model (sindy.py:469-483, 503-517, 537-551: one coefficient row over a library whose inputs

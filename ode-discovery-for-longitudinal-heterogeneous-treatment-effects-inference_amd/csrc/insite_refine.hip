@@ -91,12 +91,16 @@ __device__ __forceinline__ double dpoly(const double (&g)[D + 1], double y) {
   return f;
 }
 
+#ifndef INSITE_REFINE_SU4
+#define INSITE_REFINE_SU4 5  // sub-step unroll of the M <= 4 kernel: 7.23 -> 7.03 ms INSITE step (profiles/r03/v30); 1 = rolled
+#endif
 template <int M, int NA, int D>
 struct RefineLane {
   static constexpr int RU = M <= kRefineRegActive ? M : 1;
   // sub-step loop unrolled by odeint's 5 (the default): measured 12 active 62 -> 43 ms, 6 active 5.5 -> 5.2 ms;
-  // for M = 4 (EQ_4 bench, 9.6 -> 10.1 ms) and dense models it is slower and stays rolled
-  static constexpr int SU = (M > 4 && M <= 16) ? 5 : 1;
+  // for M = 4 rolled was faster while the sub-step held per-lane selects (9.6 vs 10.1 ms); without them unrolled
+  // wins (INSITE_REFINE_SU4); dense models stay rolled
+  static constexpr int SU = (M > 4 && M <= 16) ? 5 : (M <= 4 ? INSITE_REFINE_SU4 : 1);
   const RefineArgs& ra;
   int64_t p;
   int K;
@@ -157,16 +161,18 @@ struct RefineLane {
           for (int e = 0; e <= D; ++e) gk[e] = gam[a][e];
       if constexpr (D == 1) {
         const double hb = h * gk[1];
+        // the step's arm selects its tangent's source term once per step, not per sub-step: an inactive arm
+        // adds +0.0 and 0 * y (bitwise the untouched value for finite y), so the sub-step loop has no
+        // per-lane selects (8 v_cndmask of 18 VALU per sub-step before)
+        double ha[NA];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) ha[a] = (ak == a) ? h : 0.0;
 #pragma unroll SU
         for (int s = 0; s < ra.sub; ++s) {
 #pragma unroll
           for (int a = 0; a < NA; ++a) {
-            d[a][0] = d[a][0] + hb * d[a][0];
-            d[a][1] = d[a][1] + hb * d[a][1];
-            if (ak == a) {
-              d[a][0] += h;
-              d[a][1] += h * y;
-            }
+            d[a][0] = (d[a][0] + hb * d[a][0]) + ha[a];
+            d[a][1] = (d[a][1] + hb * d[a][1]) + ha[a] * y;
           }
           y = y + h * (gk[0] + gk[1] * y);
         }
@@ -692,6 +698,74 @@ int32_t insite_refine_arms_f64(const double* V, int64_t ld_v, int32_t T, const i
   return refine_per_arm(V, ld_v, T, nullptr, arm ? arm : &kNoArms, ld_arm, u, seq_len, n_rows, n_statics, exps, n_terms, coef0,
                         n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds, ld_p, coef_out, status_out,
                         iters_out, row_order, stream);
+}
+
+// Layout preparation for the refinement (the reference hands over patient-major [N, T] prev_outputs and per-step
+// arms, sindy.py:555-566): one pass writes the time-major V [T, N] and the arms either bit-packed [T, ceil(N/32)]
+// (a wave ballots its 64 patients' bits per step: two words, no int64 intermediates) or int8 [T, N].  A wave owns
+// 64 patients and walks the steps in chunks of kPrepTc: the 64 x kPrepTc block is read row-segment by row-segment
+// (4 rows of 128 B per load instruction) into LDS, then every lane reads its own row back and each store is a
+// coalesced 512-B (64-B for int8) step row.  (A lane-per-row gather straight from HBM touched 64 lines per
+// load instruction: 1.58 ms for the 1M x 60 INSITE set.)
+namespace {
+constexpr int kPrepTc = 16;
+constexpr int kPrepLd = kPrepTc + 1;  // odd row stride: lane-per-row reads hit distinct banks
+__global__ void __launch_bounds__(kBlock) refine_prepare_kernel(const double* __restrict__ V, int64_t ld_v,
+                                                                const int8_t* __restrict__ arm, int64_t ld_arm,
+                                                                int64_t N, int32_t T, double* __restrict__ Vt,
+                                                                int64_t ld_vt, uint32_t* __restrict__ bits,
+                                                                int64_t ld_bits, int8_t* __restrict__ arm_t,
+                                                                int64_t ld_armt) {
+  __shared__ double sv[kWavesPerBlock][kWave * kPrepLd];
+  __shared__ int sa[kWavesPerBlock][kWave * kPrepLd];
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const int64_t p0 = (int64_t)blockIdx.x * kBlock + wv * kWave;  // the wave's first patient
+  const int64_t p = p0 + lane;
+  const bool act = p < N;
+  const int64_t w0 = p0 >> 5;  // the wave's two bit words
+  double* lv = sv[wv];
+  int* la = sa[wv];
+  for (int t0 = 0; t0 < T; t0 += kPrepTc) {
+    const int tc = T - t0 < kPrepTc ? T - t0 : kPrepTc;
+#pragma unroll 4
+    for (int j = 0; j < kWave * kPrepTc / kWave; ++j) {  // element e = j * 64 + lane of the 64 x kPrepTc block
+      const int e = j * kWave + lane, r = e / kPrepTc, c = e % kPrepTc;
+      const bool ok = c < tc && p0 + r < N;
+      const int64_t row = ok ? p0 + r : 0;
+      lv[r * kPrepLd + c] = ok ? V[row * ld_v + t0 + c] : 0.0;
+      if (arm) la[r * kPrepLd + c] = ok ? (int)arm[row * ld_arm + t0 + c] : 0;
+    }
+    __syncthreads();
+    for (int c = 0; c < tc; ++c) {
+      const int64_t t = t0 + c;
+      if (act) Vt[t * ld_vt + p] = lv[lane * kPrepLd + c];
+      if (arm) {
+        const int a = la[lane * kPrepLd + c];
+        if (bits) {
+          const unsigned long long m = __builtin_amdgcn_ballot_w64(act && a != 0);
+          if (lane < 2 && (w0 + lane) * 32 < N) bits[t * ld_bits + w0 + lane] = (uint32_t)(m >> (32 * lane));
+        } else if (act) {
+          arm_t[t * ld_armt + p] = (int8_t)a;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+}  // namespace
+
+extern "C" int32_t insite_refine_prepare_f64(const double* V, int64_t ld_v, const int8_t* arm, int64_t ld_arm,
+                                             int64_t n_rows, int32_t T, double* Vt, int64_t ld_vt, uint32_t* arm_bits,
+                                             int64_t ld_bits, int8_t* arm_t, int64_t ld_armt, void* stream) {
+  if (n_rows < 0 || T < 1 || !V || !Vt || ld_v < T || ld_vt < n_rows) return INSITE_E_INVALID_ARG;
+  if (arm && (ld_arm < T || (arm_bits == nullptr) == (arm_t == nullptr))) return INSITE_E_INVALID_ARG;
+  if (arm_bits && ld_bits < (n_rows + 31) / 32) return INSITE_E_INVALID_ARG;
+  if (arm_t && ld_armt < n_rows) return INSITE_E_INVALID_ARG;
+  if (n_rows == 0) return INSITE_OK;
+  const dim3 grid((unsigned)((n_rows + kBlock - 1) / kBlock));
+  refine_prepare_kernel<<<grid, kBlock, 0, static_cast<hipStream_t>(stream)>>>(
+      V, ld_v, arm, ld_arm, n_rows, T, Vt, ld_vt, arm ? arm_bits : nullptr, ld_bits, arm ? arm_t : nullptr, ld_armt);
+  return hipGetLastError() == hipSuccess ? INSITE_OK : INSITE_E_HIP;
 }
 
 int32_t insite_refine_general_f64(const double* V, int64_t ld_v, int32_t T, const uint32_t* arm_bits,

@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(LIB_DIR, "libinsite_hip.so")
 if os.environ.get("INSITE_LIB_OVERRIDE"):
     LIB_PATH = os.environ["INSITE_LIB_OVERRIDE"]
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # status codes / enums (insite_hip.h)
 INSITE_OK = 0
@@ -55,6 +55,7 @@ EXPORTS = (
     "insite_refine_f64",
     "insite_refine_arms_f64",
     "insite_refine_general_f64",
+    "insite_refine_prepare_f64",
     "insite_gen_gram_segments_workspace_bytes",
     "insite_gen_gram_segments_f64",
     "insite_masked_sse_workspace_bytes",
@@ -141,6 +142,8 @@ _SIGNATURES = {
     "insite_refine_general_f64": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _vp, _c_i64, _vp, _vp, _c_i64, _c_i32, _c_i32,
                                            _vp, _vp, _vp, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _c_i32, _vp, _c_i64,
                                            _vp, _vp, _vp, _vp, _vp, _vp]),
+    "insite_refine_prepare_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i64, _c_i32, _vp, _c_i64, _vp, _c_i64, _vp,
+                                           _c_i64, _vp]),
     "insite_gen_gram_segments_workspace_bytes": (_c_size, [_c_i64, _c_i32, _c_i32]),
     "insite_gen_gram_segments_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i32, _c_i64,
                                               _c_i32, _vp, _c_i32, _c_i32, _c_f64, _vp, _vp, _vp, _c_size, _vp]),

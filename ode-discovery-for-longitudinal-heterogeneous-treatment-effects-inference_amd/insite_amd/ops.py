@@ -901,13 +901,34 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
     mask, qexps, A = refine_terms(lib, c0.shape[0])
     if A > 4:
         raise ValueError("at most 4 treatment arms (joint model: 2 binary treatment inputs)")
-    Vt = V.t().contiguous()
-    arm_t = arm.t().contiguous()
-    arms = pack_arm_bits(arm_t, N) if A <= 2 else arm_t
+    Vt, arms = refine_prepare(V, arm, bits=A <= 2)
     order = rk45_order(seq_len, T) if (binned and N > 64) else None
     preds, coef, status, iters = insite_refine_tm(Vt, arms, u, seq_len, c0, lib, dt, lam, tau, substeps,
                                                   revert_on_zoom_fail, order=order, nfev=nfev)
     return preds.t(), coef, status, iters
+
+
+def refine_prepare(V: torch.Tensor, arm: torch.Tensor, bits: bool = True):
+    """Patient-major V [N, T] f64 and per-step arms [N, T] int8 -> the refinement kernels' time-major Vt [T, N] and
+    arms (bit-packed int32 [T, ceil(N / 32)] when ``bits``, else int8 [T, N]) in one device pass
+    (insite_refine_prepare_f64).  Bit-packing needs arm values 0 / 1 (checked here: two arms, or the joint
+    model's combination codes of one binary input)."""
+    _dev("V", V, torch.float64, 2)
+    _dev("arm", arm, torch.int8, 2)
+    N, T = V.shape
+    if arm.shape != (N, T) or V.stride(1) != 1 or arm.stride(1) != 1:
+        raise ValueError("V and arm must be row-contiguous [N, T]")
+    if bits and N and int(arm.amax().item()) > 1:
+        raise ValueError("bit-packed arms need n_arms <= 2 (arm values 0/1)")
+    Vt = torch.empty((T, N), dtype=torch.float64, device=V.device)
+    W = (N + 31) // 32
+    at = torch.empty((T, W) if bits else (T, N), dtype=torch.int32 if bits else torch.int8, device=V.device)
+    nul = ctypes.c_void_p(0)
+    st = _lib.load().insite_refine_prepare_f64(_p(V), V.stride(0), _p(arm), arm.stride(0), N, T, _p(Vt), N,
+                                               _p(at) if bits else nul, W, nul if bits else _p(at), N,
+                                               _stream(V.device))
+    _lib.check("insite_refine_prepare_f64", st)
+    return Vt, at
 
 
 def insite_refine_tm(Vt: torch.Tensor, arms: torch.Tensor, u: torch.Tensor, seq_len: torch.Tensor, coef0,

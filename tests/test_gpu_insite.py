@@ -253,3 +253,23 @@ def test_refine_binned_rows_bitwise_equal_identity_order(dev, n_arms):
     for a, b in zip(*outs):
         assert torch.equal(a, b)
     assert (outs[0][2][sl <= tau] == -1).all() and (outs[0][2][sl > tau] >= 0).all()
+
+
+@pytest.mark.parametrize("N,T", [(1, 7), (63, 60), (100, 60), (4097, 33)])
+def test_refine_prepare_layout_equals_torch(dev, N, T):
+    """insite_refine_prepare_f64 (ABI 7): one device pass from the reference's patient-major V / per-step arms to
+    the refinement's time-major V and bit-packed (or int8) arms, bitwise what the torch transposes and
+    ops.pack_arm_bits give, ragged N (partial words and waves) included; 2-valued arms for the bit mask."""
+    from insite_amd import ops
+    g = torch.Generator(device=dev)
+    g.manual_seed(N + T)
+    V = torch.randn((N, T), generator=g, device=dev, dtype=torch.float64)
+    arm2 = torch.randint(0, 2, (N, T), generator=g, device=dev, dtype=torch.int8)
+    Vt, bits = ops.refine_prepare(V, arm2, bits=True)
+    assert torch.equal(Vt, V.t().contiguous())
+    assert torch.equal(bits, ops.pack_arm_bits(arm2.t().contiguous(), N))
+    arm4 = torch.randint(0, 4, (N, T), generator=g, device=dev, dtype=torch.int8)
+    Vt4, a8 = ops.refine_prepare(V, arm4, bits=False)
+    assert torch.equal(Vt4, Vt) and torch.equal(a8, arm4.t().contiguous())
+    with pytest.raises(ValueError):
+        ops.refine_prepare(V, arm4 + 2, bits=True)
