@@ -606,19 +606,21 @@ def insite_main(args):
         torch.cuda.synchronize(dev)
         return (time.perf_counter() - t0) / args.steps * 1e3, r
 
-    ms_binned, _ = timed(True)
-    ms_step, (preds, coef, status, iters) = timed(False)
+    ms_identity, _ = timed(False)
+    ms_step, (preds, coef, status, iters) = timed(True)    # the product default: rows binned by seq_len
     st = status.cpu().numpy()
     it = iters.cpu().numpy()
-    # roofline: the refinement kernel alone on the time-major layout (no per-call transposes), HIP events on its
-    # stream; its work = every objective/gradient evaluation (nfev per row, counted by the kernel on one
-    # untimed launch through insite_refine_general_f64) x the row's K-step window x flops per sensitivity step
-    Vt = V.t().contiguous()
-    bits = ops.pack_arm_bits(arm.t().contiguous(), N)
+    # roofline: the refinement kernel alone on the step's binned time-major inputs (the layout pass excluded), HIP
+    # events on its stream; its work = every objective/gradient evaluation (nfev per row, counted by the kernel on
+    # one untimed launch through insite_refine_general_f64) x the row's K-step window x flops per sensitivity step
+    order = ops.rk45_order(sl, T)
+    idx = order.long()
+    Vt, bits = ops.refine_prepare(V, arm, bits=True, order=order)
+    u_l, sl_l = coh.u.index_select(0, idx).contiguous(), sl.index_select(0, idx).contiguous()
     kst = torch.cuda.current_stream(dev)
 
     def kern():
-        return ops.insite_refine_tm(Vt, bits, coh.u, sl, c0, coh.lib, dt, 10.0, 5)
+        return ops.insite_refine_tm(Vt, bits, u_l, sl_l, c0, coh.lib, dt, 10.0, 5)
 
     for _ in range(2):
         kern()
@@ -630,10 +632,10 @@ def insite_main(args):
     torch.cuda.synchronize(dev)
     kern_ms = e0.elapsed_time(e1) / args.steps
     nf = torch.empty((N,), dtype=torch.int32, device=dev)
-    p2, _, s2, i2 = ops.insite_refine_tm(Vt, bits, coh.u, sl, c0, coh.lib, dt, 10.0, 5, nfev=nf)
+    p2, _, s2, i2 = ops.insite_refine_tm(Vt, bits, u_l, sl_l, c0, coh.lib, dt, 10.0, 5, nfev=nf)
     torch.cuda.synchronize(dev)
-    same = bool(torch.equal(s2, status) and torch.equal(i2, iters) and torch.equal(p2.t(), preds))
-    K = torch.clamp(sl.to(torch.int64) - 5, min=0, max=T - 1)
+    same = bool(torch.equal(s2, status[idx]) and torch.equal(i2, iters[idx]) and torch.equal(p2.t(), preds[idx]))
+    K = torch.clamp(sl_l.to(torch.int64) - 5, min=0, max=T - 1)
     A_, SUB = 2, 5
     per_step = SUB * (4 * A_ + 7) + 4 * A_ + 5     # Euler sub-steps with the A x 2 sensitivities + residual/gradient
     refine_flop = float((nf.to(torch.int64) * K).sum().item()) * per_step
@@ -649,11 +651,12 @@ def insite_main(args):
                                f"{N // 1000}k rows", "rows": N, "T": T},
         "insite": {"refined_rows": int((st >= 0).sum()), "converged": int((st == 0).sum()),
                    "zoom_failed_fallback": int((st == 3).sum()), "mean_bfgs_iterations": float(it[st >= 0].mean()),
-                   "lane_order": "identity (lane = row: coalesced time-major V)",
-                   "binned_by_seq_len_ms_per_step": ms_binned,
+                   "lane_order": "rows binned by seq_len (device counting sort), gathered into lane order and "
+                                 "scattered back by insite_refine_prepare_f64 / insite_refine_finish_f64",
+                   "identity_lane_order_ms_per_step": ms_identity,
                    "reference_wall_time_s": "88.96 s per INSITE EQ_4_A run incl. 59,000 + 11,800 refinements "
                                             "(results/2_main_table/final_with_insite.txt:2346; SURVEY.md §6)",
-                   "mean_evaluations_per_refined_row": float(nf.to(torch.float64)[status >= 0].mean().item()),
+                   "mean_evaluations_per_refined_row": float(nf.to(torch.float64)[s2 >= 0].mean().item()),
                    "evaluation_count_route_matches": same},
         "roofline": {"kernel": "insite_refine_kernel<4, 2, 1> (per-row BFGS + final Euler-5 scan)", "bound": "valu-f64",
                      "unit": "TFLOP/s", "achieved": flop / (kern_ms * 1e-3) / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
@@ -665,7 +668,7 @@ def insite_main(args):
                                     "the final scan; nfev from the kernel's own count (insite_refine_general_f64)",
                      "algorithmic_bytes": kbytes, "achieved_GBps": kbytes / (kern_ms * 1e-3) / 1e9,
                      "avg_ms_source": "HIP events on the launch stream around args.steps back-to-back launches of "
-                                      "the time-major entry (the step's transposes excluded)"},
+                                      "the time-major entry on the step's binned inputs (layout passes excluded)"},
     }
     if cpu is not None:
         out["cpu_baseline"] = cpu

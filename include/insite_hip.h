@@ -391,11 +391,20 @@ int32_t insite_gen_gram_segments_f64(const double* x, int64_t ldx, const int8_t*
  * Vt [T, ld_vt] from V [n_rows, ld_v] and, when arm [n_rows, ld_arm] is given, either the bit-packed
  * arms arm_bits [T, ld_bits >= ceil(n_rows / 32)] (bit r & 31 of word r >> 5: arm != 0; the per-arm
  * two-arm and joint two-input entries) or int8 arm_t [T, ld_armt] (exactly one of the two).  Replaces
- * three torch copies and an int64 bit-pack of the reference-side transposes.
+ * three torch copies and an int64 bit-pack of the reference-side transposes.  row_order [n_rows] (may be NULL):
+ * output column l takes row row_order[l] (rows binned by sequence length, so a wave's lanes scan similar
+ * prefixes while every kernel load stays coalesced); the refinement then runs with the identity lane order
+ * on the permuted inputs, and insite_refine_finish_f64 scatters its predictions back.
  */
 int32_t insite_refine_prepare_f64(const double* V, int64_t ld_v, const int8_t* arm, int64_t ld_arm, int64_t n_rows,
                                   int32_t T, double* Vt, int64_t ld_vt, uint32_t* arm_bits, int64_t ld_bits,
-                                  int8_t* arm_t, int64_t ld_armt, void* stream);
+                                  int8_t* arm_t, int64_t ld_armt, const int32_t* row_order, void* stream);
+
+/* The inverse of insite_refine_prepare_f64 for the refinement's predictions (ABI 7): time-major preds_tm
+ * [T, ld_t] whose column l is row row_order[l] (identity when NULL) -> patient-major preds_pm [n_rows, ld_pm],
+ * the layout the reference's predictions come in (sindy.py:658-665). */
+int32_t insite_refine_finish_f64(const double* preds_tm, int64_t ld_t, const int32_t* row_order, int64_t n_rows,
+                                 int32_t T, double* preds_pm, int64_t ld_pm, void* stream);
 
 /* INSITE refinement of ANY global model of the reference (ABI 5, csrc/insite_refine.hip): the joint
  * "one ODE" model (sindy.py:469-483, 503-517, 537-551: one coefficient row over a library whose inputs

@@ -715,7 +715,7 @@ __global__ void __launch_bounds__(kBlock) refine_prepare_kernel(const double* __
                                                                 int64_t N, int32_t T, double* __restrict__ Vt,
                                                                 int64_t ld_vt, uint32_t* __restrict__ bits,
                                                                 int64_t ld_bits, int8_t* __restrict__ arm_t,
-                                                                int64_t ld_armt) {
+                                                                int64_t ld_armt, const int32_t* __restrict__ order) {
   __shared__ double sv[kWavesPerBlock][kWave * kPrepLd];
   __shared__ int sa[kWavesPerBlock][kWave * kPrepLd];
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
@@ -731,7 +731,7 @@ __global__ void __launch_bounds__(kBlock) refine_prepare_kernel(const double* __
     for (int j = 0; j < kWave * kPrepTc / kWave; ++j) {  // element e = j * 64 + lane of the 64 x kPrepTc block
       const int e = j * kWave + lane, r = e / kPrepTc, c = e % kPrepTc;
       const bool ok = c < tc && p0 + r < N;
-      const int64_t row = ok ? p0 + r : 0;
+      const int64_t row = ok ? (order ? (int64_t)order[p0 + r] : p0 + r) : 0;
       lv[r * kPrepLd + c] = ok ? V[row * ld_v + t0 + c] : 0.0;
       if (arm) la[r * kPrepLd + c] = ok ? (int)arm[row * ld_arm + t0 + c] : 0;
     }
@@ -752,11 +752,49 @@ __global__ void __launch_bounds__(kBlock) refine_prepare_kernel(const double* __
     __syncthreads();
   }
 }
+
+// The inverse for the refinement's outputs: time-major preds [T, ld_t] whose column l is row order[l] (or l) ->
+// the reference's patient-major [N, ld_pm].  Same staging: coalesced 512-B step rows into LDS, then each load /
+// store instruction writes 4 patients' 128-B row segments.
+__global__ void __launch_bounds__(kBlock) refine_finish_kernel(const double* __restrict__ P, int64_t ld_t,
+                                                               const int32_t* __restrict__ order, int64_t N, int32_t T,
+                                                               double* __restrict__ out, int64_t ld_pm) {
+  __shared__ double sv[kWavesPerBlock][kWave * kPrepLd];
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const int64_t p0 = (int64_t)blockIdx.x * kBlock + wv * kWave;
+  const int64_t l = p0 + lane;
+  double* lv = sv[wv];
+  for (int t0 = 0; t0 < T; t0 += kPrepTc) {
+    const int tc = T - t0 < kPrepTc ? T - t0 : kPrepTc;
+    for (int c = 0; c < tc; ++c) lv[lane * kPrepLd + c] = l < N ? P[(int64_t)(t0 + c) * ld_t + l] : 0.0;
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < kPrepTc; ++j) {
+      const int e = j * kWave + lane, r = e / kPrepTc, c = e % kPrepTc;
+      if (c < tc && p0 + r < N) {
+        const int64_t row = order ? (int64_t)order[p0 + r] : p0 + r;
+        out[row * ld_pm + t0 + c] = lv[r * kPrepLd + c];
+      }
+    }
+    __syncthreads();
+  }
+}
 }  // namespace
+
+extern "C" int32_t insite_refine_finish_f64(const double* preds_tm, int64_t ld_t, const int32_t* row_order,
+                                            int64_t n_rows, int32_t T, double* preds_pm, int64_t ld_pm, void* stream) {
+  if (n_rows < 0 || T < 1 || !preds_tm || !preds_pm || ld_t < n_rows || ld_pm < T) return INSITE_E_INVALID_ARG;
+  if (n_rows == 0) return INSITE_OK;
+  const dim3 grid((unsigned)((n_rows + kBlock - 1) / kBlock));
+  refine_finish_kernel<<<grid, kBlock, 0, static_cast<hipStream_t>(stream)>>>(preds_tm, ld_t, row_order, n_rows, T,
+                                                                              preds_pm, ld_pm);
+  return hipGetLastError() == hipSuccess ? INSITE_OK : INSITE_E_HIP;
+}
 
 extern "C" int32_t insite_refine_prepare_f64(const double* V, int64_t ld_v, const int8_t* arm, int64_t ld_arm,
                                              int64_t n_rows, int32_t T, double* Vt, int64_t ld_vt, uint32_t* arm_bits,
-                                             int64_t ld_bits, int8_t* arm_t, int64_t ld_armt, void* stream) {
+                                             int64_t ld_bits, int8_t* arm_t, int64_t ld_armt,
+                                             const int32_t* row_order, void* stream) {
   if (n_rows < 0 || T < 1 || !V || !Vt || ld_v < T || ld_vt < n_rows) return INSITE_E_INVALID_ARG;
   if (arm && (ld_arm < T || (arm_bits == nullptr) == (arm_t == nullptr))) return INSITE_E_INVALID_ARG;
   if (arm_bits && ld_bits < (n_rows + 31) / 32) return INSITE_E_INVALID_ARG;
@@ -764,7 +802,8 @@ extern "C" int32_t insite_refine_prepare_f64(const double* V, int64_t ld_v, cons
   if (n_rows == 0) return INSITE_OK;
   const dim3 grid((unsigned)((n_rows + kBlock - 1) / kBlock));
   refine_prepare_kernel<<<grid, kBlock, 0, static_cast<hipStream_t>(stream)>>>(
-      V, ld_v, arm, ld_arm, n_rows, T, Vt, ld_vt, arm ? arm_bits : nullptr, ld_bits, arm ? arm_t : nullptr, ld_armt);
+      V, ld_v, arm, ld_arm, n_rows, T, Vt, ld_vt, arm ? arm_bits : nullptr, ld_bits, arm ? arm_t : nullptr, ld_armt,
+      row_order);
   return hipGetLastError() == hipSuccess ? INSITE_OK : INSITE_E_HIP;
 }
 

@@ -56,6 +56,7 @@ EXPORTS = (
     "insite_refine_arms_f64",
     "insite_refine_general_f64",
     "insite_refine_prepare_f64",
+    "insite_refine_finish_f64",
     "insite_gen_gram_segments_workspace_bytes",
     "insite_gen_gram_segments_f64",
     "insite_masked_sse_workspace_bytes",
@@ -143,7 +144,8 @@ _SIGNATURES = {
                                            _vp, _vp, _vp, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _c_i32, _vp, _c_i64,
                                            _vp, _vp, _vp, _vp, _vp, _vp]),
     "insite_refine_prepare_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i64, _c_i32, _vp, _c_i64, _vp, _c_i64, _vp,
-                                           _c_i64, _vp]),
+                                           _c_i64, _vp, _vp]),
+    "insite_refine_finish_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _vp, _c_i64, _vp]),
     "insite_gen_gram_segments_workspace_bytes": (_c_size, [_c_i64, _c_i32, _c_i32]),
     "insite_gen_gram_segments_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i32, _c_i64,
                                               _c_i32, _vp, _c_i32, _c_i32, _c_f64, _vp, _vp, _vp, _c_size, _vp]),

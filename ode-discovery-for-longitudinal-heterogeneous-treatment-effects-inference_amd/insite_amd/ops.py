@@ -867,7 +867,7 @@ def refine_terms(lib: PolyLibrary, n_coef_rows: int):
 
 def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: torch.Tensor, coef0: np.ndarray,
                   lib: PolyLibrary, dt: float, lam: float, tau: int, substeps: int = 5,
-                  revert_on_zoom_fail: bool = False, binned: bool = False, nfev: torch.Tensor | None = None):
+                  revert_on_zoom_fail: bool = False, binned: bool = True, nfev: torch.Tensor | None = None):
     """INSITE per-patient refinement (reference sindy.py:433-715).  V [N, T] f64 unscaled observations
     and arm [N, T] int8 per-step arms in the reference's patient-major layout (transposed to the
     kernel's time-major layout here), u [N, U], seq_len [N], coef0 the HOST global model [A, F].
@@ -879,8 +879,9 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
     sindy.py:628-631 reads; the default (False) keeps the iterate, which reproduces the reference's published
     runs.  ``binned``: lanes take the rows sorted by seq_len (insite_rk45_order_i32 on the
     device), so a wave's objective scans have similar lengths; scheduling only, the outputs are bitwise the
-    same.  Off by default: on the time-major V the binned lanes' scattered loads cost more than the shorter
-    scans save (1M rows, seq_len U{1..59}: 10.7 vs 9.5 ms, profiles/r02/v10_insite_bench.log).
+    same.  The rows are gathered in lane order by insite_refine_prepare_f64 and the predictions scattered back
+    by insite_refine_finish_f64, so every kernel access stays coalesced (round 2's lane -> row indirection
+    inside the kernel scattered them: 10.7 vs 9.5 ms).
     ``nfev``: an int32 [N] device tensor receiving each row's objective/gradient evaluation count (the work
     count behind bench.py's INSITE roofline); it routes every model through insite_refine_general_f64 (the
     same kernels and arithmetic as the per-arm entry points).
@@ -901,18 +902,30 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
     mask, qexps, A = refine_terms(lib, c0.shape[0])
     if A > 4:
         raise ValueError("at most 4 treatment arms (joint model: 2 binary treatment inputs)")
-    Vt, arms = refine_prepare(V, arm, bits=A <= 2)
     order = rk45_order(seq_len, T) if (binned and N > 64) else None
-    preds, coef, status, iters = insite_refine_tm(Vt, arms, u, seq_len, c0, lib, dt, lam, tau, substeps,
-                                                  revert_on_zoom_fail, order=order, nfev=nfev)
-    return preds.t(), coef, status, iters
+    Vt, arms = refine_prepare(V, arm, bits=A <= 2, order=order)
+    if order is None:
+        preds, coef, status, iters = insite_refine_tm(Vt, arms, u, seq_len, c0, lib, dt, lam, tau, substeps,
+                                                      revert_on_zoom_fail, nfev=nfev)
+        return preds.t(), coef, status, iters
+    # binned: the inputs were gathered in lane order, the kernel runs the identity order on them (coalesced
+    # loads and stores), and the outputs are scattered back to row order
+    idx = order.long()
+    u_l = u.index_select(0, idx).contiguous() if lib.n_statics else u
+    nf = torch.empty_like(nfev) if nfev is not None else None
+    preds, coef, status, iters = insite_refine_tm(Vt, arms, u_l, seq_len.index_select(0, idx).contiguous(), c0, lib,
+                                                  dt, lam, tau, substeps, revert_on_zoom_fail, nfev=nf)
+    back = lambda t: torch.empty_like(t).index_copy_(0, idx, t)   # noqa: E731
+    if nfev is not None:
+        nfev.index_copy_(0, idx, nf)
+    return refine_finish(preds, order, N), back(coef), back(status), back(iters)
 
 
-def refine_prepare(V: torch.Tensor, arm: torch.Tensor, bits: bool = True):
+def refine_prepare(V: torch.Tensor, arm: torch.Tensor, bits: bool = True, order: torch.Tensor | None = None):
     """Patient-major V [N, T] f64 and per-step arms [N, T] int8 -> the refinement kernels' time-major Vt [T, N] and
     arms (bit-packed int32 [T, ceil(N / 32)] when ``bits``, else int8 [T, N]) in one device pass
     (insite_refine_prepare_f64).  Bit-packing needs arm values 0 / 1 (checked here: two arms, or the joint
-    model's combination codes of one binary input)."""
+    model's combination codes of one binary input).  ``order`` [N] int32: output column l takes row order[l]."""
     _dev("V", V, torch.float64, 2)
     _dev("arm", arm, torch.int8, 2)
     N, T = V.shape
@@ -924,11 +937,30 @@ def refine_prepare(V: torch.Tensor, arm: torch.Tensor, bits: bool = True):
     W = (N + 31) // 32
     at = torch.empty((T, W) if bits else (T, N), dtype=torch.int32 if bits else torch.int8, device=V.device)
     nul = ctypes.c_void_p(0)
+    if order is not None:
+        _dev("order", order, torch.int32, 1)
+        if order.numel() != N:
+            raise ValueError("order must be an [N] permutation")
     st = _lib.load().insite_refine_prepare_f64(_p(V), V.stride(0), _p(arm), arm.stride(0), N, T, _p(Vt), N,
-                                               _p(at) if bits else nul, W, nul if bits else _p(at), N,
+                                               _p(at) if bits else nul, W, nul if bits else _p(at), N, _p(order),
                                                _stream(V.device))
     _lib.check("insite_refine_prepare_f64", st)
     return Vt, at
+
+
+def refine_finish(P: torch.Tensor, order: torch.Tensor | None, N: int) -> torch.Tensor:
+    """Time-major refinement predictions P [T, >= N] whose column l is row order[l] (identity when None) ->
+    patient-major [N, T] (insite_refine_finish_f64)."""
+    _dev("P", P, torch.float64, 2)
+    T = P.size(0)
+    if P.size(1) < N or P.stride(1) != 1:
+        raise ValueError("P must be row-contiguous [T, >= N]")
+    if order is not None:
+        _dev("order", order, torch.int32, 1)
+    out = torch.empty((N, T), dtype=torch.float64, device=P.device)
+    st = _lib.load().insite_refine_finish_f64(_p(P), P.stride(0), _p(order), N, T, _p(out), T, _stream(P.device))
+    _lib.check("insite_refine_finish_f64", st)
+    return out
 
 
 def insite_refine_tm(Vt: torch.Tensor, arms: torch.Tensor, u: torch.Tensor, seq_len: torch.Tensor, coef0,

@@ -38,7 +38,7 @@ def _lib_exports():
 def test_header_declares_the_abi():
     fns = _header_functions()
     assert "insite_rollout_f64" in fns and "insite_sindy_fit_f64" in fns
-    assert len(fns) == 40 and set(fns) == set(_lib_exports())
+    assert len(fns) == 41 and set(fns) == set(_lib_exports())
 
 
 def test_library_exports_every_header_symbol(L):

@@ -273,3 +273,22 @@ def test_refine_prepare_layout_equals_torch(dev, N, T):
     assert torch.equal(Vt4, Vt) and torch.equal(a8, arm4.t().contiguous())
     with pytest.raises(ValueError):
         ops.refine_prepare(V, arm4 + 2, bits=True)
+
+
+@pytest.mark.parametrize("N,T", [(5, 7), (100, 60), (4097, 33)])
+def test_refine_prepare_finish_with_row_order(dev, N, T):
+    """Binned layout (ABI 7): insite_refine_prepare_f64 with a row order gathers row order[l] into column l, and
+    insite_refine_finish_f64 scatters time-major columns back to patient-major rows -- bitwise torch indexing."""
+    from insite_amd import ops
+    g = torch.Generator(device=dev)
+    g.manual_seed(7 * N + T)
+    V = torch.randn((N, T), generator=g, device=dev, dtype=torch.float64)
+    arm = torch.randint(0, 2, (N, T), generator=g, device=dev, dtype=torch.int8)
+    order = torch.randperm(N, generator=g, device=dev).to(torch.int32)
+    Vt, bits = ops.refine_prepare(V, arm, bits=True, order=order)
+    idx = order.long()
+    assert torch.equal(Vt, V[idx].t().contiguous())
+    assert torch.equal(bits, ops.pack_arm_bits(arm[idx].t().contiguous(), N))
+    back = ops.refine_finish(Vt, order, N)
+    assert torch.equal(back, V)
+    assert torch.equal(ops.refine_finish(V.t().contiguous(), None, N), V)
