@@ -2885,9 +2885,11 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
   // start of a step (rk.py _step_impl): min_step = 10 |nextafter(t, inf) - t|, the neighbour taken on the
   // bit pattern of |t| (+1 above a non-negative t, -1 below |t| for a negative one)
   auto min_step = [&]() {
+    // |neighbour - |t||: the same two values as the two-sided form, as one select on the bit step (the
+    // two-sided expression compiled to an exec-mask branch per accepted attempt)
     const double at = fabs(t);
     const long long tb = __double_as_longlong(at);
-    return 10.0 * (t >= 0.0 ? __longlong_as_double(tb + 1ll) - at : at - __longlong_as_double(tb - 1ll));
+    return 10.0 * fabs(__longlong_as_double(tb + (t >= 0.0 ? 1ll : -1ll)) - at);
   };
   bool live = false;
   if (act && 1 < n) {
