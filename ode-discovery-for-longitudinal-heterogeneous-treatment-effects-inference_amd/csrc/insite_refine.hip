@@ -779,12 +779,79 @@ __global__ void __launch_bounds__(kBlock) refine_finish_kernel(const double* __r
     __syncthreads();
   }
 }
+
+// T <= 64 (the reference's sequences: 60 steps): one wave per block stages its 64 patients' WHOLE rows, so every
+// cache line of V is consumed in one phase (the chunked form re-touched the lines a row segment shares with the
+// next chunk after they had left the L2).  Load: one instruction per patient row (lanes = steps, up to 512 B
+// contiguous); store: one instruction per step (lanes = patients, 512 B).  Measured slower than the chunked
+// 4-wave form (INSITE step 5.03 vs 4.69 ms, profiles/r03/v37_insite_variants.txt: one wave per block at 35 KB of
+// LDS leaves 4 waves per CU), so off by default; INSITE_PREP_ROWS=1 selects it for T <= 64.
+#ifndef INSITE_PREP_ROWS
+#define INSITE_PREP_ROWS 0
+#endif
+constexpr int kRowLd = kWave + 1;
+__global__ void __launch_bounds__(kWave) refine_prepare_rows_kernel(const double* __restrict__ V, int64_t ld_v,
+                                                                    const int8_t* __restrict__ arm, int64_t ld_arm,
+                                                                    int64_t N, int32_t T, double* __restrict__ Vt,
+                                                                    int64_t ld_vt, uint32_t* __restrict__ bits,
+                                                                    int64_t ld_bits, int8_t* __restrict__ arm_t,
+                                                                    int64_t ld_armt, const int32_t* __restrict__ order) {
+  __shared__ double lv[kWave * kRowLd];
+  __shared__ int8_t la[kWave * kRowLd];
+  const int lane = threadIdx.x;
+  const int64_t p0 = (int64_t)blockIdx.x * kWave;
+  const int nr = N - p0 < kWave ? (int)(N - p0) : kWave;
+  for (int r = 0; r < nr; ++r) {
+    const int64_t row = order ? (int64_t)order[p0 + r] : p0 + r;
+    if (lane < T) {
+      lv[r * kRowLd + lane] = V[row * ld_v + lane];
+      if (arm) la[r * kRowLd + lane] = arm[row * ld_arm + lane];
+    }
+  }
+  __syncthreads();
+  const int64_t p = p0 + lane;
+  const bool act = lane < nr;
+  const int64_t w0 = p0 >> 5;
+  for (int t = 0; t < T; ++t) {
+    if (act) Vt[(int64_t)t * ld_vt + p] = lv[lane * kRowLd + t];
+    if (arm) {
+      const int a = act ? (int)la[lane * kRowLd + t] : 0;
+      if (bits) {
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(act && a != 0);
+        if (lane < 2 && (w0 + lane) * 32 < N) bits[(int64_t)t * ld_bits + w0 + lane] = (uint32_t)(m >> (32 * lane));
+      } else if (act) {
+        arm_t[(int64_t)t * ld_armt + p] = (int8_t)a;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kWave) refine_finish_rows_kernel(const double* __restrict__ P, int64_t ld_t,
+                                                                   const int32_t* __restrict__ order, int64_t N,
+                                                                   int32_t T, double* __restrict__ out, int64_t ld_pm) {
+  __shared__ double lv[kWave * kRowLd];
+  const int lane = threadIdx.x;
+  const int64_t p0 = (int64_t)blockIdx.x * kWave;
+  const int nr = N - p0 < kWave ? (int)(N - p0) : kWave;
+  if (lane < nr)
+    for (int t = 0; t < T; ++t) lv[lane * kRowLd + t] = P[(int64_t)t * ld_t + p0 + lane];
+  __syncthreads();
+  for (int r = 0; r < nr; ++r) {
+    const int64_t row = order ? (int64_t)order[p0 + r] : p0 + r;
+    if (lane < T) out[row * ld_pm + lane] = lv[r * kRowLd + lane];
+  }
+}
 }  // namespace
 
 extern "C" int32_t insite_refine_finish_f64(const double* preds_tm, int64_t ld_t, const int32_t* row_order,
                                             int64_t n_rows, int32_t T, double* preds_pm, int64_t ld_pm, void* stream) {
   if (n_rows < 0 || T < 1 || !preds_tm || !preds_pm || ld_t < n_rows || ld_pm < T) return INSITE_E_INVALID_ARG;
   if (n_rows == 0) return INSITE_OK;
+  if (INSITE_PREP_ROWS && T <= kWave) {
+    refine_finish_rows_kernel<<<dim3((unsigned)((n_rows + kWave - 1) / kWave)), kWave, 0,
+                                static_cast<hipStream_t>(stream)>>>(preds_tm, ld_t, row_order, n_rows, T, preds_pm, ld_pm);
+    return hipGetLastError() == hipSuccess ? INSITE_OK : INSITE_E_HIP;
+  }
   const dim3 grid((unsigned)((n_rows + kBlock - 1) / kBlock));
   refine_finish_kernel<<<grid, kBlock, 0, static_cast<hipStream_t>(stream)>>>(preds_tm, ld_t, row_order, n_rows, T,
                                                                               preds_pm, ld_pm);
@@ -800,6 +867,13 @@ extern "C" int32_t insite_refine_prepare_f64(const double* V, int64_t ld_v, cons
   if (arm_bits && ld_bits < (n_rows + 31) / 32) return INSITE_E_INVALID_ARG;
   if (arm_t && ld_armt < n_rows) return INSITE_E_INVALID_ARG;
   if (n_rows == 0) return INSITE_OK;
+  if (INSITE_PREP_ROWS && T <= kWave) {
+    refine_prepare_rows_kernel<<<dim3((unsigned)((n_rows + kWave - 1) / kWave)), kWave, 0,
+                                 static_cast<hipStream_t>(stream)>>>(
+        V, ld_v, arm, ld_arm, n_rows, T, Vt, ld_vt, arm ? arm_bits : nullptr, ld_bits, arm ? arm_t : nullptr, ld_armt,
+        row_order);
+    return hipGetLastError() == hipSuccess ? INSITE_OK : INSITE_E_HIP;
+  }
   const dim3 grid((unsigned)((n_rows + kBlock - 1) / kBlock));
   refine_prepare_kernel<<<grid, kBlock, 0, static_cast<hipStream_t>(stream)>>>(
       V, ld_v, arm, ld_arm, n_rows, T, Vt, ld_vt, arm ? arm_bits : nullptr, ld_bits, arm ? arm_t : nullptr, ld_armt,

@@ -103,6 +103,7 @@ for v in ${VARIANTS:-NOSTORE NOARM RT16 RT64}; do
     RWPE6) NAME=$v build -DINSITE_REFINE_WPE4=6 ;;
     RWPE8) NAME=$v build -DINSITE_REFINE_WPE4=8 ;;
     RSU1) NAME=$v build -DINSITE_REFINE_SU4=1 ;;
+    PREPROWS) NAME=$v build -DINSITE_PREP_ROWS=1 ;;
     RSU1W5) NAME=$v build -DINSITE_REFINE_SU4=1 -DINSITE_REFINE_WPE4=5 ;;
     KWPE5) NAME=$v build -DINSITE_RK45_WPE=5 ;;
     RW8_2) NAME=$v build -DINSITE_REFINE_WPE8=2 ;;
