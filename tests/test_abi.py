@@ -194,6 +194,10 @@ def test_ops_refuse_host_tensors(L):
                     torch.zeros((4, 10), dtype=torch.int8), torch.zeros((2, 7), dtype=torch.float64), lib, 0.1)
     with pytest.raises(ValueError, match="device tensor"):
         ops.stlsq(torch.eye(7, dtype=torch.float64)[None], torch.zeros((1, 7), dtype=torch.float64), 0.1, 0.5)
+    with pytest.raises(ValueError, match="device tensor"):
+        ops.refine_prepare(torch.zeros((4, 10), dtype=torch.float64), torch.zeros((4, 10), dtype=torch.int8))
+    with pytest.raises(ValueError, match="device tensor"):
+        ops.refine_finish(torch.zeros((10, 4), dtype=torch.float64), None, 4)
 
 
 def test_missing_library_fails_loudly(tmp_path):
