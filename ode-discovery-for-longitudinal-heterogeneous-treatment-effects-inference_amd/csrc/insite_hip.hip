@@ -2771,6 +2771,9 @@ rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
 #ifndef INSITE_RK45_STAGE
 #define INSITE_RK45_STAGE 1
 #endif
+#ifndef INSITE_RK45_MINSTEP_BRANCH
+#define INSITE_RK45_MINSTEP_BRANCH 0
+#endif
 #ifndef INSITE_RK45_CLOSE_BRANCH
 #define INSITE_RK45_CLOSE_BRANCH 0  // 1: round 2's close block under `if (close)` (A/B)
 #endif
@@ -2889,7 +2892,11 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
     // two-sided expression compiled to an exec-mask branch per accepted attempt)
     const double at = fabs(t);
     const long long tb = __double_as_longlong(at);
+#if INSITE_RK45_MINSTEP_BRANCH  // A/B: the two-sided form
+    return 10.0 * (t >= 0.0 ? __longlong_as_double(tb + 1ll) - at : at - __longlong_as_double(tb - 1ll));
+#else
     return 10.0 * fabs(__longlong_as_double(tb + (t >= 0.0 ? 1ll : -1ll)) - at);
+#endif
   };
   bool live = false;
   if (act && 1 < n) {
