@@ -48,11 +48,13 @@ def parse():
     ap.add_argument("--arm-format", default="bits", choices=["bits", "int8"],
                     help="per-step arms of the time-major rollout: 1-bit mask (A <= 2) or int8")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", default=None, choices=["deferred", "fused", "graph", "seq", "pipeline"],
+    ap.add_argument("--mode", default=None, choices=["deferred", "lagged", "fused", "graph", "seq", "pipeline"],
                     help="deferred (default at N = 1) / fused: ONE launch per step -- the discovery of step i and "
                          "the rollout of step i-1 in the same launch; deferred: the same with the discovery's "
-                         "reduction + STLSQ moved into the next launch (step_deferred_kernel); pipeline (default at N > 1, where the RCCL "
-                         "all-reduce sits between the gram and STLSQ): discovery | rollout on two streams, "
+                         "reduction + STLSQ moved into the next launch (step_deferred_kernel); lagged (default at "
+                         "N > 1, where the RCCL all-reduce sits between the gram and STLSQ): the deferred kernel with "
+                         "the reduction and the STLSQ in separate roles, one all-reduce per --pipe-k launches on the "
+                         "launch stream; pipeline: discovery | rollout on two streams, "
                          "consecutive steps overlapped; seq: eager launches on one stream; graph: the seq step in a "
                          "HIP graph")
     ap.add_argument("--stlsq-stream", default="discovery", choices=["discovery", "rollout"],
@@ -72,6 +74,7 @@ def parse():
                          "library's default split)")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the benched cohort (C2)")
     ap.add_argument("--force-collective", action="store_true",
                     help="C2 at N = 1: join a single-rank RCCL process group and run the N > 1 pipeline's data path "
                          "(gram, one bucketed all_reduce per batch, STLSQ) so the collective and the process "
@@ -368,7 +371,7 @@ def c3_main(args):
                     "frac": roll_bytes / (roll_ms_t * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                     "dense_kernel_avg_launch_ms": roll_dense_t},
     }
-    print(json.dumps(out))
+    emit(out)
 
 
 C5_COEF = (-1.1108, -0.1454, -1.0235)   # the EQ_4_C model of the reference log (final_with_insite.txt:182)
@@ -504,7 +507,7 @@ def c5_main(args):
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:
-        print(json.dumps(out))
+        emit(out)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -672,7 +675,7 @@ def insite_main(args):
     }
     if cpu is not None:
         out["cpu_baseline"] = cpu
-    print(json.dumps(out))
+    emit(out)
 
 
 # planted per-arm model of the F4 cohort over [1, x0, u0, x0 u0]: no treatment / chemo / radio / both
@@ -808,7 +811,7 @@ def f4_main(args):
                                "sample": f"oracle/segments_ref.py + insite_ref.rollout (numpy, vectorised over patients) "
                                          f"on {n_s} patients x {T} steps over {W} threads (patient chunks), {el:.2f} s",
                                "host": info}
-    print(json.dumps(res))
+    emit(res)
 
 
 def c4_main(args):
@@ -953,7 +956,7 @@ def c4_main(args):
                                    "kind": "port", "sample": f"oracle/insite_ref.per_patient_fit (row-form pysindy-style "
                                                             f"STLSQ per patient) on {n_s} patients over a {W}-process "
                                                             f"spawned pool, {el1:.2f} s", "host": info}
-        print(json.dumps(res))
+        emit(res)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -1011,9 +1014,17 @@ def traffic_for(config, kernel, grid=None, args=None):
     WRITE_SIZE, median per dispatch), or None when that table has no such entry.  `grid`: the launch's total
     threads when a config launches the kernel at several sizes.  `args`: the table was taken on each config's
     DEFAULT workload at N = 1 (tools/g_traffic.sh), so a line with other sizes gets None."""
-    if args is not None and (args.patients != 100_000 or args.T not in (200, 60 if config == "c4" else 200)
-                             or int(os.environ.get("WORLD_SIZE", "1")) != 1):
-        return None
+    if args is not None:   # exactly the workload the table was taken on, or nothing
+        # the configs' sentinels: --patients 100000 means 1M for every config but c2, --T 200 means 500 (c3) or
+        # 60 (c4, f4); compare the EFFECTIVE sizes, so an explicit --T 60 on c4 is its default workload too
+        big = config != "c2"
+        eff_n = 1_000_000 if (big and args.patients == 100_000) else args.patients
+        t_def = {"c3": 500, "c4": 60, "f4": 60}.get(config, 200)
+        eff_t = t_def if args.T == 200 else args.T
+        knobs = (eff_n, eff_t, args.method, args.arm_format, args.layout, args.gram_blocks, args.dstreams,
+                 int(os.environ.get("WORLD_SIZE", "1")))
+        if knobs != (1_000_000 if big else 100_000, t_def, "rk4", "bits", "time", 0, 1, 1):
+            return None
     try:
         with open(TRAFFIC_R03) as f:
             tab = json.load(f).get(config, {})
@@ -1207,9 +1218,51 @@ def deferred_run(args, dev, coh, arm_cf, coh2=None, arm_cf2=None):
     mine, outs, ys, _ = lanes[(turn[0] - 1) % S]
     last = pos[(turn[0] - 1) % S] - 1
     fin = outs[(last - 1) % 3]
+    # the last launch rolled cohort mine[last % m] out with the model finalised one launch earlier -- that of the
+    # same data cohort two launches back (m = 2): the bench line's parity check compares THAT model and y
+    used = outs[(last - 2) % 3]
     return {"ms_step": ms_step, "host_ms": host_ms, "step_ms": step_ms, "KB": KB, "NBAT": NBAT,
             "coef": fin[0], "mask": fin[1], "y": ys[last % len(mine)], "rb": rb, "gb": gb, "rotated": coh2 is not None,
-            "streams": S, "frac": (rb + gb) / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+            "streams": S, "frac": (rb + gb) / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "roll_coef": used[0], "roll_mask": used[1], "roll_cohort": mine[last % len(mine)]}
+
+
+def c2_parity(dev, coh, arm_bits, coef, mask, y, n_sample=4096, seed=11):
+    """The metric's "RMSE vs CPU ref" for the benched cohort (after the timed region): the oracle
+    (oracle/insite_ref.py: the reference's SINDy.fit + RK4 scan restated, sindy.py:190-192, 371-431) fits the SAME
+    100k x 200 cohort whose rollout the last timed launch wrote, and rolls a sample of its rows out with its own
+    model; the line reports support equality, coefficient L-inf (GPU vs oracle model) and the trajectory RMSE /
+    max relative error of the GPU y on the sampled rows against the oracle's."""
+    sys.path.insert(0, ROOT)
+    from oracle import insite_ref as R
+    N, T = coh.arm.numel(), coh.x.size(0)
+    exps = coh.lib.exps.astype(np.int64)
+    x = coh.x[:, :N].t().contiguous().cpu().numpy()
+    u, arm = coh.u.cpu().numpy(), coh.arm.cpu().numpy().astype(np.int64)
+    rows = coh.rows.cpu().numpy()
+    if not np.all(rows == rows[0]):
+        return {"skipped": "ragged rows (the vectorised oracle Gram needs equal rows)"}
+    G, b = R.gram_moments_vectorized(x, u, arm, int(rows[0]), coh.dt, exps)
+    cr = np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)])
+    cg, mg = coef.cpu().numpy(), mask.cpu().numpy()
+    rng = np.random.default_rng(seed)
+    idx = np.unique(np.concatenate([rng.choice(N, min(n_sample, N), replace=False), np.arange(min(64, N)),
+                                    np.arange(max(0, N - 64), N)]))
+    it = torch.as_tensor(idx, device=dev)
+    words = arm_bits.index_select(1, it // 32)                                   # [T, n] int32
+    arms = ((words >> (it % 32).to(torch.int32)[None, :]) & 1).t().contiguous().cpu().numpy().astype(np.int64)
+    ref = R.rollout(coh.y0[it].cpu().numpy(), coh.u[it].cpu().numpy(), arms[:, :y.size(0)], cr, exps, coh.dt,
+                    method="rk4")
+    got = y.index_select(1, it).t().cpu().numpy()
+    d = got - ref
+    return {"oracle": "oracle/insite_ref.py (numpy restatement; gram_moments_vectorized + stlsq_gram + rollout rk4)",
+            "cohort": f"the last timed launch's rollout cohort ({N} x {T}, the model it used)",
+            "support_equal": bool(np.array_equal(mg != 0, cr != 0)),
+            "coef_linf": float(np.max(np.abs(cg - cr))),
+            "y_rmse": float(np.sqrt(np.mean(d ** 2))),
+            "y_max_rel": float(np.max(np.abs(d) / np.maximum(np.abs(ref), 1e-300))),
+            "rows_sampled": int(idx.size), "steps_per_row": int(y.size(0)),
+            "tolerances": {"coef_linf": 1e-8, "y_rmse": 1e-6}}
 
 
 def c2_fused(args, dev, coh, arm_cf, cpu):
@@ -1311,13 +1364,161 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
     if iso is not None:
         out["isolated"] = dict(iso, discovery_frac=gb / (iso["discovery_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                                rollout_frac=rb / (iso["rollout_avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS)
+    if "roll_coef" in fr and not args.no_parity:
+        rc_, ra_ = fr["roll_cohort"]
+        out["parity"] = c2_parity(dev, rc_, ra_, fr["roll_coef"], fr["roll_mask"], y)
     if not args.no_north_star:
         del y
         torch.cuda.empty_cache()
         out["north_star_rollout"] = north_star_rollout(args, dev, fr["coef"], lib)
     if cpu is not None:
         out["cpu_baseline"] = cpu
-    print(json.dumps(out))
+    emit(out)
+
+
+def c2_lagged(args, dev, world, rank, coh, arm_cf, cpu, collective):
+    """C2 at N GPUs (the default at N > 1; ``--mode lagged`` also at N = 1, with --force-collective to put the
+    single-rank RCCL all-reduce in): ONE insite_fit_rollout_lagged_f64 launch per step -- the step_deferred_kernel
+    timed at N = 1 with its finalisation split into a reduction role (rank-local G|b) and a solve role (an
+    all-reduced G|b) -- and one RCCL all-reduce of a K-fit bucket per K launches ON THE LAUNCH STREAM (no event,
+    no second stream: insite_amd.dist.LaggedSchedule).  Two cohorts per rank rotate, as at N = 1, so no launch
+    re-reads x still resident in the 256 MB Infinity Cache.  value = all ranks' patients / the max-over-ranks
+    step time (weak scaling: 100k patients per GPU)."""
+    from insite_amd import ops, cohort
+    from insite_amd import dist as idist
+    N, T = args.patients, args.T
+    lib = coh.lib
+    F = lib.n_terms
+    f64 = torch.float64
+    K = max(1, args.pipe_k)
+    sched = idist.LaggedSchedule(K)
+    sd = args.seed * 1000 + 500 + rank
+    coh2 = cohort.synthetic_pkpd(N, T, seed=sd, device=dev, equation="EQ_4_C", layout="time")
+    cohs = [(coh, arm_cf), (coh2, cohort.counterfactual_arms(coh2.arm, T, seed=sd, layout="time_bits"))]
+    buckets = [idist.MomentBucket(K, 2, F, dev) for _ in range(2)]
+    ring = [(torch.zeros((2, F), dtype=f64, device=dev), torch.zeros((2, F), dtype=torch.int8, device=dev),
+             torch.zeros((2,), dtype=torch.int32, device=dev)) for _ in range(3)]
+    ys = [torch.empty((T, N), dtype=f64, device=dev) for _ in range(2)]
+    scratch = (torch.zeros((2, F, F), dtype=f64, device=dev), torch.zeros((2, F), dtype=f64, device=dev))
+    ws = ops.Workspace()
+    # the prologue's rollouts (launches < K + 2 have no solved model yet) use a plain fit of each cohort
+    warm = [ops.sindy_fit(c.x, c.u, c.arm, c.rows, c.dt, lib, 0.1, 0.5, layout="time")[0] for c, _ in cohs]
+    st = torch.cuda.current_stream(dev)
+
+    def plan(k):
+        p = sched.launch(k)
+        c, _ = cohs[k % 2]
+        red = buckets[p["reduce"][1]].bufs[p["reduce"][2]] if p["reduce"] else None
+        fit_in = fit_out = None
+        if p["fit"]:
+            _, bi, pos, r = p["fit"]
+            fit_in, fit_out = (buckets[bi].bufs[pos].G, buckets[bi].bufs[pos].b), ring[r]
+        if p["rollout"]:
+            rc_, r = p["rollout"]
+            (rcoh, rbits), cin, yy = cohs[rc_ % 2], ring[r][0], ys[rc_ % 2]
+        else:
+            (rcoh, rbits), cin, yy = cohs[k % 2], warm[k % 2], ys[k % 2]
+        launch = ops.plan_fit_rollout_lagged(
+            c.x, c.u, c.arm, c.rows, c.dt, lib, 0.1, 0.5, rcoh.y0, rcoh.u, rbits, cin, rcoh.dt, p["slot"],
+            p["reduce"] is not None, ws, (red.G, red.b) if red is not None else scratch, fit_in=fit_in,
+            fit_out=fit_out, method=args.method, T=T, y_out=yy, gram_blocks=args.gram_blocks).bind(st)
+        ar = buckets[p["allreduce_after"]] if p["allreduce_after"] is not None else None
+        return launch, ar, p
+
+    P = idist.LaggedSchedule.period(K)
+    k0 = K + 2                                   # the first steady-state launch
+    steady = {}
+    for k in range(k0, k0 + P):
+        steady[k % P] = plan(k)
+
+    def one(k):
+        launch, ar, _ = plan(k) if k < k0 else steady[k % P]
+        launch()
+        if ar is not None and collective:        # the only collective: one per K launches, on the launch stream
+            idist.reduce_bucket(ar, force=args.force_collective)
+
+    kk = [0]
+
+    def run_steps(n):
+        for _ in range(n):
+            one(kk[0])
+            kk[0] += 1
+
+    run_steps(k0 + args.warmup)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run_steps(args.steps)
+    host_ms = (time.perf_counter() - t0) / args.steps * 1e3
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = idist.max_over_ranks(time.perf_counter() - t0, dev)
+    ms_step = el / args.steps * 1e3
+    last = kk[0] - 1
+    # instrumented pass: HIP events around batches of KB launches (+ their collectives), divided by KB
+    hip = HipEvents()
+    KB, NBAT = max(args.steps // K * K, 2 * K), 3
+    tevs = [(hip.create(timing=True), hip.create(timing=True)) for _ in range(NBAT)]
+    for e0, e1 in tevs:
+        hip.record(e0, st.cuda_stream)
+        run_steps(KB)
+        hip.record(e1, st.cuda_stream)
+    torch.cuda.synchronize(dev)
+    step_ms = float(np.mean([hip.elapsed_ms(e0, e1) for e0, e1 in tevs])) / KB
+    last = kk[0] - 1
+    p_last = sched.launch(last)
+    rc_, r = p_last["rollout"]
+    coef_used, mask_used = ring[r][0], ring[r][1]
+    y = ys[rc_ % 2]
+    rb, gb = rollout_bytes(N, T, arm_bits=1), gram_bytes(N, T)
+    out = None
+    if rank == 0:
+        achieved = (rb + gb) / (step_ms * 1e-3) / 1e9
+        out = {
+            "metric": METRIC,
+            "value": N * world / (ms_step * 1e-3),
+            "unit": "patient-trajectories/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: on-device EQ_4_C PK/PD cohorts (reference distributions, Euler-5 truth + 0.01 noise)",
+            "config": {
+                "workload": f"C2: PK/PD {N // 1000}k patients/GPU x {T} steps fp64 - discovery (savgol+FD4+poly2 "
+                            f"library+Gram, one RCCL all-reduce per {K} fits, STLSQ) + {args.method.upper()} "
+                            "counterfactual rollout",
+                "patients_per_gpu": N, "T": T, "rows_per_patient": T - 2, "library_terms": F,
+                "parallelism": f"patient-shard x{world}" + (" (single-rank RCCL group: --force-collective)"
+                                                             if args.force_collective and world == 1 else ""),
+                "mode": "lagged", "fits_per_allreduce": K, "lag_launches": K + 2,
+                "discovered_support": mask_used.cpu().numpy().tolist(),
+                "finite": bool(torch.isfinite(y).all().item()), "cohorts_rotated_per_rank": 2,
+            },
+            "host_submit_ms_per_step": host_ms,
+            "roofline": {
+                "kernel": "step_deferred_kernel, lagged (gram streaming | reduction of the previous slot to rank-local "
+                          "G|b | STLSQ of an all-reduced G|b | rk4 bit-arm rollout)",
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                "algorithmic_bytes_per_launch": rb + gb,
+                "algorithmic_bytes_split": {"discovery_x_read": gb, "rollout_y_written": rb},
+                "avg_launch_ms": step_ms,
+                "avg_ms_source": f"HIP timing events on the launch stream around {NBAT} batches of {KB} launches "
+                                 f"(with their {KB // K} bucket all-reduces), divided by the batch size",
+            },
+            "timed_region": f"one lagged launch per step on one stream + one all-reduce of a {K}-fit G|b bucket "
+                            "per K launches on the same stream; no events, no second stream",
+        }
+        if cpu is not None:
+            out["cpu_baseline"] = cpu
+    return out, (cohs[rc_ % 2], coef_used, mask_used, y)
 
 
 def north_star_rollout(args, dev, coef, lib):
@@ -1354,9 +1555,26 @@ def north_star_rollout(args, dev, coef, lib):
             "patient_trajectories_per_s": Nn / (ms * 1e-3)}
 
 
+_JSON_OUT = None
+
+
+def quiet_stdout():
+    """Keep the bench's stdout to its ONE JSON line: libraries that print banners on fd 1 (RCCL's "RCCL version"
+    block at communicator init, tqdm, ...) are sent to stderr from here on; ``emit`` writes to the saved fd."""
+    global _JSON_OUT
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
+def emit(obj):
+    print(json.dumps(obj), file=_JSON_OUT or sys.stdout, flush=True)
+
+
 def main():
     args = parse()
-    launch_ranks(args)
+    launch_ranks(args)   # (N > 1 without torchrun: re-launches through torchrun as a child and exits here)
+    quiet_stdout()
     if args.config == "f4":
         return f4_main(args)
     if args.config == "c4":
@@ -1372,9 +1590,9 @@ def main():
     if os.environ.get("WORLD_SIZE", "1") == "1" and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_sample, args.T, args.method, args.seed)
     world, rank, dev = dist_setup(force_group=args.force_collective)
-    if args.force_collective:
-        args.mode = "pipeline"
-    collective = world > 1 or args.force_collective   # the pipeline's data path all-reduces G|b
+    if args.force_collective and args.mode not in ("pipeline", "lagged"):
+        args.mode = "lagged"
+    collective = world > 1 or args.force_collective   # the N > 1 data path all-reduces G|b
 
     from insite_amd import ops, cohort
     from insite_amd import dist as idist
@@ -1388,13 +1606,22 @@ def main():
     lib = coh.lib
     F = lib.n_terms
     y0 = coh.y0
-    if args.mode is None:   # N = 1: one deferred fused launch per step; N > 1: the all-reduce splits the step
-        args.mode = "deferred" if world == 1 else "pipeline"
+    if args.mode is None:   # N = 1: one deferred fused launch per step; N > 1: the same kernel, lagged
+        args.mode = "deferred" if world == 1 and not args.force_collective else "lagged"
     if args.mode in ("fused", "deferred") and world > 1:
         raise SystemExit(f"--mode {args.mode} is single-GPU (the all-reduce sits between the gram and STLSQ): "
-                         "use --mode pipeline at N > 1")
+                         "use --mode lagged (the default at N > 1) or pipeline")
     if args.mode in ("fused", "deferred"):
         return c2_fused(args, dev, coh, arm_cf, cpu)
+    if args.mode == "lagged":
+        out, (rcoh, rcoef, rmask, ry) = c2_lagged(args, dev, world, rank, coh, arm_cf, cpu, collective)
+        if out is not None:
+            if not args.no_parity:
+                out["parity"] = c2_parity(dev, rcoh[0], rcoh[1], rcoef, rmask, ry) if world == 1 else {
+                    "skipped": "N > 1: each rank's model is the all-rank fit; the single-rank parity is tests/"
+                               "test_gpu_deferred.py and test_dist.py::test_lagged_schedule_gloo_world2"}
+            emit(out)
+        return
     # per-step state in NB buffers: the discovery of step i writes coefs[i % NB] while older rollouts may
     # still read theirs (G|b and the gram workspace are only touched by the discovery stream, in order,
     # but are buffered alike to keep the plans independent).  Steps go in batches of K: one event per batch
@@ -1740,7 +1967,7 @@ def main():
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:
-        print(json.dumps(out))
+        emit(out)
     if dist.is_available() and dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()

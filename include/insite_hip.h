@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define INSITE_ABI_VERSION 7
+#define INSITE_ABI_VERSION 8
 
 /* status codes */
 #define INSITE_OK 0
@@ -169,9 +169,12 @@ int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, co
  * the same gram_blocks); the rollout half is that of insite_fit_rollout_f64 (y_out bitwise).  A stream: call k
  * uses slot k % 2, finalize_prev = (k > 0), and rolls out with the coefficients call k - 1 produced (cohort
  * k - 2); a last call with n_patients = 0, n_rows = 0 and finalize_prev = 1 finalises the stream's last
- * cohort.  Consecutive calls on one workspace must pass the same gram_blocks (0 = the default split).  Same
- * shape restrictions as insite_fit_rollout_f64.  Workspace: insite_fit_rollout_deferred_workspace_bytes (two
- * slots; the header need not be zero: this entry uses no counters). */
+ * cohort.  Each slot's header records the block count and system size its partials were streamed with (ABI 8),
+ * and the finalisation sums exactly those: consecutive calls may change gram_blocks, method or fd_kind.  A
+ * finalisation of a slot no call has streamed (or streamed for another system) writes NaN G|b and coefficients,
+ * mask 0 and iters -3.  Same shape restrictions as insite_fit_rollout_f64.  Workspace:
+ * insite_fit_rollout_deferred_workspace_bytes (two slots; the header need not be zero: this entry uses no
+ * counters). */
 size_t insite_fit_rollout_deferred_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms);
 int32_t insite_fit_rollout_deferred_f64(const double* x, int64_t ldx, int32_t n_steps, const double* u,
                                         const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics,
@@ -184,6 +187,28 @@ int32_t insite_fit_rollout_deferred_f64(const double* x, int64_t ldx, int32_t n_
                                         double drop_below, double* y_out, int64_t ld_y, int32_t gram_blocks,
                                         int32_t slot, int32_t finalize_prev, void* workspace, size_t workspace_bytes,
                                         void* stream);
+
+/* The deferred step for N > 1 ranks (ABI 8; bench.py --gpus N): between the gram and the STLSQ the ranks
+ * all-reduce G|b (one RCCL all-reduce of the Gram/moment matrices), so the finalisation splits in
+ * two roles of the same launch.  Call k streams cohort k's Gram into slot `slot` (as the deferred call); with
+ * reduce_prev = 1 one block reduces the other slot's partials to this RANK'S G_out, b_out (the same fixed-order
+ * sums, no STLSQ); with G_fit/b_fit non-NULL another block solves the STLSQ of that (all-reduced, [A, F, F] and
+ * [A, F], full symmetric G) system into coef_out, mask_out, iters_out (insite_stlsq_f64 semantics, bitwise equal
+ * on every rank given equal G|b); the other blocks roll out (y0, ru, arm_bits) with coef_in.  A stream at N > 1
+ * with K fits per all-reduce bucket: G_out of cohort c is written by call c + 1, the bucket of cohorts
+ * [jK, jK + K) is all-reduced after call jK + K on the same stream, cohort c is solved by call c + K + 1 and
+ * rolled out by call c + K + 2 (bench.py lagged_run).  G_fit and b_fit must not alias G_out/b_out of the same
+ * call.  coef_out may be NULL when G_fit is.  Workspace as insite_fit_rollout_deferred_f64 (slot records too). */
+int32_t insite_fit_rollout_lagged_f64(const double* x, int64_t ldx, int32_t n_steps, const double* u,
+                                      const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics,
+                                      int32_t n_arms, const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
+                                      double threshold, double alpha, int32_t max_iter, int32_t unbias, double* G_out,
+                                      double* b_out, const double* G_fit, const double* b_fit, double* coef_out,
+                                      int8_t* mask_out, int32_t* iters_out, const double* y0, const double* ru,
+                                      const uint32_t* arm_bits, int64_t ld_arm, const double* coef_in, int64_t n_rows,
+                                      int32_t T, double rdt, int32_t method, int32_t substeps, double drop_below,
+                                      double* y_out, int64_t ld_y, int32_t gram_blocks, int32_t slot,
+                                      int32_t reduce_prev, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Treatment-segment discovery for the cancer_sim / EQ_5 datasets, replacing
  * process_sindy_training_data's segment split (libs_m/ct/src/data/pkpd/utils.py:433-462, 607-637)

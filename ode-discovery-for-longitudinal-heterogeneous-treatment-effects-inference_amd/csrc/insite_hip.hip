@@ -2485,14 +2485,76 @@ step_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
 #ifndef INSITE_DEF_GPRIO
 #define INSITE_DEF_GPRIO 0
 #endif
+// Each slot's header records what its partials are: the launch that streams a slot writes
+// {magic, gram blocks, entries} there, and the finalisation sums exactly the recorded number of partials, so a
+// caller that changes the method / fd between calls (and with them the default block split) still gets the
+// right G|b; a slot that was never streamed (or holds another system) is flagged instead of summed.
+constexpr int kSlotRec = 112;  // unsigned index into the slot's 512-B header (counters use [0, 98))
+constexpr unsigned kSlotMagic = 0x1E5D0A7Eu;
+static_assert((kSlotRec + 3) * sizeof(unsigned) <= 512, "slot record inside the workspace header");
+
+// A finalisation whose slot record does not match: NaN G|b (and with STF > 0 NaN coefficients, mask 0,
+// iters -3), so a misuse is loud rather than silently wrong.
+template <int STF>
+__device__ void finalize_invalid(const LibDesc& lib, const GramOut& o) {
+  const int F = lib.F;
+  const double nan = __builtin_nan("");
+  for (int i = threadIdx.x; i < o.n_arms * F * F; i += kBlock) o.G[i] = nan;
+  for (int i = threadIdx.x; i < o.n_arms * F; i += kBlock) {
+    o.b[i] = nan;
+    if constexpr (STF > 0) {
+      o.coef[i] = nan;
+      if (o.mask) o.mask[i] = 0;
+    }
+  }
+  if constexpr (STF > 0)
+    if (o.iters && (int)threadIdx.x < o.n_arms) o.iters[threadIdx.x] = -3;
+}
+
+// The STLSQ of an already-reduced system in global memory (the lagged step, N > 1: G|b all-reduced across the
+// ranks between launches).  One thread per arm, the solve of tail_finish on the lower triangle of G (the full
+// symmetric G the reduction wrote), so every rank's replicated fit is bitwise that of a single rank given equal
+// G|b.
+template <int STF>
+__device__ void fit_from_gb(const double* __restrict__ G, const double* __restrict__ b, const GramOut& o) {
+  const int a = (int)threadIdx.x;
+  if (a >= o.n_arms) return;
+  double g[STF][STF], rhs[STF], c[STF];
+#pragma unroll
+  for (int i = 0; i < STF; ++i) {
+    rhs[i] = b[a * STF + i];
+#pragma unroll
+    for (int j = 0; j <= i; ++j) g[i][j] = G[(a * STF + i) * STF + j];
+  }
+  unsigned sup = 0u;
+  const int it = stlsq_solve<STF>(g, rhs, o.sp.thr, o.sp.alpha, o.sp.max_iter, o.sp.unbias, c, sup);
+#pragma unroll
+  for (int i = 0; i < STF; ++i) {
+    o.coef[a * STF + i] = c[i];
+    if (o.mask) o.mask[a * STF + i] = (int8_t)((sup >> i) & 1u);
+  }
+  if (o.iters) o.iters[a] = it;
+}
+
+// lagged = 1 (insite_fit_rollout_lagged_f64, the N > 1 schedule): block gblocks only REDUCES the previous slot to
+// the rank-local G|b (out.G, out.b; no STLSQ -- the ranks all-reduce it between launches), block gblocks + 1
+// solves the STLSQ of an all-reduced system (G_fit, b_fit -> fit), and the rollout starts at block gblocks + 2.
 template <bool SMOOTH, int METHOD>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_STEP_WPE)))
 step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
                      const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, GramW w, LibDesc lib,
                      double* __restrict__ part_cur, const double* __restrict__ part_prev, GramOut out, RolloutArgs ra,
-                     int gblocks, unsigned* __restrict__ rc) {
+                     int gblocks, unsigned* __restrict__ rc, unsigned* __restrict__ hdr_cur,
+                     const unsigned* __restrict__ hdr_prev, int lagged, const double* __restrict__ G_fit,
+                     const double* __restrict__ b_fit, GramOut fit) {
   __shared__ double smem[kGramSmem];
+  const int n_ent = out.n_arms * lib.nE;
   if ((int)blockIdx.x < gblocks) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      hdr_cur[kSlotRec] = kSlotMagic;
+      hdr_cur[kSlotRec + 1] = (unsigned)gblocks;
+      hdr_cur[kSlotRec + 2] = (unsigned)n_ent;
+    }
     if (INSITE_DEF_GPRIO) __builtin_amdgcn_s_setprio(INSITE_DEF_GPRIO);
     gram_body<1, 2, SMOOTH, true, true, 0, 7>((int)blockIdx.x, gblocks, smem, x, ldx, n_steps, u, arm, rows, N, 0, 0,
                                                  w, lib, part_cur, nullptr, out);
@@ -2501,16 +2563,33 @@ step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, con
   if ((int)blockIdx.x == gblocks) {
     if (part_prev) {
       INSITE_TREAL(49152, 8);
-      deferred_finalize<7>(part_prev, gblocks, out.n_arms * lib.nE, lib, out, smem);
+      const unsigned mg = hdr_prev[kSlotRec], nb = hdr_prev[kSlotRec + 1], ne = hdr_prev[kSlotRec + 2];
+      const bool ok = mg == kSlotMagic && ne == (unsigned)n_ent && nb >= 1u && nb <= (unsigned)kGramMaxBlocks;
+      if (!ok) {
+        if (lagged) finalize_invalid<0>(lib, out);
+        else finalize_invalid<7>(lib, out);
+      } else if (lagged) {
+        deferred_finalize<0>(part_prev, (int)nb, n_ent, lib, out, smem);
+      } else {
+        deferred_finalize<7>(part_prev, (int)nb, n_ent, lib, out, smem);
+      }
       INSITE_TREAL(49152, 9);
       INSITE_TSTAMP(49152, 0);
     }
     return;
   }
+  int first = gblocks + 1;
+  if (lagged) {
+    if ((int)blockIdx.x == gblocks + 1) {
+      if (G_fit) fit_from_gb<7>(G_fit, b_fit, fit);
+      return;
+    }
+    first = gblocks + 2;
+  }
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int64_t RW = (int64_t)(gridDim.x - gblocks - 1) * kWavesPerBlock;
-  const int64_t rw = (int64_t)((int)blockIdx.x - gblocks - 1) * kWavesPerBlock + wid;
+  const int64_t RW = (int64_t)(gridDim.x - first) * kWavesPerBlock;
+  const int64_t rw = (int64_t)((int)blockIdx.x - first) * kWavesPerBlock + wid;
   INSITE_TREAL(32768 + rw, 8);
   INSITE_THWID(32768 + rw);
   const int ng = (ra.T + kRollGS - 1) / kRollGS;
@@ -3825,7 +3904,8 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
                                const double* ru, const uint32_t* arm_bits, int64_t ld_arm, const double* coef_in,
                                int64_t n_rows, int32_t T, double rdt, int32_t method, int32_t substeps,
                                double drop_below, double* y_out, int64_t ld_y, int32_t gram_blocks, void* workspace,
-                               size_t workspace_bytes, void* stream, int deferred, int32_t slot, int32_t finalize_prev) {
+                               size_t workspace_bytes, void* stream, int deferred, int32_t slot, int32_t finalize_prev,
+                               int lagged = 0, const double* G_fit = nullptr, const double* b_fit = nullptr) {
   // ---- discovery half: insite_sindy_fit_f64's checks, restricted to the fused kernel's shape ----
   if (n_patients < 0 || !G_out || !b_out || !coef_out || n_arms != 2 || ldx < 1 || !(dt > 0.0) || n_steps < 0 ||
       ldx < n_patients || max_iter < 0 || !(threshold >= 0.0) || !(alpha >= 0.0))
@@ -3844,6 +3924,7 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
   const size_t ws_one = insite_gram_workspace_bytes(n_patients, n_arms, n_terms);
   if (!workspace || workspace_bytes < (deferred ? 2 : 1) * ws_one) return INSITE_E_WORKSPACE;
   if (deferred && (slot < 0 || slot > 1 || finalize_prev < 0 || finalize_prev > 1)) return INSITE_E_INVALID_ARG;
+  if (lagged && ((G_fit == nullptr) != (b_fit == nullptr))) return INSITE_E_INVALID_ARG;
   if (ldx > ((int64_t)1 << 31) / (8 * kGT)) return INSITE_E_UNSUPPORTED;
   // ---- rollout half: insite_rollout_f64's checks for TIME_MAJOR_BITS, shared library ----
   if (n_rows < 0 || T < 0 || substeps < 1 || !(rdt >= 0.0) || ld_arm < (n_rows + 31) / 32 || ld_y < n_rows)
@@ -3881,16 +3962,22 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
                                                     : step_deferred_kernel<true, INSITE_METHOD_EULER>)
                      : (method == INSITE_METHOD_RK4 ? step_deferred_kernel<false, INSITE_METHOD_RK4>
                                                     : step_deferred_kernel<false, INSITE_METHOD_EULER>);
+    const int nfin = lagged ? 2 : 1;  // finalisation blocks: the reduction (and, lagged, the STLSQ of G_fit|b_fit)
     int grid = resident_waves(kd) / kWavesPerBlock;
-    if (grid < 3) grid = 3;
-    // half the resident blocks stream the gram (blocks b and b + grid/2 share a CU), one finalises, the rest roll out
+    if (grid < 2 + nfin) grid = 2 + nfin;
+    // half the resident blocks stream the gram (blocks b and b + grid/2 share a CU), nfin finalise, the rest roll out
     int gb = gram_blocks > 0 ? gram_blocks : grid / 2;
-    if (gb > grid - 2) gb = grid - 2;
+    if (gb > grid - 1 - nfin) gb = grid - 1 - nfin;
     if (gb > kGramMaxBlocks) gb = kGramMaxBlocks;
     char* wsb = static_cast<char*>(workspace);
     double* part_cur = reinterpret_cast<double*>(wsb + (size_t)slot * ws_one + kGramWsHeader);
     const double* part_prev =
         finalize_prev ? reinterpret_cast<const double*>(wsb + (size_t)(1 - slot) * ws_one + kGramWsHeader) : nullptr;
+    unsigned* hdr_cur = reinterpret_cast<unsigned*>(wsb + (size_t)slot * ws_one);
+    const unsigned* hdr_prev = reinterpret_cast<const unsigned*>(wsb + (size_t)(1 - slot) * ws_one);
+    // lagged: `go` reduces only (G|b out, no STLSQ); `gf` solves the all-reduced G_fit|b_fit into coef/mask/iters
+    const GramOut gred{G_out, b_out, n_arms, nullptr, nullptr, nullptr, sp};
+    const GramOut gf{nullptr, nullptr, n_arms, coef_out, mask_out, iters_out, sp};
     if (n_patients == 0) {  // the gram blocks leave zero partials
       x = G_out;
       arm = reinterpret_cast<const int8_t*>(G_out);
@@ -3899,7 +3986,8 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
     }
     unsigned* rc = INSITE_DEF_RSTATIC < 1000 ? static_cast<unsigned*>(workspace) : nullptr;  // slot 0's header
     kd<<<dim3(grid), kBlock, 0, hs>>>(x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, part_cur,
-                                      part_prev, go, ra, gb, rc);
+                                      part_prev, lagged ? gred : go, ra, gb, rc, hdr_cur, hdr_prev, lagged, G_fit,
+                                      b_fit, gf);
     return launch_status();
   }
   // (a two-patients-per-lane rollout role with 16-B stores measured slower: 46 vs 37 us rollout-only)
@@ -3952,6 +4040,25 @@ int32_t insite_fit_rollout_deferred_f64(const double* x, int64_t ldx, int32_t n_
                          threshold, alpha, max_iter, unbias, G_out, b_out, coef_out, mask_out, iters_out, y0, ru,
                          arm_bits, ld_arm, coef_in, n_rows, T, rdt, method, substeps, drop_below, y_out, ld_y,
                          gram_blocks, workspace, workspace_bytes, stream, 1, slot, finalize_prev);
+}
+
+int32_t insite_fit_rollout_lagged_f64(const double* x, int64_t ldx, int32_t n_steps, const double* u,
+                                      const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics,
+                                      int32_t n_arms, const int8_t* exps, int32_t n_terms, int32_t fd_kind, double dt,
+                                      double threshold, double alpha, int32_t max_iter, int32_t unbias, double* G_out,
+                                      double* b_out, const double* G_fit, const double* b_fit, double* coef_out,
+                                      int8_t* mask_out, int32_t* iters_out, const double* y0, const double* ru,
+                                      const uint32_t* arm_bits, int64_t ld_arm, const double* coef_in, int64_t n_rows,
+                                      int32_t T, double rdt, int32_t method, int32_t substeps, double drop_below,
+                                      double* y_out, int64_t ld_y, int32_t gram_blocks, int32_t slot,
+                                      int32_t reduce_prev, void* workspace, size_t workspace_bytes, void* stream) {
+  if (G_fit && !coef_out) return INSITE_E_INVALID_ARG;
+  double* co = coef_out ? coef_out : G_out;  // run_fit_rollout's non-null check; never written without G_fit
+  return run_fit_rollout(x, ldx, n_steps, u, arm, rows, n_patients, n_statics, n_arms, exps, n_terms, fd_kind, dt,
+                         threshold, alpha, max_iter, unbias, G_out, b_out, co, coef_out ? mask_out : nullptr,
+                         coef_out ? iters_out : nullptr, y0, ru, arm_bits, ld_arm, coef_in, n_rows, T, rdt, method,
+                         substeps, drop_below, y_out, ld_y, gram_blocks, workspace, workspace_bytes, stream, 1, slot,
+                         reduce_prev, 1, G_fit, b_fit);
 }
 
 int32_t insite_sindy_fit_f64(const double* x, int64_t ldx, int32_t layout, int32_t n_steps, const double* u,

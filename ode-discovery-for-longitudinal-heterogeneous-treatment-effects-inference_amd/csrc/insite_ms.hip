@@ -1567,6 +1567,9 @@ int32_t insite_gram_ms_f32(const float* x, int64_t ldx, int32_t n_steps, int32_t
   if (n_terms + n_states > kMsMaxF) return INSITE_E_UNSUPPORTED;
   if (!workspace || workspace_bytes < insite_gram_ms_workspace_bytes(n_patients)) return INSITE_E_WORKSPACE;
   if (n_patients > 0 && !x) return INSITE_E_INVALID_ARG;
+  // the per-step buffer descriptor (INSITE_MS4_BUFLD) spans the S state rows of one step with 32-bit byte
+  // offsets (s * ldx * 4 and its size): refuse cohorts whose step block leaves that range
+  if ((int64_t)n_states * ldx * 4 > (int64_t)INT32_MAX) return INSITE_E_UNSUPPORTED;
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   double* part = static_cast<double*>(workspace);
   const int grid = ms_grid(n_patients);

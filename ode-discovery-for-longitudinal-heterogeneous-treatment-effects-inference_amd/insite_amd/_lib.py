@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(LIB_DIR, "libinsite_hip.so")
 if os.environ.get("INSITE_LIB_OVERRIDE"):
     LIB_PATH = os.environ["INSITE_LIB_OVERRIDE"]
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # status codes / enums (insite_hip.h)
 INSITE_OK = 0
@@ -40,6 +40,7 @@ EXPORTS = (
     "insite_fit_rollout_f64",
     "insite_fit_rollout_deferred_workspace_bytes",
     "insite_fit_rollout_deferred_f64",
+    "insite_fit_rollout_lagged_f64",
     "insite_gram_segments_workspace_bytes",
     "insite_gram_segments_f64",
     "insite_sindy_fit_segments_f64",
@@ -111,6 +112,11 @@ _SIGNATURES = {
                                                  _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_f64, _c_i32,
                                                  _c_i32, _c_f64, _vp, _c_i64, _c_i32, _c_i32, _c_i32, _vp, _c_size,
                                                  _vp]),
+    "insite_fit_rollout_lagged_f64": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp,
+                                               _c_i32, _c_i32, _c_f64, _c_f64, _c_f64, _c_i32, _c_i32, _vp, _vp, _vp,
+                                               _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i32, _c_f64,
+                                               _c_i32, _c_i32, _c_f64, _vp, _c_i64, _c_i32, _c_i32, _c_i32, _vp,
+                                               _c_size, _vp]),
     "insite_gram_segments_workspace_bytes": (_c_size, [_c_i64, _c_i32, _c_i32]),
     "insite_gram_segments_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i64, _c_i32, _c_i32,
                                           _vp, _c_i32, _c_i32, _c_f64, _vp, _vp, _vp, _c_size, _vp]),

@@ -163,3 +163,49 @@ def discover_sharded(x, u, arm, rows, dt, lib, threshold, alpha, buf: MomentBuff
     ops.gram(x, u, arm, rows, dt, lib, buf.n_arms, fd, workspace, out=(buf.G, buf.b), layout=layout)
     reduce_moments(buf, group, deterministic)
     return ops.stlsq(buf.G, buf.b, threshold, alpha, max_iter, unbias, out=out)
+
+
+class LaggedSchedule:
+    """Bookkeeping of the N > 1 lagged step (``ops.plan_fit_rollout_lagged``, insite_fit_rollout_lagged_f64): one
+    launch per step, K fits per all-reduce bucket, no cross-stream hop.  Launch k (k >= 0):
+
+    * streams cohort k's Gram into partial slot k % 2;
+    * (k >= 1) reduces slot (k - 1) % 2 -- cohort k - 1 -- to this rank's G|b at position (k - 1) % K of bucket
+      ((k - 1) // K) % 2;
+    * (k >= K + 1) solves the STLSQ of cohort k - K - 1 from its ALL-REDUCED bucket entry into coefficient ring
+      slot (k - K - 1) % 3;
+    * (k >= K + 2) rolls out cohort k - K - 2 with ring slot (k - K - 2) % 3;
+
+    and after launch k with k % K == 0, k >= K, the bucket ((k - 1) // K) % 2 (cohorts k - K .. k - 1, complete)
+    is all-reduced in place on the launch stream.  Why these lags: bucket j is written by launches jK + 1 ..
+    jK + K, reduced after jK + K, read by the solves of launches jK + K + 1 .. jK + 2K, and rewritten (as bucket
+    j + 2) from launch jK + 2K + 1 on; the solve never reads the bucket its own launch writes, and a coefficient
+    slot is written one launch before the rollout that reads it.  Every cohort gets the reference's fit-then-
+    rollout over the WHOLE cohort (all ranks' patients), K + 1 launches later than at N = 1."""
+
+    def __init__(self, k: int):
+        if k < 1:
+            raise ValueError("K >= 1 fits per bucket")
+        self.K = int(k)
+
+    def launch(self, k: int) -> dict:
+        K = self.K
+        p = {"gram": k, "slot": k % 2, "reduce": None, "fit": None, "rollout": None, "allreduce_after": None}
+        if k >= 1:
+            c = k - 1
+            p["reduce"] = (c, (c // K) % 2, c % K)
+        if k >= K + 1:
+            c = k - K - 1
+            p["fit"] = (c, (c // K) % 2, c % K, c % 3)
+        if k >= K + 2:
+            c = k - K - 2
+            p["rollout"] = (c, c % 3)
+        if k >= K and k % K == 0:
+            p["allreduce_after"] = ((k - 1) // K) % 2
+        return p
+
+    @staticmethod
+    def period(k: int) -> int:
+        """Launch plans repeat with this period (slots 2, buckets 2K, coefficient ring 3): lcm(2, 2K, 3)."""
+        import math
+        return math.lcm(2, 2 * int(k), 3)

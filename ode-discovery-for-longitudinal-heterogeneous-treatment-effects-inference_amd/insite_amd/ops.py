@@ -185,7 +185,9 @@ def _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout, stl
     F = lib.n_terms
     dev = x.device
     nbytes = L.insite_gram_workspace_bytes(N, n_arms, F)
-    ws = _ws(workspace, dev, "disc").get(nbytes, dev)
+    # workspace=False: validate and pack only (a caller that attaches its own workspace, e.g. the deferred step)
+    ws = None if workspace is False else _ws(workspace, dev, "disc").get(nbytes, dev)
+    wsp, wsn = (_p(ws), ws.numel()) if ws is not None else (ctypes.c_void_p(0), 0)
     tab = lib.ctypes_table()
     head = (_p(x), x.stride(0), lay, n_steps, _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), _p(rows), N,
             lib.n_statics, n_arms, tab.ctypes.data_as(ctypes.c_void_p), F, FD_KINDS[fd], float(dt))
@@ -194,7 +196,7 @@ def _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout, stl
             out = (torch.empty((n_arms, F, F), dtype=torch.float64, device=dev),
                    torch.empty((n_arms, F), dtype=torch.float64, device=dev))
         G, b = out
-        return "insite_gram_f64", head + (_p(G), _p(b), _p(ws), ws.numel()), dev, out, (x, u, arm, rows, tab, ws, *out)
+        return "insite_gram_f64", head + (_p(G), _p(b), wsp, wsn), dev, out, (x, u, arm, rows, tab, ws, *out)
     threshold, alpha, max_iter, unbias = stlsq_args
     if out is None:
         out = (torch.empty((n_arms, F), dtype=torch.float64, device=dev),
@@ -204,7 +206,7 @@ def _prep_gram(x, u, arm, rows, dt, lib, n_arms, fd, workspace, out, layout, stl
                torch.empty((n_arms, F), dtype=torch.float64, device=dev))
     coef, mask, iters, G, b = out
     args = head + (float(threshold), float(alpha), int(max_iter), int(bool(unbias)), _p(G), _p(b), _p(coef),
-                   _p(mask), _p(iters), _p(ws), ws.numel())
+                   _p(mask), _p(iters), wsp, wsn)
     return "insite_sindy_fit_f64", args, dev, out, (x, u, arm, rows, tab, ws, *out)
 
 
@@ -337,8 +339,15 @@ def _prep_refit_rollout(mom, u, arm, rows, n_steps, lib, global_coef, threshold,
     A, F = global_coef.shape
     if mom.size(1) != 5 or not mom.is_contiguous() or F != lib.n_terms or not global_coef.is_contiguous():
         raise ValueError("mom must be contiguous [N, 5]; global_coef a contiguous [n_arms, F] tensor")
+    _dev("arm", arm, torch.int8, 1)
+    _dev("rows", rows, torch.int32, 1)
+    _dev("y0", y0, torch.float64, 1)
     if arm.numel() != N or rows.numel() != N or y0.numel() != N:
         raise ValueError("arm/rows/y0 must have one entry per patient")
+    if lib.n_statics:
+        _dev("u", u, torch.float64, 2)
+        if u.size(0) != N or u.size(1) != lib.n_statics or not u.is_contiguous():
+            raise ValueError("u must be a contiguous [N, n_statics] tensor")
     _dev("arm_bits", arm_bits, torch.int32, 2)
     if arm_bits.size(0) < T or arm_bits.size(1) < (N + 31) // 32:
         raise ValueError("arm_bits must be [T, >= ceil(N / 32)] int32 words")
@@ -352,6 +361,12 @@ def _prep_refit_rollout(mom, u, arm, rows, n_steps, lib, global_coef, threshold,
     if out.size(0) < T or out.size(1) < N:
         raise ValueError("out must be [T, >= N]")
     fc, fm, fi = fits if fits is not None else (None, None, None)
+    for name, t, dt_, shape in (("fits coef", fc, torch.float64, (N, A, F)), ("fits mask", fm, torch.int8, (N, F)),
+                                ("fits iters", fi, torch.int32, (N,))):
+        if t is not None:   # the kernel writes these rows: wrong dtype / short tensors would be silent OOB writes
+            _dev(name, t, dt_)
+            if tuple(t.shape) != shape or not t.is_contiguous() or t.device != dev:
+                raise ValueError(f"{name} must be a contiguous {shape} {dt_} tensor on {dev}")
     tab = lib.ctypes_table()
     nul = ctypes.c_void_p(0)
     args = (_p(mom), _p(arm), _p(rows), N, int(n_steps), lib.n_statics, A, tab.ctypes.data_as(ctypes.c_void_p), F,
@@ -727,7 +742,7 @@ def _prep_fit_rollout_deferred(x, u, arm, rows, dt, lib, threshold, alpha, max_i
     if slot not in (0, 1):
         raise ValueError("slot must be 0 or 1")
     name, args, dev, outs, keep = _prep_fit_rollout(x, u, arm, rows, dt, lib, threshold, alpha, max_iter, unbias, fd,
-                                                    None, out, y0, ru, arm_bits, coef_in, rdt, method, substeps,
+                                                    False, out, y0, ru, arm_bits, coef_in, rdt, method, substeps,
                                                     drop_below, T, y_out, gram_blocks)
     nbytes = _lib.load().insite_fit_rollout_deferred_workspace_bytes(int(args[6]), 2, lib.n_terms)
     ws = workspace.claim("deferred").get(nbytes, dev)
@@ -756,6 +771,66 @@ def plan_fit_rollout_deferred(x, u, arm, rows, dt, lib, threshold, alpha, y0, ru
     return Plan(*_prep_fit_rollout_deferred(x, u, arm, rows, dt, lib, threshold, alpha, max_iter, unbias, fd,
                                             workspace, out, y0, ru, arm_bits, coef_in, rdt, method, substeps,
                                             drop_below, T, y_out, gram_blocks, slot, finalize_prev))
+
+
+def _prep_fit_rollout_lagged(x, u, arm, rows, dt, lib, threshold, alpha, max_iter, unbias, fd, workspace, red,
+                             fit_in, fit_out, y0, ru, arm_bits, coef_in, rdt, method, substeps, drop_below, T, y_out,
+                             gram_blocks, slot, reduce_prev):
+    if workspace is None:
+        raise ValueError("the lagged step keeps its partial slots between calls: pass the stream's Workspace")
+    if slot not in (0, 1):
+        raise ValueError("slot must be 0 or 1")
+    F = lib.n_terms
+    dev = x.device
+    G, b = red
+    for name, t, shape in (("G_out", G, (2, F, F)), ("b_out", b, (2, F))):
+        _dev(name, t, torch.float64)
+        if tuple(t.shape) != shape or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous {shape} f64 tensor")
+    Gf, bf = fit_in if fit_in is not None else (None, None)
+    if fit_in is not None:
+        for name, t, shape in (("G_fit", Gf, (2, F, F)), ("b_fit", bf, (2, F))):
+            _dev(name, t, torch.float64)
+            if tuple(t.shape) != shape or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous {shape} f64 tensor")
+        if Gf.data_ptr() == G.data_ptr() or bf.data_ptr() == b.data_ptr():
+            raise ValueError("G_fit / b_fit must not alias this call's G_out / b_out")
+        if fit_out is None:
+            raise ValueError("fit_out = (coef, mask, iters) receives the solve of G_fit / b_fit")
+    coef, mask, iters = fit_out if fit_out is not None else (None, None, None)
+    # the deferred packing (validation of both halves), then the lagged argument order
+    name, args, dev, outs, keep = _prep_fit_rollout(x, u, arm, rows, dt, lib, threshold, alpha, max_iter, unbias, fd,
+                                                    False, (coef if coef is not None else torch.empty(
+                                                        (2, F), dtype=torch.float64, device=dev),
+                                                        mask if mask is not None else torch.empty(
+                                                            (2, F), dtype=torch.int8, device=dev),
+                                                        iters if iters is not None else torch.empty(
+                                                            (2,), dtype=torch.int32, device=dev), G, b),
+                                                    y0, ru, arm_bits, coef_in, rdt, method, substeps, drop_below, T,
+                                                    y_out, gram_blocks)
+    nbytes = _lib.load().insite_fit_rollout_deferred_workspace_bytes(int(args[6]), 2, F)
+    ws = workspace.claim("deferred").get(nbytes, dev)
+    nul = ctypes.c_void_p(0)
+    # fit_rollout args: [0..16] discovery head, 17 G, 18 b, 19 coef, 20 mask, 21 iters, 22.. rollout, -3 gram_blocks
+    args = (args[:19] + (_p(Gf) if Gf is not None else nul, _p(bf) if bf is not None else nul)
+            + (_p(coef) if coef is not None else nul, _p(mask) if mask is not None else nul,
+               _p(iters) if iters is not None else nul)
+            + args[22:-2] + (int(slot), int(bool(reduce_prev)), _p(ws), ws.numel()))
+    return "insite_fit_rollout_lagged_f64", args, dev, (red, fit_out, outs[1]), keep + (ws, Gf, bf)
+
+
+def plan_fit_rollout_lagged(x, u, arm, rows, dt, lib, threshold, alpha, y0, ru, arm_bits, coef_in, rdt, slot,
+                            reduce_prev, workspace, red, fit_in=None, fit_out=None, method="rk4", max_iter=100,
+                            unbias=True, fd="smoothed4", substeps=None, drop_below=1e-3, T=None, y_out=None,
+                            gram_blocks=0) -> Plan:
+    """The N > 1 form of the deferred step (insite_fit_rollout_lagged_f64): streams cohort (x, u, arm, rows) into
+    slot ``slot``; with ``reduce_prev`` reduces the other slot into this rank's ``red`` = (G, b) (no STLSQ: the
+    ranks all-reduce it between calls); with ``fit_in`` = (G, b) (an all-reduced system) solves its STLSQ into
+    ``fit_out`` = (coef, mask, iters); rolls out (y0, ru, arm_bits) with ``coef_in``.  ``plan.out`` =
+    (red, fit_out, y)."""
+    return Plan(*_prep_fit_rollout_lagged(x, u, arm, rows, dt, lib, threshold, alpha, max_iter, unbias, fd, workspace,
+                                          red, fit_in, fit_out, y0, ru, arm_bits, coef_in, rdt, method, substeps,
+                                          drop_below, T, y_out, gram_blocks, slot, reduce_prev))
 
 
 def rk45_order(n_obs: torch.Tensor, T_max: int, out: torch.Tensor | None = None) -> torch.Tensor:

@@ -32,9 +32,9 @@ DATASETS = ["cancer_sim", "EQ_5_B", "EQ_5_C", "EQ_5_D"]
 
 
 def _rows(args):
-    prev, arms, stat, sl, c0, exps, tau = args
-    return [Q.refine_patient(prev[i], arms[i], stat[i], int(sl[i]), c0, exps, R.STANDARD_DT, 10.0, tau)[0]
-            for i in range(prev.shape[0])]
+    prev, arms, stat, sl, c0, exps, tau, n_inputs = args
+    return [Q.refine_patient(prev[i], arms[i], stat[i], int(sl[i]), c0, exps, R.STANDARD_DT, 10.0, tau,
+                             n_inputs=n_inputs)[0] for i in range(prev.shape[0])]
 
 
 def refine_statics(sub, eq):
@@ -47,15 +47,38 @@ def refine_statics(sub, eq):
     return prev, st
 
 
-def _refine(ex, sub, c0, exps, tau, eq):
-    prev, st = refine_statics(sub, eq)
-    arms = np.argmax(sub.data["current_treatments"], axis=-1)
+def _refine(ex, sub, c0, exps, tau, eq, joint=False):
+    if joint:   # the one-ODE model: per-step multilabel treatments (chemo, radio) as library inputs, code c + 2r
+        prev, st = R.unscale_inputs(sub.data, sub.scaling_params, 1, 1)
+        tr = np.asarray(sub.data["current_treatments"])
+        arms, n_in = (tr[..., 0] + 2 * tr[..., 1]).astype(np.int64), 2
+    else:
+        prev, st = refine_statics(sub, eq)
+        arms, n_in = np.argmax(sub.data["current_treatments"], axis=-1), 0
     sl = sub.data["sequence_lengths"].astype(np.int64)
     chunks = np.array_split(np.arange(prev.shape[0]), 256)
     out = []
-    for o in ex.map(_rows, [(prev[c], arms[c], st[c], sl[c], c0, exps, tau) for c in chunks]):
+    for o in ex.map(_rows, [(prev[c], arms[c], st[c], sl[c], c0, exps, tau, n_in) for c in chunks]):
         out += o
     return np.stack(out)
+
+
+def _decompose(P, one, c0_preds, log_all, log_last):
+    """One-step set: squared error split into the fitted window (every active entry but the last) and the last
+    (counterfactual) entry -- ours, the SINDy model's, and the published run's implied by its all/last RMSEs."""
+    act = one.data["active_entries"][..., 0]
+    tgt = one.data["unscaled_outputs"][..., 0]
+    n = act.shape[0]
+    last = act - np.concatenate([act[:, 1:], np.zeros((n, 1))], axis=1)
+    ins = act - last
+    nc = CS.TUMOUR_DEATH_THRESHOLD
+
+    def sse(pred, w):
+        return float((((pred - tgt) ** 2) * w).sum())
+    a_ = (log_all * nc / 100) ** 2 * act.sum()
+    l_ = (log_last * nc / 100) ** 2 * last.sum()
+    return {"in_window_sse": {"oracle": sse(P, ins), "sindy_model": sse(c0_preds, ins), "log_implied": a_ - l_},
+            "last_entry_sse": {"oracle": sse(P, last), "sindy_model": sse(c0_preds, last), "log_implied": l_}}
 
 
 def main():
@@ -69,7 +92,7 @@ def main():
             pipe = CS.sindy_pipeline(coll)
             c0, exps = pipe["joint_coefs"], pipe["exps"]
             one = coll["test_cf_one_step"]
-            P = _refine(ex, one, c0, exps, 1, eq)
+            P1 = P = _refine(ex, one, c0, exps, 1, eq)
             o, a, l_ = R.masked_rmse(P[..., None], one.data["unscaled_outputs"], one.data["active_entries"],
                                      CS.TUMOUR_DEATH_THRESHOLD, one_step_counterfactual=True)
             m = {"encoder_test_rmse_orig": o, "encoder_test_rmse_all": a, "encoder_test_rmse_last": l_}
@@ -80,10 +103,37 @@ def main():
                                                  seqs.data_processed_seq["active_entries"], CS.TUMOUR_DEATH_THRESHOLD)):
                 m[f"decoder_test_rmse_{k + 2}-step"] = v
             log = anchors[f"{eq}/insite"]
+            prev, st = refine_statics(one, eq)
+            P0 = R.rollout(prev[:, 0], st, np.argmax(one.data["current_treatments"], axis=-1), c0, exps,
+                           R.STANDARD_DT, "euler5")
             res[eq] = {"oracle": {k: float(v) for k, v in m.items()},
                        "log_rel_diff": {k: float(v / log[k] - 1.0) for k, v in m.items()},
+                       "one_step_decomposition": _decompose(P1, one, P0, log["encoder_test_rmse_all"],
+                                                            log["encoder_test_rmse_last"]),
                        "source": log["source"]}
             print(eq, {k: f"{v:+.2e}" for k, v in res[eq]["log_rel_diff"].items()}, flush=True)
+        # the one-ODE ablation (run.py:198-201): joint model on the np.random.seed(10) cohort (the dataset cache)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", RuntimeWarning)
+            coll = CS.make_collection(10, treatment_mode="multilabel")
+        pipe = CS.joint_pipeline(coll)
+        c0, exps = pipe["joint_coefs"], pipe["exps"]
+        one = coll["test_cf_one_step"]
+        P = _refine(ex, one, c0, exps, 1, "cancer_sim", joint=True)
+        o, a, l_ = R.masked_rmse(P[..., None], one.data["unscaled_outputs"], one.data["active_entries"],
+                                 CS.TUMOUR_DEATH_THRESHOLD, one_step_counterfactual=True)
+        m = {"encoder_test_rmse_orig": o, "encoder_test_rmse_all": a, "encoder_test_rmse_last": l_}
+        seqs = coll["test_cf_treatment_seq"]
+        P = _refine(ex, seqs, c0, exps, 5, "cancer_sim", joint=True)
+        s_ = R.autoregressive_slice(P[..., None], seqs.data["sequence_lengths"], 5)
+        for k, v in enumerate(R.n_step_rmses(s_, seqs.data_processed_seq["unscaled_outputs"],
+                                             seqs.data_processed_seq["active_entries"], CS.TUMOUR_DEATH_THRESHOLD)):
+            m[f"decoder_test_rmse_{k + 2}-step"] = v
+        log = anchors["ABLATION_ONE_ODE/cancer_sim/insite/1"]
+        res["ABLATION_ONE_ODE/cancer_sim"] = {"oracle": {k: float(v) for k, v in m.items()},
+                                              "log_rel_diff": {k: float(v / log[k] - 1.0) for k, v in m.items()},
+                                              "source": log["source"]}
+        print("one-ODE joint", {k: f"{v:+.2e}" for k, v in res["ABLATION_ONE_ODE/cancer_sim"]["log_rel_diff"].items()})
     with open(os.path.join(HERE, "segment_insite_oracle.json"), "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
 

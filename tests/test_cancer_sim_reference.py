@@ -107,3 +107,25 @@ def test_one_ode_joint_model_equals_log():
     assert np.max(np.abs(got - ref) / np.maximum(1.0, np.abs(ref))) < 1e-10
     for k in METRICS:
         assert res[k] == pytest.approx(anchor[k], rel=1e-11), k
+
+
+def test_insite_restatement_vs_published_runs_bands():
+    """The restated INSITE refinement (tests/golden/segment_insite_oracle.json, regenerated by the committed
+    make_segment_insite_oracle.py) against the PUBLISHED INSITE runs on the bit-identical cohorts: within the
+    DESIGN.md §3 bands (cancer_sim / EQ_5_C <= 1.5e-3, EQ_5_B / D <= 4 %, the one-ODE joint runs <= 22 %), and
+    the gap has the recorded shape -- the published runs' fitted window carries MORE squared error than the
+    restatement's, while their last (counterfactual) entry agrees within 1 %."""
+    import json
+    import os
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    fx = json.load(open(os.path.join(here, "segment_insite_oracle.json")))
+    bands = {"cancer_sim": 1.5e-3, "EQ_5_C": 1.0e-3, "EQ_5_B": 3.0e-2, "EQ_5_D": 4.0e-2,
+             "ABLATION_ONE_ODE/cancer_sim": 0.22}
+    for key, band in bands.items():
+        rel = fx[key]["log_rel_diff"]
+        assert len(rel) == 8 and all(abs(v) <= band for v in rel.values()), (key, rel)
+    for eq in ("cancer_sim", "EQ_5_B", "EQ_5_C", "EQ_5_D"):
+        d = fx[eq]["one_step_decomposition"]
+        w, last = d["in_window_sse"], d["last_entry_sse"]
+        assert w["oracle"] < w["log_implied"] < w["sindy_model"], (eq, w)
+        assert abs(last["log_implied"] / last["oracle"] - 1) < 1e-2, (eq, last)

@@ -190,3 +190,117 @@ def test_bucketed_allreduce_reduces_every_fit_in_one_collective():
             want = sum(10.0 * k + rr for rr in range(world))
             assert np.all(G == want) and np.all(b == -want)
 
+
+
+def _lagged_worker(rank, world, port, q, K, n_launch):
+    """Each rank plays insite_fit_rollout_lagged_f64's roles with the oracle's CPU restatements on its own
+    shard: the gram (slot write), the block reduction (slot -> bucket entry), the replicated STLSQ (bucket
+    entry -> coefficient ring) and the rollout (ring -> y), in exactly the order LaggedSchedule gives, with the
+    bucket all-reduce (gloo) after the launches it names."""
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from oracle import insite_ref as R
+    from insite_amd import dist as idist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        g = np.load(os.path.join(ROOT, "tests", "golden", "discovery_eq_4_c.npz"))
+        x, u, arm, rows = g["x"], g["u"], g["arm"], g["rows"]
+        lo, hi = idist.shard_bounds(x.shape[0], rank, world)
+        exps = R.poly_library(3, 2, True)
+        F = exps.shape[0]
+
+        def cohort_x(c):   # cohort c: the golden cohort rescaled per c (distinct systems per launch)
+            return x * (1.0 + 0.01 * c)
+
+        sched = idist.LaggedSchedule(K)
+        slots = [None, None]
+        buckets = [idist.MomentBucket(K, 2, F, "cpu") for _ in range(2)]
+        ring = [None] * 3
+        fitted, rolled = {}, {}
+        for k in range(n_launch):
+            p = sched.launch(k)
+            # roles read state as the kernel does: the gram writes slot k % 2, the reduction reads the other
+            cur = R.gram_moments(cohort_x(k)[lo:hi], u[lo:hi], arm[lo:hi], rows[lo:hi], float(g["dt"]), exps)
+            if p["reduce"] is not None:
+                c, bi, pos = p["reduce"]
+                G, b = slots[(k - 1) % 2]
+                buckets[bi].bufs[pos].G.copy_(torch.from_numpy(G))
+                buckets[bi].bufs[pos].b.copy_(torch.from_numpy(b))
+            if p["fit"] is not None:
+                c, bi, pos, r = p["fit"]
+                buf = buckets[bi].bufs[pos]
+                ring[r] = (c, np.stack([R.stlsq_gram(buf.G[a].numpy(), buf.b[a].numpy(), 0.1, 0.5)[0]
+                                        for a in range(2)]))
+                fitted[c] = ring[r][1]
+            if p["rollout"] is not None:
+                c, r = p["rollout"]
+                assert ring[r][0] == c        # the rollout reads ITS cohort's model
+                rolled[c] = ring[r][1]
+            slots[k % 2] = cur
+            if p["allreduce_after"] is not None:
+                idist.reduce_bucket(buckets[p["allreduce_after"]])
+        q.put((rank, fitted, rolled))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("K", [1, 4])
+def test_lagged_schedule_gloo_world2(K):
+    """The N > 1 lagged step's bookkeeping (insite_amd.dist.LaggedSchedule; bench.py lagged_run) over gloo with 2
+    ranks: every cohort's model is the STLSQ of the ALL-RANK Gram (equal to a single-process fit of the whole
+    cohort), identical on both ranks, and every rollout uses its own cohort's model."""
+    from oracle import insite_ref as R
+    world, n_launch = 2, 3 * K + 8
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_lagged_worker, args=(r, world, port, q, K, n_launch)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (f, ro) for r, f, ro in (q.get(timeout=180) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = np.load(os.path.join(ROOT, "tests", "golden", "discovery_eq_4_c.npz"))
+    exps = R.poly_library(3, 2, True)
+    fitted0, rolled0 = res[0]
+    assert sorted(fitted0) == list(range(n_launch - K - 1))
+    assert sorted(rolled0) == list(range(n_launch - K - 2))
+    for c, coef in fitted0.items():
+        G, b = R.gram_moments(g["x"] * (1.0 + 0.01 * c), g["u"], g["arm"], g["rows"], float(g["dt"]), exps)
+        want = np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)])
+        assert np.array_equal(coef != 0, want != 0)
+        np.testing.assert_allclose(coef, want, rtol=1e-9, atol=1e-12)
+        assert np.array_equal(coef, res[1][0][c])      # replicated solve: bitwise on both ranks
+    for c, coef in rolled0.items():
+        assert np.array_equal(coef, fitted0[c])
+
+
+def test_lagged_schedule_never_aliases():
+    """Within one launch the solve never reads the bucket entry the reduction writes, the all-reduced bucket
+    is complete (its K cohorts reduced) and not yet rewritten when its fits read it, and the rollout's ring slot
+    is never the one the solve writes."""
+    from insite_amd.dist import LaggedSchedule
+    for K in (1, 2, 4, 8):
+        s = LaggedSchedule(K)
+        reduced_at, allreduced_at = {}, {}
+        writes = {}
+        for k in range(20 * K + 10):
+            p = s.launch(k)
+            if p["reduce"]:
+                c, bi, pos = p["reduce"]
+                reduced_at[c] = k
+                writes[(bi, pos)] = c
+            if p["fit"]:
+                c, bi, pos, r = p["fit"]
+                assert writes[(bi, pos)] == c                       # entry still holds cohort c
+                assert not p["reduce"] or p["reduce"][1] != bi      # not the bucket being written
+                assert allreduced_at.get(c // K, 10 ** 9) < k        # its bucket was all-reduced before
+                assert not p["rollout"] or p["rollout"][1] != r
+            if p["allreduce_after"] is not None:
+                j = (k - 1) // K
+                assert all(reduced_at.get(c, 10 ** 9) <= k for c in range(j * K, j * K + K))
+                allreduced_at[j] = k

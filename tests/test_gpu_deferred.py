@@ -1,0 +1,218 @@
+"""The C2 bench's own kernels against the ORACLE at the bench's configuration ("RMSE vs CPU ref").
+
+* ``insite_fit_rollout_deferred_f64`` (step_deferred_kernel, the timed N = 1 launch) on the bench's own 100k x
+  200 cohort (cohort.synthetic_pkpd seed 1000 = bench.py --seed 1, rank 0): the model finalised by the stream
+  equals the oracle's SINDy fit of that cohort (support identical, coefficient L-inf < 1e-8) and the rollout the
+  next launch writes with it equals the oracle's RK4 scan on sampled rows (rtol 1e-10, RMSE < 1e-6) --
+  oracle/insite_ref.py restates sindy.py:190-192 (fit) and :371-431 (scan).
+* The slot record (ABI 8): consecutive calls that change the method (and so the default block split) still
+  finalise the right number of partials; a slot no call has streamed is flagged (iters -3, NaN), not summed.
+* ``insite_fit_rollout_lagged_f64`` (the N > 1 step): its reduction role writes the same G|b as the deferred
+  finalisation, its solve role the same coefficients from a given G|b, and a LaggedSchedule stream with K = 2
+  on one rank (the all-reduce of a single rank is the identity) reproduces the deferred stream's models and
+  trajectories bitwise.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import insite_ref as R
+
+pytestmark = pytest.mark.gpu
+
+N, T = 100_000, 200
+
+
+@pytest.fixture(scope="module")
+def bench_cohort(dev):
+    from insite_amd import cohort
+    coh = cohort.synthetic_pkpd(N, T, seed=1000, device=dev, equation="EQ_4_C", layout="time")
+    bits = cohort.counterfactual_arms(coh.arm, T, seed=1000, layout="time_bits")
+    return coh, bits
+
+
+def _outs(dev, F):
+    return (torch.zeros((2, F), dtype=torch.float64, device=dev), torch.zeros((2, F), dtype=torch.int8, device=dev),
+            torch.zeros((2,), dtype=torch.int32, device=dev), torch.zeros((2, F, F), dtype=torch.float64, device=dev),
+            torch.zeros((2, F), dtype=torch.float64, device=dev))
+
+
+def _oracle_model(coh):
+    x = coh.x[:, :N].t().contiguous().cpu().numpy()
+    u, arm = coh.u.cpu().numpy(), coh.arm.cpu().numpy().astype(np.int64)
+    exps = coh.lib.exps.astype(np.int64)
+    G, b = R.gram_moments_vectorized(x, u, arm, T - 2, coh.dt, exps)
+    return G, b, np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)])
+
+
+def _sample_rows(dev, coh, bits, coef_np, y, n=4000, seed=3):
+    rng = np.random.default_rng(seed)
+    idx = np.unique(np.concatenate([rng.choice(N, n, replace=False), np.arange(64), np.arange(N - 96, N)]))
+    it = torch.as_tensor(idx, device=dev)
+    words = bits.index_select(1, it // 32)
+    arms = ((words >> (it % 32).to(torch.int32)[None, :]) & 1).t().contiguous().cpu().numpy().astype(np.int64)
+    ref = R.rollout(coh.y0[it].cpu().numpy(), coh.u[it].cpu().numpy(), arms, coef_np,
+                    coh.lib.exps.astype(np.int64), coh.dt, method="rk4")
+    return y.index_select(1, it).t().cpu().numpy(), ref
+
+
+def test_deferred_step_on_bench_cohort_matches_oracle(dev, bench_cohort):
+    from insite_amd import ops
+    coh, bits = bench_cohort
+    lib = coh.lib
+    F = lib.n_terms
+    ws = ops.Workspace()
+    o = [_outs(dev, F) for _ in range(3)]
+    y = torch.empty((T, N), dtype=torch.float64, device=dev)
+    # the bench's stream on one cohort: call 0 streams slot 0; call 1 finalises it into o[1]; call 2 rolls the
+    # cohort out with o[1] (the model of the same cohort) while finalising call 1's slot into o[2]
+    for k in range(3):
+        ops.fit_rollout_deferred(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, coh.y0, coh.u, bits,
+                                 o[(k - 1) % 3][0], coh.dt, k % 2, k > 0, ws, method="rk4", T=T, y_out=y,
+                                 out=o[k % 3] if k > 0 else o[2])
+    torch.cuda.synchronize()
+    G, b, cr = _oracle_model(coh)
+    for j in (1, 2):   # both finalisations of the same cohort
+        coef, mask, iters, Gg, bg = (t.cpu().numpy() for t in o[j])
+        np.testing.assert_allclose(Gg, G, rtol=1e-10, atol=1e-6)
+        np.testing.assert_allclose(bg, b, rtol=1e-10, atol=1e-6)
+        assert np.array_equal(mask != 0, cr != 0)
+        assert np.max(np.abs(coef - cr)) < 1e-8
+        assert np.all(iters > 0)
+    got, ref = _sample_rows(dev, coh, bits, cr, y)
+    np.testing.assert_allclose(got, ref, rtol=1e-10)
+    assert np.sqrt(np.mean((got - ref) ** 2)) < 1e-6
+
+
+def test_deferred_slot_record_survives_method_change(dev, bench_cohort):
+    """the finalisation must sum the partial count the STREAMING call used.  rk4 and euler5 launches
+    have different default gram block counts; alternating them must still give G|b of a plain fit (rtol 1e-12)."""
+    from insite_amd import ops
+    coh, bits = bench_cohort
+    lib = coh.lib
+    F = lib.n_terms
+    ws = ops.Workspace()
+    o = [_outs(dev, F) for _ in range(2)]
+    y = torch.empty((T, N), dtype=torch.float64, device=dev)
+    cin = torch.zeros((2, F), dtype=torch.float64, device=dev)
+    for k, meth, gblk in ((0, "rk4", 0), (1, "euler5", 0), (2, "rk4", 77), (3, "euler5", 0)):
+        ops.fit_rollout_deferred(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, coh.y0, coh.u, bits, cin,
+                                 coh.dt, k % 2, k > 0, ws, method=meth, T=T, y_out=y, out=o[k % 2],
+                                 gram_blocks=gblk)
+        if k > 0:
+            torch.cuda.synchronize()
+            c2, m2, _, G2, b2 = ops.sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, layout="time")
+            np.testing.assert_allclose(o[k % 2][3].cpu().numpy(), G2.cpu().numpy(), rtol=1e-12, atol=1e-9)
+            np.testing.assert_allclose(o[k % 2][4].cpu().numpy(), b2.cpu().numpy(), rtol=1e-12, atol=1e-9)
+            assert torch.equal(o[k % 2][1], m2)
+
+
+def test_deferred_unstreamed_slot_is_flagged(dev):
+    from insite_amd import cohort, ops
+    coh = cohort.synthetic_pkpd(3000, 40, seed=3, device=dev, equation="EQ_4_C", layout="time")
+    bits = cohort.counterfactual_arms(coh.arm, 40, seed=3, layout="time_bits")
+    F = coh.lib.n_terms
+    ws = ops.Workspace()
+    ws.claim("deferred").get(1 << 22, dev).fill_(0x5A)          # garbage headers: no call streamed slot 1
+    out = _outs(dev, F)
+    ops.fit_rollout_deferred(coh.x, coh.u, coh.arm, coh.rows, coh.dt, coh.lib, 0.1, 0.5, coh.y0, coh.u, bits,
+                             torch.zeros((2, F), dtype=torch.float64, device=dev), coh.dt, 0, True, ws, T=40, out=out)
+    torch.cuda.synchronize()
+    coef, mask, iters, G, b = out
+    assert torch.all(iters == -3) and torch.isnan(coef).all() and torch.isnan(G).all() and not mask.any()
+
+
+def test_lagged_roles_equal_deferred(dev, bench_cohort):
+    """Reduction role == the deferred finalisation's G|b (bitwise: same partials, same association); solve role
+    == the deferred STLSQ on that G|b (bitwise); rollout == the deferred rollout (bitwise)."""
+    from insite_amd import ops
+    coh, bits = bench_cohort
+    lib = coh.lib
+    F = lib.n_terms
+    cin = torch.zeros((2, F), dtype=torch.float64, device=dev)
+    cin[0, 4], cin[1, 1], cin[1, 5] = -1.1107592869834308, -0.14540553723951796, -1.0234639833519243
+    # deferred reference: two calls
+    wsd = ops.Workspace()
+    od = _outs(dev, F)
+    yd = torch.empty((T, N), dtype=torch.float64, device=dev)
+    for k in range(2):
+        ops.fit_rollout_deferred(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, coh.y0, coh.u, bits, cin,
+                                 coh.dt, k, k > 0, wsd, T=T, y_out=yd, out=od)
+    # lagged: call 0 streams; call 1 reduces into (Gr, br) and solves the deferred G|b given as G_fit
+    wsl = ops.Workspace()
+    Gr = torch.zeros((2, F, F), dtype=torch.float64, device=dev)
+    br = torch.zeros((2, F), dtype=torch.float64, device=dev)
+    fit = (torch.zeros((2, F), dtype=torch.float64, device=dev), torch.zeros((2, F), dtype=torch.int8, device=dev),
+           torch.zeros((2,), dtype=torch.int32, device=dev))
+    yl = torch.empty((T, N), dtype=torch.float64, device=dev)
+    for k in range(2):
+        p = ops.plan_fit_rollout_lagged(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, coh.y0, coh.u, bits,
+                                        cin, coh.dt, k, k > 0, wsl, (Gr, br),
+                                        fit_in=(od[3], od[4]) if k > 0 else None, fit_out=fit if k > 0 else None,
+                                        T=T, y_out=yl)
+        p()
+    torch.cuda.synchronize()
+    assert torch.equal(Gr, od[3]) and torch.equal(br, od[4])
+    assert torch.equal(fit[0], od[0]) and torch.equal(fit[1], od[1]) and torch.equal(fit[2], od[2])
+    assert torch.equal(yl, yd)
+
+
+def test_lagged_stream_single_rank_matches_oracle(dev):
+    """A LaggedSchedule stream (K = 2, two rotating cohorts, the bench's lagged_run bookkeeping) on one rank:
+    every solved model equals the oracle fit of its cohort and every rollout uses its own cohort's model."""
+    from insite_amd import cohort, ops
+    from insite_amd.dist import LaggedSchedule, MomentBucket
+    n, t, K = 20_000, 80, 2
+    cohs = [cohort.synthetic_pkpd(n, t, seed=77 + j, device=dev, equation="EQ_4_C", layout="time") for j in range(2)]
+    bitss = [cohort.counterfactual_arms(c.arm, t, seed=77 + j, layout="time_bits") for j, c in enumerate(cohs)]
+    lib = cohs[0].lib
+    F = lib.n_terms
+    sched = LaggedSchedule(K)
+    buckets = [MomentBucket(K, 2, F, dev) for _ in range(2)]
+    ring = [(torch.zeros((2, F), dtype=torch.float64, device=dev), torch.zeros((2, F), dtype=torch.int8, device=dev),
+             torch.zeros((2,), dtype=torch.int32, device=dev)) for _ in range(3)]
+    ys = [torch.empty((t, n), dtype=torch.float64, device=dev) for _ in range(2)]
+    ws = ops.Workspace()
+    dummy = torch.zeros((2, F), dtype=torch.float64, device=dev)
+    Gs, bs = torch.zeros((2, F, F), dtype=torch.float64, device=dev), torch.zeros((2, F), dtype=torch.float64,
+                                                                                   device=dev)
+    solved, rolled = {}, {}
+    for k in range(2 * K + 6):
+        p = sched.launch(k)
+        c = cohs[k % 2]
+        red = (buckets[p["reduce"][1]].bufs[p["reduce"][2]].G, buckets[p["reduce"][1]].bufs[p["reduce"][2]].b) \
+            if p["reduce"] else (Gs, bs)
+        fit_in = fit_out = None
+        if p["fit"]:
+            fc, bi, pos, r = p["fit"]
+            fit_in = (buckets[bi].bufs[pos].G, buckets[bi].bufs[pos].b)
+            fit_out = ring[r]
+        if p["rollout"]:
+            rc_, r = p["rollout"]
+            rcoh, rbits, coef_in, yy = cohs[rc_ % 2], bitss[rc_ % 2], ring[r][0], ys[rc_ % 2]
+        else:
+            rcoh, rbits, coef_in, yy = c, bitss[k % 2], dummy, ys[k % 2]
+        ops.plan_fit_rollout_lagged(c.x, c.u, c.arm, c.rows, c.dt, lib, 0.1, 0.5, rcoh.y0, rcoh.u, rbits, coef_in,
+                                    rcoh.dt, p["slot"], p["reduce"] is not None, ws, red, fit_in=fit_in,
+                                    fit_out=fit_out, T=t, y_out=yy)()
+        torch.cuda.synchronize()
+        if p["fit"]:
+            solved[p["fit"][0]] = ring[p["fit"][3]][0].cpu().numpy().copy()
+        if p["rollout"]:
+            rolled[p["rollout"][0]] = (ring[p["rollout"][1]][0].cpu().numpy().copy(), yy.clone())
+        # (single rank: the all-reduce after launch k is the identity)
+    want = []
+    for j in range(2):
+        x = cohs[j].x[:, :n].t().contiguous().cpu().numpy()
+        G, b = R.gram_moments_vectorized(x, cohs[j].u.cpu().numpy(), cohs[j].arm.cpu().numpy().astype(np.int64),
+                                         t - 2, cohs[j].dt, lib.exps.astype(np.int64))
+        want.append(np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)]))
+    assert sorted(solved) == list(range(2 * K + 6 - K - 1))
+    for cc, coef in solved.items():
+        assert np.array_equal(coef != 0, want[cc % 2] != 0)
+        assert np.max(np.abs(coef - want[cc % 2])) < 1e-8
+    for cc, (coef, yy) in rolled.items():
+        assert np.array_equal(coef, solved[cc])
+        y2 = ops.rollout(cohs[cc % 2].y0, cohs[cc % 2].u, bitss[cc % 2], torch.as_tensor(coef, device=dev), lib,
+                         cohs[cc % 2].dt, method="rk4", T=t, layout="time_bits")
+        assert torch.equal(yy, y2)

@@ -144,12 +144,19 @@ def test_insite_segment_rows_match_oracle(dev, case, subset, tau):
         np.testing.assert_allclose(preds[i], p, rtol=1e-9, atol=1e-9 * np.max(np.abs(p)), err_msg=f"row {i}")
 
 
+# Published INSITE runs vs the restatement ("INSITE on the 4-arm and joint models"): the bands the
+# restated refinement sits in on the bit-identical regenerated cohorts.  Asserted, so a regression that moves the
+# GPU path (or the oracle) further from the published runs fails; the cause of the remaining gap is not pinned.
+LOG_BANDS = {"cancer_sim": 1.5e-3, "EQ_5_C": 1.0e-3, "EQ_5_B": 3.0e-2, "EQ_5_D": 4.0e-2,
+             "ABLATION_ONE_ODE/cancer_sim": 0.22}
+
+
 def test_insite_plugin_segment_metrics(dev, case):
     """The plugin end to end (SINDY.fit -> refined predictions -> metrics, insite: true) on the reference's
     cohorts equals the oracle restatement's metrics (tests/golden/segment_insite_oracle.json, made by the
-    committed make_segment_insite_oracle.py) to 1e-9 relative.  Against the PUBLISHED INSITE runs
-    (final_with_insite.txt:2362-2382) the restatement is close but not pinned: cancer_sim and EQ_5_C within
-    1e-3, EQ_5_B / D within 4 % (the fixture's log_rel_diff) -- reported, not asserted."""
+    committed make_segment_insite_oracle.py) to 1e-9 relative, and lies within LOG_BANDS of the PUBLISHED INSITE
+    runs (final_with_insite.txt:2362-2382): cancer_sim and EQ_5_C within 1.5e-3 / 1e-3, EQ_5_B / D within 3 % / 4 %
+    (the published runs' in-window fits are looser than the restatement's: DESIGN.md §3)."""
     from insite_amd.sindy import SINDY
     eq, coll = case
     ref = ORACLE_INSITE[eq]["oracle"]
@@ -157,9 +164,40 @@ def test_insite_plugin_segment_metrics(dev, case):
     m.fit(coll["train"], coll["val"])
     got = _metrics(m, coll)
     anchor = ANCHORS[f"{eq}/insite"]
-    print(eq, "log rel diff", {k: f"{got[k] / anchor[k] - 1:+.2e}" for k in METRICS})
+    rel = {k: got[k] / anchor[k] - 1 for k in METRICS}
+    print(eq, "log rel diff", {k: f"{v:+.2e}" for k, v in rel.items()})
     bad = {k: (got[k], ref[k]) for k in METRICS if got[k] != pytest.approx(ref[k], rel=1e-9)}
     assert not bad, bad
+    far = {k: v for k, v in rel.items() if abs(v) > LOG_BANDS[eq]}
+    assert not far, far
+
+
+def test_insite_plugin_joint_one_ode_metrics(dev):
+    """INSITE on the one-ODE ablation (run.py:198-201: joint_model + multilabel, the np.random.seed(10) cohort of
+    the dataset cache): the plugin's refined metrics equal the oracle restatement's (segment_insite_oracle.json)
+    to 1e-9 and lie within LOG_BANDS of the published joint INSITE runs (one_big_ode.txt:6; the restatement fits
+    tighter, up to 21 % on the 2-step metric: DESIGN.md §3)."""
+    from insite_amd import config as C
+    from insite_amd.sindy import SINDY
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        coll = CS.make_collection(10, treatment_mode="multilabel")
+    a = C.compose(["+backbone=insite", "+dataset=pkpd_sim", "model.sindy_threshold=0.001", "model.sindy_alpha=0.5",
+                   "model.lam=10.0", "model.joint_model=true", "dataset.treatment_mode=multilabel"])
+    a["model"].update({"dataset_name": "cancer_sim", "dim_treatments": 2, "dim_static_features": 1,
+                       "dim_outcomes": 1})
+    m = SINDY(a, device=dev)
+    m.fit(coll["train"], coll["val"])
+    got = _metrics(m, coll)
+    key = "ABLATION_ONE_ODE/cancer_sim"
+    ref = ORACLE_INSITE[key]["oracle"]
+    anchor = ANCHORS["ABLATION_ONE_ODE/cancer_sim/insite/1"]
+    rel = {k: got[k] / anchor[k] - 1 for k in METRICS}
+    print("one-ODE joint INSITE log rel diff", {k: f"{v:+.2e}" for k, v in rel.items()})
+    bad = {k: (got[k], ref[k]) for k in METRICS if got[k] != pytest.approx(ref[k], rel=1e-9)}
+    assert not bad, bad
+    far = {k: v for k, v in rel.items() if abs(v) > LOG_BANDS[key]}
+    assert not far, far
 
 
 def test_plugin_joint_one_ode_reproduces_log(dev):
