@@ -596,8 +596,12 @@ def insite_main(args):
     c0[0, 4], c0[1, 1], c0[1, 5] = -1.1107592869834308, -0.14540553723951796, -1.0234639833519243  # log :182
     dt = 10.0 / T
 
+    # the product's binned path as a prepared plan: the seq_len sort, the gather pass, the kernel and the scatter
+    # pass (4 C calls, no host synchronisation) inside every step
+    plan = ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5)
+
     def run(binned=False):   # binned=True: rows binned by seq_len on the device (inside every step)
-        return ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, binned=binned)
+        return plan() if binned else ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, binned=False)
 
     def timed(binned):
         for _ in range(args.warmup):
@@ -611,6 +615,8 @@ def insite_main(args):
 
     ms_identity, _ = timed(False)
     ms_step, (preds, coef, status, iters) = timed(True)    # the product default: rows binned by seq_len
+    eager = ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, binned=True)
+    plan_eq = all(bool(torch.equal(a, b)) for a, b in zip(eager, (preds, coef, status, iters)))
     st = status.cpu().numpy()
     it = iters.cpu().numpy()
     # roofline: the refinement kernel alone on the step's binned time-major inputs (the layout pass excluded), HIP
@@ -618,8 +624,7 @@ def insite_main(args):
     # one untimed launch through insite_refine_general_f64) x the row's K-step window x flops per sensitivity step
     order = ops.rk45_order(sl, T)
     idx = order.long()
-    Vt, bits = ops.refine_prepare(V, arm, bits=True, order=order)
-    u_l, sl_l = coh.u.index_select(0, idx).contiguous(), sl.index_select(0, idx).contiguous()
+    Vt, bits, u_l, sl_l = ops.refine_prepare(V, arm, bits=True, order=order, u=coh.u, seq_len=sl)
     kst = torch.cuda.current_stream(dev)
 
     def kern():
@@ -655,7 +660,9 @@ def insite_main(args):
         "insite": {"refined_rows": int((st >= 0).sum()), "converged": int((st == 0).sum()),
                    "zoom_failed_fallback": int((st == 3).sum()), "mean_bfgs_iterations": float(it[st >= 0].mean()),
                    "lane_order": "rows binned by seq_len (device counting sort), gathered into lane order and "
-                                 "scattered back by insite_refine_prepare_f64 / insite_refine_finish_f64",
+                                 "scattered back by insite_refine_prepare_f64 / insite_refine_finish_f64 "
+                                 "(ops.plan_insite_refine: 4 C calls per step, no host sync)",
+                   "plan_equals_eager": plan_eq,
                    "identity_lane_order_ms_per_step": ms_identity,
                    "reference_wall_time_s": "88.96 s per INSITE EQ_4_A run incl. 59,000 + 11,800 refinements "
                                             "(results/2_main_table/final_with_insite.txt:2346; SURVEY.md §6)",

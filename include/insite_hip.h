@@ -419,17 +419,25 @@ int32_t insite_gen_gram_segments_f64(const double* x, int64_t ldx, const int8_t*
  * three torch copies and an int64 bit-pack of the reference-side transposes.  row_order [n_rows] (may be NULL):
  * output column l takes row row_order[l] (rows binned by sequence length, so a wave's lanes scan similar
  * prefixes while every kernel load stays coalesced); the refinement then runs with the identity lane order
- * on the permuted inputs, and insite_refine_finish_f64 scatters its predictions back.
+ * on the permuted inputs, and insite_refine_finish_f64 scatters its predictions back.  ABI 8: the same pass also
+ * gathers the per-row statics u [n_rows, n_statics] -> u_out (row l = u[row_order[l]]) and the sequence lengths
+ * seq_len -> seq_len_out when those pointers are non-NULL (one launch instead of two more gathers).
  */
 int32_t insite_refine_prepare_f64(const double* V, int64_t ld_v, const int8_t* arm, int64_t ld_arm, int64_t n_rows,
                                   int32_t T, double* Vt, int64_t ld_vt, uint32_t* arm_bits, int64_t ld_bits,
-                                  int8_t* arm_t, int64_t ld_armt, const int32_t* row_order, void* stream);
+                                  int8_t* arm_t, int64_t ld_armt, const int32_t* row_order, const double* u,
+                                  int32_t n_statics, double* u_out, const int32_t* seq_len, int32_t* seq_len_out,
+                                  void* stream);
 
 /* The inverse of insite_refine_prepare_f64 for the refinement's predictions (ABI 7): time-major preds_tm
  * [T, ld_t] whose column l is row row_order[l] (identity when NULL) -> patient-major preds_pm [n_rows, ld_pm],
- * the layout the reference's predictions come in (sindy.py:658-665). */
+ * the layout the reference's predictions come in (sindy.py:658-665).  ABI 8: the same pass scatters the lane-order
+ * per-row outputs back to row order when given: coef_lane [n_rows, n_coef] -> coef_out, status_lane -> status_out,
+ * iters_lane -> iters_out (each pair NULL to skip). */
 int32_t insite_refine_finish_f64(const double* preds_tm, int64_t ld_t, const int32_t* row_order, int64_t n_rows,
-                                 int32_t T, double* preds_pm, int64_t ld_pm, void* stream);
+                                 int32_t T, double* preds_pm, int64_t ld_pm, const double* coef_lane, int32_t n_coef,
+                                 double* coef_out, const int32_t* status_lane, int32_t* status_out,
+                                 const int32_t* iters_lane, int32_t* iters_out, void* stream);
 
 /* INSITE refinement of ANY global model of the reference (ABI 5, csrc/insite_refine.hip): the joint
  * "one ODE" model (sindy.py:469-483, 503-517, 537-551: one coefficient row over a library whose inputs

@@ -63,6 +63,10 @@ struct RefineArgs {
   // every coefficient q < n_coef: arm mask, static-monomial code | state exponent << 24
   int32_t q_mask[kRefineMaxCoef], q_code[kRefineMaxCoef];
   double c0[kRefineMaxCoef];
+  // the active terms' (arm, exponent) routing as ONE scalar when it fits 32 bits: bit i * 8 + a * 2 + e set when
+  // active coefficient i feeds gamma_{a,e} (D = 1, NA <= 4, m <= 4) -- the objective's gamma sums and gradient
+  // gathers test one SGPR instead of keeping 2m kernel-argument words live in SGPRs (which spilled into VGPR lanes)
+  int32_t gmap;
 };
 
 __device__ __forceinline__ double monomial_code(int code, const double* u) {
@@ -101,6 +105,7 @@ struct RefineLane {
   // for M = 4 rolled was faster while the sub-step held per-lane selects (9.6 vs 10.1 ms); without them unrolled
   // wins (INSITE_REFINE_SU4); dense models stay rolled
   static constexpr int SU = (M > 4 && M <= 16) ? 5 : (M <= 4 ? INSITE_REFINE_SU4 : 1);
+  static constexpr bool kGmap = M <= 4 && D == 1 && NA <= 4;  // RefineArgs::gmap holds the routing
   const RefineArgs& ra;
   int64_t p;
   int K;
@@ -124,13 +129,21 @@ struct RefineLane {
     for (int i = 0; i < M; ++i) {
       if (i >= ra.m) break;
       const double t = c[i] * mono[i];
-      const int mk = ra.t_mask[i], ex = ra.t_ex[i];
+      if constexpr (kGmap) {
 #pragma unroll
-      for (int a = 0; a < NA; ++a)
-        if ((mk >> a) & 1)
+        for (int a = 0; a < NA; ++a)
 #pragma unroll
           for (int e = 0; e <= D; ++e)
-            if (ex == e) gam[a][e] += t;
+            if ((ra.gmap >> (i * 8 + a * 2 + e)) & 1) gam[a][e] += t;
+      } else {
+        const int mk = ra.t_mask[i], ex = ra.t_ex[i];
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+          if ((mk >> a) & 1)
+#pragma unroll
+            for (int e = 0; e <= D; ++e)
+              if (ex == e) gam[a][e] += t;
+      }
     }
     const double h = ra.dt / (double)ra.sub;
     double y = ra.V[p];
@@ -210,14 +223,22 @@ struct RefineLane {
       }
       const double dd = c0a[i] - c[i];
       pen += dd * dd;
-      const int mk = ra.t_mask[i], ex = ra.t_ex[i];
       double gd = 0.0;
+      if constexpr (kGmap) {
 #pragma unroll
-      for (int a = 0; a < NA; ++a)
-        if ((mk >> a) & 1)
+        for (int a = 0; a < NA; ++a)
 #pragma unroll
           for (int e = 0; e <= D; ++e)
-            if (ex == e) gd += gG[a][e];
+            if ((ra.gmap >> (i * 8 + a * 2 + e)) & 1) gd += gG[a][e];
+      } else {
+        const int mk = ra.t_mask[i], ex = ra.t_ex[i];
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+          if ((mk >> a) & 1)
+#pragma unroll
+            for (int e = 0; e <= D; ++e)
+              if (ex == e) gd += gG[a][e];
+      }
       g[i] = gd * iK * mono[i] / norm + 2.0 * ra.lam * (c[i] - c0a[i]) / (double)ra.n_coef;
     }
     return L / norm + ra.lam * pen / (double)ra.n_coef;
@@ -259,9 +280,31 @@ __device__ __forceinline__ double quadmin(double a, double fa, double fpa, doubl
 #ifndef INSITE_REFINE_WPE8
 #define INSITE_REFINE_WPE8 1
 #endif
+#ifndef INSITE_REFINE_FLAT
+#define INSITE_REFINE_FLAT 1  // the BFGS as a flat per-lane state machine (one scan per loop iteration)
+#endif
 #ifndef INSITE_REFINE_QUAD
 #define INSITE_REFINE_QUAD 0  // 1: the O(M^2) inverse-Hessian update for the unrolled kernels too
 #endif
+// The inverse Hessian of the M <= 4 kernels lives in LDS (INSITE_REFINE_HLDS, one [M*M] column of doubles per lane,
+// kBlock-strided: conflict-free): it is read once per iteration (p = -H g) and written once (the update), while
+// the line search -- ~12 objective scans per row, each a dependent fp64 chain -- needs every VGPR it can get.  In
+// VGPRs the 4-coefficient kernel at INSITE_REFINE_WPE4 = 4 waves/SIMD (<= 128 VGPRs) spilled 156 VGPRs to scratch
+// (316 B/lane): PMC 13.6 GB of traffic per launch against 1.1 GB algorithmic (profiles/traffic_r03.json).
+#ifndef INSITE_REFINE_HLDS
+#define INSITE_REFINE_HLDS 1
+#endif
+template <int M, bool LDS>
+struct HMat {
+  double v[M][M];
+  __device__ __forceinline__ double& at(int i, int j) { return v[i][j]; }
+};
+template <int M>
+struct HMat<M, true> {
+  double* base;  // &sH[threadIdx.x]; element (i, j) at base[(i * M + j) * kBlock]
+  __device__ __forceinline__ double& at(int i, int j) { return base[(i * M + j) * kBlock]; }
+};
+
 // M <= 4 with the affine RHS (the EQ_4 models: two terms per arm) is sized for INSITE_REFINE_WPE4 waves per
 // SIMD (<= 128 VGPRs; unconstrained the compiler takes 202 and runs 2 waves): the objective scan is a
 // dependent fp64 chain per lane, hidden only by other waves.
@@ -270,6 +313,8 @@ __global__ void __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(M <= 4 && D == 1 ? INSITE_REFINE_WPE4 : (M <= 8 ? INSITE_REFINE_WPE8 : 1))))
 insite_refine_kernel(RefineArgs ra) {
   constexpr int RU = RefineLane<M, NA, D>::RU;
+  constexpr bool kHL = INSITE_REFINE_HLDS && RU == M && M <= 4;
+  __shared__ double sH[(kHL ? M * M : 1) * kBlock];
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= ra.N) return;
   // lane -> row: with rows binned by seq_len the lanes of a wave scan similar prefixes; every row's
@@ -289,18 +334,275 @@ insite_refine_kernel(RefineArgs ra) {
   for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
   const int sl = ra.sl[p];
   int status = -1, nit = 0;
+#if INSITE_REFINE_FLAT
+  // ---------------- BFGS as a flat per-lane state machine: ONE objective scan per loop iteration ----------------
+  // The nested form (line search loop { scan; zoom loop { scan } }) makes a wave walk the nesting of ALL its lanes:
+  // lanes zooming and lanes doubling their trial step, lanes in their 3rd BFGS iteration and lanes in their 7th,
+  // run their scans one after the other while the others wait.  Here every iteration of the single loop evaluates
+  // each pending lane's next trial point (a line-search step a_i or a zoom step a_j) in the same scan, then
+  // advances that lane's state (jax line_search / _zoom / minimize_bfgs transitions, in their order), so a wave
+  // costs max over its lanes of the evaluation count instead of the sum over the nesting.  Per lane the arithmetic
+  // is the nested form's, operation for operation (A/B: INSITE_REFINE_FLAT=0).
   if (sl > ra.tau && ra.T >= 2) {
     ln.K = min(sl - ra.tau, ra.T - 1);
     double g[M];
     const double start = ln.fg(x, g);  // norm 1, penalty 0 at c0
     ln.norm = start * 2.5;
-    // ---------------- BFGS (jax minimize_bfgs, norm = inf, gtol 1e-5) ----------------
-    double H[M][M];
+    // jax evaluates f_to_min at c0 twice (start_res with norm_const = 1, then minimize's first value_and_grad with
+    // norm_const = 2.5 start_res, sindy.py:591-627).  At c0 the penalty and its gradient are exactly zero, so the
+    // second evaluation is the first divided by norm -- bitwise (fg's last operations are that one division plus
+    // +0.0) -- and its scan is not repeated.
+    double f = start / ln.norm + 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) g[i] = g[i] / ln.norm + 0.0;
+    HMat<M, kHL> H;
+    if constexpr (kHL) H.base = sH + threadIdx.x;
 #pragma unroll RU
     for (int i = 0; i < M; ++i)
 #pragma unroll RU
-      for (int j = 0; j < M; ++j) H[i][j] = i == j ? 1.0 : 0.0;
-    double f = ln.fg(x, g);
+      for (int j = 0; j < M; ++j) H.at(i, j) = i == j ? 1.0 : 0.0;
+    double gmax = 0.0, g2 = 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      gmax = fmax(gmax, fabs(g[i]));
+      g2 += g[i] * g[i];
+    }
+    bool converged = gmax < 1e-5, failed = false;
+    double old_old = f + sqrt(g2) / 2.0;
+    int ls_status = 0;
+    const int maxiter = 200 * ra.n_coef;
+    int k = 0;
+    // line search state (jax _LineSearchState) and zoom state (_ZoomState)
+    double pk[M], g_star[M];
+    double phi0 = 0.0, dphi0 = 0.0, a_i1 = 0.0, phi_i1 = 0.0, dphi_i1 = 0.0, a_star = 0.0, phi_star = 0.0;
+    double a_lo = 0.0, phi_lo = 0.0, dphi_lo = 0.0, a_hi = 0.0, phi_hi = 0.0, dphi_hi = 0.0, a_rec = 0.0,
+           phi_rec = 0.0, za = 0.0, zphi = 0.0, t_trial = 0.0;
+    int li = 1, zj = 0;
+    bool ls_failed = false, in_zoom = false, z_failed = false;
+    // a new line search from (x, f, g, H): p = -H g, jax's first trial min(1, 1.01 * 2 (f_k - f_{k-1}) / phi'(0))
+    auto begin_ls = [&]() {
+#pragma unroll RU
+      for (int i = 0; i < M; ++i) {
+        double s_ = 0.0;
+#pragma unroll RU
+        for (int j = 0; j < M; ++j) s_ += H.at(i, j) * g[j];
+        pk[i] = -s_;
+      }
+      phi0 = f;
+      dphi0 = ln.dot(g, pk);
+      const double cand = 1.01 * 2.0 * (phi0 - old_old) / dphi0;
+      t_trial = cand > 1.0 ? 1.0 : cand;
+      li = 1;
+      a_i1 = 0.0;
+      phi_i1 = phi0;
+      dphi_i1 = dphi0;
+      a_star = 0.0;
+      phi_star = phi0;
+#pragma unroll RU
+      for (int i = 0; i < M; ++i) g_star[i] = g[i];
+      ls_failed = false;
+      in_zoom = false;
+    };
+    // the top of a zoom iteration (everything before its evaluation): the failure test and the next trial a_j
+    auto zoom_top = [&]() {
+      const double dalpha = a_hi - a_lo;
+      const double lo = fmin(a_hi, a_lo), hi = fmax(a_hi, a_lo);
+      const double cchk = 0.2 * dalpha, qchk = 0.1 * dalpha;
+      z_failed = z_failed || (dalpha <= 1e-10);
+      const double a_cub = cubicmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi, a_rec, phi_rec);
+      const bool use_cubic = (zj > 0) && (a_cub > lo + cchk) && (a_cub < hi - cchk);
+      const double a_quad = quadmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi);
+      const bool use_quad = !use_cubic && (a_quad > lo + qchk) && (a_quad < hi - qchk);
+      double a_j = a_rec;
+      if (use_cubic) a_j = a_cub;
+      if (use_quad) a_j = a_quad;
+      if (!use_cubic && !use_quad) a_j = (a_lo + a_hi) / 2.0;
+      t_trial = a_j;
+    };
+    bool pending = !converged && k < maxiter;
+    if (pending) begin_ls();
+    while (pending) {
+      double dphi_t, g_t[M];
+      const double phi_t = ln.phi(x, pk, t_trial, dphi_t, g_t);
+      bool ls_end = false, ls_done = false;
+      if (!in_zoom) {  // the line search's trial a_i
+        const double a_i = t_trial;
+        const bool s_z1 = (phi_t > phi0 + 1e-4 * a_i * dphi0) || ((phi_t >= phi_i1) && (li > 1));
+        const bool s_i = (fabs(dphi_t) <= -0.9 * dphi0) && !s_z1;
+        const bool s_z2 = (dphi_t >= 0.0) && !s_z1 && !s_i;
+        if (s_i) {
+          a_star = a_i;
+          phi_star = phi_t;
+#pragma unroll RU
+          for (int i = 0; i < M; ++i) g_star[i] = g_t[i];
+        }
+        if (s_z1 || s_z2) {  // zoom between (lo, hi) = (a_{i-1}, a_i) or (a_i, a_{i-1}); state as jax _zoom inits it
+          if (s_z1) {
+            a_lo = a_i1; phi_lo = phi_i1; dphi_lo = dphi_i1;
+            a_hi = a_i; phi_hi = phi_t; dphi_hi = dphi_t;
+          } else {
+            a_lo = a_i; phi_lo = phi_t; dphi_lo = dphi_t;
+            a_hi = a_i1; phi_hi = phi_i1; dphi_hi = dphi_i1;
+          }
+          zj = 0;
+          z_failed = false;
+          a_rec = (a_lo + a_hi) / 2.0;
+          phi_rec = (phi_lo + phi_hi) / 2.0;
+          za = 1.0;
+          zphi = phi_lo;
+#pragma unroll RU
+          for (int i = 0; i < M; ++i) g_star[i] = g[i];
+          in_zoom = true;
+        }
+        ++li;
+        a_i1 = a_i;
+        phi_i1 = phi_t;
+        dphi_i1 = dphi_t;
+        if (in_zoom) {
+          zoom_top();
+        } else if (s_i) {
+          ls_end = ls_done = true;
+        } else if (li > 10) {
+          ls_end = true;
+        } else {
+          t_trial = a_i1 * 2.0;
+        }
+      } else {  // the zoom's trial a_j
+        const double a_j = t_trial;
+        const bool hi_to_j = (phi_t > phi0 + 1e-4 * a_j * dphi0) || (phi_t >= phi_lo);
+        const bool star_to_j = (fabs(dphi_t) <= -0.9 * dphi0) && !hi_to_j;
+        const bool hi_to_lo = (dphi_t * (a_hi - a_lo) >= 0.0) && !hi_to_j && !star_to_j;
+        const bool lo_to_j = !hi_to_j && !star_to_j;
+        if (hi_to_j) {
+          a_rec = a_hi;
+          phi_rec = phi_hi;
+          a_hi = a_j;
+          phi_hi = phi_t;
+          dphi_hi = dphi_t;
+        }
+        if (star_to_j) {
+          za = a_j;
+          zphi = phi_t;
+#pragma unroll RU
+          for (int i = 0; i < M; ++i) g_star[i] = g_t[i];
+        }
+        if (hi_to_lo) {
+          a_rec = a_hi;
+          phi_rec = phi_hi;
+          a_hi = a_lo;
+          phi_hi = phi_lo;
+          dphi_hi = dphi_lo;
+        }
+        if (lo_to_j) {
+          a_rec = a_lo;
+          phi_rec = phi_lo;
+          a_lo = a_j;
+          phi_lo = phi_t;
+          dphi_lo = dphi_t;
+        }
+        ++zj;
+        z_failed = ((z_failed ? 1 : 0) | zj) >= 30;  // jax: `failed | j >= 30` (no parentheses)
+        if (star_to_j || z_failed) {  // the zoom ends, and with it the line search (done = s_z1 | s_z2)
+          a_star = za;
+          phi_star = zphi;
+          ls_failed = ls_failed || z_failed;
+          ls_end = ls_done = true;
+        } else {
+          zoom_top();
+        }
+      }
+      if (ls_end) {
+        ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
+        failed = ls_failed || !ls_done;
+        // ---- BFGS update (minimize_bfgs body after its line_search call) ----
+        double sk[M], yk[M];
+#pragma unroll RU
+        for (int i = 0; i < M; ++i) {
+          sk[i] = a_star * pk[i];
+          yk[i] = g_star[i] - g[i];
+        }
+        const double rho = 1.0 / ln.dot(yk, sk);
+        if (isfinite(rho) && (RU == 1 || INSITE_REFINE_QUAD)) {
+          double hy[M];
+          double yhy = 0.0;
+#pragma unroll RU
+          for (int i = 0; i < M; ++i) {
+            double t = 0.0;
+#pragma unroll RU
+            for (int j = 0; j < M; ++j) t += H.at(i, j) * yk[j];
+            hy[i] = t;
+            yhy += yk[i] * t;
+          }
+          const double cs = rho * rho * yhy + rho;
+#pragma unroll RU
+          for (int i = 0; i < M; ++i)
+#pragma unroll RU
+            for (int j = 0; j < M; ++j)
+              H.at(i, j) = H.at(i, j) - rho * (sk[i] * hy[j] + hy[i] * sk[j]) + cs * (sk[i] * sk[j]);
+        } else if (isfinite(rho)) {
+          auto w = [&](int i, int q) { return (i == q ? 1.0 : 0.0) - rho * (sk[i] * yk[q]); };
+          double WH[M][M];
+#pragma unroll RU
+          for (int i = 0; i < M; ++i)
+#pragma unroll RU
+            for (int j = 0; j < M; ++j) {
+              double s_ = 0.0;
+#pragma unroll RU
+              for (int q = 0; q < M; ++q) s_ += w(i, q) * H.at(q, j);
+              WH[i][j] = s_;
+            }
+#pragma unroll RU
+          for (int i = 0; i < M; ++i)
+#pragma unroll RU
+            for (int j = 0; j < M; ++j) {
+              double s_ = 0.0;
+#pragma unroll RU
+              for (int q = 0; q < M; ++q) s_ += WH[i][q] * w(j, q);
+              H.at(i, j) = s_ + rho * (sk[i] * sk[j]);
+            }
+        }
+        double gm = 0.0;
+#pragma unroll RU
+        for (int i = 0; i < M; ++i) {
+          x[i] = x[i] + sk[i];
+          g[i] = g_star[i];
+          gm = fmax(gm, fabs(g[i]));
+        }
+        converged = gm < 1e-5;
+        old_old = f;
+        f = phi_star;
+        ++k;
+        pending = !converged && !failed && k < maxiter;
+        if (pending) begin_ls();
+      }
+    }
+    nit = k;
+    status = converged ? 0 : (k == maxiter ? 1 : (failed ? 2 + ls_status : -1));
+    if (status == 3 && ra.revert3) {  // zoom failed: the reference code keeps the global coefficients (sindy.py:628-631)
+#pragma unroll RU
+      for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
+    }
+  }
+#else
+  if (sl > ra.tau && ra.T >= 2) {
+    ln.K = min(sl - ra.tau, ra.T - 1);
+    double g[M];
+    const double start = ln.fg(x, g);  // norm 1, penalty 0 at c0
+    ln.norm = start * 2.5;
+    // jax evaluates f_to_min at c0 twice (start_res with norm_const = 1, then minimize's first value_and_grad with
+    // norm_const = 2.5 start_res, sindy.py:591-627).  At c0 the penalty and its gradient are exactly zero, so the
+    // second evaluation is the first divided by norm -- bitwise (fg's last operations are that one division plus
+    // +0.0) -- and its scan is not repeated.
+    // ---------------- BFGS (jax minimize_bfgs, norm = inf, gtol 1e-5) ----------------
+    HMat<M, kHL> H;
+    if constexpr (kHL) H.base = sH + threadIdx.x;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i)
+#pragma unroll RU
+      for (int j = 0; j < M; ++j) H.at(i, j) = i == j ? 1.0 : 0.0;
+    double f = start / ln.norm + 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) g[i] = g[i] / ln.norm + 0.0;
     double gmax = 0.0, g2 = 0.0;
 #pragma unroll RU
     for (int i = 0; i < M; ++i) {
@@ -318,7 +620,7 @@ insite_refine_kernel(RefineArgs ra) {
       for (int i = 0; i < M; ++i) {
         double s = 0.0;
 #pragma unroll RU
-        for (int j = 0; j < M; ++j) s += H[i][j] * g[j];
+        for (int j = 0; j < M; ++j) s += H.at(i, j) * g[j];
         pk[i] = -s;
       }
       // ---- line search (jax line_search, c1 1e-4, c2 0.9, maxiter 10) ----
@@ -342,9 +644,10 @@ insite_refine_kernel(RefineArgs ra) {
         int j = 0;
         double a_rec = (a_lo + a_hi) / 2.0, phi_rec = (phi_lo + phi_hi) / 2.0;
         double za = 1.0, zphi = phi_lo;
-        double zg[M];
+        // the zoom's star gradient starts as the line search's g_0 (jax _zoom: g_star = g_0) and is the line
+        // search's result: kept in g_star itself (no third gradient array live across the objective scans)
 #pragma unroll RU
-        for (int i = 0; i < M; ++i) zg[i] = g[i];
+        for (int i = 0; i < M; ++i) g_star[i] = g[i];
         while (!done && !z_failed) {
           const double dalpha = a_hi - a_lo;
           const double lo = fmin(a_hi, a_lo), hi = fmax(a_hi, a_lo);
@@ -376,7 +679,7 @@ insite_refine_kernel(RefineArgs ra) {
             za = a_j;
             zphi = phi_j;
 #pragma unroll RU
-            for (int i = 0; i < M; ++i) zg[i] = g_j[i];
+            for (int i = 0; i < M; ++i) g_star[i] = g_j[i];
           }
           if (hi_to_lo) {
             a_rec = a_hi;
@@ -397,8 +700,6 @@ insite_refine_kernel(RefineArgs ra) {
         }
         a_star = za;
         phi_star = zphi;
-#pragma unroll RU
-        for (int i = 0; i < M; ++i) g_star[i] = zg[i];
       };
       while (!ls_done && li <= 10 && !ls_failed) {
         const double a_i = li == 1 ? start_a : a_i1 * 2.0;
@@ -407,20 +708,16 @@ insite_refine_kernel(RefineArgs ra) {
         const bool s_z1 = wolfe_one(a_i, phi_i) || ((phi_i >= phi_i1) && (li > 1));
         const bool s_i = wolfe_two(dphi_i) && !s_z1;
         const bool s_z2 = (dphi_i >= 0.0) && !s_z1 && !s_i;
-        if (s_z1) {
-          bool zf;
-          zoom(a_i1, phi_i1, dphi_i1, a_i, phi_i, dphi_i, zf);
-          ls_failed = ls_failed || zf;
-        }
         if (s_i) {
           a_star = a_i;
           phi_star = phi_i;
 #pragma unroll RU
           for (int i = 0; i < M; ++i) g_star[i] = g_i[i];
         }
-        if (s_z2) {
+        if (s_z1 || s_z2) {  // at most one of the two (jax runs both zooms masked; one body here)
           bool zf;
-          zoom(a_i, phi_i, dphi_i, a_i1, phi_i1, dphi_i1, zf);
+          if (s_z1) zoom(a_i1, phi_i1, dphi_i1, a_i, phi_i, dphi_i, zf);
+          else zoom(a_i, phi_i, dphi_i, a_i1, phi_i1, dphi_i1, zf);
           ls_failed = ls_failed || zf;
         }
         ls_done = s_z1 || ls_done || s_i || s_z2;
@@ -451,7 +748,7 @@ insite_refine_kernel(RefineArgs ra) {
         for (int i = 0; i < M; ++i) {
           double t = 0.0;
 #pragma unroll RU
-          for (int j = 0; j < M; ++j) t += H[i][j] * yk[j];
+          for (int j = 0; j < M; ++j) t += H.at(i, j) * yk[j];
           hy[i] = t;
           yhy += yk[i] * t;
         }
@@ -460,20 +757,19 @@ insite_refine_kernel(RefineArgs ra) {
         for (int i = 0; i < M; ++i)
 #pragma unroll RU
           for (int j = 0; j < M; ++j)
-            H[i][j] = H[i][j] - rho * (sk[i] * hy[j] + hy[i] * sk[j]) + cs * (sk[i] * sk[j]);
+            H.at(i, j) = H.at(i, j) - rho * (sk[i] * hy[j] + hy[i] * sk[j]) + cs * (sk[i] * sk[j]);
       } else if (isfinite(rho)) {
-        double W[M][M], WH[M][M];
-#pragma unroll RU
-        for (int i = 0; i < M; ++i)
-#pragma unroll RU
-          for (int j = 0; j < M; ++j) W[i][j] = (i == j ? 1.0 : 0.0) - rho * (sk[i] * yk[j]);
+        // (w @ H) @ w.T with w = I - rho s y^T formed on the fly (the same products and summation order as the
+        // explicit w: w[i][q] = [i == q] - rho (s_i y_q)); WH in VGPRs (the line search's state is dead here)
+        auto w = [&](int i, int q) { return (i == q ? 1.0 : 0.0) - rho * (sk[i] * yk[q]); };
+        double WH[M][M];
 #pragma unroll RU
         for (int i = 0; i < M; ++i)
 #pragma unroll RU
           for (int j = 0; j < M; ++j) {
             double s = 0.0;
 #pragma unroll RU
-            for (int q = 0; q < M; ++q) s += W[i][q] * H[q][j];
+            for (int q = 0; q < M; ++q) s += w(i, q) * H.at(q, j);
             WH[i][j] = s;
           }
 #pragma unroll RU
@@ -482,8 +778,8 @@ insite_refine_kernel(RefineArgs ra) {
           for (int j = 0; j < M; ++j) {
             double s = 0.0;
 #pragma unroll RU
-            for (int q = 0; q < M; ++q) s += WH[i][q] * W[j][q];
-            H[i][j] = s + rho * (sk[i] * sk[j]);
+            for (int q = 0; q < M; ++q) s += WH[i][q] * w(j, q);
+            H.at(i, j) = s + rho * (sk[i] * sk[j]);
           }
       }
       double gm = 0.0;
@@ -505,6 +801,7 @@ insite_refine_kernel(RefineArgs ra) {
       for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
     }
   }
+#endif  // INSITE_REFINE_FLAT
   // ---------------- final Euler scan with the (refined) model, every coefficient (sindy.py:668) ----------------
   // coefficient q: the refined value if active, else the global one; resolved by comparison against the
   // active list (no dynamically indexed per-lane array, which would live in scratch)
@@ -559,7 +856,10 @@ template <int NA, int D>
 void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
   const int m = ra.m;
   if constexpr (D == 1) {
-    if (m <= 4) insite_refine_kernel<4, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+    // the sparse models get a kernel sized to their active count (register budget: INSITE_REFINE_WPE4 waves)
+    if (m <= 2) insite_refine_kernel<2, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+    else if (m == 3) insite_refine_kernel<3, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+    else if (m <= 4) insite_refine_kernel<4, NA, D><<<grid, kBlock, 0, hs>>>(ra);
     else if (m <= 8) insite_refine_kernel<8, NA, D><<<grid, kBlock, 0, hs>>>(ra);
     else if (m <= 16) insite_refine_kernel<16, NA, D><<<grid, kBlock, 0, hs>>>(ra);
     else if (m <= 36) insite_refine_kernel<36, NA, D><<<grid, kBlock, 0, hs>>>(ra);
@@ -609,6 +909,11 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
       ra.t_ucode[m] = code;
       ++m;
     }
+  }
+  if (m <= 4) {  // RefineArgs::gmap (used by the M <= 4, D = 1 kernels)
+    for (int i = 0; i < m; ++i)
+      for (int a = 0; a < n_arms; ++a)
+        if ((ra.t_mask[i] >> a) & 1) ra.gmap |= 1 << (i * 8 + a * 2 + (ra.t_ex[i] & 1));
   }
   if (n_rows == 0) return INSITE_OK;
   if (!V || (bits && !arm_bits) || !seq_len || !preds || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
@@ -710,18 +1015,48 @@ int32_t insite_refine_arms_f64(const double* V, int64_t ld_v, int32_t T, const i
 namespace {
 constexpr int kPrepTc = 16;
 constexpr int kPrepLd = kPrepTc + 1;  // odd row stride: lane-per-row reads hit distinct banks
+// per-row side arrays moved with the rows (ABI 8): lane l <- row r (prepare), row r <- lane l (finish)
+struct RowGather {
+  const double* u;
+  int32_t U;
+  double* u_out;
+  const int32_t* sl;
+  int32_t* sl_out;
+  __device__ void gather(int64_t l, int64_t r) const {
+    if (u_out)
+      for (int i = 0; i < U; ++i) u_out[l * U + i] = u[r * U + i];
+    if (sl_out) sl_out[l] = sl[r];
+  }
+};
+struct RowScatter {
+  const double* coef;
+  int32_t nc;
+  double* coef_out;
+  const int32_t* st;
+  int32_t* st_out;
+  const int32_t* it;
+  int32_t* it_out;
+  __device__ void scatter(int64_t l, int64_t r) const {
+    if (coef_out)
+      for (int q = 0; q < nc; ++q) coef_out[r * nc + q] = coef[l * nc + q];
+    if (st_out) st_out[r] = st[l];
+    if (it_out) it_out[r] = it[l];
+  }
+};
 __global__ void __launch_bounds__(kBlock) refine_prepare_kernel(const double* __restrict__ V, int64_t ld_v,
                                                                 const int8_t* __restrict__ arm, int64_t ld_arm,
                                                                 int64_t N, int32_t T, double* __restrict__ Vt,
                                                                 int64_t ld_vt, uint32_t* __restrict__ bits,
                                                                 int64_t ld_bits, int8_t* __restrict__ arm_t,
-                                                                int64_t ld_armt, const int32_t* __restrict__ order) {
+                                                                int64_t ld_armt, const int32_t* __restrict__ order,
+                                                                RowGather rg) {
   __shared__ double sv[kWavesPerBlock][kWave * kPrepLd];
   __shared__ int sa[kWavesPerBlock][kWave * kPrepLd];
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const int64_t p0 = (int64_t)blockIdx.x * kBlock + wv * kWave;  // the wave's first patient
   const int64_t p = p0 + lane;
   const bool act = p < N;
+  if (act) rg.gather(p, order ? (int64_t)order[p] : p);
   const int64_t w0 = p0 >> 5;  // the wave's two bit words
   double* lv = sv[wv];
   int* la = sa[wv];
@@ -758,11 +1093,12 @@ __global__ void __launch_bounds__(kBlock) refine_prepare_kernel(const double* __
 // store instruction writes 4 patients' 128-B row segments.
 __global__ void __launch_bounds__(kBlock) refine_finish_kernel(const double* __restrict__ P, int64_t ld_t,
                                                                const int32_t* __restrict__ order, int64_t N, int32_t T,
-                                                               double* __restrict__ out, int64_t ld_pm) {
+                                                               double* __restrict__ out, int64_t ld_pm, RowScatter rs) {
   __shared__ double sv[kWavesPerBlock][kWave * kPrepLd];
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const int64_t p0 = (int64_t)blockIdx.x * kBlock + wv * kWave;
   const int64_t l = p0 + lane;
+  if (l < N) rs.scatter(l, order ? (int64_t)order[l] : l);
   double* lv = sv[wv];
   for (int t0 = 0; t0 < T; t0 += kPrepTc) {
     const int tc = T - t0 < kPrepTc ? T - t0 : kPrepTc;
@@ -795,12 +1131,14 @@ __global__ void __launch_bounds__(kWave) refine_prepare_rows_kernel(const double
                                                                     int64_t N, int32_t T, double* __restrict__ Vt,
                                                                     int64_t ld_vt, uint32_t* __restrict__ bits,
                                                                     int64_t ld_bits, int8_t* __restrict__ arm_t,
-                                                                    int64_t ld_armt, const int32_t* __restrict__ order) {
+                                                                    int64_t ld_armt, const int32_t* __restrict__ order,
+                                                                    RowGather rg) {
   __shared__ double lv[kWave * kRowLd];
   __shared__ int8_t la[kWave * kRowLd];
   const int lane = threadIdx.x;
   const int64_t p0 = (int64_t)blockIdx.x * kWave;
   const int nr = N - p0 < kWave ? (int)(N - p0) : kWave;
+  if (lane < nr) rg.gather(p0 + lane, order ? (int64_t)order[p0 + lane] : p0 + lane);
   for (int r = 0; r < nr; ++r) {
     const int64_t row = order ? (int64_t)order[p0 + r] : p0 + r;
     if (lane < T) {
@@ -828,11 +1166,13 @@ __global__ void __launch_bounds__(kWave) refine_prepare_rows_kernel(const double
 
 __global__ void __launch_bounds__(kWave) refine_finish_rows_kernel(const double* __restrict__ P, int64_t ld_t,
                                                                    const int32_t* __restrict__ order, int64_t N,
-                                                                   int32_t T, double* __restrict__ out, int64_t ld_pm) {
+                                                                   int32_t T, double* __restrict__ out, int64_t ld_pm,
+                                                                   RowScatter rs) {
   __shared__ double lv[kWave * kRowLd];
   const int lane = threadIdx.x;
   const int64_t p0 = (int64_t)blockIdx.x * kWave;
   const int nr = N - p0 < kWave ? (int)(N - p0) : kWave;
+  if (lane < nr) rs.scatter(p0 + lane, order ? (int64_t)order[p0 + lane] : p0 + lane);
   if (lane < nr)
     for (int t = 0; t < T; ++t) lv[lane * kRowLd + t] = P[(int64_t)t * ld_t + p0 + lane];
   __syncthreads();
@@ -844,40 +1184,53 @@ __global__ void __launch_bounds__(kWave) refine_finish_rows_kernel(const double*
 }  // namespace
 
 extern "C" int32_t insite_refine_finish_f64(const double* preds_tm, int64_t ld_t, const int32_t* row_order,
-                                            int64_t n_rows, int32_t T, double* preds_pm, int64_t ld_pm, void* stream) {
+                                            int64_t n_rows, int32_t T, double* preds_pm, int64_t ld_pm,
+                                            const double* coef_lane, int32_t n_coef, double* coef_out,
+                                            const int32_t* status_lane, int32_t* status_out, const int32_t* iters_lane,
+                                            int32_t* iters_out, void* stream) {
   if (n_rows < 0 || T < 1 || !preds_tm || !preds_pm || ld_t < n_rows || ld_pm < T) return INSITE_E_INVALID_ARG;
+  if ((coef_lane == nullptr) != (coef_out == nullptr) || (status_lane == nullptr) != (status_out == nullptr) ||
+      (iters_lane == nullptr) != (iters_out == nullptr) || (coef_out && n_coef < 1))
+    return INSITE_E_INVALID_ARG;
   if (n_rows == 0) return INSITE_OK;
+  const RowScatter rs{coef_lane, n_coef, coef_out, status_lane, status_out, iters_lane, iters_out};
   if (INSITE_PREP_ROWS && T <= kWave) {
     refine_finish_rows_kernel<<<dim3((unsigned)((n_rows + kWave - 1) / kWave)), kWave, 0,
-                                static_cast<hipStream_t>(stream)>>>(preds_tm, ld_t, row_order, n_rows, T, preds_pm, ld_pm);
+                                static_cast<hipStream_t>(stream)>>>(preds_tm, ld_t, row_order, n_rows, T, preds_pm, ld_pm,
+                                                                    rs);
     return hipGetLastError() == hipSuccess ? INSITE_OK : INSITE_E_HIP;
   }
   const dim3 grid((unsigned)((n_rows + kBlock - 1) / kBlock));
   refine_finish_kernel<<<grid, kBlock, 0, static_cast<hipStream_t>(stream)>>>(preds_tm, ld_t, row_order, n_rows, T,
-                                                                              preds_pm, ld_pm);
+                                                                              preds_pm, ld_pm, rs);
   return hipGetLastError() == hipSuccess ? INSITE_OK : INSITE_E_HIP;
 }
 
 extern "C" int32_t insite_refine_prepare_f64(const double* V, int64_t ld_v, const int8_t* arm, int64_t ld_arm,
                                              int64_t n_rows, int32_t T, double* Vt, int64_t ld_vt, uint32_t* arm_bits,
                                              int64_t ld_bits, int8_t* arm_t, int64_t ld_armt,
-                                             const int32_t* row_order, void* stream) {
+                                             const int32_t* row_order, const double* u, int32_t n_statics,
+                                             double* u_out, const int32_t* seq_len, int32_t* seq_len_out,
+                                             void* stream) {
   if (n_rows < 0 || T < 1 || !V || !Vt || ld_v < T || ld_vt < n_rows) return INSITE_E_INVALID_ARG;
   if (arm && (ld_arm < T || (arm_bits == nullptr) == (arm_t == nullptr))) return INSITE_E_INVALID_ARG;
   if (arm_bits && ld_bits < (n_rows + 31) / 32) return INSITE_E_INVALID_ARG;
   if (arm_t && ld_armt < n_rows) return INSITE_E_INVALID_ARG;
+  if ((u_out && (!u || n_statics < 1 || n_statics > INSITE_MAX_STATICS)) || (seq_len_out && !seq_len))
+    return INSITE_E_INVALID_ARG;
   if (n_rows == 0) return INSITE_OK;
+  const RowGather rg{u, n_statics, u_out, seq_len, seq_len_out};
   if (INSITE_PREP_ROWS && T <= kWave) {
     refine_prepare_rows_kernel<<<dim3((unsigned)((n_rows + kWave - 1) / kWave)), kWave, 0,
                                  static_cast<hipStream_t>(stream)>>>(
         V, ld_v, arm, ld_arm, n_rows, T, Vt, ld_vt, arm ? arm_bits : nullptr, ld_bits, arm ? arm_t : nullptr, ld_armt,
-        row_order);
+        row_order, rg);
     return hipGetLastError() == hipSuccess ? INSITE_OK : INSITE_E_HIP;
   }
   const dim3 grid((unsigned)((n_rows + kBlock - 1) / kBlock));
   refine_prepare_kernel<<<grid, kBlock, 0, static_cast<hipStream_t>(stream)>>>(
       V, ld_v, arm, ld_arm, n_rows, T, Vt, ld_vt, arm ? arm_bits : nullptr, ld_bits, arm ? arm_t : nullptr, ld_armt,
-      row_order);
+      row_order, rg);
   return hipGetLastError() == hipSuccess ? INSITE_OK : INSITE_E_HIP;
 }
 

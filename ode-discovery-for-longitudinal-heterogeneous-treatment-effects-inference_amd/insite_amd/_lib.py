@@ -150,8 +150,9 @@ _SIGNATURES = {
                                            _vp, _vp, _vp, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _c_i32, _vp, _c_i64,
                                            _vp, _vp, _vp, _vp, _vp, _vp]),
     "insite_refine_prepare_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i64, _c_i32, _vp, _c_i64, _vp, _c_i64, _vp,
-                                           _c_i64, _vp, _vp]),
-    "insite_refine_finish_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _vp, _c_i64, _vp]),
+                                           _c_i64, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp]),
+    "insite_refine_finish_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _vp, _c_i64, _vp, _c_i32, _vp, _vp, _vp,
+                                          _vp, _vp, _vp]),
     "insite_gen_gram_segments_workspace_bytes": (_c_size, [_c_i64, _c_i32, _c_i32]),
     "insite_gen_gram_segments_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _c_i32, _vp, _vp, _c_i32, _c_i64,
                                               _c_i32, _vp, _c_i32, _c_i32, _c_f64, _vp, _vp, _vp, _c_size, _vp]),

@@ -978,36 +978,141 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
     if A > 4:
         raise ValueError("at most 4 treatment arms (joint model: 2 binary treatment inputs)")
     order = rk45_order(seq_len, T) if (binned and N > 64) else None
-    Vt, arms = refine_prepare(V, arm, bits=A <= 2, order=order)
     if order is None:
+        Vt, arms = refine_prepare(V, arm, bits=A <= 2, order=None)
         preds, coef, status, iters = insite_refine_tm(Vt, arms, u, seq_len, c0, lib, dt, lam, tau, substeps,
                                                       revert_on_zoom_fail, nfev=nfev)
         return preds.t(), coef, status, iters
-    # binned: the inputs were gathered in lane order, the kernel runs the identity order on them (coalesced
-    # loads and stores), and the outputs are scattered back to row order
-    idx = order.long()
-    u_l = u.index_select(0, idx).contiguous() if lib.n_statics else u
+    # binned: the rows (with their statics and sequence lengths) are gathered in lane order by ONE prepare pass,
+    # the kernel runs the identity order on them (coalesced loads and stores), and ONE finish pass scatters the
+    # predictions, coefficients, statuses and iteration counts back to row order
+    Vt, arms, u_l, sl_l = refine_prepare(V, arm, bits=A <= 2, order=order, u=u if lib.n_statics else None,
+                                         seq_len=seq_len)
     nf = torch.empty_like(nfev) if nfev is not None else None
-    preds, coef, status, iters = insite_refine_tm(Vt, arms, u_l, seq_len.index_select(0, idx).contiguous(), c0, lib,
-                                                  dt, lam, tau, substeps, revert_on_zoom_fail, nfev=nf)
-    back = lambda t: torch.empty_like(t).index_copy_(0, idx, t)   # noqa: E731
+    preds, coef, status, iters = insite_refine_tm(Vt, arms, u_l if lib.n_statics else u, sl_l, c0, lib, dt, lam, tau,
+                                                  substeps, revert_on_zoom_fail, nfev=nf)
     if nfev is not None:
-        nfev.index_copy_(0, idx, nf)
-    return refine_finish(preds, order, N), back(coef), back(status), back(iters)
+        nfev.index_copy_(0, order.long(), nf)
+    return refine_finish(preds, order, N, lane_outputs=(coef, status, iters))
 
 
-def refine_prepare(V: torch.Tensor, arm: torch.Tensor, bits: bool = True, order: torch.Tensor | None = None):
+class InsiteRefinePlan:
+    """``insite_refine`` (binned) prepared once: the inputs validated (the arm range check included) and every buffer
+    and argument packed, so a call enqueues exactly four C calls -- the seq_len counting sort
+    (insite_rk45_order_i32), the gather pass (insite_refine_prepare_f64: rows, statics, sequence lengths into lane
+    order), the refinement kernel, and the scatter pass (insite_refine_finish_f64: predictions, coefficients,
+    statuses, iteration counts back to row order) -- with no host synchronisation.  Outputs ``out`` = (preds
+    [N, T], coef [N, A, F], status [N], iters [N]), bitwise those of ``insite_refine``.  The plan keeps references
+    to its inputs: refresh them in place between calls (a serving loop) or make a new plan."""
+
+    def __init__(self, V, arm, u, seq_len, coef0, lib, dt, lam, tau, substeps=5, revert_on_zoom_fail=False):
+        L = _lib.load()
+        _dev("V", V, torch.float64, 2)
+        _dev("arm", arm, torch.int8, 2)
+        N, T = V.shape
+        if arm.shape != (N, T) or V.stride(1) != 1 or arm.stride(1) != 1 or N < 1:
+            raise ValueError("V and arm must be row-contiguous [N >= 1, T]")
+        _dev("seq_len", seq_len, torch.int32, 1)
+        if seq_len.numel() != N:
+            raise ValueError("seq_len must have one entry per row")
+        if lib.n_statics:
+            _dev("u", u, torch.float64, 2)
+            if u.size(0) != N or u.size(1) != lib.n_statics or not u.is_contiguous():
+                raise ValueError("u must be a contiguous [N, n_statics] tensor")
+        c0 = np.ascontiguousarray(coef0, dtype=np.float64)
+        if c0.ndim != 2 or c0.shape[1] != lib.n_terms:
+            raise ValueError("coef0 must be a host [A, F] array")
+        mask, qexps, A = refine_terms(lib, c0.shape[0])
+        if A > 4:
+            raise ValueError("at most 4 treatment arms (joint model: 2 binary treatment inputs)")
+        bits = A <= 2
+        if bits and int(arm.amax().item()) > 1:          # once, here: the calls never synchronise
+            raise ValueError("bit-packed arms need n_arms <= 2 (arm values 0/1)")
+        dev = V.device
+        W = (N + 31) // 32
+        U = lib.n_statics
+        self.order = torch.empty((N,), dtype=torch.int32, device=dev)
+        self.Vt = torch.empty((T, N), dtype=torch.float64, device=dev)
+        self.arms = torch.empty((T, W) if bits else (T, N), dtype=torch.int32 if bits else torch.int8, device=dev)
+        self.u_l = torch.empty_like(u) if U else None
+        self.sl_l = torch.empty_like(seq_len)
+        self.P = torch.empty((T, N), dtype=torch.float64, device=dev)
+        self.coef_l = torch.empty((N,) + c0.shape, dtype=torch.float64, device=dev)
+        self.st_l = torch.empty((N,), dtype=torch.int32, device=dev)
+        self.it_l = torch.empty((N,), dtype=torch.int32, device=dev)
+        self.out = (torch.empty((N, T), dtype=torch.float64, device=dev), torch.empty_like(self.coef_l),
+                    torch.empty_like(self.st_l), torch.empty_like(self.it_l))
+        self._ows = Workspace("scratch").get(L.insite_rk45_order_workspace_bytes(int(T)), dev)
+        nul = ctypes.c_void_p(0)
+        self._c0, self._mask, self._qexps, self._tab = c0, mask, qexps, lib.ctypes_table()
+        self._keep = (V, arm, u, seq_len)
+        self.device = dev
+        self._calls = [
+            (L.insite_rk45_order_i32, (_p(seq_len), N, int(T), _p(self.order), _p(self._ows), self._ows.numel())),
+            (L.insite_refine_prepare_f64, (_p(V), V.stride(0), _p(arm), arm.stride(0), N, T, _p(self.Vt), N,
+                                           _p(self.arms) if bits else nul, W, nul if bits else _p(self.arms), N,
+                                           _p(self.order), _p(u) if U else nul, U, _p(self.u_l) if U else nul,
+                                           _p(seq_len), _p(self.sl_l))),
+        ]
+        common = (float(dt), float(lam), int(tau), int(substeps), int(bool(revert_on_zoom_fail)), _p(self.P), N,
+                  _p(self.coef_l), _p(self.st_l), _p(self.it_l))
+        ustat = _p(self.u_l) if U else nul
+        if lib.n_inputs:
+            self._calls.append((L.insite_refine_general_f64, (
+                _p(self.Vt), N, T, _p(self.arms) if bits else nul, nul if bits else _p(self.arms), self.arms.stride(0),
+                ustat, _p(self.sl_l), N, U, c0.size, c0.ctypes.data_as(ctypes.c_void_p),
+                mask.ctypes.data_as(ctypes.c_void_p), qexps.ctypes.data_as(ctypes.c_void_p), A) + common + (nul, nul)))
+        else:
+            fn = L.insite_refine_f64 if bits else L.insite_refine_arms_f64
+            self._calls.append((fn, (_p(self.Vt), N, T, _p(self.arms), self.arms.stride(0), ustat, _p(self.sl_l), N, U,
+                                     self._tab.ctypes.data_as(ctypes.c_void_p), lib.n_terms,
+                                     c0.ctypes.data_as(ctypes.c_void_p), A) + common + (nul,)))
+        P_, co, so, io = self.out
+        self._calls.append((L.insite_refine_finish_f64, (_p(self.P), N, _p(self.order), N, T, _p(P_), T,
+                                                         _p(self.coef_l), int(c0.size), _p(co), _p(self.st_l), _p(so),
+                                                         _p(self.it_l), _p(io))))
+
+    def __call__(self, stream: torch.cuda.Stream | None = None):
+        h = ctypes.c_void_p((stream if stream is not None else torch.cuda.current_stream(self.device)).cuda_stream)
+        for fn, args in self._calls:
+            st = fn(*args, h)
+            if st:
+                _lib.check(getattr(fn, "__name__", "insite refine plan"), st)
+        return self.out
+
+
+def plan_insite_refine(V, arm, u, seq_len, coef0, lib, dt, lam, tau, substeps=5, revert_on_zoom_fail=False):
+    """``insite_refine`` (binned lane order) as a prepared plan (``InsiteRefinePlan``)."""
+    return InsiteRefinePlan(V, arm, u, seq_len, coef0, lib, dt, lam, tau, substeps, revert_on_zoom_fail)
+
+
+def refine_prepare(V: torch.Tensor, arm: torch.Tensor, bits: bool = True, order: torch.Tensor | None = None,
+                   u: torch.Tensor | None = None, seq_len: torch.Tensor | None = None, check: bool = True):
     """Patient-major V [N, T] f64 and per-step arms [N, T] int8 -> the refinement kernels' time-major Vt [T, N] and
     arms (bit-packed int32 [T, ceil(N / 32)] when ``bits``, else int8 [T, N]) in one device pass
     (insite_refine_prepare_f64).  Bit-packing needs arm values 0 / 1 (checked here: two arms, or the joint
-    model's combination codes of one binary input).  ``order`` [N] int32: output column l takes row order[l]."""
+    model's combination codes of one binary input; ``check=False`` skips that device-to-host check for a caller
+    that validated the arms once).  ``order`` [N] int32: output column l takes row order[l]; with ``u`` [N, U]
+    and / or ``seq_len`` [N] the same pass gathers them too and the result is (Vt, arms, u_l, seq_len_l)."""
     _dev("V", V, torch.float64, 2)
     _dev("arm", arm, torch.int8, 2)
     N, T = V.shape
     if arm.shape != (N, T) or V.stride(1) != 1 or arm.stride(1) != 1:
         raise ValueError("V and arm must be row-contiguous [N, T]")
-    if bits and N and int(arm.amax().item()) > 1:
+    if check and bits and N and int(arm.amax().item()) > 1:
         raise ValueError("bit-packed arms need n_arms <= 2 (arm values 0/1)")
+    side = u is not None or seq_len is not None
+    u_l = sl_l = None
+    if u is not None:
+        _dev("u", u, torch.float64, 2)
+        if u.size(0) != N or not u.is_contiguous():
+            raise ValueError("u must be a contiguous [N, n_statics] tensor")
+        u_l = torch.empty_like(u)
+    if seq_len is not None:
+        _dev("seq_len", seq_len, torch.int32, 1)
+        if seq_len.numel() != N:
+            raise ValueError("seq_len must have one entry per row")
+        sl_l = torch.empty_like(seq_len)
     Vt = torch.empty((T, N), dtype=torch.float64, device=V.device)
     W = (N + 31) // 32
     at = torch.empty((T, W) if bits else (T, N), dtype=torch.int32 if bits else torch.int8, device=V.device)
@@ -1018,14 +1123,17 @@ def refine_prepare(V: torch.Tensor, arm: torch.Tensor, bits: bool = True, order:
             raise ValueError("order must be an [N] permutation")
     st = _lib.load().insite_refine_prepare_f64(_p(V), V.stride(0), _p(arm), arm.stride(0), N, T, _p(Vt), N,
                                                _p(at) if bits else nul, W, nul if bits else _p(at), N, _p(order),
+                                               _p(u), u.size(1) if u is not None else 0, _p(u_l), _p(seq_len), _p(sl_l),
                                                _stream(V.device))
     _lib.check("insite_refine_prepare_f64", st)
-    return Vt, at
+    return (Vt, at, u_l, sl_l) if side else (Vt, at)
 
 
-def refine_finish(P: torch.Tensor, order: torch.Tensor | None, N: int) -> torch.Tensor:
+def refine_finish(P: torch.Tensor, order: torch.Tensor | None, N: int, lane_outputs: tuple | None = None):
     """Time-major refinement predictions P [T, >= N] whose column l is row order[l] (identity when None) ->
-    patient-major [N, T] (insite_refine_finish_f64)."""
+    patient-major [N, T] (insite_refine_finish_f64).  ``lane_outputs`` = (coef [N, ...] f64, status [N] int32,
+    iters [N] int32) in lane order: the same pass scatters them back to row order and the result is
+    (preds, coef, status, iters)."""
     _dev("P", P, torch.float64, 2)
     T = P.size(0)
     if P.size(1) < N or P.stride(1) != 1:
@@ -1033,9 +1141,23 @@ def refine_finish(P: torch.Tensor, order: torch.Tensor | None, N: int) -> torch.
     if order is not None:
         _dev("order", order, torch.int32, 1)
     out = torch.empty((N, T), dtype=torch.float64, device=P.device)
-    st = _lib.load().insite_refine_finish_f64(_p(P), P.stride(0), _p(order), N, T, _p(out), T, _stream(P.device))
+    nul = ctypes.c_void_p(0)
+    if lane_outputs is not None:
+        c, s_, it = lane_outputs
+        _dev("coef", c, torch.float64)
+        _dev("status", s_, torch.int32, 1)
+        _dev("iters", it, torch.int32, 1)
+        if c.size(0) != N or not c.is_contiguous() or s_.numel() != N or it.numel() != N:
+            raise ValueError("lane outputs must have one contiguous row per refined row")
+        co, so, io = torch.empty_like(c), torch.empty_like(s_), torch.empty_like(it)
+        nc = c.numel() // max(N, 1)
+        extra = (_p(c), nc, _p(co), _p(s_), _p(so), _p(it), _p(io))
+    else:
+        extra = (nul, 0, nul, nul, nul, nul, nul)
+    st = _lib.load().insite_refine_finish_f64(_p(P), P.stride(0), _p(order), N, T, _p(out), T, *extra,
+                                              _stream(P.device))
     _lib.check("insite_refine_finish_f64", st)
-    return out
+    return (out, co, so, io) if lane_outputs is not None else out
 
 
 def insite_refine_tm(Vt: torch.Tensor, arms: torch.Tensor, u: torch.Tensor, seq_len: torch.Tensor, coef0,

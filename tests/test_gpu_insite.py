@@ -292,3 +292,42 @@ def test_refine_prepare_finish_with_row_order(dev, N, T):
     back = ops.refine_finish(Vt, order, N)
     assert torch.equal(back, V)
     assert torch.equal(ops.refine_finish(V.t().contiguous(), None, N), V)
+    # ABI 8: the same passes move the per-row side arrays (statics, sequence lengths in; coefficients, statuses,
+    # iteration counts out)
+    u = torch.randn((N, 2), generator=g, device=dev, dtype=torch.float64)
+    sl = torch.randint(0, T, (N,), generator=g, device=dev, dtype=torch.int32)
+    Vt2, bits2, u_l, sl_l = ops.refine_prepare(V, arm, bits=True, order=order, u=u, seq_len=sl)
+    assert torch.equal(Vt2, Vt) and torch.equal(bits2, bits)
+    assert torch.equal(u_l, u[idx]) and torch.equal(sl_l, sl[idx])
+    c_l = torch.randn((N, 2, 7), generator=g, device=dev, dtype=torch.float64)
+    s_l = torch.randint(-1, 4, (N,), generator=g, device=dev, dtype=torch.int32)
+    i_l = torch.randint(0, 9, (N,), generator=g, device=dev, dtype=torch.int32)
+    P, c, s_, it = ops.refine_finish(Vt, order, N, lane_outputs=(c_l, s_l, i_l))
+    assert torch.equal(P, V)
+    for got, lane in ((c, c_l), (s_, s_l), (it, i_l)):
+        want = torch.empty_like(lane).index_copy_(0, idx, lane)
+        assert torch.equal(got, want)
+
+
+def test_insite_refine_plan_equals_eager(dev):
+    """ops.plan_insite_refine (the INSITE bench step: sort, gather, kernel, scatter -- 4 C calls, no host sync)
+    returns bitwise what ops.insite_refine(binned=True) returns, over repeated calls."""
+    from insite_amd import cohort, ops
+    N, T = 20_000, 60
+    coh = cohort.synthetic_pkpd(N, T, seed=31, device=dev, equation="EQ_4_C")
+    V = coh.x[:, :T].contiguous()
+    g = torch.Generator(device=dev)
+    g.manual_seed(32)
+    flip = torch.randint(1, T, (N, 1), generator=g, device=dev)
+    arm = torch.where(torch.arange(T, device=dev)[None, :] >= flip, 1 - coh.arm[:, None].to(torch.int64),
+                      coh.arm[:, None].to(torch.int64)).to(torch.int8).contiguous()
+    sl = torch.randint(1, T, (N,), generator=g, device=dev, dtype=torch.int32)
+    c0 = np.zeros((2, coh.lib.n_terms))
+    c0[0, 4], c0[1, 1], c0[1, 5] = -1.1107592869834308, -0.14540553723951796, -1.0234639833519243
+    plan = ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5)
+    want = ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5, binned=True)
+    for _ in range(2):
+        got = plan()
+        torch.cuda.synchronize()
+        for a, b in zip(got, want):
+            assert torch.equal(a, b)
