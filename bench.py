@@ -644,6 +644,19 @@ def insite_main(args):
     torch.cuda.synchronize(dev)
     same = bool(torch.equal(s2, status[idx]) and torch.equal(i2, iters[idx]) and torch.equal(p2.t(), preds[idx]))
     K = torch.clamp(sl_l.to(torch.int64) - 5, min=0, max=T - 1)
+    # SIMT divergence of the refinement: a wave runs until its slowest lane's last scan, each scan as long as its
+    # longest lane's window -- wave cost ~ max(nfev) x max(K) over its 64 lanes against the rows' own nfev x K
+    nfk = nf.to(torch.int64).cpu().numpy()
+    kk = K.cpu().numpy()
+    nw = (N + 63) // 64
+    pad = nw * 64 - N
+    nfw = np.concatenate([nfk, np.zeros(pad, np.int64)]).reshape(nw, 64)
+    kw = np.concatenate([kk, np.zeros(pad, np.int64)]).reshape(nw, 64)
+    divergence = {"row_scan_steps": int((nfk * kk).sum()),
+                  "wave_scan_steps_max_nfev_x_max_K": int((nfw.max(1) * kw.max(1)).sum() * 64),
+                  "mean_nfev": float(nfk.mean()), "mean_wave_max_nfev": float(nfw.max(1).mean()),
+                  "mean_K": float(kk.mean()), "mean_wave_max_K": float(kw.max(1).mean())}
+    divergence["ratio"] = divergence["wave_scan_steps_max_nfev_x_max_K"] / max(1, divergence["row_scan_steps"])
     A_, SUB = 2, 5
     per_step = SUB * (4 * A_ + 7) + 4 * A_ + 5     # Euler sub-steps with the A x 2 sensitivities + residual/gradient
     refine_flop = float((nf.to(torch.int64) * K).sum().item()) * per_step
@@ -667,7 +680,7 @@ def insite_main(args):
                    "reference_wall_time_s": "88.96 s per INSITE EQ_4_A run incl. 59,000 + 11,800 refinements "
                                             "(results/2_main_table/final_with_insite.txt:2346; SURVEY.md §6)",
                    "mean_evaluations_per_refined_row": float(nf.to(torch.float64)[s2 >= 0].mean().item()),
-                   "evaluation_count_route_matches": same},
+                   "evaluation_count_route_matches": same, "divergence": divergence},
         "roofline": {"kernel": "insite_refine_kernel<4, 2, 1> (per-row BFGS + final Euler-5 scan)", "bound": "valu-f64",
                      "unit": "TFLOP/s", "achieved": flop / (kern_ms * 1e-3) / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
                      "frac": flop / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,

@@ -98,7 +98,18 @@ __device__ __forceinline__ double dpoly(const double (&g)[D + 1], double y) {
 #ifndef INSITE_REFINE_SU4
 #define INSITE_REFINE_SU4 5  // sub-step unroll of the M <= 4 kernel: 7.23 -> 7.03 ms INSITE step (profiles/r03/v30); 1 = rolled
 #endif
-template <int M, int NA, int D>
+// Windowed scans (INSITE_REFINE_WIN, T <= 64, two bit arms, M <= 4, affine RHS): the objective's targets V[k + 1]
+// reach the wave through an LDS ring of kWin-step slots filled by LDS-DMA (global_load_lds_dwordx4: one instruction
+// moves 2 steps x 64 rows, 1 KiB, no VGPR destination) one slot AHEAD, and each lane's arms sit in one 64-bit mask
+// (no per-step loads at all).  With a one-step register prefetch every step of every scan waited on an L2 / MALL
+// round trip (the kernel ran ~3x its VALU time at 3 waves per SIMD).  The ring needs the wave's lanes to run the
+// scan together, so the flat loop below becomes wave-uniform in this mode (a lane with nothing pending scans 0 steps).
+constexpr int kWin = 8;
+#ifndef INSITE_REFINE_WIN
+#define INSITE_REFINE_WIN 1
+#endif
+
+template <int M, int NA, int D, bool WIN = false>
 struct RefineLane {
   static constexpr int RU = M <= kRefineRegActive ? M : 1;
   // sub-step loop unrolled by odeint's 5 (the default): measured 12 active 62 -> 43 ms, 6 active 5.5 -> 5.2 ms;
@@ -112,14 +123,43 @@ struct RefineLane {
   double norm;
   double mono[M];
   double c0a[M];
-  __device__ int armbit(int k) const {
+  uint64_t am = 0;         // WIN: arm of step k in bit k
+  double* win = nullptr;   // WIN: this wave's ring, 2 slots x kWin steps x 64 rows (step j of a slot at j * 64)
+  int64_t p0 = 0;          // WIN: the wave's first column
+  __device__ int armbit_mem(int k) const {
     if constexpr (NA == 2) return (int)((ra.arm[(int64_t)k * ra.lda + (p >> 5)] >> (p & 31)) & 1u);
     else return (int)ra.arm8[(int64_t)k * ra.lda + p];
   }
+  __device__ int armbit(int k) const {
+    if constexpr (WIN) return (int)((am >> k) & 1ull);
+    else return armbit_mem(k);
+  }
+  // WIN: LDS-DMA of target rows V[1 + c kWin .. c kWin + kWin] (clamped to T - 1) of the wave's 64 columns into ring
+  // slot `slot`; lanes 0-31 move rows 2q + 1, lanes 32-63 rows 2q + 2, 16 B (two columns) each.  Every lane of the
+  // wave must execute it (the destination is the wave-uniform slot base + lane x 16 B).
+  __device__ void fill(int c, int slot) const {
+    const int lane = threadIdx.x & (kWave - 1);
+    int64_t col = p0 + 2 * (lane & 31);
+    if (col + 1 >= ra.ldv) col = ra.ldv - 2;  // past the last column: any in-bounds pair (ldv even, never read)
+    const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(win + slot * (kWin * kWave)));
+#pragma unroll
+    for (int q = 0; q < kWin / 2; ++q) {
+      int row = c * kWin + 2 * q + (lane >> 5) + 1;
+      row = row < ra.T - 1 ? row : ra.T - 1;
+      const double* src = ra.V + (int64_t)row * ra.ldv + col;
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(src), "s"(base + q * 1024u)
+                   : "memory");
+    }
+  }
   // f and gradient at c (active coordinates)
   mutable int nev = 0;  // evaluations of f and its gradient (each one scan of the K-step window)
-  __device__ double fg(const double (&c)[M], double (&g)[M]) const {
-    ++nev;
+  // WIN: `live` = this lane's evaluation counts (its scan runs K steps); a lane with nothing pending passes false,
+  // scans 0 steps and only keeps the wave's ring loads company
+  __device__ double fg(const double (&c)[M], double (&g)[M], bool live = true) const {
+    nev += live ? 1 : 0;
     double gam[NA][D + 1];
 #pragma unroll
     for (int a = 0; a < NA; ++a)
@@ -153,16 +193,38 @@ struct RefineLane {
 #pragma unroll
       for (int e = 0; e <= D; ++e) d[a][e] = gG[a][e] = 0.0;
     double L = 0.0;
-    // step k's arm and target are requested one step ahead (issued before step k - 1's sub-steps) so the
+    const int Kl = live ? K : 0;
+    int Kw = Kl;      // WIN: the wave's longest scan (rows binned by seq_len: ~every lane's)
+    int nch = 0;
+    if constexpr (WIN) {
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) Kw = max(Kw, __shfl_xor(Kw, off));
+      nch = (Kw + kWin - 1) / kWin;
+      if (nch > 0) fill(0, 0);
+    }
+    // (non-WIN) step k's arm and target are requested one step ahead (issued before step k - 1's sub-steps) so the
     // dependent Euler chain does not wait on a load per step
-    int ak_nx = armbit(0);
-    double v_nx = ra.V[ra.ldv + p];
-    for (int k = 0; k < K; ++k) {
-      const int ak = ak_nx;
-      const double vk1 = v_nx;
-      if (k + 1 < K) {
-        ak_nx = armbit(k + 1);
-        v_nx = ra.V[(int64_t)(k + 2) * ra.ldv + p];
+    int ak_nx = WIN ? 0 : armbit(0);
+    double v_nx = WIN ? 0.0 : ra.V[ra.ldv + p];
+    const int kend = WIN ? nch * kWin : Kl;
+    for (int k = 0; k < kend; ++k) {
+      int ak;
+      double vk1;
+      if constexpr (WIN) {
+        if ((k & (kWin - 1)) == 0) {  // slot k / kWin landed; start the next one into the other slot
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (k / kWin + 1 < nch) fill(k / kWin + 1, (k / kWin + 1) & 1);
+        }
+        if (k >= Kl) continue;
+        ak = armbit(k);
+        vk1 = win[((k / kWin) & 1) * (kWin * kWave) + (k & (kWin - 1)) * kWave + (threadIdx.x & (kWave - 1))];
+      } else {
+        ak = ak_nx;
+        vk1 = v_nx;
+        if (k + 1 < Kl) {
+          ak_nx = armbit(k + 1);
+          v_nx = ra.V[(int64_t)(k + 2) * ra.ldv + p];
+        }
       }
       double gk[D + 1];
 #pragma unroll
@@ -212,7 +274,7 @@ struct RefineLane {
 #pragma unroll
         for (int e = 0; e <= D; ++e) gG[a][e] += -2.0 * r * d[a][e];
     }
-    const double iK = 1.0 / (double)K;
+    const double iK = 1.0 / (double)K;   // (a non-live WIN lane divides by its own K too; its values are unused)
     L *= iK;
     double pen = 0.0;
 #pragma unroll RU
@@ -250,11 +312,12 @@ struct RefineLane {
     return s;
   }
   // phi(t) = f(x + t pk), dphi = g . pk
-  __device__ double phi(const double (&x)[M], const double (&pk)[M], double t, double& dphi, double (&g)[M]) const {
+  __device__ double phi(const double (&x)[M], const double (&pk)[M], double t, double& dphi, double (&g)[M],
+                        bool live = true) const {
     double xt[M];
 #pragma unroll RU
     for (int i = 0; i < M; ++i) xt[i] = x[i] + t * pk[i];
-    const double f = fg(xt, g);
+    const double f = fg(xt, g, live);
     dphi = dot(g, pk);
     return f;
   }
@@ -275,7 +338,7 @@ __device__ __forceinline__ double quadmin(double a, double fa, double fpa, doubl
 }
 
 #ifndef INSITE_REFINE_WPE4
-#define INSITE_REFINE_WPE4 4
+#define INSITE_REFINE_WPE4 3  // r04: 3 waves (<= 168 VGPRs, no spills) beat 4 with spills: kernel 2.21 vs 2.30 ms (flat BFGS)
 #endif
 #ifndef INSITE_REFINE_WPE8
 #define INSITE_REFINE_WPE8 1
@@ -308,22 +371,31 @@ struct HMat<M, true> {
 // M <= 4 with the affine RHS (the EQ_4 models: two terms per arm) is sized for INSITE_REFINE_WPE4 waves per
 // SIMD (<= 128 VGPRs; unconstrained the compiler takes 202 and runs 2 waves): the objective scan is a
 // dependent fp64 chain per lane, hidden only by other waves.
-template <int M, int NA, int D>
+template <int M, int NA, int D, bool WIN = false>
 __global__ void __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(M <= 4 && D == 1 ? INSITE_REFINE_WPE4 : (M <= 8 ? INSITE_REFINE_WPE8 : 1))))
 insite_refine_kernel(RefineArgs ra) {
-  constexpr int RU = RefineLane<M, NA, D>::RU;
+  constexpr int RU = RefineLane<M, NA, D, WIN>::RU;
   constexpr bool kHL = INSITE_REFINE_HLDS && RU == M && M <= 4;
   __shared__ double sH[(kHL ? M * M : 1) * kBlock];
+  __shared__ double sV[WIN ? kWavesPerBlock * 2 * kWin * kWave : 1];
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= ra.N) return;
+  // WIN: every lane of a wave stays (the ring loads are wave-cooperative); lanes past the last row are inert
+  const bool valid = gid < ra.N;
+  if (!WIN && !valid) return;
   // lane -> row: with rows binned by seq_len the lanes of a wave scan similar prefixes; every row's
   // computation is independent of its lane, so outputs are bitwise the same in any order
-  const int64_t p = ra.order ? (int64_t)ra.order[gid] : gid;
+  const int64_t gl = valid ? gid : ra.N - 1;
+  const int64_t p = ra.order ? (int64_t)ra.order[gl] : gl;
   double uu[INSITE_MAX_STATICS];
 #pragma unroll
   for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < ra.U ? ra.u[p * ra.U + t] : 0.0;
-  RefineLane<M, NA, D> ln{ra, p, 0, 1.0, {}, {}};
+  RefineLane<M, NA, D, WIN> ln{ra, p, 0, 1.0, {}, {}};
+  if constexpr (WIN) {
+    for (int k = 0; k < ra.T; ++k) ln.am |= (uint64_t)ln.armbit_mem(k) << k;
+    ln.win = sV + (threadIdx.x / kWave) * (2 * kWin * kWave);
+    ln.p0 = gid - (threadIdx.x & (kWave - 1));
+  }
 #pragma unroll RU
   for (int i = 0; i < M; ++i) {
     ln.mono[i] = i < ra.m ? monomial_code(ra.t_ucode[i], uu) : 0.0;
@@ -332,7 +404,7 @@ insite_refine_kernel(RefineArgs ra) {
   double x[M];
 #pragma unroll RU
   for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
-  const int sl = ra.sl[p];
+  const int sl = valid ? ra.sl[p] : 0;
   int status = -1, nit = 0;
 #if INSITE_REFINE_FLAT
   // ---------------- BFGS as a flat per-lane state machine: ONE objective scan per loop iteration ----------------
@@ -343,10 +415,11 @@ insite_refine_kernel(RefineArgs ra) {
   // advances that lane's state (jax line_search / _zoom / minimize_bfgs transitions, in their order), so a wave
   // costs max over its lanes of the evaluation count instead of the sum over the nesting.  Per lane the arithmetic
   // is the nested form's, operation for operation (A/B: INSITE_REFINE_FLAT=0).
-  if (sl > ra.tau && ra.T >= 2) {
-    ln.K = min(sl - ra.tau, ra.T - 1);
+  const bool refine = sl > ra.tau && ra.T >= 2;  // (WIN: every lane enters; the inert ones scan nothing)
+  if (WIN || refine) {
+    ln.K = refine ? min(sl - ra.tau, ra.T - 1) : 0;
     double g[M];
-    const double start = ln.fg(x, g);  // norm 1, penalty 0 at c0
+    const double start = ln.fg(x, g, refine);  // norm 1, penalty 0 at c0
     ln.norm = start * 2.5;
     // jax evaluates f_to_min at c0 twice (start_res with norm_const = 1, then minimize's first value_and_grad with
     // norm_const = 2.5 start_res, sindy.py:591-627).  At c0 the penalty and its gradient are exactly zero, so the
@@ -419,11 +492,13 @@ insite_refine_kernel(RefineArgs ra) {
       if (!use_cubic && !use_quad) a_j = (a_lo + a_hi) / 2.0;
       t_trial = a_j;
     };
-    bool pending = !converged && k < maxiter;
+    bool pending = refine && !converged && k < maxiter;
     if (pending) begin_ls();
-    while (pending) {
+    // WIN: the loop runs while ANY lane of the wave has a trial pending (its scans fill the shared ring)
+    while (WIN ? __builtin_amdgcn_ballot_w64(pending) != 0 : pending) {
       double dphi_t, g_t[M];
-      const double phi_t = ln.phi(x, pk, t_trial, dphi_t, g_t);
+      const double phi_t = ln.phi(x, pk, t_trial, dphi_t, g_t, pending);
+      if (WIN && !pending) continue;
       bool ls_end = false, ls_done = false;
       if (!in_zoom) {  // the line search's trial a_i
         const double a_i = t_trial;
@@ -576,11 +651,13 @@ insite_refine_kernel(RefineArgs ra) {
         if (pending) begin_ls();
       }
     }
-    nit = k;
-    status = converged ? 0 : (k == maxiter ? 1 : (failed ? 2 + ls_status : -1));
-    if (status == 3 && ra.revert3) {  // zoom failed: the reference code keeps the global coefficients (sindy.py:628-631)
+    if (refine) {
+      nit = k;
+      status = converged ? 0 : (k == maxiter ? 1 : (failed ? 2 + ls_status : -1));
+      if (status == 3 && ra.revert3) {  // zoom failed: the reference code keeps the global coefficients (sindy.py:628-631)
 #pragma unroll RU
-      for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
+        for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
+      }
     }
   }
 #else
@@ -802,6 +879,7 @@ insite_refine_kernel(RefineArgs ra) {
     }
   }
 #endif  // INSITE_REFINE_FLAT
+  if (WIN && !valid) return;  // inert lanes past the last row: the wave-cooperative part is over
   // ---------------- final Euler scan with the (refined) model, every coefficient (sindy.py:668) ----------------
   // coefficient q: the refined value if active, else the global one; resolved by comparison against the
   // active list (no dynamically indexed per-lane array, which would live in scratch)
@@ -855,6 +933,18 @@ insite_refine_kernel(RefineArgs ra) {
 template <int NA, int D>
 void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
   const int m = ra.m;
+  // the windowed M <= 4 kernels (INSITE_REFINE_WIN): the reference's sequences (T <= 64: one 64-bit arm mask per
+  // lane), identity lane order (the binned layout gathers rows instead), even ldv (16-B ring loads)
+  const bool win = INSITE_REFINE_WIN && INSITE_REFINE_FLAT && NA == 2 && ra.T <= 64 && ra.T >= 2 && !ra.order &&
+                   ra.ldv % 2 == 0 && ((uintptr_t)ra.V & 15u) == 0;
+  if constexpr (D == 1 && NA == 2) {
+    // (m = 4: the 16-entry H in LDS plus the ring would hold the CU to 2 blocks; the per-step-load kernel runs it)
+    if (win && m <= 3) {
+      if (m <= 2) insite_refine_kernel<2, NA, D, true><<<grid, kBlock, 0, hs>>>(ra);
+      else insite_refine_kernel<3, NA, D, true><<<grid, kBlock, 0, hs>>>(ra);
+      return;
+    }
+  }
   if constexpr (D == 1) {
     // the sparse models get a kernel sized to their active count (register budget: INSITE_REFINE_WPE4 waves)
     if (m <= 2) insite_refine_kernel<2, NA, D><<<grid, kBlock, 0, hs>>>(ra);

@@ -1032,7 +1032,8 @@ class InsiteRefinePlan:
         W = (N + 31) // 32
         U = lib.n_statics
         self.order = torch.empty((N,), dtype=torch.int32, device=dev)
-        self.Vt = torch.empty((T, N), dtype=torch.float64, device=dev)
+        ldt = N + (N & 1)   # even leading dimension (the windowed kernels' 16-B ring loads)
+        self.Vt = torch.empty((T, ldt), dtype=torch.float64, device=dev)[:, :N]
         self.arms = torch.empty((T, W) if bits else (T, N), dtype=torch.int32 if bits else torch.int8, device=dev)
         self.u_l = torch.empty_like(u) if U else None
         self.sl_l = torch.empty_like(seq_len)
@@ -1049,7 +1050,7 @@ class InsiteRefinePlan:
         self.device = dev
         self._calls = [
             (L.insite_rk45_order_i32, (_p(seq_len), N, int(T), _p(self.order), _p(self._ows), self._ows.numel())),
-            (L.insite_refine_prepare_f64, (_p(V), V.stride(0), _p(arm), arm.stride(0), N, T, _p(self.Vt), N,
+            (L.insite_refine_prepare_f64, (_p(V), V.stride(0), _p(arm), arm.stride(0), N, T, _p(self.Vt), ldt,
                                            _p(self.arms) if bits else nul, W, nul if bits else _p(self.arms), N,
                                            _p(self.order), _p(u) if U else nul, U, _p(self.u_l) if U else nul,
                                            _p(seq_len), _p(self.sl_l))),
@@ -1059,12 +1060,12 @@ class InsiteRefinePlan:
         ustat = _p(self.u_l) if U else nul
         if lib.n_inputs:
             self._calls.append((L.insite_refine_general_f64, (
-                _p(self.Vt), N, T, _p(self.arms) if bits else nul, nul if bits else _p(self.arms), self.arms.stride(0),
+                _p(self.Vt), ldt, T, _p(self.arms) if bits else nul, nul if bits else _p(self.arms), self.arms.stride(0),
                 ustat, _p(self.sl_l), N, U, c0.size, c0.ctypes.data_as(ctypes.c_void_p),
                 mask.ctypes.data_as(ctypes.c_void_p), qexps.ctypes.data_as(ctypes.c_void_p), A) + common + (nul, nul)))
         else:
             fn = L.insite_refine_f64 if bits else L.insite_refine_arms_f64
-            self._calls.append((fn, (_p(self.Vt), N, T, _p(self.arms), self.arms.stride(0), ustat, _p(self.sl_l), N, U,
+            self._calls.append((fn, (_p(self.Vt), ldt, T, _p(self.arms), self.arms.stride(0), ustat, _p(self.sl_l), N, U,
                                      self._tab.ctypes.data_as(ctypes.c_void_p), lib.n_terms,
                                      c0.ctypes.data_as(ctypes.c_void_p), A) + common + (nul,)))
         P_, co, so, io = self.out
@@ -1113,7 +1114,8 @@ def refine_prepare(V: torch.Tensor, arm: torch.Tensor, bits: bool = True, order:
         if seq_len.numel() != N:
             raise ValueError("seq_len must have one entry per row")
         sl_l = torch.empty_like(seq_len)
-    Vt = torch.empty((T, N), dtype=torch.float64, device=V.device)
+    ldt = N + (N & 1)   # an even leading dimension: the windowed kernels' 16-B ring loads (insite_refine.hip)
+    Vt = torch.empty((T, ldt), dtype=torch.float64, device=V.device)[:, :N]
     W = (N + 31) // 32
     at = torch.empty((T, W) if bits else (T, N), dtype=torch.int32 if bits else torch.int8, device=V.device)
     nul = ctypes.c_void_p(0)
@@ -1121,7 +1123,7 @@ def refine_prepare(V: torch.Tensor, arm: torch.Tensor, bits: bool = True, order:
         _dev("order", order, torch.int32, 1)
         if order.numel() != N:
             raise ValueError("order must be an [N] permutation")
-    st = _lib.load().insite_refine_prepare_f64(_p(V), V.stride(0), _p(arm), arm.stride(0), N, T, _p(Vt), N,
+    st = _lib.load().insite_refine_prepare_f64(_p(V), V.stride(0), _p(arm), arm.stride(0), N, T, _p(Vt), ldt,
                                                _p(at) if bits else nul, W, nul if bits else _p(at), N, _p(order),
                                                _p(u), u.size(1) if u is not None else 0, _p(u_l), _p(seq_len), _p(sl_l),
                                                _stream(V.device))

@@ -331,3 +331,33 @@ def test_insite_refine_plan_equals_eager(dev):
         torch.cuda.synchronize()
         for a, b in zip(got, want):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N,T", [(5_000, 60), (4_097, 33), (130, 64), (777, 7)])
+def test_windowed_refine_equals_per_step_loads(dev, N, T):
+    """The windowed M <= 4 kernels (LDS ring of observation slots filled by LDS-DMA, arm masks in registers,
+    wave-uniform flat BFGS loop; identity lane order) against the per-step-load kernels (selected here by passing an
+    explicit identity row order): predictions, coefficients, statuses, iteration and evaluation counts bitwise equal,
+    incl. a partial last wave (inert lanes), odd N (padded even leading dimension) and short T."""
+    from insite_amd import cohort, ops
+    coh = cohort.synthetic_pkpd(N, T, seed=N + T, device=dev, equation="EQ_4_C")
+    V = coh.x[:, :T].contiguous()
+    g = torch.Generator(device=dev)
+    g.manual_seed(N * 3 + T)
+    flip = torch.randint(1, max(2, T), (N, 1), generator=g, device=dev)
+    arm = torch.where(torch.arange(T, device=dev)[None, :] >= flip, 1 - coh.arm[:, None].to(torch.int64),
+                      coh.arm[:, None].to(torch.int64)).to(torch.int8).contiguous()
+    sl = torch.randint(1, T + 1, (N,), generator=g, device=dev, dtype=torch.int32)
+    c0 = np.zeros((2, coh.lib.n_terms))
+    c0[0, 4], c0[1, 1], c0[1, 5] = -1.1107592869834308, -0.14540553723951796, -1.0234639833519243
+    Vt, bits = ops.refine_prepare(V, arm, bits=True)
+    assert Vt.stride(0) % 2 == 0
+    ident = torch.arange(N, device=dev, dtype=torch.int32)
+    nf_w = torch.empty((N,), dtype=torch.int32, device=dev)
+    nf_l = torch.empty((N,), dtype=torch.int32, device=dev)
+    w = ops.insite_refine_tm(Vt, bits, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5, nfev=nf_w)
+    l_ = ops.insite_refine_tm(Vt, bits, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5, order=ident, nfev=nf_l)
+    torch.cuda.synchronize()
+    for a, b in zip(w, l_):
+        assert torch.equal(a, b)
+    assert torch.equal(nf_w, nf_l)
