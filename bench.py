@@ -280,16 +280,85 @@ def cpu_baseline(n_sample, T, method, seed, ivp_per_worker=100):
                           f"{el_ivp * n_sample / n_ivp:.1f} s"}}
 
 
+def _cpu_c3_gen(job):
+    from oracle import multistate_ref as M
+    lo, hi, T, seed = job
+    x, a = M.c3_cohort(hi - lo, T, seed=seed)
+    a_cf = M.treatment_markov(hi - lo, T, np.random.default_rng(seed + 17))
+    return x, a, a_cf
+
+
+def _cpu_c3_gram_chunk(bounds):
+    from oracle import multistate_ref as M
+    lo, hi = bounds
+    d = _CPU
+    return M.ms_gram_vectorized(d["x"][lo:hi], d["a"][lo:hi], M.DT_C3, d["exps"])
+
+
+def _cpu_c3_rollout_chunk(bounds):
+    from oracle import multistate_ref as M
+    lo, hi = bounds
+    d = _CPU
+    y = M.ms_rollout(d["x"][lo:hi, 0].astype(np.float64), d["a_cf"][lo:hi], d["coef"], d["exps"], M.DT_C3, "rk4")
+    return float(y[:, -1].sum())
+
+
+def c3_cpu_baseline(per_worker, T, seed):
+    """Bounded CPU sample of the C3 workload (oracle/multistate_ref.py, numpy fp64) on the host's workers:
+    discovery (vectorised S-state Gram per chunk, partials summed, one STLSQ per state) + RK4 rollout under
+    a fresh Markov treatment sequence — the same step the GPU line times.  The cohort is generated by the
+    same pool before the clock starts."""
+    import multiprocessing as mp
+    sys.path.insert(0, ROOT)
+    from oracle import multistate_ref as M
+    info = host_info()
+    W = info["workers"]
+    n = per_worker * W
+    ctx = mp.get_context("fork")
+    with ctx.Pool(W, initializer=_cpu_worker_init) as pool:
+        parts = pool.map(_cpu_c3_gen, [(w * per_worker, (w + 1) * per_worker, T, seed + 101 * w) for w in range(W)])
+    _CPU.update(x=np.concatenate([p[0] for p in parts]), a=np.concatenate([p[1] for p in parts]),
+                a_cf=np.concatenate([p[2] for p in parts]), exps=M.c3_library())
+    del parts
+    chunks = [(w * per_worker, (w + 1) * per_worker) for w in range(W)]
+    with ctx.Pool(W, initializer=_cpu_worker_init) as pool:
+        pool.map(abs, range(W))
+        t0 = time.perf_counter()
+        gb = pool.map(_cpu_c3_gram_chunk, chunks)
+        G = sum(q[0] for q in gb)
+        B = sum(q[1] for q in gb)
+        _CPU["coef"] = M.ms_stlsq(G, B)[0]
+        el_disc = time.perf_counter() - t0
+    with ctx.Pool(W, initializer=_cpu_worker_init) as pool:   # forked after the fit: workers see the model
+        pool.map(abs, range(W))
+        t1 = time.perf_counter()
+        pool.map(_cpu_c3_rollout_chunk, chunks)
+        el_roll = time.perf_counter() - t1
+    truth = M.c3_truth_coef(_CPU["exps"])
+    support_ok = bool(np.array_equal(np.abs(_CPU["coef"]) > 0, truth != 0))
+    for k in ("x", "a", "a_cf", "coef"):
+        _CPU.pop(k, None)
+    return {"value": n / (el_disc + el_roll), "unit": "patient-trajectories/s", "cores": W, "kind": "port",
+            "sample": f"oracle/multistate_ref.py numpy fp64 over a {W}-process pool: {n} C3 patients x {T} steps, "
+                      f"discovery (chunked S-state Gram + STLSQ per state) {el_disc:.2f} s + RK4 rollout "
+                      f"{el_roll:.2f} s; support equals truth: {support_ok}",
+            "host": info}
+
+
 def c3_main(args):
     """Configuration C3 (BASELINE.json configs[2]): 5-state coupled ODE + binary per-step treatment,
     1M patients x 500 steps, fp32 storage, fp64 Gram on MFMA.  One step = discovery (gram_ms on f64
     MFMA + fixed-order finalize + one wave-STLSQ per state) + RK4 counterfactual rollout of every
     patient under a fresh treatment sequence.  Single GPU (patients would shard like C2)."""
+    N = args.patients if args.patients != 100_000 else 1_000_000
+    T = args.T if args.T != 200 else 500
+    cpu = None
+    if os.environ.get("WORLD_SIZE", "1") == "1" and not args.no_cpu_baseline:
+        # 2000 patients per worker (~0.8 s of discovery + rollout each; the cohort build is untimed)
+        cpu = c3_cpu_baseline(max(64, min(2000, args.cpu_sample // 50)), T, args.seed + 3)
     from insite_amd import multistate as MS
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    N = args.patients if args.patients != 100_000 else 1_000_000
-    T = args.T if args.T != 200 else 500
     coh = MS.synthetic_c3(N, T, seed=args.seed, device=dev)
     g = torch.Generator(device=dev)
     g.manual_seed(args.seed + 17)
@@ -371,6 +440,8 @@ def c3_main(args):
                     "frac": roll_bytes / (roll_ms_t * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                     "dense_kernel_avg_launch_ms": roll_dense_t},
     }
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     emit(out)
 
 
@@ -391,7 +462,29 @@ def _cpu_rk45_chunk(bounds):
     return hi - lo
 
 
-def c5_cpu_baseline(n_sample, seed):
+def _cpu_rk45_ivp_chunk(bounds):
+    """scipy.integrate.solve_ivp(RK45, rtol = atol = 1.4e-8) over every observation interval of each patient
+    with the interval's arm held (the call the restatement in oracle/rk45_ref.py is pinned to)."""
+    from scipy.integrate import solve_ivp
+    from oracle import rk45_ref as K
+    lo, hi = bounds
+    d = _CPU
+    acc = 0.0
+    for p in range(lo, hi):
+        al, be = K.patient_rates(d["u"][p], d["coef"], d["exps"])
+        y = float(d["y0"][p])
+        for k in range(int(d["n"][p]) - 1):
+            a = int(d["arm"][p, k])
+            t0, t1 = float(d["t"][p, k]), float(d["t"][p, k + 1])
+            if t1 > t0:
+                sol = solve_ivp(lambda t, v, a=a: al[a] + be[a] * v, (t0, t1), [y], method="RK45",
+                                rtol=K.RTOL, atol=K.ATOL)
+                y = float(sol.y[0, -1])
+        acc += y
+    return acc
+
+
+def c5_cpu_baseline(n_sample, seed, ivp_per_worker=40):
     """oracle/rk45_ref.py (scipy 1.15 RK45 restated, pinned to solve_ivp at 1e-13) on a process pool over
     a bounded sample of the C5 workload, before any GPU context exists."""
     import multiprocessing as mp
@@ -407,14 +500,25 @@ def c5_cpu_baseline(n_sample, seed):
     _CPU.update(t=t, n=n, y0=rng.uniform(1, 50, n_sample), u=rng.normal(0.5, 0.05, (n_sample, 2)),
                 arm=rng.integers(0, 2, (n_sample, t.shape[1])), coef=coef, exps=R.poly_library(3, 2, True))
     chunks = [(int(c[0]), int(c[-1]) + 1) for c in np.array_split(np.arange(n_sample), W) if c.size]
+    n_ivp = min(n_sample, ivp_per_worker * W)
+    ivp_chunks = [(int(c[0]), int(c[-1]) + 1) for c in np.array_split(np.arange(n_ivp), W) if c.size]
     with mp.get_context("fork").Pool(W, initializer=_cpu_worker_init) as pool:
         pool.map(abs, range(W))
         t0 = time.perf_counter()
         pool.map(_cpu_rk45_chunk, chunks)
         el = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        pool.map(_cpu_rk45_ivp_chunk, ivp_chunks)
+        el_ivp = time.perf_counter() - t1
     return {"value": n_sample / el, "unit": "patient-trajectories/s", "cores": W, "kind": "port",
             "sample": f"oracle/rk45_ref.py (scipy RK45 restated) on {n_sample} irregular-grid patients over {W} "
-                      f"worker processes, {el:.2f} s", "host": info}
+                      f"worker processes, {el:.2f} s", "host": info,
+            "scipy_solve_ivp": {
+                "value": n_ivp / el_ivp, "unit": "patient-trajectories/s", "cores": W,
+                "kind": "scipy.integrate.solve_ivp(method='RK45', rtol=atol=1.4e-8) per observation interval",
+                "sample": f"{n_ivp} irregular-grid patients on {W} workers in {el_ivp:.2f} s (one solve_ivp call per "
+                          f"interval, arm held over it, as the reference integrates per interval); the rate "
+                          f"extrapolates linearly in patients"}}
 
 
 def c5_main(args):
