@@ -700,39 +700,43 @@ def insite_main(args):
     c0[0, 4], c0[1, 1], c0[1, 5] = -1.1107592869834308, -0.14540553723951796, -1.0234639833519243  # log :182
     dt = 10.0 / T
 
-    # the product's binned path as a prepared plan: the seq_len sort, the gather pass, the kernel and the scatter
-    # pass (4 C calls, no host synchronisation) inside every step
+    # the product's binned path as a prepared plan: the seq_len sort and the refinement on the patient-major rows
+    # (insite_refine_rows_f64, ABI 9: 2 C calls, no host synchronisation) inside every step
     plan = ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5)
+    plan_prep = ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, rows=False)   # ABI 8 route
 
-    def run(binned=False):   # binned=True: rows binned by seq_len on the device (inside every step)
-        return plan() if binned else ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, binned=False)
+    def run(mode):   # "binned": rows binned by seq_len on the device (inside every step)
+        if mode == "binned":
+            return plan()
+        if mode == "prepare":
+            return plan_prep()
+        return ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, binned=False)
 
-    def timed(binned):
+    def timed(mode):
         for _ in range(args.warmup):
-            run(binned)
+            run(mode)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            r = run(binned)
+            r = run(mode)
         torch.cuda.synchronize(dev)
         return (time.perf_counter() - t0) / args.steps * 1e3, r
 
-    ms_identity, _ = timed(False)
-    ms_step, (preds, coef, status, iters) = timed(True)    # the product default: rows binned by seq_len
+    ms_identity, _ = timed("identity")
+    ms_prepare, prep_out = timed("prepare")
+    ms_step, (preds, coef, status, iters) = timed("binned")    # the product default: rows binned by seq_len
     eager = ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, binned=True)
     plan_eq = all(bool(torch.equal(a, b)) for a, b in zip(eager, (preds, coef, status, iters)))
+    prep_eq = all(bool(torch.equal(a, b)) for a, b in zip(prep_out, (preds, coef, status, iters)))
     st = status.cpu().numpy()
     it = iters.cpu().numpy()
-    # roofline: the refinement kernel alone on the step's binned time-major inputs (the layout pass excluded), HIP
-    # events on its stream; its work = every objective/gradient evaluation (nfev per row, counted by the kernel on
-    # one untimed launch through insite_refine_general_f64) x the row's K-step window x flops per sensitivity step
-    order = ops.rk45_order(sl, T)
-    idx = order.long()
-    Vt, bits, u_l, sl_l = ops.refine_prepare(V, arm, bits=True, order=order, u=coh.u, seq_len=sl)
+    # roofline: the refinement kernel alone (the plan's second call, its lane order computed by the steps above),
+    # HIP events on its stream; its work = every objective/gradient evaluation (nfev per row, counted by the kernel
+    # on one untimed launch) x the row's K-step window x flops per sensitivity step
     kst = torch.cuda.current_stream(dev)
 
     def kern():
-        return ops.insite_refine_tm(Vt, bits, u_l, sl_l, c0, coh.lib, dt, 10.0, 5)
+        plan.call(1, kst)
 
     for _ in range(2):
         kern()
@@ -743,11 +747,14 @@ def insite_main(args):
     e1.record(kst)
     torch.cuda.synchronize(dev)
     kern_ms = e0.elapsed_time(e1) / args.steps
-    nf = torch.empty((N,), dtype=torch.int32, device=dev)
-    p2, _, s2, i2 = ops.insite_refine_tm(Vt, bits, u_l, sl_l, c0, coh.lib, dt, 10.0, 5, nfev=nf)
+    nf_row = torch.empty((N,), dtype=torch.int32, device=dev)
+    plan_nf = ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, nfev=nf_row)
+    p2, _, s2, i2 = plan_nf()
+    order = plan_nf.order.long()           # lane -> row: the waves as the kernel formed them
     torch.cuda.synchronize(dev)
-    same = bool(torch.equal(s2, status[idx]) and torch.equal(i2, iters[idx]) and torch.equal(p2.t(), preds[idx]))
-    K = torch.clamp(sl_l.to(torch.int64) - 5, min=0, max=T - 1)
+    same = bool(torch.equal(s2, status) and torch.equal(i2, iters) and torch.equal(p2, preds))
+    nf = nf_row[order]
+    K = torch.clamp(sl[order].to(torch.int64) - 5, min=0, max=T - 1)
     # SIMT divergence of the refinement: a wave runs until its slowest lane's last scan, each scan as long as its
     # longest lane's window -- wave cost ~ max(nfev) x max(K) over its 64 lanes against the rows' own nfev x K
     nfk = nf.to(torch.int64).cpu().numpy()
@@ -766,7 +773,9 @@ def insite_main(args):
     refine_flop = float((nf.to(torch.int64) * K).sum().item()) * per_step
     final_flop = float(N) * T * SUB * 4            # the refined model's final Euler scan over the whole row
     flop = refine_flop + final_flop
-    kbytes = N * T * (8 + 8) + T * ((N + 31) // 32) * 4 + N * (8 * 2 + 4) + N * (2 * coh.lib.n_terms * 8 + 8)
+    # V read + int8 arms read + predictions written, statics + seq_len + lane order read, coefficients + status +
+    # iterations written
+    kbytes = N * T * (8 + 1 + 8) + N * (8 * 2 + 4 + 4) + N * (2 * coh.lib.n_terms * 8 + 8)
     out = {
         "metric": METRIC, "value": N / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
@@ -776,16 +785,19 @@ def insite_main(args):
                                f"{N // 1000}k rows", "rows": N, "T": T},
         "insite": {"refined_rows": int((st >= 0).sum()), "converged": int((st == 0).sum()),
                    "zoom_failed_fallback": int((st == 3).sum()), "mean_bfgs_iterations": float(it[st >= 0].mean()),
-                   "lane_order": "rows binned by seq_len (device counting sort), gathered into lane order and "
-                                 "scattered back by insite_refine_prepare_f64 / insite_refine_finish_f64 "
-                                 "(ops.plan_insite_refine: 4 C calls per step, no host sync)",
+                   "lane_order": "rows binned by seq_len (device counting sort); the kernel gathers its lanes' "
+                                 "patient-major rows through its LDS ring and stores the predictions as row "
+                                 "segments (insite_refine_rows_f64; ops.plan_insite_refine: 2 C calls per step, "
+                                 "no host sync)",
                    "plan_equals_eager": plan_eq,
                    "identity_lane_order_ms_per_step": ms_identity,
                    "reference_wall_time_s": "88.96 s per INSITE EQ_4_A run incl. 59,000 + 11,800 refinements "
                                             "(results/2_main_table/final_with_insite.txt:2346; SURVEY.md §6)",
-                   "mean_evaluations_per_refined_row": float(nf.to(torch.float64)[s2 >= 0].mean().item()),
-                   "evaluation_count_route_matches": same, "divergence": divergence},
-        "roofline": {"kernel": "insite_refine_kernel<4, 2, 1> (per-row BFGS + final Euler-5 scan)", "bound": "valu-f64",
+                   "mean_evaluations_per_refined_row": float(nf_row.to(torch.float64)[s2 >= 0].mean().item()),
+                   "evaluation_count_route_matches": same, "divergence": divergence,
+                   "prepare_route_ms_per_step": ms_prepare, "prepare_route_equal": prep_eq},
+        "roofline": {"kernel": "insite_refine_kernel<3, 2, 1, WIN, PM> (per-row BFGS + final Euler-5 scan on the "
+                               "patient-major rows)", "bound": "valu-f64",
                      "unit": "TFLOP/s", "achieved": flop / (kern_ms * 1e-3) / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
                      "frac": flop / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
                      "traffic": traffic_for("insite", "insite_refine_kernel", args=args), "avg_launch_ms": kern_ms,
@@ -795,7 +807,7 @@ def insite_main(args):
                                     "the final scan; nfev from the kernel's own count (insite_refine_general_f64)",
                      "algorithmic_bytes": kbytes, "achieved_GBps": kbytes / (kern_ms * 1e-3) / 1e9,
                      "avg_ms_source": "HIP events on the launch stream around args.steps back-to-back launches of "
-                                      "the time-major entry on the step's binned inputs (layout passes excluded)"},
+                                      "insite_refine_rows_f64 with the step's lane order (the sort excluded)"},
     }
     if cpu is not None:
         out["cpu_baseline"] = cpu

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define INSITE_ABI_VERSION 8
+#define INSITE_ABI_VERSION 9
 
 /* status codes */
 #define INSITE_OK 0
@@ -460,6 +460,26 @@ int32_t insite_refine_general_f64(const double* V, int64_t ld_v, int32_t T, cons
                                   double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail,
                                   double* preds, int64_t ld_p, double* coef_out, int32_t* status_out,
                                   int32_t* iters_out, int32_t* nfev_out, const int32_t* row_order, void* stream);
+
+/* The refinement on the reference's OWN row layout (ABI 9): _get_fine_tuned_predictions hands over the patient-major
+ * prev_outputs [N, T], per-step treatments, statics and sequence lengths (sindy.py:555-566) and takes back the
+ * patient-major predictions (sindy.py:658-665).  insite_refine_general_f64 semantics (model description, objective,
+ * BFGS, status, outputs bitwise equal), without the prepare / finish passes: the windowed kernel gathers the rows of
+ * its lanes (row_order: lane l refines row row_order[l], NULL = identity) straight from V through its LDS ring and
+ * stores the predictions through the same ring as 64-B row segments.
+ *   V [n_rows, ld_v] f64, ld_v even and V 16-B aligned; arm [n_rows, ld_arm] int8 with values 0 / 1 (n_arms <= 2);
+ *   u [n_rows, n_statics], seq_len [n_rows]; preds [n_rows, ld_p], coef_out [n_rows, n_coef], status_out / iters_out
+ *   / nfev_out [n_rows] -- every per-row array in ROW order.  ld_v, ld_arm, ld_p >= T.
+ * Returns INSITE_E_UNSUPPORTED outside the windowed kernel's shape (T not in [2, 64], more than 3 active
+ * coefficients, a state exponent >= 2 in the model, odd ld_v / unaligned V): the caller then takes the
+ * prepare / insite_refine_general_f64 / finish route, which covers every model. */
+int32_t insite_refine_rows_f64(const double* V, int64_t ld_v, int32_t T, const int8_t* arm, int64_t ld_arm,
+                               const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
+                               int32_t n_coef, const double* coef0, const int32_t* coef_arm_mask,
+                               const int8_t* coef_exps, int32_t n_arms, double dt, double lam, int32_t tau,
+                               int32_t substeps, int32_t revert_on_zoom_fail, double* preds, int64_t ld_p,
+                               double* coef_out, int32_t* status_out, int32_t* iters_out, int32_t* nfev_out,
+                               const int32_t* row_order, void* stream);
 
 /* General one-state discovery (insite_gen.hip): libraries with state exponents up to 4 and/or per-step
  * binary treatment INPUTS — the reference's degree-4 ablation (PolynomialLibrary(degree=4,

@@ -57,6 +57,10 @@ struct RefineArgs {
   int64_t ldv, lda, ldp, N;
   int32_t T, tau, sub, U, A, m, n_coef;
   int32_t revert3;      // 1: BFGS status 3 reverts to the global model (sindy.py:628-631); 0: keep the iterate
+  int32_t pm;           // 1: the row layout below (WIN kernels only)
+  // row layout (insite_refine_rows_f64): V [N, ldv], arm8 [N, lda] and preds [N, ldp] patient-major, every per-row
+  // array indexed by the row order[lane] selects; st16 = 16-B prediction stores (preds 16-B aligned, ldp even)
+  int32_t st16;
   double dt, lam;
   // active coefficients i < m: flat index, arm mask, state exponent, static-monomial code
   int32_t t_flat[kRefineMaxCoef], t_mask[kRefineMaxCoef], t_ex[kRefineMaxCoef], t_ucode[kRefineMaxCoef];
@@ -109,7 +113,17 @@ constexpr int kWin = 8;
 #define INSITE_REFINE_WIN 1
 #endif
 
-template <int M, int NA, int D, bool WIN = false>
+// Row layout (PM, insite_refine_rows_f64): the same ring over the reference's patient-major V gathered through the
+// lane order.  A slot holds COLUMNS [8c, 8c + 8) of the wave's 64 rows (the target of step k is column k + 1); one
+// LDS-DMA instruction moves 16 rows x 64 B (4 lanes x 16 B per row), and lane 4m + j of instruction q writes the
+// 16-B piece ((j + m / 4) & 3) of row 16 q + m: the swizzle spreads a step's 64 reads (row r reads its own column)
+// over all 64 banks, 2 passes per ds_read_b64 as in the time-major ring.
+__device__ __forceinline__ int pm_slot_index(int r, int col) {
+  const int s = col & (kWin - 1), m = r & 15;
+  return ((col >> 3) & 1) * (kWin * kWave) + (r >> 4) * 128 + m * 8 + ((((s >> 1) - (m >> 2)) & 3) << 1) + (s & 1);
+}
+
+template <int M, int NA, int D, bool WIN = false, bool PM = false>
 struct RefineLane {
   static constexpr int RU = M <= kRefineRegActive ? M : 1;
   // sub-step loop unrolled by odeint's 5 (the default): measured 12 active 62 -> 43 ms, 6 active 5.5 -> 5.2 ms;
@@ -127,7 +141,8 @@ struct RefineLane {
   double* win = nullptr;   // WIN: this wave's ring, 2 slots x kWin steps x 64 rows (step j of a slot at j * 64)
   int64_t p0 = 0;          // WIN: the wave's first column
   __device__ int armbit_mem(int k) const {
-    if constexpr (NA == 2) return (int)((ra.arm[(int64_t)k * ra.lda + (p >> 5)] >> (p & 31)) & 1u);
+    if constexpr (PM) return ra.arm8[p * ra.lda + k] != 0 ? 1 : 0;
+    else if constexpr (NA == 2) return (int)((ra.arm[(int64_t)k * ra.lda + (p >> 5)] >> (p & 31)) & 1u);
     else return (int)ra.arm8[(int64_t)k * ra.lda + p];
   }
   __device__ int armbit(int k) const {
@@ -139,6 +154,24 @@ struct RefineLane {
   // wave must execute it (the destination is the wave-uniform slot base + lane x 16 B).
   __device__ void fill(int c, int slot) const {
     const int lane = threadIdx.x & (kWave - 1);
+    if constexpr (PM) {
+      const int m = lane >> 2, pk = ((lane & 3) + (m >> 2)) & 3;
+      int col = c * kWin + 2 * pk;
+      if (col + 2 > ra.ldv) col = 0;  // past the row's end: any in-row pair (never read: targets stop at T - 1)
+      const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(win + slot * (kWin * kWave)));
+      const int prow = (int)p;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = __shfl(prow, 16 * q + m);
+        const double* src = ra.V + (int64_t)row * ra.ldv + col;
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(src), "s"(base + q * 1024u)
+                     : "memory");
+      }
+      return;
+    }
     int64_t col = p0 + 2 * (lane & 31);
     if (col + 1 >= ra.ldv) col = ra.ldv - 2;  // past the last column: any in-bounds pair (ldv even, never read)
     const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(win + slot * (kWin * kWave)));
@@ -186,7 +219,7 @@ struct RefineLane {
       }
     }
     const double h = ra.dt / (double)ra.sub;
-    double y = ra.V[p];
+    double y = PM ? ra.V[p * ra.ldv] : ra.V[p];
     double d[NA][D + 1], gG[NA][D + 1];
 #pragma unroll
     for (int a = 0; a < NA; ++a)
@@ -199,18 +232,28 @@ struct RefineLane {
     if constexpr (WIN) {
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) Kw = max(Kw, __shfl_xor(Kw, off));
-      nch = (Kw + kWin - 1) / kWin;
+      nch = PM ? (Kw > 0 ? Kw / kWin + 1 : 0) : (Kw + kWin - 1) / kWin;  // PM: column chunks 0 .. Kw / kWin
       if (nch > 0) fill(0, 0);
     }
     // (non-WIN) step k's arm and target are requested one step ahead (issued before step k - 1's sub-steps) so the
     // dependent Euler chain does not wait on a load per step
     int ak_nx = WIN ? 0 : armbit(0);
     double v_nx = WIN ? 0.0 : ra.V[ra.ldv + p];
-    const int kend = WIN ? nch * kWin : Kl;
+    const int kend = WIN ? (PM ? Kw : nch * kWin) : Kl;
     for (int k = 0; k < kend; ++k) {
       int ak;
       double vk1;
-      if constexpr (WIN) {
+      if constexpr (WIN && PM) {
+        const int col = k + 1;
+        if (k == 0 || (col & (kWin - 1)) == 0) {  // column chunk col / kWin landed; start the next one
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          const int nx = col / kWin + 1;
+          if (nx < nch) fill(nx, nx & 1);
+        }
+        if (k >= Kl) continue;
+        ak = armbit(k);
+        vk1 = win[pm_slot_index(threadIdx.x & (kWave - 1), col)];
+      } else if constexpr (WIN) {
         if ((k & (kWin - 1)) == 0) {  // slot k / kWin landed; start the next one into the other slot
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if (k / kWin + 1 < nch) fill(k / kWin + 1, (k / kWin + 1) & 1);
@@ -371,11 +414,11 @@ struct HMat<M, true> {
 // M <= 4 with the affine RHS (the EQ_4 models: two terms per arm) is sized for INSITE_REFINE_WPE4 waves per
 // SIMD (<= 128 VGPRs; unconstrained the compiler takes 202 and runs 2 waves): the objective scan is a
 // dependent fp64 chain per lane, hidden only by other waves.
-template <int M, int NA, int D, bool WIN = false>
+template <int M, int NA, int D, bool WIN = false, bool PM = false>
 __global__ void __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(M <= 4 && D == 1 ? INSITE_REFINE_WPE4 : (M <= 8 ? INSITE_REFINE_WPE8 : 1))))
 insite_refine_kernel(RefineArgs ra) {
-  constexpr int RU = RefineLane<M, NA, D, WIN>::RU;
+  constexpr int RU = RefineLane<M, NA, D, WIN, PM>::RU;
   constexpr bool kHL = INSITE_REFINE_HLDS && RU == M && M <= 4;
   __shared__ double sH[(kHL ? M * M : 1) * kBlock];
   __shared__ double sV[WIN ? kWavesPerBlock * 2 * kWin * kWave : 1];
@@ -390,7 +433,7 @@ insite_refine_kernel(RefineArgs ra) {
   double uu[INSITE_MAX_STATICS];
 #pragma unroll
   for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < ra.U ? ra.u[p * ra.U + t] : 0.0;
-  RefineLane<M, NA, D, WIN> ln{ra, p, 0, 1.0, {}, {}};
+  RefineLane<M, NA, D, WIN, PM> ln{ra, p, 0, 1.0, {}, {}};
   if constexpr (WIN) {
     for (int k = 0; k < ra.T; ++k) ln.am |= (uint64_t)ln.armbit_mem(k) << k;
     ln.win = sV + (threadIdx.x / kWave) * (2 * kWin * kWave);
@@ -879,7 +922,8 @@ insite_refine_kernel(RefineArgs ra) {
     }
   }
 #endif  // INSITE_REFINE_FLAT
-  if (WIN && !valid) return;  // inert lanes past the last row: the wave-cooperative part is over
+  if (WIN && !PM && !valid) return;  // inert lanes past the last row: the wave-cooperative part is over
+  // (PM: they stay -- the predictions leave through the wave's staging slot, every lane storing 4 rows' pieces)
   // ---------------- final Euler scan with the (refined) model, every coefficient (sindy.py:668) ----------------
   // coefficient q: the refined value if active, else the global one; resolved by comparison against the
   // active list (no dynamically indexed per-lane array, which would live in scratch)
@@ -906,7 +950,7 @@ insite_refine_kernel(RefineArgs ra) {
           if (ex == e) gam[a][e] += t;
   }
   const double h = ra.dt / (double)ra.sub;
-  double y = ra.V[p];
+  double y = PM ? ra.V[p * ra.ldv] : ra.V[p];
   for (int k = 0; k < ra.T; ++k) {
     const int ak = ln.armbit(k);
     double gk[D + 1];
@@ -921,8 +965,39 @@ insite_refine_kernel(RefineArgs ra) {
       if constexpr (D == 1) y = y + h * (gk[0] + gk[1] * y);
       else y = y + h * poly<D>(gk, y);
     }
-    ra.preds[(int64_t)k * ra.ldp + p] = y;
+    if constexpr (PM) {
+      // stage step k in slot 0 (the ring is idle now) at the column-k position of this lane's row; after 8 steps
+      // (or the last) every lane stores 16 B (two steps) of 4 rows: 64-B row segments, the whole 128-B lines of a
+      // row written by consecutive flushes of the same wave
+      const int lane = threadIdx.x & (kWave - 1);
+      ln.win[pm_slot_index(lane, k & (kWin - 1))] = y;
+      if ((k & (kWin - 1)) == kWin - 1 || k == ra.T - 1) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int m = lane >> 2, pk = ((lane & 3) + (m >> 2)) & 3;
+        const int col = (k & ~(kWin - 1)) + 2 * pk;
+        const int prow = (int)p;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 16 * q + m;
+          const int row = __shfl(prow, r);
+          const double2 v = *reinterpret_cast<const double2*>(ln.win + q * 128 + m * 8 + (lane & 3) * 2);
+          if (ln.p0 + r < ra.N && col < ra.T) {
+            double* dst = ra.preds + (int64_t)row * ra.ldp + col;
+            if (col + 1 < ra.T && ra.st16) {
+              *reinterpret_cast<double2*>(dst) = v;
+            } else {
+              dst[0] = v.x;
+              if (col + 1 < ra.T) dst[1] = v.y;
+            }
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    } else {
+      ra.preds[(int64_t)k * ra.ldp + p] = y;
+    }
   }
+  if (PM && !valid) return;
   if (ra.coef_out)
     for (int q = 0; q < ra.n_coef; ++q) ra.coef_out[p * ra.n_coef + q] = coef_at(q);
   if (ra.status) ra.status[p] = status;
@@ -938,6 +1013,11 @@ void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
   const bool win = INSITE_REFINE_WIN && INSITE_REFINE_FLAT && NA == 2 && ra.T <= 64 && ra.T >= 2 && !ra.order &&
                    ra.ldv % 2 == 0 && ((uintptr_t)ra.V & 15u) == 0;
   if constexpr (D == 1 && NA == 2) {
+    if (ra.pm) {  // insite_refine_rows_f64 checked m <= 3, T <= 64, the 16-B alignment of V
+      if (m <= 2) insite_refine_kernel<2, NA, D, true, true><<<grid, kBlock, 0, hs>>>(ra);
+      else insite_refine_kernel<3, NA, D, true, true><<<grid, kBlock, 0, hs>>>(ra);
+      return;
+    }
     // (m = 4: the 16-entry H in LDS plus the ring would hold the CU to 2 blocks; the per-step-load kernel runs it)
     if (win && m <= 3) {
       if (m <= 2) insite_refine_kernel<2, NA, D, true><<<grid, kBlock, 0, hs>>>(ra);
@@ -967,12 +1047,14 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
                       int32_t n_coef, const double* coef0, const int32_t* mask, const int8_t* exps, int32_t n_arms,
                       double dt, double lam, int32_t tau, int32_t substeps, int32_t revert_on_zoom_fail,
                       double* preds, int64_t ld_p, double* coef_out, int32_t* status_out, int32_t* iters_out,
-                      const int32_t* row_order, void* stream, int32_t* nfev_out = nullptr) {
+                      const int32_t* row_order, void* stream, int32_t* nfev_out = nullptr, bool pm = false) {
   const bool bits = arm8 == nullptr;
-  if (n_rows < 0 || T < 1 || n_arms < 1 || n_arms > (bits ? 2 : 4) || substeps < 1 || !(dt > 0.0) ||
-      !(lam >= 0.0) || tau < 0 || ld_v < n_rows || ld_p < n_rows || n_statics < 0 ||
-      n_statics > INSITE_MAX_STATICS || ld_arm < (bits ? (n_rows + 31) / 32 : n_rows) || !coef0 || !mask ||
-      !exps || n_coef < 1)
+  // pm: the row layout of insite_refine_rows_f64 (patient-major V / arm8 / preds, leading dimensions >= T)
+  const int64_t ld_min = pm ? T : n_rows;
+  if (n_rows < 0 || T < 1 || n_arms < 1 || n_arms > (bits || pm ? 2 : 4) || substeps < 1 || !(dt > 0.0) ||
+      !(lam >= 0.0) || tau < 0 || ld_v < ld_min || ld_p < ld_min || n_statics < 0 ||
+      n_statics > INSITE_MAX_STATICS || ld_arm < (pm ? T : (bits ? (n_rows + 31) / 32 : n_rows)) || !coef0 ||
+      !mask || !exps || n_coef < 1 || (pm && bits))
     return INSITE_E_INVALID_ARG;
   if (n_coef > kRefineMaxCoef) return INSITE_E_UNSUPPORTED;
   RefineArgs ra{};
@@ -1005,6 +1087,8 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
       for (int a = 0; a < n_arms; ++a)
         if ((ra.t_mask[i] >> a) & 1) ra.gmap |= 1 << (i * 8 + a * 2 + (ra.t_ex[i] & 1));
   }
+  if (pm && (D != 1 || m > 3 || T < 2 || T > 64 || (ld_v & 1) || ((uintptr_t)V & 15u) || n_rows > INT32_MAX))
+    return INSITE_E_UNSUPPORTED;  // the windowed row kernel's shape (the reference's sequences: T <= 64, <= 3 active)
   if (n_rows == 0) return INSITE_OK;
   if (!V || (bits && !arm_bits) || !seq_len || !preds || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
   ra.V = V;
@@ -1032,9 +1116,11 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
   ra.dt = dt;
   ra.lam = lam;
   ra.m = m;
+  ra.pm = pm ? 1 : 0;
+  ra.st16 = ((uintptr_t)preds & 15u) == 0 && (ld_p & 1) == 0;
   const dim3 grid((unsigned)((n_rows + kBlock - 1) / kBlock));
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
-  if (bits) {
+  if (bits || pm) {
     if (D == 1) launch_refine<2, 1>(ra, grid, hs);
     else launch_refine<2, 4>(ra, grid, hs);
   } else {
@@ -1336,4 +1422,18 @@ int32_t insite_refine_general_f64(const double* V, int64_t ld_v, int32_t T, cons
   return refine_launch(V, ld_v, T, arm_bits, arm_bits ? nullptr : (arm ? arm : &kNoArms), ld_arm, u, seq_len, n_rows, n_statics, n_coef,
                        coef0, coef_arm_mask, coef_exps, n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds,
                        ld_p, coef_out, status_out, iters_out, row_order, stream, nfev_out);
+}
+
+int32_t insite_refine_rows_f64(const double* V, int64_t ld_v, int32_t T, const int8_t* arm, int64_t ld_arm,
+                               const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
+                               int32_t n_coef, const double* coef0, const int32_t* coef_arm_mask,
+                               const int8_t* coef_exps, int32_t n_arms, double dt, double lam, int32_t tau,
+                               int32_t substeps, int32_t revert_on_zoom_fail, double* preds, int64_t ld_p,
+                               double* coef_out, int32_t* status_out, int32_t* iters_out, int32_t* nfev_out,
+                               const int32_t* row_order, void* stream) {
+  static const int8_t kNoArms = 0;
+  if (!arm && n_rows > 0) return INSITE_E_INVALID_ARG;
+  return refine_launch(V, ld_v, T, nullptr, arm ? arm : &kNoArms, ld_arm, u, seq_len, n_rows, n_statics, n_coef, coef0,
+                       coef_arm_mask, coef_exps, n_arms, dt, lam, tau, substeps, revert_on_zoom_fail, preds, ld_p,
+                       coef_out, status_out, iters_out, row_order, stream, nfev_out, true);
 }

@@ -20,10 +20,11 @@ LIB_PATH = os.path.join(LIB_DIR, "libinsite_hip.so")
 if os.environ.get("INSITE_LIB_OVERRIDE"):
     LIB_PATH = os.environ["INSITE_LIB_OVERRIDE"]
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # status codes / enums (insite_hip.h)
 INSITE_OK = 0
+INSITE_E_UNSUPPORTED = -2   # include/insite_hip.h
 FD_SMOOTHED4, FD_ORDER4, FD_ORDER1, FD_SMOOTHED1 = 0, 1, 2, 3
 METHOD_EULER, METHOD_RK4 = 0, 1
 LAYOUT_PATIENT_MAJOR, LAYOUT_TIME_MAJOR, LAYOUT_TIME_MAJOR_BITS, LAYOUT_PATIENT_MAJOR_BITS = 0, 1, 2, 3
@@ -56,6 +57,7 @@ EXPORTS = (
     "insite_refine_f64",
     "insite_refine_arms_f64",
     "insite_refine_general_f64",
+    "insite_refine_rows_f64",
     "insite_refine_prepare_f64",
     "insite_refine_finish_f64",
     "insite_gen_gram_segments_workspace_bytes",
@@ -149,6 +151,9 @@ _SIGNATURES = {
     "insite_refine_general_f64": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _vp, _c_i64, _vp, _vp, _c_i64, _c_i32, _c_i32,
                                            _vp, _vp, _vp, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _c_i32, _vp, _c_i64,
                                            _vp, _vp, _vp, _vp, _vp, _vp]),
+    "insite_refine_rows_f64": (_c_i32, [_vp, _c_i64, _c_i32, _vp, _c_i64, _vp, _vp, _c_i64, _c_i32, _c_i32, _vp,
+                                        _vp, _vp, _c_i32, _c_f64, _c_f64, _c_i32, _c_i32, _c_i32, _vp, _c_i64, _vp,
+                                        _vp, _vp, _vp, _vp, _vp]),
     "insite_refine_prepare_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i64, _c_i32, _vp, _c_i64, _vp, _c_i64, _vp,
                                            _c_i64, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp]),
     "insite_refine_finish_f64": (_c_i32, [_vp, _c_i64, _vp, _c_i64, _c_i32, _vp, _c_i64, _vp, _c_i32, _vp, _vp, _vp,

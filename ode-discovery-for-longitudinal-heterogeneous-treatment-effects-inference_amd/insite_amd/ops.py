@@ -7,6 +7,7 @@ tensors raise ``ValueError`` and a missing library raises ``InsiteLibraryError``
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -940,9 +941,37 @@ def refine_terms(lib: PolyLibrary, n_coef_rows: int):
     return np.ascontiguousarray(mask), np.ascontiguousarray(exps, dtype=np.int8), A
 
 
+def _refine_rows_call(V, arm, u, seq_len, c0, mask, qexps, A, lib, dt, lam, tau, substeps, revert, outs, nfev, order,
+                      n_rows=None):
+    """Argument tuple of insite_refine_rows_f64 (the row-layout refinement: no prepare / finish passes)."""
+    nul = ctypes.c_void_p(0)
+    P_, co, so, io = outs
+    N = V.size(0) if n_rows is None else n_rows
+    return (_p(V), V.stride(0), V.size(1), _p(arm), arm.stride(0), _p(u) if lib.n_statics else nul, _p(seq_len), N,
+            lib.n_statics, int(c0.size), c0.ctypes.data_as(ctypes.c_void_p), mask.ctypes.data_as(ctypes.c_void_p),
+            qexps.ctypes.data_as(ctypes.c_void_p), A, float(dt), float(lam), int(tau), int(substeps),
+            int(bool(revert)), _p(P_), P_.stride(0), _p(co), _p(so), _p(io), _p(nfev) if nfev is not None else nul,
+            _p(order) if order is not None else nul)
+
+
+def refine_rows_supported(V, arm, u, seq_len, c0, mask, qexps, A, lib, outs) -> bool:
+    """Whether insite_refine_rows_f64 takes this model and layout: the library's own answer, asked with zero rows
+    (argument and shape checks only, nothing launched).  INSITE_REFINE_ROWS=0 in the environment says no."""
+    if A > 2 or os.environ.get("INSITE_REFINE_ROWS", "1") == "0":
+        return False
+    args = _refine_rows_call(V, arm, u, seq_len, c0, mask, qexps, A, lib, 1.0, 0.0, 0, 1, False, outs, None, None,
+                             n_rows=0)
+    st = _lib.load().insite_refine_rows_f64(*args, ctypes.c_void_p(0))
+    if st == _lib.INSITE_E_UNSUPPORTED:
+        return False
+    _lib.check("insite_refine_rows_f64", st)
+    return True
+
+
 def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: torch.Tensor, coef0: np.ndarray,
                   lib: PolyLibrary, dt: float, lam: float, tau: int, substeps: int = 5,
-                  revert_on_zoom_fail: bool = False, binned: bool = True, nfev: torch.Tensor | None = None):
+                  revert_on_zoom_fail: bool = False, binned: bool = True, nfev: torch.Tensor | None = None,
+                  rows: bool | None = None):
     """INSITE per-patient refinement (reference sindy.py:433-715).  V [N, T] f64 unscaled observations
     and arm [N, T] int8 per-step arms in the reference's patient-major layout (transposed to the
     kernel's time-major layout here), u [N, U], seq_len [N], coef0 the HOST global model [A, F].
@@ -960,6 +989,10 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
     ``nfev``: an int32 [N] device tensor receiving each row's objective/gradient evaluation count (the work
     count behind bench.py's INSITE roofline); it routes every model through insite_refine_general_f64 (the
     same kernels and arithmetic as the per-arm entry points).
+    ``rows`` (ABI 9): None / True take insite_refine_rows_f64 -- the windowed kernel on the patient-major rows
+    themselves, no prepare / finish passes -- whenever the library reports the model and layout in its shape (two
+    arms, <= 3 active coefficients, affine RHS, T <= 64); False forces the prepare / kernel / finish route.  The
+    outputs are bitwise the same either way.
     Returns (preds [N, T], coef [N, A, F], status [N], iterations [N])."""
     _dev("V", V, torch.float64, 2)
     _dev("arm", arm, torch.int8, 2)
@@ -977,6 +1010,29 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
     mask, qexps, A = refine_terms(lib, c0.shape[0])
     if A > 4:
         raise ValueError("at most 4 treatment arms (joint model: 2 binary treatment inputs)")
+    if rows is not False and A <= 2:
+        if lib.n_statics and u.size(0) != N:
+            raise ValueError("u must have one row per refined row")
+        if seq_len.numel() != N:
+            raise ValueError("seq_len must have one entry per row")
+        if nfev is not None:
+            _dev("nfev", nfev, torch.int32, 1)
+            if nfev.numel() != N:
+                raise ValueError("nfev must have one entry per row")
+        outs = (torch.empty((N, T), dtype=torch.float64, device=V.device),
+                torch.empty((N,) + c0.shape, dtype=torch.float64, device=V.device),
+                torch.empty((N,), dtype=torch.int32, device=V.device), torch.empty((N,), dtype=torch.int32, device=V.device))
+        if N and V.stride(1) == 1 and arm.stride(1) == 1 and \
+                refine_rows_supported(V, arm, u, seq_len, c0, mask, qexps, A, lib, outs):
+            if int(arm.amax().item()) > 1:
+                raise ValueError("two-arm models need arm values 0/1")
+            order = rk45_order(seq_len, T) if (binned and N > 64) else None
+            args = _refine_rows_call(V, arm, u, seq_len, c0, mask, qexps, A, lib, dt, lam, tau, substeps,
+                                     revert_on_zoom_fail, outs, nfev, order)
+            _run(("insite_refine_rows_f64", args, V.device, None))
+            return outs
+        if rows:
+            raise ValueError("insite_refine_rows_f64 does not take this model / layout (INSITE_E_UNSUPPORTED)")
     order = rk45_order(seq_len, T) if (binned and N > 64) else None
     if order is None:
         Vt, arms = refine_prepare(V, arm, bits=A <= 2, order=None)
@@ -998,14 +1054,16 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
 
 class InsiteRefinePlan:
     """``insite_refine`` (binned) prepared once: the inputs validated (the arm range check included) and every buffer
-    and argument packed, so a call enqueues exactly four C calls -- the seq_len counting sort
+    and argument packed, so a call enqueues two C calls in the row layout (``mode`` "rows", ABI 9: the seq_len
+    counting sort and insite_refine_rows_f64) or else four -- the seq_len counting sort
     (insite_rk45_order_i32), the gather pass (insite_refine_prepare_f64: rows, statics, sequence lengths into lane
     order), the refinement kernel, and the scatter pass (insite_refine_finish_f64: predictions, coefficients,
     statuses, iteration counts back to row order) -- with no host synchronisation.  Outputs ``out`` = (preds
     [N, T], coef [N, A, F], status [N], iters [N]), bitwise those of ``insite_refine``.  The plan keeps references
     to its inputs: refresh them in place between calls (a serving loop) or make a new plan."""
 
-    def __init__(self, V, arm, u, seq_len, coef0, lib, dt, lam, tau, substeps=5, revert_on_zoom_fail=False):
+    def __init__(self, V, arm, u, seq_len, coef0, lib, dt, lam, tau, substeps=5, revert_on_zoom_fail=False,
+                 rows=None, nfev=None):
         L = _lib.load()
         _dev("V", V, torch.float64, 2)
         _dev("arm", arm, torch.int8, 2)
@@ -1032,6 +1090,33 @@ class InsiteRefinePlan:
         W = (N + 31) // 32
         U = lib.n_statics
         self.order = torch.empty((N,), dtype=torch.int32, device=dev)
+        self._ows = Workspace("scratch").get(L.insite_rk45_order_workspace_bytes(int(T)), dev)
+        self._c0, self._mask, self._qexps, self._tab = c0, mask, qexps, lib.ctypes_table()
+        self._keep = (V, arm, u, seq_len, nfev)
+        self.device = dev
+        order_call = (L.insite_rk45_order_i32, (_p(seq_len), N, int(T), _p(self.order), _p(self._ows),
+                                                self._ows.numel()))
+        if nfev is not None:
+            _dev("nfev", nfev, torch.int32, 1)
+            if nfev.numel() != N:
+                raise ValueError("nfev must have one entry per row")
+        if rows is not False and bits:
+            outs = (torch.empty((N, T), dtype=torch.float64, device=dev),
+                    torch.empty((N,) + c0.shape, dtype=torch.float64, device=dev),
+                    torch.empty((N,), dtype=torch.int32, device=dev), torch.empty((N,), dtype=torch.int32, device=dev))
+            if refine_rows_supported(V, arm, u, seq_len, c0, mask, qexps, A, lib, outs):
+                # the row layout (ABI 9): two C calls, the counting sort and the refinement on the rows themselves
+                self.mode = "rows"
+                self.out = outs
+                self._calls = [order_call, (L.insite_refine_rows_f64, _refine_rows_call(
+                    V, arm, u, seq_len, c0, mask, qexps, A, lib, dt, lam, tau, substeps, revert_on_zoom_fail, outs,
+                    nfev, self.order))]
+                return
+            if rows:
+                raise ValueError("insite_refine_rows_f64 does not take this model / layout (INSITE_E_UNSUPPORTED)")
+        if nfev is not None:
+            raise ValueError("nfev needs the row-layout plan")
+        self.mode = "prepare"
         ldt = N + (N & 1)   # even leading dimension (the windowed kernels' 16-B ring loads)
         self.Vt = torch.empty((T, ldt), dtype=torch.float64, device=dev)[:, :N]
         self.arms = torch.empty((T, W) if bits else (T, N), dtype=torch.int32 if bits else torch.int8, device=dev)
@@ -1043,13 +1128,9 @@ class InsiteRefinePlan:
         self.it_l = torch.empty((N,), dtype=torch.int32, device=dev)
         self.out = (torch.empty((N, T), dtype=torch.float64, device=dev), torch.empty_like(self.coef_l),
                     torch.empty_like(self.st_l), torch.empty_like(self.it_l))
-        self._ows = Workspace("scratch").get(L.insite_rk45_order_workspace_bytes(int(T)), dev)
         nul = ctypes.c_void_p(0)
-        self._c0, self._mask, self._qexps, self._tab = c0, mask, qexps, lib.ctypes_table()
-        self._keep = (V, arm, u, seq_len)
-        self.device = dev
         self._calls = [
-            (L.insite_rk45_order_i32, (_p(seq_len), N, int(T), _p(self.order), _p(self._ows), self._ows.numel())),
+            order_call,
             (L.insite_refine_prepare_f64, (_p(V), V.stride(0), _p(arm), arm.stride(0), N, T, _p(self.Vt), ldt,
                                            _p(self.arms) if bits else nul, W, nul if bits else _p(self.arms), N,
                                            _p(self.order), _p(u) if U else nul, U, _p(self.u_l) if U else nul,
@@ -1074,17 +1155,24 @@ class InsiteRefinePlan:
                                                          _p(self.it_l), _p(io))))
 
     def __call__(self, stream: torch.cuda.Stream | None = None):
-        h = ctypes.c_void_p((stream if stream is not None else torch.cuda.current_stream(self.device)).cuda_stream)
-        for fn, args in self._calls:
-            st = fn(*args, h)
-            if st:
-                _lib.check(getattr(fn, "__name__", "insite refine plan"), st)
+        for i in range(len(self._calls)):
+            self.call(i, stream)
         return self.out
 
+    def call(self, i: int, stream: torch.cuda.Stream | None = None):
+        """Enqueue the plan's i-th C call alone (bench.py times the refinement kernel this way)."""
+        h = ctypes.c_void_p((stream if stream is not None else torch.cuda.current_stream(self.device)).cuda_stream)
+        fn, args = self._calls[i]
+        st = fn(*args, h)
+        if st:
+            _lib.check(getattr(fn, "__name__", "insite refine plan"), st)
 
-def plan_insite_refine(V, arm, u, seq_len, coef0, lib, dt, lam, tau, substeps=5, revert_on_zoom_fail=False):
-    """``insite_refine`` (binned lane order) as a prepared plan (``InsiteRefinePlan``)."""
-    return InsiteRefinePlan(V, arm, u, seq_len, coef0, lib, dt, lam, tau, substeps, revert_on_zoom_fail)
+
+def plan_insite_refine(V, arm, u, seq_len, coef0, lib, dt, lam, tau, substeps=5, revert_on_zoom_fail=False,
+                       rows=None, nfev=None):
+    """``insite_refine`` (binned lane order) as a prepared plan (``InsiteRefinePlan``).  ``rows`` as in
+    ``insite_refine``; ``nfev`` (row layout only) an int32 [N] tensor receiving each row's evaluation count."""
+    return InsiteRefinePlan(V, arm, u, seq_len, coef0, lib, dt, lam, tau, substeps, revert_on_zoom_fail, rows, nfev)
 
 
 def refine_prepare(V: torch.Tensor, arm: torch.Tensor, bits: bool = True, order: torch.Tensor | None = None,

@@ -38,7 +38,7 @@ def _lib_exports():
 def test_header_declares_the_abi():
     fns = _header_functions()
     assert "insite_rollout_f64" in fns and "insite_sindy_fit_f64" in fns
-    assert len(fns) == 42 and set(fns) == set(_lib_exports())
+    assert len(fns) == 43 and set(fns) == set(_lib_exports())
 
 
 def test_library_exports_every_header_symbol(L):
@@ -62,7 +62,7 @@ def test_nm_shows_c_linkage():
 
 def test_version_and_strerror(L):
     from insite_amd import _lib
-    assert L.insite_abi_version() == _lib.ABI_VERSION == 8
+    assert L.insite_abi_version() == _lib.ABI_VERSION == 9
     assert L.insite_strerror(0) == b"ok"
     for code in (-1, -2, -3, -4):
         s = L.insite_strerror(code)

@@ -361,3 +361,66 @@ def test_windowed_refine_equals_per_step_loads(dev, N, T):
     for a, b in zip(w, l_):
         assert torch.equal(a, b)
     assert torch.equal(nf_w, nf_l)
+
+
+@pytest.mark.parametrize("N,T,ld,m", [(5_000, 60, 60, 3), (4_097, 34, 34, 3), (130, 64, 64, 2), (777, 7, 8, 3),
+                                      (1, 2, 2, 3), (65, 33, 40, 2)])
+def test_refine_rows_layout_equals_prepare_route(dev, N, T, ld, m):
+    """insite_refine_rows_f64 (ABI 9: the windowed kernel on the patient-major rows gathered through the lane order,
+    predictions stored through the LDS ring as row segments, no prepare / finish passes) against the prepare /
+    kernel / finish route: predictions, coefficients, statuses, iteration and evaluation counts bitwise equal.  Ragged
+    seq_len (rows <= tau skipped), a partial last wave, padded leading dimensions, T = 2 and the M = 2 / M = 3
+    kernels; binned and identity lane orders; the plan takes the same route."""
+    from insite_amd import cohort, ops
+    coh = cohort.synthetic_pkpd(N, T, seed=N + 7 * T, device=dev, equation="EQ_4_C")
+    V = torch.zeros((N, ld), dtype=torch.float64, device=dev)[:, :T]
+    V.copy_(coh.x[:, :T])
+    g = torch.Generator(device=dev)
+    g.manual_seed(N * 5 + T)
+    flip = torch.randint(1, max(2, T), (N, 1), generator=g, device=dev)
+    arm = torch.zeros((N, ld), dtype=torch.int8, device=dev)[:, :T]
+    arm.copy_(torch.where(torch.arange(T, device=dev)[None, :] >= flip, 1 - coh.arm[:, None].to(torch.int64),
+                          coh.arm[:, None].to(torch.int64)).to(torch.int8))
+    sl = torch.randint(1, T + 1, (N,), generator=g, device=dev, dtype=torch.int32)
+    c0 = np.zeros((2, coh.lib.n_terms))
+    c0[0, 4], c0[1, 1] = -1.1107592869834308, -0.14540553723951796
+    if m == 3:
+        c0[1, 5] = -1.0234639833519243
+    Vc, ac = V.contiguous(), arm.contiguous()
+    for binned in (True, False):
+        nf_r = torch.empty((N,), dtype=torch.int32, device=dev)
+        nf_p = torch.empty((N,), dtype=torch.int32, device=dev)
+        r = ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5, binned=binned, nfev=nf_r, rows=True)
+        p = ops.insite_refine(Vc, ac, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5, binned=binned, nfev=nf_p, rows=False)
+        torch.cuda.synchronize()
+        for a, b in zip(r, p):
+            assert torch.equal(a, b)
+        assert torch.equal(nf_r, nf_p)
+        assert (r[2][sl <= 5] == -1).all()
+    plan = ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5)
+    assert plan.mode == "rows"
+    got = plan()
+    torch.cuda.synchronize()
+    for a, b in zip(got, p):
+        assert torch.equal(a, b)
+
+
+def test_refine_rows_unsupported_shapes_fall_back(dev):
+    """Outside the windowed row kernel's shape (odd leading dimension, T > 64, four arms) the library answers
+    INSITE_E_UNSUPPORTED without launching, insite_refine(rows=None) takes the prepare route and rows=True raises."""
+    from insite_amd import cohort, ops
+    for N, T in ((300, 33), (300, 70)):
+        coh = cohort.synthetic_pkpd(N, T, seed=3, device=dev, equation="EQ_4_C")
+        V = coh.x[:, :T].contiguous()
+        arm = coh.arm[:, None].expand(N, T).to(torch.int8).contiguous()
+        sl = torch.full((N,), T, dtype=torch.int32, device=dev)
+        c0 = np.zeros((2, coh.lib.n_terms))
+        c0[0, 4], c0[1, 1] = -1.1, -0.145
+        a = ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5)
+        b = ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5, rows=False)
+        torch.cuda.synchronize()
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+        with pytest.raises(ValueError):
+            ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5, rows=True)
+        assert ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5).mode == "prepare"
