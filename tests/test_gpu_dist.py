@@ -105,3 +105,123 @@ def test_two_rank_discovery_and_metrics_equal_single_rank(dev):
     for det in (False, True):
         np.testing.assert_array_equal(out[0][1][det][0], out[1][1][det][0])
     np.testing.assert_array_equal(out[0][1][True][2], out[1][1][True][2])
+
+
+NL, TL, KL = 20_480, 80, 2          # lagged stream: shard bounds on whole arm-bit words (10,240 = 320 x 32)
+
+
+def _lagged_cohorts(dev):
+    from insite_amd import cohort
+    cohs = [cohort.synthetic_pkpd(NL, TL, seed=77 + j, device=dev, equation="EQ_4_C", layout="time") for j in range(2)]
+    bits = [cohort.counterfactual_arms(c.arm, TL, seed=77 + j, layout="time_bits") for j, c in enumerate(cohs)]
+    return cohs, bits
+
+
+def _lagged_worker(rank, world, port, q):
+    """One rank of the N > 1 C2 schedule (bench.py c2_lagged): its shard of two rotating cohorts, one
+    insite_fit_rollout_lagged_f64 launch per step, the K-fit bucket all-reduced after the launches the
+    LaggedSchedule names (gloo here, RCCL in the bench)."""
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import types
+    import torch.distributed as dist
+    from insite_amd import dist as idist
+    from insite_amd import ops
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        full, fbits = _lagged_cohorts(dev)
+        lo, hi = idist.shard_bounds(NL, rank, world)
+        assert lo % 32 == 0 and hi % 32 == 0
+        cohs, bitss = [], []
+        for c, b in zip(full, fbits):
+            s = types.SimpleNamespace(x=c.x[:, lo:hi].contiguous(), u=c.u[lo:hi].contiguous(),
+                                      arm=c.arm[lo:hi].contiguous(), rows=c.rows[lo:hi].contiguous(),
+                                      y0=c.y0[lo:hi].contiguous(), dt=c.dt)
+            cohs.append(s)
+            bitss.append(b[:, lo // 32:hi // 32].contiguous())
+        lib = full[0].lib
+        F = lib.n_terms
+        n = hi - lo
+        sched = idist.LaggedSchedule(KL)
+        buckets = [idist.MomentBucket(KL, 2, F, dev) for _ in range(2)]
+        ring = [(torch.zeros((2, F), dtype=torch.float64, device=dev), torch.zeros((2, F), dtype=torch.int8, device=dev),
+                 torch.zeros((2,), dtype=torch.int32, device=dev)) for _ in range(3)]
+        ys = [torch.empty((TL, n), dtype=torch.float64, device=dev) for _ in range(2)]
+        ws = ops.Workspace()
+        dummy = torch.zeros((2, F), dtype=torch.float64, device=dev)
+        Gs, bs = torch.zeros((2, F, F), dtype=torch.float64, device=dev), torch.zeros((2, F), dtype=torch.float64,
+                                                                                       device=dev)
+        solved, rolled = {}, {}
+        for k in range(2 * KL + 6):
+            p = sched.launch(k)
+            c = cohs[k % 2]
+            red = (buckets[p["reduce"][1]].bufs[p["reduce"][2]].G, buckets[p["reduce"][1]].bufs[p["reduce"][2]].b) \
+                if p["reduce"] else (Gs, bs)
+            fit_in = fit_out = None
+            if p["fit"]:
+                fc, bi, pos, r = p["fit"]
+                fit_in = (buckets[bi].bufs[pos].G, buckets[bi].bufs[pos].b)
+                fit_out = ring[r]
+            if p["rollout"]:
+                rc_, r = p["rollout"]
+                rcoh, rbits, coef_in, yy = cohs[rc_ % 2], bitss[rc_ % 2], ring[r][0], ys[rc_ % 2]
+            else:
+                rcoh, rbits, coef_in, yy = c, bitss[k % 2], dummy, ys[k % 2]
+            ops.plan_fit_rollout_lagged(c.x, c.u, c.arm, c.rows, c.dt, lib, 0.1, 0.5, rcoh.y0, rcoh.u, rbits, coef_in,
+                                        rcoh.dt, p["slot"], p["reduce"] is not None, ws, red, fit_in=fit_in,
+                                        fit_out=fit_out, T=TL, y_out=yy)()
+            torch.cuda.synchronize()
+            if p["allreduce_after"] is not None:
+                idist.reduce_bucket(buckets[p["allreduce_after"]])
+                torch.cuda.synchronize()
+            if p["fit"]:
+                solved[p["fit"][0]] = ring[p["fit"][3]][0].cpu().numpy().copy()
+            if p["rollout"]:
+                rolled[p["rollout"][0] % 2] = (p["rollout"][0], yy.cpu().numpy().copy())
+        q.put((rank, lo, hi, solved, rolled))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_two_rank_lagged_stream_matches_oracle_and_single_rank_rollout(dev):
+    """The N > 1 form of the headline kernel (ABI 8 lagged step) with 2 ranks on one GPU: every model both ranks
+    solve is bitwise the same on the two ranks and equals the oracle fit of the WHOLE cohort (support identical,
+    L-inf < 1e-8); every rank's rollout of its shard is bitwise the single-process rollout of those patients with
+    that model."""
+    from insite_amd import ops
+    from oracle import insite_ref as R
+    full, fbits = _lagged_cohorts(dev)
+    lib = full[0].lib
+    want = []
+    for c in full:
+        x = c.x[:, :NL].t().contiguous().cpu().numpy()
+        G, b = R.gram_moments_vectorized(x, c.u.cpu().numpy(), c.arm.cpu().numpy().astype(np.int64), TL - 2, c.dt,
+                                         lib.exps.astype(np.int64))
+        want.append(np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)]))
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_lagged_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s0, s1 = out[0][3], out[1][3]
+    assert sorted(s0) == sorted(s1) == list(range(2 * KL + 6 - KL - 1))
+    for cc in s0:
+        np.testing.assert_array_equal(s0[cc], s1[cc])
+        assert np.array_equal(s0[cc] != 0, want[cc % 2] != 0)
+        assert np.max(np.abs(s0[cc] - want[cc % 2])) < 1e-8
+    for rank, lo, hi, solved, rolled in out:
+        for j, (cc, y) in rolled.items():
+            yy = ops.rollout(full[j].y0, full[j].u, fbits[j], torch.as_tensor(solved[cc], device=dev), lib, full[j].dt,
+                             method="rk4", T=TL, layout="time_bits")
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(y, yy[:, lo:hi].cpu().numpy())
