@@ -391,7 +391,12 @@ class SINDY:
                                                        self.library, self.dt, float(self.lam), int(tau), substeps=5,
                                                        revert_on_zoom_fail=self.insite_revert_on_zoom_fail)
         self.insite_status, self.insite_iters, self.insite_coefs = status, iters, coef
-        return ((preds - mean) / std).contiguous()
+        scaled = ((preds - mean) / std).contiguous()
+        # the reference refuses refined predictions with NaN or Inf (sindy.py:710): a refined model that blows up
+        # inside the row's horizon ends the run there, not in a metric later
+        if not bool(torch.isfinite(scaled).all()):
+            raise AssertionError("Scaled_preds contains NaN or Inf")
+        return scaled
 
     def get_predictions(self, dataset) -> np.ndarray:
         logger.info("Predictions for %s.", getattr(dataset, "subset_name", "?"))

@@ -424,3 +424,26 @@ def test_refine_rows_unsupported_shapes_fall_back(dev):
         with pytest.raises(ValueError):
             ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5, rows=True)
         assert ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5).mode == "prepare"
+
+
+def test_plugin_insite_rejects_non_finite_refined_predictions(dev, model, monkeypatch):
+    """The reference asserts that the refined predictions hold no NaN or Inf (sindy.py:710); the plugin raises the
+    same AssertionError when the refinement returns a row whose refined model blew up."""
+    from insite_amd import config as C
+    from insite_amd import sindy as S
+    coll, x, u, arm, c0 = model
+    args = C.compose(["+backbone=insite", "+dataset=pkpd_sim", "dataset.equation_str=EQ_4_C",
+                      "model.dataset_name=EQ_4_C", "model.sindy_threshold=0.1", "model.sindy_alpha=0.5",
+                      "model.lam=10.0"])
+    m = S.SINDY(args, device=dev)
+    m.fit(coll["train"])
+    real = S.ops.insite_refine
+
+    def blown(*a, **k):
+        preds, coef, status, iters = real(*a, **k)
+        preds[3, -1] = float("inf")
+        return preds, coef, status, iters
+
+    monkeypatch.setattr(S.ops, "insite_refine", blown)
+    with pytest.raises(AssertionError, match="NaN or Inf"):
+        m.get_predictions(coll["test_cf_one_step"])

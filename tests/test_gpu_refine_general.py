@@ -34,22 +34,30 @@ def _run(dev, V, arms, u, sl, c0, lib, tau, lam=10.0):
 
 
 def _check(dev, V, arms, u, sl, c0, lib, tau, n_inputs=0):
+    """Every row: identical BFGS status, refined coefficients to 1e-7 relative.  Predictions: rows whose oracle
+    prediction is finite everywhere are compared at RMSE <= 1e-6 (relative beyond unit scale, the x^2 / x^3
+    models grow); rows whose refined model blows up inside the horizon (the reference's run would stop at its
+    NaN / Inf assertion, sindy.py:710 -- tests/test_gpu_insite.py checks the plugin does the same) must blow up at
+    the same steps, and are compared on their finite prefix.  Returns (status, number of blown-up rows)."""
     preds, coef, status, iters = _run(dev, V, arms, u, sl, c0, lib, tau)
     ex = lib.exps.astype(np.int64)
-    agree = 0
+    agree = blown = 0
     for p in range(V.shape[0]):
-        rp, rc, rs, ri = Q.refine_patient(V[p], arms[p], u[p], sl[p], c0, ex, DT, 10.0, tau, n_inputs=n_inputs)
+        # the line search's trial points of a polynomial model overflow in IEEE arithmetic (jax's as well); those
+        # objective values are inf / NaN and rejected by the Wolfe tests, as in the reference
+        with np.errstate(over="ignore", invalid="ignore"):
+            rp, rc, rs, ri = Q.refine_patient(V[p], arms[p], u[p], sl[p], c0, ex, DT, 10.0, tau, n_inputs=n_inputs)
         assert status[p] == rs, (p, status[p], rs)
         if np.abs(coef[p] - rc).max() <= 1e-7 * max(1.0, np.abs(rc).max()):
             agree += 1
-        fin = np.isfinite(rp)                                   # a refined model may leave the window unstable
+        fin = np.isfinite(rp)
+        blown += int(not fin.all())
         assert np.array_equal(np.isfinite(preds[p]), fin), p
-        # a refined polynomial model may blow up late in the window (x^3 terms): relative beyond unit scale
         err = np.abs(preds[p][fin] - rp[fin]) / np.maximum(1.0, np.abs(rp[fin]))
         assert np.sqrt(np.mean(err ** 2)) <= 1e-6, p
     assert agree == V.shape[0]
     assert (status[sl <= tau] == -1).all() and (iters[sl > tau] > 0).all()
-    return status
+    return status, blown
 
 
 def _rows(V, seed, tau, N):
@@ -132,8 +140,11 @@ def test_degree4_refinement_matches_oracle(dev, n_arms):
                                                                           ex, DT, T - 1)])
         V[p] += 1e-3 * rng.normal(size=T)
     tau = 3
-    st = _check(dev, V, arms, u, _rows(V, 11, tau, N), c0, lib, tau)
+    st, blown = _check(dev, V, arms, u, _rows(V, 11, tau, N), c0, lib, tau)
     assert (st >= 0).sum() > N // 2
+    # the oracle's refined models blow up on 7 (2 arms) / 2 (4 arms) of the 96 rows of this seeded problem
+    # (checked on the CPU restatement); the GPU reproduces exactly those rows' non-finite steps (asserted above)
+    assert blown == {2: 7, 4: 2}[n_arms]
 
 
 def test_plugin_joint_insite_end_to_end(dev):

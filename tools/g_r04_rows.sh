@@ -1,7 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_insite.py tests/test_gpu_dist.py -x -v --timeout 120 --timeout-method thread > gpurun_out/r04_rows_tests.txt 2>&1 || { tail -30 gpurun_out/r04_rows_tests.txt; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_insite.py tests/test_gpu_dist.py tests/test_gpu_refine_general.py -x -v --timeout 120 --timeout-method thread > gpurun_out/r04_rows_tests.txt 2>&1 || { tail -30 gpurun_out/r04_rows_tests.txt; exit 1; }
 tail -3 gpurun_out/r04_rows_tests.txt
 timeout -k 10 300 python bench.py --config insite --no-cpu-baseline --steps 5 --warmup 2 > gpurun_out/r04_rows_bench.jsonl 2> gpurun_out/r04_rows_bench.err || { tail -20 gpurun_out/r04_rows_bench.err; exit 1; }
 cat gpurun_out/r04_rows_bench.jsonl
