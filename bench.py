@@ -84,7 +84,7 @@ def parse():
                          "re-reads data the 256 MB Infinity Cache still holds)")
     ap.add_argument("--isolated", action="store_true",
                     help="also time each C2 kernel in isolation (back-to-back launches on one stream)")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "insite", "f4"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "insite", "insite4", "f4"],
                     help="c2: BASELINE configs[1], the headline line (default); c3: configs[2], the 5-state fp32 "
                          "system (parity-test configuration, measured separately)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"),
@@ -816,6 +816,184 @@ def insite_main(args):
 
 # planted per-arm model of the F4 cohort over [1, x0, u0, x0 u0]: no treatment / chemo / radio / both
 F4_COEF = [[0.0, 0.20, 0.0, 0.0], [0.0, 0.0, 0.0, -0.60], [0.0, -0.30, 0.0, 0.0], [0.0, -0.25, 0.0, -0.90]]
+
+
+def _insite4_rows(N, T, seed, device):
+    """The INSITE4 rows (cancer_sim / EQ_5 shape): F4's 4-arm cohort (planted per-arm model, Markov arms, Euler-5
+    truth + 0.01 noise) patient-major, arm index = treatment code (chemo | radio << 1), seq_len U{1..59}."""
+    from insite_amd import cohort
+    coh = cohort.synthetic_segments(N, T, seed=seed, device=device, coef=F4_COEF, dt=0.1)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed + 1)
+    sl = torch.randint(1, T, (N,), generator=g, device=device, dtype=torch.int32)
+    return coh.x[:T].t().contiguous(), coh.arm.t().contiguous(), coh.u, sl, coh.lib, coh.dt
+
+
+def _insite4_models(V, arm, u, dt, lib, n_fit=20_000):
+    """The three global models the 4-arm INSITE line refines: (1) ``sparse`` = the planted per-arm model scaled by
+    1.1 (5 active terms: every row has something to refine), (2) ``dense`` = (1) with the 11 zero terms at 0.01 --
+    all 16 active, as the reference's cancer_sim model (final_with_insite.txt:2326 logs 16 non-zero terms), and
+    (3) ``joint`` = the one-ODE model over [x0, chemo, radio, u0] (sindy.py:503-517) least-squares fitted to forward
+    differences of the first ``n_fit`` rows, |c| <= 1e-3 dropped."""
+    from insite_amd.library import polynomial_library
+    base = np.array(F4_COEF) * 1.1
+    lib_j = polynomial_library(1, 2, True, n_inputs=2)
+    n = min(n_fit, V.size(0))
+    x = V[:n].cpu().numpy()
+    a = arm[:n].cpu().numpy().astype(np.int64)
+    uu = u[:n, 0].cpu().numpy()
+    T = x.shape[1]
+    cols = np.stack([x[:, :-1], (a[:, :-1] & 1).astype(np.float64), ((a[:, :-1] >> 1) & 1).astype(np.float64),
+                     np.repeat(uu[:, None], T - 1, axis=1)], axis=-1).reshape(-1, 4)
+    ex = lib_j.exps.astype(np.int64)
+    theta = np.prod(cols[:, None, :] ** ex[None, :, :], axis=2)
+    xd = ((x[:, 1:] - x[:, :-1]) / dt).reshape(-1)
+    cj = np.linalg.lstsq(theta, xd, rcond=None)[0]
+    cj[np.abs(cj) <= 1e-3] = 0.0
+    return {"sparse": (base, lib), "dense": (np.where(base != 0, base, 0.01), lib), "joint": (cj[None, :], lib_j)}
+
+
+def _insite4_rows_np(N, T, seed, dt=0.1, switch_p=0.1, noise=0.01):
+    """Host rows of the same distribution as _insite4_rows (numpy; for the CPU leg, drawn before any GPU context):
+    u ~ N(0.5, 0.05), y0 ~ U(1, 5), Markov arms over 4 codes (switch 0.1 per step), Euler-5 of F4's model."""
+    rng = np.random.default_rng(seed)
+    c = np.array(F4_COEF)
+    u = rng.normal(0.5, 0.05, (N, 1))
+    y = rng.uniform(1.0, 5.0, N)
+    arm = np.empty((N, T), dtype=np.int8)
+    cur = rng.integers(0, 4, N)
+    x = np.empty((N, T + 1))
+    x[:, 0] = y
+    h = dt / 5.0
+    for k in range(T):
+        arm[:, k] = cur
+        ca = c[cur]
+        for _ in range(5):
+            y = y + h * (ca[:, 0] + ca[:, 1] * y + ca[:, 2] * u[:, 0] + ca[:, 3] * y * u[:, 0])
+        x[:, k + 1] = y
+        sw = rng.random(N) < switch_p
+        cur = np.where(sw, rng.integers(0, 4, N), cur)
+    x += noise * rng.normal(size=x.shape)
+    sl = rng.integers(1, T, N).astype(np.int32)
+    return x[:, :T], arm, u, sl
+
+
+def _cpu_refine4_chunk(bounds):
+    from oracle import insite_refine_ref as Q
+    lo, hi = bounds
+    d = _CPU
+    for i in range(lo, hi):
+        Q.refine_patient(d["V"][i], d["arm"][i], d["u"][i], int(d["sl"][i]), d["c0"], d["ex"], d["dt"], 10.0, 5)
+    return hi - lo
+
+
+def insite4_cpu_baseline(V, arm, u, sl, c0, ex, dt, per_worker=256):
+    """Bounded CPU sample of the 4-arm dense INSITE workload: the oracle's restatement of the jax BFGS refinement
+    (oracle/insite_refine_ref.py) on up to per_worker x workers host rows of the benched distribution
+    (_insite4_rows_np), over the host's workers (a forked pool: call before the GPU context exists)."""
+    import multiprocessing as mp
+    sys.path.insert(0, ROOT)
+    info = host_info()
+    W = info["workers"]
+    n = min(W * per_worker, V.shape[0])
+    _CPU.update(V=V[:n], arm=arm[:n], u=u[:n], sl=sl[:n], c0=c0, ex=ex, dt=dt)
+    chunks = [(int(a[0]), int(a[-1]) + 1) for a in np.array_split(np.arange(n), W) if a.size]
+    with mp.get_context("fork").Pool(W, initializer=_cpu_worker_init) as pool:
+        pool.map(abs, range(W))
+        t0 = time.perf_counter()
+        pool.map(_cpu_refine4_chunk, chunks)
+        el = time.perf_counter() - t0
+    for k in ("V", "arm", "u", "sl"):
+        _CPU.pop(k, None)
+    return {"value": n / el, "unit": "patient-trajectories/s", "cores": W, "kind": "port",
+            "sample": f"oracle/insite_refine_ref.py (jax BFGS restated, numpy) on {n} host rows of the benched "
+                      f"4-arm distribution (T = 60, seq_len U{{1..59}}) with the dense model (16 active coefficients) "
+                      f"over a {W}-process pool, {el:.2f} s", "host": info}
+
+
+def insite4_main(args):
+    """INSITE refinement of the 4-arm models (the cancer_sim / EQ_5 path, sindy.py:484-551; the reference's slowest
+    published path, cancer_sim INSITE 83.5 s, final_with_insite.txt:2326): 1M rows x T = 60 with int8 per-step arms
+    0..3, one static, tau = 5, lam = 10 (config/config.yaml:24-27).  Three global models: sparse per-arm (5 active
+    terms, the register-resident M = 8 kernel), dense per-arm (16 active, the M = 16 kernel -- the line's value,
+    as the reference's cancer_sim model is dense) and the joint one-ODE model (insite_refine_general_f64's folded
+    treatment combinations).  One step = one refinement of every row: the seq_len sort, the gather pass, the kernel
+    and the scatter pass (ops.plan_insite_refine, 4 C calls)."""
+    from insite_amd import ops
+    N = args.patients if args.patients != 100_000 else 1_000_000
+    T = 60
+    cpu = None
+    if not args.no_cpu_baseline:   # host rows first (no GPU context yet: the pool forks)
+        from insite_amd.library import polynomial_library
+        Vc, ac, uc, slc = _insite4_rows_np(4096, T, args.seed + 41)
+        c_dense = np.where(np.array(F4_COEF) != 0, np.array(F4_COEF) * 1.1, 0.01)
+        cpu = insite4_cpu_baseline(Vc, ac, uc, slc, c_dense, polynomial_library(1, 2, True).exps.astype(np.int64), 0.1)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    V, arm, u, sl, lib, dt = _insite4_rows(N, T, args.seed + 41, dev)
+    models = _insite4_models(V, arm, u, dt, lib)
+    st_ = torch.cuda.current_stream(dev)
+    res = {}
+    for name, (c0, lb) in models.items():
+        plan = ops.plan_insite_refine(V, arm, u, sl, c0, lb, dt, 10.0, 5)
+        for _ in range(args.warmup):
+            plan()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            preds, coef, status, iters = plan()
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t0) / args.steps * 1e3
+        kidx = len(plan._calls) - 2              # [sort, prepare, kernel, finish]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st_)
+        for _ in range(args.steps):
+            plan.call(kidx, st_)
+        e1.record(st_)
+        torch.cuda.synchronize(dev)
+        kern_ms = e0.elapsed_time(e1) / args.steps
+        nf = torch.empty((N,), dtype=torch.int32, device=dev)
+        p2, _, s2, _ = ops.insite_refine(V, arm, u, sl, c0, lb, dt, 10.0, 5, nfev=nf)
+        torch.cuda.synchronize(dev)
+        K = torch.clamp(sl.to(torch.int64) - 5, min=0, max=T - 1)
+        A_, SUB = 4, 5
+        per_step = SUB * (4 * A_ + 7) + 4 * A_ + 5
+        flop = float((nf.to(torch.int64) * K).sum().item()) * per_step + float(N) * T * SUB * 4
+        stn = status.cpu().numpy()
+        m_act = int((np.abs(c0) > 1e-3).sum())
+        res[name] = {"active_coefficients": m_act, "ms_per_step": ms, "kernel_ms": kern_ms,
+                     "kernel": f"insite_refine_kernel<{2 if m_act <= 2 else 3 if m_act == 3 else 4 if m_act <= 4 else 8 if m_act <= 8 else 16 if m_act <= 16 else 36}, 4, 1>",
+                     "valu_f64_TFLOPs": flop / (kern_ms * 1e-3) / 1e12,
+                     "frac": flop / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
+                     "refined_rows": int((stn >= 0).sum()), "converged": int((stn == 0).sum()),
+                     "mean_bfgs_iterations": float(iters.cpu().numpy()[stn >= 0].mean()),
+                     "mean_evaluations_per_refined_row": float(nf.to(torch.float64)[s2 >= 0].mean().item()),
+                     "equal_to_nfev_route": bool(torch.equal(p2, preds) and torch.equal(s2, status)),
+                     "finite_predictions": bool(torch.isfinite(preds).all().item()), "algorithmic_flop": flop}
+    d = res["dense"]
+    kb = N * T * (8 + 1 + 8) + N * (8 + 4) + N * (16 * 8 + 8)
+    out = {
+        "metric": METRIC, "value": N / (d["ms_per_step"] * 1e-3), "unit": "patient-trajectories/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": d["ms_per_step"], "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: on-device 4-arm cohort (F4's planted model, Markov arms, Euler-5 truth + 0.01 noise), "
+                "T=60, seq_len U{1..59}",
+        "config": {"workload": f"INSITE refinement, 4 arms (cancer_sim / EQ_5 path; BFGS per row, tau=5, lam=10) + "
+                               f"Euler-5 rollout, {N // 1000}k rows; value = the dense per-arm model", "rows": N,
+                   "T": T, "arms": 4},
+        "models": res,
+        "roofline": {"kernel": d["kernel"] + " (dense per-arm model: rolled loops, per-lane scratch state)",
+                     "bound": "valu-f64", "unit": "TFLOP/s", "achieved": d["valu_f64_TFLOPs"],
+                     "peak": FP64_VALU_PEAK_TFLOPS, "frac": d["frac"],
+                     "traffic": traffic_for("insite4", "insite_refine_kernel", args=args),
+                     "avg_launch_ms": d["kernel_ms"], "algorithmic_flop": d["algorithmic_flop"],
+                     "flop_method": "sum over refined rows of nfev_r x K_r x (5 x (4A + 7) + 4A + 5), A = 4 arms, + N x T "
+                                    "x 5 x 4 for the final scan; nfev from the kernel's own count",
+                     "algorithmic_bytes": kb, "achieved_GBps": kb / (d["kernel_ms"] * 1e-3) / 1e9},
+    }
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+    emit(out)
 
 
 def f4_main(args):
@@ -1715,6 +1893,8 @@ def main():
         return f4_main(args)
     if args.config == "c4":
         return c4_main(args)
+    if args.config == "insite4":
+        return insite4_main(args)
     if args.config == "insite":
         return insite_main(args)
     if args.config == "c3":
