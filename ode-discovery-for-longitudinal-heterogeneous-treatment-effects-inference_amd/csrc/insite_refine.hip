@@ -123,6 +123,15 @@ __device__ __forceinline__ int pm_slot_index(int r, int col) {
   return ((col >> 3) & 1) * (kWin * kWave) + (r >> 4) * 128 + m * 8 + ((((s >> 1) - (m >> 2)) & 3) << 1) + (s & 1);
 }
 
+// The ring's wait: the hardware wait for the LDS-DMA loads (inline asm: the compiler does not track them) AND the
+// same wait as a builtin the compiler's waitcnt pass sees, so it knows its own earlier loads (the scan's y0) have
+// completed too.  With the asm alone the pass kept a vmcnt(0) for y0 inside the sub-step loop -- which, executed
+// with a ring prefetch in flight, waited for the prefetch every step that issued one.
+__device__ __forceinline__ void ring_wait() {
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0) expcnt(7) lgkmcnt(15)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <int M, int NA, int D, bool WIN = false, bool PM = false>
 struct RefineLane {
   static constexpr int RU = M <= kRefineRegActive ? M : 1;
@@ -233,7 +242,11 @@ struct RefineLane {
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) Kw = max(Kw, __shfl_xor(Kw, off));
       nch = PM ? (Kw > 0 ? Kw / kWin + 1 : 0) : (Kw + kWin - 1) / kWin;  // PM: column chunks 0 .. Kw / kWin
+      // chunk 0 waited for here, unconditionally (with y0: the compiler then knows no load of its own is pending
+      // inside the loop), chunk 1 prefetched; the loop waits at each later chunk boundary
       if (nch > 0) fill(0, 0);
+      ring_wait();
+      if (nch > 1) fill(1, 1);
     }
     // (non-WIN) step k's arm and target are requested one step ahead (issued before step k - 1's sub-steps) so the
     // dependent Euler chain does not wait on a load per step
@@ -245,8 +258,8 @@ struct RefineLane {
       double vk1;
       if constexpr (WIN && PM) {
         const int col = k + 1;
-        if (k == 0 || (col & (kWin - 1)) == 0) {  // column chunk col / kWin landed; start the next one
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if ((col & (kWin - 1)) == 0) {  // column chunk col / kWin landed; start the next one
+          ring_wait();
           const int nx = col / kWin + 1;
           if (nx < nch) fill(nx, nx & 1);
         }
@@ -254,8 +267,8 @@ struct RefineLane {
         ak = armbit(k);
         vk1 = win[pm_slot_index(threadIdx.x & (kWave - 1), col)];
       } else if constexpr (WIN) {
-        if ((k & (kWin - 1)) == 0) {  // slot k / kWin landed; start the next one into the other slot
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (k > 0 && (k & (kWin - 1)) == 0) {  // slot k / kWin landed; start the next one into the other slot
+          ring_wait();
           if (k / kWin + 1 < nch) fill(k / kWin + 1, (k / kWin + 1) & 1);
         }
         if (k >= Kl) continue;

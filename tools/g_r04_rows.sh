@@ -8,3 +8,6 @@ cat gpurun_out/r04_rows_bench.jsonl
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r04_rows_prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --config insite --no-cpu-baseline --steps 5 --warmup 2 > $GRAFT_REPO_ROOT/gpurun_out/r04_rows_prof.log 2>&1 || exit 1
 bash $GRAFT_REPO_ROOT/tools/g_r04_refine_pmc.sh
+cd $GRAFT_REPO_ROOT
+timeout -k 10 400 python bench.py --config insite4 --steps 3 --warmup 1 > gpurun_out/r04_insite4.jsonl 2> gpurun_out/r04_insite4.err || { tail -20 gpurun_out/r04_insite4.err; exit 1; }
+cat gpurun_out/r04_insite4.jsonl
