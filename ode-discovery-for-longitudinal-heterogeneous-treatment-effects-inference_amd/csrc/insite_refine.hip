@@ -118,9 +118,13 @@ constexpr int kWin = 8;
 // LDS-DMA instruction moves 16 rows x 64 B (4 lanes x 16 B per row), and lane 4m + j of instruction q writes the
 // 16-B piece ((j + m / 4) & 3) of row 16 q + m: the swizzle spreads a step's 64 reads (row r reads its own column)
 // over all 64 banks, 2 passes per ds_read_b64 as in the time-major ring.
+// Element (row r, column col): slot (col / 8) & 1, instruction r / 16, row r % 16 = m, and within the row's 64 B the
+// piece ((col % 8) / 2 - m / 4) & 3, element col & 1 -- i.e. (col - 2 (m / 4)) & 7 (an even shift keeps the low
+// bit), so a lane adds its constant pm_lane_rot to the column and masks: 3 integer ops per read.
+__device__ __forceinline__ int pm_lane_base(int r) { return (r >> 4) * 128 + (r & 15) * 8; }
+__device__ __forceinline__ int pm_lane_rot(int r) { return (-2 * ((r & 15) >> 2)) & 7; }
 __device__ __forceinline__ int pm_slot_index(int r, int col) {
-  const int s = col & (kWin - 1), m = r & 15;
-  return ((col >> 3) & 1) * (kWin * kWave) + (r >> 4) * 128 + m * 8 + ((((s >> 1) - (m >> 2)) & 3) << 1) + (s & 1);
+  return ((col >> 3) & 1) * (kWin * kWave) + pm_lane_base(r) + ((col + pm_lane_rot(r)) & 7);
 }
 
 // The ring's wait: the hardware wait for the LDS-DMA loads (inline asm: the compiler does not track them) AND the
@@ -253,6 +257,7 @@ struct RefineLane {
     int ak_nx = WIN ? 0 : armbit(0);
     double v_nx = WIN ? 0.0 : ra.V[ra.ldv + p];
     const int kend = WIN ? (PM ? Kw : nch * kWin) : Kl;
+    const int lbase = PM ? pm_lane_base(threadIdx.x & (kWave - 1)) : 0, lrot = PM ? pm_lane_rot(threadIdx.x & (kWave - 1)) : 0;
     for (int k = 0; k < kend; ++k) {
       int ak;
       double vk1;
@@ -265,7 +270,7 @@ struct RefineLane {
         }
         if (k >= Kl) continue;
         ak = armbit(k);
-        vk1 = win[pm_slot_index(threadIdx.x & (kWave - 1), col)];
+        vk1 = win[((col >> 3) & 1) * (kWin * kWave) + lbase + ((col + lrot) & 7)];
       } else if constexpr (WIN) {
         if (k > 0 && (k & (kWin - 1)) == 0) {  // slot k / kWin landed; start the next one into the other slot
           ring_wait();
