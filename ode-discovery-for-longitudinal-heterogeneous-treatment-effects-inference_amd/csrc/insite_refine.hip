@@ -29,6 +29,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 
 #include "insite_hip.h"
@@ -1023,6 +1024,440 @@ insite_refine_kernel(RefineArgs ra) {
   if (ra.nfev) ra.nfev[p] = ln.nev;
 }
 
+// ------------------------------------------------------------------------------------------------------------------
+// Dynamic lane -> row assignment (row layout; INSITE_REFINE_DYN, runtime switch INSITE_REFINE_DYN=0 in the environment)
+// ------------------------------------------------------------------------------------------------------------------
+// With one row per lane a wave runs as long as its slowest row: rows binned by seq_len scan similar windows, but the
+// number of evaluations per row (BFGS iterations x line-search trials) still varies, and the static kernel's lanes
+// idle ~40 % of the wave's scans (bench.py INSITE line: divergence ratio 1.67).  Here a block owns a contiguous range
+// of rows_per_block lane-order rows (2-4 per lane) and its lanes take them from an LDS counter: a lane whose row is
+// done writes the row's coefficients / status / iterations / evaluation count and, once INSITE_REFINE_DYN_REFILL
+// lanes of its wave are idle (or none is busy), the wave claims that many rows with ONE LDS atomic and the new lanes
+// start with their first evaluation (at c0, norm 1) in the next scan.  The row layout's ring gathers whatever rows the
+// lanes hold (fill() shuffles each lane's row), so lanes of a wave need not hold neighbouring rows.  Per row the
+// arithmetic is the static kernel's operation for operation (BfgsFlat is its flat state machine), so every output is
+// bitwise the same; the final Euler scan runs in insite_refine_final_kernel from the written coefficients.
+#ifndef INSITE_REFINE_DYN
+#define INSITE_REFINE_DYN 1
+#endif
+#ifndef INSITE_REFINE_DYN_REFILL
+#define INSITE_REFINE_DYN_REFILL 8
+#endif
+
+// jax minimize_bfgs + line_search + _zoom as the per-lane flat state machine of insite_refine_kernel (FLAT), its state
+// in one struct so a lane can restart it on a new row
+template <int M, bool kHL, int RU, class Lane>
+struct BfgsFlat {
+  HMat<M, kHL> H;
+  double x[M], g[M], pk[M], g_star[M];
+  double f, old_old, phi0, dphi0, a_i1, phi_i1, dphi_i1, a_star, phi_star;
+  double a_lo, phi_lo, dphi_lo, a_hi, phi_hi, dphi_hi, a_rec, phi_rec, za, zphi, t_trial;
+  int li, zj, k, ls_status;
+  bool ls_failed, in_zoom, z_failed, converged, failed;
+  __device__ void begin_ls(const Lane& ln) {
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      double s_ = 0.0;
+#pragma unroll RU
+      for (int j = 0; j < M; ++j) s_ += H.at(i, j) * g[j];
+      pk[i] = -s_;
+    }
+    phi0 = f;
+    dphi0 = ln.dot(g, pk);
+    const double cand = 1.01 * 2.0 * (phi0 - old_old) / dphi0;
+    t_trial = cand > 1.0 ? 1.0 : cand;
+    li = 1;
+    a_i1 = 0.0;
+    phi_i1 = phi0;
+    dphi_i1 = dphi0;
+    a_star = 0.0;
+    phi_star = phi0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) g_star[i] = g[i];
+    ls_failed = false;
+    in_zoom = false;
+  }
+  __device__ void zoom_top() {
+    const double dalpha = a_hi - a_lo;
+    const double lo = fmin(a_hi, a_lo), hi = fmax(a_hi, a_lo);
+    const double cchk = 0.2 * dalpha, qchk = 0.1 * dalpha;
+    z_failed = z_failed || (dalpha <= 1e-10);
+    const double a_cub = cubicmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi, a_rec, phi_rec);
+    const bool use_cubic = (zj > 0) && (a_cub > lo + cchk) && (a_cub < hi - cchk);
+    const double a_quad = quadmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi);
+    const bool use_quad = !use_cubic && (a_quad > lo + qchk) && (a_quad < hi - qchk);
+    double a_j = a_rec;
+    if (use_cubic) a_j = a_cub;
+    if (use_quad) a_j = a_quad;
+    if (!use_cubic && !use_quad) a_j = (a_lo + a_hi) / 2.0;
+    t_trial = a_j;
+  }
+  // the first evaluation s, gs (at c0, norm 1) -> minimize_bfgs's initial state; returns whether a trial is pending
+  __device__ bool start(double s, const double (&gs)[M], Lane& ln, int maxiter) {
+    ln.norm = s * 2.5;
+    f = s / ln.norm + 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) g[i] = gs[i] / ln.norm + 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i)
+#pragma unroll RU
+      for (int j = 0; j < M; ++j) H.at(i, j) = i == j ? 1.0 : 0.0;
+    double gmax = 0.0, g2 = 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      gmax = fmax(gmax, fabs(g[i]));
+      g2 += g[i] * g[i];
+    }
+    converged = gmax < 1e-5;
+    failed = false;
+    old_old = f + sqrt(g2) / 2.0;
+    ls_status = 0;
+    k = 0;
+    const bool pending = !converged && k < maxiter;
+    if (pending) begin_ls(ln);
+    return pending;
+  }
+  // one trial's value / slope / gradient -> the next state (insite_refine_kernel's FLAT loop body); returns pending
+  __device__ bool advance(double phi_t, double dphi_t, const double (&g_t)[M], const Lane& ln, int maxiter) {
+    bool ls_end = false, ls_done = false;
+    if (!in_zoom) {
+      const double a_i = t_trial;
+      const bool s_z1 = (phi_t > phi0 + 1e-4 * a_i * dphi0) || ((phi_t >= phi_i1) && (li > 1));
+      const bool s_i = (fabs(dphi_t) <= -0.9 * dphi0) && !s_z1;
+      const bool s_z2 = (dphi_t >= 0.0) && !s_z1 && !s_i;
+      if (s_i) {
+        a_star = a_i;
+        phi_star = phi_t;
+#pragma unroll RU
+        for (int i = 0; i < M; ++i) g_star[i] = g_t[i];
+      }
+      if (s_z1 || s_z2) {
+        if (s_z1) {
+          a_lo = a_i1; phi_lo = phi_i1; dphi_lo = dphi_i1;
+          a_hi = a_i; phi_hi = phi_t; dphi_hi = dphi_t;
+        } else {
+          a_lo = a_i; phi_lo = phi_t; dphi_lo = dphi_t;
+          a_hi = a_i1; phi_hi = phi_i1; dphi_hi = dphi_i1;
+        }
+        zj = 0;
+        z_failed = false;
+        a_rec = (a_lo + a_hi) / 2.0;
+        phi_rec = (phi_lo + phi_hi) / 2.0;
+        za = 1.0;
+        zphi = phi_lo;
+#pragma unroll RU
+        for (int i = 0; i < M; ++i) g_star[i] = g[i];
+        in_zoom = true;
+      }
+      ++li;
+      a_i1 = a_i;
+      phi_i1 = phi_t;
+      dphi_i1 = dphi_t;
+      if (in_zoom) {
+        zoom_top();
+      } else if (s_i) {
+        ls_end = ls_done = true;
+      } else if (li > 10) {
+        ls_end = true;
+      } else {
+        t_trial = a_i1 * 2.0;
+      }
+    } else {
+      const double a_j = t_trial;
+      const bool hi_to_j = (phi_t > phi0 + 1e-4 * a_j * dphi0) || (phi_t >= phi_lo);
+      const bool star_to_j = (fabs(dphi_t) <= -0.9 * dphi0) && !hi_to_j;
+      const bool hi_to_lo = (dphi_t * (a_hi - a_lo) >= 0.0) && !hi_to_j && !star_to_j;
+      const bool lo_to_j = !hi_to_j && !star_to_j;
+      if (hi_to_j) {
+        a_rec = a_hi;
+        phi_rec = phi_hi;
+        a_hi = a_j;
+        phi_hi = phi_t;
+        dphi_hi = dphi_t;
+      }
+      if (star_to_j) {
+        za = a_j;
+        zphi = phi_t;
+#pragma unroll RU
+        for (int i = 0; i < M; ++i) g_star[i] = g_t[i];
+      }
+      if (hi_to_lo) {
+        a_rec = a_hi;
+        phi_rec = phi_hi;
+        a_hi = a_lo;
+        phi_hi = phi_lo;
+        dphi_hi = dphi_lo;
+      }
+      if (lo_to_j) {
+        a_rec = a_lo;
+        phi_rec = phi_lo;
+        a_lo = a_j;
+        phi_lo = phi_t;
+        dphi_lo = dphi_t;
+      }
+      ++zj;
+      z_failed = ((z_failed ? 1 : 0) | zj) >= 30;  // jax: `failed | j >= 30` (no parentheses)
+      if (star_to_j || z_failed) {
+        a_star = za;
+        phi_star = zphi;
+        ls_failed = ls_failed || z_failed;
+        ls_end = ls_done = true;
+      } else {
+        zoom_top();
+      }
+    }
+    if (!ls_end) return true;
+    ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
+    failed = ls_failed || !ls_done;
+    double sk[M], yk[M];
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      sk[i] = a_star * pk[i];
+      yk[i] = g_star[i] - g[i];
+    }
+    const double rho = 1.0 / ln.dot(yk, sk);
+    if (isfinite(rho) && (RU == 1 || INSITE_REFINE_QUAD)) {
+      double hy[M];
+      double yhy = 0.0;
+#pragma unroll RU
+      for (int i = 0; i < M; ++i) {
+        double t = 0.0;
+#pragma unroll RU
+        for (int j = 0; j < M; ++j) t += H.at(i, j) * yk[j];
+        hy[i] = t;
+        yhy += yk[i] * t;
+      }
+      const double cs = rho * rho * yhy + rho;
+#pragma unroll RU
+      for (int i = 0; i < M; ++i)
+#pragma unroll RU
+        for (int j = 0; j < M; ++j)
+          H.at(i, j) = H.at(i, j) - rho * (sk[i] * hy[j] + hy[i] * sk[j]) + cs * (sk[i] * sk[j]);
+    } else if (isfinite(rho)) {
+      auto w = [&](int i, int q) { return (i == q ? 1.0 : 0.0) - rho * (sk[i] * yk[q]); };
+      double WH[M][M];
+#pragma unroll RU
+      for (int i = 0; i < M; ++i)
+#pragma unroll RU
+        for (int j = 0; j < M; ++j) {
+          double s_ = 0.0;
+#pragma unroll RU
+          for (int q = 0; q < M; ++q) s_ += w(i, q) * H.at(q, j);
+          WH[i][j] = s_;
+        }
+#pragma unroll RU
+      for (int i = 0; i < M; ++i)
+#pragma unroll RU
+        for (int j = 0; j < M; ++j) {
+          double s_ = 0.0;
+#pragma unroll RU
+          for (int q = 0; q < M; ++q) s_ += WH[i][q] * w(j, q);
+          H.at(i, j) = s_ + rho * (sk[i] * sk[j]);
+        }
+    }
+    double gm = 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      x[i] = x[i] + sk[i];
+      g[i] = g_star[i];
+      gm = fmax(gm, fabs(g[i]));
+    }
+    converged = gm < 1e-5;
+    old_old = f;
+    f = phi_star;
+    ++k;
+    const bool pending = !converged && !failed && k < maxiter;
+    if (pending) begin_ls(ln);
+    return pending;
+  }
+};
+
+template <int M>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_REFINE_WPE4)))
+insite_refine_dyn_kernel(RefineArgs ra, int64_t rows_per_block) {
+  constexpr int NA = 2, D = 1;
+  using Lane = RefineLane<M, NA, D, true, true>;
+  constexpr int RU = Lane::RU;
+  constexpr bool kHL = INSITE_REFINE_HLDS && RU == M && M <= 4;
+  __shared__ double sH[(kHL ? M * M : 1) * kBlock];
+  __shared__ double sV[kWavesPerBlock * 2 * kWin * kWave];
+  __shared__ unsigned s_next;  // the block's next unclaimed row, relative to r_lo
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t r_lo = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r_hi = min(ra.N, r_lo + rows_per_block);
+  if (threadIdx.x == 0) s_next = 0u;
+  __syncthreads();
+  if (r_lo >= r_hi) return;  // (block-uniform)
+  auto row_of = [&](int64_t q) -> int64_t { return ra.order ? (int64_t)ra.order[q] : q; };
+  Lane ln{ra, row_of(r_lo), 0, 1.0, {}, {}};  // an idle lane keeps a valid row for the ring's gathers
+  ln.win = sV + (threadIdx.x / kWave) * (2 * kWin * kWave);
+#pragma unroll RU
+  for (int i = 0; i < M; ++i) {
+    ln.c0a[i] = i < ra.m ? ra.c0[ra.t_flat[i]] : 0.0;
+    ln.mono[i] = 0.0;
+  }
+  BfgsFlat<M, kHL, RU, Lane> B;
+  if constexpr (kHL) B.H.base = sH + threadIdx.x;
+  B.t_trial = 0.0;
+#pragma unroll RU
+  for (int i = 0; i < M; ++i) B.x[i] = B.pk[i] = 0.0;
+  const int maxiter = 200 * ra.n_coef;
+  bool has = false, exhausted = false, pending = false, fresh = false;
+  // a finished row: coefficients (every q: the refined value if active, else the global one), status, iterations
+  auto finish = [&](int status, int nit) {
+    const int64_t p = ln.p;
+    if (status == 3 && ra.revert3) {  // zoom failed: the reference code keeps the global coefficients (sindy.py:628-631)
+#pragma unroll RU
+      for (int i = 0; i < M; ++i) B.x[i] = ln.c0a[i];
+    }
+    for (int q = 0; q < ra.n_coef; ++q) {
+      double c = ra.c0[q];
+#pragma unroll RU
+      for (int i = 0; i < M; ++i)
+        if (i < ra.m && ra.t_flat[i] == q) c = B.x[i];
+      ra.coef_out[p * ra.n_coef + q] = c;
+    }
+    if (ra.status) ra.status[p] = status;
+    if (ra.iters) ra.iters[p] = nit;
+    if (ra.nfev) ra.nfev[p] = ln.nev;
+    has = pending = false;
+  };
+  // wave-uniform: the idle lanes take the block's next rows (one LDS atomic for the wave)
+  auto claim = [&]() {
+    const uint64_t want = __builtin_amdgcn_ballot_w64(!has && !exhausted);
+    if (want == 0ull) return;
+    const int leader = __ffsll((unsigned long long)want) - 1;
+    unsigned base = 0u;
+    if (lane == leader) base = atomicAdd(&s_next, (unsigned)__popcll(want));
+    base = __shfl(base, leader);
+    if (has || exhausted) return;
+    const int64_t q = r_lo + (int64_t)base + __popcll(want & ((1ull << lane) - 1ull));
+    if (q >= r_hi) {
+      exhausted = true;
+      return;
+    }
+    const int64_t p = row_of(q);
+    ln.p = p;
+    ln.nev = 0;
+    double uu[INSITE_MAX_STATICS];
+#pragma unroll
+    for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < ra.U ? ra.u[p * ra.U + t] : 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) ln.mono[i] = i < ra.m ? monomial_code(ra.t_ucode[i], uu) : 0.0;
+    uint64_t am = 0ull;
+    for (int k = 0; k < ra.T; ++k) am |= (uint64_t)(ra.arm8[p * ra.lda + k] != 0 ? 1 : 0) << k;
+    ln.am = am;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      B.x[i] = ln.c0a[i];
+      B.pk[i] = 0.0;
+    }
+    B.t_trial = 0.0;
+    B.k = 0;
+    has = true;
+    const int sl = ra.sl[p];
+    if (sl > ra.tau && ra.T >= 2) {
+      ln.K = min(sl - ra.tau, ra.T - 1);
+      ln.norm = 1.0;
+      pending = fresh = true;
+    } else {
+      ln.K = 0;
+      finish(-1, 0);
+    }
+  };
+  claim();
+  while (__builtin_amdgcn_ballot_w64(has || !exhausted) != 0ull) {
+    double dphi_t, g_t[M];
+    // a fresh row evaluates at c0 itself (t 0, direction 0: x + 0 * 0 is x bit for bit), the others their trial
+    const double phi_t = ln.phi(B.x, B.pk, B.t_trial, dphi_t, g_t, pending);
+    if (pending) {
+      bool more;
+      if (fresh) {
+        more = B.start(phi_t, g_t, ln, maxiter);
+        fresh = false;
+      } else {
+        more = B.advance(phi_t, dphi_t, g_t, ln, maxiter);
+      }
+      if (!more)
+        finish(B.converged ? 0 : (B.k == maxiter ? 1 : (B.failed ? 2 + B.ls_status : -1)), B.k);
+    }
+    const uint64_t idle = __builtin_amdgcn_ballot_w64(!has && !exhausted);
+    if (idle != 0ull && (__popcll(idle) >= INSITE_REFINE_DYN_REFILL || __builtin_amdgcn_ballot_w64(pending) == 0ull))
+      claim();
+  }
+}
+
+// The final Euler scan of the row layout from the refined coefficients insite_refine_dyn_kernel wrote (sindy.py:668):
+// insite_refine_kernel's final scan, operation for operation, on identity rows (a wave's 64 rows are contiguous),
+// the predictions leaving through the same LDS staging as 64-B row segments.
+template <int M>
+__global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs ra) {
+  constexpr int NA = 2, D = 1;
+  __shared__ double sV[kWavesPerBlock * kWin * kWave];
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t p0 = gid - lane;
+  if (p0 >= ra.N) return;  // (wave-uniform)
+  const bool valid = gid < ra.N;
+  const int64_t p = valid ? gid : ra.N - 1;
+  double* st = sV + (threadIdx.x / kWave) * (kWin * kWave);
+  double uu[INSITE_MAX_STATICS];
+#pragma unroll
+  for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < ra.U ? ra.u[p * ra.U + t] : 0.0;
+  double gam[NA][D + 1];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int e = 0; e <= D; ++e) gam[a][e] = 0.0;
+  for (int q = 0; q < ra.n_coef; ++q) {
+    const int code = ra.q_code[q], mk = ra.q_mask[q], ex = code >> 24;
+    const double t = ra.coef_out[p * ra.n_coef + q] * monomial_code(code & 0xffffff, uu);
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+      if ((mk >> a) & 1)
+#pragma unroll
+        for (int e = 0; e <= D; ++e)
+          if (ex == e) gam[a][e] += t;
+  }
+  uint64_t am = 0ull;
+  for (int k = 0; k < ra.T; ++k) am |= (uint64_t)(ra.arm8[p * ra.lda + k] != 0 ? 1 : 0) << k;
+  const double h = ra.dt / (double)ra.sub;
+  double y = ra.V[p * ra.ldv];
+  for (int k = 0; k < ra.T; ++k) {
+    const int ak = (int)((am >> k) & 1ull);
+    double gk[D + 1];
+#pragma unroll
+    for (int e = 0; e <= D; ++e) gk[e] = gam[0][e];
+#pragma unroll
+    for (int a = 1; a < NA; ++a)
+      if (ak == a)
+#pragma unroll
+        for (int e = 0; e <= D; ++e) gk[e] = gam[a][e];
+    for (int s = 0; s < ra.sub; ++s) y = y + h * (gk[0] + gk[1] * y);
+    st[pm_slot_index(lane, k & (kWin - 1))] = y;
+    if ((k & (kWin - 1)) == kWin - 1 || k == ra.T - 1) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int m = lane >> 2, pk = ((lane & 3) + (m >> 2)) & 3;
+      const int col = (k & ~(kWin - 1)) + 2 * pk;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t r = p0 + 16 * q + m;
+        const double2 v = *reinterpret_cast<const double2*>(st + q * 128 + m * 8 + (lane & 3) * 2);
+        if (r < ra.N && col < ra.T) {
+          double* dst = ra.preds + r * ra.ldp + col;
+          if (col + 1 < ra.T && ra.st16) {
+            *reinterpret_cast<double2*>(dst) = v;
+          } else {
+            dst[0] = v.x;
+            if (col + 1 < ra.T) dst[1] = v.y;
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  }
+}
+
 template <int NA, int D>
 void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
   const int m = ra.m;
@@ -1032,6 +1467,23 @@ void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
                    ra.ldv % 2 == 0 && ((uintptr_t)ra.V & 15u) == 0;
   if constexpr (D == 1 && NA == 2) {
     if (ra.pm) {  // insite_refine_rows_f64 checked m <= 3, T <= 64, the 16-B alignment of V
+      const char* dv = getenv("INSITE_REFINE_DYN");
+      if (INSITE_REFINE_DYN && ra.coef_out && !(dv && dv[0] == '0')) {
+        // rows per block: ~2.5 rounds of resident blocks (3 per CU at 3 waves / SIMD), whole waves; override
+        // INSITE_REFINE_DYN_RPB
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        int64_t rpb = (ra.N + (int64_t)cus * 3 * 5 / 2 - 1) / ((int64_t)cus * 3 * 5 / 2);
+        rpb = (rpb + kBlock - 1) / kBlock * kBlock;
+        const char* rv = getenv("INSITE_REFINE_DYN_RPB");
+        if (rv && atoll(rv) > 0) rpb = atoll(rv);
+        if (rpb < kBlock) rpb = kBlock;
+        const dim3 gd((unsigned)((ra.N + rpb - 1) / rpb));
+        if (m <= 2) insite_refine_dyn_kernel<2><<<gd, kBlock, 0, hs>>>(ra, rpb);
+        else insite_refine_dyn_kernel<3><<<gd, kBlock, 0, hs>>>(ra, rpb);
+        insite_refine_final_kernel<2><<<grid, kBlock, 0, hs>>>(ra);
+        return;
+      }
       if (m <= 2) insite_refine_kernel<2, NA, D, true, true><<<grid, kBlock, 0, hs>>>(ra);
       else insite_refine_kernel<3, NA, D, true, true><<<grid, kBlock, 0, hs>>>(ra);
       return;

@@ -447,3 +447,36 @@ def test_plugin_insite_rejects_non_finite_refined_predictions(dev, model, monkey
     monkeypatch.setattr(S.ops, "insite_refine", blown)
     with pytest.raises(AssertionError, match="NaN or Inf"):
         m.get_predictions(coll["test_cf_one_step"])
+
+
+@pytest.mark.parametrize("N,T,m,rpb", [(20_000, 60, 3, None), (5_000, 60, 2, "256"), (777, 33, 3, "512"),
+                                       (130, 8, 3, None)])
+def test_refine_rows_dynamic_assignment_equals_static(dev, monkeypatch, N, T, m, rpb):
+    """insite_refine_rows_f64's dynamic lane -> row assignment (lanes take the next row of their block's range from an
+    LDS counter when theirs is done; the final scan in its own kernel from the written coefficients) against the
+    static one-row-per-lane kernel (INSITE_REFINE_DYN=0): every output bitwise equal, incl. rows <= tau (finished at
+    claim), ragged block ranges (rows per block 256 / 512 / the default) and a partial last block."""
+    from insite_amd import cohort, ops
+    coh = cohort.synthetic_pkpd(N, T, seed=N + 3 * T, device=dev, equation="EQ_4_C")
+    V = coh.x[:, :T].contiguous()
+    g = torch.Generator(device=dev)
+    g.manual_seed(N + T)
+    flip = torch.randint(1, max(2, T), (N, 1), generator=g, device=dev)
+    arm = torch.where(torch.arange(T, device=dev)[None, :] >= flip, 1 - coh.arm[:, None].to(torch.int64),
+                      coh.arm[:, None].to(torch.int64)).to(torch.int8).contiguous()
+    sl = torch.randint(1, T + 1, (N,), generator=g, device=dev, dtype=torch.int32)
+    c0 = np.zeros((2, coh.lib.n_terms))
+    c0[0, 4], c0[1, 1] = -1.1107592869834308, -0.14540553723951796
+    if m == 3:
+        c0[1, 5] = -1.0234639833519243
+    if rpb is not None:
+        monkeypatch.setenv("INSITE_REFINE_DYN_RPB", rpb)
+    outs = {}
+    for dyn in ("1", "0"):
+        monkeypatch.setenv("INSITE_REFINE_DYN", dyn)
+        nf = torch.empty((N,), dtype=torch.int32, device=dev)
+        r = ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5, nfev=nf, rows=True)
+        torch.cuda.synchronize()
+        outs[dyn] = tuple(t.clone() for t in r) + (nf,)
+    for a, b in zip(outs["1"], outs["0"]):
+        assert torch.equal(a, b)
