@@ -1472,7 +1472,8 @@ void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
         // rows per block: ~2.5 rounds of resident blocks (3 per CU at 3 waves / SIMD), whole waves; override
         // INSITE_REFINE_DYN_RPB
         int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+          cus = 256;
         int64_t rpb = (ra.N + (int64_t)cus * 3 * 5 / 2 - 1) / ((int64_t)cus * 3 * 5 / 2);
         rpb = (rpb + kBlock - 1) / kBlock * kBlock;
         const char* rv = getenv("INSITE_REFINE_DYN_RPB");
