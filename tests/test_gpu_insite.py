@@ -449,7 +449,7 @@ def test_plugin_insite_rejects_non_finite_refined_predictions(dev, model, monkey
         m.get_predictions(coll["test_cf_one_step"])
 
 
-@pytest.mark.parametrize("N,T,m,rpb", [(20_000, 60, 3, None), (5_000, 60, 2, "256"), (777, 33, 3, "512"),
+@pytest.mark.parametrize("N,T,m,rpb", [(20_000, 60, 3, None), (5_000, 60, 2, "256"), (777, 34, 3, "512"),
                                        (130, 8, 3, None)])
 def test_refine_rows_dynamic_assignment_equals_static(dev, monkeypatch, N, T, m, rpb):
     """insite_refine_rows_f64's dynamic lane -> row assignment (lanes take the next row of their block's range from an
