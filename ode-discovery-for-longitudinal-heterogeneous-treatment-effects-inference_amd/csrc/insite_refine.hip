@@ -1274,7 +1274,7 @@ struct BfgsFlat {
 
 template <int M>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_REFINE_WPE4)))
-insite_refine_dyn_kernel(RefineArgs ra, int64_t rows_per_block) {
+insite_refine_dyn_kernel(RefineArgs ra, int64_t rows_per_block, int refill) {
   constexpr int NA = 2, D = 1;
   using Lane = RefineLane<M, NA, D, true, true>;
   constexpr int RU = Lane::RU;
@@ -1382,7 +1382,7 @@ insite_refine_dyn_kernel(RefineArgs ra, int64_t rows_per_block) {
         finish(B.converged ? 0 : (B.k == maxiter ? 1 : (B.failed ? 2 + B.ls_status : -1)), B.k);
     }
     const uint64_t idle = __builtin_amdgcn_ballot_w64(!has && !exhausted);
-    if (idle != 0ull && (__popcll(idle) >= INSITE_REFINE_DYN_REFILL || __builtin_amdgcn_ballot_w64(pending) == 0ull))
+    if (idle != 0ull && (__popcll(idle) >= refill || __builtin_amdgcn_ballot_w64(pending) == 0ull))
       claim();
   }
 }
@@ -1480,8 +1480,10 @@ void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
         if (rv && atoll(rv) > 0) rpb = atoll(rv);
         if (rpb < kBlock) rpb = kBlock;
         const dim3 gd((unsigned)((ra.N + rpb - 1) / rpb));
-        if (m <= 2) insite_refine_dyn_kernel<2><<<gd, kBlock, 0, hs>>>(ra, rpb);
-        else insite_refine_dyn_kernel<3><<<gd, kBlock, 0, hs>>>(ra, rpb);
+        const char* fv = getenv("INSITE_REFINE_DYN_REFILL");
+        const int refill = fv && atoi(fv) > 0 ? atoi(fv) : INSITE_REFINE_DYN_REFILL;
+        if (m <= 2) insite_refine_dyn_kernel<2><<<gd, kBlock, 0, hs>>>(ra, rpb, refill);
+        else insite_refine_dyn_kernel<3><<<gd, kBlock, 0, hs>>>(ra, rpb, refill);
         insite_refine_final_kernel<2><<<grid, kBlock, 0, hs>>>(ra);
         return;
       }
