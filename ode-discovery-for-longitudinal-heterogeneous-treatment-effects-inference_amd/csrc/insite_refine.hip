@@ -1388,19 +1388,41 @@ insite_refine_dyn_kernel(RefineArgs ra, int64_t rows_per_block, int refill) {
 }
 
 // The final Euler scan of the row layout from the refined coefficients insite_refine_dyn_kernel wrote (sindy.py:668):
-// insite_refine_kernel's final scan, operation for operation, on identity rows (a wave's 64 rows are contiguous),
-// the predictions leaving through the same LDS staging as 64-B row segments.
+// insite_refine_kernel's final scan, operation for operation, on identity rows (a wave's 64 rows are contiguous).  A
+// wave stages its rows' coefficients and arm bytes in LDS with coalesced loads first (64 rows x n_coef doubles and
+// 64 x lda bytes are contiguous runs; lane-per-row loads of them touched 64 lines per instruction and fetched 2 GB
+// per launch for ~0.2 GB of data), and the predictions leave through the same staging as 64-B row segments.
+constexpr int kFinalMaxCoef = 16;  // coefficients staged per row (larger models read theirs per lane)
 template <int M>
-__global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs ra) {
+__global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs ra, int staged_arm) {
   constexpr int NA = 2, D = 1;
-  __shared__ double sV[kWavesPerBlock * kWin * kWave];
+  // per wave: [64 x kFinalMaxCoef doubles | 64 x 64 arm bytes], its first 4 KB reused as the prediction staging once
+  // the coefficients and arms are in registers (48 KB per block: 3 blocks per CU)
+  constexpr int kWaveLds = kWave * kFinalMaxCoef * 8 + kWave * 64;
+  __shared__ __attribute__((aligned(16))) uint8_t sL[kWavesPerBlock * kWaveLds];
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int lane = threadIdx.x & (kWave - 1);
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const int64_t p0 = gid - lane;
   if (p0 >= ra.N) return;  // (wave-uniform)
   const bool valid = gid < ra.N;
   const int64_t p = valid ? gid : ra.N - 1;
-  double* st = sV + (threadIdx.x / kWave) * (kWin * kWave);
+  const int nrow = ra.N - p0 < kWave ? (int)(ra.N - p0) : kWave;
+  double* st = reinterpret_cast<double*>(sL + wv * kWaveLds);
+  const bool stage_c = ra.n_coef <= kFinalMaxCoef;
+  double* sc = st;
+  uint32_t* sa = reinterpret_cast<uint32_t*>(sL + wv * kWaveLds + kWave * kFinalMaxCoef * 8);
+  if (stage_c) {
+    const double* src = ra.coef_out + p0 * ra.n_coef;
+    const int cnt = nrow * ra.n_coef;
+    for (int i = lane; i < cnt; i += kWave) sc[i] = src[i];
+  }
+  if (staged_arm) {  // lda % 4 == 0, 4-byte aligned rows, T <= 64
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(ra.arm8 + p0 * ra.lda);
+    const int cnt = nrow * (int)(ra.lda / 4);
+    for (int i = lane; i < cnt; i += kWave) sa[i] = src[i];
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
   double uu[INSITE_MAX_STATICS];
 #pragma unroll
   for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < ra.U ? ra.u[p * ra.U + t] : 0.0;
@@ -1409,9 +1431,11 @@ __global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs 
   for (int a = 0; a < NA; ++a)
 #pragma unroll
     for (int e = 0; e <= D; ++e) gam[a][e] = 0.0;
+  const int lr = valid ? lane : nrow - 1;
   for (int q = 0; q < ra.n_coef; ++q) {
     const int code = ra.q_code[q], mk = ra.q_mask[q], ex = code >> 24;
-    const double t = ra.coef_out[p * ra.n_coef + q] * monomial_code(code & 0xffffff, uu);
+    const double c = stage_c ? sc[lr * ra.n_coef + q] : ra.coef_out[p * ra.n_coef + q];
+    const double t = c * monomial_code(code & 0xffffff, uu);
 #pragma unroll
     for (int a = 0; a < NA; ++a)
       if ((mk >> a) & 1)
@@ -1420,9 +1444,16 @@ __global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs 
           if (ex == e) gam[a][e] += t;
   }
   uint64_t am = 0ull;
-  for (int k = 0; k < ra.T; ++k) am |= (uint64_t)(ra.arm8[p * ra.lda + k] != 0 ? 1 : 0) << k;
+  if (staged_arm) {
+    const uint8_t* row = reinterpret_cast<const uint8_t*>(sa) + lr * ra.lda;
+    for (int k = 0; k < ra.T; ++k) am |= (uint64_t)(row[k] != 0 ? 1 : 0) << k;
+  } else {
+    for (int k = 0; k < ra.T; ++k) am |= (uint64_t)(ra.arm8[p * ra.lda + k] != 0 ? 1 : 0) << k;
+  }
   const double h = ra.dt / (double)ra.sub;
   double y = ra.V[p * ra.ldv];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's staged reads done before the staging reuse
+  __builtin_amdgcn_wave_barrier();
   for (int k = 0; k < ra.T; ++k) {
     const int ak = (int)((am >> k) & 1ull);
     double gk[D + 1];
@@ -1484,7 +1515,8 @@ void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
         const int refill = fv && atoi(fv) > 0 ? atoi(fv) : INSITE_REFINE_DYN_REFILL;
         if (m <= 2) insite_refine_dyn_kernel<2><<<gd, kBlock, 0, hs>>>(ra, rpb, refill);
         else insite_refine_dyn_kernel<3><<<gd, kBlock, 0, hs>>>(ra, rpb, refill);
-        insite_refine_final_kernel<2><<<grid, kBlock, 0, hs>>>(ra);
+        const int staged_arm = (ra.lda % 4 == 0) && (((uintptr_t)ra.arm8 & 3u) == 0) && ra.lda <= 64;
+        insite_refine_final_kernel<2><<<grid, kBlock, 0, hs>>>(ra, staged_arm);
         return;
       }
       if (m <= 2) insite_refine_kernel<2, NA, D, true, true><<<grid, kBlock, 0, hs>>>(ra);
