@@ -1345,7 +1345,17 @@ insite_refine_dyn_kernel(RefineArgs ra, int64_t rows_per_block, int refill) {
 #pragma unroll RU
     for (int i = 0; i < M; ++i) ln.mono[i] = i < ra.m ? monomial_code(ra.t_ucode[i], uu) : 0.0;
     uint64_t am = 0ull;
-    for (int k = 0; k < ra.T; ++k) am |= (uint64_t)(ra.arm8[p * ra.lda + k] != 0 ? 1 : 0) << k;
+    if ((ra.lda & 3) == 0 && ((uintptr_t)ra.arm8 & 3u) == 0) {  // the row's arm bytes as words (lda >= T)
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(ra.arm8 + p * ra.lda);
+      for (int j = 0; 4 * j < ra.T; ++j) {
+        const uint32_t v = w[j];
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if (4 * j + b < ra.T) am |= (uint64_t)(((v >> (8 * b)) & 0xffu) != 0u ? 1 : 0) << (4 * j + b);
+      }
+    } else {
+      for (int k = 0; k < ra.T; ++k) am |= (uint64_t)(ra.arm8[p * ra.lda + k] != 0 ? 1 : 0) << k;
+    }
     ln.am = am;
 #pragma unroll RU
     for (int i = 0; i < M; ++i) {
