@@ -27,6 +27,7 @@
 // spills) vs rolled 62 ms; M = 36 rolled O(M^3) 1437 ms vs O(M^2) 108 ms; M = 8 5.5 ms.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -1028,15 +1029,18 @@ insite_refine_kernel(RefineArgs ra) {
 // Dynamic lane -> row assignment (row layout; INSITE_REFINE_DYN, runtime switch INSITE_REFINE_DYN=0 in the environment)
 // ------------------------------------------------------------------------------------------------------------------
 // With one row per lane a wave runs as long as its slowest row: rows binned by seq_len scan similar windows, but the
-// number of evaluations per row (BFGS iterations x line-search trials) still varies, and the static kernel's lanes
-// idle ~40 % of the wave's scans (bench.py INSITE line: divergence ratio 1.67).  Here a block owns a contiguous range
-// of rows_per_block lane-order rows (2-4 per lane) and its lanes take them from an LDS counter: a lane whose row is
-// done writes the row's coefficients / status / iterations / evaluation count and, once INSITE_REFINE_DYN_REFILL
-// lanes of its wave are idle (or none is busy), the wave claims that many rows with ONE LDS atomic and the new lanes
-// start with their first evaluation (at c0, norm 1) in the next scan.  The row layout's ring gathers whatever rows the
-// lanes hold (fill() shuffles each lane's row), so lanes of a wave need not hold neighbouring rows.  Per row the
-// arithmetic is the static kernel's operation for operation (BfgsFlat is its flat state machine), so every output is
-// bitwise the same; the final Euler scan runs in insite_refine_final_kernel from the written coefficients.
+// number of evaluations per row (BFGS iterations x line-search trials) still varies (mean 10, wave maximum 17.8 on the
+// INSITE bench: lanes idle ~40 % of the scans).  Here a persistent grid (the resident block count) takes rows from ONE
+// device-wide queue in lane order -- rows sorted by seq_len, longest first: waves claiming at the same time hold rows
+// of the same window length, and the cheapest rows come last (a longest-first schedule; per-block row ranges were
+// measured slower: with rows sorted by length the blocks' work differs by the window length, profiles/r04).  A lane
+// whose row is done writes the row's coefficients / status / iterations / evaluation count; once refill lanes of its
+// wave are idle (or none is busy) the wave claims that many rows with one atomic and the new lanes start with their
+// first evaluation (at c0, norm 1) in the next scan.  The row layout's ring gathers whatever rows the lanes hold
+// (fill() shuffles each lane's row), so lanes of a wave need not hold neighbouring rows.  Per row the arithmetic is the
+// static kernel's operation for operation (BfgsFlat is its flat state machine), so every output is bitwise the same;
+// the final Euler scan runs in insite_refine_final_kernel from the written coefficients.  The queue head is one of
+// kRefineQueues device words, zeroed on the stream before each launch (independent streams rotate through them).
 #ifndef INSITE_REFINE_DYN
 #define INSITE_REFINE_DYN 1
 #endif
@@ -1274,22 +1278,16 @@ struct BfgsFlat {
 
 template <int M>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_REFINE_WPE4)))
-insite_refine_dyn_kernel(RefineArgs ra, int64_t rows_per_block, int refill) {
+insite_refine_dyn_kernel(RefineArgs ra, unsigned* queue, int refill) {
   constexpr int NA = 2, D = 1;
   using Lane = RefineLane<M, NA, D, true, true>;
   constexpr int RU = Lane::RU;
   constexpr bool kHL = INSITE_REFINE_HLDS && RU == M && M <= 4;
   __shared__ double sH[(kHL ? M * M : 1) * kBlock];
   __shared__ double sV[kWavesPerBlock * 2 * kWin * kWave];
-  __shared__ unsigned s_next;  // the block's next unclaimed row, relative to r_lo
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t r_lo = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t r_hi = min(ra.N, r_lo + rows_per_block);
-  if (threadIdx.x == 0) s_next = 0u;
-  __syncthreads();
-  if (r_lo >= r_hi) return;  // (block-uniform)
   auto row_of = [&](int64_t q) -> int64_t { return ra.order ? (int64_t)ra.order[q] : q; };
-  Lane ln{ra, row_of(r_lo), 0, 1.0, {}, {}};  // an idle lane keeps a valid row for the ring's gathers
+  Lane ln{ra, row_of(0), 0, 1.0, {}, {}};  // an idle lane keeps a valid row for the ring's gathers
   ln.win = sV + (threadIdx.x / kWave) * (2 * kWin * kWave);
 #pragma unroll RU
   for (int i = 0; i < M; ++i) {
@@ -1328,11 +1326,11 @@ insite_refine_dyn_kernel(RefineArgs ra, int64_t rows_per_block, int refill) {
     if (want == 0ull) return;
     const int leader = __ffsll((unsigned long long)want) - 1;
     unsigned base = 0u;
-    if (lane == leader) base = atomicAdd(&s_next, (unsigned)__popcll(want));
+    if (lane == leader) base = atomicAdd(queue, (unsigned)__popcll(want));
     base = __shfl(base, leader);
     if (has || exhausted) return;
-    const int64_t q = r_lo + (int64_t)base + __popcll(want & ((1ull << lane) - 1ull));
-    if (q >= r_hi) {
+    const int64_t q = (int64_t)base + __popcll(want & ((1ull << lane) - 1ull));
+    if (q >= ra.N) {
       exhausted = true;
       return;
     }
@@ -1499,6 +1497,17 @@ __global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs 
   }
 }
 
+// The dynamic kernel's queue heads: device words handed out round-robin per launch (zeroed on the launch's stream
+// first); kRefineQueues launches may be in flight on independent streams at once.
+constexpr int kRefineQueues = 64;
+__device__ unsigned g_refine_queue[kRefineQueues];
+unsigned* refine_queue_slot() {
+  static std::atomic<unsigned> next{0};
+  void* base = nullptr;
+  if (hipGetSymbolAddress(&base, HIP_SYMBOL(g_refine_queue)) != hipSuccess || !base) return nullptr;
+  return static_cast<unsigned*>(base) + (next.fetch_add(1u) % kRefineQueues);
+}
+
 template <int NA, int D>
 void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
   const int m = ra.m;
@@ -1510,24 +1519,30 @@ void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
     if (ra.pm) {  // insite_refine_rows_f64 checked m <= 3, T <= 64, the 16-B alignment of V
       const char* dv = getenv("INSITE_REFINE_DYN");
       if (INSITE_REFINE_DYN && ra.coef_out && !(dv && dv[0] == '0')) {
-        // rows per block: ~2.5 rounds of resident blocks (3 per CU at 3 waves / SIMD), whole waves; override
-        // INSITE_REFINE_DYN_RPB
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        // a persistent grid: every resident block of the kernel (the occupancy query), capped by the row count
+        int dev = 0, cus = 256, per_cu = 3;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
           cus = 256;
-        int64_t rpb = (ra.N + (int64_t)cus * 3 * 5 / 2 - 1) / ((int64_t)cus * 3 * 5 / 2);
-        rpb = (rpb + kBlock - 1) / kBlock * kBlock;
-        const char* rv = getenv("INSITE_REFINE_DYN_RPB");
-        if (rv && atoll(rv) > 0) rpb = atoll(rv);
-        if (rpb < kBlock) rpb = kBlock;
-        const dim3 gd((unsigned)((ra.N + rpb - 1) / rpb));
-        const char* fv = getenv("INSITE_REFINE_DYN_REFILL");
-        const int refill = fv && atoi(fv) > 0 ? atoi(fv) : INSITE_REFINE_DYN_REFILL;
-        if (m <= 2) insite_refine_dyn_kernel<2><<<gd, kBlock, 0, hs>>>(ra, rpb, refill);
-        else insite_refine_dyn_kernel<3><<<gd, kBlock, 0, hs>>>(ra, rpb, refill);
-        const int staged_arm = (ra.lda % 4 == 0) && (((uintptr_t)ra.arm8 & 3u) == 0) && ra.lda <= 64;
-        insite_refine_final_kernel<2><<<grid, kBlock, 0, hs>>>(ra, staged_arm);
-        return;
+        hipError_t oe = m <= 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, insite_refine_dyn_kernel<2>, kBlock, 0)
+                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, insite_refine_dyn_kernel<3>, kBlock, 0);
+        if (oe != hipSuccess || per_cu < 1) per_cu = 3;
+        int64_t nb = (int64_t)cus * per_cu;
+        const char* gv = getenv("INSITE_REFINE_DYN_BLOCKS");
+        if (gv && atoll(gv) > 0) nb = atoll(gv);
+        const int64_t need = (ra.N + kBlock - 1) / kBlock;
+        if (nb > need) nb = need;
+        unsigned* queue = refine_queue_slot();
+        if (queue && hipMemsetAsync(queue, 0, sizeof(unsigned), hs) == hipSuccess) {  // else: the static kernel
+          const dim3 gd((unsigned)nb);
+          const char* fv = getenv("INSITE_REFINE_DYN_REFILL");
+          const int refill = fv && atoi(fv) > 0 ? atoi(fv) : INSITE_REFINE_DYN_REFILL;
+          if (m <= 2) insite_refine_dyn_kernel<2><<<gd, kBlock, 0, hs>>>(ra, queue, refill);
+          else insite_refine_dyn_kernel<3><<<gd, kBlock, 0, hs>>>(ra, queue, refill);
+          const int staged_arm = (ra.lda % 4 == 0) && (((uintptr_t)ra.arm8 & 3u) == 0) && ra.lda <= 64;
+          insite_refine_final_kernel<2><<<grid, kBlock, 0, hs>>>(ra, staged_arm);
+          return;
+        }
       }
       if (m <= 2) insite_refine_kernel<2, NA, D, true, true><<<grid, kBlock, 0, hs>>>(ra);
       else insite_refine_kernel<3, NA, D, true, true><<<grid, kBlock, 0, hs>>>(ra);
