@@ -1041,8 +1041,13 @@ insite_refine_kernel(RefineArgs ra) {
 // static kernel's operation for operation (BfgsFlat is its flat state machine), so every output is bitwise the same;
 // the final Euler scan runs in insite_refine_final_kernel from the written coefficients.  The queue head is one of
 // kRefineQueues device words, zeroed on the stream before each launch (independent streams rotate through them).
+// Measured (profiles/r04/dyn_sweep.txt, 1M rows): 2.25 ms per INSITE step against 2.16 for the static one-row-per-lane
+// kernel, refill thresholds 2-32 and 512-1536 blocks no better; per-block row ranges 2.13-10 ms.  The lanes' rows sit
+// at different BFGS phases, so every loop iteration issues the union of the start / line-search / zoom / update /
+// finish paths, which costs what the better lane occupancy saves.  Kept as a knob (INSITE_REFINE_DYN=1 in the
+// environment, or -DINSITE_REFINE_DYN=1), bitwise-tested against the static kernel.
 #ifndef INSITE_REFINE_DYN
-#define INSITE_REFINE_DYN 1
+#define INSITE_REFINE_DYN 0
 #endif
 #ifndef INSITE_REFINE_DYN_REFILL
 #define INSITE_REFINE_DYN_REFILL 8
@@ -1518,7 +1523,8 @@ void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
   if constexpr (D == 1 && NA == 2) {
     if (ra.pm) {  // insite_refine_rows_f64 checked m <= 3, T <= 64, the 16-B alignment of V
       const char* dv = getenv("INSITE_REFINE_DYN");
-      if (INSITE_REFINE_DYN && ra.coef_out && !(dv && dv[0] == '0')) {
+      const bool dyn = dv ? dv[0] == '1' : INSITE_REFINE_DYN != 0;
+      if (dyn && ra.coef_out) {
         // a persistent grid: every resident block of the kernel (the occupancy query), capped by the row count
         int dev = 0, cus = 256, per_cu = 3;
         if (hipGetDevice(&dev) != hipSuccess ||
