@@ -431,6 +431,234 @@ struct HMat<M, true> {
   __device__ __forceinline__ double& at(int i, int j) { return base[(i * M + j) * kBlock]; }
 };
 
+// jax minimize_bfgs + line_search + _zoom as a flat per-lane state machine (INSITE_REFINE_FLAT): its state in one
+// struct, advanced once per objective evaluation (insite_refine_kernel; insite_refine_dyn_kernel restarts it per row)
+template <int M, bool kHL, int RU, class Lane>
+struct BfgsFlat {
+  HMat<M, kHL> H;
+  double x[M], g[M], pk[M], g_star[M];
+  double f, old_old, phi0, dphi0, a_i1, phi_i1, dphi_i1, a_star, phi_star;
+  double a_lo, phi_lo, dphi_lo, a_hi, phi_hi, dphi_hi, a_rec, phi_rec, za, zphi, t_trial;
+  int li, zj, k, ls_status;
+  bool ls_failed, in_zoom, z_failed, converged, failed;
+  __device__ void begin_ls(const Lane& ln) {
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      double s_ = 0.0;
+#pragma unroll RU
+      for (int j = 0; j < M; ++j) s_ += H.at(i, j) * g[j];
+      pk[i] = -s_;
+    }
+    phi0 = f;
+    dphi0 = ln.dot(g, pk);
+    const double cand = 1.01 * 2.0 * (phi0 - old_old) / dphi0;
+    t_trial = cand > 1.0 ? 1.0 : cand;
+    li = 1;
+    a_i1 = 0.0;
+    phi_i1 = phi0;
+    dphi_i1 = dphi0;
+    a_star = 0.0;
+    phi_star = phi0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) g_star[i] = g[i];
+    ls_failed = false;
+    in_zoom = false;
+  }
+  __device__ void zoom_top() {
+    const double dalpha = a_hi - a_lo;
+    const double lo = fmin(a_hi, a_lo), hi = fmax(a_hi, a_lo);
+    const double cchk = 0.2 * dalpha, qchk = 0.1 * dalpha;
+    z_failed = z_failed || (dalpha <= 1e-10);
+    const double a_cub = cubicmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi, a_rec, phi_rec);
+    const bool use_cubic = (zj > 0) && (a_cub > lo + cchk) && (a_cub < hi - cchk);
+    const double a_quad = quadmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi);
+    const bool use_quad = !use_cubic && (a_quad > lo + qchk) && (a_quad < hi - qchk);
+    double a_j = a_rec;
+    if (use_cubic) a_j = a_cub;
+    if (use_quad) a_j = a_quad;
+    if (!use_cubic && !use_quad) a_j = (a_lo + a_hi) / 2.0;
+    t_trial = a_j;
+  }
+  // the first evaluation s, gs (at c0, norm 1) -> minimize_bfgs's initial state; returns whether a trial is pending
+  __device__ bool start(double s, const double (&gs)[M], Lane& ln, int maxiter) {
+    ln.norm = s * 2.5;
+    f = s / ln.norm + 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) g[i] = gs[i] / ln.norm + 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i)
+#pragma unroll RU
+      for (int j = 0; j < M; ++j) H.at(i, j) = i == j ? 1.0 : 0.0;
+    double gmax = 0.0, g2 = 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      gmax = fmax(gmax, fabs(g[i]));
+      g2 += g[i] * g[i];
+    }
+    converged = gmax < 1e-5;
+    failed = false;
+    old_old = f + sqrt(g2) / 2.0;
+    ls_status = 0;
+    k = 0;
+    const bool pending = !converged && k < maxiter;
+    if (pending) begin_ls(ln);
+    return pending;
+  }
+  // one trial's value / slope / gradient -> the next state (insite_refine_kernel's FLAT loop body); returns pending
+  __device__ bool advance(double phi_t, double dphi_t, const double (&g_t)[M], const Lane& ln, int maxiter) {
+    bool ls_end = false, ls_done = false;
+    if (!in_zoom) {
+      const double a_i = t_trial;
+      const bool s_z1 = (phi_t > phi0 + 1e-4 * a_i * dphi0) || ((phi_t >= phi_i1) && (li > 1));
+      const bool s_i = (fabs(dphi_t) <= -0.9 * dphi0) && !s_z1;
+      const bool s_z2 = (dphi_t >= 0.0) && !s_z1 && !s_i;
+      if (s_i) {
+        a_star = a_i;
+        phi_star = phi_t;
+#pragma unroll RU
+        for (int i = 0; i < M; ++i) g_star[i] = g_t[i];
+      }
+      if (s_z1 || s_z2) {
+        if (s_z1) {
+          a_lo = a_i1; phi_lo = phi_i1; dphi_lo = dphi_i1;
+          a_hi = a_i; phi_hi = phi_t; dphi_hi = dphi_t;
+        } else {
+          a_lo = a_i; phi_lo = phi_t; dphi_lo = dphi_t;
+          a_hi = a_i1; phi_hi = phi_i1; dphi_hi = dphi_i1;
+        }
+        zj = 0;
+        z_failed = false;
+        a_rec = (a_lo + a_hi) / 2.0;
+        phi_rec = (phi_lo + phi_hi) / 2.0;
+        za = 1.0;
+        zphi = phi_lo;
+#pragma unroll RU
+        for (int i = 0; i < M; ++i) g_star[i] = g[i];
+        in_zoom = true;
+      }
+      ++li;
+      a_i1 = a_i;
+      phi_i1 = phi_t;
+      dphi_i1 = dphi_t;
+      if (in_zoom) {
+        zoom_top();
+      } else if (s_i) {
+        ls_end = ls_done = true;
+      } else if (li > 10) {
+        ls_end = true;
+      } else {
+        t_trial = a_i1 * 2.0;
+      }
+    } else {
+      const double a_j = t_trial;
+      const bool hi_to_j = (phi_t > phi0 + 1e-4 * a_j * dphi0) || (phi_t >= phi_lo);
+      const bool star_to_j = (fabs(dphi_t) <= -0.9 * dphi0) && !hi_to_j;
+      const bool hi_to_lo = (dphi_t * (a_hi - a_lo) >= 0.0) && !hi_to_j && !star_to_j;
+      const bool lo_to_j = !hi_to_j && !star_to_j;
+      if (hi_to_j) {
+        a_rec = a_hi;
+        phi_rec = phi_hi;
+        a_hi = a_j;
+        phi_hi = phi_t;
+        dphi_hi = dphi_t;
+      }
+      if (star_to_j) {
+        za = a_j;
+        zphi = phi_t;
+#pragma unroll RU
+        for (int i = 0; i < M; ++i) g_star[i] = g_t[i];
+      }
+      if (hi_to_lo) {
+        a_rec = a_hi;
+        phi_rec = phi_hi;
+        a_hi = a_lo;
+        phi_hi = phi_lo;
+        dphi_hi = dphi_lo;
+      }
+      if (lo_to_j) {
+        a_rec = a_lo;
+        phi_rec = phi_lo;
+        a_lo = a_j;
+        phi_lo = phi_t;
+        dphi_lo = dphi_t;
+      }
+      ++zj;
+      z_failed = ((z_failed ? 1 : 0) | zj) >= 30;  // jax: `failed | j >= 30` (no parentheses)
+      if (star_to_j || z_failed) {
+        a_star = za;
+        phi_star = zphi;
+        ls_failed = ls_failed || z_failed;
+        ls_end = ls_done = true;
+      } else {
+        zoom_top();
+      }
+    }
+    if (!ls_end) return true;
+    ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
+    failed = ls_failed || !ls_done;
+    double sk[M], yk[M];
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      sk[i] = a_star * pk[i];
+      yk[i] = g_star[i] - g[i];
+    }
+    const double rho = 1.0 / ln.dot(yk, sk);
+    if (isfinite(rho) && (RU == 1 || INSITE_REFINE_QUAD)) {
+      double hy[M];
+      double yhy = 0.0;
+#pragma unroll RU
+      for (int i = 0; i < M; ++i) {
+        double t = 0.0;
+#pragma unroll RU
+        for (int j = 0; j < M; ++j) t += H.at(i, j) * yk[j];
+        hy[i] = t;
+        yhy += yk[i] * t;
+      }
+      const double cs = rho * rho * yhy + rho;
+#pragma unroll RU
+      for (int i = 0; i < M; ++i)
+#pragma unroll RU
+        for (int j = 0; j < M; ++j)
+          H.at(i, j) = H.at(i, j) - rho * (sk[i] * hy[j] + hy[i] * sk[j]) + cs * (sk[i] * sk[j]);
+    } else if (isfinite(rho)) {
+      auto w = [&](int i, int q) { return (i == q ? 1.0 : 0.0) - rho * (sk[i] * yk[q]); };
+      double WH[M][M];
+#pragma unroll RU
+      for (int i = 0; i < M; ++i)
+#pragma unroll RU
+        for (int j = 0; j < M; ++j) {
+          double s_ = 0.0;
+#pragma unroll RU
+          for (int q = 0; q < M; ++q) s_ += w(i, q) * H.at(q, j);
+          WH[i][j] = s_;
+        }
+#pragma unroll RU
+      for (int i = 0; i < M; ++i)
+#pragma unroll RU
+        for (int j = 0; j < M; ++j) {
+          double s_ = 0.0;
+#pragma unroll RU
+          for (int q = 0; q < M; ++q) s_ += WH[i][q] * w(j, q);
+          H.at(i, j) = s_ + rho * (sk[i] * sk[j]);
+        }
+    }
+    double gm = 0.0;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      x[i] = x[i] + sk[i];
+      g[i] = g_star[i];
+      gm = fmax(gm, fabs(g[i]));
+    }
+    converged = gm < 1e-5;
+    old_old = f;
+    f = phi_star;
+    ++k;
+    const bool pending = !converged && !failed && k < maxiter;
+    if (pending) begin_ls(ln);
+    return pending;
+  }
+};
+
 // M <= 4 with the affine RHS (the EQ_4 models: two terms per arm) is sized for INSITE_REFINE_WPE4 waves per
 // SIMD (<= 128 VGPRs; unconstrained the compiler takes 202 and runs 2 waves): the objective scan is a
 // dependent fp64 chain per lane, hidden only by other waves.
@@ -481,246 +709,35 @@ insite_refine_kernel(RefineArgs ra) {
   const bool refine = sl > ra.tau && ra.T >= 2;  // (WIN: every lane enters; the inert ones scan nothing)
   if (WIN || refine) {
     ln.K = refine ? min(sl - ra.tau, ra.T - 1) : 0;
+    BfgsFlat<M, kHL, RU, RefineLane<M, NA, D, WIN, PM>> B;
+    if constexpr (kHL) B.H.base = sH + threadIdx.x;
+#pragma unroll RU
+    for (int i = 0; i < M; ++i) {
+      B.x[i] = x[i];
+      B.pk[i] = 0.0;
+    }
+    B.t_trial = 0.0;
     double g[M];
-    const double start = ln.fg(x, g, refine);  // norm 1, penalty 0 at c0
-    ln.norm = start * 2.5;
     // jax evaluates f_to_min at c0 twice (start_res with norm_const = 1, then minimize's first value_and_grad with
     // norm_const = 2.5 start_res, sindy.py:591-627).  At c0 the penalty and its gradient are exactly zero, so the
     // second evaluation is the first divided by norm -- bitwise (fg's last operations are that one division plus
-    // +0.0) -- and its scan is not repeated.
-    double f = start / ln.norm + 0.0;
-#pragma unroll RU
-    for (int i = 0; i < M; ++i) g[i] = g[i] / ln.norm + 0.0;
-    HMat<M, kHL> H;
-    if constexpr (kHL) H.base = sH + threadIdx.x;
-#pragma unroll RU
-    for (int i = 0; i < M; ++i)
-#pragma unroll RU
-      for (int j = 0; j < M; ++j) H.at(i, j) = i == j ? 1.0 : 0.0;
-    double gmax = 0.0, g2 = 0.0;
-#pragma unroll RU
-    for (int i = 0; i < M; ++i) {
-      gmax = fmax(gmax, fabs(g[i]));
-      g2 += g[i] * g[i];
-    }
-    bool converged = gmax < 1e-5, failed = false;
-    double old_old = f + sqrt(g2) / 2.0;
-    int ls_status = 0;
+    // +0.0) -- and its scan is not repeated (BfgsFlat::start).
+    const double start = ln.fg(B.x, g, refine);  // norm 1, penalty 0 at c0
     const int maxiter = 200 * ra.n_coef;
-    int k = 0;
-    // line search state (jax _LineSearchState) and zoom state (_ZoomState)
-    double pk[M], g_star[M];
-    double phi0 = 0.0, dphi0 = 0.0, a_i1 = 0.0, phi_i1 = 0.0, dphi_i1 = 0.0, a_star = 0.0, phi_star = 0.0;
-    double a_lo = 0.0, phi_lo = 0.0, dphi_lo = 0.0, a_hi = 0.0, phi_hi = 0.0, dphi_hi = 0.0, a_rec = 0.0,
-           phi_rec = 0.0, za = 0.0, zphi = 0.0, t_trial = 0.0;
-    int li = 1, zj = 0;
-    bool ls_failed = false, in_zoom = false, z_failed = false;
-    // a new line search from (x, f, g, H): p = -H g, jax's first trial min(1, 1.01 * 2 (f_k - f_{k-1}) / phi'(0))
-    auto begin_ls = [&]() {
-#pragma unroll RU
-      for (int i = 0; i < M; ++i) {
-        double s_ = 0.0;
-#pragma unroll RU
-        for (int j = 0; j < M; ++j) s_ += H.at(i, j) * g[j];
-        pk[i] = -s_;
-      }
-      phi0 = f;
-      dphi0 = ln.dot(g, pk);
-      const double cand = 1.01 * 2.0 * (phi0 - old_old) / dphi0;
-      t_trial = cand > 1.0 ? 1.0 : cand;
-      li = 1;
-      a_i1 = 0.0;
-      phi_i1 = phi0;
-      dphi_i1 = dphi0;
-      a_star = 0.0;
-      phi_star = phi0;
-#pragma unroll RU
-      for (int i = 0; i < M; ++i) g_star[i] = g[i];
-      ls_failed = false;
-      in_zoom = false;
-    };
-    // the top of a zoom iteration (everything before its evaluation): the failure test and the next trial a_j
-    auto zoom_top = [&]() {
-      const double dalpha = a_hi - a_lo;
-      const double lo = fmin(a_hi, a_lo), hi = fmax(a_hi, a_lo);
-      const double cchk = 0.2 * dalpha, qchk = 0.1 * dalpha;
-      z_failed = z_failed || (dalpha <= 1e-10);
-      const double a_cub = cubicmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi, a_rec, phi_rec);
-      const bool use_cubic = (zj > 0) && (a_cub > lo + cchk) && (a_cub < hi - cchk);
-      const double a_quad = quadmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi);
-      const bool use_quad = !use_cubic && (a_quad > lo + qchk) && (a_quad < hi - qchk);
-      double a_j = a_rec;
-      if (use_cubic) a_j = a_cub;
-      if (use_quad) a_j = a_quad;
-      if (!use_cubic && !use_quad) a_j = (a_lo + a_hi) / 2.0;
-      t_trial = a_j;
-    };
-    bool pending = refine && !converged && k < maxiter;
-    if (pending) begin_ls();
+    bool pending = B.start(start, g, ln, maxiter) && refine;
     // WIN: the loop runs while ANY lane of the wave has a trial pending (its scans fill the shared ring)
     while (WIN ? __builtin_amdgcn_ballot_w64(pending) != 0 : pending) {
       double dphi_t, g_t[M];
-      const double phi_t = ln.phi(x, pk, t_trial, dphi_t, g_t, pending);
+      const double phi_t = ln.phi(B.x, B.pk, B.t_trial, dphi_t, g_t, pending);
       if (WIN && !pending) continue;
-      bool ls_end = false, ls_done = false;
-      if (!in_zoom) {  // the line search's trial a_i
-        const double a_i = t_trial;
-        const bool s_z1 = (phi_t > phi0 + 1e-4 * a_i * dphi0) || ((phi_t >= phi_i1) && (li > 1));
-        const bool s_i = (fabs(dphi_t) <= -0.9 * dphi0) && !s_z1;
-        const bool s_z2 = (dphi_t >= 0.0) && !s_z1 && !s_i;
-        if (s_i) {
-          a_star = a_i;
-          phi_star = phi_t;
-#pragma unroll RU
-          for (int i = 0; i < M; ++i) g_star[i] = g_t[i];
-        }
-        if (s_z1 || s_z2) {  // zoom between (lo, hi) = (a_{i-1}, a_i) or (a_i, a_{i-1}); state as jax _zoom inits it
-          if (s_z1) {
-            a_lo = a_i1; phi_lo = phi_i1; dphi_lo = dphi_i1;
-            a_hi = a_i; phi_hi = phi_t; dphi_hi = dphi_t;
-          } else {
-            a_lo = a_i; phi_lo = phi_t; dphi_lo = dphi_t;
-            a_hi = a_i1; phi_hi = phi_i1; dphi_hi = dphi_i1;
-          }
-          zj = 0;
-          z_failed = false;
-          a_rec = (a_lo + a_hi) / 2.0;
-          phi_rec = (phi_lo + phi_hi) / 2.0;
-          za = 1.0;
-          zphi = phi_lo;
-#pragma unroll RU
-          for (int i = 0; i < M; ++i) g_star[i] = g[i];
-          in_zoom = true;
-        }
-        ++li;
-        a_i1 = a_i;
-        phi_i1 = phi_t;
-        dphi_i1 = dphi_t;
-        if (in_zoom) {
-          zoom_top();
-        } else if (s_i) {
-          ls_end = ls_done = true;
-        } else if (li > 10) {
-          ls_end = true;
-        } else {
-          t_trial = a_i1 * 2.0;
-        }
-      } else {  // the zoom's trial a_j
-        const double a_j = t_trial;
-        const bool hi_to_j = (phi_t > phi0 + 1e-4 * a_j * dphi0) || (phi_t >= phi_lo);
-        const bool star_to_j = (fabs(dphi_t) <= -0.9 * dphi0) && !hi_to_j;
-        const bool hi_to_lo = (dphi_t * (a_hi - a_lo) >= 0.0) && !hi_to_j && !star_to_j;
-        const bool lo_to_j = !hi_to_j && !star_to_j;
-        if (hi_to_j) {
-          a_rec = a_hi;
-          phi_rec = phi_hi;
-          a_hi = a_j;
-          phi_hi = phi_t;
-          dphi_hi = dphi_t;
-        }
-        if (star_to_j) {
-          za = a_j;
-          zphi = phi_t;
-#pragma unroll RU
-          for (int i = 0; i < M; ++i) g_star[i] = g_t[i];
-        }
-        if (hi_to_lo) {
-          a_rec = a_hi;
-          phi_rec = phi_hi;
-          a_hi = a_lo;
-          phi_hi = phi_lo;
-          dphi_hi = dphi_lo;
-        }
-        if (lo_to_j) {
-          a_rec = a_lo;
-          phi_rec = phi_lo;
-          a_lo = a_j;
-          phi_lo = phi_t;
-          dphi_lo = dphi_t;
-        }
-        ++zj;
-        z_failed = ((z_failed ? 1 : 0) | zj) >= 30;  // jax: `failed | j >= 30` (no parentheses)
-        if (star_to_j || z_failed) {  // the zoom ends, and with it the line search (done = s_z1 | s_z2)
-          a_star = za;
-          phi_star = zphi;
-          ls_failed = ls_failed || z_failed;
-          ls_end = ls_done = true;
-        } else {
-          zoom_top();
-        }
-      }
-      if (ls_end) {
-        ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
-        failed = ls_failed || !ls_done;
-        // ---- BFGS update (minimize_bfgs body after its line_search call) ----
-        double sk[M], yk[M];
-#pragma unroll RU
-        for (int i = 0; i < M; ++i) {
-          sk[i] = a_star * pk[i];
-          yk[i] = g_star[i] - g[i];
-        }
-        const double rho = 1.0 / ln.dot(yk, sk);
-        if (isfinite(rho) && (RU == 1 || INSITE_REFINE_QUAD)) {
-          double hy[M];
-          double yhy = 0.0;
-#pragma unroll RU
-          for (int i = 0; i < M; ++i) {
-            double t = 0.0;
-#pragma unroll RU
-            for (int j = 0; j < M; ++j) t += H.at(i, j) * yk[j];
-            hy[i] = t;
-            yhy += yk[i] * t;
-          }
-          const double cs = rho * rho * yhy + rho;
-#pragma unroll RU
-          for (int i = 0; i < M; ++i)
-#pragma unroll RU
-            for (int j = 0; j < M; ++j)
-              H.at(i, j) = H.at(i, j) - rho * (sk[i] * hy[j] + hy[i] * sk[j]) + cs * (sk[i] * sk[j]);
-        } else if (isfinite(rho)) {
-          auto w = [&](int i, int q) { return (i == q ? 1.0 : 0.0) - rho * (sk[i] * yk[q]); };
-          double WH[M][M];
-#pragma unroll RU
-          for (int i = 0; i < M; ++i)
-#pragma unroll RU
-            for (int j = 0; j < M; ++j) {
-              double s_ = 0.0;
-#pragma unroll RU
-              for (int q = 0; q < M; ++q) s_ += w(i, q) * H.at(q, j);
-              WH[i][j] = s_;
-            }
-#pragma unroll RU
-          for (int i = 0; i < M; ++i)
-#pragma unroll RU
-            for (int j = 0; j < M; ++j) {
-              double s_ = 0.0;
-#pragma unroll RU
-              for (int q = 0; q < M; ++q) s_ += WH[i][q] * w(j, q);
-              H.at(i, j) = s_ + rho * (sk[i] * sk[j]);
-            }
-        }
-        double gm = 0.0;
-#pragma unroll RU
-        for (int i = 0; i < M; ++i) {
-          x[i] = x[i] + sk[i];
-          g[i] = g_star[i];
-          gm = fmax(gm, fabs(g[i]));
-        }
-        converged = gm < 1e-5;
-        old_old = f;
-        f = phi_star;
-        ++k;
-        pending = !converged && !failed && k < maxiter;
-        if (pending) begin_ls();
-      }
+      pending = B.advance(phi_t, dphi_t, g_t, ln, maxiter);
     }
     if (refine) {
-      nit = k;
-      status = converged ? 0 : (k == maxiter ? 1 : (failed ? 2 + ls_status : -1));
-      if (status == 3 && ra.revert3) {  // zoom failed: the reference code keeps the global coefficients (sindy.py:628-631)
+      nit = B.k;
+      status = B.converged ? 0 : (B.k == maxiter ? 1 : (B.failed ? 2 + B.ls_status : -1));
 #pragma unroll RU
-        for (int i = 0; i < M; ++i) x[i] = ln.c0a[i];
-      }
+      for (int i = 0; i < M; ++i)  // zoom failed: the reference code keeps the global coefficients (sindy.py:628-631)
+        x[i] = (status == 3 && ra.revert3) ? ln.c0a[i] : B.x[i];
     }
   }
 #else
@@ -1052,234 +1069,6 @@ insite_refine_kernel(RefineArgs ra) {
 #ifndef INSITE_REFINE_DYN_REFILL
 #define INSITE_REFINE_DYN_REFILL 8
 #endif
-
-// jax minimize_bfgs + line_search + _zoom as the per-lane flat state machine of insite_refine_kernel (FLAT), its state
-// in one struct so a lane can restart it on a new row
-template <int M, bool kHL, int RU, class Lane>
-struct BfgsFlat {
-  HMat<M, kHL> H;
-  double x[M], g[M], pk[M], g_star[M];
-  double f, old_old, phi0, dphi0, a_i1, phi_i1, dphi_i1, a_star, phi_star;
-  double a_lo, phi_lo, dphi_lo, a_hi, phi_hi, dphi_hi, a_rec, phi_rec, za, zphi, t_trial;
-  int li, zj, k, ls_status;
-  bool ls_failed, in_zoom, z_failed, converged, failed;
-  __device__ void begin_ls(const Lane& ln) {
-#pragma unroll RU
-    for (int i = 0; i < M; ++i) {
-      double s_ = 0.0;
-#pragma unroll RU
-      for (int j = 0; j < M; ++j) s_ += H.at(i, j) * g[j];
-      pk[i] = -s_;
-    }
-    phi0 = f;
-    dphi0 = ln.dot(g, pk);
-    const double cand = 1.01 * 2.0 * (phi0 - old_old) / dphi0;
-    t_trial = cand > 1.0 ? 1.0 : cand;
-    li = 1;
-    a_i1 = 0.0;
-    phi_i1 = phi0;
-    dphi_i1 = dphi0;
-    a_star = 0.0;
-    phi_star = phi0;
-#pragma unroll RU
-    for (int i = 0; i < M; ++i) g_star[i] = g[i];
-    ls_failed = false;
-    in_zoom = false;
-  }
-  __device__ void zoom_top() {
-    const double dalpha = a_hi - a_lo;
-    const double lo = fmin(a_hi, a_lo), hi = fmax(a_hi, a_lo);
-    const double cchk = 0.2 * dalpha, qchk = 0.1 * dalpha;
-    z_failed = z_failed || (dalpha <= 1e-10);
-    const double a_cub = cubicmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi, a_rec, phi_rec);
-    const bool use_cubic = (zj > 0) && (a_cub > lo + cchk) && (a_cub < hi - cchk);
-    const double a_quad = quadmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi);
-    const bool use_quad = !use_cubic && (a_quad > lo + qchk) && (a_quad < hi - qchk);
-    double a_j = a_rec;
-    if (use_cubic) a_j = a_cub;
-    if (use_quad) a_j = a_quad;
-    if (!use_cubic && !use_quad) a_j = (a_lo + a_hi) / 2.0;
-    t_trial = a_j;
-  }
-  // the first evaluation s, gs (at c0, norm 1) -> minimize_bfgs's initial state; returns whether a trial is pending
-  __device__ bool start(double s, const double (&gs)[M], Lane& ln, int maxiter) {
-    ln.norm = s * 2.5;
-    f = s / ln.norm + 0.0;
-#pragma unroll RU
-    for (int i = 0; i < M; ++i) g[i] = gs[i] / ln.norm + 0.0;
-#pragma unroll RU
-    for (int i = 0; i < M; ++i)
-#pragma unroll RU
-      for (int j = 0; j < M; ++j) H.at(i, j) = i == j ? 1.0 : 0.0;
-    double gmax = 0.0, g2 = 0.0;
-#pragma unroll RU
-    for (int i = 0; i < M; ++i) {
-      gmax = fmax(gmax, fabs(g[i]));
-      g2 += g[i] * g[i];
-    }
-    converged = gmax < 1e-5;
-    failed = false;
-    old_old = f + sqrt(g2) / 2.0;
-    ls_status = 0;
-    k = 0;
-    const bool pending = !converged && k < maxiter;
-    if (pending) begin_ls(ln);
-    return pending;
-  }
-  // one trial's value / slope / gradient -> the next state (insite_refine_kernel's FLAT loop body); returns pending
-  __device__ bool advance(double phi_t, double dphi_t, const double (&g_t)[M], const Lane& ln, int maxiter) {
-    bool ls_end = false, ls_done = false;
-    if (!in_zoom) {
-      const double a_i = t_trial;
-      const bool s_z1 = (phi_t > phi0 + 1e-4 * a_i * dphi0) || ((phi_t >= phi_i1) && (li > 1));
-      const bool s_i = (fabs(dphi_t) <= -0.9 * dphi0) && !s_z1;
-      const bool s_z2 = (dphi_t >= 0.0) && !s_z1 && !s_i;
-      if (s_i) {
-        a_star = a_i;
-        phi_star = phi_t;
-#pragma unroll RU
-        for (int i = 0; i < M; ++i) g_star[i] = g_t[i];
-      }
-      if (s_z1 || s_z2) {
-        if (s_z1) {
-          a_lo = a_i1; phi_lo = phi_i1; dphi_lo = dphi_i1;
-          a_hi = a_i; phi_hi = phi_t; dphi_hi = dphi_t;
-        } else {
-          a_lo = a_i; phi_lo = phi_t; dphi_lo = dphi_t;
-          a_hi = a_i1; phi_hi = phi_i1; dphi_hi = dphi_i1;
-        }
-        zj = 0;
-        z_failed = false;
-        a_rec = (a_lo + a_hi) / 2.0;
-        phi_rec = (phi_lo + phi_hi) / 2.0;
-        za = 1.0;
-        zphi = phi_lo;
-#pragma unroll RU
-        for (int i = 0; i < M; ++i) g_star[i] = g[i];
-        in_zoom = true;
-      }
-      ++li;
-      a_i1 = a_i;
-      phi_i1 = phi_t;
-      dphi_i1 = dphi_t;
-      if (in_zoom) {
-        zoom_top();
-      } else if (s_i) {
-        ls_end = ls_done = true;
-      } else if (li > 10) {
-        ls_end = true;
-      } else {
-        t_trial = a_i1 * 2.0;
-      }
-    } else {
-      const double a_j = t_trial;
-      const bool hi_to_j = (phi_t > phi0 + 1e-4 * a_j * dphi0) || (phi_t >= phi_lo);
-      const bool star_to_j = (fabs(dphi_t) <= -0.9 * dphi0) && !hi_to_j;
-      const bool hi_to_lo = (dphi_t * (a_hi - a_lo) >= 0.0) && !hi_to_j && !star_to_j;
-      const bool lo_to_j = !hi_to_j && !star_to_j;
-      if (hi_to_j) {
-        a_rec = a_hi;
-        phi_rec = phi_hi;
-        a_hi = a_j;
-        phi_hi = phi_t;
-        dphi_hi = dphi_t;
-      }
-      if (star_to_j) {
-        za = a_j;
-        zphi = phi_t;
-#pragma unroll RU
-        for (int i = 0; i < M; ++i) g_star[i] = g_t[i];
-      }
-      if (hi_to_lo) {
-        a_rec = a_hi;
-        phi_rec = phi_hi;
-        a_hi = a_lo;
-        phi_hi = phi_lo;
-        dphi_hi = dphi_lo;
-      }
-      if (lo_to_j) {
-        a_rec = a_lo;
-        phi_rec = phi_lo;
-        a_lo = a_j;
-        phi_lo = phi_t;
-        dphi_lo = dphi_t;
-      }
-      ++zj;
-      z_failed = ((z_failed ? 1 : 0) | zj) >= 30;  // jax: `failed | j >= 30` (no parentheses)
-      if (star_to_j || z_failed) {
-        a_star = za;
-        phi_star = zphi;
-        ls_failed = ls_failed || z_failed;
-        ls_end = ls_done = true;
-      } else {
-        zoom_top();
-      }
-    }
-    if (!ls_end) return true;
-    ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
-    failed = ls_failed || !ls_done;
-    double sk[M], yk[M];
-#pragma unroll RU
-    for (int i = 0; i < M; ++i) {
-      sk[i] = a_star * pk[i];
-      yk[i] = g_star[i] - g[i];
-    }
-    const double rho = 1.0 / ln.dot(yk, sk);
-    if (isfinite(rho) && (RU == 1 || INSITE_REFINE_QUAD)) {
-      double hy[M];
-      double yhy = 0.0;
-#pragma unroll RU
-      for (int i = 0; i < M; ++i) {
-        double t = 0.0;
-#pragma unroll RU
-        for (int j = 0; j < M; ++j) t += H.at(i, j) * yk[j];
-        hy[i] = t;
-        yhy += yk[i] * t;
-      }
-      const double cs = rho * rho * yhy + rho;
-#pragma unroll RU
-      for (int i = 0; i < M; ++i)
-#pragma unroll RU
-        for (int j = 0; j < M; ++j)
-          H.at(i, j) = H.at(i, j) - rho * (sk[i] * hy[j] + hy[i] * sk[j]) + cs * (sk[i] * sk[j]);
-    } else if (isfinite(rho)) {
-      auto w = [&](int i, int q) { return (i == q ? 1.0 : 0.0) - rho * (sk[i] * yk[q]); };
-      double WH[M][M];
-#pragma unroll RU
-      for (int i = 0; i < M; ++i)
-#pragma unroll RU
-        for (int j = 0; j < M; ++j) {
-          double s_ = 0.0;
-#pragma unroll RU
-          for (int q = 0; q < M; ++q) s_ += w(i, q) * H.at(q, j);
-          WH[i][j] = s_;
-        }
-#pragma unroll RU
-      for (int i = 0; i < M; ++i)
-#pragma unroll RU
-        for (int j = 0; j < M; ++j) {
-          double s_ = 0.0;
-#pragma unroll RU
-          for (int q = 0; q < M; ++q) s_ += WH[i][q] * w(j, q);
-          H.at(i, j) = s_ + rho * (sk[i] * sk[j]);
-        }
-    }
-    double gm = 0.0;
-#pragma unroll RU
-    for (int i = 0; i < M; ++i) {
-      x[i] = x[i] + sk[i];
-      g[i] = g_star[i];
-      gm = fmax(gm, fabs(g[i]));
-    }
-    converged = gm < 1e-5;
-    old_old = f;
-    f = phi_star;
-    ++k;
-    const bool pending = !converged && !failed && k < maxiter;
-    if (pending) begin_ls(ln);
-    return pending;
-  }
-};
 
 template <int M>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_REFINE_WPE4)))
