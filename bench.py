@@ -800,7 +800,8 @@ def insite_main(args):
                                "patient-major rows)", "bound": "valu-f64",
                      "unit": "TFLOP/s", "achieved": flop / (kern_ms * 1e-3) / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
                      "frac": flop / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
-                     "traffic": traffic_for("insite", "insite_refine_kernel", args=args), "avg_launch_ms": kern_ms,
+                     "traffic": traffic_for("insite", "insite_refine_kernel<3, 2, 1, true, true>", args=args),
+                     "avg_launch_ms": kern_ms,
                      "algorithmic_flop": flop, "flop_per_sensitivity_step": per_step,
                      "flop_method": "sum over refined rows of nfev_r x K_r (K_r = min(seq_len - tau, T - 1)) x "
                                     "(5 Euler sub-steps x (4A + 7) + 4A + 5) with A = 2 arms, + N x T x 5 x 4 for "
@@ -985,7 +986,9 @@ def insite4_main(args):
         "roofline": {"kernel": d["kernel"] + " (dense per-arm model: rolled loops, per-lane scratch state)",
                      "bound": "valu-f64", "unit": "TFLOP/s", "achieved": d["valu_f64_TFLOPs"],
                      "peak": FP64_VALU_PEAK_TFLOPS, "frac": d["frac"],
-                     "traffic": traffic_for("insite4", "insite_refine_kernel", args=args),
+                     "traffic": traffic_for("insite4", "insite_refine_kernel<16, 4, 1", args=args),
+                     "traffic_note": "per-lane scratch state of the rolled M = 16 kernel (6.3 KB per lane): the "
+                                     "counters put it at ~374 GB of HBM traffic per launch, the kernel's bound",
                      "avg_launch_ms": d["kernel_ms"], "algorithmic_flop": d["algorithmic_flop"],
                      "flop_method": "sum over refined rows of nfev_r x K_r x (5 x (4A + 7) + 4A + 5), A = 4 arms, + N x T "
                                     "x 5 x 4 for the final scan; nfev from the kernel's own count",
@@ -1319,12 +1322,12 @@ def dist_setup(force_group: bool = False):
     return world, rank, dev
 
 
-TRAFFIC_R03 = os.path.join(ROOT, "profiles", "traffic_r03.json")
+TRAFFIC_R04 = os.path.join(ROOT, "profiles", "traffic_r04.json")
 
 
 def traffic_for(config, kernel, grid=None, args=None):
     """HBM bytes per launch of `kernel` (symbol prefix) in the bench line `config`, from the committed PMC passes
-    (profiles/traffic_r03.json, tools/g_traffic.sh + tools/traffic_summary.py: FETCH_SIZE x 2 calibration +
+    (profiles/traffic_r04.json, tools/g_traffic.sh + tools/traffic_summary.py: FETCH_SIZE x 2 calibration +
     WRITE_SIZE, median per dispatch), or None when that table has no such entry.  `grid`: the launch's total
     threads when a config launches the kernel at several sizes.  `args`: the table was taken on each config's
     DEFAULT workload at N = 1 (tools/g_traffic.sh), so a line with other sizes gets None."""
@@ -1340,7 +1343,7 @@ def traffic_for(config, kernel, grid=None, args=None):
         if knobs != (1_000_000 if big else 100_000, t_def, "rk4", "bits", "time", 0, 1, 1):
             return None
     try:
-        with open(TRAFFIC_R03) as f:
+        with open(TRAFFIC_R04) as f:
             tab = json.load(f).get(config, {})
     except Exception:
         return None
