@@ -75,6 +75,15 @@ struct RefineArgs {
   int32_t gmap;
 };
 
+// The kernels read RefineArgs (a by-value kernel argument, ~2.9 KB of tables) through a pointer into the kernarg
+// segment (constant address space): binding a reference to the by-value parameter itself made the compiler copy
+// the whole struct into per-lane scratch at kernel entry and index the copy with vector loads -- 6.3 KB of scratch
+// per lane in the rolled M = 16 kernel, whose counters showed ~374 GB of HBM traffic per 1M-row launch.
+typedef const __attribute__((address_space(4))) RefineArgs KArgs;
+__device__ __forceinline__ KArgs& kernel_args() {
+  return *(KArgs*)(__builtin_amdgcn_kernarg_segment_ptr());
+}
+
 __device__ __forceinline__ double monomial_code(int code, const double* u) {
   double m = 1.0;
 #pragma unroll
@@ -146,7 +155,7 @@ struct RefineLane {
   // wins (INSITE_REFINE_SU4); dense models stay rolled
   static constexpr int SU = (M > 4 && M <= 16) ? 5 : (M <= 4 ? INSITE_REFINE_SU4 : 1);
   static constexpr bool kGmap = M <= 4 && D == 1 && NA <= 4;  // RefineArgs::gmap holds the routing
-  const RefineArgs& ra;
+  KArgs& ra;
   int64_t p;
   int K;
   double norm;
@@ -603,7 +612,8 @@ struct BfgsFlat {
       yk[i] = g_star[i] - g[i];
     }
     const double rho = 1.0 / ln.dot(yk, sk);
-    if (isfinite(rho) && (RU == 1 || INSITE_REFINE_QUAD)) {
+    if constexpr (RU == 1 || INSITE_REFINE_QUAD) {  // (compile-time: the rolled kernels never hold the WH temporary)
+     if (isfinite(rho)) {
       double hy[M];
       double yhy = 0.0;
 #pragma unroll RU
@@ -620,6 +630,7 @@ struct BfgsFlat {
 #pragma unroll RU
         for (int j = 0; j < M; ++j)
           H.at(i, j) = H.at(i, j) - rho * (sk[i] * hy[j] + hy[i] * sk[j]) + cs * (sk[i] * sk[j]);
+     }
     } else if (isfinite(rho)) {
       auto w = [&](int i, int q) { return (i == q ? 1.0 : 0.0) - rho * (sk[i] * yk[q]); };
       double WH[M][M];
@@ -665,7 +676,8 @@ struct BfgsFlat {
 template <int M, int NA, int D, bool WIN = false, bool PM = false>
 __global__ void __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(M <= 4 && D == 1 ? INSITE_REFINE_WPE4 : (M <= 8 ? INSITE_REFINE_WPE8 : 1))))
-insite_refine_kernel(RefineArgs ra) {
+insite_refine_kernel(RefineArgs) {
+  KArgs& ra = kernel_args();  // (the parameter itself is never named: see KArgs)
   constexpr int RU = RefineLane<M, NA, D, WIN, PM>::RU;
   constexpr bool kHL = INSITE_REFINE_HLDS && RU == M && M <= 4;
   __shared__ double sH[(kHL ? M * M : 1) * kBlock];
@@ -1072,7 +1084,8 @@ insite_refine_kernel(RefineArgs ra) {
 
 template <int M>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_REFINE_WPE4)))
-insite_refine_dyn_kernel(RefineArgs ra, unsigned* queue, int refill) {
+insite_refine_dyn_kernel(RefineArgs, unsigned* queue, int refill) {
+  KArgs& ra = kernel_args();
   constexpr int NA = 2, D = 1;
   using Lane = RefineLane<M, NA, D, true, true>;
   constexpr int RU = Lane::RU;
@@ -1196,7 +1209,8 @@ insite_refine_dyn_kernel(RefineArgs ra, unsigned* queue, int refill) {
 // per launch for ~0.2 GB of data), and the predictions leave through the same staging as 64-B row segments.
 constexpr int kFinalMaxCoef = 16;  // coefficients staged per row (larger models read theirs per lane)
 template <int M>
-__global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs ra, int staged_arm) {
+__global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs, int staged_arm) {
+  KArgs& ra = kernel_args();
   constexpr int NA = 2, D = 1;
   // per wave: [64 x kFinalMaxCoef doubles | 64 x 64 arm bytes], its first 4 KB reused as the prediction staging once
   // the coefficients and arms are in registers (48 KB per block: 3 blocks per CU)
