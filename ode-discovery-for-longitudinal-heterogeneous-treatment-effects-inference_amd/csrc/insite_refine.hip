@@ -1305,6 +1305,431 @@ __global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs,
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------------
+// Cooperative refinement of the dense 4-arm models (INSITE_REFINE_COOP): 9-16 active coefficients, int8 arms
+// ------------------------------------------------------------------------------------------------------------------
+// The rolled one-row-per-lane M = 16 kernel keeps the 16 x 16 inverse Hessian and a dozen 16-vectors in per-lane
+// scratch (3.9 KB a lane): on the cancer_sim-shaped dense model (4 arms x 4 terms, the reference's slowest published
+// path) its PMC traffic was ~374 GB per 1M-row launch, 66-72 ms.  Here a row is refined by a group of 8 lanes:
+// lane j of a group owns coordinates j and j + 8 (their x, g, p, g* and their two rows of H, in VGPRs) and the
+// sensitivity of tangent (arm j / 2, exponent j % 2) -- the 8 tangents of a 4-arm affine model.  Every lane runs the
+// row's state chain y (so the tangents need no broadcast), and the scalars of the line search / zoom, replicated.
+// Everything the single-lane kernel sums over coordinates (gamma, the penalty, dot products, H y, y^T H y) is
+// summed in ITS order from values shuffled within the group, so the outputs are bitwise those of the M = 16 kernel
+// (tested); the QUAD inverse-Hessian update is the one that kernel runs (RU = 1).  Shuffles only read lanes of the
+// reading lane's own group, whose lanes always branch together (their replicated scalars are equal).
+#ifndef INSITE_REFINE_COOP
+#define INSITE_REFINE_COOP 1
+#endif
+#ifndef INSITE_REFINE_COOP_WPE
+#define INSITE_REFINE_COOP_WPE 2
+#endif
+constexpr int kCoopG = 8;  // lanes per row
+
+template <int MC, int NA>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_REFINE_COOP_WPE)))
+insite_refine_coop_kernel(RefineArgs) {
+  constexpr int S = MC / kCoopG;  // coordinates per lane: i = j + kCoopG s
+  static_assert(MC % kCoopG == 0 && NA * 2 <= kCoopG, "one tangent per lane");
+  KArgs& ra = kernel_args();
+  const int lane = threadIdx.x & (kWave - 1);
+  const int j = lane & (kCoopG - 1);
+  const int gbase = lane & ~(kCoopG - 1);
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((gt - lane) / kCoopG >= ra.N) return;  // (wave-uniform)
+  const int64_t gr = gt / kCoopG;            // lane-order row of this group
+  const bool valid = gr < ra.N;
+  const int64_t grc = valid ? gr : ra.N - 1;
+  const int64_t p = ra.order ? (int64_t)ra.order[grc] : grc;
+  const int ta = j >> 1, te = j & 1;  // this lane's tangent (arm, exponent)
+  // coordinate i of a distributed vector: lane i % 8 of the group, slot i / 8
+  auto gat = [&](const double (&v)[S], int i) -> double { return __shfl(v[i / kCoopG], gbase + (i % kCoopG)); };
+  double uu[INSITE_MAX_STATICS];
+#pragma unroll
+  for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < ra.U ? ra.u[p * ra.U + t] : 0.0;
+  double mono[S], c0a[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int i = j + kCoopG * s;
+    mono[s] = i < ra.m ? monomial_code(ra.t_ucode[i], uu) : 0.0;
+    c0a[s] = i < ra.m ? ra.c0[ra.t_flat[i]] : 0.0;
+  }
+  const int sl = valid ? ra.sl[p] : 0;
+  const bool refine = sl > ra.tau && ra.T >= 2;
+  const int K = refine ? min(sl - ra.tau, ra.T - 1) : 0;
+  double norm = 1.0;
+  int nev = 0;
+  // f and its gradient at c (RefineLane::fg, D = 1, the non-windowed scan); every lane of the wave calls it
+  auto fg = [&](const double (&c)[S], double (&g)[S], bool live) -> double {
+    nev += live ? 1 : 0;
+    double gam[NA][2];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) gam[a][0] = gam[a][1] = 0.0;
+#pragma unroll
+    for (int i = 0; i < MC; ++i) {
+      if (i >= ra.m) break;
+      const double t = gat(c, i) * gat(mono, i);
+      const int mk = ra.t_mask[i], ex = ra.t_ex[i];
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+        if ((mk >> a) & 1)
+#pragma unroll
+          for (int e = 0; e <= 1; ++e)
+            if (ex == e) gam[a][e] += t;
+    }
+    const double h = ra.dt / (double)ra.sub;
+    double y = ra.V[p];
+    double d = 0.0, gGo = 0.0, L = 0.0;
+    const int Kl = live ? K : 0;
+    int Kw = Kl;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) Kw = max(Kw, __shfl_xor(Kw, off));
+    int ak_nx = Kw > 0 ? (int)ra.arm8[p] : 0;
+    double v_nx = Kw > 0 ? ra.V[ra.ldv + p] : 0.0;
+    for (int k = 0; k < Kw; ++k) {
+      const int ak = ak_nx;
+      const double vk1 = v_nx;
+      if (k + 1 < Kw) {
+        ak_nx = (int)ra.arm8[(int64_t)(k + 1) * ra.lda + p];
+        v_nx = ra.V[(int64_t)(k + 2) * ra.ldv + p];
+      }
+      if (k < Kl) {
+        double gk0 = gam[0][0], gk1 = gam[0][1];
+#pragma unroll
+        for (int a = 1; a < NA; ++a)
+          if (ak == a) {
+            gk0 = gam[a][0];
+            gk1 = gam[a][1];
+          }
+        const double hb = h * gk1;
+        const double ha = (ak == ta) ? h : 0.0;
+#pragma unroll 5
+        for (int s = 0; s < ra.sub; ++s) {
+          d = (d + hb * d) + (te ? ha * y : ha);
+          y = y + h * (gk0 + gk1 * y);
+        }
+        const double r = vk1 - y;
+        L += r * r;
+        gGo += -2.0 * r * d;
+      }
+    }
+    const double iK = 1.0 / (double)K;
+    L *= iK;
+    double gG[NA][2];
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int e = 0; e <= 1; ++e) gG[a][e] = __shfl(gGo, gbase + 2 * a + e);
+    double pen = 0.0;
+#pragma unroll
+    for (int i = 0; i < MC; ++i) {
+      const double ci = gat(c, i), c0i = gat(c0a, i);
+      if (i >= ra.m) {
+        if (i % kCoopG == j) g[i / kCoopG] = 0.0;
+        continue;
+      }
+      const double dd = c0i - ci;
+      pen += dd * dd;
+      if (i % kCoopG == j) {
+        const int mk = ra.t_mask[i], ex = ra.t_ex[i];
+        double gd = 0.0;
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+          if ((mk >> a) & 1)
+#pragma unroll
+            for (int e = 0; e <= 1; ++e)
+              if (ex == e) gd += gG[a][e];
+        g[i / kCoopG] = gd * iK * mono[i / kCoopG] / norm + 2.0 * ra.lam * (ci - c0i) / (double)ra.n_coef;
+      }
+    }
+    return L / norm + ra.lam * pen / (double)ra.n_coef;
+  };
+  auto dot = [&](const double (&a)[S], const double (&b)[S]) -> double {
+    double s_ = 0.0;
+#pragma unroll
+    for (int i = 0; i < MC; ++i) s_ += gat(a, i) * gat(b, i);
+    return s_;
+  };
+  // ---- the flat BFGS state machine (BfgsFlat with the vectors distributed; the QUAD update of RU = 1) ----
+  double x[S], g[S], pk[S], g_star[S], Hr[S][MC];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    x[s] = c0a[s];
+    pk[s] = 0.0;
+  }
+  double f = 0.0, old_old = 0.0, phi0 = 0.0, dphi0 = 0.0, a_i1 = 0.0, phi_i1 = 0.0, dphi_i1 = 0.0, a_star = 0.0,
+         phi_star = 0.0, a_lo = 0.0, phi_lo = 0.0, dphi_lo = 0.0, a_hi = 0.0, phi_hi = 0.0, dphi_hi = 0.0, a_rec = 0.0,
+         phi_rec = 0.0, za = 0.0, zphi = 0.0, t_trial = 0.0;
+  int li = 1, zj = 0, k = 0, ls_status = 0;
+  bool ls_failed = false, in_zoom = false, z_failed = false, converged = false, failed = false;
+  const int maxiter = 200 * ra.n_coef;
+  auto begin_ls = [&]() {
+#pragma unroll
+    for (int s = 0; s < S; ++s) pk[s] = 0.0;
+    double acc[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) acc[s] = 0.0;
+#pragma unroll
+    for (int q = 0; q < MC; ++q) {
+      const double gq = gat(g, q);
+#pragma unroll
+      for (int s = 0; s < S; ++s) acc[s] += Hr[s][q] * gq;
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) pk[s] = -acc[s];
+    phi0 = f;
+    dphi0 = dot(g, pk);
+    const double cand = 1.01 * 2.0 * (phi0 - old_old) / dphi0;
+    t_trial = cand > 1.0 ? 1.0 : cand;
+    li = 1;
+    a_i1 = 0.0;
+    phi_i1 = phi0;
+    dphi_i1 = dphi0;
+    a_star = 0.0;
+    phi_star = phi0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) g_star[s] = g[s];
+    ls_failed = false;
+    in_zoom = false;
+  };
+  auto zoom_top = [&]() {
+    const double dalpha = a_hi - a_lo;
+    const double lo = fmin(a_hi, a_lo), hi = fmax(a_hi, a_lo);
+    const double cchk = 0.2 * dalpha, qchk = 0.1 * dalpha;
+    z_failed = z_failed || (dalpha <= 1e-10);
+    const double a_cub = cubicmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi, a_rec, phi_rec);
+    const bool use_cubic = (zj > 0) && (a_cub > lo + cchk) && (a_cub < hi - cchk);
+    const double a_quad = quadmin(a_lo, phi_lo, dphi_lo, a_hi, phi_hi);
+    const bool use_quad = !use_cubic && (a_quad > lo + qchk) && (a_quad < hi - qchk);
+    double a_j = a_rec;
+    if (use_cubic) a_j = a_cub;
+    if (use_quad) a_j = a_quad;
+    if (!use_cubic && !use_quad) a_j = (a_lo + a_hi) / 2.0;
+    t_trial = a_j;
+  };
+  // the start: one scan at c0 (norm 1, penalty 0), minimize_bfgs's initial state
+  bool pending = false;
+  {
+    double g0[S];
+    const double start = fg(x, g0, refine);
+    norm = start * 2.5;
+    f = start / norm + 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) g[s] = g0[s] / norm + 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int q = 0; q < MC; ++q) Hr[s][q] = (j + kCoopG * s) == q ? 1.0 : 0.0;
+    double gmax = 0.0, g2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < MC; ++i) {
+      const double gi = gat(g, i);
+      gmax = fmax(gmax, fabs(gi));
+      g2 += gi * gi;
+    }
+    converged = gmax < 1e-5;
+    old_old = f + sqrt(g2) / 2.0;
+    pending = refine && !converged && k < maxiter;
+    if (!converged && k < maxiter) begin_ls();  // (group-uniform; inert rows' values are never used)
+  }
+  while (__builtin_amdgcn_ballot_w64(pending) != 0ull) {
+    double xt[S], g_t[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) xt[s] = x[s] + t_trial * pk[s];
+    const double phi_t = fg(xt, g_t, pending);
+    const double dphi_t = dot(g_t, pk);
+    if (!pending) continue;
+    bool ls_end = false, ls_done = false;
+    if (!in_zoom) {
+      const double a_i = t_trial;
+      const bool s_z1 = (phi_t > phi0 + 1e-4 * a_i * dphi0) || ((phi_t >= phi_i1) && (li > 1));
+      const bool s_i = (fabs(dphi_t) <= -0.9 * dphi0) && !s_z1;
+      const bool s_z2 = (dphi_t >= 0.0) && !s_z1 && !s_i;
+      if (s_i) {
+        a_star = a_i;
+        phi_star = phi_t;
+#pragma unroll
+        for (int s = 0; s < S; ++s) g_star[s] = g_t[s];
+      }
+      if (s_z1 || s_z2) {
+        if (s_z1) {
+          a_lo = a_i1; phi_lo = phi_i1; dphi_lo = dphi_i1;
+          a_hi = a_i; phi_hi = phi_t; dphi_hi = dphi_t;
+        } else {
+          a_lo = a_i; phi_lo = phi_t; dphi_lo = dphi_t;
+          a_hi = a_i1; phi_hi = phi_i1; dphi_hi = dphi_i1;
+        }
+        zj = 0;
+        z_failed = false;
+        a_rec = (a_lo + a_hi) / 2.0;
+        phi_rec = (phi_lo + phi_hi) / 2.0;
+        za = 1.0;
+        zphi = phi_lo;
+#pragma unroll
+        for (int s = 0; s < S; ++s) g_star[s] = g[s];
+        in_zoom = true;
+      }
+      ++li;
+      a_i1 = a_i;
+      phi_i1 = phi_t;
+      dphi_i1 = dphi_t;
+      if (in_zoom) {
+        zoom_top();
+      } else if (s_i) {
+        ls_end = ls_done = true;
+      } else if (li > 10) {
+        ls_end = true;
+      } else {
+        t_trial = a_i1 * 2.0;
+      }
+    } else {
+      const double a_j = t_trial;
+      const bool hi_to_j = (phi_t > phi0 + 1e-4 * a_j * dphi0) || (phi_t >= phi_lo);
+      const bool star_to_j = (fabs(dphi_t) <= -0.9 * dphi0) && !hi_to_j;
+      const bool hi_to_lo = (dphi_t * (a_hi - a_lo) >= 0.0) && !hi_to_j && !star_to_j;
+      const bool lo_to_j = !hi_to_j && !star_to_j;
+      if (hi_to_j) {
+        a_rec = a_hi;
+        phi_rec = phi_hi;
+        a_hi = a_j;
+        phi_hi = phi_t;
+        dphi_hi = dphi_t;
+      }
+      if (star_to_j) {
+        za = a_j;
+        zphi = phi_t;
+#pragma unroll
+        for (int s = 0; s < S; ++s) g_star[s] = g_t[s];
+      }
+      if (hi_to_lo) {
+        a_rec = a_hi;
+        phi_rec = phi_hi;
+        a_hi = a_lo;
+        phi_hi = phi_lo;
+        dphi_hi = dphi_lo;
+      }
+      if (lo_to_j) {
+        a_rec = a_lo;
+        phi_rec = phi_lo;
+        a_lo = a_j;
+        phi_lo = phi_t;
+        dphi_lo = dphi_t;
+      }
+      ++zj;
+      z_failed = ((z_failed ? 1 : 0) | zj) >= 30;  // jax: `failed | j >= 30` (no parentheses)
+      if (star_to_j || z_failed) {
+        a_star = za;
+        phi_star = zphi;
+        ls_failed = ls_failed || z_failed;
+        ls_end = ls_done = true;
+      } else {
+        zoom_top();
+      }
+    }
+    if (!ls_end) continue;
+    ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
+    failed = ls_failed || !ls_done;
+    double sk[S], yk[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      sk[s] = a_star * pk[s];
+      yk[s] = g_star[s] - g[s];
+    }
+    const double rho = 1.0 / dot(yk, sk);
+    if (isfinite(rho)) {
+      double hy[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) hy[s] = 0.0;
+#pragma unroll
+      for (int q = 0; q < MC; ++q) {
+        const double yq = gat(yk, q);
+#pragma unroll
+        for (int s = 0; s < S; ++s) hy[s] += Hr[s][q] * yq;
+      }
+      double yhy = 0.0;
+#pragma unroll
+      for (int i = 0; i < MC; ++i) yhy += gat(yk, i) * gat(hy, i);
+      const double cs = rho * rho * yhy + rho;
+#pragma unroll
+      for (int q = 0; q < MC; ++q) {
+        const double hq = gat(hy, q), sq = gat(sk, q);
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+          Hr[s][q] = Hr[s][q] - rho * (sk[s] * hq + hy[s] * sq) + cs * (sk[s] * sq);
+      }
+    }
+    double gm = 0.0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      x[s] = x[s] + sk[s];
+      g[s] = g_star[s];
+    }
+#pragma unroll
+    for (int i = 0; i < MC; ++i) gm = fmax(gm, fabs(gat(g, i)));
+    converged = gm < 1e-5;
+    old_old = f;
+    f = phi_star;
+    ++k;
+    pending = !converged && !failed && k < maxiter;
+    if (pending) begin_ls();
+  }
+  int status = -1, nit = 0;
+  if (refine) {
+    nit = k;
+    status = converged ? 0 : (k == maxiter ? 1 : (failed ? 2 + ls_status : -1));
+    if (status == 3 && ra.revert3) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) x[s] = c0a[s];
+    }
+  }
+  // ---- final Euler scan with every coefficient (insite_refine_kernel's, replicated in the group's lanes) ----
+  double xf[MC];
+#pragma unroll
+  for (int i = 0; i < MC; ++i) xf[i] = gat(x, i);
+  auto coef_at = [&](int q) -> double {
+    double c = ra.c0[q];
+#pragma unroll
+    for (int i = 0; i < MC; ++i)
+      if (i < ra.m && ra.t_flat[i] == q) c = xf[i];
+    return c;
+  };
+  if (!valid) return;
+  double gam[NA][2];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) gam[a][0] = gam[a][1] = 0.0;
+  for (int q = 0; q < ra.n_coef; ++q) {
+    const int code = ra.q_code[q], mk = ra.q_mask[q], ex = code >> 24;
+    const double t = coef_at(q) * monomial_code(code & 0xffffff, uu);
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+      if ((mk >> a) & 1)
+#pragma unroll
+        for (int e = 0; e <= 1; ++e)
+          if (ex == e) gam[a][e] += t;
+  }
+  const double h = ra.dt / (double)ra.sub;
+  double y = ra.V[p];
+  for (int kk = 0; kk < ra.T; ++kk) {
+    const int ak = (int)ra.arm8[(int64_t)kk * ra.lda + p];
+    double gk0 = gam[0][0], gk1 = gam[0][1];
+#pragma unroll
+    for (int a = 1; a < NA; ++a)
+      if (ak == a) {
+        gk0 = gam[a][0];
+        gk1 = gam[a][1];
+      }
+    for (int s = 0; s < ra.sub; ++s) y = y + h * (gk0 + gk1 * y);
+    if ((kk & (kCoopG - 1)) == j) ra.preds[(int64_t)kk * ra.ldp + p] = y;
+  }
+  if (ra.coef_out)
+    for (int q = j; q < ra.n_coef; q += kCoopG) ra.coef_out[p * ra.n_coef + q] = coef_at(q);
+  if (j == 0) {
+    if (ra.status) ra.status[p] = status;
+    if (ra.iters) ra.iters[p] = nit;
+    if (ra.nfev) ra.nfev[p] = nev;
+  }
+}
+
 // The dynamic kernel's queue heads: device words handed out round-robin per launch (zeroed on the launch's stream
 // first); kRefineQueues launches may be in flight on independent streams at once.
 constexpr int kRefineQueues = 64;
@@ -1370,7 +1795,16 @@ void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
     else if (m == 3) insite_refine_kernel<3, NA, D><<<grid, kBlock, 0, hs>>>(ra);
     else if (m <= 4) insite_refine_kernel<4, NA, D><<<grid, kBlock, 0, hs>>>(ra);
     else if (m <= 8) insite_refine_kernel<8, NA, D><<<grid, kBlock, 0, hs>>>(ra);
-    else if (m <= 16) insite_refine_kernel<16, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+    else if (m <= 16) {
+      const char* cv = getenv("INSITE_REFINE_COOP");
+      const bool coop = cv ? cv[0] == '1' : INSITE_REFINE_COOP != 0;
+      if (NA == 4 && coop) {  // the dense 4-arm models (int8 arms): 8 lanes per row
+        const dim3 gc((unsigned)((ra.N * kCoopG + kBlock - 1) / kBlock));
+        insite_refine_coop_kernel<16, 4><<<gc, kBlock, 0, hs>>>(ra);
+      } else {
+        insite_refine_kernel<16, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+      }
+    }
     else if (m <= 36) insite_refine_kernel<36, NA, D><<<grid, kBlock, 0, hs>>>(ra);
     else insite_refine_kernel<kRefineMaxCoef, NA, D><<<grid, kBlock, 0, hs>>>(ra);
   } else {

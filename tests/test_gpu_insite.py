@@ -480,3 +480,41 @@ def test_refine_rows_dynamic_assignment_equals_static(dev, monkeypatch, N, T, m,
         outs[dyn] = tuple(t.clone() for t in r) + (nf,)
     for a, b in zip(outs["1"], outs["0"]):
         assert torch.equal(a, b)
+
+
+F4_COEF = [[0.0, 0.20, 0.0, 0.0], [0.0, 0.0, 0.0, -0.60], [0.0, -0.30, 0.0, 0.0], [0.0, -0.25, 0.0, -0.90]]
+
+
+@pytest.mark.parametrize("N,joint", [(3_000, False), (517, False), (2_000, True)])
+def test_cooperative_dense_refine_equals_single_lane(dev, monkeypatch, N, joint):
+    """The cooperative kernel for the dense 4-arm models (8 lanes per row, H rows and coordinates distributed,
+    INSITE_REFINE_COOP) against the one-row-per-lane M = 16 kernel (INSITE_REFINE_COOP=0): predictions,
+    coefficients, statuses, iteration and evaluation counts bitwise equal -- the dense per-arm model (16 active
+    coefficients, cancer_sim's shape) and the joint one-ODE model over (x, chemo, radio, u0); ragged seq_len incl.
+    rows <= tau, a partial last wave."""
+    from insite_amd import cohort, ops
+    from insite_amd.library import polynomial_library
+    T = 60
+    coh = cohort.synthetic_segments(N, T, seed=N + 11, device=dev, coef=F4_COEF, dt=0.1)
+    V = coh.x[:T].t().contiguous()
+    arm = coh.arm.t().contiguous()
+    g = torch.Generator(device=dev)
+    g.manual_seed(N)
+    sl = torch.randint(1, T + 1, (N,), generator=g, device=dev, dtype=torch.int32)
+    if joint:
+        lib = polynomial_library(1, 2, True, n_inputs=2)
+        c0 = np.array([[-0.36, 0.33, 0.49, 0.074, 0.80, -0.45, -0.45, -0.29, 0.19, -1.15, -0.34]])
+    else:
+        lib = coh.lib
+        base = np.array(F4_COEF) * 1.1
+        c0 = np.where(base != 0, base, 0.01)
+    outs = {}
+    for coop in ("1", "0"):
+        monkeypatch.setenv("INSITE_REFINE_COOP", coop)
+        nf = torch.empty((N,), dtype=torch.int32, device=dev)
+        r = ops.insite_refine(V, arm, coh.u, sl, c0, lib, coh.dt, 10.0, 5, nfev=nf)
+        torch.cuda.synchronize()
+        outs[coop] = tuple(t.clone() for t in r) + (nf,)
+    assert (outs["1"][2][sl <= 5] == -1).all() and (outs["1"][2][sl > 5] >= 0).all()
+    for a, b in zip(outs["1"], outs["0"]):
+        assert torch.equal(a, b)
