@@ -1405,7 +1405,8 @@ insite_refine_coop_kernel(RefineArgs) {
         const double ha = (ak == ta) ? h : 0.0;
 #pragma unroll 5
         for (int s = 0; s < ra.sub; ++s) {
-          d = (d + hb * d) + (te ? ha * y : ha);
+          // the single-lane kernel's two expressions (same contraction: a select inside one would split the fma)
+          d = te ? (d + hb * d) + ha * y : (d + hb * d) + ha;
           y = y + h * (gk0 + gk1 * y);
         }
         const double r = vk1 - y;
