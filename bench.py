@@ -827,7 +827,7 @@ def _insite4_rows(N, T, seed, device):
     g = torch.Generator(device=device)
     g.manual_seed(seed + 1)
     sl = torch.randint(1, T, (N,), generator=g, device=device, dtype=torch.int32)
-    return coh.x[:T].t().contiguous(), coh.arm.t().contiguous(), coh.u, sl, coh.lib, coh.dt
+    return coh.x[:T, :N].t().contiguous(), coh.arm[:, :N].t().contiguous(), coh.u, sl, coh.lib, coh.dt
 
 
 def _insite4_models(V, arm, u, dt, lib, n_fit=20_000):

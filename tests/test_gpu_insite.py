@@ -498,8 +498,8 @@ def test_cooperative_dense_refine_equals_single_lane(dev, monkeypatch, N, joint)
     from insite_amd.library import polynomial_library
     T = 60
     coh = cohort.synthetic_segments(N, T, seed=N + 11, device=dev, coef=F4_COEF, dt=0.1)
-    V = coh.x[:T].t().contiguous()
-    arm = coh.arm.t().contiguous()
+    V = coh.x[:T, :N].t().contiguous()
+    arm = coh.arm[:, :N].t().contiguous()
     g = torch.Generator(device=dev)
     g.manual_seed(N)
     sl = torch.randint(1, T + 1, (N,), generator=g, device=dev, dtype=torch.int32)
