@@ -138,6 +138,12 @@ __device__ __forceinline__ int pm_slot_index(int r, int col) {
   return ((col >> 3) & 1) * (kWin * kWave) + pm_lane_base(r) + ((col + pm_lane_rot(r)) & 7);
 }
 
+// NC (`#pragma clang fp contract(off)` in a block): the per-evaluation and per-iteration sums over coefficients (gamma,
+// the gradient and penalty, dot products, H g, the inverse-Hessian update, the final model's gamma) are computed
+// without fused multiply-adds, so every kernel that computes them -- the one-lane-per-row kernels with their loops
+// rolled or unrolled, the cooperative kernel with its values shuffled in -- rounds them identically (the compiler's
+// contraction choices differed between those code shapes: ~1e-13 apart, and on ill-conditioned joint-model rows a
+// different BFGS path).  The scan's per-step arithmetic stays contracted (the same code in every kernel).
 // The ring's wait: the hardware wait for the LDS-DMA loads (inline asm: the compiler does not track them) AND the
 // same wait as a builtin the compiler's waitcnt pass sees, so it knows its own earlier loads (the scan's y0) have
 // completed too.  With the asm alone the pass kept a vmcnt(0) for y0 inside the sub-step loop -- which, executed
@@ -224,6 +230,7 @@ struct RefineLane {
       for (int e = 0; e <= D; ++e) gam[a][e] = 0.0;
 #pragma unroll RU
     for (int i = 0; i < M; ++i) {
+#pragma clang fp contract(off)  // NC
       if (i >= ra.m) break;
       const double t = c[i] * mono[i];
       if constexpr (kGmap) {
@@ -351,6 +358,7 @@ struct RefineLane {
     double pen = 0.0;
 #pragma unroll RU
     for (int i = 0; i < M; ++i) {
+#pragma clang fp contract(off)  // NC
       if (i >= ra.m) {
         g[i] = 0.0;
         continue;
@@ -378,6 +386,7 @@ struct RefineLane {
     return L / norm + ra.lam * pen / (double)ra.n_coef;
   }
   __device__ double dot(const double (&a)[M], const double (&b)[M]) const {
+#pragma clang fp contract(off)  // NC
     double s = 0.0;
 #pragma unroll RU
     for (int i = 0; i < M; ++i) s += a[i] * b[i];
@@ -451,6 +460,7 @@ struct BfgsFlat {
   int li, zj, k, ls_status;
   bool ls_failed, in_zoom, z_failed, converged, failed;
   __device__ void begin_ls(const Lane& ln) {
+#pragma clang fp contract(off)  // NC
 #pragma unroll RU
     for (int i = 0; i < M; ++i) {
       double s_ = 0.0;
@@ -490,6 +500,7 @@ struct BfgsFlat {
   }
   // the first evaluation s, gs (at c0, norm 1) -> minimize_bfgs's initial state; returns whether a trial is pending
   __device__ bool start(double s, const double (&gs)[M], Lane& ln, int maxiter) {
+#pragma clang fp contract(off)  // NC
     ln.norm = s * 2.5;
     f = s / ln.norm + 0.0;
 #pragma unroll RU
@@ -605,6 +616,11 @@ struct BfgsFlat {
     if (!ls_end) return true;
     ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
     failed = ls_failed || !ls_done;
+    return update(ln, maxiter);
+  }
+  // the inverse-Hessian update and the next iterate (minimize_bfgs after its line search)
+  __device__ bool update(const Lane& ln, int maxiter) {
+#pragma clang fp contract(off)  // NC
     double sk[M], yk[M];
 #pragma unroll RU
     for (int i = 0; i < M; ++i) {
@@ -989,6 +1005,7 @@ insite_refine_kernel(RefineArgs) {
 #pragma unroll
     for (int e = 0; e <= D; ++e) gam[a][e] = 0.0;
   for (int q = 0; q < ra.n_coef; ++q) {
+#pragma clang fp contract(off)  // NC
     const int code = ra.q_code[q], mk = ra.q_mask[q], ex = code >> 24;
     const double t = coef_at(q) * monomial_code(code & 0xffffff, uu);
 #pragma unroll
@@ -1315,9 +1332,9 @@ __global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs,
 // sensitivity of tangent (arm j / 2, exponent j % 2) -- the 8 tangents of a 4-arm affine model.  Every lane runs the
 // row's state chain y (so the tangents need no broadcast), and the scalars of the line search / zoom, replicated.
 // Everything the single-lane kernel sums over coordinates (gamma, the penalty, dot products, H y, y^T H y) is
-// summed in ITS order from values shuffled within the group, and the QUAD inverse-Hessian update is the one that
-// kernel runs (RU = 1): the BFGS path is the same (statuses, iteration and evaluation counts equal, tested) and the
-// values agree to ~1e-13 (the compiler contracts a few multiply-adds differently in the two kernels).  Shuffles only read lanes of the
+// summed in ITS order from values shuffled within the group, without contraction in both kernels ("NC"), and the
+// QUAD inverse-Hessian update is the one that kernel runs (RU = 1): the outputs are bitwise the M = 16 kernel's
+// (tested).  Shuffles only read lanes of the
 // reading lane's own group, whose lanes always branch together (their replicated scalars are equal).
 #ifndef INSITE_REFINE_COOP
 #define INSITE_REFINE_COOP 1
@@ -1368,6 +1385,7 @@ insite_refine_coop_kernel(RefineArgs) {
     for (int a = 0; a < NA; ++a) gam[a][0] = gam[a][1] = 0.0;
 #pragma unroll
     for (int i = 0; i < MC; ++i) {
+#pragma clang fp contract(off)  // NC
       if (i >= ra.m) break;
       const double t = gat(c, i) * gat(mono, i);
       const int mk = ra.t_mask[i], ex = ra.t_ex[i];
@@ -1425,6 +1443,7 @@ insite_refine_coop_kernel(RefineArgs) {
     double pen = 0.0;
 #pragma unroll
     for (int i = 0; i < MC; ++i) {
+#pragma clang fp contract(off)  // NC
       const double ci = gat(c, i), c0i = gat(c0a, i);
       if (i >= ra.m) {
         if (i % kCoopG == j) g[i / kCoopG] = 0.0;
@@ -1447,6 +1466,7 @@ insite_refine_coop_kernel(RefineArgs) {
     return L / norm + ra.lam * pen / (double)ra.n_coef;
   };
   auto dot = [&](const double (&a)[S], const double (&b)[S]) -> double {
+#pragma clang fp contract(off)  // NC
     double s_ = 0.0;
 #pragma unroll
     for (int i = 0; i < MC; ++i) s_ += gat(a, i) * gat(b, i);
@@ -1466,6 +1486,7 @@ insite_refine_coop_kernel(RefineArgs) {
   bool ls_failed = false, in_zoom = false, z_failed = false, converged = false, failed = false;
   const int maxiter = 200 * ra.n_coef;
   auto begin_ls = [&]() {
+#pragma clang fp contract(off)  // NC
 #pragma unroll
     for (int s = 0; s < S; ++s) pk[s] = 0.0;
     double acc[S];
@@ -1512,6 +1533,7 @@ insite_refine_coop_kernel(RefineArgs) {
   // the start: one scan at c0 (norm 1, penalty 0), minimize_bfgs's initial state
   bool pending = false;
   {
+#pragma clang fp contract(off)  // NC
     double g0[S];
     const double start = fg(x, g0, refine);
     norm = start * 2.5;
@@ -1631,6 +1653,8 @@ insite_refine_coop_kernel(RefineArgs) {
     if (!ls_end) continue;
     ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
     failed = ls_failed || !ls_done;
+    {
+#pragma clang fp contract(off)  // NC
     double sk[S], yk[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -1673,6 +1697,7 @@ insite_refine_coop_kernel(RefineArgs) {
     f = phi_star;
     ++k;
     pending = !converged && !failed && k < maxiter;
+    }
     if (pending) begin_ls();
   }
   int status = -1, nit = 0;
@@ -1700,6 +1725,7 @@ insite_refine_coop_kernel(RefineArgs) {
 #pragma unroll
   for (int a = 0; a < NA; ++a) gam[a][0] = gam[a][1] = 0.0;
   for (int q = 0; q < ra.n_coef; ++q) {
+#pragma clang fp contract(off)  // NC
     const int code = ra.q_code[q], mk = ra.q_mask[q], ex = code >> 24;
     const double t = coef_at(q) * monomial_code(code & 0xffffff, uu);
 #pragma unroll
