@@ -325,10 +325,11 @@ struct RefineLane {
         for (int s = 0; s < ra.sub; ++s) {
 #pragma unroll
           for (int a = 0; a < NA; ++a) {
-            d[a][0] = (d[a][0] + hb * d[a][0]) + ha[a];
-            d[a][1] = (d[a][1] + hb * d[a][1]) + ha[a] * y;
+            // explicit fused forms (the cooperative kernel computes the same chain: see NC)
+            d[a][0] = fma(hb, d[a][0], d[a][0]) + ha[a];
+            d[a][1] = fma(ha[a], y, fma(hb, d[a][1], d[a][1]));
           }
-          y = y + h * (gk[0] + gk[1] * y);
+          y = fma(h, fma(gk[1], y, gk[0]), y);
         }
       } else {
         for (int s = 0; s < ra.sub; ++s) {
@@ -347,11 +348,12 @@ struct RefineLane {
         }
       }
       const double r = vk1 - y;
-      L += r * r;
+      L = fma(r, r, L);
+      const double r2 = -2.0 * r;
 #pragma unroll
       for (int a = 0; a < NA; ++a)
 #pragma unroll
-        for (int e = 0; e <= D; ++e) gG[a][e] += -2.0 * r * d[a][e];
+        for (int e = 0; e <= D; ++e) gG[a][e] = fma(r2, d[a][e], gG[a][e]);
     }
     const double iK = 1.0 / (double)K;   // (a non-live WIN lane divides by its own K too; its values are unused)
     L *= iK;
@@ -397,7 +399,7 @@ struct RefineLane {
                         bool live = true) const {
     double xt[M];
 #pragma unroll RU
-    for (int i = 0; i < M; ++i) xt[i] = x[i] + t * pk[i];
+    for (int i = 0; i < M; ++i) xt[i] = fma(t, pk[i], x[i]);
     const double f = fg(xt, g, live);
     dphi = dot(g, pk);
     return f;
@@ -484,6 +486,7 @@ struct BfgsFlat {
     in_zoom = false;
   }
   __device__ void zoom_top() {
+#pragma clang fp contract(off)  // NC
     const double dalpha = a_hi - a_lo;
     const double lo = fmin(a_hi, a_lo), hi = fmax(a_hi, a_lo);
     const double cchk = 0.2 * dalpha, qchk = 0.1 * dalpha;
@@ -526,6 +529,7 @@ struct BfgsFlat {
   }
   // one trial's value / slope / gradient -> the next state (insite_refine_kernel's FLAT loop body); returns pending
   __device__ bool advance(double phi_t, double dphi_t, const double (&g_t)[M], const Lane& ln, int maxiter) {
+#pragma clang fp contract(off)  // NC
     bool ls_end = false, ls_done = false;
     if (!in_zoom) {
       const double a_i = t_trial;
@@ -1424,13 +1428,13 @@ insite_refine_coop_kernel(RefineArgs) {
         const double ha = (ak == ta) ? h : 0.0;
 #pragma unroll 5
         for (int s = 0; s < ra.sub; ++s) {
-          // the single-lane kernel's two expressions (same contraction: a select inside one would split the fma)
-          d = te ? (d + hb * d) + ha * y : (d + hb * d) + ha;
-          y = y + h * (gk0 + gk1 * y);
+          const double dh = fma(hb, d, d);
+          d = te ? fma(ha, y, dh) : dh + ha;
+          y = fma(h, fma(gk1, y, gk0), y);
         }
         const double r = vk1 - y;
-        L += r * r;
-        gGo += -2.0 * r * d;
+        L = fma(r, r, L);
+        gGo = fma(-2.0 * r, d, gGo);
       }
     }
     const double iK = 1.0 / (double)K;
@@ -1516,6 +1520,7 @@ insite_refine_coop_kernel(RefineArgs) {
     in_zoom = false;
   };
   auto zoom_top = [&]() {
+#pragma clang fp contract(off)  // NC
     const double dalpha = a_hi - a_lo;
     const double lo = fmin(a_hi, a_lo), hi = fmax(a_hi, a_lo);
     const double cchk = 0.2 * dalpha, qchk = 0.1 * dalpha;
@@ -1559,11 +1564,13 @@ insite_refine_coop_kernel(RefineArgs) {
   while (__builtin_amdgcn_ballot_w64(pending) != 0ull) {
     double xt[S], g_t[S];
 #pragma unroll
-    for (int s = 0; s < S; ++s) xt[s] = x[s] + t_trial * pk[s];
+    for (int s = 0; s < S; ++s) xt[s] = fma(t_trial, pk[s], x[s]);
     const double phi_t = fg(xt, g_t, pending);
     const double dphi_t = dot(g_t, pk);
     if (!pending) continue;
     bool ls_end = false, ls_done = false;
+    {
+#pragma clang fp contract(off)  // NC
     if (!in_zoom) {
       const double a_i = t_trial;
       const bool s_z1 = (phi_t > phi0 + 1e-4 * a_i * dphi0) || ((phi_t >= phi_i1) && (li > 1));
@@ -1649,6 +1656,7 @@ insite_refine_coop_kernel(RefineArgs) {
       } else {
         zoom_top();
       }
+    }
     }
     if (!ls_end) continue;
     ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
