@@ -963,7 +963,8 @@ def insite4_main(args):
         stn = status.cpu().numpy()
         m_act = int((np.abs(c0) > 1e-3).sum())
         res[name] = {"active_coefficients": m_act, "ms_per_step": ms, "kernel_ms": kern_ms,
-                     "kernel": f"insite_refine_kernel<{2 if m_act <= 2 else 3 if m_act == 3 else 4 if m_act <= 4 else 8 if m_act <= 8 else 16 if m_act <= 16 else 36}, 4, 1>",
+                     "kernel": ("insite_refine_coop_kernel<16, 4>" if 8 < m_act <= 16 and os.environ.get("INSITE_REFINE_COOP", "1") != "0"
+                                else f"insite_refine_kernel<{2 if m_act <= 2 else 3 if m_act == 3 else 4 if m_act <= 4 else 8 if m_act <= 8 else 16 if m_act <= 16 else 36}, 4, 1>"),
                      "valu_f64_TFLOPs": flop / (kern_ms * 1e-3) / 1e12,
                      "frac": flop / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
                      "refined_rows": int((stn >= 0).sum()), "converged": int((stn == 0).sum()),
@@ -983,12 +984,10 @@ def insite4_main(args):
                                f"Euler-5 rollout, {N // 1000}k rows; value = the dense per-arm model", "rows": N,
                    "T": T, "arms": 4},
         "models": res,
-        "roofline": {"kernel": d["kernel"] + " (dense per-arm model: rolled loops, per-lane scratch state)",
+        "roofline": {"kernel": d["kernel"] + " (dense per-arm model: 8 lanes per row, H rows in VGPRs)",
                      "bound": "valu-f64", "unit": "TFLOP/s", "achieved": d["valu_f64_TFLOPs"],
                      "peak": FP64_VALU_PEAK_TFLOPS, "frac": d["frac"],
-                     "traffic": traffic_for("insite4", "insite_refine_kernel<16, 4, 1", args=args),
-                     "traffic_note": "per-lane scratch state of the rolled M = 16 kernel (6.3 KB per lane): the "
-                                     "counters put it at ~374 GB of HBM traffic per launch, the kernel's bound",
+                     "traffic": traffic_for("insite4", d["kernel"].split("<")[0] + "<16, 4", args=args),
                      "avg_launch_ms": d["kernel_ms"], "algorithmic_flop": d["algorithmic_flop"],
                      "flop_method": "sum over refined rows of nfev_r x K_r x (5 x (4A + 7) + 4A + 5), A = 4 arms, + N x T "
                                     "x 5 x 4 for the final scan; nfev from the kernel's own count",
