@@ -2536,6 +2536,26 @@ __device__ void fit_from_gb(const double* __restrict__ G, const double* __restri
   if (o.iters) o.iters[a] = it;
 }
 
+// XCD-aware rollout ranges (INSITE_DEF_XCD): the hardware places block b on XCD b % 8, and the rollout role cuts its
+// (tile, arm group) units into consecutive ranges per wave.  The arm-bit words of 16 neighbouring tiles share a
+// 128-B line of the time-major bit mask, so with consecutive ranges on consecutive (round-robin) XCDs every XCD's L2
+// fetched most of those lines: PMC reads 189 MB per launch against 167 MB of data (profiles/traffic_r04.json).  The
+// rollout blocks are ranked XCD-major instead -- the blocks of one XCD take one contiguous eighth of the tiles -- so a
+// line is fetched by one XCD (at the seven boundaries by two).  Which wave rolls out a patient never reaches y.
+#ifndef INSITE_DEF_XCD
+#define INSITE_DEF_XCD 1
+#endif
+constexpr int kXcds = 8;
+// #{ i in [0, n) : i % kXcds == x } for n >= 0
+__device__ __forceinline__ int64_t xcd_count(int64_t n, int x) { return (n + kXcds - 1 - x) / kXcds; }
+// rank of block b among the blocks [lo, hi) ordered XCD-major (by b % kXcds, then b)
+__device__ __forceinline__ int64_t xcd_rank(int64_t b, int64_t lo, int64_t hi) {
+  const int x = (int)(b % kXcds);
+  int64_t r = xcd_count(b, x) - xcd_count(lo, x);
+  for (int q = 0; q < x; ++q) r += xcd_count(hi, q) - xcd_count(lo, q);
+  return r;
+}
+
 // lagged = 1 (insite_fit_rollout_lagged_f64, the N > 1 schedule): block gblocks only REDUCES the previous slot to
 // the rank-local G|b (out.G, out.b; no STLSQ -- the ranks all-reduce it between launches), block gblocks + 1
 // solves the STLSQ of an all-reduced system (G_fit, b_fit -> fit), and the rollout starts at block gblocks + 2.
@@ -2589,7 +2609,9 @@ step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, con
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int64_t RW = (int64_t)(gridDim.x - first) * kWavesPerBlock;
-  const int64_t rw = (int64_t)((int)blockIdx.x - first) * kWavesPerBlock + wid;
+  const int64_t rblk = INSITE_DEF_XCD ? xcd_rank((int64_t)blockIdx.x, first, (int64_t)gridDim.x)
+                                      : (int64_t)((int)blockIdx.x - first);
+  const int64_t rw = rblk * kWavesPerBlock + wid;
   INSITE_TREAL(32768 + rw, 8);
   INSITE_THWID(32768 + rw);
   const int ng = (ra.T + kRollGS - 1) / kRollGS;
