@@ -1340,6 +1340,9 @@ __global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs,
 // QUAD inverse-Hessian update is the one that kernel runs (RU = 1): the outputs are bitwise the M = 16 kernel's
 // (tested).  Shuffles only read lanes of the
 // reading lane's own group, whose lanes always branch together (their replicated scalars are equal).
+// STG (T <= 64): the wave's 8 rows of V and of the arms are staged in LDS once (lane k loads step k of all 8 rows),
+// and every scan reads them there.  Read from global memory per step, each step of an evaluation waited for its
+// one-step-ahead loads: at 2 waves per SIMD the scan was latency-bound (~30 us per wave-evaluation).
 #ifndef INSITE_REFINE_COOP
 #define INSITE_REFINE_COOP 1
 #endif
@@ -1348,7 +1351,8 @@ __global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs,
 #endif
 constexpr int kCoopG = 8;  // lanes per row
 
-template <int MC, int NA>
+constexpr int kCoopStT = 64;  // staged steps (STG)
+template <int MC, int NA, bool STG>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_REFINE_COOP_WPE)))
 insite_refine_coop_kernel(RefineArgs) {
   constexpr int S = MC / kCoopG;  // coordinates per lane: i = j + kCoopG s
@@ -1364,6 +1368,28 @@ insite_refine_coop_kernel(RefineArgs) {
   const int64_t grc = valid ? gr : ra.N - 1;
   const int64_t p = ra.order ? (int64_t)ra.order[grc] : grc;
   const int ta = j >> 1, te = j & 1;  // this lane's tangent (arm, exponent)
+  // the wave's rows staged in LDS: [step][row slot] doubles / arm bytes (row slot = lane / 8)
+  __shared__ double sV[STG ? kWavesPerBlock * kCoopStT * kCoopG : 1];
+  __shared__ int8_t sA[STG ? kWavesPerBlock * kCoopStT * kCoopG : 1];
+  const int rs = lane / kCoopG, wv = threadIdx.x / kWave;
+  double* const wV = sV + (STG ? wv * kCoopStT * kCoopG : 0);
+  int8_t* const wA = sA + (STG ? wv * kCoopStT * kCoopG : 0);
+  if constexpr (STG) {  // (ra.T <= kCoopStT, checked at the launch)
+    long long pg[kCoopG];
+#pragma unroll
+    for (int g = 0; g < kCoopG; ++g) pg[g] = __shfl((long long)p, g * kCoopG);
+    if (lane < ra.T) {
+#pragma unroll
+      for (int g = 0; g < kCoopG; ++g) {
+        wV[lane * kCoopG + g] = ra.V[(int64_t)lane * ra.ldv + pg[g]];
+        wA[lane * kCoopG + g] = ra.arm8[(int64_t)lane * ra.lda + pg[g]];
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+  auto v_at = [&](int k) -> double { return STG ? wV[k * kCoopG + rs] : ra.V[(int64_t)k * ra.ldv + p]; };
+  auto a_at = [&](int k) -> int { return STG ? (int)wA[k * kCoopG + rs] : (int)ra.arm8[(int64_t)k * ra.lda + p]; };
   // coordinate i of a distributed vector: lane i % 8 of the group, slot i / 8
   auto gat = [&](const double (&v)[S], int i) -> double { return __shfl(v[i / kCoopG], gbase + (i % kCoopG)); };
   double uu[INSITE_MAX_STATICS];
@@ -1401,20 +1427,20 @@ insite_refine_coop_kernel(RefineArgs) {
             if (ex == e) gam[a][e] += t;
     }
     const double h = ra.dt / (double)ra.sub;
-    double y = ra.V[p];
+    double y = v_at(0);
     double d = 0.0, gGo = 0.0, L = 0.0;
     const int Kl = live ? K : 0;
     int Kw = Kl;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) Kw = max(Kw, __shfl_xor(Kw, off));
-    int ak_nx = Kw > 0 ? (int)ra.arm8[p] : 0;
-    double v_nx = Kw > 0 ? ra.V[ra.ldv + p] : 0.0;
+    int ak_nx = Kw > 0 ? a_at(0) : 0;
+    double v_nx = Kw > 0 ? v_at(1) : 0.0;
     for (int k = 0; k < Kw; ++k) {
       const int ak = ak_nx;
       const double vk1 = v_nx;
       if (k + 1 < Kw) {
-        ak_nx = (int)ra.arm8[(int64_t)(k + 1) * ra.lda + p];
-        v_nx = ra.V[(int64_t)(k + 2) * ra.ldv + p];
+        ak_nx = a_at(k + 1);
+        v_nx = v_at(k + 2);
       }
       if (k < Kl) {
         double gk0 = gam[0][0], gk1 = gam[0][1];
@@ -1744,9 +1770,9 @@ insite_refine_coop_kernel(RefineArgs) {
           if (ex == e) gam[a][e] += t;
   }
   const double h = ra.dt / (double)ra.sub;
-  double y = ra.V[p];
+  double y = v_at(0);
   for (int kk = 0; kk < ra.T; ++kk) {
-    const int ak = (int)ra.arm8[(int64_t)kk * ra.lda + p];
+    const int ak = a_at(kk);
     double gk0 = gam[0][0], gk1 = gam[0][1];
 #pragma unroll
     for (int a = 1; a < NA; ++a)
@@ -1836,7 +1862,8 @@ void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
       const bool coop = cv ? cv[0] == '1' : INSITE_REFINE_COOP != 0;
       if (NA == 4 && coop) {  // the dense 4-arm models (int8 arms): 8 lanes per row
         const dim3 gc((unsigned)((ra.N * kCoopG + kBlock - 1) / kBlock));
-        insite_refine_coop_kernel<16, 4><<<gc, kBlock, 0, hs>>>(ra);
+        if (ra.T <= kCoopStT) insite_refine_coop_kernel<16, 4, true><<<gc, kBlock, 0, hs>>>(ra);
+        else insite_refine_coop_kernel<16, 4, false><<<gc, kBlock, 0, hs>>>(ra);
       } else {
         insite_refine_kernel<16, NA, D><<<grid, kBlock, 0, hs>>>(ra);
       }
