@@ -2011,7 +2011,9 @@ constexpr int kRollGS = 32;  // steps per arm group
 // PR: 0 = one global model (ra.coef [A, F]), 1 = per-patient rows (ra.coef + p * coef_stride), 2 = the
 // factual arm's row refitted in the prologue from the patient's moments (RefitArgs rf; C4's fit folded into
 // its rollout: no per-patient coefficient round trip through HBM, one launch less).
-template <int METHOD, int NARM, int PR>
+// SR (step range): g_begin / g_end are STEPS [k_begin, k_end) instead of groups -- the stored steps of a range cut
+// at any step (the deferred step's step-balanced rollout ranges); earlier steps of the first group integrate only.
+template <int METHOD, int NARM, int PR, bool SR = false>
 __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const LibDesc& lib, const int lane,
                                                    const int64_t tile, const int g_begin, const int g_end,
                                                    const RefitArgs rf = RefitArgs{}) {
@@ -2086,10 +2088,11 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
   const int64_t arow = ra.lda * 4;   // bit rows: lda counts 32-bit words
   const int64_t abase = (p0 >> 5) * 4;
   const int arec_tail = ((nvalid + 31) >> 5) * 4;
-  const int kend = g_end * kRollGS < ra.T ? g_end * kRollGS : ra.T;  // one past the last step of the range
-  const int kbeg = g_begin * kRollGS;                                // first stored step
-  auto y_rsrc = [&](int k0) {  // rows [k0, min(k0 + kTG, T)); empty (all stores dropped) past T
-    const int rows = ra.T - k0 < kTG ? ra.T - k0 : kTG;
+  const int kend = SR ? (g_end < ra.T ? g_end : ra.T)
+                      : (g_end * kRollGS < ra.T ? g_end * kRollGS : ra.T);  // one past the last step of the range
+  const int kbeg = SR ? g_begin : g_begin * kRollGS;                   // first stored step
+  auto y_rsrc = [&](int k0) {  // rows [k0, min(k0 + kTG, kend)); empty (all stores dropped) past kend
+    const int rows = kend - k0 < kTG ? kend - k0 : kTG;
     return __builtin_amdgcn_make_buffer_rsrc((void*)(ra.y + (int64_t)(rows > 0 ? k0 : 0) * ra.ldy + p0), (short)0,
                                              rows > 0 ? (int)(((int64_t)(rows - 1) * ra.ldy + nvalid) * 8) : 0,
                                              0x00020000);
@@ -2144,15 +2147,16 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
       if (k0 < kend) {  // uniform
         const unsigned wb = bit_transpose32(aring[d], lane);
         aring[d] = grp_load(k0 + kAG * kRollGS);
-        if (k0 >= kbeg) {  // uniform: a stored group
+        if (SR ? k0 + kRollGS > kbeg : k0 >= kbeg) {  // uniform: a stored group
 #pragma unroll
           for (int hh = 0; hh < kRollGS / kTG; ++hh) {
             const __amdgpu_buffer_rsrc_t ys = y_rsrc(k0 + hh * kTG);
 #pragma unroll
             for (int i = 0; i < kTG; ++i) {
               step((int)((wb >> (hh * kTG + i)) & 1u));
-              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y), ys, yoff + (unsigned)(i * ra.ldy * 8),
-                                                    0, kStoreAux);
+              // SR: steps before kbeg (uniform) store through the dropped offset
+              const unsigned so = (!SR || k0 + hh * kTG + i >= kbeg) ? yoff + (unsigned)(i * ra.ldy * 8) : kOOB;
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y), ys, so, 0, kStoreAux);
             }
           }
         } else {  // a group before the range: integrate only
@@ -2381,6 +2385,21 @@ __device__ __forceinline__ void rollout_units(const RolloutArgs& ra, const LibDe
     q += ge - gb;
   }
 }
+// The bit-arm rollout of the (tile, step) pairs [s, s1) (tile-major, T steps a tile): one step-range
+// rollout_bits_range per tile.  Every wave of the deferred step stores the same number of steps (+-1), where the
+// (tile, 32-step group) units left ranges of 10 or 11 units with one or two 8-step tail groups among them: 272 to
+// 328 stored steps per wave at C2's shape.
+template <int METHOD>
+__device__ __forceinline__ void rollout_steps(const RolloutArgs& ra, const LibDesc& lib, const int lane, int64_t s,
+                                              const int64_t s1) {
+  while (s < s1) {
+    const int64_t tile = s / ra.T;
+    const int kb = (int)(s - tile * ra.T);
+    const int ke = s1 - s < (int64_t)(ra.T - kb) ? kb + (int)(s1 - s) : ra.T;
+    rollout_bits_range<METHOD, 2, false, true>(ra, lib, lane, tile, kb, ke);
+    s += ke - kb;
+  }
+}
 // Units [S, units) in chunks of `chunk` units claimed with the agent-scope counter rc[0] (the next claim in flight
 // while a chunk is stored); rc[1] counts the waves done claiming, and the last of the `waves` participants resets
 // both.  Which wave stores a chunk never reaches y (every chunk is a rollout_bits_range).
@@ -2545,6 +2564,16 @@ __device__ void fit_from_gb(const double* __restrict__ G, const double* __restri
 #ifndef INSITE_DEF_XCD
 #define INSITE_DEF_XCD 1
 #endif
+// INSITE_DEF_STEPS (A/B, off): the rollout role's ranges balanced in stored steps (rollout_steps) instead of (tile,
+// group) units.  Measured slower on one box, interleaved 3 x 100 steps: 0.0738-0.0743 ms vs 0.0715-0.0721 ms with the
+// unit ranges (profiles/r04/steps/): the per-step store predicate and the mid-group range ends cost more than the
+// 272-328 stored steps per wave of the unit split.
+#ifndef INSITE_DEF_STEPS
+#define INSITE_DEF_STEPS 0
+#endif
+#if INSITE_DEF_STEPS && INSITE_DEF_RSTATIC < 1000
+#error "the claimed rollout tail (INSITE_DEF_RSTATIC < 1000) cuts (tile, group) units: build with INSITE_DEF_STEPS=0"
+#endif
 constexpr int kXcds = 8;
 // #{ i in [0, n) : i % kXcds == x } for n >= 0
 __device__ __forceinline__ int64_t xcd_count(int64_t n, int x) { return (n + kXcds - 1 - x) / kXcds; }
@@ -2616,9 +2645,16 @@ step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, con
   INSITE_THWID(32768 + rw);
   const int ng = (ra.T + kRollGS - 1) / kRollGS;
   const int64_t units = (ra.N + kWave - 1) / kWave * ng;  // (tile, arm group) pairs, tile-major
+#if INSITE_DEF_STEPS  // (the claimed tail, INSITE_DEF_RSTATIC < 1000, needs INSITE_DEF_STEPS=0)
+  (void)units;
+  (void)rc;
+  const int64_t SS = (ra.N + kWave - 1) / kWave * ra.T;  // (tile, step) pairs
+  rollout_steps<METHOD>(ra, lib, lane, rw * SS / RW, (rw + 1) * SS / RW);
+#else
   const int64_t S = rc ? units * INSITE_DEF_RSTATIC / 1000 : units;
   rollout_units<METHOD>(ra, lib, lane, rw * S / RW, (rw + 1) * S / RW, ng);
   if (rc) rollout_claimed<METHOD>(ra, lib, lane, S, units, ng, INSITE_DEF_RCHUNK, rc, RW);
+#endif
   INSITE_TSTAMP(32768 + rw, 0);
   INSITE_TREAL(32768 + rw, 9);
 }
