@@ -148,6 +148,41 @@ __device__ __forceinline__ int pm_slot_index(int r, int col) {
 // same wait as a builtin the compiler's waitcnt pass sees, so it knows its own earlier loads (the scan's y0) have
 // completed too.  With the asm alone the pass kept a vmcnt(0) for y0 inside the sub-step loop -- which, executed
 // with a ring prefetch in flight, waited for the prefetch every step that issued one.
+// CF (INSITE_REFINE_CF, the objective scans of the affine models, D = 1): the n = ra.sub Euler sub-steps of a step
+// on arm a are the affine map y <- P_a y + B_a with q = 1 + h gamma_{a,1}, P_a = q^n, B_a = h gamma_{a,0} S,
+// S = sum_{j<n} q^j, and the tangents follow in closed form from the step's start y:
+//   d/dgamma_{b,e} <- P_a d                         (b != a: the other arms' tangents only scale)
+//   d/dgamma_{a,0} <- P_a d + h S,   d/dgamma_{a,1} <- P_a d + n h q^(n-1) y + h^2 gamma_{a,0} sum_{j<=n-2} (j+1) q^j
+// (the sums of the recurrences d <- q d + h, d <- q d + h y_s over the sub-steps): one FMA per value and step instead
+// of n.  The objective's rounding is the restatement's own (the oracle and the reference differentiate the sub-step
+// form; jax in reverse mode): the GPU matches the oracle per row to the tests' tolerances, and the final predictions
+// (sindy.py:668) keep the sub-step form.  Every kernel computing an objective uses it (the single-lane, dynamic and
+// cooperative kernels stay bitwise equal to each other).
+#ifndef INSITE_REFINE_CF
+#define INSITE_REFINE_CF 1
+#endif
+// the per-arm constants of CF for one evaluation
+struct CfArm {
+  double P, B, hS, C1, C2;
+};
+__device__ __forceinline__ CfArm cf_arm(double g0, double g1, double h, int n) {
+  const double q = 1.0 + h * g1;
+  double pw = 1.0, S = 0.0, Cs = 0.0, qn1 = 1.0;
+  for (int j = 0; j < n; ++j) {  // pw = q^j
+    if (j + 1 < n) Cs = fma((double)(j + 1), pw, Cs);
+    S += pw;
+    qn1 = pw;
+    pw *= q;
+  }
+  CfArm c;
+  c.P = pw;
+  c.B = h * g0 * S;
+  c.hS = h * S;
+  c.C1 = (double)n * h * qn1;
+  c.C2 = h * h * g0 * Cs;
+  return c;
+}
+
 __device__ __forceinline__ void ring_wait() {
   __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0) expcnt(7) lgkmcnt(15)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -276,6 +311,12 @@ struct RefineLane {
     double v_nx = WIN ? 0.0 : ra.V[ra.ldv + p];
     const int kend = WIN ? (PM ? Kw : nch * kWin) : Kl;
     const int lbase = PM ? pm_lane_base(threadIdx.x & (kWave - 1)) : 0, lrot = PM ? pm_lane_rot(threadIdx.x & (kWave - 1)) : 0;
+    constexpr bool kCf = INSITE_REFINE_CF && D == 1;
+    CfArm cfa[kCf ? NA : 1];
+    if constexpr (kCf) {
+#pragma unroll
+      for (int a = 0; a < NA; ++a) cfa[a] = cf_arm(gam[a][0], gam[a][1], h, ra.sub);
+    }
     for (int k = 0; k < kend; ++k) {
       int ak;
       double vk1;
@@ -313,7 +354,19 @@ struct RefineLane {
         if (ak == a)
 #pragma unroll
           for (int e = 0; e <= D; ++e) gk[e] = gam[a][e];
-      if constexpr (D == 1) {
+      if constexpr (kCf) {
+        CfArm c = cfa[0];
+#pragma unroll
+        for (int a = 1; a < NA; ++a)
+          if (ak == a) c = cfa[a];
+        const double a1 = fma(c.C1, y, c.C2);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+          d[a][0] = fma(c.P, d[a][0], ak == a ? c.hS : 0.0);
+          d[a][1] = fma(c.P, d[a][1], ak == a ? a1 : 0.0);
+        }
+        y = fma(c.P, y, c.B);
+      } else if constexpr (D == 1) {
         const double hb = h * gk[1];
         // the step's arm selects its tangent's source term once per step, not per sub-step: an inactive arm
         // adds +0.0 and 0 * y (bitwise the untouched value for finite y), so the sub-step loop has no
@@ -1435,6 +1488,11 @@ insite_refine_coop_kernel(RefineArgs) {
     for (int off = 32; off >= 1; off >>= 1) Kw = max(Kw, __shfl_xor(Kw, off));
     int ak_nx = Kw > 0 ? a_at(0) : 0;
     double v_nx = Kw > 0 ? v_at(1) : 0.0;
+    CfArm cfa[INSITE_REFINE_CF ? NA : 1];
+    if constexpr (INSITE_REFINE_CF) {
+#pragma unroll
+      for (int a = 0; a < NA; ++a) cfa[a] = cf_arm(gam[a][0], gam[a][1], h, ra.sub);
+    }
     for (int k = 0; k < Kw; ++k) {
       const int ak = ak_nx;
       const double vk1 = v_nx;
@@ -1442,7 +1500,18 @@ insite_refine_coop_kernel(RefineArgs) {
         ak_nx = a_at(k + 1);
         v_nx = v_at(k + 2);
       }
-      if (k < Kl) {
+      if (INSITE_REFINE_CF && k < Kl) {
+        CfArm c = cfa[0];
+#pragma unroll
+        for (int a = 1; a < NA; ++a)
+          if (ak == a) c = cfa[a];
+        const double add = ak == ta ? (te ? fma(c.C1, y, c.C2) : c.hS) : 0.0;
+        d = fma(c.P, d, add);
+        y = fma(c.P, y, c.B);
+        const double r = vk1 - y;
+        L = fma(r, r, L);
+        gGo = fma(-2.0 * r, d, gGo);
+      } else if (k < Kl) {
         double gk0 = gam[0][0], gk1 = gam[0][1];
 #pragma unroll
         for (int a = 1; a < NA; ++a)
