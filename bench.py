@@ -805,7 +805,10 @@ def insite_main(args):
                      "algorithmic_flop": flop, "flop_per_sensitivity_step": per_step,
                      "flop_method": "sum over refined rows of nfev_r x K_r (K_r = min(seq_len - tau, T - 1)) x "
                                     "(5 Euler sub-steps x (4A + 7) + 4A + 5) with A = 2 arms, + N x T x 5 x 4 for "
-                                    "the final scan; nfev from the kernel's own count (insite_refine_general_f64)",
+                                    "the final scan; nfev from the kernel's own count (insite_refine_general_f64).  The reference's "
+                                    "sub-step work: the kernel evaluates the objective scans' sub-steps in closed form "
+                                    "(INSITE_REFINE_CF, one FMA per value and step), so this is work done per second "
+                                    "in the reference's terms, not executed instructions",
                      "algorithmic_bytes": kbytes, "achieved_GBps": kbytes / (kern_ms * 1e-3) / 1e9,
                      "avg_ms_source": "HIP events on the launch stream around args.steps back-to-back launches of "
                                       "insite_refine_rows_f64 with the step's lane order (the sort excluded)"},
@@ -990,7 +993,8 @@ def insite4_main(args):
                      "traffic": traffic_for("insite4", d["kernel"].split("<")[0] + "<16, 4", args=args),
                      "avg_launch_ms": d["kernel_ms"], "algorithmic_flop": d["algorithmic_flop"],
                      "flop_method": "sum over refined rows of nfev_r x K_r x (5 x (4A + 7) + 4A + 5), A = 4 arms, + N x T "
-                                    "x 5 x 4 for the final scan; nfev from the kernel's own count",
+                                    "x 5 x 4 for the final scan; nfev from the kernel's own count (the reference's sub-step work; "
+                                    "the objective scans run it in closed form, INSITE_REFINE_CF)",
                      "algorithmic_bytes": kb, "achieved_GBps": kb / (d["kernel_ms"] * 1e-3) / 1e9},
     }
     if cpu is not None:
