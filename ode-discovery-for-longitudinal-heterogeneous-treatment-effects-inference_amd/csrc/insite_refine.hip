@@ -1399,12 +1399,37 @@ __global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs,
 #ifndef INSITE_REFINE_COOP
 #define INSITE_REFINE_COOP 1
 #endif
+#ifndef INSITE_REFINE_SWZ
+#define INSITE_REFINE_SWZ 1  // the group gathers as ds_swizzle (0: ds_bpermute through __shfl)
+#endif
 #ifndef INSITE_REFINE_COOP_WPE
 #define INSITE_REFINE_COOP_WPE 2
 #endif
 constexpr int kCoopG = 8;  // lanes per row
 
 constexpr int kCoopStT = 64;  // staged steps (STG)
+// lane C of the reading lane's 8-lane group: ds_swizzle in bitmask mode (and 0x18, or C: the group's base within the
+// 32-lane half, plus C) -- the value of __shfl(v, group base + C) without the per-lane address of ds_bpermute
+template <int C>
+__device__ __forceinline__ double grp_lane(double v) {
+  static_assert(C >= 0 && C < 8, "lane of an 8-lane group");
+  constexpr int kPat = 0x18 | (C << 5);
+  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), kPat);
+  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), kPat);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double grp_lane(double v, int c) {  // c a constant after unrolling
+  switch (c & 7) {
+    case 0: return grp_lane<0>(v);
+    case 1: return grp_lane<1>(v);
+    case 2: return grp_lane<2>(v);
+    case 3: return grp_lane<3>(v);
+    case 4: return grp_lane<4>(v);
+    case 5: return grp_lane<5>(v);
+    case 6: return grp_lane<6>(v);
+    default: return grp_lane<7>(v);
+  }
+}
 template <int MC, int NA, bool STG>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_REFINE_COOP_WPE)))
 insite_refine_coop_kernel(RefineArgs) {
@@ -1444,7 +1469,9 @@ insite_refine_coop_kernel(RefineArgs) {
   auto v_at = [&](int k) -> double { return STG ? wV[k * kCoopG + rs] : ra.V[(int64_t)k * ra.ldv + p]; };
   auto a_at = [&](int k) -> int { return STG ? (int)wA[k * kCoopG + rs] : (int)ra.arm8[(int64_t)k * ra.lda + p]; };
   // coordinate i of a distributed vector: lane i % 8 of the group, slot i / 8
-  auto gat = [&](const double (&v)[S], int i) -> double { return __shfl(v[i / kCoopG], gbase + (i % kCoopG)); };
+  auto gat = [&](const double (&v)[S], int i) -> double {
+    return INSITE_REFINE_SWZ ? grp_lane(v[i / kCoopG], i % kCoopG) : __shfl(v[i / kCoopG], gbase + (i % kCoopG));
+  };
   double uu[INSITE_MAX_STATICS];
 #pragma unroll
   for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < ra.U ? ra.u[p * ra.U + t] : 0.0;
@@ -1538,7 +1565,7 @@ insite_refine_coop_kernel(RefineArgs) {
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
-      for (int e = 0; e <= 1; ++e) gG[a][e] = __shfl(gGo, gbase + 2 * a + e);
+      for (int e = 0; e <= 1; ++e) gG[a][e] = INSITE_REFINE_SWZ ? grp_lane(gGo, 2 * a + e) : __shfl(gGo, gbase + 2 * a + e);
     double pen = 0.0;
 #pragma unroll
     for (int i = 0; i < MC; ++i) {
