@@ -161,6 +161,14 @@ __device__ __forceinline__ int pm_slot_index(int r, int col) {
 #ifndef INSITE_REFINE_CF
 #define INSITE_REFINE_CF 1
 #endif
+// RELOAD: the objective re-reads the active terms' routing (t_mask / t_ex, kernel-argument words) in every
+// evaluation through a pointer laundered by an empty asm, instead of the compiler keeping 2 M of them live in SGPRs
+// across the whole BFGS (the M = 16 cooperative kernel spilled 262 SGPRs into VGPR lanes; 72 after).  Cooperative
+// kernel only: the single-lane kernels evaluate inside per-lane control flow, where the SGPR-constrained asm operand
+// is not available (the backend rejects the VGPR -> SGPR copy).
+#ifndef INSITE_REFINE_RELOAD
+#define INSITE_REFINE_RELOAD 1
+#endif
 // the per-arm constants of CF for one evaluation
 struct CfArm {
   double P, B, hS, C1, C2;
@@ -258,6 +266,7 @@ struct RefineLane {
   // scans 0 steps and only keeps the wave's ring loads company
   __device__ double fg(const double (&c)[M], double (&g)[M], bool live = true) const {
     nev += live ? 1 : 0;
+    const auto tmk = ra.t_mask, tex = ra.t_ex;  // (the single-lane kernels call fg in divergent code: no RELOAD)
     double gam[NA][D + 1];
 #pragma unroll
     for (int a = 0; a < NA; ++a)
@@ -275,7 +284,7 @@ struct RefineLane {
           for (int e = 0; e <= D; ++e)
             if ((ra.gmap >> (i * 8 + a * 2 + e)) & 1) gam[a][e] += t;
       } else {
-        const int mk = ra.t_mask[i], ex = ra.t_ex[i];
+        const int mk = tmk[i], ex = tex[i];
 #pragma unroll
         for (int a = 0; a < NA; ++a)
           if ((mk >> a) & 1)
@@ -428,7 +437,7 @@ struct RefineLane {
           for (int e = 0; e <= D; ++e)
             if ((ra.gmap >> (i * 8 + a * 2 + e)) & 1) gd += gG[a][e];
       } else {
-        const int mk = ra.t_mask[i], ex = ra.t_ex[i];
+        const int mk = tmk[i], ex = tex[i];
 #pragma unroll
         for (int a = 0; a < NA; ++a)
           if ((mk >> a) & 1)
@@ -1490,6 +1499,11 @@ insite_refine_coop_kernel(RefineArgs) {
   // f and its gradient at c (RefineLane::fg, D = 1, the non-windowed scan); every lane of the wave calls it
   auto fg = [&](const double (&c)[S], double (&g)[S], bool live) -> double {
     nev += live ? 1 : 0;
+    // the routing tables re-read (scalar loads) in every evaluation: the laundered pointers keep the compiler from
+    // holding 2 MC kernel-argument words live in SGPRs across the BFGS (they spilled into VGPR lanes)
+    typedef const __attribute__((address_space(4))) int32_t* KInt;
+    KInt tmk = ra.t_mask, tex = ra.t_ex;
+    if (INSITE_REFINE_RELOAD) asm volatile("" : "+s"(tmk), "+s"(tex));
     double gam[NA][2];
 #pragma unroll
     for (int a = 0; a < NA; ++a) gam[a][0] = gam[a][1] = 0.0;
@@ -1498,7 +1512,7 @@ insite_refine_coop_kernel(RefineArgs) {
 #pragma clang fp contract(off)  // NC
       if (i >= ra.m) break;
       const double t = gat(c, i) * gat(mono, i);
-      const int mk = ra.t_mask[i], ex = ra.t_ex[i];
+      const int mk = tmk[i], ex = tex[i];
 #pragma unroll
       for (int a = 0; a < NA; ++a)
         if ((mk >> a) & 1)
@@ -1578,7 +1592,7 @@ insite_refine_coop_kernel(RefineArgs) {
       const double dd = c0i - ci;
       pen += dd * dd;
       if (i % kCoopG == j) {
-        const int mk = ra.t_mask[i], ex = ra.t_ex[i];
+        const int mk = tmk[i], ex = tex[i];
         double gd = 0.0;
 #pragma unroll
         for (int a = 0; a < NA; ++a)
