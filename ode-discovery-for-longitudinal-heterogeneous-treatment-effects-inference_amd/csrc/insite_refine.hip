@@ -1507,11 +1507,21 @@ insite_refine_coop_kernel(RefineArgs) {
     double gam[NA][2];
 #pragma unroll
     for (int a = 0; a < NA; ++a) gam[a][0] = gam[a][1] = 0.0;
+    // per-coordinate values are formed on their owner lane and gathered once (the same roundings as forming them
+    // from two gathered operands on the reading lane: one gather per coordinate instead of two)
+    double tm[S], sq[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+#pragma clang fp contract(off)  // NC
+      tm[s] = c[s] * mono[s];
+      const double dd = c0a[s] - c[s];
+      sq[s] = dd * dd;
+    }
 #pragma unroll
     for (int i = 0; i < MC; ++i) {
 #pragma clang fp contract(off)  // NC
       if (i >= ra.m) break;
-      const double t = gat(c, i) * gat(mono, i);
+      const double t = gat(tm, i);  // c_i m_i, formed on coordinate i's lane
       const int mk = tmk[i], ex = tex[i];
 #pragma unroll
       for (int a = 0; a < NA; ++a)
@@ -1584,14 +1594,14 @@ insite_refine_coop_kernel(RefineArgs) {
 #pragma unroll
     for (int i = 0; i < MC; ++i) {
 #pragma clang fp contract(off)  // NC
-      const double ci = gat(c, i), c0i = gat(c0a, i);
+      const double sqi = gat(sq, i);
       if (i >= ra.m) {
         if (i % kCoopG == j) g[i / kCoopG] = 0.0;
         continue;
       }
-      const double dd = c0i - ci;
-      pen += dd * dd;
+      pen += sqi;
       if (i % kCoopG == j) {
+        const double ci = c[i / kCoopG], c0i = c0a[i / kCoopG];
         const int mk = tmk[i], ex = tex[i];
         double gd = 0.0;
 #pragma unroll
@@ -1607,9 +1617,12 @@ insite_refine_coop_kernel(RefineArgs) {
   };
   auto dot = [&](const double (&a)[S], const double (&b)[S]) -> double {
 #pragma clang fp contract(off)  // NC
+    double pr[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) pr[s] = a[s] * b[s];
     double s_ = 0.0;
 #pragma unroll
-    for (int i = 0; i < MC; ++i) s_ += gat(a, i) * gat(b, i);
+    for (int i = 0; i < MC; ++i) s_ += gat(pr, i);
     return s_;
   };
   // ---- the flat BFGS state machine (BfgsFlat with the vectors distributed; the QUAD update of RU = 1) ----
@@ -1816,9 +1829,7 @@ insite_refine_coop_kernel(RefineArgs) {
 #pragma unroll
         for (int s = 0; s < S; ++s) hy[s] += Hr[s][q] * yq;
       }
-      double yhy = 0.0;
-#pragma unroll
-      for (int i = 0; i < MC; ++i) yhy += gat(yk, i) * gat(hy, i);
+      const double yhy = dot(yk, hy);  // sum_i yk_i hy_i in coordinate order
       const double cs = rho * rho * yhy + rho;
 #pragma unroll
       for (int q = 0; q < MC; ++q) {
@@ -1835,7 +1846,9 @@ insite_refine_coop_kernel(RefineArgs) {
       g[s] = g_star[s];
     }
 #pragma unroll
-    for (int i = 0; i < MC; ++i) gm = fmax(gm, fabs(gat(g, i)));
+    for (int s = 0; s < S; ++s) gm = fmax(gm, fabs(g[s]));
+#pragma unroll
+    for (int off = 1; off < kCoopG; off <<= 1) gm = fmax(gm, __shfl_xor(gm, off));  // (max: any order)
     converged = gm < 1e-5;
     old_old = f;
     f = phi_star;
