@@ -1411,6 +1411,12 @@ __global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs,
 #ifndef INSITE_REFINE_SWZ
 #define INSITE_REFINE_SWZ 1  // the group gathers as ds_swizzle (0: ds_bpermute through __shfl)
 #endif
+#ifndef INSITE_REFINE_COOP8
+#define INSITE_REFINE_COOP8 0  // A/B: the cooperative kernel for 5-8 active terms on 4 arms
+#endif
+// (measured: the sparse 4-arm line's 5-term model 11.3 ms cooperative vs 6.5 ms one lane per row -- with one
+// coordinate a lane the group's 8-fold replicated scan and line search cost more than the single-lane kernel's
+// spills; profiles/r04/coop8/)
 #ifndef INSITE_REFINE_COOP_WPE
 #define INSITE_REFINE_COOP_WPE 2
 #endif
@@ -1979,7 +1985,17 @@ void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
     if (m <= 2) insite_refine_kernel<2, NA, D><<<grid, kBlock, 0, hs>>>(ra);
     else if (m == 3) insite_refine_kernel<3, NA, D><<<grid, kBlock, 0, hs>>>(ra);
     else if (m <= 4) insite_refine_kernel<4, NA, D><<<grid, kBlock, 0, hs>>>(ra);
-    else if (m <= 8) insite_refine_kernel<8, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+    else if (m <= 8) {
+      const char* cv = getenv("INSITE_REFINE_COOP8");
+      const bool coop = cv ? cv[0] == '1' : INSITE_REFINE_COOP8 != 0;
+      if (NA == 4 && coop) {  // the sparse 4-arm models with 5-8 active terms: 8 lanes per row, one coordinate a lane
+        const dim3 gc((unsigned)((ra.N * kCoopG + kBlock - 1) / kBlock));
+        if (ra.T <= kCoopStT) insite_refine_coop_kernel<8, 4, true><<<gc, kBlock, 0, hs>>>(ra);
+        else insite_refine_coop_kernel<8, 4, false><<<gc, kBlock, 0, hs>>>(ra);
+      } else {
+        insite_refine_kernel<8, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+      }
+    }
     else if (m <= 16) {
       const char* cv = getenv("INSITE_REFINE_COOP");
       const bool coop = cv ? cv[0] == '1' : INSITE_REFINE_COOP != 0;
