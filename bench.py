@@ -967,7 +967,7 @@ def insite4_main(args):
         m_act = int((np.abs(c0) > 1e-3).sum())
         res[name] = {"active_coefficients": m_act, "ms_per_step": ms, "kernel_ms": kern_ms,
                      "kernel": ("insite_refine_coop_kernel<16, 4>" if 8 < m_act <= 16 and os.environ.get("INSITE_REFINE_COOP", "1") != "0"
-                                else f"insite_refine_kernel<{2 if m_act <= 2 else 3 if m_act == 3 else 4 if m_act <= 4 else 8 if m_act <= 8 else 16 if m_act <= 16 else 36}, 4, 1>"),
+                                else f"insite_refine_kernel<{2 if m_act <= 2 else 3 if m_act == 3 else 4 if m_act <= 4 else 6 if m_act <= 6 else 8 if m_act <= 8 else 16 if m_act <= 16 else 36}, 4, 1>"),
                      "valu_f64_TFLOPs": flop / (kern_ms * 1e-3) / 1e12,
                      "frac": flop / (kern_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
                      "refined_rows": int((stn >= 0).sum()), "converged": int((stn == 0).sum()),

@@ -1411,6 +1411,9 @@ __global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs,
 #ifndef INSITE_REFINE_SWZ
 #define INSITE_REFINE_SWZ 1  // the group gathers as ds_swizzle (0: ds_bpermute through __shfl)
 #endif
+#ifndef INSITE_REFINE_M6
+#define INSITE_REFINE_M6 1  // a kernel sized for 5-6 active terms (the M = 8 one held its state in AGPRs at 1 wave)
+#endif
 #ifndef INSITE_REFINE_COOP8
 #define INSITE_REFINE_COOP8 0  // A/B: the cooperative kernel for 5-8 active terms on 4 arms
 #endif
@@ -1985,6 +1988,7 @@ void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
     if (m <= 2) insite_refine_kernel<2, NA, D><<<grid, kBlock, 0, hs>>>(ra);
     else if (m == 3) insite_refine_kernel<3, NA, D><<<grid, kBlock, 0, hs>>>(ra);
     else if (m <= 4) insite_refine_kernel<4, NA, D><<<grid, kBlock, 0, hs>>>(ra);
+    else if (m <= 6 && INSITE_REFINE_M6) insite_refine_kernel<6, NA, D><<<grid, kBlock, 0, hs>>>(ra);
     else if (m <= 8) {
       const char* cv = getenv("INSITE_REFINE_COOP8");
       const bool coop = cv ? cv[0] == '1' : INSITE_REFINE_COOP8 != 0;
