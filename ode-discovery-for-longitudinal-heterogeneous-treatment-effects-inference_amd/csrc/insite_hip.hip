@@ -2911,6 +2911,9 @@ rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
 #ifndef INSITE_RK45_MINSTEP_BRANCH
 #define INSITE_RK45_MINSTEP_BRANCH 0
 #endif
+#ifndef INSITE_RK45_HSEL
+#define INSITE_RK45_HSEL 1
+#endif
 #ifndef INSITE_RK45_CLOSE_BRANCH
 #define INSITE_RK45_CLOSE_BRANCH 0  // 1: round 2's close block under `if (close)` (A/B)
 #endif
@@ -3179,12 +3182,28 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
       }
 #endif
       const double r5 = rk45_inv_root5(rarg);
+#if INSITE_RK45_HSEL
+      // every candidate computed, then selected: the conditional form compiled to three exec-mask branches
+      double factor = fmin(10.0, 0.9 * r5);
+      factor = err == 0.0 ? 10.0 : factor;
+      const double factor_r = fmin(1.0, factor);
+      factor = rejected ? factor_r : factor;
+      const double h_init = init_h(r5);
+      const double h_acc = h_abs * factor;
+      const double h_rej = h_abs * fmax(0.2, 0.9 * r5);
+      const double ms = min_step();
+      double h_next = acc ? h_acc : h_rej;
+      h_next = close ? h_init : h_next;
+      const double h_new = fmax(h_next, ms);
+      h_abs = acc ? h_new : h_next;
+#else
       double factor = err == 0.0 ? 10.0 : fmin(10.0, 0.9 * r5);
       if (rejected) factor = fmin(1.0, factor);
       const double h_next = close ? init_h(r5) : acc ? h_abs * factor : h_abs * fmax(0.2, 0.9 * r5);
       // a new step starts after an accept or a close (gating the bit-exact min_step on a wave ballot of the
       // steps it could raise measured slower: 0.93 -> 0.98 ms, profiles/r02/c5_minstep/)
       h_abs = acc ? fmax(h_next, min_step()) : h_next;
+#endif
       rejected = !acc;
     }
   }
