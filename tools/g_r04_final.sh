@@ -9,7 +9,7 @@ tail -2 $O/smoke.txt
 timeout -k 10 300 python bench.py > $O/bench_default.jsonl 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
 python3 -c "
 import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('default', round(d['ms_per_step'],5), 'frac', round(d['roofline']['frac'],4), d.get('parity'))" $O/bench_default.jsonl
-for c in insite insite4; do
+for c in ${LINES:-insite insite4}; do
   timeout -k 10 400 python bench.py --config $c > $O/bench_$c.jsonl 2> $O/bench_$c.err || { echo "bench $c failed"; tail -5 $O/bench_$c.err; exit 1; }
   python3 -c "
 import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); cb=d.get('cpu_baseline') or {}
