@@ -435,6 +435,11 @@ constexpr int kGramSmem = kWavesPerBlock * kWave * kGSlot;  // doubles of LDS pe
 #ifndef INSITE_GRAM_ORDER
 #define INSITE_GRAM_ORDER 0
 #endif
+// cache policy of the gram's time-major x loads (A/B: 2 = non-temporal, x is read once per launch; measured slower
+// on the C2 step, 0.0706-0.0709 vs 0.0685-0.0692 ms launches, profiles/r04/lnt/)
+#ifndef INSITE_GRAM_LOAD_AUX
+#define INSITE_GRAM_LOAD_AUX 0
+#endif
 __device__ __forceinline__ int64_t gram_item_tile(int64_t item, int n_seg, int64_t n_tiles) {
   return INSITE_GRAM_ORDER ? item % n_tiles : item / n_seg;
 }
@@ -528,7 +533,8 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
         (void*)(x + (int64_t)(nrow > 0 ? t0 : 0) * ldx + q0), (short)0, bytes, 0x00020000);
 #pragma unroll
     for (int i = 0; i < kGT; ++i)
-      v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, qoff + (unsigned)(i * ldx * 8), 0, 0));
+      v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, qoff + (unsigned)(i * ldx * 8), 0,
+                                                                             INSITE_GRAM_LOAD_AUX));
   };
   for (int64_t cur = ranged ? wv * units / nW : wv; cur < c_end;) {
     const Piece pc = piece_of(cur);
