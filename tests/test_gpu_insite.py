@@ -485,17 +485,17 @@ def test_refine_rows_dynamic_assignment_equals_static(dev, monkeypatch, N, T, m,
 F4_COEF = [[0.0, 0.20, 0.0, 0.0], [0.0, 0.0, 0.0, -0.60], [0.0, -0.30, 0.0, 0.0], [0.0, -0.25, 0.0, -0.90]]
 
 
-@pytest.mark.parametrize("N,joint", [(3_000, False), (517, False), (2_000, True)])
-def test_cooperative_dense_refine_equals_single_lane(dev, monkeypatch, N, joint):
+@pytest.mark.parametrize("N,joint,T", [(3_000, False, 60), (517, False, 60), (2_000, True, 60), (600, False, 80)])
+def test_cooperative_dense_refine_equals_single_lane(dev, monkeypatch, N, joint, T):
     """The cooperative kernel for the dense 4-arm models (8 lanes per row, H rows and coordinates distributed,
     INSITE_REFINE_COOP) against the one-row-per-lane M = 16 kernel (INSITE_REFINE_COOP=0): predictions,
     coefficients, statuses, iteration and evaluation counts bitwise equal (every sum over coefficients is taken in the
     single-lane kernel's order and without contraction in both, insite_refine.hip "NC") -- the dense per-arm model
     (16 active coefficients, cancer_sim's shape) and the joint one-ODE model over (x, chemo, radio, u0); ragged
-    seq_len incl. rows <= tau, a partial last wave."""
+    seq_len incl. rows <= tau, a partial last wave; T = 80 takes the kernel's unstaged path (rows read per step,
+    T > 64)."""
     from insite_amd import cohort, ops
     from insite_amd.library import polynomial_library
-    T = 60
     coh = cohort.synthetic_segments(N, T, seed=N + 11, device=dev, coef=F4_COEF, dt=0.1)
     V = coh.x[:T, :N].t().contiguous()
     arm = coh.arm[:, :N].t().contiguous()
