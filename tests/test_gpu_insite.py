@@ -56,6 +56,32 @@ def test_refine_matches_oracle(dev, model, tau):
     assert (status[sl <= tau] == -1).all() and (iters[sl > tau] > 0).all()
 
 
+def test_refine_matches_oracle_long_rows(dev):
+    """T = 90 > 64: the refinement's per-step-load kernel (no window ring, no 64-bit arm mask) with the closed-form
+    objective scans, against the oracle row by row (statuses, coefficients, predictions), arm switches included."""
+    coll = R.make_collection("EQ_4_C", {"train": 120, "val": 10, "test": 10}, seq_length=90, seed=5)
+    tr = coll["train"]
+    x, u, arm, rows = R.de_format(tr.data, tr.scaling_params)
+    G, b = R.gram_moments(x, u, arm, rows, R.STANDARD_DT, EX)
+    c0 = np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)])
+    rng = np.random.default_rng(90)
+    N, T, tau = 100, x.shape[1], 5
+    assert T > 64
+    V = x[:N].copy()
+    arms = np.repeat(arm[:N, None], T, axis=1).astype(np.int8)
+    flip = rng.integers(10, T, N)
+    for i in range(0, N, 2):
+        arms[i, flip[i]:] = 1 - arms[i, flip[i]:]
+    sl = rng.integers(1, T + 1, N).astype(np.int32)
+    sl[:3] = [tau, tau + 1, T]
+    preds, coef, status, iters = _run(dev, V, arms, u[:N], sl, c0, tau)
+    for p in range(N):
+        rp, rc, rs, ri = Q.refine_patient(V[p], arms[p], u[p], sl[p], c0, EX, R.STANDARD_DT, 10.0, tau)
+        assert status[p] == rs, (p, status[p], rs)
+        assert np.abs(coef[p] - rc).max() <= 1e-7 * max(1.0, np.abs(rc).max()), p
+        assert np.sqrt(np.mean((preds[p] - rp) ** 2)) <= 1e-6
+
+
 def test_refined_model_fits_better_than_global(dev, model):
     coll, x, u, arm, c0 = model
     N, T = 100, x.shape[1]
