@@ -74,7 +74,9 @@ def parse():
                          "library's default split)")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
     ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
-    ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the benched cohort (C2)")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the oracle check of the benched cohort (every line: a sample of the last timed step's "
+                         "rows through the oracle after the timed region)")
     ap.add_argument("--force-collective", action="store_true",
                     help="C2 at N = 1: join a single-rank RCCL process group and run the N > 1 pipeline's data path "
                          "(gram, one bucketed all_reduce per batch, STLSQ) so the collective and the process "
@@ -440,6 +442,8 @@ def c3_main(args):
                     "frac": roll_bytes / (roll_ms_t * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                     "dense_kernel_avg_launch_ms": roll_dense_t},
     }
+    if not args.no_parity:
+        out["parity"] = c3_parity(coh, a_cf, lib, T, G, B, coef, mask, y)
     if cpu is not None:
         out["cpu_baseline"] = cpu
     emit(out)
@@ -608,6 +612,9 @@ def c5_main(args):
                  "wave_divergence": float((per_wave.max(dim=1).values.mean() / per_wave.mean()).item()),
                  "rhs_evals_per_s": float(st.sum() * 6 / (launch_ms * 1e-3))},
     }
+    if world == 1 and not args.no_parity:
+        out["parity"] = c5_parity(y0, u, arm, t_obs, n_obs, coef, lib, y, steps,
+                                  ops.rk45_order(n_obs, Tm) if order else torch.arange(N, device=dev))
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:
@@ -615,6 +622,300 @@ def c5_main(args):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------------------------------
+# Oracle parity of the timed cohorts (the metric's "RMSE vs CPU ref" for every line): after
+# the timed region, a sample of the rows the last timed step computed goes through the oracle restatement on a
+# SPAWNED pool of the host's workers (fresh interpreters that never touch the GPU; fork is not safe once this
+# process holds a GPU context).  The checker only -- nothing here is timed or feeds the product path.
+# --------------------------------------------------------------------------------------------------
+def _par_init():
+    _cpu_worker_init()
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+
+
+def parity_map(fn, jobs):
+    import multiprocessing as mp
+    W = min(host_info()["workers"], len(jobs))
+    if W <= 1:
+        _par_init()
+        return [fn(j) for j in jobs]
+    with mp.get_context("spawn").Pool(W, initializer=_par_init) as pool:
+        return pool.map(fn, jobs)
+
+
+def sample_rows(N, n, seed, extra=()):
+    """A fixed sample of row indices: n random rows, the first and last 64 and any ``extra`` (e.g. the first and
+    last lanes of a binned order)."""
+    rng = np.random.default_rng(seed)
+    idx = [rng.choice(N, min(n, N), replace=False), np.arange(min(64, N)), np.arange(max(0, N - 64), N)]
+    idx += [np.asarray(e, dtype=np.int64).reshape(-1) for e in extra]
+    return np.unique(np.concatenate(idx))
+
+
+def _par_refine_job(job):
+    from oracle import insite_refine_ref as Q
+    V, arm, u, sl, c0, ex, dt, lam, tau, n_in = job
+    out = [Q.refine_patient(V[i], arm[i], u[i], int(sl[i]), c0, ex, dt, lam, tau, n_inputs=n_in)
+           for i in range(V.shape[0])]
+    return (np.stack([o[0] for o in out]), np.stack([np.asarray(o[1]).reshape(-1) for o in out]),
+            np.array([o[2] for o in out]), np.array([o[3] for o in out]))
+
+
+def insite_parity(V, arm, u, sl, c0, lib, dt, lam, tau, preds, coef, status, iters, n_sample=4096, seed=13,
+                  extra=()):
+    """The INSITE lines' parity: ``n_sample`` rows of the timed cohort (plus ``extra``, e.g. the first / last lanes
+    of the binned order) through oracle/insite_refine_ref.refine_patient (the reference's jax BFGS restated,
+    sindy.py:587-665, 781-794) against the rows the last timed step wrote: per-row status and iteration count
+    equality (reported as fractions: the GPU's closed-form objective scans round differently from the sub-step
+    form, so an ill-conditioned row can take another BFGS path), refined coefficients, predictions."""
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    N, T = V.shape
+    idx = sample_rows(N, n_sample, seed, extra)
+    it = torch.as_tensor(idx, device=V.device)
+
+    def h(t):
+        return t.index_select(0, it).cpu().numpy()
+    Vh, ah, uh, slh = h(V), h(arm).astype(np.int64), h(u), h(sl)
+    ex = lib.exps.astype(np.int64)
+    W = host_info()["workers"]
+    parts = [c for c in np.array_split(np.arange(idx.size), 4 * W) if c.size]
+    t0 = time.perf_counter()
+    res = parity_map(_par_refine_job, [(Vh[c], ah[c], uh[c], slh[c], np.asarray(c0, dtype=np.float64), ex, dt, lam,
+                                        tau, int(lib.n_inputs)) for c in parts])
+    el = time.perf_counter() - t0
+    P, C = np.concatenate([r[0] for r in res]), np.concatenate([r[1] for r in res])
+    S, I = np.concatenate([r[2] for r in res]), np.concatenate([r[3] for r in res])
+    gp, gc, gs, gi = h(preds), h(coef).reshape(idx.size, -1), h(status), h(iters)
+    same = gs == S
+    ref_ = S >= 0
+    d = gp - P
+    rel = np.abs(d) / np.maximum(np.abs(P), 1e-300)
+    return {"oracle": "oracle/insite_refine_ref.refine_patient (jax BFGS + line search + zoom restated, numpy; "
+                      "sindy.py:587-665, 781-794)",
+            "cohort": f"the last timed step's rows ({N} x {T})", "rows_sampled": int(idx.size),
+            "refined_rows": int(ref_.sum()), "status_equal_frac": float(same.mean()),
+            "iterations_equal_frac": float((gi[ref_] == I[ref_]).mean()) if ref_.any() else 1.0,
+            "pred_rmse": float(np.sqrt(np.mean(d ** 2))), "pred_max_rel": float(rel.max()),
+            "pred_max_rel_status_equal": float(rel[same].max()) if same.any() else None,
+            "coef_linf": float(np.abs(gc - C).max()),
+            "coef_linf_status_equal": float(np.abs(gc - C)[same].max()) if same.any() else None,
+            "oracle_seconds": el,
+            "tolerances": {"status_equal_frac": 1.0, "pred_rmse": 1e-6, "coef_linf_status_equal": 1e-7}}
+
+
+def _par_rk45_job(job):
+    from oracle import rk45_ref as K
+    return K.rollout_rk45(*job)
+
+
+def c5_parity(y0, u, arm, t_obs, n_obs, coef, lib, y, steps, order, n_sample=4096, seed=5):
+    """C5: sampled rows of the timed cohort (first / last lanes of the binned order included) through
+    oracle/rk45_ref.rollout_rk45 (scipy 1.15 solve_ivp RK45 restated, pinned to solve_ivp at 1e-13) against the
+    trajectories and per-patient attempt counts the last timed launch wrote."""
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    N = y0.numel()
+    o = order.cpu().numpy()
+    idx = sample_rows(N, n_sample, seed, extra=(o[:64], o[-64:], o[N // 2 - 32:N // 2 + 32]))
+    it = torch.as_tensor(idx, device=y0.device)
+    tn = t_obs.index_select(1, it).t().contiguous().cpu().numpy()
+    nn, y0h, uh, ah = (v.index_select(0, it).cpu().numpy() for v in (n_obs, y0, u, arm))
+    ch, ex = coef.cpu().numpy(), lib.exps.astype(np.int64)
+    parts = [c for c in np.array_split(np.arange(idx.size), 4 * host_info()["workers"]) if c.size]
+    t0 = time.perf_counter()
+    res = parity_map(_par_rk45_job, [(y0h[c], uh[c], ah[c], tn[c], nn[c], ch, ex) for c in parts])
+    el = time.perf_counter() - t0
+    ref = np.concatenate([r[0] for r in res])
+    rs = np.concatenate([r[1] for r in res])
+    got = y.index_select(0, it).cpu().numpy()[:, :ref.shape[1]]
+    st = steps.index_select(0, it).cpu().numpy()
+    valid = ~np.isnan(ref)
+    same = st == rs
+    d = np.where(valid, got - ref, 0.0)
+    rel = np.abs(d) / np.where(valid, np.abs(ref), 1.0)
+    return {"oracle": "oracle/rk45_ref.rollout_rk45 (scipy 1.15 RK45 restated, pinned to solve_ivp)",
+            "cohort": f"the last timed launch's rows ({N} patients)", "rows_sampled": int(idx.size),
+            "attempts_equal_frac": float(same.mean()), "y_rmse": float(np.sqrt(np.sum(d ** 2) / valid.sum())),
+            "y_max_rel": float(rel.max()), "y_max_rel_attempts_equal": float(rel[same].max()) if same.any() else None,
+            "oracle_seconds": el, "tolerances": {"y_rmse": 1e-6, "y_max_rel": 1e-9, "attempts_equal_frac": 0.999}}
+
+
+def _unpack_bits_rows(bits, idx, T):
+    """time-major bit words [T, W] (int32 tensor) -> [n, T] int64 arms of the rows idx (tensor on its device)."""
+    words = bits[:T].index_select(1, idx // 32)
+    return ((words >> (idx % 32).to(torch.int32)[None, :]) & 1).t().contiguous().cpu().numpy().astype(np.int64)
+
+
+def _par_gram_job(job):
+    from oracle import insite_ref as R
+    return R.gram_moments_vectorized(*job)
+
+
+def _par_ppfit_roll_job(job):
+    from oracle import insite_ref as R
+    x, u, arm, rows, dt, ex, gc, y0, arms_cf = job
+    pc, pm, pi = R.per_patient_fit(x, u, arm, rows, dt, ex, gc, 0.1, 0.5)
+    return pc, pm, pi, R.rollout(y0, u, arms_cf, pc, ex, dt, method="euler5")
+
+
+def c4_parity(coh, arm_cf, lib, T, gcoef, gmask, pout, y, n_sample=4096, seed=3):
+    """C4: the global model against the oracle's Gram-form STLSQ over the WHOLE timed cohort (chunked vectorised
+    Gram on the host's workers), and on sampled rows the per-patient refits (oracle/insite_ref.per_patient_fit, the
+    LSQIntialMask restatement, pkpd_simulation.py:791-800) and their Euler-5 rollouts (sindy.py:767-778) against
+    the refits and the trajectories of the last timed launch."""
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    from oracle import insite_ref as R
+    N = coh.arm.numel()
+    rows = coh.rows.cpu().numpy()
+    if not np.all(rows == rows[0]):
+        return {"skipped": "ragged rows (the vectorised oracle Gram needs equal rows)"}
+    ex = lib.exps.astype(np.int64)
+    un, an = coh.u.cpu().numpy(), coh.arm.cpu().numpy().astype(np.int64)
+    W = host_info()["workers"]
+    bounds = [(int(c[0]), int(c[-1]) + 1) for c in np.array_split(np.arange(N), 2 * W) if c.size]
+    t0 = time.perf_counter()
+    gb = parity_map(_par_gram_job, [(coh.x[:T, lo:hi].t().contiguous().cpu().numpy(), un[lo:hi], an[lo:hi],
+                                     int(rows[0]), coh.dt, ex) for lo, hi in bounds])
+    G, b = sum(q[0] for q in gb), sum(q[1] for q in gb)
+    cr = np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)])
+    idx = sample_rows(N, n_sample, seed)
+    it = torch.as_tensor(idx, device=coh.x.device)
+    xs = coh.x[:T].index_select(1, it).t().contiguous().cpu().numpy()
+    us, ars, rws = un[idx], an[idx], rows[idx]
+    y0 = coh.y0.index_select(0, it).cpu().numpy()
+    acf = _unpack_bits_rows(arm_cf, it, T)
+    gc = gcoef.cpu().numpy()
+    parts = [c for c in np.array_split(np.arange(idx.size), 4 * W) if c.size]
+    res = parity_map(_par_ppfit_roll_job, [(xs[c], us[c], ars[c], rws[c], coh.dt, ex, gc, y0[c], acf[c])
+                                           for c in parts])
+    el = time.perf_counter() - t0
+    pc = np.concatenate([r[0] for r in res])
+    pm = np.concatenate([r[1] for r in res])
+    pi = np.concatenate([r[2] for r in res])
+    yr = np.concatenate([r[3] for r in res])
+    got_y = y.index_select(1, it).t().cpu().numpy()
+    d = got_y - yr
+    gpc = pout[0].index_select(0, it).cpu().numpy()
+    return {"oracle": "oracle/insite_ref.py (gram_moments_vectorized + stlsq_gram over the whole cohort; "
+                      "per_patient_fit + rollout euler5 on the sample)",
+            "cohort": f"the timed cohort ({N} x {T})", "rows_sampled": int(idx.size),
+            "global_support_equal": bool(np.array_equal(gmask.cpu().numpy() != 0, cr != 0)),
+            "global_coef_linf": float(np.abs(gc - cr).max()),
+            "per_patient_support_equal_frac": float((pout[1].index_select(0, it).cpu().numpy() == pm).all(1).mean()),
+            "per_patient_iterations_equal_frac": float((pout[2].index_select(0, it).cpu().numpy() == pi).mean()),
+            "per_patient_coef_linf": float(np.abs(gpc - pc).max()),
+            "y_rmse": float(np.sqrt(np.mean(d ** 2))),
+            "y_max_rel": float((np.abs(d) / np.maximum(np.abs(yr), 1e-300)).max()), "oracle_seconds": el,
+            "tolerances": {"global_coef_linf": 1e-8, "per_patient_coef_linf": 1e-8, "y_rmse": 1e-6}}
+
+
+def _par_seg_gram_job(job):
+    from oracle import segments_ref as S
+    return S.gram_segments_vectorized(*job)
+
+
+def _par_roll_job(job):
+    from oracle import insite_ref as R
+    y0, u, arms, coef, ex, dt, method = job
+    return R.rollout(y0, u, arms, coef, ex, dt, method=method)
+
+
+def f4_parity(coh, arm_cf, lib, T, coef, mask, y, n_sample=4096, seed=31):
+    """F4: the four per-arm models against the oracle's segment Gram (oracle/segments_ref.gram_segments_vectorized,
+    the reference's segment walk in index form, pkpd/utils.py:433-462, 607-637) over the WHOLE timed cohort + STLSQ
+    (threshold 0.001), and the Euler-5 4-arm rollout of sampled rows against the trajectories of the last step."""
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    from oracle import insite_ref as R
+    N = coh.u.size(0)
+    ex = lib.exps.astype(np.int64)
+    un = coh.u.cpu().numpy()
+    sl = coh.seq_len.cpu().numpy().astype(np.int64)
+    W = host_info()["workers"]
+    bounds = [(int(c[0]), int(c[-1]) + 1) for c in np.array_split(np.arange(N), 2 * W) if c.size]
+    t0 = time.perf_counter()
+    gb = parity_map(_par_seg_gram_job, [(coh.x[:, lo:hi].t().contiguous().cpu().numpy(), un[lo:hi],
+                                         coh.arm[:, lo:hi].t().contiguous().cpu().numpy().astype(np.int64), sl[lo:hi],
+                                         coh.dt, ex) for lo, hi in bounds])
+    G, b = sum(q[0] for q in gb), sum(q[1] for q in gb)
+    cr = np.stack([R.stlsq_gram(G[k], b[k], 0.001, 0.5)[0] for k in range(4)])
+    idx = sample_rows(N, n_sample, seed)
+    it = torch.as_tensor(idx, device=coh.x.device)
+    y0 = coh.x[0].index_select(0, it).cpu().numpy()
+    acf = arm_cf[:T].index_select(1, it).t().contiguous().cpu().numpy().astype(np.int64)
+    parts = [c for c in np.array_split(np.arange(idx.size), 4 * W) if c.size]
+    yr = np.concatenate(parity_map(_par_roll_job, [(y0[c], un[idx][c], acf[c], cr, ex, coh.dt, "euler5")
+                                                   for c in parts]))
+    el = time.perf_counter() - t0
+    d = y.index_select(1, it).t().cpu().numpy() - yr
+    return {"oracle": "oracle/segments_ref.gram_segments_vectorized + insite_ref.stlsq_gram over the whole cohort; "
+                      "insite_ref.rollout euler5 on the sample",
+            "cohort": f"the timed cohort ({N} x {T}, 4 arms)", "rows_sampled": int(idx.size),
+            "support_equal": bool(np.array_equal(mask.cpu().numpy() != 0, cr != 0)),
+            "coef_linf": float(np.abs(coef.cpu().numpy() - cr).max()),
+            "y_rmse": float(np.sqrt(np.mean(d ** 2))),
+            "y_max_rel": float((np.abs(d) / np.maximum(np.abs(yr), 1e-300)).max()), "oracle_seconds": el,
+            "tolerances": {"coef_linf": 1e-8, "y_rmse": 1e-6}}
+
+
+def _par_ms_roll_job(job):
+    from oracle import multistate_ref as M
+    y0, a, coef, ex, dt = job
+    return M.ms_rollout(y0, a, coef, ex, dt, "rk4")
+
+
+def c3_parity(coh, a_cf, lib, T, G, B, coef, mask, y, n_sample=2048, seed=23):
+    """C3: the Gram of sampled sub-cohorts (first tile, an unaligned middle range, the partial last tile) through
+    the product kernel against oracle/multistate_ref.ms_gram, the STLSQ of the timed step's full Gram against
+    ms_stlsq, and the fp32 RK4 rollout of sampled rows against ms_rollout (fp64)."""
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    from insite_amd import multistate as MS
+    from insite_amd import ops
+    from oracle import multistate_ref as M
+    N = coh.x.size(2)
+    ex = lib.exps.astype(np.int64)
+
+    def unpack(bits, lo, hi):
+        b_ = bits[:T].cpu().numpy().view(np.uint32)
+        r = np.arange(lo, hi)
+        return ((b_[:, r >> 5] >> (r & 31).astype(np.uint32)) & 1).T.astype(np.int8)
+    t0 = time.perf_counter()
+    cuts = [(0, 64), (N // 2 - 32, N // 2 + 64), (max(0, N - 96), N)]
+    gmax = 0.0
+    for lo, hi in cuts:
+        lo -= lo % 32
+        g_, b_ = MS.gram_ms(coh.x[:, :, lo:hi].contiguous(), coh.a[:, lo // 32:(hi + 31) // 32].contiguous(), lib,
+                            coh.dt, workspace=ops.Workspace())
+        xn = np.transpose(coh.x[:, :, lo:hi].cpu().numpy(), (2, 0, 1))
+        Gr, Br = M.ms_gram(xn, unpack(coh.a, lo, hi), np.full(hi - lo, T), coh.dt, ex)
+        gmax = max(gmax, float(np.max(np.abs(g_.cpu().numpy() - Gr) / np.maximum(np.abs(Gr), 1.0))),
+                   float(np.max(np.abs(b_.cpu().numpy() - Br) / np.maximum(np.abs(Br), 1.0))))
+    c_ref, m_ref, _ = M.ms_stlsq(G.cpu().numpy(), B.cpu().numpy())
+    idx = sample_rows(N, n_sample, seed)
+    it = torch.as_tensor(idx, device=coh.x.device)
+    y0 = coh.y0.index_select(1, it).t().cpu().numpy().astype(np.float64)
+    words = a_cf[:T].index_select(1, it // 32)
+    acf = ((words >> (it % 32).to(torch.int32)[None, :]) & 1).t().contiguous().cpu().numpy().astype(np.int8)
+    cg = coef.cpu().numpy()
+    parts = [c for c in np.array_split(np.arange(idx.size), 4 * host_info()["workers"]) if c.size]
+    yr = np.concatenate(parity_map(_par_ms_roll_job, [(y0[c], acf[c], cg, ex, coh.dt) for c in parts]))
+    el = time.perf_counter() - t0
+    got = np.transpose(y.index_select(2, it).cpu().numpy(), (2, 0, 1)).astype(np.float64)
+    rel = np.abs(got - yr) / np.maximum(np.abs(yr), 1e-2)
+    return {"oracle": "oracle/multistate_ref.py (ms_gram on sampled sub-cohorts, ms_stlsq on the step's Gram, "
+                      "ms_rollout rk4 fp64 on sampled rows)",
+            "cohort": f"the timed cohort ({N} x {T} x {lib.n_states})", "rows_sampled": int(idx.size),
+            "gram_max_rel_sampled_tiles": gmax, "support_equal": bool(np.array_equal(mask.cpu().numpy() != 0, m_ref)),
+            "coef_linf": float(np.abs(cg - c_ref).max()),
+            "y_max_rel_fp32_vs_fp64": float(rel.max()), "y_rmse": float(np.sqrt(np.mean((got - yr) ** 2))),
+            "oracle_seconds": el,
+            "tolerances": {"gram_max_rel_sampled_tiles": 1e-10, "coef_linf": 1e-8, "y_max_rel_fp32_vs_fp64": 1e-4}}
 
 
 def _cpu_pp_init(*data):
@@ -813,6 +1114,10 @@ def insite_main(args):
                      "avg_ms_source": "HIP events on the launch stream around args.steps back-to-back launches of "
                                       "insite_refine_rows_f64 with the step's lane order (the sort excluded)"},
     }
+    if not args.no_parity:
+        o_ = plan.order.long()
+        out["parity"] = insite_parity(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, preds, coef, status, iters,
+                                      extra=(o_[:64].cpu().numpy(), o_[-64:].cpu().numpy()))
     if cpu is not None:
         out["cpu_baseline"] = cpu
     emit(out)
@@ -975,6 +1280,11 @@ def insite4_main(args):
                      "mean_evaluations_per_refined_row": float(nf.to(torch.float64)[s2 >= 0].mean().item()),
                      "equal_to_nfev_route": bool(torch.equal(p2, preds) and torch.equal(s2, status)),
                      "finite_predictions": bool(torch.isfinite(preds).all().item()), "algorithmic_flop": flop}
+        if not args.no_parity:   # the dense / joint oracle rows cost ~4 ms each on one host core
+            o_ = plan.order.long() if getattr(plan, "order", None) is not None else torch.arange(N, device=dev)
+            res[name]["parity"] = insite_parity(V, arm, u, sl, c0, lb, dt, 10.0, 5, preds, coef, status, iters,
+                                                n_sample=4096 if name == "sparse" else 2048, seed=17,
+                                                extra=(o_[:64].cpu().numpy(), o_[-64:].cpu().numpy()))
     d = res["dense"]
     kb = N * T * (8 + 1 + 8) + N * (8 + 4) + N * (16 * 8 + 8)
     out = {
@@ -997,6 +1307,8 @@ def insite4_main(args):
                                     "the objective scans run it in closed form, INSITE_REFINE_CF)",
                      "algorithmic_bytes": kb, "achieved_GBps": kb / (d["kernel_ms"] * 1e-3) / 1e9},
     }
+    if "parity" in d:
+        out["parity"] = dict(d["parity"], model="dense (the line's value); every model's in models.*.parity")
     if cpu is not None:
         out["cpu_baseline"] = cpu
     emit(out)
@@ -1092,6 +1404,8 @@ def f4_main(args):
                     "algorithmic_bytes": rb, "achieved_GBps": rb / (roll_ms * 1e-3) / 1e9,
                     "frac": rb / (roll_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS},
     }
+    if not args.no_parity:
+        res["parity"] = f4_parity(coh, arm_cf, lib, T, out[0], out[1], y)
     if not args.no_cpu_baseline:
         sys.path.insert(0, ROOT)
         from oracle import insite_ref as R
@@ -1251,6 +1565,9 @@ def c4_main(args):
                 "per_patient_fit_GBps": pb / (pp_ms * 1e-3) / 1e9, "rollout_ms": roll_ms, "rollout_bytes": rb,
                 "rollout_GBps": rb / (roll_ms * 1e-3) / 1e9, "sum_ms": pp_ms + roll_ms},
         }
+        if world == 1 and not args.no_parity:
+            sys.path.insert(0, ROOT)
+            res["parity"] = c4_parity(coh, arm_cf, lib, T, gout[0], gout[1], pout, y)
         if world == 1 and not args.no_cpu_baseline:
             sys.path.insert(0, ROOT)
             from oracle import insite_ref as R
@@ -2286,6 +2603,9 @@ def main():
         del y
         torch.cuda.empty_cache()
         out["north_star_rollout"] = north_star_rollout(args, dev, coef, lib)
+    if world == 1 and not args.no_parity:
+        out["parity"] = c5_parity(y0, u, arm, t_obs, n_obs, coef, lib, y, steps,
+                                  ops.rk45_order(n_obs, Tm) if order else torch.arange(N, device=dev))
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:

@@ -307,8 +307,11 @@ def line_search(fg, xk, pk, old_fval, old_old_fval, gfk, maxiter=LS_MAXITER):
                 status=status, nfev=st["nfev"])
 
 
-def minimize_bfgs(fg, x0, maxiter, gtol=GTOL):
-    """jax minimize_bfgs (norm = inf): returns (x, f, status, iterations, function evaluations)."""
+def minimize_bfgs(fg, x0, maxiter, gtol=GTOL, ls_maxiter=LS_MAXITER):
+    """jax minimize_bfgs (norm = inf): returns (x, f, status, iterations, function evaluations).
+    ``gtol`` / ``maxiter`` / ``ls_maxiter`` are jax's ``minimize_bfgs`` options (defaults 1e-5, 200 * size,
+    10); the reference passes none of them (sindy.py:627), they are exposed for the stopping-control sweep
+    (tools/insite_stop_sweep.py)."""
     d = x0.size
     H = np.eye(d)
     f, g = fg(x0)
@@ -321,7 +324,7 @@ def minimize_bfgs(fg, x0, maxiter, gtol=GTOL):
     ls_status = 0
     while (not converged) and (not failed) and k < maxiter:
         p = -(H @ g)
-        ls = line_search(fg, x, p, f, old_old, g)
+        ls = line_search(fg, x, p, f, old_old, g, maxiter=ls_maxiter)
         nfev += ls["nfev"]
         failed = ls["failed"]
         ls_status = ls["status"]
@@ -364,11 +367,14 @@ def euler5_rollout(V0, arms, u, coef, exps, dt, T, n_inputs=0):
     return out
 
 
-def refine_patient(V, arms, u, sl, c0, exps, dt, lam, tau, revert_on_zoom_fail=False, n_inputs=0):
+def refine_patient(V, arms, u, sl, c0, exps, dt, lam, tau, revert_on_zoom_fail=False, n_inputs=0,
+                   gtol=GTOL, maxiter=None, ls_maxiter=LS_MAXITER, revert_statuses=None):
     """One patient of ``simulate_cancer_volume_with_fine_tuning`` (sindy.py:570-668).  Returns
     (preds [T'], refined coefficients [A, F], status, iterations); status -1 = skipped (sl <= tau).
     ``revert_on_zoom_fail``: status 3 keeps c0 (sindy.py:628-631); default False = the published runs
-    (module docstring).  ``n_inputs`` > 0: the joint model (c0 [1, F], arms = treatment bit codes)."""
+    (module docstring).  ``n_inputs`` > 0: the joint model (c0 [1, F], arms = treatment bit codes).
+    ``gtol`` / ``maxiter`` (default 200 * c0.size, jax's) / ``ls_maxiter`` / ``revert_statuses`` (a set of
+    statuses that keep c0, overriding ``revert_on_zoom_fail``) exist for the stopping-control sweep only."""
     T = V.shape[0]
     c0 = np.asarray(c0, dtype=np.float64)
     if sl <= tau:
@@ -377,9 +383,12 @@ def refine_patient(V, arms, u, sl, c0, exps, dt, lam, tau, revert_on_zoom_fail=F
     pb = PatientProblem(V, arms, u, c0, exps, K, dt, lam, n_inputs=n_inputs)
     start, _ = pb.value_and_grad(pb.c0)          # norm_const = 1, penalty 0 at c0
     pb.norm = start * 2.5
-    x, f, status, k, _ = minimize_bfgs(pb.value_and_grad, pb.c0.copy(), maxiter=200 * c0.size)
+    x, f, status, k, _ = minimize_bfgs(pb.value_and_grad, pb.c0.copy(),
+                                       maxiter=200 * c0.size if maxiter is None else int(maxiter),
+                                       gtol=gtol, ls_maxiter=ls_maxiter)
     c = c0.copy()
-    if status != 3 or not revert_on_zoom_fail:
+    revert = (status in revert_statuses) if revert_statuses is not None else (status == 3 and revert_on_zoom_fail)
+    if not revert:
         for xi, t in zip(x, pb.terms):
             c.flat[t[0]] = xi
     return euler5_rollout(V[0], arms, u, c, exps, dt, T, n_inputs), c, status, k

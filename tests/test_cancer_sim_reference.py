@@ -26,6 +26,7 @@ import numpy as np
 import pytest
 
 from oracle import cancer_sim_ref as CS
+from oracle import insite_ref as R
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ANCHORS = json.load(open(os.path.join(HERE, "golden", "reference_log_anchors.json")))
@@ -109,23 +110,64 @@ def test_one_ode_joint_model_equals_log():
         assert res[k] == pytest.approx(anchor[k], rel=1e-11), k
 
 
-def test_insite_restatement_vs_published_runs_bands():
+def test_insite_restatement_vs_published_runs_frozen_gap():
     """The restated INSITE refinement (tests/golden/segment_insite_oracle.json, regenerated by the committed
-    make_segment_insite_oracle.py) against the PUBLISHED INSITE runs on the bit-identical cohorts: within the
-    DESIGN.md §3 bands (cancer_sim / EQ_5_C <= 1.5e-3, EQ_5_B / D <= 4 %, the one-ODE joint runs <= 22 %), and
-    the gap has the recorded shape -- the published runs' fitted window carries MORE squared error than the
-    restatement's, while their last (counterfactual) entry agrees within 1 %."""
+    make_segment_insite_oracle.py) against the PUBLISHED INSITE runs on the bit-identical cohorts: every metric's
+    relative gap equals its FROZEN value (tests/golden/insite_published_gap.json, 5e-4 absolute) -- the published
+    runs are not reproducible by the restated algorithm (the round-5 stopping-control sweep moves no
+    gap), so the gap itself is pinned and a move of either sign fails.  The gap has the recorded shape: the
+    published runs' fitted window carries MORE squared error than the restatement's, while their last
+    (counterfactual) entry agrees within 1 %."""
     import json
     import os
     here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
     fx = json.load(open(os.path.join(here, "segment_insite_oracle.json")))
-    bands = {"cancer_sim": 1.5e-3, "EQ_5_C": 1.0e-3, "EQ_5_B": 3.0e-2, "EQ_5_D": 4.0e-2,
-             "ABLATION_ONE_ODE/cancer_sim": 0.22}
-    for key, band in bands.items():
+    frozen = json.load(open(os.path.join(here, "insite_published_gap.json")))
+    tol = frozen["tolerance_abs"]
+    assert set(frozen["gap"]) == set(fx)
+    for key, gap in frozen["gap"].items():
         rel = fx[key]["log_rel_diff"]
-        assert len(rel) == 8 and all(abs(v) <= band for v in rel.values()), (key, rel)
+        assert set(rel) == set(gap) and len(rel) == 8, key
+        off = {k: (rel[k], gap[k]) for k in gap if abs(rel[k] - gap[k]) > tol}
+        assert not off, (key, off)
     for eq in ("cancer_sim", "EQ_5_B", "EQ_5_C", "EQ_5_D"):
         d = fx[eq]["one_step_decomposition"]
         w, last = d["in_window_sse"], d["last_entry_sse"]
         assert w["oracle"] < w["log_implied"] < w["sindy_model"], (eq, w)
         assert abs(last["log_implied"] / last["oracle"] - 1) < 1e-2, (eq, last)
+
+
+def _refine_rows_eq5(args):
+    from oracle import insite_refine_ref as Q
+    prev, arms, stat, sl, c0, exps = args
+    return [Q.refine_patient(prev[i], arms[i], stat[i], int(sl[i]), c0, exps, R.STANDARD_DT, 10.0, 1)[0]
+            for i in range(prev.shape[0])]
+
+
+def test_insite_restatement_reproduces_fixture_eq5d_one_step():
+    """The fixture is the restatement's own output: EQ_5_D's one-step INSITE metrics recomputed live (21,860
+    refinements over the host's cores) equal segment_insite_oracle.json to 1e-9 -- so the frozen published-run gap
+    above is the live oracle's, not a stale file's."""
+    import json
+    import os
+    from concurrent.futures import ProcessPoolExecutor
+    fx = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                     "segment_insite_oracle.json")))["EQ_5_D"]["oracle"]
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        coll = CS.make_collection(1, equation="EQ_5_D")
+    pipe = CS.sindy_pipeline(coll)
+    one = coll["test_cf_one_step"]
+    U = one.data["static_features"].shape[-1]
+    prev, st = R.unscale_inputs(one.data, one.scaling_params, 1, U)
+    st = np.repeat(st[:, :1], U, axis=1)                    # the EQ_5 refinement's u1 = static_features[0]
+    arms = np.argmax(one.data["current_treatments"], axis=-1)
+    sl = one.data["sequence_lengths"].astype(np.int64)
+    chunks = np.array_split(np.arange(prev.shape[0]), 64)
+    with ProcessPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        P = np.stack([p for o in ex.map(_refine_rows_eq5, [(prev[c], arms[c], st[c], sl[c], pipe["joint_coefs"],
+                                                               pipe["exps"]) for c in chunks]) for p in o])
+    m = R.masked_rmse(P[..., None], one.data["unscaled_outputs"], one.data["active_entries"],
+                      CS.TUMOUR_DEATH_THRESHOLD, one_step_counterfactual=True)
+    for v, k in zip(m, ["encoder_test_rmse_orig", "encoder_test_rmse_all", "encoder_test_rmse_last"]):
+        assert v == pytest.approx(fx[k], rel=1e-9), k
