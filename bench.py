@@ -701,10 +701,12 @@ def insite_parity(V, arm, u, sl, c0, lib, dt, lam, tau, preds, coef, status, ite
             "iterations_equal_frac": float((gi[ref_] == I[ref_]).mean()) if ref_.any() else 1.0,
             "pred_rmse": float(np.sqrt(np.mean(d ** 2))), "pred_max_rel": float(rel.max()),
             "pred_max_rel_status_equal": float(rel[same].max()) if same.any() else None,
+            "status_mismatch_pairs_gpu_oracle": {f"{a}/{b}": int(((gs == a) & (S == b)).sum())
+                                                 for a, b in sorted(set(zip(gs[~same].tolist(), S[~same].tolist())))},
             "coef_linf": float(np.abs(gc - C).max()),
             "coef_linf_status_equal": float(np.abs(gc - C)[same].max()) if same.any() else None,
             "oracle_seconds": el,
-            "tolerances": {"status_equal_frac": 1.0, "pred_rmse": 1e-6, "coef_linf_status_equal": 1e-7}}
+            "tolerances": {"status_equal_frac": 0.995, "pred_rmse": 1e-6, "coef_linf": 1e-7}}
 
 
 def _par_rk45_job(job):
@@ -976,6 +978,25 @@ def insite_cpu_baseline(seed, per_worker=2000):
                       f"U{{1..59}}) over a {W}-process pool, {el:.2f} s", "host": info}
 
 
+def insite_rows(N, T, seed, dev):
+    """The INSITE line's rows (also tests/test_gpu_insite.py's bench-size parity cohort): an on-device EQ_4_C
+    cohort, patient-major V [N, T], per-step int8 arms (the factual arm flipped at a random step), seq_len
+    U{1..T-1}, and the global model of the EQ_4_C log (final_with_insite.txt:182).  Returns
+    (cohort, V, arm, seq_len, c0, dt)."""
+    from insite_amd import cohort
+    coh = cohort.synthetic_pkpd(N, T, seed=seed + 9, device=dev, equation="EQ_4_C")
+    V = coh.x[:, :T].contiguous()
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed + 10)
+    flip = torch.randint(1, T, (N, 1), generator=g, device=dev)
+    arm = torch.where(torch.arange(T, device=dev)[None, :] >= flip, 1 - coh.arm[:, None].to(torch.int64),
+                      coh.arm[:, None].to(torch.int64)).to(torch.int8).contiguous()
+    sl = torch.randint(1, T, (N,), generator=g, device=dev, dtype=torch.int32)
+    c0 = np.zeros((2, coh.lib.n_terms))
+    c0[0, 4], c0[1, 1], c0[1, 5] = -1.1107592869834308, -0.14540553723951796, -1.0234639833519243  # log :182
+    return coh, V, arm, sl, c0, 10.0 / T
+
+
 def insite_main(args):
     """INSITE per-patient refinement (reference sindy.py:433-715): every row of a
     counterfactual evaluation set refines the global EQ_4_C model by BFGS on its observed prefix
@@ -984,22 +1005,12 @@ def insite_main(args):
     refinement of every row (1M rows; the reference's tau-step test set has 59,000)."""
     # the CPU leg first, while this process has no GPU context (its worker pool forks)
     cpu = None if args.no_cpu_baseline else insite_cpu_baseline(args.seed)
-    from insite_amd import ops, cohort
+    from insite_amd import ops
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     N = args.patients if args.patients != 100_000 else 1_000_000
     T = 60
-    coh = cohort.synthetic_pkpd(N, T, seed=args.seed + 9, device=dev, equation="EQ_4_C")
-    V = coh.x[:, :T].contiguous()
-    g = torch.Generator(device=dev)
-    g.manual_seed(args.seed + 10)
-    flip = torch.randint(1, T, (N, 1), generator=g, device=dev)
-    arm = torch.where(torch.arange(T, device=dev)[None, :] >= flip, 1 - coh.arm[:, None].to(torch.int64),
-                      coh.arm[:, None].to(torch.int64)).to(torch.int8).contiguous()
-    sl = torch.randint(1, T, (N,), generator=g, device=dev, dtype=torch.int32)
-    c0 = np.zeros((2, coh.lib.n_terms))
-    c0[0, 4], c0[1, 1], c0[1, 5] = -1.1107592869834308, -0.14540553723951796, -1.0234639833519243  # log :182
-    dt = 10.0 / T
+    coh, V, arm, sl, c0, dt = insite_rows(N, T, args.seed, dev)
 
     # the product's binned path as a prepared plan: the seq_len sort and the refinement on the patient-major rows
     # (insite_refine_rows_f64, ABI 9: 2 C calls, no host synchronisation) inside every step

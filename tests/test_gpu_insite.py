@@ -545,3 +545,29 @@ def test_cooperative_dense_refine_equals_single_lane(dev, monkeypatch, N, joint,
     assert (outs["1"][2][sl <= 5] == -1).all() and (outs["1"][2][sl > 5] >= 0).all()
     for a, b in zip(outs["1"], outs["0"]):
         assert torch.equal(a, b)
+
+
+def test_refine_rows_on_bench_cohort_sampled_against_oracle(dev):
+    """the INSITE line's OWN 1M-row cohort (bench.insite_rows, seed as ``bench.py --config
+    insite``) through the product call the line times (ops.plan_insite_refine: the device seq_len sort +
+    insite_refine_rows_f64 on binned lanes), ~4k sampled rows -- the first and last 64 lanes of the binned order
+    among them -- against oracle/insite_refine_ref.refine_patient (bench.insite_parity, the line's own parity
+    check): refined coefficients to 1e-7 and prediction RMSE <= 1e-6 on EVERY sampled row; statuses and iteration
+    counts equal on >= 99.5 % of them.  The rest (7 of 4,349 on the first box run, 0.16 %) are rows where the two
+    roundings of the objective -- the kernel's closed-form scans (INSITE_REFINE_CF) and the oracle's sub-step form --
+    end the search differently at rounding-level flatness (e.g. converged vs a failed final zoom) with the SAME
+    iterate: their coefficients still agree to ~1e-10."""
+    import bench
+    from insite_amd import ops
+    coh, V, arm, sl, c0, dt = bench.insite_rows(1_000_000, 60, 1, dev)
+    plan = ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5)
+    preds, coef, status, iters = plan()
+    torch.cuda.synchronize()
+    o = plan.order.long()
+    par = bench.insite_parity(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, preds, coef, status, iters,
+                              extra=(o[:64].cpu().numpy(), o[-64:].cpu().numpy()))
+    print(par)
+    assert par["rows_sampled"] >= 4096
+    assert par["status_equal_frac"] >= 0.995 and par["iterations_equal_frac"] >= 0.995, par
+    assert par["coef_linf"] <= 1e-7, par
+    assert par["pred_rmse"] <= 1e-6, par
