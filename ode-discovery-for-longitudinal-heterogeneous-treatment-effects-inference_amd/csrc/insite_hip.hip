@@ -2583,6 +2583,19 @@ __device__ void fit_from_gb(const double* __restrict__ G, const double* __restri
 constexpr int kXcds = 8;
 // #{ i in [0, n) : i % kXcds == x } for n >= 0
 __device__ __forceinline__ int64_t xcd_count(int64_t n, int x) { return (n + kXcds - 1 - x) / kXcds; }
+// The claimed rollout tail (INSITE_DEF_RSTATIC < 1000) with one head per XCD slot (INSITE_DEF_XHEADS, VERDICT r04
+// item 5): round 3's single device-scope head took every claim of the chip -- 2-4k claims per launch against the
+// ~88 dequeues / us one word sustains (MI355X_MICROARCH.md "dequeue") -- and measured 35-65 % slower.  Here the tail
+// [S, units) is cut into kXcds contiguous segments; the waves of the rollout blocks with b % kXcds == x (XCD x under
+// the dispatcher's round robin -- speed only: the protocol is agent-scope atomics, correct under any placement) claim
+// chunks of segment x from head x, each head on its own 128-B line of the workspace's claim area (after the two
+// slots), with its own done counter: the last wave of slot x to finish claiming resets both, so every launch leaves
+// the area zero.  With fewer than kXcds rollout blocks one head serves all.
+#ifndef INSITE_DEF_XHEADS
+#define INSITE_DEF_XHEADS 1
+#endif
+constexpr int kClaimLineWords = 32;                      // one 128-B line per head (head word 0, done word 1)
+constexpr size_t kDefClaimBytes = (size_t)kXcds * kClaimLineWords * sizeof(unsigned);
 // rank of block b among the blocks [lo, hi) ordered XCD-major (by b % kXcds, then b)
 __device__ __forceinline__ int64_t xcd_rank(int64_t b, int64_t lo, int64_t hi) {
   const int x = (int)(b % kXcds);
@@ -2659,7 +2672,17 @@ step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, con
 #else
   const int64_t S = rc ? units * INSITE_DEF_RSTATIC / 1000 : units;
   rollout_units<METHOD>(ra, lib, lane, rw * S / RW, (rw + 1) * S / RW, ng);
-  if (rc) rollout_claimed<METHOD>(ra, lib, lane, S, units, ng, INSITE_DEF_RCHUNK, rc, RW);
+  if (rc) {
+    const int64_t nrb = (int64_t)gridDim.x - first;
+    if (INSITE_DEF_XHEADS && nrb >= kXcds) {
+      const int xs = (int)(blockIdx.x % kXcds);
+      const int64_t wx = (xcd_count((int64_t)gridDim.x, xs) - xcd_count(first, xs)) * kWavesPerBlock;
+      const int64_t lo = S + (units - S) * xs / kXcds, hi = S + (units - S) * (xs + 1) / kXcds;
+      rollout_claimed<METHOD>(ra, lib, lane, lo, hi, ng, INSITE_DEF_RCHUNK, rc + xs * kClaimLineWords, wx);
+    } else {
+      rollout_claimed<METHOD>(ra, lib, lane, S, units, ng, INSITE_DEF_RCHUNK, rc, RW);
+    }
+  }
 #endif
   INSITE_TSTAMP(32768 + rw, 0);
   INSITE_TREAL(32768 + rw, 9);
@@ -4005,7 +4028,7 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
       if (exps[j * (1 + n_statics)] > INSITE_MAX_STATE_DEGREE) return INSITE_E_UNSUPPORTED;
   }
   const size_t ws_one = insite_gram_workspace_bytes(n_patients, n_arms, n_terms);
-  if (!workspace || workspace_bytes < (deferred ? 2 : 1) * ws_one) return INSITE_E_WORKSPACE;
+  if (!workspace || workspace_bytes < (deferred ? 2 * ws_one + kDefClaimBytes : ws_one)) return INSITE_E_WORKSPACE;
   if (deferred && (slot < 0 || slot > 1 || finalize_prev < 0 || finalize_prev > 1)) return INSITE_E_INVALID_ARG;
   if (lagged && ((G_fit == nullptr) != (b_fit == nullptr))) return INSITE_E_INVALID_ARG;
   if (ldx > ((int64_t)1 << 31) / (8 * kGT)) return INSITE_E_UNSUPPORTED;
@@ -4067,7 +4090,8 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
       rows = reinterpret_cast<const int32_t*>(G_out);
       u = G_out;
     }
-    unsigned* rc = INSITE_DEF_RSTATIC < 1000 ? static_cast<unsigned*>(workspace) : nullptr;  // slot 0's header
+    // the claim area after the two slots (zero between calls; used by the claimed-tail build only)
+    unsigned* rc = INSITE_DEF_RSTATIC < 1000 ? reinterpret_cast<unsigned*>(wsb + 2 * ws_one) : nullptr;
     kd<<<dim3(grid), kBlock, 0, hs>>>(x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, part_cur,
                                       part_prev, lagged ? gred : go, ra, gb, rc, hdr_cur, hdr_prev, lagged, G_fit,
                                       b_fit, gf);
@@ -4105,7 +4129,7 @@ int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, co
 
 size_t insite_fit_rollout_deferred_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms) {
   const size_t one = insite_gram_workspace_bytes(n_patients, n_arms, n_terms);
-  return one ? 2 * one : 0;
+  return one ? 2 * one + kDefClaimBytes : 0;
 }
 
 int32_t insite_fit_rollout_deferred_f64(const double* x, int64_t ldx, int32_t n_steps, const double* u,

@@ -229,3 +229,12 @@ def test_pack_arm_bits_roundtrip():
         assert torch.equal(bits.to(torch.int8), a[:, :N])
     with pytest.raises(ValueError):
         ops.pack_arm_bits(torch.full((2, 4), 2, dtype=torch.int8))
+
+
+def test_deferred_workspace_holds_two_slots_and_the_claim_area():
+    """insite_fit_rollout_deferred_workspace_bytes = two discovery slots + the 1-KiB claim area of the claimed
+    rollout tail (one 128-B line per XCD slot; insite_hip.h)."""
+    from insite_amd import _lib
+    L = _lib.load()
+    for n in (1, 1000, 100_000):
+        assert L.insite_fit_rollout_deferred_workspace_bytes(n, 2, 7) == 2 * L.insite_gram_workspace_bytes(n, 2, 7) + 1024
