@@ -89,6 +89,9 @@ def parse():
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "insite", "insite4", "f4"],
                     help="c2: BASELINE configs[1], the headline line (default); c3: configs[2], the 5-state fp32 "
                          "system (parity-test configuration, measured separately)")
+    ap.add_argument("--insite-only-binned", action="store_true",
+                    help="--config insite: time only the product route (skip the identity-order and prepare-route "
+                         "comparisons; for counter runs)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"),
                     help="per-launch HBM bytes from the rocprofv3 PMC passes (profiles/), if present")
     return ap.parse_args()
@@ -1034,12 +1037,13 @@ def insite_main(args):
         torch.cuda.synchronize(dev)
         return (time.perf_counter() - t0) / args.steps * 1e3, r
 
-    ms_identity, _ = timed("identity")
-    ms_prepare, prep_out = timed("prepare")
+    only = args.insite_only_binned            # (profiling: the other routes' launches stay out of the counters)
+    ms_identity, _ = (None, None) if only else timed("identity")
+    ms_prepare, prep_out = (None, None) if only else timed("prepare")
     ms_step, (preds, coef, status, iters) = timed("binned")    # the product default: rows binned by seq_len
     eager = ops.insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, binned=True)
     plan_eq = all(bool(torch.equal(a, b)) for a, b in zip(eager, (preds, coef, status, iters)))
-    prep_eq = all(bool(torch.equal(a, b)) for a, b in zip(prep_out, (preds, coef, status, iters)))
+    prep_eq = None if only else all(bool(torch.equal(a, b)) for a, b in zip(prep_out, (preds, coef, status, iters)))
     st = status.cpu().numpy()
     it = iters.cpu().numpy()
     # roofline: the refinement kernel alone (the plan's second call, its lane order computed by the steps above),
