@@ -161,14 +161,6 @@ __device__ __forceinline__ int pm_slot_index(int r, int col) {
 #ifndef INSITE_REFINE_CF
 #define INSITE_REFINE_CF 1
 #endif
-// RELOAD: the objective re-reads the active terms' routing (t_mask / t_ex, kernel-argument words) in every
-// evaluation through a pointer laundered by an empty asm, instead of the compiler keeping 2 M of them live in SGPRs
-// across the whole BFGS (the M = 16 cooperative kernel spilled 262 SGPRs into VGPR lanes; 72 after).  Cooperative
-// kernel only: the single-lane kernels evaluate inside per-lane control flow, where the SGPR-constrained asm operand
-// is not available (the backend rejects the VGPR -> SGPR copy).
-#ifndef INSITE_REFINE_RELOAD
-#define INSITE_REFINE_RELOAD 1
-#endif
 // the per-arm constants of CF for one evaluation
 struct CfArm {
   double P, B, hS, C1, C2;
@@ -592,7 +584,7 @@ struct BfgsFlat {
   // one trial's value / slope / gradient -> the next state (insite_refine_kernel's FLAT loop body); returns pending
   __device__ bool advance(double phi_t, double dphi_t, const double (&g_t)[M], const Lane& ln, int maxiter) {
 #pragma clang fp contract(off)  // NC
-    bool ls_end = false, ls_done = false;
+    bool ls_end = false, ls_done = false, next_zoom = false;
     if (!in_zoom) {
       const double a_i = t_trial;
       const bool s_z1 = (phi_t > phi0 + 1e-4 * a_i * dphi0) || ((phi_t >= phi_i1) && (li > 1));
@@ -627,7 +619,7 @@ struct BfgsFlat {
       phi_i1 = phi_t;
       dphi_i1 = dphi_t;
       if (in_zoom) {
-        zoom_top();
+        next_zoom = true;
       } else if (s_i) {
         ls_end = ls_done = true;
       } else if (li > 10) {
@@ -676,9 +668,12 @@ struct BfgsFlat {
         ls_failed = ls_failed || z_failed;
         ls_end = ls_done = true;
       } else {
-        zoom_top();
+        next_zoom = true;
       }
     }
+    // the next zoom trial, from either branch: ONE copy of zoom_top (its five divisions and a square root), so a wave
+    // whose lanes are in both phases issues it once rather than twice
+    if (next_zoom) zoom_top();
     if (!ls_end) return true;
     ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
     failed = ls_failed || !ls_done;
@@ -1505,17 +1500,27 @@ insite_refine_coop_kernel(RefineArgs) {
   const int K = refine ? min(sl - ra.tau, ra.T - 1) : 0;
   double norm = 1.0;
   int nev = 0;
+  // Per-lane routing, once (round 5): lane j's tangent (ta, te) receives active coefficient i when bit i of `rbits`
+  // is set, and its own coordinates i = j + 8 s carry (omk[s], oex[s]).  Every sum of the objective is still taken
+  // in the single-lane kernel's order; what changes is WHO computes it: before, every lane walked all MC coefficients
+  // with the (uniform but compiler-opaque) routing as selects -- 8 conditional adds per coefficient for gamma, and
+  // each coordinate's gradient (two divisions) computed under an owner-lane mask, so the wave issued all MC of them:
+  // ~1,600 of the loop's ~2,900 VALU per evaluation (profiles/r05/coop/).
+  unsigned rbits = 0u;
+  int omk[S], oex[S];
+  for (int i = 0; i < ra.m && i < MC; ++i) {
+    const int mk = ra.t_mask[i], ex = ra.t_ex[i];
+    if (((mk >> ta) & 1) && ex == te) rbits |= 1u << i;
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int i = j + kCoopG * s;
+    omk[s] = i < ra.m ? ra.t_mask[i] : 0;
+    oex[s] = i < ra.m ? ra.t_ex[i] : 0;
+  }
   // f and its gradient at c (RefineLane::fg, D = 1, the non-windowed scan); every lane of the wave calls it
   auto fg = [&](const double (&c)[S], double (&g)[S], bool live) -> double {
     nev += live ? 1 : 0;
-    // the routing tables re-read (scalar loads) in every evaluation: the laundered pointers keep the compiler from
-    // holding 2 MC kernel-argument words live in SGPRs across the BFGS (they spilled into VGPR lanes)
-    typedef const __attribute__((address_space(4))) int32_t* KInt;
-    KInt tmk = ra.t_mask, tex = ra.t_ex;
-    if (INSITE_REFINE_RELOAD) asm volatile("" : "+s"(tmk), "+s"(tex));
-    double gam[NA][2];
-#pragma unroll
-    for (int a = 0; a < NA; ++a) gam[a][0] = gam[a][1] = 0.0;
     // per-coordinate values are formed on their owner lane and gathered once (the same roundings as forming them
     // from two gathered operands on the reading lane: one gather per coordinate instead of two)
     double tm[S], sq[S];
@@ -1526,19 +1531,21 @@ insite_refine_coop_kernel(RefineArgs) {
       const double dd = c0a[s] - c[s];
       sq[s] = dd * dd;
     }
+    // gamma_{ta,te} on lane j (the coefficients routed to it, in coefficient order: the single-lane kernel's sum),
+    // then gathered: lane 2a + e holds gamma_{a,e}
+    double gown = 0.0;
 #pragma unroll
     for (int i = 0; i < MC; ++i) {
 #pragma clang fp contract(off)  // NC
       if (i >= ra.m) break;
       const double t = gat(tm, i);  // c_i m_i, formed on coordinate i's lane
-      const int mk = tmk[i], ex = tex[i];
-#pragma unroll
-      for (int a = 0; a < NA; ++a)
-        if ((mk >> a) & 1)
-#pragma unroll
-          for (int e = 0; e <= 1; ++e)
-            if (ex == e) gam[a][e] += t;
+      if ((rbits >> i) & 1u) gown += t;
     }
+    double gam[NA][2];
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int e = 0; e <= 1; ++e) gam[a][e] = grp_lane(gown, 2 * a + e);
     const double h = ra.dt / (double)ra.sub;
     double y = v_at(0);
     double d = 0.0, gGo = 0.0, L = 0.0;
@@ -1604,23 +1611,25 @@ insite_refine_coop_kernel(RefineArgs) {
     for (int i = 0; i < MC; ++i) {
 #pragma clang fp contract(off)  // NC
       const double sqi = gat(sq, i);
-      if (i >= ra.m) {
-        if (i % kCoopG == j) g[i / kCoopG] = 0.0;
+      if (i >= ra.m) break;
+      pen += sqi;
+    }
+    // the gradient of this lane's own coordinates only (each lane its S, not the wave all MC under owner masks)
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+#pragma clang fp contract(off)  // NC
+      if (j + kCoopG * s >= ra.m) {
+        g[s] = 0.0;
         continue;
       }
-      pen += sqi;
-      if (i % kCoopG == j) {
-        const double ci = c[i / kCoopG], c0i = c0a[i / kCoopG];
-        const int mk = tmk[i], ex = tex[i];
-        double gd = 0.0;
+      double gd = 0.0;
 #pragma unroll
-        for (int a = 0; a < NA; ++a)
-          if ((mk >> a) & 1)
+      for (int a = 0; a < NA; ++a)
+        if ((omk[s] >> a) & 1)
 #pragma unroll
-            for (int e = 0; e <= 1; ++e)
-              if (ex == e) gd += gG[a][e];
-        g[i / kCoopG] = gd * iK * mono[i / kCoopG] / norm + 2.0 * ra.lam * (ci - c0i) / (double)ra.n_coef;
-      }
+          for (int e = 0; e <= 1; ++e)
+            if (oex[s] == e) gd += gG[a][e];
+      g[s] = gd * iK * mono[s] / norm + 2.0 * ra.lam * (c[s] - c0a[s]) / (double)ra.n_coef;
     }
     return L / norm + ra.lam * pen / (double)ra.n_coef;
   };
@@ -1726,7 +1735,7 @@ insite_refine_coop_kernel(RefineArgs) {
     const double phi_t = fg(xt, g_t, pending);
     const double dphi_t = dot(g_t, pk);
     if (!pending) continue;
-    bool ls_end = false, ls_done = false;
+    bool ls_end = false, ls_done = false, next_zoom = false;
     {
 #pragma clang fp contract(off)  // NC
     if (!in_zoom) {
@@ -1763,7 +1772,7 @@ insite_refine_coop_kernel(RefineArgs) {
       phi_i1 = phi_t;
       dphi_i1 = dphi_t;
       if (in_zoom) {
-        zoom_top();
+        next_zoom = true;
       } else if (s_i) {
         ls_end = ls_done = true;
       } else if (li > 10) {
@@ -1812,9 +1821,10 @@ insite_refine_coop_kernel(RefineArgs) {
         ls_failed = ls_failed || z_failed;
         ls_end = ls_done = true;
       } else {
-        zoom_top();
+        next_zoom = true;
       }
     }
+    if (next_zoom) zoom_top();  // one copy for both phases (BfgsFlat::advance)
     }
     if (!ls_end) continue;
     ls_status = ls_failed ? 1 : (li > 10 ? 3 : 0);
