@@ -1462,7 +1462,14 @@ insite_refine_coop_kernel(RefineArgs) {
   // the wave's rows staged in LDS: [step][row slot] doubles / arm bytes (row slot = lane / 8)
   __shared__ double sV[STG ? kWavesPerBlock * kCoopStT * kCoopG : 1];
   __shared__ int8_t sA[STG ? kWavesPerBlock * kCoopStT * kCoopG : 1];
+  // the per-arm closed-form constants of the current evaluation (CfArm: P, B, hS, C1, C2), [row slot][arm][5] per
+  // wave: written once per evaluation by the (ta, te = 0) lane of each arm, read per step by every lane of the row
+  // at its step's arm (the 8 lanes of a row read one address: an LDS broadcast) -- instead of every lane computing
+  // all NA arms' constants and selecting one per step through NA - 1 branchy register copies (5 moves each)
+  constexpr int kCf5 = 5;
+  __shared__ double sCf[INSITE_REFINE_CF ? kWavesPerBlock * kCoopG * NA * kCf5 : 1];
   const int rs = lane / kCoopG, wv = threadIdx.x / kWave;
+  double* const wCf = sCf + (INSITE_REFINE_CF ? wv * kCoopG * NA * kCf5 : 0);
   double* const wV = sV + (STG ? wv * kCoopStT * kCoopG : 0);
   int8_t* const wA = sA + (STG ? wv * kCoopStT * kCoopG : 0);
   if constexpr (STG) {  // (ra.T <= kCoopStT, checked at the launch)
@@ -1541,12 +1548,28 @@ insite_refine_coop_kernel(RefineArgs) {
       const double t = gat(tm, i);  // c_i m_i, formed on coordinate i's lane
       if ((rbits >> i) & 1u) gown += t;
     }
-    double gam[NA][2];
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int e = 0; e <= 1; ++e) gam[a][e] = grp_lane(gown, 2 * a + e);
     const double h = ra.dt / (double)ra.sub;
+    double gam[NA][2];
+    if constexpr (INSITE_REFINE_CF) {
+      // arm ta's constants from (gamma_{ta,0}, gamma_{ta,1}) -- this lane's and its pair partner's (lane j ^ 1) --
+      // computed by both lanes of the pair and stored by the te = 0 one
+      const double gp = __shfl_xor(gown, 1);
+      const CfArm c = cf_arm(te ? gp : gown, te ? gown : gp, h, ra.sub);
+      if (te == 0) {
+        double* const q = wCf + (rs * NA + ta) * kCf5;
+        q[0] = c.P;
+        q[1] = c.B;
+        q[2] = c.hS;
+        q[3] = c.C1;
+        q[4] = c.C2;
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else {
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int e = 0; e <= 1; ++e) gam[a][e] = grp_lane(gown, 2 * a + e);
+    }
     double y = v_at(0);
     double d = 0.0, gGo = 0.0, L = 0.0;
     const int Kl = live ? K : 0;
@@ -1555,11 +1578,6 @@ insite_refine_coop_kernel(RefineArgs) {
     for (int off = 32; off >= 1; off >>= 1) Kw = max(Kw, __shfl_xor(Kw, off));
     int ak_nx = Kw > 0 ? a_at(0) : 0;
     double v_nx = Kw > 0 ? v_at(1) : 0.0;
-    CfArm cfa[INSITE_REFINE_CF ? NA : 1];
-    if constexpr (INSITE_REFINE_CF) {
-#pragma unroll
-      for (int a = 0; a < NA; ++a) cfa[a] = cf_arm(gam[a][0], gam[a][1], h, ra.sub);
-    }
     for (int k = 0; k < Kw; ++k) {
       const int ak = ak_nx;
       const double vk1 = v_nx;
@@ -1568,10 +1586,13 @@ insite_refine_coop_kernel(RefineArgs) {
         v_nx = v_at(k + 2);
       }
       if (INSITE_REFINE_CF && k < Kl) {
-        CfArm c = cfa[0];
-#pragma unroll
-        for (int a = 1; a < NA; ++a)
-          if (ak == a) c = cfa[a];
+        const double* const q = wCf + (rs * NA + ak) * kCf5;
+        CfArm c;
+        c.P = q[0];
+        c.B = q[1];
+        c.hS = q[2];
+        c.C1 = q[3];
+        c.C2 = q[4];
         const double add = ak == ta ? (te ? fma(c.C1, y, c.C2) : c.hS) : 0.0;
         d = fma(c.P, d, add);
         y = fma(c.P, y, c.B);
