@@ -64,6 +64,13 @@ def parse():
     ap.add_argument("--dstreams", type=int, default=1,
                     help="deferred mode: independent streams of cohorts, launch k on stream k %% S (1 = one stream)")
     ap.add_argument("--pipe-k", type=int, default=4, help="pipeline: steps per batch (one event per batch per stream)")
+    ap.add_argument("--lag-k", type=int, default=16,
+                    help="lagged mode: fits per all-reduce bucket (profiles/r05/lagk: at N = 1 with the single-rank RCCL "
+                         "collective, K = 4 / 8 / 16 all within 1.2-2 %% of the deferred step)")
+    ap.add_argument("--lag-delay", type=int, default=1, choices=[0, 1],
+                    help="lagged mode: 0 = the bucket all-reduce in order on the launch stream, 1 = issued async and "
+                         "waited for K launches later (insite_amd.dist.LaggedSchedule delay; at K = 16 as cheap as 0 "
+                         "at N = 1, and the N > 1 collective's latency runs beside K launches)")
     ap.add_argument("--pipe-rs", type=int, default=2, help="pipeline: rollout streams taking alternate batches")
     ap.add_argument("--fused-graph", action="store_true",
                     help="fused mode: replay the ping-pong pair of step launches from a HIP graph")
@@ -2032,8 +2039,9 @@ def c2_lagged(args, dev, world, rank, coh, arm_cf, cpu, collective):
     """C2 at N GPUs (the default at N > 1; ``--mode lagged`` also at N = 1, with --force-collective to put the
     single-rank RCCL all-reduce in): ONE insite_fit_rollout_lagged_f64 launch per step -- the step_deferred_kernel
     timed at N = 1 with its finalisation split into a reduction role (rank-local G|b) and a solve role (an
-    all-reduced G|b) -- and one RCCL all-reduce of a K-fit bucket per K launches ON THE LAUNCH STREAM (no event,
-    no second stream: insite_amd.dist.LaggedSchedule).  Two cohorts per rank rotate, as at N = 1, so no launch
+    all-reduced G|b) -- and one RCCL all-reduce of a K-fit bucket per K launches (insite_amd.dist.LaggedSchedule):
+    by default (--lag-delay 1, --lag-k 16) issued async and waited for by the launch stream only K launches later,
+    so the collective runs beside the launches (delay 0: in order on the launch stream).  Two cohorts per rank rotate, as at N = 1, so no launch
     re-reads x still resident in the 256 MB Infinity Cache.  value = all ranks' patients / the max-over-ranks
     step time (weak scaling: 100k patients per GPU)."""
     from insite_amd import ops, cohort
@@ -2042,12 +2050,12 @@ def c2_lagged(args, dev, world, rank, coh, arm_cf, cpu, collective):
     lib = coh.lib
     F = lib.n_terms
     f64 = torch.float64
-    K = max(1, args.pipe_k)
-    sched = idist.LaggedSchedule(K)
+    K = max(1, args.lag_k)
+    sched = idist.LaggedSchedule(K, delay=args.lag_delay)
     sd = args.seed * 1000 + 500 + rank
     coh2 = cohort.synthetic_pkpd(N, T, seed=sd, device=dev, equation="EQ_4_C", layout="time")
     cohs = [(coh, arm_cf), (coh2, cohort.counterfactual_arms(coh2.arm, T, seed=sd, layout="time_bits"))]
-    buckets = [idist.MomentBucket(K, 2, F, dev) for _ in range(2)]
+    buckets = [idist.MomentBucket(K, 2, F, dev) for _ in range(sched.NB)]
     ring = [(torch.zeros((2, F), dtype=f64, device=dev), torch.zeros((2, F), dtype=torch.int8, device=dev),
              torch.zeros((2,), dtype=torch.int32, device=dev)) for _ in range(3)]
     ys = [torch.empty((T, N), dtype=f64, device=dev) for _ in range(2)]
@@ -2074,20 +2082,28 @@ def c2_lagged(args, dev, world, rank, coh, arm_cf, cpu, collective):
             c.x, c.u, c.arm, c.rows, c.dt, lib, 0.1, 0.5, rcoh.y0, rcoh.u, rbits, cin, rcoh.dt, p["slot"],
             p["reduce"] is not None, ws, (red.G, red.b) if red is not None else scratch, fit_in=fit_in,
             fit_out=fit_out, method=args.method, T=T, y_out=yy, gram_blocks=args.gram_blocks).bind(st)
-        ar = buckets[p["allreduce_after"]] if p["allreduce_after"] is not None else None
+        ar = p["allreduce_after"]
         return launch, ar, p
 
-    P = idist.LaggedSchedule.period(K)
-    k0 = K + 2                                   # the first steady-state launch
+    P = sched.period_of()
+    k0 = sched.lag                               # the first steady-state launch
     steady = {}
     for k in range(k0, k0 + P):
         steady[k % P] = plan(k)
+    pending = {}                                 # delay 1: bucket -> the in-flight all-reduce's work handle
 
     def one(k):
-        launch, ar, _ = plan(k) if k < k0 else steady[k % P]
+        launch, ar, p = plan(k) if k < k0 else steady[k % P]
+        if p["wait_before"] is not None and p["wait_before"] in pending:
+            pending.pop(p["wait_before"]).wait()     # the launch stream waits for the collective (no host block)
         launch()
-        if ar is not None and collective:        # the only collective: one per K launches, on the launch stream
-            idist.reduce_bucket(ar, force=args.force_collective)
+        if ar is not None and collective:        # the only collective: one per K launches
+            if sched.D:
+                h = idist.reduce_bucket(buckets[ar], force=args.force_collective, async_op=True)
+                if h is not None:
+                    pending[ar] = h
+            else:                                # in order on the launch stream
+                idist.reduce_bucket(buckets[ar], force=args.force_collective)
 
     kk = [0]
 
@@ -2149,7 +2165,9 @@ def c2_lagged(args, dev, world, rank, coh, arm_cf, cpu, collective):
                 "patients_per_gpu": N, "T": T, "rows_per_patient": T - 2, "library_terms": F,
                 "parallelism": f"patient-shard x{world}" + (" (single-rank RCCL group: --force-collective)"
                                                              if args.force_collective and world == 1 else ""),
-                "mode": "lagged", "fits_per_allreduce": K, "lag_launches": K + 2,
+                "mode": "lagged", "fits_per_allreduce": K, "lag_launches": sched.lag,
+                "allreduce": ("async, waited K launches later (LaggedSchedule delay 1)" if sched.D else
+                              "in order on the launch stream"),
                 "discovered_support": mask_used.cpu().numpy().tolist(),
                 "finite": bool(torch.isfinite(y).all().item()), "cohorts_rotated_per_rank": 2,
             },
@@ -2166,7 +2184,8 @@ def c2_lagged(args, dev, world, rank, coh, arm_cf, cpu, collective):
                                  f"(with their {KB // K} bucket all-reduces), divided by the batch size",
             },
             "timed_region": f"one lagged launch per step on one stream + one all-reduce of a {K}-fit G|b bucket "
-                            "per K launches on the same stream; no events, no second stream",
+                            "per K launches (" + ("issued async on RCCL's stream, the launch stream waiting for it K "
+                                                  "launches later" if sched.D else "on the same stream, in order") + ")",
         }
         if cpu is not None:
             out["cpu_baseline"] = cpu

@@ -46,15 +46,20 @@ class MomentBucket:
             self.bufs.append(b)
 
 
-def reduce_bucket(bucket: MomentBucket, group=None, deterministic: bool = False, force: bool = False) -> MomentBucket:
+def reduce_bucket(bucket: MomentBucket, group=None, deterministic: bool = False, force: bool = False,
+                  async_op: bool = False):
     """Sum every partial system of the bucket over all ranks in place, in one collective (``force``: issue it
-    on a single-rank group too -- the bench's --force-collective measurement of the collective's cost)."""
+    on a single-rank group too -- the bench's --force-collective measurement of the collective's cost).
+    ``async_op``: return the collective's work handle (None when no collective ran); its ``wait()`` makes the
+    current stream wait for the result (NCCL/RCCL; gloo blocks the host).  Otherwise the bucket is returned."""
     if _world(group) > 1 or (force and dist.is_available() and dist.is_initialized()):
         if deterministic:
             fixed_order_sum(bucket.flat, group)
         else:
-            dist.all_reduce(bucket.flat, op=dist.ReduceOp.SUM, group=group)
-    return bucket
+            w = dist.all_reduce(bucket.flat, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+            if async_op:
+                return w
+    return None if async_op else bucket
 
 
 def shard_bounds(n_total: int, rank: int, world: int) -> tuple[int, int]:
@@ -167,45 +172,66 @@ def discover_sharded(x, u, arm, rows, dt, lib, threshold, alpha, buf: MomentBuff
 
 class LaggedSchedule:
     """Bookkeeping of the N > 1 lagged step (``ops.plan_fit_rollout_lagged``, insite_fit_rollout_lagged_f64): one
-    launch per step, K fits per all-reduce bucket, no cross-stream hop.  Launch k (k >= 0):
+    launch per step, K fits per all-reduce bucket.  With ``delay`` D (0 or 1), NB = 2 + D buckets rotate and launch k
+    (k >= 0):
 
     * streams cohort k's Gram into partial slot k % 2;
     * (k >= 1) reduces slot (k - 1) % 2 -- cohort k - 1 -- to this rank's G|b at position (k - 1) % K of bucket
-      ((k - 1) // K) % 2;
-    * (k >= K + 1) solves the STLSQ of cohort k - K - 1 from its ALL-REDUCED bucket entry into coefficient ring
-      slot (k - K - 1) % 3;
-    * (k >= K + 2) rolls out cohort k - K - 2 with ring slot (k - K - 2) % 3;
+      ((k - 1) // K) % NB;
+    * (k >= (1 + D) K + 1) solves the STLSQ of cohort c = k - (1 + D) K - 1 from its ALL-REDUCED bucket entry into
+      coefficient ring slot c % 3;
+    * (k >= (1 + D) K + 2) rolls out cohort k - (1 + D) K - 2 with its ring slot;
 
-    and after launch k with k % K == 0, k >= K, the bucket ((k - 1) // K) % 2 (cohorts k - K .. k - 1, complete)
-    is all-reduced in place on the launch stream.  Why these lags: bucket j is written by launches jK + 1 ..
-    jK + K, reduced after jK + K, read by the solves of launches jK + K + 1 .. jK + 2K, and rewritten (as bucket
-    j + 2) from launch jK + 2K + 1 on; the solve never reads the bucket its own launch writes, and a coefficient
-    slot is written one launch before the rollout that reads it.  Every cohort gets the reference's fit-then-
-    rollout over the WHOLE cohort (all ranks' patients), K + 1 launches later than at N = 1."""
+    and after launch k with k % K == 0, k >= K, the bucket ((k - 1) // K) % NB (cohorts k - K .. k - 1, complete) is
+    all-reduced.  D = 0: on the launch stream, in order (the next launch's solves read it).  D = 1 (round 5): issued
+    asynchronously (``all_reduce(async_op=True)``: RCCL's own stream, ordered after the launch) and waited for
+    (``wait_before``: the launch stream waits on the collective's completion, the host does not block) only before
+    the launch whose solve first reads that bucket, K launches later -- the collective runs beside K launches
+    instead of between two of them.  Bucket j is written by launches jK + 1 .. jK + K, reduced after jK + K, read
+    by the solves of launches jK + (1 + D) K + 1 .. jK + (2 + D) K and rewritten (as bucket j + NB) from launch
+    jK + NB K + 1 on; the solve never reads the bucket its own launch writes, and a coefficient slot is written one
+    launch before the rollout that reads it.  Every cohort gets the reference's fit-then-rollout over the WHOLE
+    cohort (all ranks' patients), (1 + D) K + 1 launches later than at N = 1."""
 
-    def __init__(self, k: int):
+    def __init__(self, k: int, delay: int = 0):
         if k < 1:
             raise ValueError("K >= 1 fits per bucket")
+        if delay not in (0, 1):
+            raise ValueError("delay is 0 (in-order all-reduce) or 1 (overlapped)")
         self.K = int(k)
+        self.D = int(delay)
+        self.NB = 2 + self.D
+
+    @property
+    def lag(self) -> int:
+        """Launches between a cohort's Gram and its rollout."""
+        return (1 + self.D) * self.K + 2
 
     def launch(self, k: int) -> dict:
-        K = self.K
-        p = {"gram": k, "slot": k % 2, "reduce": None, "fit": None, "rollout": None, "allreduce_after": None}
+        K, NB, L = self.K, self.NB, (1 + self.D) * self.K
+        p = {"gram": k, "slot": k % 2, "reduce": None, "fit": None, "rollout": None, "allreduce_after": None,
+             "wait_before": None}
         if k >= 1:
             c = k - 1
-            p["reduce"] = (c, (c // K) % 2, c % K)
-        if k >= K + 1:
-            c = k - K - 1
-            p["fit"] = (c, (c // K) % 2, c % K, c % 3)
-        if k >= K + 2:
-            c = k - K - 2
+            p["reduce"] = (c, (c // K) % NB, c % K)
+        if k >= L + 1:
+            c = k - L - 1
+            p["fit"] = (c, (c // K) % NB, c % K, c % 3)
+            if self.D and c % K == 0:     # the first solve from bucket c // K: its all-reduce must be complete
+                p["wait_before"] = (c // K) % NB
+        if k >= L + 2:
+            c = k - L - 2
             p["rollout"] = (c, c % 3)
         if k >= K and k % K == 0:
-            p["allreduce_after"] = ((k - 1) // K) % 2
+            p["allreduce_after"] = ((k - 1) // K) % NB
         return p
 
-    @staticmethod
-    def period(k: int) -> int:
-        """Launch plans repeat with this period (slots 2, buckets 2K, coefficient ring 3): lcm(2, 2K, 3)."""
+    def period_of(self) -> int:
+        """Launch plans repeat with this period (slots 2, buckets NB K, coefficient ring 3)."""
         import math
-        return math.lcm(2, 2 * int(k), 3)
+        return math.lcm(2, self.NB * self.K, 3)
+
+    @staticmethod
+    def period(k: int, delay: int = 0) -> int:
+        import math
+        return math.lcm(2, (2 + int(delay)) * int(k), 3)

@@ -192,11 +192,12 @@ def test_bucketed_allreduce_reduces_every_fit_in_one_collective():
 
 
 
-def _lagged_worker(rank, world, port, q, K, n_launch):
+def _lagged_worker(rank, world, port, q, K, n_launch, delay=0):
     """Each rank plays insite_fit_rollout_lagged_f64's roles with the oracle's CPU restatements on its own
     shard: the gram (slot write), the block reduction (slot -> bucket entry), the replicated STLSQ (bucket
     entry -> coefficient ring) and the rollout (ring -> y), in exactly the order LaggedSchedule gives, with the
-    bucket all-reduce (gloo) after the launches it names."""
+    bucket all-reduce (gloo) after the launches it names -- with delay 1 issued async and waited for only before
+    the launch whose solve first reads the bucket (``wait_before``)."""
     import sys
     for p in (ROOT, PKG):
         if p not in sys.path:
@@ -214,13 +215,16 @@ def _lagged_worker(rank, world, port, q, K, n_launch):
         def cohort_x(c):   # cohort c: the golden cohort rescaled per c (distinct systems per launch)
             return x * (1.0 + 0.01 * c)
 
-        sched = idist.LaggedSchedule(K)
+        sched = idist.LaggedSchedule(K, delay)
         slots = [None, None]
-        buckets = [idist.MomentBucket(K, 2, F, "cpu") for _ in range(2)]
+        buckets = [idist.MomentBucket(K, 2, F, "cpu") for _ in range(sched.NB)]
+        handles = {}
         ring = [None] * 3
         fitted, rolled = {}, {}
         for k in range(n_launch):
             p = sched.launch(k)
+            if p["wait_before"] is not None:
+                handles.pop(p["wait_before"]).wait()
             # roles read state as the kernel does: the gram writes slot k % 2, the reduction reads the other
             cur = R.gram_moments(cohort_x(k)[lo:hi], u[lo:hi], arm[lo:hi], rows[lo:hi], float(g["dt"]), exps)
             if p["reduce"] is not None:
@@ -240,24 +244,30 @@ def _lagged_worker(rank, world, port, q, K, n_launch):
                 rolled[c] = ring[r][1]
             slots[k % 2] = cur
             if p["allreduce_after"] is not None:
-                idist.reduce_bucket(buckets[p["allreduce_after"]])
+                if delay:
+                    handles[p["allreduce_after"]] = idist.reduce_bucket(buckets[p["allreduce_after"]], async_op=True)
+                else:
+                    idist.reduce_bucket(buckets[p["allreduce_after"]])
+        for h in handles.values():
+            h.wait()
         q.put((rank, fitted, rolled))
     finally:
         dist.barrier()
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("K", [1, 4])
-def test_lagged_schedule_gloo_world2(K):
+@pytest.mark.parametrize("K,delay", [(1, 0), (4, 0), (1, 1), (4, 1)])
+def test_lagged_schedule_gloo_world2(K, delay):
     """The N > 1 lagged step's bookkeeping (insite_amd.dist.LaggedSchedule; bench.py lagged_run) over gloo with 2
     ranks: every cohort's model is the STLSQ of the ALL-RANK Gram (equal to a single-process fit of the whole
     cohort), identical on both ranks, and every rollout uses its own cohort's model."""
     from oracle import insite_ref as R
-    world, n_launch = 2, 3 * K + 8
+    world, n_launch = 2, 4 * K + 8
+    L = (1 + delay) * K
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_lagged_worker, args=(r, world, port, q, K, n_launch)) for r in range(world)]
+    procs = [ctx.Process(target=_lagged_worker, args=(r, world, port, q, K, n_launch, delay)) for r in range(world)]
     for p in procs:
         p.start()
     res = {r: (f, ro) for r, f, ro in (q.get(timeout=180) for _ in range(world))}
@@ -267,8 +277,8 @@ def test_lagged_schedule_gloo_world2(K):
     g = np.load(os.path.join(ROOT, "tests", "golden", "discovery_eq_4_c.npz"))
     exps = R.poly_library(3, 2, True)
     fitted0, rolled0 = res[0]
-    assert sorted(fitted0) == list(range(n_launch - K - 1))
-    assert sorted(rolled0) == list(range(n_launch - K - 2))
+    assert sorted(fitted0) == list(range(n_launch - L - 1))
+    assert sorted(rolled0) == list(range(n_launch - L - 2))
     for c, coef in fitted0.items():
         G, b = R.gram_moments(g["x"] * (1.0 + 0.01 * c), g["u"], g["arm"], g["rows"], float(g["dt"]), exps)
         want = np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)])
@@ -284,12 +294,16 @@ def test_lagged_schedule_never_aliases():
     is complete (its K cohorts reduced) and not yet rewritten when its fits read it, and the rollout's ring slot
     is never the one the solve writes."""
     from insite_amd.dist import LaggedSchedule
-    for K in (1, 2, 4, 8):
-        s = LaggedSchedule(K)
-        reduced_at, allreduced_at = {}, {}
+    for K, D in [(K, D) for K in (1, 2, 4, 8) for D in (0, 1)]:
+        s = LaggedSchedule(K, D)
+        reduced_at, allreduced_at, waited_at = {}, {}, {}
         writes = {}
         for k in range(20 * K + 10):
             p = s.launch(k)
+            if p["wait_before"] is not None:                # delay 1: waited for K launches after its issue
+                j = next(jj for jj in allreduced_at if jj % s.NB == p["wait_before"] and jj not in waited_at)
+                assert k - allreduced_at[j] >= K
+                waited_at[j] = k
             if p["reduce"]:
                 c, bi, pos = p["reduce"]
                 reduced_at[c] = k
@@ -299,6 +313,7 @@ def test_lagged_schedule_never_aliases():
                 assert writes[(bi, pos)] == c                       # entry still holds cohort c
                 assert not p["reduce"] or p["reduce"][1] != bi      # not the bucket being written
                 assert allreduced_at.get(c // K, 10 ** 9) < k        # its bucket was all-reduced before
+                assert not D or waited_at.get(c // K, 10 ** 9) <= k   # ... and waited for (delay 1)
                 assert not p["rollout"] or p["rollout"][1] != r
             if p["allreduce_after"] is not None:
                 j = (k - 1) // K

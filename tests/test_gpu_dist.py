@@ -117,7 +117,7 @@ def _lagged_cohorts(dev):
     return cohs, bits
 
 
-def _lagged_worker(rank, world, port, q):
+def _lagged_worker(rank, world, port, q, delay=0):
     """One rank of the N > 1 C2 schedule (bench.py c2_lagged): its shard of two rotating cohorts, one
     insite_fit_rollout_lagged_f64 launch per step, the K-fit bucket all-reduced after the launches the
     LaggedSchedule names (gloo here, RCCL in the bench)."""
@@ -146,8 +146,9 @@ def _lagged_worker(rank, world, port, q):
         lib = full[0].lib
         F = lib.n_terms
         n = hi - lo
-        sched = idist.LaggedSchedule(KL)
-        buckets = [idist.MomentBucket(KL, 2, F, dev) for _ in range(2)]
+        sched = idist.LaggedSchedule(KL, delay)
+        buckets = [idist.MomentBucket(KL, 2, F, dev) for _ in range(sched.NB)]
+        handles = {}
         ring = [(torch.zeros((2, F), dtype=torch.float64, device=dev), torch.zeros((2, F), dtype=torch.int8, device=dev),
                  torch.zeros((2,), dtype=torch.int32, device=dev)) for _ in range(3)]
         ys = [torch.empty((TL, n), dtype=torch.float64, device=dev) for _ in range(2)]
@@ -156,8 +157,11 @@ def _lagged_worker(rank, world, port, q):
         Gs, bs = torch.zeros((2, F, F), dtype=torch.float64, device=dev), torch.zeros((2, F), dtype=torch.float64,
                                                                                        device=dev)
         solved, rolled = {}, {}
-        for k in range(2 * KL + 6):
+        for k in range(sched.lag + KL + 4):
             p = sched.launch(k)
+            if p["wait_before"] is not None:           # delay 1: the async all-reduce issued K launches ago
+                handles.pop(p["wait_before"]).wait()
+                torch.cuda.synchronize()
             c = cohs[k % 2]
             red = (buckets[p["reduce"][1]].bufs[p["reduce"][2]].G, buckets[p["reduce"][1]].bufs[p["reduce"][2]].b) \
                 if p["reduce"] else (Gs, bs)
@@ -176,8 +180,11 @@ def _lagged_worker(rank, world, port, q):
                                         fit_out=fit_out, T=TL, y_out=yy)()
             torch.cuda.synchronize()
             if p["allreduce_after"] is not None:
-                idist.reduce_bucket(buckets[p["allreduce_after"]])
-                torch.cuda.synchronize()
+                if delay:
+                    handles[p["allreduce_after"]] = idist.reduce_bucket(buckets[p["allreduce_after"]], async_op=True)
+                else:
+                    idist.reduce_bucket(buckets[p["allreduce_after"]])
+                    torch.cuda.synchronize()
             if p["fit"]:
                 solved[p["fit"][0]] = ring[p["fit"][3]][0].cpu().numpy().copy()
             if p["rollout"]:
@@ -188,7 +195,8 @@ def _lagged_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_two_rank_lagged_stream_matches_oracle_and_single_rank_rollout(dev):
+@pytest.mark.parametrize("delay", [0, 1])
+def test_two_rank_lagged_stream_matches_oracle_and_single_rank_rollout(dev, delay):
     """The N > 1 form of the headline kernel (ABI 8 lagged step) with 2 ranks on one GPU: every model both ranks
     solve is bitwise the same on the two ranks and equals the oracle fit of the WHOLE cohort (support identical,
     L-inf < 1e-8); every rank's rollout of its shard is bitwise the single-process rollout of those patients with
@@ -206,7 +214,7 @@ def test_two_rank_lagged_stream_matches_oracle_and_single_rank_rollout(dev):
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_lagged_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_lagged_worker, args=(r, world, port, q, delay)) for r in range(world)]
     for p in procs:
         p.start()
     out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
@@ -214,7 +222,7 @@ def test_two_rank_lagged_stream_matches_oracle_and_single_rank_rollout(dev):
         p.join(timeout=60)
         assert p.exitcode == 0
     s0, s1 = out[0][3], out[1][3]
-    assert sorted(s0) == sorted(s1) == list(range(2 * KL + 6 - KL - 1))
+    assert sorted(s0) == sorted(s1) == list(range(KL + 4 + 1))   # launches lag + KL + 4, fits from launch lag - 1
     for cc in s0:
         np.testing.assert_array_equal(s0[cc], s1[cc])
         assert np.array_equal(s0[cc] != 0, want[cc % 2] != 0)
