@@ -425,10 +425,16 @@ def c3_main(args):
     truth = MS.c3_truth_coef(lib, device=dev)
     rows = N * T
     gflop = 2.0 * (F * (F + 1) / 2 + F * S) * rows          # algorithmic: G upper triangle + B per row
-    # issued by gram_ms4_kernel (insite_ms.hip Ms4): NB 4x4 block types (row group rg <= column group cg over
-    # Y = Theta, Z = [Theta | xdot]), 16 FMA = 32 flop each per row
+    # issued by gram_ms4_kernel (insite_ms.hip): NB 4x4x4 f64 blocks per row, 16 FMA = 32 flop each -- the C3
+    # library's moment cover (csrc/ms4_cover_c3.inc, kMs4CoverNB) or, for other libraries, the column-group form
+    # (row group rg <= column group cg over Y = Theta, Z = [Theta | xdot])
     rg, cg = (F + 3) // 4, (F + S + 3) // 4
     nb4 = rg * cg - rg * (rg - 1) // 2
+    if (F, S) == (22, 5):
+        import re
+        inc = open(os.path.join(ROOT, "ode-discovery-for-longitudinal-heterogeneous-treatment-effects-inference_amd",
+                                "csrc", "ms4_cover_c3.inc")).read()
+        nb4 = int(re.search(r"kMs4CoverNB = (\d+)", inc).group(1))
     mfma_flop = nb4 * 32.0 * rows
     roll_bytes = T * N * S * 4 + N * S * 4 + T * ((N + 31) // 32) * 4
     gram_bytes = T * N * S * 4 + T * ((N + 31) // 32) * 4
@@ -444,7 +450,7 @@ def c3_main(args):
         "roofline": {"kernel": "gram_ms4_kernel", "bound": "mfma", "achieved": gflop / (gram_ms_t * 1e-3) / 1e12,
                      "peak": 78.6, "unit": "TFLOP/s", "frac": gflop / (gram_ms_t * 1e-3) / 1e12 / 78.6,
                      "traffic": traffic_for("c3", "gram_ms4_kernel", args=args), "avg_launch_ms": gram_ms_t,
-                     "issued_mfma_TFLOPs": mfma_flop / (gram_ms_t * 1e-3) / 1e12,
+                     "issued_mfma_TFLOPs": mfma_flop / (gram_ms_t * 1e-3) / 1e12, "mfma_blocks_per_row": nb4,
                      "hbm_GBps": gram_bytes / (gram_ms_t * 1e-3) / 1e9},
         "rollout": {"kernel": "ms_rollout_sparse (hipRTC, support-specialised; rk4, fp32)", "bound": "hbm",
                     "avg_launch_ms": roll_ms_t, "model_terms": int(support[0].sum()),

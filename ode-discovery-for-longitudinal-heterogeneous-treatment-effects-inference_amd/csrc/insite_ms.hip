@@ -555,6 +555,7 @@ struct Ms4Z {
   static constexpr int CG = PG + QG;            // Z side
   static constexpr int NB = RG * CG - RG * (RG - 1) / 2;
   static constexpr int STRIDE = (4 * PG) | 1;   // odd, >= every pure position
+  static constexpr bool kCover = false;
   static_assert(4 * CG <= kMsMaxF, "column map");
   int pos_a[CG][4], pos_b[CG][4];  // staged positions of the factors (pure groups: pos_b unused)
   int col[4 * CG];                 // logical column of slot 4 g + i: 0..F-1 library, F..F+S-1 xdot, -1 pad
@@ -644,6 +645,18 @@ __device__ __forceinline__ Ms4ZPtr<Ms4Z<S, NZ, INTER>::QG> ms4z_ptrs(const doubl
   return p;
 }
 
+// compiler-only ordering of LDS accesses (the hardware keeps one wave's DS instructions in order)
+__device__ __forceinline__ void ms4z_order() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+#ifndef INSITE_MS4_SKEW
+#define INSITE_MS4_SKEW 0
+#endif
+#ifndef INSITE_MS4_SKEW_EARLY
+#define INSITE_MS4_SKEW_EARLY 0
+#endif
+
 __device__ __forceinline__ void ms4z_sync() {
 #if INSITE_MS4Z_SYNC
   wave_lds_sync();
@@ -728,14 +741,143 @@ __device__ __forceinline__ void ms4z_passes(const Ms4ZPtr<Ms4Z<S, NZ, INTER>::QG
   }
 }
 
+// ---- moment cover (C3, default): fewer blocks over the distinct moments ----
+// The Theta | xdot column groups above issue 27 blocks (432 cells per row) for 363 entries, but those entries
+// hold only 257 distinct moments: G entries are monomials z^g of degree <= 4 in z = (x_1..x_5, a), and a is
+// 0/1 (a^2 = a), so the 253 G entries are 147 moments; B adds 110.  tools/ms4_cover.py searches operand groups
+// -- each slot a product of <= 2 staged pure values (one LDS read, or two reads + one multiply; the same
+// staging as Ms4Z) -- whose pairwise 4 x 4 blocks cover all 257, and emits the groups, the block list and the
+// entry -> (block, m, n) map of ms4_finalize_cover (ms4_cover_c3.inc).  The products are exact in f64 wherever
+// the old form's were (x and a are fp32 values: products of two are exact); only operands xdot * x would round
+// once more, and the emitted cover has none.
+#include "ms4_cover_c3.inc"
 template <int S, int NZ, bool INTER>
-__device__ __forceinline__ void ms_emit4z(double* __restrict__ wrow, const Ms4ZPtr<Ms4Z<S, NZ, INTER>::QG>& pp,
-                                          bool valid, const double (&z)[NZ + 1], const double (&xd)[S],
-                                          double (&acc)[Ms4Z<S, NZ, INTER>::NB]) {
+struct Ms4Cover {
+  using LZ = Ms4Z<S, NZ, INTER>;
+  static_assert(S == 5 && NZ == 6 && INTER, "the emitted cover is the C3 library's");
+  static constexpr int F = LZ::F, STRIDE = LZ::STRIDE, NG = kMs4CoverNG, NB = kMs4CoverNB;
+  static constexpr bool kCover = true;
+  static constexpr bool prod(int g) { return kMs4CoverProd[g] != 0; }
+  static_assert(LZ::NPURE == 4 * LZ::PG, "every staged position holds a pure value (no pads)");
+  static_assert(4 * LZ::PG < 256, "factor positions fit a byte");
+};
+struct Ms4CPtr {
+  const double* row;  // &P[R0][0]
+  unsigned pa[(kMs4CoverNG + 3) / 4], pb[(kMs4CoverNG + 3) / 4];
+  __device__ const double* at_a(int g) const { return row + ((pa[g >> 2] >> (8 * (g & 3))) & 0xffu); }
+  __device__ const double* at_b(int g) const { return row + ((pb[g >> 2] >> (8 * (g & 3))) & 0xffu); }
+};
+template <int S, int NZ, bool INTER>
+__device__ __forceinline__ Ms4CPtr ms4c_ptrs(const double* wbase, int lane) {
+  using LC = Ms4Cover<S, NZ, INTER>;
+  const int k = lane >> 4, b = (lane >> 2) & 3, i = lane & 3;
+  const int r0 = 32 * (k >> 1) + 4 * (4 * (k & 1) + b);  // the rows of Ms4Z's conflict-free read pattern
+  Ms4CPtr p;
+  p.row = wbase + r0 * LC::STRIDE;
+#pragma unroll
+  for (int q = 0; q < (LC::NG + 3) / 4; ++q) p.pa[q] = p.pb[q] = 0u;
+#pragma unroll
+  for (int g = 0; g < LC::NG; ++g) {
+    unsigned a = kMs4CoverPA[g][0], bb = kMs4CoverPB[g][0];
+#pragma unroll
+    for (int ii = 1; ii < 4; ++ii) {
+      if (i == ii) {
+        a = kMs4CoverPA[g][ii];
+        bb = kMs4CoverPB[g][ii];
+      }
+    }
+    p.pa[g >> 2] |= a << (8 * (g & 3));
+    p.pb[g >> 2] |= bb << (8 * (g & 3));
+  }
+  return p;
+}
+// Operands of one pass (rows r of the staged buffer at offset boff doubles): per group the first factor, and the
+// second for the product groups.
+template <int S, int NZ, bool INTER>
+__device__ __forceinline__ void ms4c_fetch(const Ms4CPtr& pp, int off, double (&ra)[kMs4CoverNG],
+                                           double (&rb)[kMs4CoverNG]) {
+#pragma unroll
+  for (int g = 0; g < kMs4CoverNG; ++g) {
+    ra[g] = pp.at_a(g)[off];
+    if (Ms4Cover<S, NZ, INTER>::prod(g)) rb[g] = pp.at_b(g)[off];
+  }
+}
+// The 4 passes over the buffer at boff; PRE: pass 0's operands were fetched by the caller (ra0 / rb0), so their
+// LDS latency hid behind the caller's own work.
+template <int S, int NZ, bool INTER, bool PRE>
+__device__ __forceinline__ void ms4c_passes(const Ms4CPtr& pp, int boff, const double (&ra0)[kMs4CoverNG],
+                                            const double (&rb0)[kMs4CoverNG], double (&acc)[kMs4CoverNB]) {
+  using LC = Ms4Cover<S, NZ, INTER>;
+  double ra[2][LC::NG], rb[2][LC::NG];  // rb: product groups only; operands of pass r + 1 read during pass r
+  if constexpr (PRE) {
+#pragma unroll
+    for (int g = 0; g < LC::NG; ++g) {
+      ra[0][g] = ra0[g];
+      rb[0][g] = rb0[g];
+    }
+  } else {
+    ms4c_fetch<S, NZ, INTER>(pp, boff, ra[0], rb[0]);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#if INSITE_MS4_SCHED
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    if (r < 3) ms4c_fetch<S, NZ, INTER>(pp, boff + (r + 1) * LC::STRIDE, ra[(r + 1) & 1], rb[(r + 1) & 1]);
+    double v[LC::NG];
+#pragma unroll
+    for (int g = 0; g < LC::NG; ++g) v[g] = LC::prod(g) ? ra[r & 1][g] * rb[r & 1][g] : ra[r & 1][g];
+#pragma unroll
+    for (int t = 0; t < LC::NB; ++t)
+#if INSITE_MS4_ABL_NOMFMA
+      if (t == 0) acc[t] += v[kMs4CoverBU[t]] + v[kMs4CoverBV[t]];
+#else
+      acc[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(v[kMs4CoverBU[t]], v[kMs4CoverBV[t]], acc[t], 0, 0, 0);
+#endif
+  }
+}
+template <int S, int NZ, bool INTER>
+__device__ __forceinline__ void ms4c_passes(const Ms4CPtr& pp, double (&acc)[kMs4CoverNB]) {
+  double unused[kMs4CoverNG];
+  ms4c_passes<S, NZ, INTER, false>(pp, 0, unused, unused, acc);
+}
+
+// The cover stages the same pure values, at the positions kMs4CoverStage gives (bank-conflict-free reads).
+template <int S, int NZ>
+__device__ __forceinline__ void ms4c_stage(double* __restrict__ wp, double one, const double (&z)[NZ + 1],
+                                           const double (&xd)[S], bool valid) {
+  wp[kMs4CoverStage[0]] = one;
+#pragma unroll
+  for (int s = 1; s <= NZ; ++s) wp[kMs4CoverStage[s]] = valid ? z[s] : 0.0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) wp[kMs4CoverStage[NZ + 1 + s]] = valid ? xd[s] : 0.0;
+}
+
+// layout-generic per-lane read pointers, staging and passes
+template <int S, int NZ, bool INTER, class M4>
+__device__ __forceinline__ void ms4_stage(double* __restrict__ wp, const double (&z)[NZ + 1], const double (&xd)[S]) {
+  if constexpr (M4::kCover) ms4c_stage<S, NZ>(wp, 1.0, z, xd, true);
+  else ms4z_stage<S, NZ, INTER>(wp, z, xd);
+}
+template <int S, int NZ, bool INTER, class M4>
+__device__ __forceinline__ auto ms4_ptrs(const double* wbase, int lane) {
+  if constexpr (M4::kCover) return ms4c_ptrs<S, NZ, INTER>(wbase, lane);
+  else return ms4z_ptrs<S, NZ, INTER>(wbase, lane);
+}
+template <int S, int NZ, bool INTER, class PP, int NBX>
+__device__ __forceinline__ void ms4_passes(const PP& pp, double (&acc)[NBX]) {
+  if constexpr (std::is_same<PP, Ms4CPtr>::value) ms4c_passes<S, NZ, INTER>(pp, acc);
+  else ms4z_passes<S, NZ, INTER>(pp, acc);
+}
+
+template <int S, int NZ, bool INTER, class PP, int NBX>
+__device__ __forceinline__ void ms_emit4z(double* __restrict__ wrow, const PP& pp, bool valid,
+                                          const double (&z)[NZ + 1], const double (&xd)[S], double (&acc)[NBX]) {
   ms4z_sync();
-  ms4z_stage_masked<S, NZ, INTER>(wrow, valid, z, xd);
+  if constexpr (std::is_same<PP, Ms4CPtr>::value) ms4c_stage<S, NZ>(wrow, valid ? 1.0 : 0.0, z, xd, valid);
+  else ms4z_stage_masked<S, NZ, INTER>(wrow, valid, z, xd);
   ms4z_sync();
-  ms4z_passes<S, NZ, INTER>(pp, acc);
+  ms4_passes<S, NZ, INTER>(pp, acc);
 }
 
 // The full-row form's geometry in the same vocabulary (column map = identity over [Theta | xdot]).
@@ -744,6 +886,7 @@ struct Ms4Full {
   static constexpr int F = PolyCols<NZ, INTER>::F;
   using M4 = Ms4<S, F>;
   static constexpr int RG = M4::RG, CG = M4::CG, NB = M4::NB, STRIDE = kMs4Stride;
+  static constexpr bool kCover = false;
   int col[4 * CG];
   __host__ __device__ constexpr Ms4Full() : col() {
     for (int j = 0; j < 4 * CG; ++j) col[j] = j < F + S ? j : -1;
@@ -753,8 +896,16 @@ struct Ms4Full {
 #ifndef INSITE_MS4_FULLROW
 #define INSITE_MS4_FULLROW 0
 #endif
+// INSITE_MS4_COVER (default 1): the C3 library (5 states + one binary input, interaction only) takes the moment
+// cover; the other libraries (and INSITE_MS4_COVER=0) the Theta | xdot column groups
+#ifndef INSITE_MS4_COVER
+#define INSITE_MS4_COVER 1
+#endif
 template <int S, int NZ, bool INTER>
-using Ms4Layout = typename std::conditional<INSITE_MS4_FULLROW != 0, Ms4Full<S, NZ, INTER>, Ms4Z<S, NZ, INTER>>::type;
+using Ms4Layout = typename std::conditional<
+    INSITE_MS4_FULLROW != 0, Ms4Full<S, NZ, INTER>,
+    typename std::conditional<INSITE_MS4_COVER != 0 && S == 5 && NZ == 6 && INTER, Ms4Cover<S, NZ, INTER>,
+                              Ms4Z<S, NZ, INTER>>::type>::type;
 
 template <int S, int NIN, bool INTER>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_MS_WPE)))
@@ -763,8 +914,17 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
                 int nchunk) {
   constexpr int NZ = S + NIN;
   using M4 = Ms4Layout<S, NZ, INTER>;
-  // per wave: 64 staged rows, then (staged-factor form) 64 trash rows that invalid interior rows go to
-  constexpr int kWaveStage = (INSITE_MS4_FULLROW ? 1 : 2) * kWave * M4::STRIDE;
+  // INSITE_MS4_SKEW (A/B, default off): the interior stages row t into one of two buffers while the passes run
+  // over row t - 1 in the other, whose pass-0 operands are read ahead of the stores -- the staging stores and the
+  // first reads no longer sit between the VALU work and the MFMAs.  Measured neutral-to-slower (7.92 / 7.93 ms
+  // with the reads ahead of the stores / of the derivative work, vs 7.86 ms, profiles/r05/c3/): the LDS waits
+  // (SQ_WAIT_INST_LDS ~237 cycles per wave-step) were already covered by the partner wave's MFMAs.
+  constexpr bool kSkew = INSITE_MS4_SKEW && M4::kCover && !INSITE_MS4_FULLROW && !INSITE_MS4Z_MASKSEL;
+  static_assert(kMs4Ring % 2 == 0, "buffer parity of step t = parity of its ring slot");
+  constexpr int kBuf = kWave * M4::STRIDE;  // doubles per staged 64-row buffer
+  // per wave: 64 staged rows (two buffers when skewed), then (staged-factor form) 64 trash rows that invalid
+  // interior rows go to
+  constexpr int kWaveStage = (INSITE_MS4_FULLROW ? 1 : kSkew ? 3 : 2) * kBuf;
   static_assert(M4::NB * 16 * kWavesPerBlock <= kWavesPerBlock * kWaveStage, "block reduction fits the stage");
   __shared__ double stage[kWavesPerBlock * kWaveStage];
   const int lane = threadIdx.x & (kWave - 1);
@@ -775,7 +935,7 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
   double* wbase = stage + wid * kWaveStage;
   double* wrow = wbase + lane * M4::STRIDE;
 #if !INSITE_MS4_FULLROW
-  const auto zptr = ms4z_ptrs<S, NZ, INTER>(wbase, lane);
+  const auto zptr = ms4_ptrs<S, NZ, INTER, M4>(wbase, lane);
 #endif
   double acc[M4::NB];
 #pragma unroll
@@ -859,6 +1019,17 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
 #endif
             if (t >= ea) {  // row r = t - 4: raw x[r], xdot from x[r-4 .. r+4] (slots i-8 .. i)
               const int r = t - 4;
+              // skewed: step t stages into buffer (t - ts) & 1 = i & 1 and passes over the other (row t - 1)
+              const int cb = (i & 1) * kBuf, pbf = kBuf - cb;  // constants once unrolled
+              // skewed: pass-0 operands of row t - 1 (read unconditionally -- at t == ea the stale buffer's
+              // values go unused -- so they are not live across steps)
+              double pa0[kMs4CoverNG], pb0[kMs4CoverNG];
+#if INSITE_MS4_SKEW_EARLY
+              if constexpr (kSkew) {
+                ms4c_fetch<S, NZ, INTER>(zptr, pbf, pa0, pb0);
+                __builtin_amdgcn_sched_barrier(0);  // issued before the derivative work
+              }
+#endif
               if ((r & 31) == 0) wcur = word(r >> 5);
               double z[NZ + 1], xd[S];
               z[0] = 1.0;
@@ -883,16 +1054,36 @@ gram_ms4_kernel(const float* __restrict__ x, int64_t ldx, int n_steps, const uin
 #else
               // rows past a lane's end go to its trash row; its staged row is zeroed once, at the first
               // such row (t == tz), and stays zero for the rest of the interior
-              ms4z_sync();
-              ms4z_stage<S, NZ, INTER>(t <= L - 1 ? wrow : wrow + kWave * M4::STRIDE, z, xd);
-              if (t == tzc) ms4z_zero<S, NZ, INTER>(wrow);
-              ms4z_sync();
-              ms4z_passes<S, NZ, INTER>(zptr, acc);
+              if constexpr (kSkew) {
+                // the LDS executes one wave's DS instructions in issue order: the stores of row t cannot pass the
+                // reads of row t - 2 (same buffer, step t - 1), and row t - 1's stores are complete before this
+                // step's reads of it -- only the compiler's order is pinned here.  A lane past its end zeroes its
+                // row in both buffers (steps tzc, tzc + 1), its rows go to the trash row.
+#if !INSITE_MS4_SKEW_EARLY
+                ms4c_fetch<S, NZ, INTER>(zptr, pbf, pa0, pb0);  // ahead of the stores
+#endif
+                ms4z_order();
+                ms4_stage<S, NZ, INTER, M4>(t <= L - 1 ? wrow + cb : wrow + 2 * kBuf, z, xd);
+                if (t == tzc || t == tzc + 1) ms4z_zero<S, NZ, INTER>(wrow + cb);
+                ms4z_order();
+                if (t > ea) ms4c_passes<S, NZ, INTER, true>(zptr, pbf, pa0, pb0, acc);
+              } else {
+                ms4z_sync();
+                ms4_stage<S, NZ, INTER, M4>(t <= L - 1 ? wrow : wrow + kBuf, z, xd);
+                if (t == tzc) ms4z_zero<S, NZ, INTER>(wrow);
+                ms4z_sync();
+                ms4_passes<S, NZ, INTER>(zptr, acc);
+              }
 #endif
 #endif
             }
           }
         }
+      }
+      if constexpr (kSkew) {  // the chunk's last row (step eb - 1) has not had its passes
+        ms4z_order();
+        double unused[kMs4CoverNG];
+        ms4c_passes<S, NZ, INTER, false>(zptr, ((eb - 1 - ts) & 1) * kBuf, unused, unused, acc);
       }
     }
 
@@ -1006,6 +1197,19 @@ __global__ void __launch_bounds__(kWave) ms4_finalize(const double* __restrict__
   } else if (b < F) {
     B[(int64_t)b * S + (a - F)] = v;
   }
+}
+
+// The moment cover's finalize: one lane per output entry (G row-major, then B row-major) reduces the partial
+// its moment lives in, in block order (symmetric G entries read the same partial: bitwise equal halves).
+__global__ void __launch_bounds__(kWave) ms4_finalize_cover(const double* __restrict__ partial, int nblk, int nb,
+                                                            int F, double* __restrict__ G, double* __restrict__ B) {
+  const int e = blockIdx.x * kWave + threadIdx.x;
+  if (e >= kMs4CoverEntries) return;
+  const int q = kMs4CoverMap[e];
+  double v = 0.0;
+  for (int g = 0; g < nblk; ++g) v += partial[(int64_t)g * nb * 16 + q];
+  if (e < F * F) G[e] = v;
+  else B[e - F * F] = v;
 }
 
 // Fixed-order reduction of the tile partials and scatter into G [F, F] (symmetric) and B [F, S].
@@ -1596,13 +1800,18 @@ int32_t insite_gram_ms_f32(const float* x, int64_t ldx, int32_t n_steps, int32_t
   ms_finalize<<<(kMsTiles * 256 + kWave - 1) / kWave, kWave, 0, hs>>>(part, grid, n_terms, n_states, G_out, B_out);
 #else
   int nb = 0, cgn = 0;
+  bool cover = false;
   Ms4Map map{};
   auto geom = [&](auto m4) {
     using M4 = decltype(m4);
     static_assert(M4::NB * 16 <= kMsTiles * 256, "workspace holds the block partials");
     nb = M4::NB;
-    cgn = M4::CG;
-    for (int j = 0; j < kMsMaxF; ++j) map.col[j] = j < 4 * M4::CG ? m4.col[j] : -1;
+    if constexpr (M4::kCover) {
+      cover = true;
+    } else {
+      cgn = M4::CG;
+      for (int j = 0; j < kMsMaxF; ++j) map.col[j] = j < 4 * M4::CG ? m4.col[j] : -1;
+    }
   };
 #ifdef INSITE_MS4_NCHUNK
   const int nchunk = INSITE_MS4_NCHUNK;
@@ -1626,8 +1835,13 @@ int32_t insite_gram_ms_f32(const float* x, int64_t ldx, int32_t n_steps, int32_t
   }
   int32_t st = launch_status();
   if (st != INSITE_OK) return st;
-  ms4_finalize<<<(nb * 16 + kWave - 1) / kWave, kWave, 0, hs>>>(part, grid, nb, cgn, n_terms, n_states, map, G_out,
-                                                                B_out);
+  if (cover) {
+    if (n_terms * n_terms + n_terms * n_states != kMs4CoverEntries) return INSITE_E_INVALID_ARG;
+    ms4_finalize_cover<<<(kMs4CoverEntries + kWave - 1) / kWave, kWave, 0, hs>>>(part, grid, nb, n_terms, G_out, B_out);
+  } else {
+    ms4_finalize<<<(nb * 16 + kWave - 1) / kWave, kWave, 0, hs>>>(part, grid, nb, cgn, n_terms, n_states, map, G_out,
+                                                                  B_out);
+  }
 #endif
   return launch_status();
 }
