@@ -1308,8 +1308,15 @@ def insite4_main(args):
                      "mean_evaluations_per_refined_row": float(nf.to(torch.float64)[s2 >= 0].mean().item()),
                      "equal_to_nfev_route": bool(torch.equal(p2, preds) and torch.equal(s2, status)),
                      "finite_predictions": bool(torch.isfinite(preds).all().item()), "algorithmic_flop": flop}
+        # evaluation-count divergence inside a wave: a wave runs as many objective scans as its slowest row
+        # (8 rows a wave in the cooperative kernel, 64 in the one-row-per-lane kernels), rows in the lane order
+        o_ = plan.order.long() if getattr(plan, "order", None) is not None else torch.arange(N, device=dev)
+        rpw = 8 if res[name]["kernel"].startswith("insite_refine_coop") else 64
+        nfo = nf.index_select(0, o_).to(torch.float64)
+        nfo = torch.cat([nfo, nfo.new_zeros((-N) % rpw)]).view(-1, rpw)
+        res[name]["wave_divergence"] = {"rows_per_wave": rpw, "max_over_mean_evaluations":
+                                        float(nfo.max(1).values.sum().item() * rpw / max(nfo.sum().item(), 1.0))}
         if not args.no_parity:   # the dense / joint oracle rows cost ~4 ms each on one host core
-            o_ = plan.order.long() if getattr(plan, "order", None) is not None else torch.arange(N, device=dev)
             res[name]["parity"] = insite_parity(V, arm, u, sl, c0, lb, dt, 10.0, 5, preds, coef, status, iters,
                                                 n_sample=4096 if name == "sparse" else 2048, seed=17,
                                                 extra=(o_[:64].cpu().numpy(), o_[-64:].cpu().numpy()))

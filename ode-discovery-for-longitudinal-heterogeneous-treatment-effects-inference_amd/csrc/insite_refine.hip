@@ -188,6 +188,31 @@ __device__ __forceinline__ void ring_wait() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// Sums over the M coordinates of the BFGS vectors (dot products, the penalty, y^T H y, |g|^2).  M = 16 (the dense
+// models; INSITE_REFINE_TREE): in the association of the cooperative kernel's 8-lane group reduction -- lane j holds
+// coordinates j and j + 8, then butterfly pairs (j, j^1), (j, j^2), (j, j^4) -- so the cooperative kernel takes its
+// dot products with three in-group exchanges instead of 16 gathers and 16 dependent adds, and stays bitwise equal to
+// this kernel; the leading 0.0 + keeps the sequential sum's +0 for an all-zero sum.  Other M: coordinate order.
+#ifndef INSITE_REFINE_TREE
+#define INSITE_REFINE_TREE 1
+#endif
+template <int M>
+__device__ __forceinline__ double coord_sum(const double (&v)[M]) {
+#pragma clang fp contract(off)  // NC
+  if constexpr (M == 16 && INSITE_REFINE_TREE) {
+    double l[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) l[j] = v[j] + v[j + 8];
+    const double m0 = l[0] + l[1], m1 = l[2] + l[3], m2 = l[4] + l[5], m3 = l[6] + l[7];
+    return 0.0 + ((m0 + m1) + (m2 + m3));
+  } else {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) s += v[i];
+    return s;
+  }
+}
+
 template <int M, int NA, int D, bool WIN = false, bool PM = false>
 struct RefineLane {
   static constexpr int RU = M <= kRefineRegActive ? M : 1;
@@ -411,16 +436,18 @@ struct RefineLane {
     }
     const double iK = 1.0 / (double)K;   // (a non-live WIN lane divides by its own K too; its values are unused)
     L *= iK;
-    double pen = 0.0;
+    double pen = 0.0, sq[M];
 #pragma unroll RU
     for (int i = 0; i < M; ++i) {
 #pragma clang fp contract(off)  // NC
+      sq[i] = 0.0;
       if (i >= ra.m) {
         g[i] = 0.0;
         continue;
       }
       const double dd = c0a[i] - c[i];
-      pen += dd * dd;
+      if constexpr (M == 16 && INSITE_REFINE_TREE) sq[i] = dd * dd;
+      else pen += dd * dd;
       double gd = 0.0;
       if constexpr (kGmap) {
 #pragma unroll
@@ -439,14 +466,15 @@ struct RefineLane {
       }
       g[i] = gd * iK * mono[i] / norm + 2.0 * ra.lam * (c[i] - c0a[i]) / (double)ra.n_coef;
     }
+    if constexpr (M == 16 && INSITE_REFINE_TREE) pen = coord_sum(sq);
     return L / norm + ra.lam * pen / (double)ra.n_coef;
   }
   __device__ double dot(const double (&a)[M], const double (&b)[M]) const {
 #pragma clang fp contract(off)  // NC
-    double s = 0.0;
+    double pr[M];
 #pragma unroll RU
-    for (int i = 0; i < M; ++i) s += a[i] * b[i];
-    return s;
+    for (int i = 0; i < M; ++i) pr[i] = a[i] * b[i];
+    return coord_sum(pr);
   }
   // phi(t) = f(x + t pk), dphi = g . pk
   __device__ double phi(const double (&x)[M], const double (&pk)[M], double t, double& dphi, double (&g)[M],
@@ -566,12 +594,13 @@ struct BfgsFlat {
     for (int i = 0; i < M; ++i)
 #pragma unroll RU
       for (int j = 0; j < M; ++j) H.at(i, j) = i == j ? 1.0 : 0.0;
-    double gmax = 0.0, g2 = 0.0;
+    double gmax = 0.0, g2 = 0.0, gsq[M];
 #pragma unroll RU
     for (int i = 0; i < M; ++i) {
       gmax = fmax(gmax, fabs(g[i]));
-      g2 += g[i] * g[i];
+      gsq[i] = g[i] * g[i];
     }
+    g2 = coord_sum(gsq);
     converged = gmax < 1e-5;
     failed = false;
     old_old = f + sqrt(g2) / 2.0;
@@ -691,16 +720,16 @@ struct BfgsFlat {
     const double rho = 1.0 / ln.dot(yk, sk);
     if constexpr (RU == 1 || INSITE_REFINE_QUAD) {  // (compile-time: the rolled kernels never hold the WH temporary)
      if (isfinite(rho)) {
-      double hy[M];
-      double yhy = 0.0;
+      double hy[M], yh[M];
 #pragma unroll RU
       for (int i = 0; i < M; ++i) {
         double t = 0.0;
 #pragma unroll RU
         for (int j = 0; j < M; ++j) t += H.at(i, j) * yk[j];
         hy[i] = t;
-        yhy += yk[i] * t;
+        yh[i] = yk[i] * t;
       }
+      const double yhy = coord_sum(yh);
       const double cs = rho * rho * yhy + rho;
 #pragma unroll RU
       for (int i = 0; i < M; ++i)
@@ -849,12 +878,13 @@ insite_refine_kernel(RefineArgs) {
     double f = start / ln.norm + 0.0;
 #pragma unroll RU
     for (int i = 0; i < M; ++i) g[i] = g[i] / ln.norm + 0.0;
-    double gmax = 0.0, g2 = 0.0;
+    double gmax = 0.0, gsq[M];
 #pragma unroll RU
     for (int i = 0; i < M; ++i) {
       gmax = fmax(gmax, fabs(g[i]));
-      g2 += g[i] * g[i];
+      gsq[i] = g[i] * g[i];
     }
+    const double g2 = coord_sum(gsq);
     bool converged = gmax < 1e-5, failed = false;
     double old_old = f + sqrt(g2) / 2.0;
     int ls_status = 0;
@@ -988,16 +1018,16 @@ insite_refine_kernel(RefineArgs) {
         //   = H - rho (s (H y)^T + (H y) s^T) + (rho^2 y^T H y + rho) s s^T   (H symmetric),
         // instead of two O(M^3) products through two more M x M scratch matrices; the association order
         // differs from the oracle's w @ H @ w.T (jax's three-operand einsum fixes none either)
-        double hy[M];
-        double yhy = 0.0;
+        double hy[M], yh[M];
 #pragma unroll RU
         for (int i = 0; i < M; ++i) {
           double t = 0.0;
 #pragma unroll RU
           for (int j = 0; j < M; ++j) t += H.at(i, j) * yk[j];
           hy[i] = t;
-          yhy += yk[i] * t;
+          yh[i] = yk[i] * t;
         }
+        const double yhy = coord_sum(yh);
         const double cs = rho * rho * yhy + rho;
 #pragma unroll RU
         for (int i = 0; i < M; ++i)
@@ -1418,6 +1448,9 @@ __global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs,
 #ifndef INSITE_REFINE_COOP_WPE
 #define INSITE_REFINE_COOP_WPE 2
 #endif
+#ifndef INSITE_COOP_SCAN_PIPE
+#define INSITE_COOP_SCAN_PIPE 1  // the cooperative kernel's software-pipelined closed-form scan (0: the step-wise one)
+#endif
 constexpr int kCoopG = 8;  // lanes per row
 
 constexpr int kCoopStT = 64;  // staged steps (STG)
@@ -1442,6 +1475,23 @@ __device__ __forceinline__ double grp_lane(double v, int c) {  // c a constant a
     case 6: return grp_lane<6>(v);
     default: return grp_lane<7>(v);
   }
+}
+// lane j ^ X of the reading lane's 8-lane group (ds_swizzle bitmask mode: and 0x1f, xor X)
+template <int X>
+__device__ __forceinline__ double grp_xor(double v) {
+  constexpr int kPat = 0x1f | (X << 10);
+  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), kPat);
+  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), kPat);
+  return __hiloint2double(hi, lo);
+}
+// coord_sum<16> over the group: v = the lane's own pair (coordinates j and j + 8) summed; every lane gets the same
+// bits (each butterfly level adds two equal-valued operands in either order)
+__device__ __forceinline__ double grp_tree_sum(double v) {
+#pragma clang fp contract(off)  // NC
+  v = v + grp_xor<1>(v);
+  v = v + grp_xor<2>(v);
+  v = v + grp_xor<4>(v);
+  return 0.0 + v;
 }
 template <int MC, int NA, bool STG>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_REFINE_COOP_WPE)))
@@ -1576,6 +1626,62 @@ insite_refine_coop_kernel(RefineArgs) {
     int Kw = Kl;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) Kw = max(Kw, __shfl_xor(Kw, off));
+#if INSITE_COOP_SCAN_PIPE
+    if constexpr (STG && INSITE_REFINE_CF) {
+      // software-pipelined scan: step k's arm constants (5 doubles from the LDS table) and target are read during
+      // step k - 1, and its arm index during step k - 2, so no step waits on an LDS round trip of its own (the
+      // per-step table lookup after the arm read exposed two dependent LDS latencies a step); the addition term
+      // is formed branch-free.  The arithmetic is the CF branch below, op for op.
+      const double* const wCfr = wCf + rs * NA * kCf5;
+      const int last = ra.T - 1;  // staged steps 0 .. T - 1: reads past the scan are clamped (values unused)
+      struct Step {
+        double P, B, hS, C1, C2, v;
+        int a;
+      };
+      auto load = [&](int a, int k) -> Step {  // constants of arm a and the target of step k (k + 1's sample)
+        const double* const q = wCfr + a * kCf5;
+        return Step{q[0], q[1], q[2], q[3], q[4], v_at(min(k + 1, last)), a};
+      };
+      auto step = [&](const Step& c, int k) {
+        if (k < Kl) {
+          const double tv = te ? fma(c.C1, y, c.C2) : c.hS;
+          const double add = c.a == ta ? tv : 0.0;
+          d = fma(c.P, d, add);
+          y = fma(c.P, y, c.B);
+          const double r = c.v - y;
+          L = fma(r, r, L);
+          gGo = fma(-2.0 * r, d, gGo);
+        }
+      };
+      if (Kw > 0) {
+        // two register sets alternate (s0, s1): while step k computes, step k + 1's constants are in flight, their
+        // arm index read three steps earlier (arm k + j in am[(k + j) % 4]) -- the LDS counter is in order, so an
+        // arm read one step ahead made the next lookup wait for everything issued in between
+        int am[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) am[q] = a_at(min(q, last));
+        Step s0 = load(am[0], 0), s1;
+        for (int k = 0; k < Kw; k += 4) {  // (Kw wave-uniform: the breaks are uniform)
+          s1 = load(am[1], k + 1);
+          am[0] = a_at(min(k + 4, last));
+          step(s0, k);
+          if (k + 1 >= Kw) break;
+          s0 = load(am[2], k + 2);
+          am[1] = a_at(min(k + 5, last));
+          step(s1, k + 1);
+          if (k + 2 >= Kw) break;
+          s1 = load(am[3], k + 3);
+          am[2] = a_at(min(k + 6, last));
+          step(s0, k + 2);
+          if (k + 3 >= Kw) break;
+          s0 = load(am[0], k + 4);
+          am[3] = a_at(min(k + 7, last));
+          step(s1, k + 3);
+        }
+      }
+    } else
+#endif
+    {
     int ak_nx = Kw > 0 ? a_at(0) : 0;
     double v_nx = Kw > 0 ? v_at(1) : 0.0;
     for (int k = 0; k < Kw; ++k) {
@@ -1620,6 +1726,7 @@ insite_refine_coop_kernel(RefineArgs) {
         gGo = fma(-2.0 * r, d, gGo);
       }
     }
+    }
     const double iK = 1.0 / (double)K;
     L *= iK;
     double gG[NA][2];
@@ -1628,12 +1735,17 @@ insite_refine_coop_kernel(RefineArgs) {
 #pragma unroll
       for (int e = 0; e <= 1; ++e) gG[a][e] = INSITE_REFINE_SWZ ? grp_lane(gGo, 2 * a + e) : __shfl(gGo, gbase + 2 * a + e);
     double pen = 0.0;
+    if constexpr (MC == 16 && INSITE_REFINE_TREE) {
+#pragma clang fp contract(off)  // NC
+      pen = grp_tree_sum((j < ra.m ? sq[0] : 0.0) + (j + kCoopG < ra.m ? sq[1] : 0.0));
+    } else {
 #pragma unroll
     for (int i = 0; i < MC; ++i) {
 #pragma clang fp contract(off)  // NC
       const double sqi = gat(sq, i);
       if (i >= ra.m) break;
       pen += sqi;
+    }
     }
     // the gradient of this lane's own coordinates only (each lane its S, not the wave all MC under owner masks)
 #pragma unroll
@@ -1659,10 +1771,14 @@ insite_refine_coop_kernel(RefineArgs) {
     double pr[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) pr[s] = a[s] * b[s];
-    double s_ = 0.0;
+    if constexpr (MC == 16 && INSITE_REFINE_TREE) {
+      return grp_tree_sum(pr[0] + pr[1]);
+    } else {
+      double s_ = 0.0;
 #pragma unroll
-    for (int i = 0; i < MC; ++i) s_ += gat(pr, i);
-    return s_;
+      for (int i = 0; i < MC; ++i) s_ += gat(pr, i);
+      return s_;
+    }
   };
   // ---- the flat BFGS state machine (BfgsFlat with the vectors distributed; the QUAD update of RU = 1) ----
   double x[S], g[S], pk[S], g_star[S], Hr[S][MC];
@@ -1738,11 +1854,18 @@ insite_refine_coop_kernel(RefineArgs) {
 #pragma unroll
       for (int q = 0; q < MC; ++q) Hr[s][q] = (j + kCoopG * s) == q ? 1.0 : 0.0;
     double gmax = 0.0, g2 = 0.0;
+    if constexpr (MC == 16 && INSITE_REFINE_TREE) {
+      gmax = fmax(fabs(g[0]), fabs(g[1]));
+#pragma unroll
+      for (int off = 1; off < kCoopG; off <<= 1) gmax = fmax(gmax, __shfl_xor(gmax, off));  // (max: any order)
+      g2 = dot(g, g);
+    } else {
 #pragma unroll
     for (int i = 0; i < MC; ++i) {
       const double gi = gat(g, i);
       gmax = fmax(gmax, fabs(gi));
       g2 += gi * gi;
+    }
     }
     converged = gmax < 1e-5;
     old_old = f + sqrt(g2) / 2.0;
