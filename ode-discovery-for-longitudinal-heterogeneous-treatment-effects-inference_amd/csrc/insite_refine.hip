@@ -1448,12 +1448,16 @@ __global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs,
 #ifndef INSITE_REFINE_COOP_WPE
 #define INSITE_REFINE_COOP_WPE 2
 #endif
+#ifndef INSITE_COOP_LDSV
+#define INSITE_COOP_LDSV 1  // the cooperative kernel's whole-vector exchanges through LDS (0: per-coordinate swizzles)
+#endif
 #ifndef INSITE_COOP_SCAN_PIPE
 #define INSITE_COOP_SCAN_PIPE 1  // the cooperative kernel's software-pipelined closed-form scan (0: the step-wise one)
 #endif
 constexpr int kCoopG = 8;  // lanes per row
 
 constexpr int kCoopStT = 64;  // staged steps (STG)
+constexpr int kCoopStPad = 8;
 // lane C of the reading lane's 8-lane group: ds_swizzle in bitmask mode (and 0x18, or C: the group's base within the
 // 32-lane half, plus C) -- the value of __shfl(v, group base + C) without the per-lane address of ds_bpermute
 template <int C>
@@ -1510,8 +1514,13 @@ insite_refine_coop_kernel(RefineArgs) {
   const int64_t p = ra.order ? (int64_t)ra.order[grc] : grc;
   const int ta = j >> 1, te = j & 1;  // this lane's tangent (arm, exponent)
   // the wave's rows staged in LDS: [step][row slot] doubles / arm bytes (row slot = lane / 8)
-  __shared__ double sV[STG ? kWavesPerBlock * kCoopStT * kCoopG : 1];
+  // (the pipelined scan reads up to 4 steps past its end unclamped: kCoopStPad steps of padding, never used)
+  constexpr int kPipe = STG && INSITE_REFINE_CF && INSITE_COOP_SCAN_PIPE;
+  constexpr int kStT = kCoopStT + (kPipe ? kCoopStPad : 0);
+  __shared__ double sV[STG ? kWavesPerBlock * kStT * kCoopG : 1];
   __shared__ int8_t sA[STG ? kWavesPerBlock * kCoopStT * kCoopG : 1];
+  // kPipe: step k's arm as the byte offset of its constants in the row's table, (row slot * NA + arm) * 40
+  __shared__ int sO[kPipe ? kWavesPerBlock * kStT * kCoopG : 1];
   // the per-arm closed-form constants of the current evaluation (CfArm: P, B, hS, C1, C2), [row slot][arm][5] per
   // wave: written once per evaluation by the (ta, te = 0) lane of each arm, read per step by every lane of the row
   // at its step's arm (the 8 lanes of a row read one address: an LDS broadcast) -- instead of every lane computing
@@ -1520,8 +1529,9 @@ insite_refine_coop_kernel(RefineArgs) {
   __shared__ double sCf[INSITE_REFINE_CF ? kWavesPerBlock * kCoopG * NA * kCf5 : 1];
   const int rs = lane / kCoopG, wv = threadIdx.x / kWave;
   double* const wCf = sCf + (INSITE_REFINE_CF ? wv * kCoopG * NA * kCf5 : 0);
-  double* const wV = sV + (STG ? wv * kCoopStT * kCoopG : 0);
+  double* const wV = sV + (STG ? wv * kStT * kCoopG : 0);
   int8_t* const wA = sA + (STG ? wv * kCoopStT * kCoopG : 0);
+  int* const wO = sO + (kPipe ? wv * kStT * kCoopG : 0);
   if constexpr (STG) {  // (ra.T <= kCoopStT, checked at the launch)
     long long pg[kCoopG];
 #pragma unroll
@@ -1530,7 +1540,9 @@ insite_refine_coop_kernel(RefineArgs) {
 #pragma unroll
       for (int g = 0; g < kCoopG; ++g) {
         wV[lane * kCoopG + g] = ra.V[(int64_t)lane * ra.ldv + pg[g]];
-        wA[lane * kCoopG + g] = ra.arm8[(int64_t)lane * ra.lda + pg[g]];
+        const int8_t am = ra.arm8[(int64_t)lane * ra.lda + pg[g]];
+        wA[lane * kCoopG + g] = am;
+        if constexpr (kPipe) wO[lane * kCoopG + g] = (g * NA + am) * kCf5 * (int)sizeof(double);
       }
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1542,6 +1554,28 @@ insite_refine_coop_kernel(RefineArgs) {
   auto gat = [&](const double (&v)[S], int i) -> double {
     return INSITE_REFINE_SWZ ? grp_lane(v[i / kCoopG], i % kCoopG) : __shfl(v[i / kCoopG], gbase + (i % kCoopG));
   };
+  // LDSV: a distributed vector reaches every lane of its group through LDS -- each lane stores its S coordinates
+  // (2 ds_write_b64), then every lane reads the MC values in coordinate order two at a time (MC / 2 ds_read_b128,
+  // one address per group: a broadcast) -- instead of one 2 x ds_swizzle gather per coordinate (32 LDS
+  // instructions for 16 values, 10 here).  Two buffers per group (the inverse-Hessian update needs sk and H yk at
+  // once).  The LDS keeps one wave's accesses in issue order; only the compiler's order is pinned (vx_sync).
+  constexpr int kVx = INSITE_COOP_LDSV && MC == 2 * kCoopG ? MC : 2;
+  __shared__ __attribute__((aligned(16))) double sVx[kWavesPerBlock * kCoopG * 2 * kVx];
+  double* const wVx = sVx + (wv * kCoopG + rs) * 2 * kVx;
+  auto vx_sync = [&]() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto vx_store = [&](const double (&v)[S], int buf) {
+    vx_sync();
+#pragma unroll
+    for (int s = 0; s < S; ++s) wVx[buf * kVx + j + kCoopG * s] = v[s];
+    vx_sync();
+  };
+  auto vx_load2 = [&](int buf, int q) -> double2 {  // coordinates 2 q and 2 q + 1
+    return *reinterpret_cast<const double2*>(wVx + buf * kVx + 2 * q);
+  };
+  constexpr bool kLdsv = INSITE_COOP_LDSV && MC == 2 * kCoopG;
   double uu[INSITE_MAX_STATICS];
 #pragma unroll
   for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < ra.U ? ra.u[p * ra.U + t] : 0.0;
@@ -1591,12 +1625,23 @@ insite_refine_coop_kernel(RefineArgs) {
     // gamma_{ta,te} on lane j (the coefficients routed to it, in coefficient order: the single-lane kernel's sum),
     // then gathered: lane 2a + e holds gamma_{a,e}
     double gown = 0.0;
+    if constexpr (kLdsv) {
+      vx_store(tm, 0);
+#pragma unroll
+      for (int q = 0; q < MC / 2; ++q) {
+#pragma clang fp contract(off)  // NC
+        const double2 t = vx_load2(0, q);
+        if ((rbits >> (2 * q)) & 1u) gown += t.x;
+        if ((rbits >> (2 * q + 1)) & 1u) gown += t.y;
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < MC; ++i) {
 #pragma clang fp contract(off)  // NC
       if (i >= ra.m) break;
       const double t = gat(tm, i);  // c_i m_i, formed on coordinate i's lane
       if ((rbits >> i) & 1u) gown += t;
+    }
     }
     const double h = ra.dt / (double)ra.sub;
     double gam[NA][2];
@@ -1632,20 +1677,23 @@ insite_refine_coop_kernel(RefineArgs) {
       // step k - 1, and its arm index during step k - 2, so no step waits on an LDS round trip of its own (the
       // per-step table lookup after the arm read exposed two dependent LDS latencies a step); the addition term
       // is formed branch-free.  The arithmetic is the CF branch below, op for op.
-      const double* const wCfr = wCf + rs * NA * kCf5;
-      const int last = ra.T - 1;  // staged steps 0 .. T - 1: reads past the scan are clamped (values unused)
+      // row slot rs's staged steps: target of step k at vr[8 (k + 1)], its arm's constants at wCf + or[8 k] bytes
+      const double* const vr = wV + rs;
+      const int* const orow = wO + rs;
+      const char* const cfb = reinterpret_cast<const char*>(wCf);
       struct Step {
         double P, B, hS, C1, C2, v;
-        int a;
+        int off;
       };
-      auto load = [&](int a, int k) -> Step {  // constants of arm a and the target of step k (k + 1's sample)
-        const double* const q = wCfr + a * kCf5;
-        return Step{q[0], q[1], q[2], q[3], q[4], v_at(min(k + 1, last)), a};
+      auto load = [&](int off, int k) -> Step {  // constants at byte offset off and the target of step k
+        const double* const q = reinterpret_cast<const double*>(cfb + off);
+        return Step{q[0], q[1], q[2], q[3], q[4], vr[(k + 1) * kCoopG], off};
       };
+      const int own = (rs * NA + ta) * kCf5 * (int)sizeof(double);  // this lane's tangent arm, as an offset
       auto step = [&](const Step& c, int k) {
         if (k < Kl) {
           const double tv = te ? fma(c.C1, y, c.C2) : c.hS;
-          const double add = c.a == ta ? tv : 0.0;
+          const double add = c.off == own ? tv : 0.0;
           d = fma(c.P, d, add);
           y = fma(c.P, y, c.B);
           const double r = c.v - y;
@@ -1655,27 +1703,28 @@ insite_refine_coop_kernel(RefineArgs) {
       };
       if (Kw > 0) {
         // two register sets alternate (s0, s1): while step k computes, step k + 1's constants are in flight, their
-        // arm index read three steps earlier (arm k + j in am[(k + j) % 4]) -- the LDS counter is in order, so an
-        // arm read one step ahead made the next lookup wait for everything issued in between
+        // offset read three steps earlier (step k + j's in am[(k + j) % 4]) -- the LDS counter is in order, so an
+        // arm read one step ahead made the next lookup wait for everything issued in between.  Reads past the
+        // scan's end land in the padding (their values are never used).
         int am[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) am[q] = a_at(min(q, last));
+        for (int q = 0; q < 4; ++q) am[q] = orow[q * kCoopG];
         Step s0 = load(am[0], 0), s1;
         for (int k = 0; k < Kw; k += 4) {  // (Kw wave-uniform: the breaks are uniform)
           s1 = load(am[1], k + 1);
-          am[0] = a_at(min(k + 4, last));
+          am[0] = orow[(k + 4) * kCoopG];
           step(s0, k);
           if (k + 1 >= Kw) break;
           s0 = load(am[2], k + 2);
-          am[1] = a_at(min(k + 5, last));
+          am[1] = orow[(k + 5) * kCoopG];
           step(s1, k + 1);
           if (k + 2 >= Kw) break;
           s1 = load(am[3], k + 3);
-          am[2] = a_at(min(k + 6, last));
+          am[2] = orow[(k + 6) * kCoopG];
           step(s0, k + 2);
           if (k + 3 >= Kw) break;
           s0 = load(am[0], k + 4);
-          am[3] = a_at(min(k + 7, last));
+          am[3] = orow[(k + 7) * kCoopG];
           step(s1, k + 3);
         }
       }
@@ -1730,10 +1779,22 @@ insite_refine_coop_kernel(RefineArgs) {
     const double iK = 1.0 / (double)K;
     L *= iK;
     double gG[NA][2];
+    if constexpr (kLdsv) {  // tangent 2 a + e's gradient part sits on lane 2 a + e: one store, NA reads
+      vx_sync();
+      wVx[j] = gGo;
+      vx_sync();
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        const double2 t = vx_load2(0, a);
+        gG[a][0] = t.x;
+        gG[a][1] = t.y;
+      }
+    } else {
 #pragma unroll
     for (int a = 0; a < NA; ++a)
 #pragma unroll
       for (int e = 0; e <= 1; ++e) gG[a][e] = INSITE_REFINE_SWZ ? grp_lane(gGo, 2 * a + e) : __shfl(gGo, gbase + 2 * a + e);
+    }
     double pen = 0.0;
     if constexpr (MC == 16 && INSITE_REFINE_TREE) {
 #pragma clang fp contract(off)  // NC
@@ -1800,11 +1861,24 @@ insite_refine_coop_kernel(RefineArgs) {
     double acc[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) acc[s] = 0.0;
+    if constexpr (kLdsv) {
+      vx_store(g, 0);
+#pragma unroll
+      for (int q = 0; q < MC / 2; ++q) {
+        const double2 gq = vx_load2(0, q);
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          acc[s] += Hr[s][2 * q] * gq.x;
+          acc[s] += Hr[s][2 * q + 1] * gq.y;
+        }
+      }
+    } else {
 #pragma unroll
     for (int q = 0; q < MC; ++q) {
       const double gq = gat(g, q);
 #pragma unroll
       for (int s = 0; s < S; ++s) acc[s] += Hr[s][q] * gq;
+    }
     }
 #pragma unroll
     for (int s = 0; s < S; ++s) pk[s] = -acc[s];
@@ -1986,20 +2060,47 @@ insite_refine_coop_kernel(RefineArgs) {
       double hy[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) hy[s] = 0.0;
+      if constexpr (kLdsv) {
+        vx_store(yk, 0);
+#pragma unroll
+        for (int q = 0; q < MC / 2; ++q) {
+          const double2 yq = vx_load2(0, q);
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            hy[s] += Hr[s][2 * q] * yq.x;
+            hy[s] += Hr[s][2 * q + 1] * yq.y;
+          }
+        }
+      } else {
 #pragma unroll
       for (int q = 0; q < MC; ++q) {
         const double yq = gat(yk, q);
 #pragma unroll
         for (int s = 0; s < S; ++s) hy[s] += Hr[s][q] * yq;
       }
-      const double yhy = dot(yk, hy);  // sum_i yk_i hy_i in coordinate order
+      }
+      const double yhy = dot(yk, hy);  // sum_i yk_i hy_i (coord_sum's order)
       const double cs = rho * rho * yhy + rho;
+      if constexpr (kLdsv) {
+        vx_store(hy, 0);
+        vx_store(sk, 1);
+#pragma unroll
+        for (int q = 0; q < MC / 2; ++q) {
+          const double2 hq = vx_load2(0, q), sq = vx_load2(1, q);
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            Hr[s][2 * q] = Hr[s][2 * q] - rho * (sk[s] * hq.x + hy[s] * sq.x) + cs * (sk[s] * sq.x);
+            Hr[s][2 * q + 1] = Hr[s][2 * q + 1] - rho * (sk[s] * hq.y + hy[s] * sq.y) + cs * (sk[s] * sq.y);
+          }
+        }
+      } else {
 #pragma unroll
       for (int q = 0; q < MC; ++q) {
         const double hq = gat(hy, q), sq = gat(sk, q);
 #pragma unroll
         for (int s = 0; s < S; ++s)
           Hr[s][q] = Hr[s][q] - rho * (sk[s] * hq + hy[s] * sq) + cs * (sk[s] * sq);
+      }
       }
     }
     double gm = 0.0;
@@ -2032,7 +2133,16 @@ insite_refine_coop_kernel(RefineArgs) {
   // ---- final Euler scan with every coefficient (insite_refine_kernel's, replicated in the group's lanes) ----
   double xf[MC];
 #pragma unroll
-  for (int i = 0; i < MC; ++i) xf[i] = gat(x, i);
+  for (int i = 0; i < MC; ++i) xf[i] = kLdsv ? 0.0 : gat(x, i);
+  if constexpr (kLdsv) {
+    vx_store(x, 0);
+#pragma unroll
+    for (int q = 0; q < MC / 2; ++q) {
+      const double2 xq = vx_load2(0, q);
+      xf[2 * q] = xq.x;
+      xf[2 * q + 1] = xq.y;
+    }
+  }
   auto coef_at = [&](int q) -> double {
     double c = ra.c0[q];
 #pragma unroll
