@@ -196,6 +196,12 @@ __device__ __forceinline__ void ring_wait() {
 #ifndef INSITE_REFINE_TREE
 #define INSITE_REFINE_TREE 1
 #endif
+// INSITE_REFINE_FUSEDUPD (M = 16): H g and H y as FMA chains, and the inverse-Hessian update in the rank-2 form
+// H + s u^T + w s^T, w = -rho H y, u = cs s + w (2 FMAs an element instead of 5 multiplies and 3 adds); the single-
+// lane and cooperative kernels run the same operations (bitwise equal), the oracle's association differs as before.
+#ifndef INSITE_REFINE_FUSEDUPD
+#define INSITE_REFINE_FUSEDUPD 1
+#endif
 template <int M>
 __device__ __forceinline__ double coord_sum(const double (&v)[M]) {
 #pragma clang fp contract(off)  // NC
@@ -549,7 +555,10 @@ struct BfgsFlat {
     for (int i = 0; i < M; ++i) {
       double s_ = 0.0;
 #pragma unroll RU
-      for (int j = 0; j < M; ++j) s_ += H.at(i, j) * g[j];
+      for (int j = 0; j < M; ++j) {
+        if constexpr (M == 16 && INSITE_REFINE_FUSEDUPD) s_ = fma(H.at(i, j), g[j], s_);
+        else s_ += H.at(i, j) * g[j];
+      }
       pk[i] = -s_;
     }
     phi0 = f;
@@ -725,17 +734,33 @@ struct BfgsFlat {
       for (int i = 0; i < M; ++i) {
         double t = 0.0;
 #pragma unroll RU
-        for (int j = 0; j < M; ++j) t += H.at(i, j) * yk[j];
+        for (int j = 0; j < M; ++j) {
+          if constexpr (M == 16 && INSITE_REFINE_FUSEDUPD) t = fma(H.at(i, j), yk[j], t);
+          else t += H.at(i, j) * yk[j];
+        }
         hy[i] = t;
         yh[i] = yk[i] * t;
       }
       const double yhy = coord_sum(yh);
       const double cs = rho * rho * yhy + rho;
+      if constexpr (M == 16 && INSITE_REFINE_FUSEDUPD) {
+        double w[M], u[M];
+#pragma unroll RU
+        for (int i = 0; i < M; ++i) {
+          w[i] = -rho * hy[i];
+          u[i] = fma(cs, sk[i], w[i]);
+        }
+#pragma unroll RU
+        for (int i = 0; i < M; ++i)
+#pragma unroll RU
+          for (int j = 0; j < M; ++j) H.at(i, j) = fma(sk[i], u[j], fma(w[i], sk[j], H.at(i, j)));
+      } else {
 #pragma unroll RU
       for (int i = 0; i < M; ++i)
 #pragma unroll RU
         for (int j = 0; j < M; ++j)
           H.at(i, j) = H.at(i, j) - rho * (sk[i] * hy[j] + hy[i] * sk[j]) + cs * (sk[i] * sk[j]);
+      }
      }
     } else if (isfinite(rho)) {
       auto w = [&](int i, int q) { return (i == q ? 1.0 : 0.0) - rho * (sk[i] * yk[q]); };
@@ -1576,6 +1601,7 @@ insite_refine_coop_kernel(RefineArgs) {
     return *reinterpret_cast<const double2*>(wVx + buf * kVx + 2 * q);
   };
   constexpr bool kLdsv = INSITE_COOP_LDSV && MC == 2 * kCoopG;
+  static_assert(!(MC == 16 && INSITE_REFINE_FUSEDUPD && !kLdsv), "the fused update (M = 16) is written for LDSV");
   double uu[INSITE_MAX_STATICS];
 #pragma unroll
   for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = t < ra.U ? ra.u[p * ra.U + t] : 0.0;
@@ -1868,8 +1894,13 @@ insite_refine_coop_kernel(RefineArgs) {
         const double2 gq = vx_load2(0, q);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-          acc[s] += Hr[s][2 * q] * gq.x;
-          acc[s] += Hr[s][2 * q + 1] * gq.y;
+          if constexpr (INSITE_REFINE_FUSEDUPD) {
+            acc[s] = fma(Hr[s][2 * q], gq.x, acc[s]);
+            acc[s] = fma(Hr[s][2 * q + 1], gq.y, acc[s]);
+          } else {
+            acc[s] += Hr[s][2 * q] * gq.x;
+            acc[s] += Hr[s][2 * q + 1] * gq.y;
+          }
         }
       }
     } else {
@@ -2067,8 +2098,13 @@ insite_refine_coop_kernel(RefineArgs) {
           const double2 yq = vx_load2(0, q);
 #pragma unroll
           for (int s = 0; s < S; ++s) {
-            hy[s] += Hr[s][2 * q] * yq.x;
-            hy[s] += Hr[s][2 * q + 1] * yq.y;
+            if constexpr (INSITE_REFINE_FUSEDUPD) {
+              hy[s] = fma(Hr[s][2 * q], yq.x, hy[s]);
+              hy[s] = fma(Hr[s][2 * q + 1], yq.y, hy[s]);
+            } else {
+              hy[s] += Hr[s][2 * q] * yq.x;
+              hy[s] += Hr[s][2 * q + 1] * yq.y;
+            }
           }
         }
       } else {
@@ -2081,7 +2117,25 @@ insite_refine_coop_kernel(RefineArgs) {
       }
       const double yhy = dot(yk, hy);  // sum_i yk_i hy_i (coord_sum's order)
       const double cs = rho * rho * yhy + rho;
-      if constexpr (kLdsv) {
+      if constexpr (kLdsv && INSITE_REFINE_FUSEDUPD) {
+        double w[S], u[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          w[s] = -rho * hy[s];
+          u[s] = fma(cs, sk[s], w[s]);
+        }
+        vx_store(u, 0);
+        vx_store(sk, 1);
+#pragma unroll
+        for (int q = 0; q < MC / 2; ++q) {
+          const double2 uq = vx_load2(0, q), sq = vx_load2(1, q);
+#pragma unroll
+          for (int s = 0; s < S; ++s) {
+            Hr[s][2 * q] = fma(sk[s], uq.x, fma(w[s], sq.x, Hr[s][2 * q]));
+            Hr[s][2 * q + 1] = fma(sk[s], uq.y, fma(w[s], sq.y, Hr[s][2 * q + 1]));
+          }
+        }
+      } else if constexpr (kLdsv) {
         vx_store(hy, 0);
         vx_store(sk, 1);
 #pragma unroll

@@ -72,6 +72,13 @@ for pa in range(NPURE):
         cost = 1 if pb == 0 else 2
         if m not in OPS or OPS[m][1] > cost:
             OPS[m] = ((pa, pb), cost)
+if os.environ.get("MS4_COVER_TRIPLES"):  # search-only: operands of three staged factors (3 reads, 2 multiplies)
+    for pa in range(1, NZ + 1):
+        for pb in range(1, pa + 1):
+            for pc in range(1, pb + 1):
+                m = mono(pa, pb, pc)
+                if m not in OPS:
+                    OPS[m] = ((pa, pb, pc), 3)
 OPL = list(OPS)
 NO = len(OPL)
 
@@ -150,7 +157,7 @@ def gcost(groups):
     for g in groups:
         c = max(OPS[OPL[u]][1] for u in g)
         reads += c
-        muls += c == 2
+        muls += c - 1
     return reads, muls
 
 
