@@ -1063,9 +1063,12 @@ def insite_main(args):
     # HIP events on its stream; its work = every objective/gradient evaluation (nfev per row, counted by the kernel
     # on one untimed launch) x the row's K-step window x flops per sensitivity step
     kst = torch.cuda.current_stream(dev)
+    # the kernel's call index in the plan: [sort, rows kernel] in rows mode, [sort, prepare, kernel, finish] when the
+    # row kernel refused the shape (prepare mode)
+    kidx_ins = {"rows": 1, "prepare": 2}[plan.mode]
 
     def kern():
-        plan.call(1, kst)
+        plan.call(kidx_ins, kst)
 
     for _ in range(2):
         kern()

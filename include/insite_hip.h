@@ -171,7 +171,8 @@ int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, co
  * k - 2); a last call with n_patients = 0, n_rows = 0 and finalize_prev = 1 finalises the stream's last
  * cohort.  Each slot's header records the block count and system size its partials were streamed with (ABI 8),
  * and the finalisation sums exactly those: consecutive calls may change gram_blocks, method or fd_kind.  A
- * finalisation of a slot no call has streamed (or streamed for another system) writes NaN G|b and coefficients,
+ * finalisation of a slot no call has streamed (or streamed for another system: the record holds a fingerprint of
+ * the library's columns, statics count and arm count) writes NaN G|b and coefficients,
  * mask 0 and iters -3.  Same shape restrictions as insite_fit_rollout_f64.  Workspace:
  * insite_fit_rollout_deferred_workspace_bytes: two slots (their headers need not be zero) and a 1-KiB claim area
  * after them that must be zero before the first call (a zero-filled buffer); every call leaves it zero. */
@@ -472,7 +473,11 @@ int32_t insite_refine_general_f64(const double* V, int64_t ld_v, int32_t T, cons
  *   / nfev_out [n_rows] -- every per-row array in ROW order.  ld_v, ld_arm, ld_p >= T.
  * Returns INSITE_E_UNSUPPORTED outside the windowed kernel's shape (T not in [2, 64], more than 3 active
  * coefficients, a state exponent >= 2 in the model, odd ld_v / unaligned V): the caller then takes the
- * prepare / insite_refine_general_f64 / finish route, which covers every model. */
+ * prepare / insite_refine_general_f64 / finish route, which covers every model.
+ * Concurrency: the opt-in dynamic row assignment (INSITE_REFINE_DYN=1 in the environment; off by default) takes its
+ * queue heads from 64 device words handed out round-robin per call, so at most 64 such calls may be in flight at
+ * once across independent streams -- a 65th shares a head with a running call (rows skipped or refined twice).  The
+ * default static kernel has no such limit. */
 int32_t insite_refine_rows_f64(const double* V, int64_t ld_v, int32_t T, const int8_t* arm, int64_t ld_arm,
                                const double* u, const int32_t* seq_len, int64_t n_rows, int32_t n_statics,
                                int32_t n_coef, const double* coef0, const int32_t* coef_arm_mask,

@@ -2516,7 +2516,25 @@ step_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
 // right G|b; a slot that was never streamed (or holds another system) is flagged instead of summed.
 constexpr int kSlotRec = 112;  // unsigned index into the slot's 512-B header (counters use [0, 98))
 constexpr unsigned kSlotMagic = 0x1E5D0A7Eu;
-static_assert((kSlotRec + 3) * sizeof(unsigned) <= 512, "slot record inside the workspace header");
+static_assert((kSlotRec + 4) * sizeof(unsigned) <= 512, "slot record inside the workspace header");
+// The slot record's 4th word: a fingerprint of the streamed system (FNV-1a over the library's column codes, F, the
+// statics count and the arm count), so a slot streamed for another system of the same shape (same F and arm
+// count, other exponents or statics) is flagged at finalisation like an unstreamed one.  The derivative kind,
+// method and block count may change between calls (the partials are the same system's G|b).
+__host__ __device__ inline unsigned slot_fingerprint(const LibDesc& lib, int n_arms) {
+  unsigned h = 2166136261u;
+  auto mix = [&](unsigned v) {
+    for (int k = 0; k < 4; ++k) {
+      h ^= (v >> (8 * k)) & 0xffu;
+      h *= 16777619u;
+    }
+  };
+  mix((unsigned)lib.F);
+  mix((unsigned)lib.U);
+  mix((unsigned)n_arms);
+  for (int j = 0; j < lib.F && j < INSITE_MAX_TERMS; ++j) mix((unsigned)lib.ucode[j]);
+  return h;
+}
 
 // A finalisation whose slot record does not match: NaN G|b (and with STF > 0 NaN coefficients, mask 0,
 // iters -3), so a misuse is loud rather than silently wrong.
@@ -2614,7 +2632,7 @@ step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, con
                      double* __restrict__ part_cur, const double* __restrict__ part_prev, GramOut out, RolloutArgs ra,
                      int gblocks, unsigned* __restrict__ rc, unsigned* __restrict__ hdr_cur,
                      const unsigned* __restrict__ hdr_prev, int lagged, const double* __restrict__ G_fit,
-                     const double* __restrict__ b_fit, GramOut fit) {
+                     const double* __restrict__ b_fit, GramOut fit, unsigned fprint) {
   __shared__ double smem[kGramSmem];
   const int n_ent = out.n_arms * lib.nE;
   if ((int)blockIdx.x < gblocks) {
@@ -2622,6 +2640,7 @@ step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, con
       hdr_cur[kSlotRec] = kSlotMagic;
       hdr_cur[kSlotRec + 1] = (unsigned)gblocks;
       hdr_cur[kSlotRec + 2] = (unsigned)n_ent;
+      hdr_cur[kSlotRec + 3] = fprint;
     }
     if (INSITE_DEF_GPRIO) __builtin_amdgcn_s_setprio(INSITE_DEF_GPRIO);
     gram_body<1, 2, SMOOTH, true, true, 0, 7>((int)blockIdx.x, gblocks, smem, x, ldx, n_steps, u, arm, rows, N, 0, 0,
@@ -2632,7 +2651,8 @@ step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, con
     if (part_prev) {
       INSITE_TREAL(49152, 8);
       const unsigned mg = hdr_prev[kSlotRec], nb = hdr_prev[kSlotRec + 1], ne = hdr_prev[kSlotRec + 2];
-      const bool ok = mg == kSlotMagic && ne == (unsigned)n_ent && nb >= 1u && nb <= (unsigned)kGramMaxBlocks;
+      const bool ok = mg == kSlotMagic && ne == (unsigned)n_ent && nb >= 1u && nb <= (unsigned)kGramMaxBlocks &&
+                      hdr_prev[kSlotRec + 3] == fprint;
       if (!ok) {
         if (lagged) finalize_invalid<0>(lib, out);
         else finalize_invalid<7>(lib, out);
@@ -4094,7 +4114,7 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
     unsigned* rc = INSITE_DEF_RSTATIC < 1000 ? reinterpret_cast<unsigned*>(wsb + 2 * ws_one) : nullptr;
     kd<<<dim3(grid), kBlock, 0, hs>>>(x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, part_cur,
                                       part_prev, lagged ? gred : go, ra, gb, rc, hdr_cur, hdr_prev, lagged, G_fit,
-                                      b_fit, gf);
+                                      b_fit, gf, slot_fingerprint(lib, n_arms));
     return launch_status();
   }
   // (a two-patients-per-lane rollout role with 16-B stores measured slower: 46 vs 37 us rollout-only)

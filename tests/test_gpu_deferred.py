@@ -122,6 +122,32 @@ def test_deferred_unstreamed_slot_is_flagged(dev):
     assert torch.all(iters == -3) and torch.isnan(coef).all() and torch.isnan(G).all() and not mask.any()
 
 
+def test_deferred_slot_streamed_for_another_system_is_flagged(dev):
+    """A slot streamed with one 7-term library and finalised by a call with another of the same shape (the same
+    columns in another order: same F, arm count and statics) is flagged through the slot record's fingerprint, not
+    summed as this library's G|b; the same library finalises normally."""
+    from insite_amd import cohort, ops
+    from insite_amd.library import PolyLibrary
+    coh = cohort.synthetic_pkpd(3000, 40, seed=3, device=dev, equation="EQ_4_C", layout="time")
+    bits = cohort.counterfactual_arms(coh.arm, 40, seed=3, layout="time_bits")
+    F = coh.lib.n_terms
+    other = PolyLibrary(np.ascontiguousarray(coh.lib.exps[::-1]), coh.lib.input_names, coh.lib.n_inputs)
+    cin = torch.zeros((2, F), dtype=torch.float64, device=dev)
+    for lib2, flagged in ((other, True), (coh.lib, False)):
+        ws = ops.Workspace()
+        out = [_outs(dev, F) for _ in range(2)]
+        ops.fit_rollout_deferred(coh.x, coh.u, coh.arm, coh.rows, coh.dt, coh.lib, 0.1, 0.5, coh.y0, coh.u, bits, cin,
+                                 coh.dt, 0, False, ws, T=40, out=out[0])
+        ops.fit_rollout_deferred(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib2, 0.1, 0.5, coh.y0, coh.u, bits, cin,
+                                 coh.dt, 1, True, ws, T=40, out=out[1])
+        torch.cuda.synchronize()
+        coef, mask, iters, G, b = out[1]
+        if flagged:
+            assert torch.all(iters == -3) and torch.isnan(coef).all() and torch.isnan(G).all() and not mask.any()
+        else:
+            assert torch.all(iters >= 0) and torch.isfinite(G).all()
+
+
 def test_lagged_roles_equal_deferred(dev, bench_cohort):
     """Reduction role == the deferred finalisation's G|b (bitwise: same partials, same association); solve role
     == the deferred STLSQ on that G|b (bitwise); rollout == the deferred rollout (bitwise)."""

@@ -475,13 +475,15 @@ def test_plugin_insite_rejects_non_finite_refined_predictions(dev, model, monkey
         m.get_predictions(coll["test_cf_one_step"])
 
 
-@pytest.mark.parametrize("N,T,m,rpb", [(20_000, 60, 3, None), (5_000, 60, 2, "256"), (777, 34, 3, "512"),
-                                       (130, 8, 3, None)])
-def test_refine_rows_dynamic_assignment_equals_static(dev, monkeypatch, N, T, m, rpb):
-    """insite_refine_rows_f64's dynamic lane -> row assignment (lanes take the next row of their block's range from an
-    LDS counter when theirs is done; the final scan in its own kernel from the written coefficients) against the
-    static one-row-per-lane kernel (INSITE_REFINE_DYN=0): every output bitwise equal, incl. rows <= tau (finished at
-    claim), ragged block ranges (rows per block 256 / 512 / the default) and a partial last block."""
+@pytest.mark.parametrize("N,T,m,refill,blocks", [(20_000, 60, 3, None, None), (5_000, 60, 2, "1", None),
+                                                 (777, 34, 3, "64", "2"), (130, 8, 3, "8", "1"),
+                                                 (3_000, 60, 3, "8", "2")])
+def test_refine_rows_dynamic_assignment_equals_static(dev, monkeypatch, N, T, m, refill, blocks):
+    """insite_refine_rows_f64's dynamic lane -> row assignment (a wave's idle lanes take the next rows from a
+    device-wide queue head with one atomic once at least `refill` of them are idle, INSITE_REFINE_DYN_REFILL; the
+    final scan in its own kernel from the written coefficients) against the static one-row-per-lane kernel
+    (INSITE_REFINE_DYN=0): every output bitwise equal, incl. rows <= tau (finished at claim), thresholds 1 / 8 / 64
+    and a persistent grid of 1 or 2 blocks (INSITE_REFINE_DYN_BLOCKS: every lane cycles through many rows)."""
     from insite_amd import cohort, ops
     coh = cohort.synthetic_pkpd(N, T, seed=N + 3 * T, device=dev, equation="EQ_4_C")
     V = coh.x[:, :T].contiguous()
@@ -495,8 +497,10 @@ def test_refine_rows_dynamic_assignment_equals_static(dev, monkeypatch, N, T, m,
     c0[0, 4], c0[1, 1] = -1.1107592869834308, -0.14540553723951796
     if m == 3:
         c0[1, 5] = -1.0234639833519243
-    if rpb is not None:
-        monkeypatch.setenv("INSITE_REFINE_DYN_RPB", rpb)
+    if refill is not None:
+        monkeypatch.setenv("INSITE_REFINE_DYN_REFILL", refill)
+    if blocks is not None:
+        monkeypatch.setenv("INSITE_REFINE_DYN_BLOCKS", blocks)
     outs = {}
     for dyn in ("1", "0"):
         monkeypatch.setenv("INSITE_REFINE_DYN", dyn)
