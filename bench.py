@@ -618,7 +618,14 @@ def c5_main(args):
         "roofline": {"kernel": "rollout_rk45_kernel", "bound": "valu-f64", "unit": "TFLOP/s",
                      "achieved": flop / (launch_ms * 1e-3) / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
                      "frac": flop / (launch_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
-                     "traffic": traffic_for("c5", "rollout_rk45_flat_kernel", args=args),
+                     "traffic": c5_traffic_calibrated(args),
+                     "traffic_method": "PMC FETCH_SIZE / WRITE_SIZE of the kernel (profiles/traffic_r04.json) "
+                                       "divided by this access shape's calibration factors (profiles/r05/c5cal/"
+                                       "calibration.json: window-refill reads 0.617, 64-B sector writes 1.081), not "
+                                       "the wide-streaming x2",
+                     "traffic_blanket_x2": traffic_for("c5", "rollout_rk45_flat_kernel", args=args),
+                     "data_bytes": float(N * (8 * 3 + 4) + n_obs.to(torch.float64).sum().item() * 8 * 2
+                                         + N * ((Tm + 30) // 32) * 4),
                      "avg_launch_ms": launch_ms, "flop_per_attempt": RK45_FLOP_PER_ATTEMPT,
                      "issued_incl_divergence_TFLOPs": issued / (launch_ms * 1e-3) / 1e12,
                      "algorithmic_bytes": N * (8 * 3 + 4) + N * Tm * 8 * 2 + N * ((Tm + 30) // 32) * 4,
@@ -1145,6 +1152,24 @@ def insite_main(args):
                      "avg_ms_source": "HIP events on the launch stream around args.steps back-to-back launches of "
                                       "insite_refine_rows_f64 with the step's lane order (the sort excluded)"},
     }
+    # the same kernel in EXECUTED terms: instruction counters, and the bytes the kernel streams as executed -- every
+    # objective scan of a wave refills its LDS ring for all 64 rows up to the wave's longest window, in 8-step slots,
+    # as long as any lane has a trial pending (wave max nfev x slots(wave max K + 1) x 64 rows x 8 B), plus the final
+    # scan's V + arms read and the predictions written -- against the measured traffic
+    ex = pmc_executed("profiles/r05/refine_pmc_base/summary.json", "insite_refine_kernel<3, 2, 1, true, true>",
+                      args=args, config="insite")
+    if ex is not None:
+        ring_b = float((nfw.max(1) * ((kw.max(1) + 1 + 7) // 8 * 8)).sum()) * 64 * 8
+        ex["executed_ring_read_bytes"] = ring_b
+        ex["row_window_read_bytes"] = float((nf.to(torch.int64) * (K + 1)).sum().item()) * 8
+        ex["final_scan_bytes"] = float(N * T * (8 + 1 + 8))
+        if "fetch_bytes_raw" in ex:
+            # two calibrations bracket this shape (the ring's DMA moves 64-B runs of 16 rows per instruction):
+            # wide streaming (FETCH_SIZE = 1/2 of the bytes) and C5's 64-B per-row runs (0.617, profiles/r05/c5cal)
+            exe = ring_b + N * T * (8 + 1)
+            ex["fetch_over_executed_reads_x2"] = ex["fetch_bytes_x2"] / exe
+            ex["fetch_over_executed_reads_runcal"] = ex["fetch_bytes_raw"] / 0.617 / exe
+        out["roofline"]["executed"] = ex
     if not args.no_parity:
         o_ = plan.order.long()
         out["parity"] = insite_parity(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, preds, coef, status, iters,
@@ -1345,6 +1370,10 @@ def insite4_main(args):
                                     "the objective scans run it in closed form, INSITE_REFINE_CF)",
                      "algorithmic_bytes": kb, "achieved_GBps": kb / (d["kernel_ms"] * 1e-3) / 1e9},
     }
+    ex = pmc_executed("profiles/r05/coop_pmc2/summary.json", "insite_refine_coop_kernel<16, 4, true>")
+    if ex is not None and N == 1_000_000:
+        ex["note"] = "counters averaged over the dense and joint models' launches (16 dispatches)"
+        out["roofline"]["executed"] = ex
     if "parity" in d:
         out["parity"] = dict(d["parity"], model="dense (the line's value); every model's in models.*.parity")
     if cpu is not None:
@@ -1711,6 +1740,60 @@ def traffic_for(config, kernel, grid=None, args=None):
         return None
     best = max(hits, key=lambda v: v.get("dispatches") or 0)
     return best.get("hbm_bytes")
+
+
+def pmc_executed(path, kernel, args=None, config=None):
+    """Executed-instruction view of one kernel from a committed rocprofv3 --pmc summary (tools/pmc_summary.py of
+    tools/g_r05_refine_pmc.sh passes, taken on the line's default workload): VALU instructions per launch and
+    their share of the SIMD cycles (SQ_INSTS_VALU x 4 cycles over 1024 SIMDs x the kernel's cycles, SQ_BUSY_CYCLES /
+    32 shader engines), SALU / LDS / vector-memory instruction counts, FETCH_SIZE (x2: wide-streaming calibration)
+    and WRITE_SIZE bytes.  None when the summary is absent or the line runs a non-default workload."""
+    if args is not None and config is not None and traffic_for(config, kernel, args=args) is None:
+        return None
+    try:
+        with open(os.path.join(ROOT, path)) as f:
+            d = json.load(f)
+    except Exception:
+        return None
+    v = {}
+    for run in d.values():
+        for k, x in run.items():
+            if k.startswith(kernel):
+                v[k.split()[-1]] = x["mean"]
+    if "SQ_INSTS_VALU" not in v or "SQ_BUSY_CYCLES" not in v:
+        return None
+    cyc = v["SQ_BUSY_CYCLES"] / 32.0
+    out = {"pmc_source": path, "kernel_cycles": cyc, "valu_instructions": v["SQ_INSTS_VALU"],
+           "valu_busy_frac": v["SQ_INSTS_VALU"] * 4.0 / (1024.0 * cyc),
+           "salu_instructions": v.get("SQ_INSTS_SALU"), "lds_instructions": v.get("SQ_INSTS_LDS"),
+           "vmem_read_instructions": v.get("SQ_INSTS_VMEM_RD"), "waves": v.get("SQ_WAVES")}
+    if "FETCH_SIZE" in v:
+        out["fetch_bytes_raw"] = v["FETCH_SIZE"] * 1024
+        out["fetch_bytes_x2"] = v["FETCH_SIZE"] * 1024 * 2
+    if "WRITE_SIZE" in v:
+        out["write_bytes"] = v["WRITE_SIZE"] * 1024
+    return out
+
+
+def c5_traffic_calibrated(args):
+    """The RK45 kernel's HBM bytes per launch with its own access shape's calibration (window refills: FETCH_SIZE
+    reports 0.617 of the bytes; 64-B sector writes: WRITE_SIZE 1.081; tools/probe/window_probe.hip), from the
+    committed counters of the default C5 workload, or None."""
+    if traffic_for("c5", "rollout_rk45_flat_kernel", args=args) is None:
+        return None
+    try:
+        with open(TRAFFIC_R04) as f:
+            tab = json.load(f)["c5"]
+        with open(os.path.join(ROOT, "profiles", "r05", "c5cal", "calibration.json")) as f:
+            cal = json.load(f)
+    except Exception:
+        return None
+    hits = [v for v in tab.values() if v.get("kernel", "").startswith("rollout_rk45_flat_kernel")]
+    if not hits:
+        return None
+    v = max(hits, key=lambda v: v.get("dispatches") or 0)
+    return (v["FETCH_SIZE_KiB_median"] * 1024 / cal["fetch_factor"]
+            + v["WRITE_SIZE_KiB_median"] * 1024 / cal["write_factor"])
 
 
 def step_traffic(args):
