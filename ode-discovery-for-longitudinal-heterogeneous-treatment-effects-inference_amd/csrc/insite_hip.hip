@@ -2957,6 +2957,12 @@ rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
 #ifndef INSITE_RK45_STAGE
 #define INSITE_RK45_STAGE 1
 #endif
+#ifndef INSITE_RK45_BUFREFILL
+#define INSITE_RK45_BUFREFILL 1
+#endif
+#ifndef INSITE_RK45_FULLSEC
+#define INSITE_RK45_FULLSEC 1  // whole-sector flushes as 16-B stores (0: every flush element by element)
+#endif
 #ifndef INSITE_RK45_MINSTEP_BRANCH
 #define INSITE_RK45_MINSTEP_BRANCH 0
 #endif
@@ -3030,8 +3036,21 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
   const int64_t ystep = PM ? 1 : ra.ldy;
   const int64_t tstep = PM ? 1 : ra.ldt;
   const double* trow = ra.t + (PM ? pc * ra.ldt : pc);
+  // INSITE_RK45_BUFREFILL (PM): the window through a buffer descriptor over t -- one 32-bit offset per lane and
+  // immediate offsets for the 8 elements, unclamped (elements past the row's last observation are never used; past
+  // the array the hardware returns 0) -- instead of 8 clamped 64-bit addresses (~30 VALU per refill event)
+  const bool tbuf = PM && INSITE_RK45_BUFREFILL && (int64_t)ra.N * ra.ldt * 8 <= (int64_t)INT32_MAX;
+  const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)ra.t, (short)0, (int)(tbuf ? (int64_t)ra.N * ra.ldt * 8 : 0), 0x00020000);
   auto refill = [&](int from) {  // elements clamped to n - 1 (n >= 2 for a live lane)
     base = from;
+    if (tbuf) {
+      const unsigned off = (unsigned)((pc * ra.ldt + from) * 8);
+#pragma unroll
+      for (int j = 0; j < kRkWin; ++j)
+        tw[j * kWave] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(trs, off + 8u * j, 0, 0));
+      return;
+    }
 #pragma unroll
     for (int j0 = 0; j0 < kRkWin; j0 += 8) {
       double v[8];
@@ -3182,10 +3201,28 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
               double v[8];
 #pragma unroll
               for (int j = 0; j < 8; ++j) v[j] = yr[j * kWave];
+#if INSITE_RK45_FULLSEC
+              // a whole sector (every flush but a row's first / last partial one): four 16-B stores at immediate
+              // offsets -- the per-element form below costs ~35 VALU of offset selects, and with 64 lanes some lane
+              // flushes in ~94 % of the iterations, so the wave paid them nearly every attempt
+              if (slot_lo == 0 && slot == 7) {
+                typedef double d2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+                for (int j = 0; j < 8; j += 2)
+                  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d2{v[j], v[j + 1]}), yrs,
+                                                         sb + 8u * j, 0, 0);
+              } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v[j]), yrs,
+                                                        (j >= slot_lo && j <= slot) ? sb + 8u * j : kOOB, 0, 0);
+              }
+#else
 #pragma unroll
               for (int j = 0; j < 8; ++j)
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v[j]), yrs,
                                                       (j >= slot_lo && j <= slot) ? sb + 8u * j : kOOB, 0, 0);
+#endif
             } else if (slot_lo == 0 && slot == 7) {
               double v[8];
 #pragma unroll
