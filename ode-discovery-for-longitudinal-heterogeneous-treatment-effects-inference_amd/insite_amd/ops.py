@@ -847,20 +847,9 @@ def rk45_order(n_obs: torch.Tensor, T_max: int, out: torch.Tensor | None = None)
     return _run(("insite_rk45_order_i32", args, n_obs.device, out))
 
 
-def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_obs: torch.Tensor,
-                 n_obs: torch.Tensor, coef: torch.Tensor, lib: PolyLibrary, rtol: float = 1.4e-8, atol: float = 1.4e-8,
-                 drop_below: float = 1e-3, out: torch.Tensor | None = None, steps: torch.Tensor | None = None,
-                 order: torch.Tensor | bool | None = True, layout: str = "time"):
-    """Adaptive RK45 rollout on per-patient irregular observation grids (insite_rollout_rk45_f64;
-    configuration C5).  y0 [N] f64, u [N,U] f64, n_obs [N] int32, coef [A,F] or [N,A,F].
-    layout "time":    t_obs [T_max, >=N] f64, arm_bits [T_max, >=ceil(N/32)] int32 (pack_arm_bits of the
-                      time-major arms), y [T_max, N] (row k = state at t_obs[k + 1]);
-    layout "patient": t_obs [N, >=T_max] f64, arm_bits [N, >=ceil((T_max-1)/32)] int32 (pack_arm_bits of
-                      the patient-major arms [N, T]), y [N, T_max] -- the fast layout (DESIGN.md §5).
-    ``order``: True bins the rows by n_obs on the device first (``rk45_order``, part of the call), a [N]
-    int32 permutation is used as given, None/False runs lane r on row r.  Outputs do not depend on it.
-    Returns (y, step attempts [N] int32); y elements past a patient's grid are left as they were (NaN
-    when ``out`` is None)."""
+def _rk45_prep(y0, u, arm_bits, t_obs, n_obs, coef, lib, rtol, atol, drop_below, out, steps, order, layout,
+               plan):
+    """rollout_rk45's validation and argument packing; plan=True returns the packed calls (plan_rollout_rk45)."""
     if layout not in ("time", "patient"):
         raise ValueError("layout must be 'time' or 'patient'")
     pm = layout == "patient"
@@ -902,8 +891,15 @@ def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_ob
             raise ValueError(f"out must be {'[N, >=T_max]' if pm else '[T_max, >=N]'}")
     if steps is None:
         steps = torch.empty((N,), dtype=torch.int32, device=y0.device)
+    order_call = None
     if order is True:
-        order = rk45_order(n_obs, Tm)
+        if plan:   # the plan bins into its own buffer with its own workspace, per call
+            order = torch.empty((N,), dtype=torch.int32, device=n_obs.device)
+            wsb = _lib.load().insite_rk45_order_workspace_bytes(int(Tm))
+            ows = torch.zeros((max(1, (wsb + 7) // 8),), dtype=torch.float64, device=n_obs.device)
+            order_call = ("insite_rk45_order_i32", (_p(n_obs), N, int(Tm), _p(order), _p(ows), wsb), (order, ows))
+        else:
+            order = rk45_order(n_obs, Tm)
     elif order is False:
         order = None
     elif order is not None:
@@ -915,7 +911,58 @@ def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_ob
             t_obs.stride(0), _p(n_obs), _p(coef), stride, tab.ctypes.data_as(ctypes.c_void_p), F, N, Tm,
             lib.n_statics, A, float(rtol), float(atol), float(drop_below), _p(out), out.stride(0), _p(steps),
             _p(order), _lib.LAYOUT_PATIENT_MAJOR_BITS if pm else _lib.LAYOUT_TIME_MAJOR_BITS)
+    if plan:
+        keep = (y0, u, arm_bits, t_obs, n_obs, coef, tab, out, steps, order)
+        return order_call, ("insite_rollout_rk45_f64", args, keep), (out, steps)
     return _run(("insite_rollout_rk45_f64", args, y0.device, (out, steps)))
+
+
+def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_obs: torch.Tensor,
+                 n_obs: torch.Tensor, coef: torch.Tensor, lib: PolyLibrary, rtol: float = 1.4e-8, atol: float = 1.4e-8,
+                 drop_below: float = 1e-3, out: torch.Tensor | None = None, steps: torch.Tensor | None = None,
+                 order: torch.Tensor | bool | None = True, layout: str = "time"):
+    """Adaptive RK45 rollout on per-patient irregular observation grids (insite_rollout_rk45_f64;
+    configuration C5).  y0 [N] f64, u [N,U] f64, n_obs [N] int32, coef [A,F] or [N,A,F].
+    layout "time":    t_obs [T_max, >=N] f64, arm_bits [T_max, >=ceil(N/32)] int32 (pack_arm_bits of the
+                      time-major arms), y [T_max, N] (row k = state at t_obs[k + 1]);
+    layout "patient": t_obs [N, >=T_max] f64, arm_bits [N, >=ceil((T_max-1)/32)] int32 (pack_arm_bits of
+                      the patient-major arms [N, T]), y [N, T_max] -- the fast layout (DESIGN.md §5).
+    ``order``: True bins the rows by n_obs on the device first (``rk45_order``, part of the call), a [N]
+    int32 permutation is used as given, None/False runs lane r on row r.  Outputs do not depend on it.
+    Returns (y, step attempts [N] int32); y elements past a patient's grid are left as they were (NaN
+    when ``out`` is None)."""
+    return _rk45_prep(y0, u, arm_bits, t_obs, n_obs, coef, lib, rtol, atol, drop_below, out, steps, order, layout,
+                      False)
+
+
+class Rk45Plan:
+    """``rollout_rk45`` prepared once (inputs validated, buffers and arguments packed): a call enqueues the n_obs
+    counting sort into the plan's own order buffer (when binning) and the RK45 rollout -- two C calls, no host
+    work beyond them.  ``out`` = (y, step attempts), bitwise those of ``rollout_rk45``.  The plan keeps references
+    to its inputs: refresh them in place between calls or make a new plan."""
+
+    def __init__(self, calls, device, out):
+        L = _lib.load()
+        self._calls = [(getattr(L, name), args) for name, args, _ in calls]
+        self._keep = tuple(k for _, _, k in calls)
+        self.device = torch.device(device)
+        self.out = out
+
+    def __call__(self, stream: torch.cuda.Stream | None = None):
+        h = ctypes.c_void_p((stream if stream is not None else torch.cuda.current_stream(self.device)).cuda_stream)
+        for fn, args in self._calls:
+            st = fn(*args, h)
+            if st:
+                _lib.check(getattr(fn, "__name__", "rk45 plan"), st)
+        return self.out
+
+
+def plan_rollout_rk45(y0, u, arm_bits, t_obs, n_obs, coef, lib, rtol=1.4e-8, atol=1.4e-8, drop_below=1e-3, out=None,
+                      steps=None, order=True, layout="time") -> Rk45Plan:
+    """``rollout_rk45`` as a plan (the C5 bench's per-step call): the same validation, done once."""
+    order_call, call, outs = _rk45_prep(y0, u, arm_bits, t_obs, n_obs, coef, lib, rtol, atol, drop_below, out, steps,
+                                        order, layout, True)
+    return Rk45Plan(([order_call] if order_call else []) + [call], y0.device, outs)
 
 
 def refine_terms(lib: PolyLibrary, n_coef_rows: int):

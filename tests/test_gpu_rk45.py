@@ -169,3 +169,30 @@ def test_rk45_zero_length_intervals_and_short_grids(dev, layout):
     rel = np.abs(y[valid] - ref[valid]) / np.abs(ref[valid])
     assert rel.max() < 1e-9, rel.max()
     assert np.mean(steps == ref_steps) >= 0.99
+
+
+@pytest.mark.parametrize("layout", ["time", "patient"])
+def test_rk45_plan_equals_eager(dev, layout):
+    """plan_rollout_rk45 (the C5 bench's per-step call: the counting sort into the plan's own order buffer, then the
+    rollout; two C calls) gives bit-identical outputs to rollout_rk45, called twice (the plan reused)."""
+    from insite_amd import ops
+    from insite_amd.library import polynomial_library
+    ex, t, n, u, arm, y0, coef = _setup(2000, 31)
+    lib = polynomial_library(2, 2, True)
+    N, Tm = t.shape
+    tn = np.nan_to_num(t, nan=0.0)
+    if layout == "patient":
+        tt = torch.tensor(np.ascontiguousarray(tn), device=dev)
+        bits = ops.pack_arm_bits(torch.tensor(np.ascontiguousarray(arm[:, :Tm]), device=dev), Tm)
+    else:
+        tt = torch.tensor(np.ascontiguousarray(tn.T), device=dev)
+        bits = ops.pack_arm_bits(torch.tensor(np.ascontiguousarray(arm[:, :Tm].T), device=dev), N)
+    args = (torch.tensor(y0, device=dev), torch.tensor(u, device=dev), bits, tt, torch.tensor(n, device=dev),
+            torch.tensor(np.ascontiguousarray(coef), device=dev), lib)
+    y_e, s_e = ops.rollout_rk45(*args, layout=layout)
+    plan = ops.plan_rollout_rk45(*args, layout=layout)
+    for _ in range(2):
+        y_p, s_p = plan()
+        torch.cuda.synchronize()
+        assert torch.equal(torch.isnan(y_p), torch.isnan(y_e))
+        assert torch.equal(torch.nan_to_num(y_p), torch.nan_to_num(y_e)) and torch.equal(s_p, s_e)
