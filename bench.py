@@ -623,7 +623,7 @@ def c5_main(args):
                      "achieved": flop / (launch_ms * 1e-3) / 1e12, "peak": FP64_VALU_PEAK_TFLOPS,
                      "frac": flop / (launch_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS,
                      "traffic": c5_traffic_calibrated(args),
-                     "traffic_method": "PMC FETCH_SIZE / WRITE_SIZE of the kernel (profiles/traffic_r04.json) "
+                     "traffic_method": "PMC FETCH_SIZE / WRITE_SIZE of the kernel (profiles/traffic_r05.json, else r04) "
                                        "divided by this access shape's calibration factors (profiles/r05/c5cal/"
                                        "calibration.json: window-refill reads 0.617, 64-B sector writes 1.081), not "
                                        "the wide-streaming x2",
@@ -1714,11 +1714,12 @@ def dist_setup(force_group: bool = False):
 
 
 TRAFFIC_R04 = os.path.join(ROOT, "profiles", "traffic_r04.json")
+TRAFFIC_R05 = os.path.join(ROOT, "profiles", "traffic_r05.json")
 
 
 def traffic_for(config, kernel, grid=None, args=None):
     """HBM bytes per launch of `kernel` (symbol prefix) in the bench line `config`, from the committed PMC passes
-    (profiles/traffic_r04.json, tools/g_traffic.sh + tools/traffic_summary.py: FETCH_SIZE x 2 calibration +
+    (profiles/traffic_r05.json, else traffic_r04.json; tools/g_traffic.sh + tools/traffic_summary.py: FETCH_SIZE x 2 +
     WRITE_SIZE, median per dispatch), or None when that table has no such entry.  `grid`: the launch's total
     threads when a config launches the kernel at several sizes.  `args`: the table was taken on each config's
     DEFAULT workload at N = 1 (tools/g_traffic.sh), so a line with other sizes gets None."""
@@ -1733,13 +1734,18 @@ def traffic_for(config, kernel, grid=None, args=None):
                  int(os.environ.get("WORLD_SIZE", "1")))
         if knobs != (1_000_000 if big else 100_000, t_def, "rk4", "bits", "time", 0, 1, 1):
             return None
-    try:
-        with open(TRAFFIC_R04) as f:
-            tab = json.load(f).get(config, {})
-    except Exception:
-        return None
-    hits = [v for v in tab.values() if v.get("kernel", "").startswith(kernel)
-            and (grid is None or str(v.get("grid_size")) == str(grid))]
+    # this round's table first (taken on the kernels as they are now), the previous round's for configs it lacks
+    hits = []
+    for path in (TRAFFIC_R05, TRAFFIC_R04):
+        try:
+            with open(path) as f:
+                tab = json.load(f).get(config, {})
+        except Exception:
+            continue
+        hits = [v for v in tab.values() if v.get("kernel", "").startswith(kernel)
+                and (grid is None or str(v.get("grid_size")) == str(grid))]
+        if hits:
+            break
     if not hits:
         return None
     best = max(hits, key=lambda v: v.get("dispatches") or 0)
@@ -1786,13 +1792,20 @@ def c5_traffic_calibrated(args):
     if traffic_for("c5", "rollout_rk45_flat_kernel", args=args) is None:
         return None
     try:
-        with open(TRAFFIC_R04) as f:
-            tab = json.load(f)["c5"]
         with open(os.path.join(ROOT, "profiles", "r05", "c5cal", "calibration.json")) as f:
             cal = json.load(f)
     except Exception:
         return None
-    hits = [v for v in tab.values() if v.get("kernel", "").startswith("rollout_rk45_flat_kernel")]
+    hits = []
+    for path in (TRAFFIC_R05, TRAFFIC_R04):
+        try:
+            with open(path) as f:
+                tab = json.load(f).get("c5", {})
+        except Exception:
+            continue
+        hits = [v for v in tab.values() if v.get("kernel", "").startswith("rollout_rk45_flat_kernel")]
+        if hits:
+            break
     if not hits:
         return None
     v = max(hits, key=lambda v: v.get("dispatches") or 0)
