@@ -1497,7 +1497,9 @@ inline int ms4_chunks(int64_t N, int n_steps, int grid) {
 inline int ms_grid(int64_t N) {
   int64_t tiles = (N + kWave - 1) / kWave;
   int64_t g = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-  if (g > kMsMaxBlocks) g = kMsMaxBlocks;
+  // one resident round: 256 CUs x INSITE_MS_WPE blocks of 4 waves (one wave per SIMD per block)
+  constexpr int kResident = 256 * INSITE_MS_WPE < kMsMaxBlocks ? 256 * INSITE_MS_WPE : kMsMaxBlocks;
+  if (g > kResident) g = kResident;
   if (g < 1) g = 1;
   return (int)g;
 }
