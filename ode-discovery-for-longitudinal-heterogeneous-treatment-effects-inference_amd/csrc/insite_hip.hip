@@ -2970,7 +2970,7 @@ rollout_rk45_kernel(Rk45Args ra, LibDesc lib) {
 #define INSITE_RK45_HSEL 1
 #endif
 #ifndef INSITE_RK45_CLOSE_BRANCH
-#define INSITE_RK45_CLOSE_BRANCH 0  // 1: round 2's close block under `if (close)` (A/B)
+#define INSITE_RK45_CLOSE_BRANCH 1  // the close block under `if (close)` (0: branch-free selects, A/B)
 #endif
 constexpr int kRkWin = INSITE_RK45_WIN;
 constexpr int kRkStage = INSITE_RK45_STAGE ? 8 : 1;
