@@ -2983,7 +2983,8 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
   __shared__ double y_ring[kWavesPerBlock * kRkStage * kWave];  // PM staging ring [slot][lane]
   const int64_t lane_id = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool act = lane_id < ra.N;
-  int64_t p = act ? (ra.order ? (int64_t)ra.order[lane_id] : lane_id) : ra.N - 1;  // this lane's row
+  // this lane's row (an order entry out of range -- never from insite_rk45_order_i32 -- is clamped, not followed)
+  int64_t p = act ? (ra.order ? (int64_t)min((unsigned)ra.order[lane_id], (unsigned)(ra.N - 1)) : lane_id) : ra.N - 1;
   p = p < 0 ? 0 : p >= ra.N ? ra.N - 1 : p;  // memory-safe on a malformed order (documented: a permutation)
   const int64_t pc = p;
   double* tw = t_win + (threadIdx.x / kWave) * (kRkWin * kWave) + (threadIdx.x & (kWave - 1));
@@ -3300,48 +3301,82 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
 // attempt count grows with its number of observation intervals, so lanes are given rows grouped by n_obs
 // (descending: the longest waves are dispatched first and short ones fill the tail).  Counting sort in two
 // passes over n_obs; the order inside a bin is whatever the atomics give -- every row's trajectory is
-// independent of the lane it runs on, so outputs do not depend on it.
+// independent of the lane it runs on, so outputs do not depend on it.  A block's rows of one bin land together
+// (one cursor atomic per bin and block): with 4096-row chunks a wave's rows mostly come from one 4096-row range,
+// which the rollout's row-major reads like -- 1024- and 2048-row chunks measured 0.785 / 0.748 ms against 0.733
+// (kernel), 8192 the same, 16384 slower (profiles/r05/c5_order/).  Measured and dropped (round 5): the histogram's
+// scan in the count pass's last block (a ticket after device-scope fences: the count pass 9 -> 21 us) and both
+// passes as one launch with a grid barrier on per-block epoch flags (63 us against ~26 for memset + two passes).
 constexpr int kRkBinMax = 1024;   // bins: key = min(n_obs, min(T_max, kRkBinMax - 1))
-constexpr int kRkBinChunk = 4096; // rows per block
+#ifndef INSITE_RK45_BIN_CHUNK
+#define INSITE_RK45_BIN_CHUNK 4096  // rows per block of the two passes
+#endif
+constexpr int kRkBinChunk = INSITE_RK45_BIN_CHUNK;
+static_assert(kRkBinChunk % kBlock == 0, "rows per binning block: a multiple of the block");
 __device__ __forceinline__ int rk45_bin(int32_t n, int nb) { return nb - 1 - (n < 0 ? 0 : n > nb - 1 ? nb - 1 : n); }
 
 __global__ void __launch_bounds__(kBlock) rk45_bin_count_kernel(const int32_t* __restrict__ nobs, int64_t N, int nb,
                                                                  unsigned* __restrict__ hist) {
   __shared__ unsigned h[kRkBinMax];
+  constexpr int kPer = kRkBinChunk / kBlock;
   for (int b = threadIdx.x; b < nb; b += kBlock) h[b] = 0u;
   __syncthreads();
   const int64_t lo = (int64_t)blockIdx.x * kRkBinChunk;
-  for (int j = threadIdx.x; j < kRkBinChunk; j += kBlock)
-    if (lo + j < N) atomicAdd(&h[rk45_bin(nobs[lo + j], nb)], 1u);
+  int bin[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int64_t i = lo + q * kBlock + threadIdx.x;
+    bin[q] = i < N ? rk45_bin(nobs[i], nb) : -1;
+  }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q)
+    if (bin[q] >= 0) atomicAdd(&h[bin[q]], 1u);
   __syncthreads();
   for (int b = threadIdx.x; b < nb; b += kBlock)
     if (h[b]) atomicAdd(&hist[b], h[b]);
 }
 
+// every block scans the (small) global histogram itself: the bins' totals loaded by all threads at once, then one
+// wave's shuffle scan (lane l owns bins [l per, (l + 1) per)) -- round 4 had thread 0 walk it serially
 __global__ void __launch_bounds__(kBlock) rk45_bin_scatter_kernel(const int32_t* __restrict__ nobs, int64_t N, int nb,
                                                                    const unsigned* __restrict__ hist,
                                                                    unsigned* __restrict__ cursor,
                                                                    int32_t* __restrict__ order) {
-  __shared__ unsigned base[kRkBinMax], cnt[kRkBinMax];
+  __shared__ unsigned base[kRkBinMax], cnt[kRkBinMax], tot[kRkBinMax];
   constexpr int kPer = kRkBinChunk / kBlock;
-  for (int b = threadIdx.x; b < nb; b += kBlock) cnt[b] = 0u;
-  if (threadIdx.x == 0) {  // exclusive scan of the global histogram (nb <= 1024 serial adds, once per block)
-    unsigned acc = 0u;
-    for (int b = 0; b < nb; ++b) {
-      base[b] = acc;
-      acc += hist[b];
-    }
-  }
-  __syncthreads();
   const int64_t lo = (int64_t)blockIdx.x * kRkBinChunk;
   int bin[kPer];
-  unsigned rank[kPer];
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
     const int64_t i = lo + q * kBlock + threadIdx.x;
     bin[q] = i < N ? rk45_bin(nobs[i], nb) : -1;
-    rank[q] = bin[q] >= 0 ? atomicAdd(&cnt[bin[q]], 1u) : 0u;
   }
+  for (int b = threadIdx.x; b < nb; b += kBlock) {
+    cnt[b] = 0u;
+    tot[b] = hist[b];
+  }
+  __syncthreads();
+  if (threadIdx.x < kWave) {
+    const int lane = threadIdx.x, per = (nb + kWave - 1) / kWave, b0 = lane * per;
+    unsigned sum = 0u;
+    for (int j = 0; j < per; ++j)
+      if (b0 + j < nb) sum += tot[b0 + j];
+    unsigned inc = sum;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const unsigned u = __shfl_up(inc, off);
+      if (lane >= off) inc += u;
+    }
+    unsigned acc = inc - sum;
+    for (int j = 0; j < per; ++j)
+      if (b0 + j < nb) {
+        base[b0 + j] = acc;
+        acc += tot[b0 + j];
+      }
+  }
+  unsigned rank[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) rank[q] = bin[q] >= 0 ? atomicAdd(&cnt[bin[q]], 1u) : 0u;
   __syncthreads();
   for (int b = threadIdx.x; b < nb; b += kBlock)
     if (cnt[b]) base[b] += atomicAdd(&cursor[b], cnt[b]);

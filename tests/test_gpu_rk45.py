@@ -106,7 +106,7 @@ def test_device_irregular_grid(dev):
 def test_rk45_order_is_a_binned_permutation(dev):
     from insite_amd import ops
     rng = np.random.default_rng(11)
-    for N, Tm in [(1, 60), (5000, 60), (70_001, 60), (3000, 2000)]:
+    for N, Tm in [(1, 60), (5000, 60), (70_001, 60), (3000, 2000), (1_000_003, 60)]:
         n = rng.integers(-2, Tm + 5, N).astype(np.int32)
         o = ops.rk45_order(torch.tensor(n, device=dev), Tm).cpu().numpy()
         assert np.array_equal(np.sort(o), np.arange(N))
