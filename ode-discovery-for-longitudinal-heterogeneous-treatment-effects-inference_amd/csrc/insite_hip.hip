@@ -2622,9 +2622,14 @@ __device__ __forceinline__ int64_t xcd_rank(int64_t b, int64_t lo, int64_t hi) {
   return r;
 }
 
-// lagged = 1 (insite_fit_rollout_lagged_f64, the N > 1 schedule): block gblocks only REDUCES the previous slot to
-// the rank-local G|b (out.G, out.b; no STLSQ -- the ranks all-reduce it between launches), block gblocks + 1
-// solves the STLSQ of an all-reduced system (G_fit, b_fit -> fit), and the rollout starts at block gblocks + 2.
+// lagged = 1 (insite_fit_rollout_lagged_f64, the N > 1 schedule): block gblocks REDUCES the previous slot to the
+// rank-local G|b (out.G, out.b; no STLSQ -- the ranks all-reduce it between launches) and then solves the STLSQ of
+// an all-reduced system (G_fit, b_fit -> fit; a bucket the reduction never writes), so the rollout keeps the
+// deferred step's blocks (INSITE_LAG_MERGED; 0: the solve on a block of its own, round 4, the rollout one block
+// shorter).
+#ifndef INSITE_LAG_MERGED
+#define INSITE_LAG_MERGED 1
+#endif
 template <bool SMOOTH, int METHOD>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_STEP_WPE)))
 step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
@@ -2664,10 +2669,11 @@ step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, con
       INSITE_TREAL(49152, 9);
       INSITE_TSTAMP(49152, 0);
     }
+    if (INSITE_LAG_MERGED && lagged && G_fit) fit_from_gb<7>(G_fit, b_fit, fit);  // (another bucket: no sync)
     return;
   }
   int first = gblocks + 1;
-  if (lagged) {
+  if (lagged && !INSITE_LAG_MERGED) {
     if ((int)blockIdx.x == gblocks + 1) {
       if (G_fit) fit_from_gb<7>(G_fit, b_fit, fit);
       return;
@@ -4160,7 +4166,7 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
                                                     : step_deferred_kernel<true, INSITE_METHOD_EULER>)
                      : (method == INSITE_METHOD_RK4 ? step_deferred_kernel<false, INSITE_METHOD_RK4>
                                                     : step_deferred_kernel<false, INSITE_METHOD_EULER>);
-    const int nfin = lagged ? 2 : 1;  // finalisation blocks: the reduction (and, lagged, the STLSQ of G_fit|b_fit)
+    const int nfin = lagged && !INSITE_LAG_MERGED ? 2 : 1;  // finalisation blocks (the reduction [+ the STLSQ])
     int grid = resident_waves(kd) / kWavesPerBlock;
     if (grid < 2 + nfin) grid = 2 + nfin;
     // half the resident blocks stream the gram (blocks b and b + grid/2 share a CU), nfin finalise, the rest roll out
