@@ -161,6 +161,9 @@ __device__ __forceinline__ int pm_slot_index(int r, int col) {
 #ifndef INSITE_REFINE_CF
 #define INSITE_REFINE_CF 1
 #endif
+#ifndef INSITE_REFINE_SCAN_UNROLL
+#define INSITE_REFINE_SCAN_UNROLL 1
+#endif
 // the per-arm constants of CF for one evaluation
 struct CfArm {
   double P, B, hS, C1, C2;
@@ -181,6 +184,21 @@ __device__ __forceinline__ CfArm cf_arm(double g0, double g1, double h, int n) {
   c.C1 = (double)n * h * qn1;
   c.C2 = h * h * g0 * Cs;
   return c;
+}
+
+// fma as the three-address VOP3 form (INSITE_REFINE_FMA3): the compiler's two-address v_fmac ties the result to the
+// addend -- in the unrolled scan a fresh select -- and then moves it back to the tangent's register (5 moves a step)
+#ifndef INSITE_REFINE_FMA3
+#define INSITE_REFINE_FMA3 1
+#endif
+__device__ __forceinline__ double fma3(double a, double b, double c) {
+#if INSITE_REFINE_FMA3
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+#else
+  return fma(a, b, c);
+#endif
 }
 
 __device__ __forceinline__ void ring_wait() {
@@ -349,7 +367,47 @@ struct RefineLane {
 #pragma unroll
       for (int a = 0; a < NA; ++a) cfa[a] = cf_arm(gam[a][0], gam[a][1], h, ra.sub);
     }
-    for (int k = 0; k < kend; ++k) {
+    // INSITE_REFINE_SCAN_UNROLL (the row kernel's closed-form scan, WIN + PM, two arms): the loop runs over the ring's
+    // column chunks and unrolls a chunk's 8 columns, so a step's column, ring offset and arm bit are compile-time
+    // pieces (no loop-carried register rotation, the chunk check once per chunk) and the arm's constants are chosen
+    // by selects instead of a divergent branch -- the same operations in the same order as the loop below
+    constexpr bool kUnr = INSITE_REFINE_SCAN_UNROLL && WIN && PM && kCf && NA == 2;
+    if constexpr (kUnr) {
+      for (int c = 0; c < nch; ++c) {
+        if (c > 0) {  // column chunk c landed; start the next one
+          ring_wait();
+          if (c + 1 < nch) fill(c + 1, (c + 1) & 1);
+        }
+        const double* ws = win + (c & 1) * (kWin * kWave) + lbase;
+        const uint32_t amc = (uint32_t)(c == 0 ? (am << 1) : (am >> (kWin * c - 1)));  // bit j: arm of step 8c + j - 1
+#pragma unroll
+        for (int j = 0; j < kWin; ++j) {
+          const int k = kWin * c + j - 1;
+          if (k < 0 || k >= Kw) continue;  // wave-uniform
+          if (k < Kl) {
+            const bool a1 = ((amc >> j) & 1u) != 0u;
+            const double vk1 = ws[(j + lrot) & (kWin - 1)];
+            // only P and B are selected: each arm's own source terms come from its own constants (the inactive
+            // arm's C1 y + C2 is formed and dropped), the active arm's values are the loop's
+            const double P = a1 ? cfa[1].P : cfa[0].P, B = a1 ? cfa[1].B : cfa[0].B;
+            const double a1v0 = fma(cfa[0].C1, y, cfa[0].C2), a1v1 = fma(cfa[1].C1, y, cfa[1].C2);
+            d[0][0] = fma3(P, d[0][0], a1 ? 0.0 : cfa[0].hS);
+            d[0][1] = fma3(P, d[0][1], a1 ? 0.0 : a1v0);
+            d[1][0] = fma3(P, d[1][0], a1 ? cfa[1].hS : 0.0);
+            d[1][1] = fma3(P, d[1][1], a1 ? a1v1 : 0.0);
+            y = fma3(P, y, B);
+            const double r = vk1 - y;
+            L = fma(r, r, L);
+            const double r2 = -2.0 * r;
+#pragma unroll
+            for (int a = 0; a < NA; ++a)
+#pragma unroll
+              for (int e = 0; e <= D; ++e) gG[a][e] = fma(r2, d[a][e], gG[a][e]);
+          }
+        }
+      }
+    }
+    for (int k = 0; k < (kUnr ? 0 : kend); ++k) {
       int ak;
       double vk1;
       if constexpr (WIN && PM) {
