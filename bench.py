@@ -34,9 +34,10 @@ HBM_PEAK_GBPS = 8000.0     # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
 
 # Untimed warmup steps when --warmup is not given.  The C5 rollout reaches its steady state only after a few dozen
 # calls (5 warmup steps: 0.79 ms/step by the wall clock while the per-launch events already read 0.73; 60: 0.71 and
-# 0.715 agree), C4 and F4 after a few hundred of their short steps (5 %); C2, C3 and INSITE do not move
-# (profiles/r05/warm/).  Warmup is outside the timed region either way and the line reports the count used.
-WARMUP_DEFAULT = {"c5": 60, "c4": 200, "f4": 200}
+# 0.715 agree), C4 and F4 after a few hundred of their short steps (5 %), the C3 Gram's launches 0.8 % after 20
+# (8.15 -> 8.08 ms); C2 and INSITE do not move (profiles/r05/warm/).  Warmup is outside the timed region either way
+# and the line reports the count used.
+WARMUP_DEFAULT = {"c5": 60, "c4": 200, "f4": 200, "c3": 20}
 
 
 def parse():
@@ -44,7 +45,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=None,
-                    help="untimed warmup steps (default: 5; C5 60, C4 / F4 200 -- see WARMUP_DEFAULT)")
+                    help="untimed warmup steps (default: 5; C5 60, C4 / F4 200, C3 20 -- see WARMUP_DEFAULT)")
     ap.add_argument("--rk45-identity-order", action="store_true",
                     help="C5 ablation: lane r runs row r (no binning by n_obs)")
     ap.add_argument("--patients", type=int, default=100_000, help="patients per GPU (C2: 100k)")
