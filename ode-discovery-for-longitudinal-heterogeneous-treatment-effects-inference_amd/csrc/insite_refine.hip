@@ -164,6 +164,9 @@ __device__ __forceinline__ int pm_slot_index(int r, int col) {
 #ifndef INSITE_REFINE_SCAN_UNROLL
 #define INSITE_REFINE_SCAN_UNROLL 1
 #endif
+#ifndef INSITE_REFINE_SCAN_LROT
+#define INSITE_REFINE_SCAN_LROT 1
+#endif
 // the per-arm constants of CF for one evaluation
 struct CfArm {
   double P, B, hS, C1, C2;
@@ -386,7 +389,11 @@ struct RefineLane {
           if (k < 0 || k >= Kw) continue;  // wave-uniform
           if (k < Kl) {
             const bool a1 = ((amc >> j) & 1u) != 0u;
-            const double vk1 = ws[(j + lrot) & (kWin - 1)];
+            int lr = lrot;
+#if INSITE_REFINE_SCAN_LROT
+            asm("" : "+v"(lr));  // the ring offset formed per step: 8 hoisted offsets held ~8 more VGPRs (spills)
+#endif
+            const double vk1 = ws[(j + lr) & (kWin - 1)];
             // only P and B are selected: each arm's own source terms come from its own constants (the inactive
             // arm's C1 y + C2 is formed and dropped), the active arm's values are the loop's
             const double P = a1 ? cfa[1].P : cfa[0].P, B = a1 ? cfa[1].B : cfa[0].B;
