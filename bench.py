@@ -1172,7 +1172,7 @@ def insite_main(args):
     # objective scan of a wave refills its LDS ring for all 64 rows up to the wave's longest window, in 8-step slots,
     # as long as any lane has a trial pending (wave max nfev x slots(wave max K + 1) x 64 rows x 8 B), plus the final
     # scan's V + arms read and the predictions written -- against the measured traffic
-    ex = pmc_executed("profiles/r05/refine_pmc_base/summary.json", "insite_refine_kernel<3, 2, 1, true, true>",
+    ex = pmc_executed("profiles/r05/refine_pmc_scan/summary.json", "insite_refine_kernel<3, 2, 1, true, true>",
                       args=args, config="insite")
     if ex is not None:
         ring_b = float((nfw.max(1) * ((kw.max(1) + 1 + 7) // 8 * 8)).sum()) * 64 * 8
