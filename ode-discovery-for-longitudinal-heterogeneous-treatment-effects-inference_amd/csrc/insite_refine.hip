@@ -164,6 +164,9 @@ __device__ __forceinline__ int pm_slot_index(int r, int col) {
 #ifndef INSITE_REFINE_SCAN_UNROLL
 #define INSITE_REFINE_SCAN_UNROLL 1
 #endif
+#ifndef INSITE_REFINE_HOIST
+#define INSITE_REFINE_HOIST 1  // 1 / K and dt / sub once per row (RefineLane::setK); measured neutral (profiles/r05/scan/run_hoist)
+#endif
 #ifndef INSITE_REFINE_SCAN_LROT
 #define INSITE_REFINE_SCAN_LROT 1
 #endif
@@ -254,6 +257,12 @@ struct RefineLane {
   double norm;
   double mono[M];
   double c0a[M];
+  double iKv = 0.0, hv = 0.0;  // 1 / K and the sub-step dt / sub, once per row (were two divisions per evaluation)
+  __device__ void setK(int k) {
+    K = k;
+    iKv = 1.0 / (double)k;
+    hv = ra.dt / (double)ra.sub;
+  }
   uint64_t am = 0;         // WIN: arm of step k in bit k
   double* win = nullptr;   // WIN: this wave's ring, 2 slots x kWin steps x 64 rows (step j of a slot at j * 64)
   int64_t p0 = 0;          // WIN: the wave's first column
@@ -337,7 +346,7 @@ struct RefineLane {
               if (ex == e) gam[a][e] += t;
       }
     }
-    const double h = ra.dt / (double)ra.sub;
+    const double h = INSITE_REFINE_HOIST ? hv : ra.dt / (double)ra.sub;
     double y = PM ? ra.V[p * ra.ldv] : ra.V[p];
     double d[NA][D + 1], gG[NA][D + 1];
 #pragma unroll
@@ -505,7 +514,7 @@ struct RefineLane {
 #pragma unroll
         for (int e = 0; e <= D; ++e) gG[a][e] = fma(r2, d[a][e], gG[a][e]);
     }
-    const double iK = 1.0 / (double)K;   // (a non-live WIN lane divides by its own K too; its values are unused)
+    const double iK = INSITE_REFINE_HOIST ? iKv : 1.0 / (double)K;   // (a non-live WIN lane: its own K; values unused)
     L *= iK;
     double pen = 0.0, sq[M];
 #pragma unroll RU
@@ -916,7 +925,7 @@ insite_refine_kernel(RefineArgs) {
   // is the nested form's, operation for operation (A/B: INSITE_REFINE_FLAT=0).
   const bool refine = sl > ra.tau && ra.T >= 2;  // (WIN: every lane enters; the inert ones scan nothing)
   if (WIN || refine) {
-    ln.K = refine ? min(sl - ra.tau, ra.T - 1) : 0;
+    ln.setK(refine ? min(sl - ra.tau, ra.T - 1) : 0);
     BfgsFlat<M, kHL, RU, RefineLane<M, NA, D, WIN, PM>> B;
     if constexpr (kHL) B.H.base = sH + threadIdx.x;
 #pragma unroll RU
@@ -950,7 +959,7 @@ insite_refine_kernel(RefineArgs) {
   }
 #else
   if (sl > ra.tau && ra.T >= 2) {
-    ln.K = min(sl - ra.tau, ra.T - 1);
+    ln.setK(min(sl - ra.tau, ra.T - 1));
     double g[M];
     const double start = ln.fg(x, g);  // norm 1, penalty 0 at c0
     ln.norm = start * 2.5;
@@ -1370,11 +1379,11 @@ insite_refine_dyn_kernel(RefineArgs, unsigned* queue, int refill) {
     has = true;
     const int sl = ra.sl[p];
     if (sl > ra.tau && ra.T >= 2) {
-      ln.K = min(sl - ra.tau, ra.T - 1);
+      ln.setK(min(sl - ra.tau, ra.T - 1));
       ln.norm = 1.0;
       pending = fresh = true;
     } else {
-      ln.K = 0;
+      ln.setK(0);
       finish(-1, 0);
     }
   };
