@@ -2698,7 +2698,9 @@ step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, con
 #else
   const int64_t S = rc ? units * INSITE_DEF_RSTATIC / 1000 : units;
   rollout_units<METHOD>(ra, lib, lane, rw * S / RW, (rw + 1) * S / RW, ng);
-  if (rc) {
+  // (compiled only into the claimed-tail build: the dead claim paths in the default kernel took it from 232 to 248
+  // VGPRs with a 104-B stack frame and the C2 launch 0.066 -> 0.069 ms, profiles/r05/c2reg/)
+  if (INSITE_DEF_RSTATIC < 1000 && rc) {
     const int64_t nrb = (int64_t)gridDim.x - first;
     if (INSITE_DEF_XHEADS && nrb >= kXcds) {
       const int xs = (int)(blockIdx.x % kXcds);
