@@ -15,6 +15,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -89,7 +90,13 @@ def parse():
                     help="fused mode: blocks of the step kernel's resident round given to the discovery (0 = the "
                          "library's default split)")
     ap.add_argument("--cpu-sample", type=int, default=100_000, help="patients in the timed CPU sample")
-    ap.add_argument("--no-north-star", action="store_true", help="skip the 1M x 500 rollout roofline probe")
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="skip the north-star blocks of the C2 line: the 1M x 500 rollout roofline probe and the full "
+                         "1M x 500 deferred step (discovery + RK4 rollout, north_star_step)")
+    ap.add_argument("--ns-steps", type=int, default=10, help="timed launches of the north_star_step block")
+    ap.add_argument("--no-c3-block", action="store_true",
+                    help="skip the compact C3 block (BASELINE configs[2], the largest single-GPU configuration) of "
+                         "the default C2 line")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle check of the benched cohort (every line: a sample of the last timed step's "
                          "rows through the oracle after the timed region)")
@@ -102,7 +109,7 @@ def parse():
                          "re-reads data the 256 MB Infinity Cache still holds)")
     ap.add_argument("--isolated", action="store_true",
                     help="also time each C2 kernel in isolation (back-to-back launches on one stream)")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "insite", "insite4", "f4"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "insite", "insite4", "f4", "ns"],
                     help="c2: BASELINE configs[1], the headline line (default); c3: configs[2], the 5-state fp32 "
                          "system (parity-test configuration, measured separately)")
     ap.add_argument("--insite-only-binned", action="store_true",
@@ -197,6 +204,22 @@ def host_info():
     return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "sched_affinity": aff, "workers": workers}
 
 
+@contextlib.contextmanager
+def worker_pool(ctx, W, initializer, initargs=()):
+    """A process pool that ends with close() + join(): the workers exit on their own once the work is done.  (The
+    Pool context manager's terminate() SIGTERMs them, which under rocprofv3 -- whose preloaded library the workers
+    inherit -- printed an "Aborted at" stack per worker into every profiler log)"""
+    pool = ctx.Pool(W, initializer=initializer, initargs=initargs)
+    try:
+        yield pool
+    except BaseException:
+        pool.terminate()
+        pool.join()
+        raise
+    pool.close()
+    pool.join()
+
+
 _CPU = {}
 
 
@@ -273,7 +296,7 @@ def cpu_baseline(n_sample, T, method, seed, ivp_per_worker=100):
                 exps=R.poly_library(3, 2, True), dt=R.MAX_TIME_HORIZON / T, T=T, method=method)
     chunks = [(int(a[0]), int(a[-1]) + 1) for a in np.array_split(np.arange(n_sample), W) if a.size]
     ctx = mp.get_context("fork")          # no GPU context exists yet in this process
-    with ctx.Pool(W, initializer=_cpu_worker_init) as pool:
+    with worker_pool(ctx, W, _cpu_worker_init) as pool:
         pool.map(abs, range(W))           # workers up before the clock starts
         t0 = time.perf_counter()
         parts = pool.map(_cpu_gram_chunk, chunks)
@@ -281,7 +304,7 @@ def cpu_baseline(n_sample, T, method, seed, ivp_per_worker=100):
         b = sum(q[1] for q in parts)
         _CPU["coef"] = np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)])
         el_disc = time.perf_counter() - t0
-    with ctx.Pool(W, initializer=_cpu_worker_init) as pool:   # forked after the fit: workers see the coefficients
+    with worker_pool(ctx, W, _cpu_worker_init) as pool:   # forked after the fit: workers see the coefficients
         pool.map(abs, range(W))
         t1 = time.perf_counter()
         pool.map(_cpu_rollout_chunk, chunks)
@@ -339,13 +362,13 @@ def c3_cpu_baseline(per_worker, T, seed):
     W = info["workers"]
     n = per_worker * W
     ctx = mp.get_context("fork")
-    with ctx.Pool(W, initializer=_cpu_worker_init) as pool:
+    with worker_pool(ctx, W, _cpu_worker_init) as pool:
         parts = pool.map(_cpu_c3_gen, [(w * per_worker, (w + 1) * per_worker, T, seed + 101 * w) for w in range(W)])
     _CPU.update(x=np.concatenate([p[0] for p in parts]), a=np.concatenate([p[1] for p in parts]),
                 a_cf=np.concatenate([p[2] for p in parts]), exps=M.c3_library())
     del parts
     chunks = [(w * per_worker, (w + 1) * per_worker) for w in range(W)]
-    with ctx.Pool(W, initializer=_cpu_worker_init) as pool:
+    with worker_pool(ctx, W, _cpu_worker_init) as pool:
         pool.map(abs, range(W))
         t0 = time.perf_counter()
         gb = pool.map(_cpu_c3_gram_chunk, chunks)
@@ -353,7 +376,7 @@ def c3_cpu_baseline(per_worker, T, seed):
         B = sum(q[1] for q in gb)
         _CPU["coef"] = M.ms_stlsq(G, B)[0]
         el_disc = time.perf_counter() - t0
-    with ctx.Pool(W, initializer=_cpu_worker_init) as pool:   # forked after the fit: workers see the model
+    with worker_pool(ctx, W, _cpu_worker_init) as pool:   # forked after the fit: workers see the model
         pool.map(abs, range(W))
         t1 = time.perf_counter()
         pool.map(_cpu_c3_rollout_chunk, chunks)
@@ -380,9 +403,18 @@ def c3_main(args):
     if os.environ.get("WORLD_SIZE", "1") == "1" and not args.no_cpu_baseline:
         # 2000 patients per worker (~0.8 s of discovery + rollout each; the cohort build is untimed)
         cpu = c3_cpu_baseline(max(64, min(2000, args.cpu_sample // 50)), T, args.seed + 3)
-    from insite_amd import multistate as MS
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    out = c3_measure(args, dev, N, T, args.steps, args.warmup, not args.no_parity)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+    emit(out)
+
+
+def c3_measure(args, dev, N, T, steps, warmup, parity=True):
+    """The C3 line's measurement (c3_main; also the compact ``c3`` block of the default C2 line):
+    ``steps`` timed discovery + rollout steps after ``warmup``, per-kernel HIP-event averages, the oracle parity."""
+    from insite_amd import multistate as MS
     coh = MS.synthetic_c3(N, T, seed=args.seed, device=dev)
     g = torch.Generator(device=dev)
     g.manual_seed(args.seed + 17)
@@ -410,16 +442,16 @@ def c3_main(args):
     disc()
     torch.cuda.synchronize(dev)
     support[0] = mask.cpu().numpy() != 0
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         disc()
         roll()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         disc()
         roll()
     torch.cuda.synchronize(dev)
-    ms_step = (time.perf_counter() - t0) / args.steps * 1e3
+    ms_step = (time.perf_counter() - t0) / steps * 1e3
 
     def timed(fn, n):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -430,7 +462,7 @@ def c3_main(args):
         torch.cuda.synchronize(dev)
         return e0.elapsed_time(e1) / n
 
-    n_roof = max(args.steps, 5)
+    n_roof = max(steps, 5)
     gram_ms_t = timed(lambda: MS.gram_ms(coh.x, coh.a, lib, coh.dt, out=(G, B)), n_roof)
     roll_ms_t = timed(roll, n_roof)
     roll_dense_t = timed(lambda: MS.rollout_ms(coh.y0, a_cf, coef, lib, coh.dt, T, method="rk4", out=y), n_roof)
@@ -452,7 +484,7 @@ def c3_main(args):
     gram_bytes = T * N * S * 4 + T * ((N + 31) // 32) * 4
     out = {
         "metric": METRIC, "value": N / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": 1,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+        "steps": steps, "warmup": warmup, "ms_per_step": ms_step, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32 (storage, rollout) / f64 (Gram, STLSQ)",
         "data": "synthetic: on-device C3 cohort (planted 5-state system, Markov treatment, RK4-10 truth)",
         "config": {"workload": f"C3: 5-state + binary treatment, {N // 1000}k patients x {T} steps: discovery "
@@ -470,11 +502,9 @@ def c3_main(args):
                     "frac": roll_bytes / (roll_ms_t * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                     "dense_kernel_avg_launch_ms": roll_dense_t},
     }
-    if not args.no_parity:
+    if parity:
         out["parity"] = c3_parity(coh, a_cf, lib, T, G, B, coef, mask, y)
-    if cpu is not None:
-        out["cpu_baseline"] = cpu
-    emit(out)
+    return out
 
 
 C5_COEF = (-1.1108, -0.1454, -1.0235)   # the EQ_4_C model of the reference log (final_with_insite.txt:182)
@@ -534,7 +564,7 @@ def c5_cpu_baseline(n_sample, seed, ivp_per_worker=40):
     chunks = [(int(c[0]), int(c[-1]) + 1) for c in np.array_split(np.arange(n_sample), W) if c.size]
     n_ivp = min(n_sample, ivp_per_worker * W)
     ivp_chunks = [(int(c[0]), int(c[-1]) + 1) for c in np.array_split(np.arange(n_ivp), W) if c.size]
-    with mp.get_context("fork").Pool(W, initializer=_cpu_worker_init) as pool:
+    with worker_pool(mp.get_context("fork"), W, _cpu_worker_init) as pool:
         pool.map(abs, range(W))
         t0 = time.perf_counter()
         pool.map(_cpu_rk45_chunk, chunks)
@@ -551,6 +581,15 @@ def c5_cpu_baseline(n_sample, seed, ivp_per_worker=40):
                 "sample": f"{n_ivp} irregular-grid patients on {W} workers in {el_ivp:.2f} s (one solve_ivp call per "
                           f"interval, arm held over it, as the reference integrates per interval); the rate "
                           f"extrapolates linearly in patients"}}
+
+
+def _binned_divergence(st, chunk):
+    """Wave divergence (sum of per-wave max / sum of attempts) if the lanes took the rows sorted by attempt count inside
+    consecutive ``chunk``-row ranges (descending), whole waves of 64."""
+    n = st.numel() // chunk * chunk
+    srt = torch.sort(st[:n].view(-1, chunk), dim=1, descending=True).values.reshape(-1)
+    w = srt[: n // 64 * 64].view(-1, 64)
+    return float((w.max(dim=1).values.mean() / w.mean()).item()) if w.numel() else None
 
 
 def c5_main(args):
@@ -649,6 +688,12 @@ def c5_main(args):
         "rk45": {"mean_attempts_per_patient": float(st.mean()),
                  "mean_attempts_per_interval": float(st.sum() / intervals.sum()),
                  "wave_divergence": float((per_wave.max(dim=1).values.mean() / per_wave.mean()).item()),
+                 #  the same figure under its explicit name: a wave's flat loop runs its slowest
+                 # lane's attempt count, so sum over waves of max / sum of attempts is the issued-work inflation
+                 "attempts_max_over_mean_per_wave": float((per_wave.max(dim=1).values.mean() / per_wave.mean()).item()),
+                 # what binning by the previous call's per-patient attempt count (a C5 step re-rolls the same cohort)
+                 # would give, rows sorted by attempts inside the same 4096-row chunks the n_obs binning uses
+                 "attempts_max_over_mean_if_binned_by_attempts": _binned_divergence(st, 4096),
                  "rhs_evals_per_s": float(st.sum() * 6 / (launch_ms * 1e-3))},
     }
     if world == 1 and not args.no_parity:
@@ -681,7 +726,7 @@ def parity_map(fn, jobs):
     if W <= 1:
         _par_init()
         return [fn(j) for j in jobs]
-    with mp.get_context("spawn").Pool(W, initializer=_par_init) as pool:
+    with worker_pool(mp.get_context("spawn"), W, _par_init) as pool:
         return pool.map(fn, jobs)
 
 
@@ -696,15 +741,16 @@ def sample_rows(N, n, seed, extra=()):
 
 def _par_refine_job(job):
     from oracle import insite_refine_ref as Q
-    V, arm, u, sl, c0, ex, dt, lam, tau, n_in = job
-    out = [Q.refine_patient(V[i], arm[i], u[i], int(sl[i]), c0, ex, dt, lam, tau, n_inputs=n_in)
-           for i in range(V.shape[0])]
+    V, arm, u, sl, c0, ex, dt, lam, tau, n_in = job[:10]
+    rev = bool(job[10]) if len(job) > 10 else False
+    out = [Q.refine_patient(V[i], arm[i], u[i], int(sl[i]), c0, ex, dt, lam, tau, n_inputs=n_in,
+                            revert_on_zoom_fail=rev) for i in range(V.shape[0])]
     return (np.stack([o[0] for o in out]), np.stack([np.asarray(o[1]).reshape(-1) for o in out]),
             np.array([o[2] for o in out]), np.array([o[3] for o in out]))
 
 
 def insite_parity(V, arm, u, sl, c0, lib, dt, lam, tau, preds, coef, status, iters, n_sample=4096, seed=13,
-                  extra=()):
+                  extra=(), revert=False):
     """The INSITE lines' parity: ``n_sample`` rows of the timed cohort (plus ``extra``, e.g. the first / last lanes
     of the binned order) through oracle/insite_refine_ref.refine_patient (the reference's jax BFGS restated,
     sindy.py:587-665, 781-794) against the rows the last timed step wrote: per-row status and iteration count
@@ -724,7 +770,7 @@ def insite_parity(V, arm, u, sl, c0, lib, dt, lam, tau, preds, coef, status, ite
     parts = [c for c in np.array_split(np.arange(idx.size), 4 * W) if c.size]
     t0 = time.perf_counter()
     res = parity_map(_par_refine_job, [(Vh[c], ah[c], uh[c], slh[c], np.asarray(c0, dtype=np.float64), ex, dt, lam,
-                                        tau, int(lib.n_inputs)) for c in parts])
+                                        tau, int(lib.n_inputs), revert) for c in parts])
     el = time.perf_counter() - t0
     P, C = np.concatenate([r[0] for r in res]), np.concatenate([r[1] for r in res])
     S, I = np.concatenate([r[2] for r in res]), np.concatenate([r[3] for r in res])
@@ -745,6 +791,15 @@ def insite_parity(V, arm, u, sl, c0, lib, dt, lam, tau, preds, coef, status, ite
             "coef_linf": float(np.abs(gc - C).max()),
             "coef_linf_status_equal": float(np.abs(gc - C)[same].max()) if same.any() else None,
             "oracle_seconds": el,
+            **({"revert_on_zoom_fail": True,
+                # the status-mismatch rows under the literal revert (sindy.py:628-631): one side keeps c0, the other
+                # its BFGS iterate, so their predictions differ by the refinement itself -- reported, not toleranced
+                "mismatch_rows": int((~same).sum()),
+                "pred_rmse_status_equal": float(np.sqrt(np.mean(d[same] ** 2))) if same.any() else None,
+                "pred_max_rel_status_mismatch": float(rel[~same].max()) if (~same).any() else None,
+                "mismatch_reverted_side_is_c0": bool(all(
+                    np.array_equal((gc if gs[i] == 3 else C)[i], np.asarray(c0, dtype=np.float64).reshape(-1)[:gc.shape[1]])
+                    for i in np.flatnonzero(~same) if 3 in (gs[i], S[i])))} if revert else {}),
             "tolerances": {"status_equal_frac": 0.995, "pred_rmse": 1e-6, "coef_linf": 1e-7}}
 
 
@@ -1007,7 +1062,7 @@ def insite_cpu_baseline(seed, per_worker=2000):
                 u=np.stack([sim["observed_static_c_0"], sim["observed_static_c_1"]], axis=1),
                 sl=rng.integers(1, T, size=n), c0=c0, dt=10.0 / T)
     chunks = [(int(a[0]), int(a[-1]) + 1) for a in np.array_split(np.arange(n), W) if a.size]
-    with mp.get_context("fork").Pool(W, initializer=_cpu_worker_init) as pool:
+    with worker_pool(mp.get_context("fork"), W, _cpu_worker_init) as pool:
         pool.map(abs, range(W))
         t0 = time.perf_counter()
         pool.map(_cpu_refine_chunk, chunks)
@@ -1133,7 +1188,7 @@ def insite_main(args):
     kbytes = N * T * (8 + 1 + 8) + N * (8 * 2 + 4 + 4) + N * (2 * coh.lib.n_terms * 8 + 8)
     out = {
         "metric": METRIC, "value": N / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": 1,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+        "steps": steps, "warmup": warmup, "ms_per_step": ms_step, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: on-device EQ_4_C cohort, T=60, seq_len U{1..59}, arm flip at a random step",
         "config": {"workload": f"INSITE refinement (BFGS per row, tau=5, lam=10) + Euler-5 rollout, "
@@ -1190,6 +1245,12 @@ def insite_main(args):
         o_ = plan.order.long()
         out["parity"] = insite_parity(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, preds, coef, status, iters,
                                       extra=(o_[:64].cpu().numpy(), o_[-64:].cpu().numpy()))
+        # the literal reading of sindy.py:628-631 (status 3 reverts to the global model): the same
+        # rows through the product call with revert_on_zoom_fail and the oracle with the same flag (untimed)
+        rplan = ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, revert_on_zoom_fail=True)
+        rp, rc, rs_, ri = (t.clone() for t in rplan())
+        out["parity_revert_mode"] = insite_parity(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, rp, rc, rs_, ri,
+                                                  extra=(o_[:64].cpu().numpy(), o_[-64:].cpu().numpy()), revert=True)
     if cpu is not None:
         out["cpu_baseline"] = cpu
     emit(out)
@@ -1279,7 +1340,7 @@ def insite4_cpu_baseline(V, arm, u, sl, c0, ex, dt, per_worker=256):
     n = min(W * per_worker, V.shape[0])
     _CPU.update(V=V[:n], arm=arm[:n], u=u[:n], sl=sl[:n], c0=c0, ex=ex, dt=dt)
     chunks = [(int(a[0]), int(a[-1]) + 1) for a in np.array_split(np.arange(n), W) if a.size]
-    with mp.get_context("fork").Pool(W, initializer=_cpu_worker_init) as pool:
+    with worker_pool(mp.get_context("fork"), W, _cpu_worker_init) as pool:
         pool.map(abs, range(W))
         t0 = time.perf_counter()
         pool.map(_cpu_refine4_chunk, chunks)
@@ -1456,7 +1517,7 @@ def f4_main(args):
     achieved = gb / (gram_ms * 1e-3) / 1e9
     res = {
         "metric": METRIC, "value": N / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": 1,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+        "steps": steps, "warmup": warmup, "ms_per_step": ms_step, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: on-device 4-arm cohort (planted per-arm model, Markov arms p=0.1, Euler-5 truth + 0.01 noise)",
         "config": {"workload": f"F4: cancer_sim/EQ_5 path, {N // 1000}k patients x {T} steps, 4 arms: segment-split "
@@ -1666,8 +1727,7 @@ def c4_main(args):
             ex = lib.exps.astype(np.int64)
             chunks = [(int(q[0]), int(q[-1]) + 1) for q in np.array_split(np.arange(n_s), W) if q.size]
             # the sample travels to the workers at start-up (initargs), outside the clock
-            with mp.get_context("spawn").Pool(W, initializer=_cpu_pp_init,
-                                               initargs=(xs, us, ar, rw, coh.dt, ex, gc)) as pool:
+            with worker_pool(mp.get_context("spawn"), W, _cpu_pp_init, (xs, us, ar, rw, coh.dt, ex, gc)) as pool:
                 pool.map(abs, range(W))
                 t1 = time.perf_counter()
                 pool.map(_cpu_pp_fit_chunk, chunks)
@@ -1740,7 +1800,7 @@ def traffic_for(config, kernel, grid=None, args=None):
         # 60 (c4, f4); compare the EFFECTIVE sizes, so an explicit --T 60 on c4 is its default workload too
         big = config != "c2"
         eff_n = 1_000_000 if (big and args.patients == 100_000) else args.patients
-        t_def = {"c3": 500, "c4": 60, "f4": 60}.get(config, 200)
+        t_def = {"c3": 500, "c4": 60, "f4": 60, "ns": 500}.get(config, 200)
         eff_t = t_def if args.T == 200 else args.T
         knobs = (eff_n, eff_t, args.method, args.arm_format, args.layout, args.gram_blocks, args.dstreams,
                  int(os.environ.get("WORLD_SIZE", "1")))
@@ -2014,22 +2074,32 @@ def deferred_run(args, dev, coh, arm_cf, coh2=None, arm_cf2=None):
             "roll_coef": used[0], "roll_mask": used[1], "roll_cohort": mine[last % len(mine)]}
 
 
-def c2_parity(dev, coh, arm_bits, coef, mask, y, n_sample=4096, seed=11):
+def c2_parity(dev, coh, arm_bits, coef, mask, y, n_sample=4096, seed=11, pooled=False):
     """The metric's "RMSE vs CPU ref" for the benched cohort (after the timed region): the oracle
     (oracle/insite_ref.py: the reference's SINDy.fit + RK4 scan restated, sindy.py:190-192, 371-431) fits the SAME
-    100k x 200 cohort whose rollout the last timed launch wrote, and rolls a sample of its rows out with its own
-    model; the line reports support equality, coefficient L-inf (GPU vs oracle model) and the trajectory RMSE /
-    max relative error of the GPU y on the sampled rows against the oracle's."""
+    cohort whose rollout the last timed launch wrote (C2: 100k x 200; the north-star step: 1M x 500), and rolls a
+    sample of its rows out with its own model; the line reports support equality, coefficient L-inf (GPU vs oracle
+    model) and the trajectory RMSE / max relative error of the GPU y on the sampled rows against the oracle's.
+    ``pooled``: the whole-cohort Gram in patient chunks and the sampled rollouts on a spawned pool of the host's
+    workers (the chunk Grams summed in chunk order; the 1M x 500 cohort is 500M samples)."""
     sys.path.insert(0, ROOT)
     from oracle import insite_ref as R
     N, T = coh.arm.numel(), coh.x.size(0)
     exps = coh.lib.exps.astype(np.int64)
-    x = coh.x[:, :N].t().contiguous().cpu().numpy()
     u, arm = coh.u.cpu().numpy(), coh.arm.cpu().numpy().astype(np.int64)
     rows = coh.rows.cpu().numpy()
     if not np.all(rows == rows[0]):
         return {"skipped": "ragged rows (the vectorised oracle Gram needs equal rows)"}
-    G, b = R.gram_moments_vectorized(x, u, arm, int(rows[0]), coh.dt, exps)
+    t0 = time.perf_counter()
+    W = host_info()["workers"] if pooled else 1
+    if pooled:
+        bounds = [(int(c[0]), int(c[-1]) + 1) for c in np.array_split(np.arange(N), 2 * W) if c.size]
+        gb = parity_map(_par_gram_job, [(coh.x[:, lo:hi].t().contiguous().cpu().numpy(), u[lo:hi], arm[lo:hi],
+                                         int(rows[0]), coh.dt, exps) for lo, hi in bounds])
+        G, b = sum(q[0] for q in gb), sum(q[1] for q in gb)
+    else:
+        x = coh.x[:, :N].t().contiguous().cpu().numpy()
+        G, b = R.gram_moments_vectorized(x, u, arm, int(rows[0]), coh.dt, exps)
     cr = np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)])
     cg, mg = coef.cpu().numpy(), mask.cpu().numpy()
     rng = np.random.default_rng(seed)
@@ -2038,8 +2108,14 @@ def c2_parity(dev, coh, arm_bits, coef, mask, y, n_sample=4096, seed=11):
     it = torch.as_tensor(idx, device=dev)
     words = arm_bits.index_select(1, it // 32)                                   # [T, n] int32
     arms = ((words >> (it % 32).to(torch.int32)[None, :]) & 1).t().contiguous().cpu().numpy().astype(np.int64)
-    ref = R.rollout(coh.y0[it].cpu().numpy(), coh.u[it].cpu().numpy(), arms[:, :y.size(0)], cr, exps, coh.dt,
-                    method="rk4")
+    y0s, us = coh.y0[it].cpu().numpy(), coh.u[it].cpu().numpy()
+    if pooled:
+        parts = [c for c in np.array_split(np.arange(idx.size), 4 * W) if c.size]
+        ref = np.concatenate(parity_map(_par_roll_job, [(y0s[c], us[c], arms[c, :y.size(0)], cr, exps, coh.dt, "rk4")
+                                                        for c in parts]))
+    else:
+        ref = R.rollout(y0s, us, arms[:, :y.size(0)], cr, exps, coh.dt, method="rk4")
+    el = time.perf_counter() - t0
     got = y.index_select(1, it).t().cpu().numpy()
     d = got - ref
     return {"oracle": "oracle/insite_ref.py (numpy restatement; gram_moments_vectorized + stlsq_gram + rollout rk4)",
@@ -2048,7 +2124,8 @@ def c2_parity(dev, coh, arm_bits, coef, mask, y, n_sample=4096, seed=11):
             "coef_linf": float(np.max(np.abs(cg - cr))),
             "y_rmse": float(np.sqrt(np.mean(d ** 2))),
             "y_max_rel": float(np.max(np.abs(d) / np.maximum(np.abs(ref), 1e-300))),
-            "rows_sampled": int(idx.size), "steps_per_row": int(y.size(0)),
+            "rows_sampled": int(idx.size), "steps_per_row": int(y.size(0)), "oracle_seconds": el,
+            **({"oracle_workers": W} if pooled else {}),
             "tolerances": {"coef_linf": 1e-8, "y_rmse": 1e-6}}
 
 
@@ -2158,6 +2235,28 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
         del y
         torch.cuda.empty_cache()
         out["north_star_rollout"] = north_star_rollout(args, dev, fr["coef"], lib)
+    # the two larger configurations in the driver's own line: BASELINE.json north_star's
+    # 1M x 500 through the headline kernel, and C3 (configs[2], the largest single-GPU configuration), each with its
+    # roofline and oracle parity; the C2 figures above are the line's value.  A failure here never costs the line.
+    fr = None
+    torch.cuda.empty_cache()
+    if not args.no_north_star and deferred and args.patients == 100_000 and args.T == 200:
+        try:
+            out["north_star_step"] = north_star_step(args, dev)
+        except Exception as exc:
+            out["north_star_step"] = {"error": f"{type(exc).__name__}: {exc}"}
+        torch.cuda.empty_cache()
+    if not args.no_c3_block and deferred and args.patients == 100_000 and args.T == 200:
+        try:
+            c3 = c3_measure(args, dev, 1_000_000, 500, 5, 2, not args.no_parity)
+            out["c3"] = {k: c3[k] for k in ("value", "ms_per_step", "steps", "warmup", "dtype", "config", "roofline",
+                                            "rollout", "parity") if k in c3}
+            out["c3"]["note"] = ("BASELINE configs[2] (5-state + binary treatment, 1M x 500): discovery (S-state Gram "
+                                 "on f64 MFMA + STLSQ per state) + RK4 rollout; CPU leg and PMC traffic in the "
+                                 "standalone line (bench.py --config c3)")
+        except Exception as exc:
+            out["c3"] = {"error": f"{type(exc).__name__}: {exc}"}
+        torch.cuda.empty_cache()
     if cpu is not None:
         out["cpu_baseline"] = cpu
     emit(out)
@@ -2320,6 +2419,59 @@ def c2_lagged(args, dev, world, rank, coh, arm_cf, cpu, collective):
     return out, (cohs[rc_ % 2], coef_used, mask_used, y)
 
 
+def north_star_step(args, dev):
+    """BASELINE.json north_star's own configuration through the headline kernel: the full deferred
+    step -- step_deferred_kernel: gram streaming of cohort k | finalisation (reduction + STLSQ) of cohort k-1 | RK4
+    bit-arm rollout of cohort k-2 with its own model -- on 1M patients x 500 steps fp64, two rotating EQ_4_C cohorts
+    (2 x 4 GB of x, 2 x 4 GB of y: no launch re-reads data the Infinity Cache holds), ``--ns-steps`` timed launches,
+    the roofline from HIP events on the launch stream, and the oracle parity of the model and the trajectories the
+    last timed launch used (the whole-cohort oracle fit on the host's workers)."""
+    from insite_amd import cohort
+    ns = argparse.Namespace(**vars(args))
+    ns.patients, ns.T, ns.steps, ns.warmup, ns.dstreams, ns.gram_blocks = 1_000_000, 500, max(2, args.ns_steps), 3, 1, 0
+    N, T = ns.patients, ns.T
+    sd = [args.seed * 1000 + 900, args.seed * 1000 + 901]
+    cohs = [cohort.synthetic_pkpd(N, T, seed=s_, device=dev, equation="EQ_4_C", layout="time") for s_ in sd]
+    arms = [cohort.counterfactual_arms(c.arm, T, seed=s_, layout="time_bits") for c, s_ in zip(cohs, sd)]
+    torch.cuda.synchronize(dev)
+    fr = deferred_run(ns, dev, cohs[0], arms[0], cohs[1], arms[1])
+    rb, gb = fr["rb"], fr["gb"]
+    out = {"workload": "north star: PK/PD EQ_4_C 1M patients x 500 steps fp64 - discovery (savgol+FD4+poly2 "
+                       "library+Gram, STLSQ) + RK4 counterfactual rollout, one step_deferred_kernel launch per step",
+           "patients": N, "T": T, "steps": ns.steps, "warmup": ns.warmup, "cohorts_rotated": 2,
+           "ms_per_step": fr["ms_step"], "patient_trajectories_per_s": N / (fr["ms_step"] * 1e-3),
+           "discovered_support": fr["mask"].cpu().numpy().tolist(),
+           "finite": bool(torch.isfinite(fr["y"]).all().item()),
+           "roofline": {"kernel": "step_deferred_kernel<true, rk4>", "bound": "hbm", "peak": HBM_PEAK_GBPS,
+                        "unit": "GB/s", "achieved": (rb + gb) / (fr["step_ms"] * 1e-3) / 1e9,
+                        "frac": (rb + gb) / (fr["step_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                        "avg_launch_ms": fr["step_ms"], "algorithmic_bytes_per_launch": rb + gb,
+                        "algorithmic_bytes_split": {"discovery_x_read": gb, "rollout_y_written": rb},
+                        "avg_ms_source": f"HIP timing events on the launch stream around {fr['NBAT']} batches of "
+                                         f"{fr['KB']} back-to-back launches, divided by the batch size",
+                        "traffic": traffic_for("ns", "step_deferred_kernel", args=args)},
+           "step_aggregate_frac": (rb + gb) / (fr["ms_step"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+           "target": "north_star: >= 0.40 of the HBM roofline at 1M x 500 on one GPU"}
+    if not args.no_parity:
+        rc_, ra_ = fr["roll_cohort"]
+        out["parity"] = c2_parity(dev, rc_, ra_, fr["roll_coef"], fr["roll_mask"], fr["y"], pooled=True)
+    return out
+
+
+def ns_main(args):
+    """--config ns: the north_star_step block of the default line as a line of its own (counter / profiler runs)."""
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    ns = north_star_step(args, dev)
+    emit({"metric": METRIC, "value": ns["patient_trajectories_per_s"], "unit": "patient-trajectories/s", "n_gpus": 1,
+          "steps": ns["steps"], "warmup": ns["warmup"], "ms_per_step": ns["ms_per_step"], "higher_is_better": True,
+          "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+          "data": "synthetic: on-device EQ_4_C PK/PD cohorts (reference distributions, Euler-5 truth + 0.01 noise)",
+          "config": {"workload": ns["workload"], "patients": ns["patients"], "T": ns["T"]},
+          **{k: v for k, v in ns.items() if k in ("roofline", "parity", "discovered_support", "finite",
+                                                  "step_aggregate_frac")}})
+
+
 def north_star_rollout(args, dev, coef, lib):
     """The 1M x 500 RK4 rollout alone (the north star's >= 40 % roofline target), events around each launch."""
     from insite_amd import ops
@@ -2386,6 +2538,8 @@ def main():
         return c3_main(args)
     if args.config == "c5":
         return c5_main(args)
+    if args.config == "ns":
+        return ns_main(args)
     # the CPU leg runs first, while this process has no GPU context (its worker pool forks)
     cpu = None
     if os.environ.get("WORLD_SIZE", "1") == "1" and not args.no_cpu_baseline:

@@ -3047,10 +3047,13 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
   const double* trow = ra.t + (PM ? pc * ra.ldt : pc);
   // INSITE_RK45_BUFREFILL (PM): the window through a buffer descriptor over t -- one 32-bit offset per lane and
   // immediate offsets for the 8 elements, unclamped (elements past the row's last observation are never used; past
-  // the array the hardware returns 0) -- instead of 8 clamped 64-bit addresses (~30 VALU per refill event)
-  const bool tbuf = PM && INSITE_RK45_BUFREFILL && (int64_t)ra.N * ra.ldt * 8 <= (int64_t)INT32_MAX;
-  const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)ra.t, (short)0, (int)(tbuf ? (int64_t)ra.N * ra.ldt * 8 : 0), 0x00020000);
+  // the array the hardware returns 0) -- instead of 8 clamped 64-bit addresses (~30 VALU per refill event).  The
+  // records end at the last row's T_max-th element, not at N * ldt: a t_obs view whose last row is narrower than
+  // ldt (as_strided) is never read past its storage
+  const int64_t t_rec = ((int64_t)(ra.N - 1) * ra.ldt + ra.Tmax) * 8;
+  const bool tbuf = PM && INSITE_RK45_BUFREFILL && t_rec <= (int64_t)INT32_MAX;
+  const __amdgpu_buffer_rsrc_t trs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)ra.t, (short)0, (int)(tbuf ? t_rec : 0), 0x00020000);
   auto refill = [&](int from) {  // elements clamped to n - 1 (n >= 2 for a live lane)
     base = from;
     if (tbuf) {
@@ -4190,8 +4193,11 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
       rows = reinterpret_cast<const int32_t*>(G_out);
       u = G_out;
     }
-    // the claim area after the two slots (zero between calls; used by the claimed-tail build only)
+    // the claim area after the two slots (used by the claimed-tail build only).  Its offset depends on the cohort
+    // size, so a grow-only workspace reused for another N would put the heads on stale partial bytes: the claimed
+    // build zeroes it before every launch (the default build never touches it)
     unsigned* rc = INSITE_DEF_RSTATIC < 1000 ? reinterpret_cast<unsigned*>(wsb + 2 * ws_one) : nullptr;
+    if (rc && hipMemsetAsync(rc, 0, kDefClaimBytes, hs) != hipSuccess) return INSITE_E_HIP;
     kd<<<dim3(grid), kBlock, 0, hs>>>(x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, part_cur,
                                       part_prev, lagged ? gred : go, ra, gb, rc, hdr_cur, hdr_prev, lagged, G_fit,
                                       b_fit, gf, slot_fingerprint(lib, n_arms));

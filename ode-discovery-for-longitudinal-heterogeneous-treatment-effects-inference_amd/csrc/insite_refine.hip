@@ -1613,7 +1613,8 @@ insite_refine_coop_kernel(RefineArgs) {
   const int64_t p = ra.order ? (int64_t)ra.order[grc] : grc;
   const int ta = j >> 1, te = j & 1;  // this lane's tangent (arm, exponent)
   // the wave's rows staged in LDS: [step][row slot] doubles / arm bytes (row slot = lane / 8)
-  // (the pipelined scan reads up to 4 steps past its end unclamped: kCoopStPad steps of padding, never used)
+  // (the pipelined scan reads up to 4 steps past its end unclamped: kCoopStPad steps of padding whose offsets are
+  // staged as valid table entries and whose values are never used)
   constexpr int kPipe = STG && INSITE_REFINE_CF && INSITE_COOP_SCAN_PIPE;
   constexpr int kStT = kCoopStT + (kPipe ? kCoopStPad : 0);
   __shared__ double sV[STG ? kWavesPerBlock * kStT * kCoopG : 1];
@@ -1639,16 +1640,32 @@ insite_refine_coop_kernel(RefineArgs) {
 #pragma unroll
       for (int g = 0; g < kCoopG; ++g) {
         wV[lane * kCoopG + g] = ra.V[(int64_t)lane * ra.ldv + pg[g]];
-        const int8_t am = ra.arm8[(int64_t)lane * ra.lda + pg[g]];
+        // the arm clamped to [0, NA) (the documented contract; an out-of-range byte must not index another row's
+        // or another wave's constants -- ADVICE r05)
+        const int8_t a8 = ra.arm8[(int64_t)lane * ra.lda + pg[g]];
+        const int8_t am = a8 < 0 ? (int8_t)0 : a8 >= NA ? (int8_t)(NA - 1) : a8;
         wA[lane * kCoopG + g] = am;
         if constexpr (kPipe) wO[lane * kCoopG + g] = (g * NA + am) * kCf5 * (int)sizeof(double);
       }
+    }
+    if constexpr (kPipe) {
+      // the pipelined scan's look-ahead reads offsets up to ~6 steps past the row's last step: steps [T, kStT) hold
+      // the row's own arm-0 offset (a valid table entry; the values read through it are never used)
+      for (int k = lane; k < kStT; k += kWave)
+        if (k >= ra.T) {
+#pragma unroll
+          for (int g = 0; g < kCoopG; ++g) wO[k * kCoopG + g] = g * NA * kCf5 * (int)sizeof(double);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
   }
   auto v_at = [&](int k) -> double { return STG ? wV[k * kCoopG + rs] : ra.V[(int64_t)k * ra.ldv + p]; };
-  auto a_at = [&](int k) -> int { return STG ? (int)wA[k * kCoopG + rs] : (int)ra.arm8[(int64_t)k * ra.lda + p]; };
+  auto a_at = [&](int k) -> int {  // (staged arms are clamped at staging; unstaged ones here)
+    if constexpr (STG) return (int)wA[k * kCoopG + rs];
+    const int a = (int)ra.arm8[(int64_t)k * ra.lda + p];
+    return a < 0 ? 0 : a >= NA ? NA - 1 : a;
+  };
   // coordinate i of a distributed vector: lane i % 8 of the group, slot i / 8
   auto gat = [&](const double (&v)[S], int i) -> double {
     return INSITE_REFINE_SWZ ? grp_lane(v[i / kCoopG], i % kCoopG) : __shfl(v[i / kCoopG], gbase + (i % kCoopG));

@@ -242,3 +242,63 @@ def test_lagged_stream_single_rank_matches_oracle(dev):
         y2 = ops.rollout(cohs[cc % 2].y0, cohs[cc % 2].u, bitss[cc % 2], torch.as_tensor(coef, device=dev), lib,
                          cohs[cc % 2].dt, method="rk4", T=t, layout="time_bits")
         assert torch.equal(yy, y2)
+
+
+def _ns_gram_job(job):
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    from oracle import insite_ref as Q
+    return Q.gram_moments_vectorized(*job)
+
+
+def test_deferred_step_north_star_1m_x_500_matches_oracle(dev):
+    """BASELINE.json north_star's configuration (1M patients x 500 steps, fp64) through the timed N = 1 kernel, as the
+    default bench line's ``north_star_step`` block runs it (cohort seed 1900 = bench.py --seed 1): the finalised model
+    against the oracle's SINDy fit of the WHOLE cohort (the oracle Gram in 32 patient chunks on a spawned pool, summed
+    in chunk order; G|b rtol 1e-10, support identical, coefficient L-inf < 1e-8 -- north_star's bar) and the rollout
+    the next launch writes with it against the oracle's RK4 scan on sampled rows (rtol 1e-10, RMSE < 1e-6)."""
+    import multiprocessing as mp
+    import os
+    from insite_amd import cohort, ops
+    Nn, Tn = 1_000_000, 500
+    coh = cohort.synthetic_pkpd(Nn, Tn, seed=1900, device=dev, equation="EQ_4_C", layout="time")
+    bits = cohort.counterfactual_arms(coh.arm, Tn, seed=1900, layout="time_bits")
+    lib = coh.lib
+    F = lib.n_terms
+    ws = ops.Workspace()
+    o = [_outs(dev, F) for _ in range(3)]
+    y = torch.empty((Tn, Nn), dtype=torch.float64, device=dev)
+    for k in range(3):
+        ops.fit_rollout_deferred(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, coh.y0, coh.u, bits,
+                                 o[(k - 1) % 3][0], coh.dt, k % 2, k > 0, ws, method="rk4", T=Tn, y_out=y,
+                                 out=o[k % 3] if k > 0 else o[2])
+    torch.cuda.synchronize()
+    u, arm = coh.u.cpu().numpy(), coh.arm.cpu().numpy().astype(np.int64)
+    exps = lib.exps.astype(np.int64)
+    bounds = [(int(c[0]), int(c[-1]) + 1) for c in np.array_split(np.arange(Nn), 32)]
+    jobs = [(coh.x[:, lo:hi].t().contiguous().cpu().numpy(), u[lo:hi], arm[lo:hi], Tn - 2, coh.dt, exps)
+            for lo, hi in bounds]
+    W = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS") or 8), os.cpu_count() or 1))
+    with mp.get_context("spawn").Pool(W) as pool:
+        parts = pool.map(_ns_gram_job, jobs)
+    del jobs
+    G, b = sum(q[0] for q in parts), sum(q[1] for q in parts)
+    cr = np.stack([R.stlsq_gram(G[a], b[a], 0.1, 0.5)[0] for a in range(2)])
+    for j in (1, 2):
+        coef, mask, iters, Gg, bg = (t.cpu().numpy() for t in o[j])
+        np.testing.assert_allclose(Gg, G, rtol=1e-10, atol=1e-6)
+        np.testing.assert_allclose(bg, b, rtol=1e-10, atol=1e-6)
+        assert np.array_equal(mask != 0, cr != 0)
+        assert np.max(np.abs(coef - cr)) < 1e-8
+    rng = np.random.default_rng(5)
+    idx = np.unique(np.concatenate([rng.choice(Nn, 3000, replace=False), np.arange(64), np.arange(Nn - 96, Nn)]))
+    it = torch.as_tensor(idx, device=dev)
+    words = bits.index_select(1, it // 32)
+    arms = ((words >> (it % 32).to(torch.int32)[None, :]) & 1).t().contiguous().cpu().numpy().astype(np.int64)
+    ref = R.rollout(coh.y0[it].cpu().numpy(), coh.u[it].cpu().numpy(), arms, cr, exps, coh.dt, method="rk4")
+    got = y.index_select(1, it).t().cpu().numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-10)
+    assert np.sqrt(np.mean((got - ref) ** 2)) < 1e-6

@@ -117,10 +117,14 @@ def _lagged_cohorts(dev):
     return cohs, bits
 
 
-def _lagged_worker(rank, world, port, q, delay=0):
+def _lagged_worker(rank, world, port, q, delay=0, sync=True):
     """One rank of the N > 1 C2 schedule (bench.py c2_lagged): its shard of two rotating cohorts, one
     insite_fit_rollout_lagged_f64 launch per step, the K-fit bucket all-reduced after the launches the
-    LaggedSchedule names (gloo here, RCCL in the bench)."""
+    LaggedSchedule names (gloo here, RCCL in the bench).  sync=False is the bench's own form: no host
+    synchronisation between launches -- the collectives are ordered only by the launch stream (an async all-reduce
+    reads the bucket after the launch that wrote it, and handle.wait() makes the launch stream wait for it), the
+    models and trajectories are cloned on the stream where the launches leave them and copied to the host only after
+    every pending handle has been waited for."""
     import sys
     for p in (ROOT, PKG):
         if p not in sys.path:
@@ -161,7 +165,8 @@ def _lagged_worker(rank, world, port, q, delay=0):
             p = sched.launch(k)
             if p["wait_before"] is not None:           # delay 1: the async all-reduce issued K launches ago
                 handles.pop(p["wait_before"]).wait()
-                torch.cuda.synchronize()
+                if sync:
+                    torch.cuda.synchronize()
             c = cohs[k % 2]
             red = (buckets[p["reduce"][1]].bufs[p["reduce"][2]].G, buckets[p["reduce"][1]].bufs[p["reduce"][2]].b) \
                 if p["reduce"] else (Gs, bs)
@@ -178,25 +183,32 @@ def _lagged_worker(rank, world, port, q, delay=0):
             ops.plan_fit_rollout_lagged(c.x, c.u, c.arm, c.rows, c.dt, lib, 0.1, 0.5, rcoh.y0, rcoh.u, rbits, coef_in,
                                         rcoh.dt, p["slot"], p["reduce"] is not None, ws, red, fit_in=fit_in,
                                         fit_out=fit_out, T=TL, y_out=yy)()
-            torch.cuda.synchronize()
+            if sync:
+                torch.cuda.synchronize()
             if p["allreduce_after"] is not None:
                 if delay:
                     handles[p["allreduce_after"]] = idist.reduce_bucket(buckets[p["allreduce_after"]], async_op=True)
                 else:
                     idist.reduce_bucket(buckets[p["allreduce_after"]])
-                    torch.cuda.synchronize()
-            if p["fit"]:
-                solved[p["fit"][0]] = ring[p["fit"][3]][0].cpu().numpy().copy()
+                    if sync:
+                        torch.cuda.synchronize()
+            if p["fit"]:     # stream-ordered clones (the ring / y buffers are reused by later launches)
+                solved[p["fit"][0]] = ring[p["fit"][3]][0].clone()
             if p["rollout"]:
-                rolled[p["rollout"][0] % 2] = (p["rollout"][0], yy.cpu().numpy().copy())
+                rolled[p["rollout"][0] % 2] = (p["rollout"][0], yy.clone())
+        for h in handles.values():                     # every outstanding collective before the results leave
+            h.wait()
+        torch.cuda.synchronize()
+        solved = {k: v.cpu().numpy() for k, v in solved.items()}
+        rolled = {k: (c, y.cpu().numpy()) for k, (c, y) in rolled.items()}
         q.put((rank, lo, hi, solved, rolled))
     finally:
         dist.barrier()
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("delay", [0, 1])
-def test_two_rank_lagged_stream_matches_oracle_and_single_rank_rollout(dev, delay):
+@pytest.mark.parametrize("delay,sync", [(0, True), (1, True), (1, False)])
+def test_two_rank_lagged_stream_matches_oracle_and_single_rank_rollout(dev, delay, sync):
     """The N > 1 form of the headline kernel (ABI 8 lagged step) with 2 ranks on one GPU: every model both ranks
     solve is bitwise the same on the two ranks and equals the oracle fit of the WHOLE cohort (support identical,
     L-inf < 1e-8); every rank's rollout of its shard is bitwise the single-process rollout of those patients with
@@ -214,7 +226,7 @@ def test_two_rank_lagged_stream_matches_oracle_and_single_rank_rollout(dev, dela
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_lagged_worker, args=(r, world, port, q, delay)) for r in range(world)]
+    procs = [ctx.Process(target=_lagged_worker, args=(r, world, port, q, delay, sync)) for r in range(world)]
     for p in procs:
         p.start()
     out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r[0])

@@ -575,3 +575,33 @@ def test_refine_rows_on_bench_cohort_sampled_against_oracle(dev):
     assert par["status_equal_frac"] >= 0.995 and par["iterations_equal_frac"] >= 0.995, par
     assert par["coef_linf"] <= 1e-7, par
     assert par["pred_rmse"] <= 1e-6, par
+
+
+def test_refine_rows_revert_mode_on_bench_cohort_sampled_against_oracle(dev):
+    """the literal status-3 revert of sindy.py:628-631 (``insite_revert_on_zoom_fail: true``) at the
+    INSITE line's bench size -- the line's own 1M-row cohort through the product call with the revert flag, ~4k sampled
+    rows against oracle/insite_refine_ref.refine_patient(revert_on_zoom_fail=True).  On every row whose status agrees
+    the predictions agree to the default mode's bar (RMSE <= 1e-6) and so do the coefficients; statuses agree on >= 99.5
+    % of the rows; on the few status-mismatch rows (the closed-form scans' rounding ending a search as converged where
+    the oracle's sub-step form ends it in a failed zoom, or the reverse) the side that reports status 3 holds exactly
+    c0 -- the difference there is the revert decision itself, not the refinement."""
+    import bench
+    from insite_amd import ops
+    coh, V, arm, sl, c0, dt = bench.insite_rows(1_000_000, 60, 1, dev)
+    plan = ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, revert_on_zoom_fail=True)
+    preds, coef, status, iters = plan()
+    torch.cuda.synchronize()
+    o = plan.order.long()
+    par = bench.insite_parity(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, preds, coef, status, iters,
+                              extra=(o[:64].cpu().numpy(), o[-64:].cpu().numpy()), revert=True)
+    print(par)
+    assert par["rows_sampled"] >= 4096
+    assert par["status_equal_frac"] >= 0.995, par
+    assert par["coef_linf_status_equal"] <= 1e-7, par
+    assert par["pred_rmse_status_equal"] <= 1e-6, par
+    assert par["mismatch_reverted_side_is_c0"], par
+    # statuses 3 on the GPU side keep c0 exactly over the whole cohort
+    s3 = (status == 3).nonzero().flatten()
+    if s3.numel():
+        c0t = torch.as_tensor(np.asarray(c0, dtype=np.float64), device=dev)
+        assert torch.equal(coef.index_select(0, s3), c0t.expand(s3.numel(), *c0t.shape))

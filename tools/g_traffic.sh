@@ -11,7 +11,7 @@ for spec in "${SPECS[@]}"; do
   name=${spec%%:*}; argsx=${spec#*:}
   for C in FETCH_SIZE WRITE_SIZE; do
     d=$O/pmc/$name/$( [ $C = FETCH_SIZE ] && echo fetch || echo write )
-    timeout -s KILL ${PMC_LIMIT:-150} rocprofv3 --pmc $C -d $d -o run --output-format csv -- python3 bench.py $argsx --no-cpu-baseline --steps 5 --warmup 2 > $O/${name}_$C.log 2>&1 || { echo "pmc $name $C failed"; tail -5 $O/${name}_$C.log; exit 1; }
+    timeout -s KILL ${PMC_LIMIT:-150} rocprofv3 --pmc $C -d $d -o run --output-format csv -- python3 bench.py $argsx --no-cpu-baseline --no-parity --steps 5 --warmup 2 > $O/${name}_$C.log 2>&1 || { echo "pmc $name $C failed"; tail -5 $O/${name}_$C.log; exit 1; }
   done
   echo "pmc $name ok"
 done
