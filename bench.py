@@ -1188,7 +1188,7 @@ def insite_main(args):
     kbytes = N * T * (8 + 1 + 8) + N * (8 * 2 + 4 + 4) + N * (2 * coh.lib.n_terms * 8 + 8)
     out = {
         "metric": METRIC, "value": N / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": 1,
-        "steps": steps, "warmup": warmup, "ms_per_step": ms_step, "higher_is_better": True,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: on-device EQ_4_C cohort, T=60, seq_len U{1..59}, arm flip at a random step",
         "config": {"workload": f"INSITE refinement (BFGS per row, tau=5, lam=10) + Euler-5 rollout, "
@@ -1517,7 +1517,7 @@ def f4_main(args):
     achieved = gb / (gram_ms * 1e-3) / 1e9
     res = {
         "metric": METRIC, "value": N / (ms_step * 1e-3), "unit": "patient-trajectories/s", "n_gpus": 1,
-        "steps": steps, "warmup": warmup, "ms_per_step": ms_step, "higher_is_better": True,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: on-device 4-arm cohort (planted per-arm model, Markov arms p=0.1, Euler-5 truth + 0.01 noise)",
         "config": {"workload": f"F4: cancer_sim/EQ_5 path, {N // 1000}k patients x {T} steps, 4 arms: segment-split "
@@ -1787,6 +1787,7 @@ def dist_setup(force_group: bool = False):
 
 TRAFFIC_R04 = os.path.join(ROOT, "profiles", "traffic_r04.json")
 TRAFFIC_R05 = os.path.join(ROOT, "profiles", "traffic_r05.json")
+TRAFFIC_R06 = os.path.join(ROOT, "profiles", "traffic_r06.json")
 
 
 def traffic_for(config, kernel, grid=None, args=None):
@@ -1808,7 +1809,7 @@ def traffic_for(config, kernel, grid=None, args=None):
             return None
     # this round's table first (taken on the kernels as they are now), the previous round's for configs it lacks
     hits = []
-    for path in (TRAFFIC_R05, TRAFFIC_R04):
+    for path in (TRAFFIC_R06, TRAFFIC_R05, TRAFFIC_R04):
         try:
             with open(path) as f:
                 tab = json.load(f).get(config, {})
@@ -1869,7 +1870,7 @@ def c5_traffic_calibrated(args):
     except Exception:
         return None
     hits = []
-    for path in (TRAFFIC_R05, TRAFFIC_R04):
+    for path in (TRAFFIC_R06, TRAFFIC_R05, TRAFFIC_R04):
         try:
             with open(path) as f:
                 tab = json.load(f).get("c5", {})

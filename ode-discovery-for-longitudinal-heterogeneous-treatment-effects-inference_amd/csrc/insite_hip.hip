@@ -405,6 +405,88 @@ __device__ void deferred_finalize(const double* __restrict__ part, const int nbl
 static_assert(kTailMaxEnt + 8 + INSITE_MAX_ARMS * (INSITE_MAX_TERMS * INSITE_MAX_TERMS + INSITE_MAX_TERMS) +
                       kTailMaxEnt <= kWavesPerBlock * kWave * kGSlot,
               "deferred_finalize holds at least one group's sums in the gram kernel's LDS array");
+
+// ---- Dynamic gram tail (INSITE_DEF_DYN): the deferred step's gram waves stream a static share
+// of the tiles as before (one contiguous range per wave, block partials), then CLAIM fixed pieces of the remaining
+// tail tiles -- (tile, range of kGT-step groups), never crossing a tile -- from per-XCD heads, each piece's Gram
+// contribution stored in a partial slot of its own, indexed by PIECE, not by wave.  The next launch's finaliser sums
+// the block partials and then the piece partials in one fixed order (dyn_finalize), so G|b do not depend on which
+// wave took which piece.  Claims are agent-scope fetch-adds on one 128-B line per XCD (a wave claims from the head
+// of the XCD its block runs on -- blockIdx % 8 under the dispatcher's round robin; speed only, correctness does not
+// depend on placement -- and moves on to the other heads when its own is exhausted); the next piece is claimed while
+// the current one streams.  The last wave to finish claiming (a 64-bit done word: waves << 32 | pieces) stores the
+// number of pieces processed into the slot record and resets the claim area, so every launch leaves it zero, and the
+// finaliser flags a slot whose pieces do not add up (NaN, iters -3) instead of summing it.
+struct DynGram {
+  unsigned* claim;   // kXcds head lines + one done line (kClaimWords words each); zero between launches
+  double* ppart;     // piece partials [P][n_ent] (after the block partials of the slot)
+  unsigned* hdr;     // the slot header (record word kSlotRec + 4: pieces processed)
+  int64_t tile0;     // tiles [0, tile0) static, [tile0, n_tiles) claimed
+  int64_t P;         // pieces: (n_tiles - tile0) * ppt
+  int32_t pg;        // kGT-step groups per piece
+  int32_t ppt;       // pieces per tail tile
+  int32_t waves;     // gram waves taking part (the done count)
+};
+constexpr int kClaimWords = 32;  // one 128-B line per head
+constexpr int kDynRecDone = 116;  // slot-header words (after the slot record, kSlotRec = 112 .. 115): pieces processed
+constexpr int kDynRecP = 117;     //   and pieces streamed (the finaliser checks they agree)
+constexpr int kDynHeads = 8;
+constexpr size_t kDynClaimBytes = (size_t)(kDynHeads + 1) * kClaimWords * sizeof(unsigned);
+
+// The fixed-order finalisation of the dynamic gram's slot: rows = block partials then piece partials, [R][n_ent].
+// 256 threads take (row group, entry pair): the rows are cut into NGR contiguous row groups, each summed in row order
+// with 16-B loads and kDynUnroll of them in flight per thread (the slot is ~1 MB at C2's shape, so one block needs
+// ~100 KB in flight to read it in ~15 us beside the streaming), then the NGR group sums in group order.
+constexpr int kDynUnroll = 16;
+template <int STF>
+__device__ void dyn_finalize(const double* __restrict__ part, const int R, const int n_ent, const LibDesc& lib,
+                             const GramOut& o, double* red) {
+  constexpr int kOff = kTailMaxEnt + 8 + INSITE_MAX_ARMS * (INSITE_MAX_TERMS * INSITE_MAX_TERMS + INSITE_MAX_TERMS);
+  const int npair = (n_ent + 1) / 2;
+  const int ngr = kBlock / npair;  // >= 1 (n_ent <= kTailMaxEnt <= 2 * kBlock)
+  double* gsum = red + kOff;       // [ngr][2 * npair]
+  const int t = (int)threadIdx.x;
+  if (t < ngr * npair) {
+    const int gq = t / npair, pp = t - gq * npair;
+    const int r0 = (int)((int64_t)gq * R / ngr), r1 = (int)((int64_t)(gq + 1) * R / ngr);
+    double ax = 0.0, ay = 0.0;
+    const bool odd_last = 2 * pp + 1 >= n_ent;  // (n_ent odd: the last pair's second entry does not exist)
+    for (int r = r0; r < r1; r += kDynUnroll) {
+      double vx[kDynUnroll], vy[kDynUnroll];
+#pragma unroll
+      for (int j = 0; j < kDynUnroll; ++j) {
+        const int rr = r + j < r1 ? r + j : r0;
+        const double* q = part + (int64_t)rr * n_ent + 2 * pp;
+        if ((n_ent & 1) == 0) {
+          const double2 v = *reinterpret_cast<const double2*>(q);
+          vx[j] = v.x;
+          vy[j] = v.y;
+        } else {
+          vx[j] = q[0];
+          vy[j] = odd_last ? 0.0 : q[1];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kDynUnroll; ++j) {
+        ax += r + j < r1 ? vx[j] : 0.0;
+        ay += r + j < r1 ? vy[j] : 0.0;
+      }
+    }
+    gsum[gq * 2 * npair + 2 * pp] = ax;
+    gsum[gq * 2 * npair + 2 * pp + 1] = ay;
+  }
+  __syncthreads();
+  for (int q = t; q < n_ent; q += kBlock) {
+    double acc = 0.0;
+    for (int g = 0; g < ngr; ++g) acc += gsum[g * 2 * npair + q];
+    red[q] = acc;
+  }
+  __syncthreads();
+  tail_finish<STF>(red, n_ent, lib, o);
+}
+static_assert(kTailMaxEnt + 8 + INSITE_MAX_ARMS * (INSITE_MAX_TERMS * INSITE_MAX_TERMS + INSITE_MAX_TERMS) +
+                      2 * kBlock + 64 <= kWavesPerBlock * kWave * kGSlot,
+              "dyn_finalize's group sums fit the gram kernel's LDS array");
 static_assert(kTailMaxEnt + 8 + INSITE_MAX_ARMS * (INSITE_MAX_TERMS * INSITE_MAX_TERMS + INSITE_MAX_TERMS) <=
                   kWavesPerBlock * kWave * kGSlot,
               "tail scratch fits the gram kernel's LDS array");
@@ -446,12 +528,41 @@ __device__ __forceinline__ int64_t gram_item_tile(int64_t item, int n_seg, int64
 __device__ __forceinline__ int gram_item_seg(int64_t item, int n_seg, int64_t n_tiles) {
   return INSITE_GRAM_ORDER ? (int)(item / n_tiles) : (int)(item - (item / n_seg) * n_seg);
 }
-template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, int MOM, int STF = 0>
+// The block's partial (fixed order: wave 0..3 per entry) -> compact partial[block][a * nE + e], write-through.
+template <bool MFMA, int NARM>
+__device__ __forceinline__ void gram_block_partial(const int vblk, double* __restrict__ smem, const LibDesc& lib,
+                                                   const GramOut& out, double* __restrict__ partial, const dbl4& cacc,
+                                                   const double (&acc)[NARM], const int wid, const int lane) {
+  __syncthreads();
+  double* red = smem;
+  const int n_ent = out.n_arms * lib.nE;  // the Gram entries the tail needs (<= kTailMaxEnt)
+  if constexpr (MFMA) {
+    // canonical C[row][col], row = (lane >> 4) + 4 j, col = lane & 15
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[wid * 256 + ((lane >> 4) + 4 * j) * 16 + (lane & 15)] = cacc[j];
+  } else {
+#pragma unroll
+    for (int a = 0; a < NARM; ++a) red[(wid * NARM + a) * kWave + lane] = acc[a];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < n_ent; idx += kBlock) {
+    const int a = idx / lib.nE, e = idx - a * lib.nE;
+    const int q = MFMA ? (a * lib.F + lib.ei[e]) * 16 + lib.qcol[e] : a * kWave + e;
+    constexpr int stride = MFMA ? 256 : NARM * kWave;
+    double v = red[q];
+#pragma unroll
+    for (int ww = 1; ww < kWavesPerBlock; ++ww) v += red[ww * stride + q];
+    tail_store(partial + (int64_t)vblk * n_ent + idx, v);
+  }
+}
+
+template <int VEC, int NARM, bool SMOOTH, bool MFMA, bool TM, int MOM, int STF = 0, int DYN = 0>
 __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, double* __restrict__ smem,
             const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
             const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, int seg, int n_seg,
             const GramW& w, const LibDesc& lib, double* __restrict__ partial, unsigned* __restrict__ cnt,
-            const GramOut& out) {
+            const GramOut& out, const DynGram* __restrict__ dgp = nullptr) {
+  static_assert(!DYN || (TM && MFMA && MOM == 0), "the claimed gram tail is the deferred step's (time-major, MFMA)");
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform (SGPR)
   double* xt = smem + wid * (kWave * kGSlot);
@@ -496,7 +607,9 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
   const int64_t nW = (int64_t)vgrid * kWavesPerBlock;
   const int64_t wv = (int64_t)vblk * kWavesPerBlock + wid;
   const int64_t units = ranged ? n_tiles * ng : n_tiles * n_seg;
-  const int64_t c_end = ranged ? (wv + 1) * units / nW : units;
+  // DYN: only the tiles [0, tile0) are cut into static ranges; the rest is claimed piece by piece
+  const int64_t units_s = (DYN && ranged) ? dgp->tile0 * ng : units;
+  const int64_t c_end = ranged ? (wv + 1) * units_s / nW : units;
   struct Piece {
     int64_t tile, next;
     int s0, sE;
@@ -536,9 +649,88 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
       v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, qoff + (unsigned)(i * ldx * 8), 0,
                                                                              INSITE_GRAM_LOAD_AUX));
   };
-  for (int64_t cur = ranged ? wv * units / nW : wv; cur < c_end;) {
-    const Piece pc = piece_of(cur);
-    cur = pc.next;
+  // ---- DYN state: claims are fetch-adds by lane 0 on the head of kDynHeads it is on; the piece index is read
+  // (readfirstlane) only at wave-uniform points ----
+  int64_t dq = -1, dnext = -1;        // the claimed piece being processed / the next one (once read)
+  bool dnext_ok = false, dinfl = false, dexh = !DYN || dgp->P <= 0;
+  int dphase = 0, dh = (int)(blockIdx.x % kDynHeads), dtried = 0;
+  unsigned dcl = 0u, dmine = 0u;
+  auto dyn_issue = [&]() {
+    if constexpr (DYN) {
+      if (lane == 0) dcl = __hip_atomic_fetch_add(dgp->claim + dh * kClaimWords, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      dinfl = true;
+    }
+  };
+  auto dyn_read = [&]() -> int64_t {  // the in-flight claim's piece, moving on to the other heads when exhausted
+    if constexpr (DYN) {
+      for (;;) {
+        const int64_t idx = (int64_t)__builtin_amdgcn_readfirstlane(dcl);
+        const int64_t lo = dh * dgp->P / kDynHeads, hi = (dh + 1) * dgp->P / kDynHeads;
+        dinfl = false;
+        if (lo + idx < hi) return lo + idx;
+        if (++dtried >= kDynHeads) {
+          dexh = true;
+          return -1;
+        }
+        dh = (dh + 1) % kDynHeads;
+        dyn_issue();
+      }
+    }
+    return -1;
+  };
+  auto dyn_piece = [&](int64_t q) -> Piece {
+    Piece pc;
+    const int64_t tt = q / dgp->ppt;
+    const int j = (int)(q - tt * dgp->ppt);
+    pc.tile = dgp->tile0 + tt;
+    pc.s0 = j * dgp->pg * kGT;
+    pc.sE = min(ng, (j + 1) * dgp->pg) * kGT;
+    pc.next = 0;
+    return pc;
+  };
+  int64_t cur = ranged ? wv * units_s / nW : wv;
+  for (;;) {
+    Piece pc;
+    if (cur < c_end) {
+      pc = piece_of(cur);
+      cur = pc.next;
+      if constexpr (DYN)  // the last static piece: the first claim in flight while it streams
+        if (!(cur < c_end) && !dexh) dyn_issue();
+    } else {
+      if constexpr (!DYN) {
+        break;
+      } else {
+        if (dphase == 0) {  // every static range done: this block's partial (a block barrier), then claimed pieces
+          gram_block_partial<MFMA, NARM>(vblk, smem, lib, out, partial, cacc, acc, wid, lane);
+          __syncthreads();  // (the block's LDS is the waves' staging area again from here)
+          cacc = {0.0, 0.0, 0.0, 0.0};
+          dphase = 1;
+        } else {  // the previous claimed piece's contribution -> its own slot (wave-local, no barrier)
+          wave_lds_sync();
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xt[((lane >> 4) + 4 * j) * 16 + (lane & 15)] = cacc[j];
+          wave_lds_sync();
+          const int n_ent = out.n_arms * lib.nE;
+          for (int idx = lane; idx < n_ent; idx += kWave) {
+            const int a = idx / lib.nE, e = idx - a * lib.nE;
+            dgp->ppart[dq * n_ent + idx] = xt[(a * lib.F + lib.ei[e]) * 16 + lib.qcol[e]];
+          }
+          wave_lds_sync();
+          cacc = {0.0, 0.0, 0.0, 0.0};
+        }
+        if (!dnext_ok) {
+          if (!dinfl && !dexh) dyn_issue();
+          dnext = dinfl ? dyn_read() : -1;
+        }
+        dnext_ok = false;
+        dq = dnext;
+        if (dq < 0) break;
+        ++dmine;
+        pc = dyn_piece(dq);
+        if (!dexh) dyn_issue();  // the next claim in flight while this piece streams
+      }
+    }
     const int64_t tile = pc.tile;
     const int64_t p0 = tile * kWave;
     const int64_t p = p0 + lane;
@@ -785,8 +977,19 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
         }
 #ifndef INSITE_GRAM_NO_XPREFETCH
         {  // every tile of this item consumed: request the wave's next item's first tiles
-          if (cur < c_end) {  // uniform
-            const Piece np = piece_of(cur);
+          bool have = cur < c_end;  // uniform
+          Piece np;
+          if (have) {
+            np = piece_of(cur);
+          } else if constexpr (DYN) {
+            if (dinfl) {  // the claim issued when this piece started: read it here, where only the tail loads are left
+              dnext = dyn_read();
+              dnext_ok = true;
+              have = dnext >= 0;
+              if (have) np = dyn_piece(dnext);
+            }
+          }
+          if (have) {
             const int64_t np0 = np.tile * kWave;
             const int ntb = np.s0 == 0 ? 0 : np.s0 - kWarm;
             const int ns1p = min(np.sE, n_steps);
@@ -950,29 +1153,25 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
   INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 5);
   // ---- block reduction (fixed order) -> compact partial[block][a * nE + e] -> gram_tail ----
   if constexpr (MOM == 1) return;
-  __syncthreads();
-  double* red = smem;
-  const int n_ent = out.n_arms * lib.nE;  // the Gram entries the tail needs (<= kTailMaxEnt)
-  if constexpr (MFMA) {
-    // canonical C[row][col], row = (lane >> 4) + 4 j, col = lane & 15
+  if constexpr (DYN) {  // (the block partial was taken at the static -> claimed transition; dq < 0: all heads dry)
+    if (lane == 0) {
+      unsigned long long* dw = reinterpret_cast<unsigned long long*>(dgp->claim + kDynHeads * kClaimWords);
+      const unsigned long long old = __hip_atomic_fetch_add(dw, (1ull << 32) | (unsigned long long)dmine,
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((unsigned)(old >> 32) == (unsigned)dgp->waves - 1u) {  // the last wave: every claim has returned
+        __hip_atomic_store(dgp->hdr + kDynRecDone, (unsigned)old + dmine, __ATOMIC_RELAXED,  // pieces processed,
+                           __HIP_MEMORY_SCOPE_AGENT);                                // for the finaliser's check
 #pragma unroll
-    for (int j = 0; j < 4; ++j) red[wid * 256 + ((lane >> 4) + 4 * j) * 16 + (lane & 15)] = cacc[j];
-  } else {
-#pragma unroll
-    for (int a = 0; a < NARM; ++a) red[(wid * NARM + a) * kWave + lane] = acc[a];
+        for (int h = 0; h < kDynHeads; ++h)
+          __hip_atomic_store(dgp->claim + h * kClaimWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    return;
   }
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < n_ent; idx += kBlock) {
-    const int a = idx / lib.nE, e = idx - a * lib.nE;
-    const int q = MFMA ? (a * lib.F + lib.ei[e]) * 16 + lib.qcol[e] : a * kWave + e;
-    constexpr int stride = MFMA ? 256 : NARM * kWave;
-    double v = red[q];
-#pragma unroll
-    for (int ww = 1; ww < kWavesPerBlock; ++ww) v += red[ww * stride + q];
-    tail_store(partial + (int64_t)vblk * n_ent + idx, v);
-  }
+  gram_block_partial<MFMA, NARM>(vblk, smem, lib, out, partial, cacc, acc, wid, lane);
   INSITE_TSTAMP(blockIdx.x * kWavesPerBlock + wid, 6);
-  if (cnt) gram_tail<STF>(vblk, vgrid, partial, n_ent, cnt, lib, out, smem);  // null: the deferred step's partials
+  if (cnt) gram_tail<STF>(vblk, vgrid, partial, out.n_arms * lib.nE, cnt, lib, out, smem);  // null: the deferred step's
   INSITE_TREAL(blockIdx.x * kWavesPerBlock + wid, 9);
 }
 
@@ -2510,6 +2709,24 @@ step_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
 #ifndef INSITE_DEF_GPRIO
 #define INSITE_DEF_GPRIO 0
 #endif
+// INSITE_DEF_DYN: the claimed gram tail (DynGram) -- 0 never, 1 always, 2 (default) by size: a launch takes the claimed
+// instantiation when its gram waves stream at least INSITE_DEF_DYN_MIN (tile, kGT-step group) units each.  Measured
+// (profiles/r06/dyn/): at the north-star 1M x 500 (488 units a wave) the claimed tail is 9 % faster; at C2's 100k x 200
+// (20 units a wave) 20-35 % slower -- the per-piece warm-ups, contractions and partial stores and the finaliser's
+// ~1 MB of piece partials (one block, latency-bound beside the streaming) cost more than the ~10 us of spread they
+// recover.  INSITE_DEF_DYN_TAIL: per mille of the tiles claimed; INSITE_DEF_DYN_PG: kGT-step groups per piece.
+#ifndef INSITE_DEF_DYN
+#define INSITE_DEF_DYN 2
+#endif
+#ifndef INSITE_DEF_DYN_MIN
+#define INSITE_DEF_DYN_MIN 128
+#endif
+#ifndef INSITE_DEF_DYN_TAIL
+#define INSITE_DEF_DYN_TAIL 250
+#endif
+#ifndef INSITE_DEF_DYN_PG
+#define INSITE_DEF_DYN_PG 2
+#endif
 // Each slot's header records what its partials are: the launch that streams a slot writes
 // {magic, gram blocks, entries} there, and the finalisation sums exactly the recorded number of partials, so a
 // caller that changes the method / fd between calls (and with them the default block split) still gets the
@@ -2517,6 +2734,7 @@ step_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
 constexpr int kSlotRec = 112;  // unsigned index into the slot's 512-B header (counters use [0, 98))
 constexpr unsigned kSlotMagic = 0x1E5D0A7Eu;
 static_assert((kSlotRec + 4) * sizeof(unsigned) <= 512, "slot record inside the workspace header");
+static_assert(kDynRecDone >= kSlotRec + 4 && (kDynRecP + 1) * sizeof(unsigned) <= 512, "DYN record words in the header");
 // The slot record's 4th word: a fingerprint of the streamed system (FNV-1a over the library's column codes, F, the
 // statics count and the arm count), so a slot streamed for another system of the same shape (same F and arm
 // count, other exponents or statics) is flagged at finalisation like an unstreamed one.  The derivative kind,
@@ -2614,6 +2832,11 @@ __device__ __forceinline__ int64_t xcd_count(int64_t n, int x) { return (n + kXc
 #endif
 constexpr int kClaimLineWords = 32;                      // one 128-B line per head (head word 0, done word 1)
 constexpr size_t kDefClaimBytes = (size_t)kXcds * kClaimLineWords * sizeof(unsigned);
+// The deferred step's workspace: [claim area, kDefAreaBytes][slot 0][slot 1].  The claim area (the claimed rollout
+// tail's or the claimed gram tail's heads) sits at offset 0 so that its place does not move with the cohort size
+// (a grow-only workspace reused for another N left the heads on stale partial bytes).
+constexpr size_t kDefAreaBytes = 2048;
+static_assert(kDefClaimBytes <= kDefAreaBytes && kDynClaimBytes <= kDefAreaBytes, "claim areas fit the header area");
 // rank of block b among the blocks [lo, hi) ordered XCD-major (by b % kXcds, then b)
 __device__ __forceinline__ int64_t xcd_rank(int64_t b, int64_t lo, int64_t hi) {
   const int x = (int)(b % kXcds);
@@ -2630,14 +2853,14 @@ __device__ __forceinline__ int64_t xcd_rank(int64_t b, int64_t lo, int64_t hi) {
 #ifndef INSITE_LAG_MERGED
 #define INSITE_LAG_MERGED 1
 #endif
-template <bool SMOOTH, int METHOD>
+template <bool SMOOTH, int METHOD, int DYN = 0>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_STEP_WPE)))
 step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
                      const int8_t* __restrict__ arm, const int32_t* __restrict__ rows, int64_t N, GramW w, LibDesc lib,
                      double* __restrict__ part_cur, const double* __restrict__ part_prev, GramOut out, RolloutArgs ra,
                      int gblocks, unsigned* __restrict__ rc, unsigned* __restrict__ hdr_cur,
                      const unsigned* __restrict__ hdr_prev, int lagged, const double* __restrict__ G_fit,
-                     const double* __restrict__ b_fit, GramOut fit, unsigned fprint) {
+                     const double* __restrict__ b_fit, GramOut fit, unsigned fprint, DynGram dg) {
   __shared__ double smem[kGramSmem];
   const int n_ent = out.n_arms * lib.nE;
   if ((int)blockIdx.x < gblocks) {
@@ -2646,21 +2869,33 @@ step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, con
       hdr_cur[kSlotRec + 1] = (unsigned)gblocks;
       hdr_cur[kSlotRec + 2] = (unsigned)n_ent;
       hdr_cur[kSlotRec + 3] = fprint;
+      // the slot's format for the next finalisation: P claimed pieces after the block partials (0: static), and the
+      // processed count the last claiming wave stores at the end -- a sentinel until then (agent-scope stores, ordered
+      // at the memory side: the same word is written from another XCD at the end of the launch)
+      __hip_atomic_store(hdr_cur + kDynRecP, DYN ? (unsigned)dg.P : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (DYN) __hip_atomic_store(hdr_cur + kDynRecDone, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (INSITE_DEF_GPRIO) __builtin_amdgcn_s_setprio(INSITE_DEF_GPRIO);
-    gram_body<1, 2, SMOOTH, true, true, 0, 7>((int)blockIdx.x, gblocks, smem, x, ldx, n_steps, u, arm, rows, N, 0, 0,
-                                                 w, lib, part_cur, nullptr, out);
+    gram_body<1, 2, SMOOTH, true, true, 0, 7, DYN>((int)blockIdx.x, gblocks, smem, x, ldx, n_steps, u, arm,
+                                                              rows, N, 0, 0, w, lib, part_cur, nullptr, out, &dg);
     return;
   }
   if ((int)blockIdx.x == gblocks) {
     if (part_prev) {
       INSITE_TREAL(49152, 8);
       const unsigned mg = hdr_prev[kSlotRec], nb = hdr_prev[kSlotRec + 1], ne = hdr_prev[kSlotRec + 2];
-      const bool ok = mg == kSlotMagic && ne == (unsigned)n_ent && nb >= 1u && nb <= (unsigned)kGramMaxBlocks &&
-                      hdr_prev[kSlotRec + 3] == fprint;
+      bool ok = mg == kSlotMagic && ne == (unsigned)n_ent && nb >= 1u && nb <= (unsigned)kGramMaxBlocks &&
+                hdr_prev[kSlotRec + 3] == fprint;
+      // a slot streamed with the claimed tail: every claimed piece processed (rows = its block partials + its piece
+      // partials, summed by dyn_finalize); a static slot (P = 0): the block partials (deferred_finalize)
+      const unsigned np = hdr_prev[kDynRecP];
+      if (np > 0u) ok = ok && hdr_prev[kDynRecDone] == np;
       if (!ok) {
         if (lagged) finalize_invalid<0>(lib, out);
         else finalize_invalid<7>(lib, out);
+      } else if (np > 0u) {
+        if (lagged) dyn_finalize<0>(part_prev, (int)(nb + np), n_ent, lib, out, smem);
+        else dyn_finalize<7>(part_prev, (int)(nb + np), n_ent, lib, out, smem);
       } else if (lagged) {
         deferred_finalize<0>(part_prev, (int)nb, n_ent, lib, out, smem);
       } else {
@@ -4131,7 +4366,7 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
       if (exps[j * (1 + n_statics)] > INSITE_MAX_STATE_DEGREE) return INSITE_E_UNSUPPORTED;
   }
   const size_t ws_one = insite_gram_workspace_bytes(n_patients, n_arms, n_terms);
-  if (!workspace || workspace_bytes < (deferred ? 2 * ws_one + kDefClaimBytes : ws_one)) return INSITE_E_WORKSPACE;
+  if (!workspace || workspace_bytes < (deferred ? 2 * ws_one + kDefAreaBytes : ws_one)) return INSITE_E_WORKSPACE;
   if (deferred && (slot < 0 || slot > 1 || finalize_prev < 0 || finalize_prev > 1)) return INSITE_E_INVALID_ARG;
   if (lagged && ((G_fit == nullptr) != (b_fit == nullptr))) return INSITE_E_INVALID_ARG;
   if (ldx > ((int64_t)1 << 31) / (8 * kGT)) return INSITE_E_UNSUPPORTED;
@@ -4167,23 +4402,36 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
   const bool smooth = fd_kind == INSITE_FD_SMOOTHED4;
   if (n_statics == 0) u = x ? x : G_out;
   if (deferred) {
-    auto kd = smooth ? (method == INSITE_METHOD_RK4 ? step_deferred_kernel<true, INSITE_METHOD_RK4>
-                                                    : step_deferred_kernel<true, INSITE_METHOD_EULER>)
-                     : (method == INSITE_METHOD_RK4 ? step_deferred_kernel<false, INSITE_METHOD_RK4>
-                                                    : step_deferred_kernel<false, INSITE_METHOD_EULER>);
+    auto pick = [&](auto k_t_rk4, auto k_t_eu, auto k_f_rk4, auto k_f_eu) {
+      return smooth ? (method == INSITE_METHOD_RK4 ? k_t_rk4 : k_t_eu) : (method == INSITE_METHOD_RK4 ? k_f_rk4 : k_f_eu);
+    };
+    auto kd0 = pick(step_deferred_kernel<true, INSITE_METHOD_RK4, 0>, step_deferred_kernel<true, INSITE_METHOD_EULER, 0>,
+                    step_deferred_kernel<false, INSITE_METHOD_RK4, 0>, step_deferred_kernel<false, INSITE_METHOD_EULER, 0>);
+    auto kd1 = pick(step_deferred_kernel<true, INSITE_METHOD_RK4, 1>, step_deferred_kernel<true, INSITE_METHOD_EULER, 1>,
+                    step_deferred_kernel<false, INSITE_METHOD_RK4, 1>, step_deferred_kernel<false, INSITE_METHOD_EULER, 1>);
     const int nfin = lagged && !INSITE_LAG_MERGED ? 2 : 1;  // finalisation blocks (the reduction [+ the STLSQ])
-    int grid = resident_waves(kd) / kWavesPerBlock;
-    if (grid < 2 + nfin) grid = 2 + nfin;
     // half the resident blocks stream the gram (blocks b and b + grid/2 share a CU), nfin finalise, the rest roll out
-    int gb = gram_blocks > 0 ? gram_blocks : grid / 2;
-    if (gb > grid - 1 - nfin) gb = grid - 1 - nfin;
-    if (gb > kGramMaxBlocks) gb = kGramMaxBlocks;
+    auto split = [&](auto k, int& grid_, int& gb_) {
+      grid_ = resident_waves(k) / kWavesPerBlock;
+      if (grid_ < 2 + nfin) grid_ = 2 + nfin;
+      gb_ = gram_blocks > 0 ? gram_blocks : grid_ / 2;
+      if (gb_ > grid_ - 1 - nfin) gb_ = grid_ - 1 - nfin;
+      if (gb_ > kGramMaxBlocks) gb_ = kGramMaxBlocks;
+    };
+    int grid = 0, gb = 0;
+    split(kd0, grid, gb);
+    // the claimed gram tail (INSITE_DEF_DYN) where the gram waves' ranges are long enough to pay for it
+    const int64_t units_all = (n_patients + kWave - 1) / kWave * ((n_steps + kGT - 1) / kGT);
+    const bool dyn = n_patients > 0 && (INSITE_DEF_DYN == 1 ||
+                                        (INSITE_DEF_DYN == 2 && units_all >= (int64_t)INSITE_DEF_DYN_MIN * gb * kWavesPerBlock));
+    if (dyn) split(kd1, grid, gb);
     char* wsb = static_cast<char*>(workspace);
-    double* part_cur = reinterpret_cast<double*>(wsb + (size_t)slot * ws_one + kGramWsHeader);
+    char* slots = wsb + kDefAreaBytes;
+    double* part_cur = reinterpret_cast<double*>(slots + (size_t)slot * ws_one + kGramWsHeader);
     const double* part_prev =
-        finalize_prev ? reinterpret_cast<const double*>(wsb + (size_t)(1 - slot) * ws_one + kGramWsHeader) : nullptr;
-    unsigned* hdr_cur = reinterpret_cast<unsigned*>(wsb + (size_t)slot * ws_one);
-    const unsigned* hdr_prev = reinterpret_cast<const unsigned*>(wsb + (size_t)(1 - slot) * ws_one);
+        finalize_prev ? reinterpret_cast<const double*>(slots + (size_t)(1 - slot) * ws_one + kGramWsHeader) : nullptr;
+    unsigned* hdr_cur = reinterpret_cast<unsigned*>(slots + (size_t)slot * ws_one);
+    const unsigned* hdr_prev = reinterpret_cast<const unsigned*>(slots + (size_t)(1 - slot) * ws_one);
     // lagged: `go` reduces only (G|b out, no STLSQ); `gf` solves the all-reduced G_fit|b_fit into coef/mask/iters
     const GramOut gred{G_out, b_out, n_arms, nullptr, nullptr, nullptr, sp};
     const GramOut gf{nullptr, nullptr, n_arms, coef_out, mask_out, iters_out, sp};
@@ -4193,14 +4441,40 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
       rows = reinterpret_cast<const int32_t*>(G_out);
       u = G_out;
     }
-    // the claim area after the two slots (used by the claimed-tail build only).  Its offset depends on the cohort
-    // size, so a grow-only workspace reused for another N would put the heads on stale partial bytes: the claimed
-    // build zeroes it before every launch (the default build never touches it)
-    unsigned* rc = INSITE_DEF_RSTATIC < 1000 ? reinterpret_cast<unsigned*>(wsb + 2 * ws_one) : nullptr;
+    // the claim area at offset 0 (the claimed rollout tail's, INSITE_DEF_RSTATIC < 1000, a knob build: zeroed before
+    // every launch, since the chunks its heads skip would otherwise go unrolled silently)
+    unsigned* rc = INSITE_DEF_RSTATIC < 1000 ? reinterpret_cast<unsigned*>(wsb) : nullptr;
     if (rc && hipMemsetAsync(rc, 0, kDefClaimBytes, hs) != hipSuccess) return INSITE_E_HIP;
+    // the claimed gram tail (INSITE_DEF_DYN): its heads in the same area, self-resetting; a stale area shows up as a
+    // piece count that does not add up, which the next finalisation flags (NaN G|b, iters -3)
+    DynGram dg{reinterpret_cast<unsigned*>(wsb), nullptr, hdr_cur, 0, 0, 1, 1, gb * kWavesPerBlock};
+    if (dyn) {
+      const int64_t n_tiles = (n_patients + kWave - 1) / kWave;
+      const int ngs = (n_steps + kGT - 1) / kGT;
+      const int n_ent = n_arms * lib.nE;
+      const size_t per_block = narm_pad(n_arms) * kWave > 256 ? (size_t)narm_pad(n_arms) * kWave : 256;
+      const int64_t rows_cap = (int64_t)((kGramMaxBlocks + (kGramMaxBlocks + kTailGroup - 1) / kTailGroup) * per_block /
+                                         (size_t)n_ent);
+      const int64_t pcap = rows_cap - gb;  // piece rows after the gb block rows, inside one slot
+      int64_t tail = n_tiles * INSITE_DEF_DYN_TAIL / 1000;
+      int pg = INSITE_DEF_DYN_PG < 1 ? 1 : (INSITE_DEF_DYN_PG > ngs ? ngs : INSITE_DEF_DYN_PG);
+      int ppt = (ngs + pg - 1) / pg;
+      if (tail * ppt > pcap && tail > 0) {  // coarser pieces, then fewer tail tiles, to stay inside the slot
+        const int64_t pmax = pcap / tail > 1 ? pcap / tail : 1;
+        pg = (int)((ngs + pmax - 1) / pmax);
+        ppt = (ngs + pg - 1) / pg;
+        if (tail * ppt > pcap) tail = pcap / ppt;
+      }
+      dg.ppart = part_cur + (int64_t)gb * n_ent;
+      dg.tile0 = n_tiles - tail;
+      dg.P = tail * ppt;
+      dg.pg = pg;
+      dg.ppt = ppt;
+    }
+    auto kd = dyn ? kd1 : kd0;
     kd<<<dim3(grid), kBlock, 0, hs>>>(x, ldx, n_steps, u, arm, rows, n_patients, make_gram_w(dt), lib, part_cur,
                                       part_prev, lagged ? gred : go, ra, gb, rc, hdr_cur, hdr_prev, lagged, G_fit,
-                                      b_fit, gf, slot_fingerprint(lib, n_arms));
+                                      b_fit, gf, slot_fingerprint(lib, n_arms), dg);
     return launch_status();
   }
   // (a two-patients-per-lane rollout role with 16-B stores measured slower: 46 vs 37 us rollout-only)
@@ -4235,7 +4509,7 @@ int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, co
 
 size_t insite_fit_rollout_deferred_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms) {
   const size_t one = insite_gram_workspace_bytes(n_patients, n_arms, n_terms);
-  return one ? 2 * one + kDefClaimBytes : 0;
+  return one ? 2 * one + kDefAreaBytes : 0;
 }
 
 int32_t insite_fit_rollout_deferred_f64(const double* x, int64_t ldx, int32_t n_steps, const double* u,

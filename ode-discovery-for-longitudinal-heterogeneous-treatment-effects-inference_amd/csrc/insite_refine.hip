@@ -582,8 +582,14 @@ __device__ __forceinline__ double quadmin(double a, double fa, double fpa, doubl
   return a - fpa / (2.0 * B);
 }
 
+// waves per SIMD of the M <= 4 affine kernels.  r04: 3 waves (<= 168 VGPRs) beat 4 with spills (kernel 2.21 vs 2.30 ms,
+// flat BFGS) and 2 (2.01 vs 1.89 ms/step after the closed-form scans); r06: after the round-5 scan
+// unroll the 3-wave M = 3 row kernel held 30 spilled VGPRs (scratch writes ~0.65 GB a launch), and 2 waves without
+// spills measured 1.667-1.674 vs 1.724-1.730 ms/step on one box, interleaved (profiles/r06/refine_ab/) -- so 2.  (The
+// per-lane LDS table of the arm constants the verdict named does not fit at 3 waves: H columns 18 KB + the ring 32 KB
+// per 256-thread block = 150 of the CU's 160 KB at 3 blocks; the 10 constants would add 20 KB a block.)
 #ifndef INSITE_REFINE_WPE4
-#define INSITE_REFINE_WPE4 3  // r04: 3 waves (<= 168 VGPRs, no spills) beat 4 with spills: kernel 2.21 vs 2.30 ms (flat BFGS)
+#define INSITE_REFINE_WPE4 2
 #endif
 #ifndef INSITE_REFINE_WPE8
 #define INSITE_REFINE_WPE8 1
@@ -1553,6 +1559,22 @@ __global__ void __launch_bounds__(kBlock) insite_refine_final_kernel(RefineArgs,
 #ifndef INSITE_COOP_SCAN_PIPE
 #define INSITE_COOP_SCAN_PIPE 1  // the cooperative kernel's software-pipelined closed-form scan (0: the step-wise one)
 #endif
+// INSITE_COOP_SCAN_SPLIT: the pipelined scan in two ranges -- steps below the wave's shortest
+// live window without the per-lane `k < K` guard (its exec-mask save / branch / restore is 3 SALU + a compare a
+// step), then the rest guarded.  Lanes with nothing pending run the unguarded range too; their values are never used
+// (every consumer of fg's results is under `pending`, and a row's 8 lanes share its liveness).  Live lanes issue the
+// same operations in the same order: bitwise the guarded scan.
+template <bool B>
+struct ScanGuard {
+  static constexpr bool value = B;
+};
+// Measured slower (profiles/r06/refine_ab/: dense 11.26-11.31 vs 10.94-11.04 ms/step, joint 12.51-12.72 vs 12.27-12.41,
+// interleaved on one box) although the unguarded range issues 104 instead of 125 instructions per 4 steps (14 SALU
+// instead of 24): the second copy of the scan, inlined into both objective calls, costs more than it saves.  Kept as a
+// knob, off.
+#ifndef INSITE_COOP_SCAN_SPLIT
+#define INSITE_COOP_SCAN_SPLIT 0
+#endif
 constexpr int kCoopG = 8;  // lanes per row
 
 constexpr int kCoopStT = 64;  // staged steps (STG)
@@ -1818,32 +1840,57 @@ insite_refine_coop_kernel(RefineArgs) {
           gGo = fma(-2.0 * r, d, gGo);
         }
       };
-      if (Kw > 0) {
-        // two register sets alternate (s0, s1): while step k computes, step k + 1's constants are in flight, their
-        // offset read three steps earlier (step k + j's in am[(k + j) % 4]) -- the LDS counter is in order, so an
-        // arm read one step ahead made the next lookup wait for everything issued in between.  Reads past the
-        // scan's end land in the padding (their values are never used).
+      auto step_all = [&](const Step& c) {  // step without the per-lane guard (SPLIT's first range)
+        const double tv = te ? fma(c.C1, y, c.C2) : c.hS;
+        const double add = c.off == own ? tv : 0.0;
+        d = fma(c.P, d, add);
+        y = fma(c.P, y, c.B);
+        const double r = c.v - y;
+        L = fma(r, r, L);
+        gGo = fma(-2.0 * r, d, gGo);
+      };
+      // two register sets alternate (s0, s1): while step k computes, step k + 1's constants are in flight, their
+      // offset read three steps earlier (step k + j's in am[(k + j) % 4]) -- the LDS counter is in order, so an
+      // arm read one step ahead made the next lookup wait for everything issued in between.  Reads past the
+      // scan's end land in the padding (offsets staged valid, values never used).
+      auto scan_range = [&](const int kb, const int ke, auto guarded) {  // steps [kb, ke), ke wave-uniform
+        constexpr bool G = decltype(guarded)::value;
+        auto st = [&](const Step& c, int k) {
+          if constexpr (G) step(c, k);
+          else step_all(c);
+        };
         int am[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) am[q] = orow[q * kCoopG];
-        Step s0 = load(am[0], 0), s1;
-        for (int k = 0; k < Kw; k += 4) {  // (Kw wave-uniform: the breaks are uniform)
+        for (int q = 0; q < 4; ++q) am[q] = orow[(kb + q) * kCoopG];
+        Step s0 = load(am[0], kb), s1;
+        for (int k = kb; k < ke; k += 4) {  // (the breaks are uniform)
           s1 = load(am[1], k + 1);
           am[0] = orow[(k + 4) * kCoopG];
-          step(s0, k);
-          if (k + 1 >= Kw) break;
+          st(s0, k);
+          if (k + 1 >= ke) break;
           s0 = load(am[2], k + 2);
           am[1] = orow[(k + 5) * kCoopG];
-          step(s1, k + 1);
-          if (k + 2 >= Kw) break;
+          st(s1, k + 1);
+          if (k + 2 >= ke) break;
           s1 = load(am[3], k + 3);
           am[2] = orow[(k + 6) * kCoopG];
-          step(s0, k + 2);
-          if (k + 3 >= Kw) break;
+          st(s0, k + 2);
+          if (k + 3 >= ke) break;
           s0 = load(am[0], k + 4);
           am[3] = orow[(k + 7) * kCoopG];
-          step(s1, k + 3);
+          st(s1, k + 3);
         }
+      };
+      if (Kw > 0) {
+        int Km = 0;  // steps [0, Km) unguarded
+        if constexpr (INSITE_COOP_SCAN_SPLIT) {  // the wave's shortest live window (lanes with nothing pending: Kw)
+          Km = Kl > 0 ? Kl : Kw;
+#pragma unroll
+          for (int off = 32; off >= 1; off >>= 1) Km = min(Km, __shfl_xor(Km, off));
+          Km = __builtin_amdgcn_readfirstlane(Km);
+          scan_range(0, Km, ScanGuard<false>{});
+        }
+        if (Km < Kw) scan_range(Km, Kw, ScanGuard<true>{});
       }
     } else
 #endif

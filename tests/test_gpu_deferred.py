@@ -302,3 +302,43 @@ def test_deferred_step_north_star_1m_x_500_matches_oracle(dev):
     got = y.index_select(1, it).t().cpu().numpy()
     np.testing.assert_allclose(got, ref, rtol=1e-10)
     assert np.sqrt(np.mean((got - ref) ** 2)) < 1e-6
+
+
+def test_claimed_gram_tail_stale_claim_area_is_flagged(dev):
+    """The claimed gram tail (INSITE_DEF_DYN, taken where the gram waves stream >= 128 units each: this 300k x 460
+    cohort, 136k units) keeps its per-XCD heads in the workspace's claim area, self-resetting.  A stale area (a head
+    left on a value past its segment, as a reused buffer could hold) makes that launch skip the segment's pieces: the
+    next finalisation of its slot must flag it (NaN G|b, iters -3), not sum a partial Gram, and the launch after it
+    (the area reset by the stale launch's last wave) must finalise the right model again (G|b vs the static fit of the
+    same cohort, rtol 1e-10)."""
+    from insite_amd import cohort, ops
+    Nn, Tn = 300_000, 460
+    coh = cohort.synthetic_pkpd(Nn, Tn, seed=4242, device=dev, equation="EQ_4_C", layout="time")
+    bits = cohort.counterfactual_arms(coh.arm, Tn, seed=4242, layout="time_bits")
+    lib = coh.lib
+    F = lib.n_terms
+    ws = ops.Workspace()
+    o = [_outs(dev, F) for _ in range(4)]
+    y = torch.empty((Tn, Nn), dtype=torch.float64, device=dev)
+    cin = torch.zeros((2, F), dtype=torch.float64, device=dev)
+
+    def call(k, out):
+        ops.fit_rollout_deferred(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, coh.y0, coh.u, bits, cin,
+                                 coh.dt, k % 2, k > 0, ws, method="rk4", T=Tn, y_out=y, out=out)
+    call(0, o[0])
+    torch.cuda.synchronize()
+    buf = next(iter(ws._buf.values()))
+    buf[0:4] = torch.tensor([0xFF, 0xFF, 0xFF, 0x0F], dtype=torch.uint8, device=dev)   # head 0 stale
+    call(1, o[1])          # streams slot 1 with the stale head; finalises slot 0 (clean)
+    call(2, o[2])          # finalises slot 1: flagged
+    call(3, o[3])          # finalises slot 0 (streamed by call 2 after the reset): clean
+    torch.cuda.synchronize()
+    ref = ops.sindy_fit(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, layout="time")
+    torch.cuda.synchronize()
+    Gr, br = ref[3].cpu().numpy(), ref[4].cpu().numpy()
+    for j in (1, 3):
+        np.testing.assert_allclose(o[j][3].cpu().numpy(), Gr, rtol=1e-10, atol=1e-6)
+        np.testing.assert_allclose(o[j][4].cpu().numpy(), br, rtol=1e-10, atol=1e-6)
+        assert np.array_equal(o[j][1].cpu().numpy(), ref[1].cpu().numpy())
+    assert torch.isnan(o[2][3]).all() and torch.isnan(o[2][0]).all()
+    assert (o[2][2] == -3).all()
