@@ -174,9 +174,9 @@ int32_t insite_fit_rollout_f64(const double* x, int64_t ldx, int32_t n_steps, co
  * finalisation of a slot no call has streamed (or streamed for another system: the record holds a fingerprint of
  * the library's columns, statics count and arm count) writes NaN G|b and coefficients,
  * mask 0 and iters -3.  Same shape restrictions as insite_fit_rollout_f64.  Workspace:
- * insite_fit_rollout_deferred_workspace_bytes: a 2-KiB claim area at offset 0 that must be zero before the first call
- * (a zero-filled buffer; every call leaves it zero, and its place does not depend on the cohort size), then the two
- * slots (their headers need not be zero). */
+ * insite_fit_rollout_deferred_workspace_bytes: 4 KiB of claim areas at offset 0 that must be zero before the first call
+ * (a zero-filled buffer; every call leaves them zero, and their place does not depend on the cohort size), then the
+ * two slots (their headers need not be zero). */
 size_t insite_fit_rollout_deferred_workspace_bytes(int64_t n_patients, int32_t n_arms, int32_t n_terms);
 int32_t insite_fit_rollout_deferred_f64(const double* x, int64_t ldx, int32_t n_steps, const double* u,
                                         const int8_t* arm, const int32_t* rows, int64_t n_patients, int32_t n_statics,

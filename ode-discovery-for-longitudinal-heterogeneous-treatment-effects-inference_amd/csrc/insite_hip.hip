@@ -2832,11 +2832,14 @@ __device__ __forceinline__ int64_t xcd_count(int64_t n, int x) { return (n + kXc
 #endif
 constexpr int kClaimLineWords = 32;                      // one 128-B line per head (head word 0, done word 1)
 constexpr size_t kDefClaimBytes = (size_t)kXcds * kClaimLineWords * sizeof(unsigned);
-// The deferred step's workspace: [claim area, kDefAreaBytes][slot 0][slot 1].  The claim area (the claimed rollout
+// The deferred step's workspace: [claim areas, kDefAreaBytes][slot 0][slot 1].  The claim areas (the claimed rollout
 // tail's or the claimed gram tail's heads) sits at offset 0 so that its place does not move with the cohort size
 // (a grow-only workspace reused for another N left the heads on stale partial bytes).
-constexpr size_t kDefAreaBytes = 2048;
-static_assert(kDefClaimBytes <= kDefAreaBytes && kDynClaimBytes <= kDefAreaBytes, "claim areas fit the header area");
+// [0, 2 KiB): the claimed gram tail's heads; [2 KiB, 4 KiB): the claimed rollout tail's (both may run in one launch)
+constexpr size_t kDefAreaBytes = 4096;
+constexpr size_t kDefRollClaimOff = 2048;
+static_assert(kDynClaimBytes <= kDefRollClaimOff && kDefRollClaimOff + kDefClaimBytes <= kDefAreaBytes,
+              "claim areas fit the header area");
 // rank of block b among the blocks [lo, hi) ordered XCD-major (by b % kXcds, then b)
 __device__ __forceinline__ int64_t xcd_rank(int64_t b, int64_t lo, int64_t hi) {
   const int x = (int)(b % kXcds);
@@ -4443,7 +4446,7 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
     }
     // the claim area at offset 0 (the claimed rollout tail's, INSITE_DEF_RSTATIC < 1000, a knob build: zeroed before
     // every launch, since the chunks its heads skip would otherwise go unrolled silently)
-    unsigned* rc = INSITE_DEF_RSTATIC < 1000 ? reinterpret_cast<unsigned*>(wsb) : nullptr;
+    unsigned* rc = INSITE_DEF_RSTATIC < 1000 ? reinterpret_cast<unsigned*>(wsb + kDefRollClaimOff) : nullptr;
     if (rc && hipMemsetAsync(rc, 0, kDefClaimBytes, hs) != hipSuccess) return INSITE_E_HIP;
     // the claimed gram tail (INSITE_DEF_DYN): its heads in the same area, self-resetting; a stale area shows up as a
     // piece count that does not add up, which the next finalisation flags (NaN G|b, iters -3)

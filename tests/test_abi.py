@@ -232,10 +232,10 @@ def test_pack_arm_bits_roundtrip():
 
 
 def test_deferred_workspace_holds_two_slots_and_the_claim_area():
-    """insite_fit_rollout_deferred_workspace_bytes = the 2-KiB claim area at offset 0 (the claimed gram tail's nine
-    128-B head / done lines, or the claimed rollout tail's eight; its place does not move with the cohort size) + two
-    discovery slots (insite_hip.h)."""
+    """insite_fit_rollout_deferred_workspace_bytes = the 4-KiB claim areas at offset 0 (the claimed gram tail's nine
+    128-B head / done lines, then the claimed rollout tail's eight; their place does not move with the cohort size) +
+    two discovery slots (insite_hip.h)."""
     from insite_amd import _lib
     L = _lib.load()
     for n in (1, 1000, 100_000, 1_000_000):
-        assert L.insite_fit_rollout_deferred_workspace_bytes(n, 2, 7) == 2 * L.insite_gram_workspace_bytes(n, 2, 7) + 2048
+        assert L.insite_fit_rollout_deferred_workspace_bytes(n, 2, 7) == 2 * L.insite_gram_workspace_bytes(n, 2, 7) + 4096

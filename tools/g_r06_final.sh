@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU recipe (round 6, final): PART=a -- every GPU test, smoke(), the default bench line (C2 + north_star_step + c3
-# blocks), rocprofv3 kernel stats of the C2 line alone and of the north-star line; PART=b -- the secondary lines with
+# blocks), rocprofv3 kernel stats of the same command; PART=b -- the secondary lines with
 # their parity blocks, then (TRAFFIC) the PMC traffic passes of the named configs.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -24,8 +24,9 @@ print("c3", c3.get("error") or (round(c3["ms_per_step"], 3), round(c3["roofline"
 print("nsr", d.get("north_star_rollout", {}).get("frac_of_8TBps"))
 PY
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof_c2 -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-parity --no-north-star --no-c3-block > $GRAFT_REPO_ROOT/$O/prof_c2.log 2>&1 && echo PROF c2 ok
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof_ns -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --config ns --no-parity > $GRAFT_REPO_ROOT/$O/prof_ns.log 2>&1 && echo PROF ns ok
+# the default line's own command (its C2 launches are step_deferred_kernel<.., 0>, the north-star block's the claimed
+# instantiation <.., 1>: two rows of one profile, from the same process layout as the line)
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof_default -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-parity > $GRAFT_REPO_ROOT/$O/prof_default.jsonl 2> $GRAFT_REPO_ROOT/$O/prof_default.log && echo PROF default ok
 else
 for c in ${LINES:-c3 c4 c5 f4 insite insite4}; do
   timeout -k 10 400 python bench.py --config $c > $O/bench_$c.jsonl 2> $O/bench_$c.err || { echo "bench $c failed"; tail -5 $O/bench_$c.err; exit 1; }
