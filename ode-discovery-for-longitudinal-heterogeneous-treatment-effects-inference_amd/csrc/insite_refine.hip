@@ -167,8 +167,11 @@ __device__ __forceinline__ int pm_slot_index(int r, int col) {
 #ifndef INSITE_REFINE_HOIST
 #define INSITE_REFINE_HOIST 1  // 1 / K and dt / sub once per row (RefineLane::setK); measured neutral (profiles/r05/scan/run_hoist)
 #endif
+// INSITE_REFINE_SCAN_LROT 1: the ring offset formed per step (round 5: at 3 waves per SIMD the 8 hoisted offsets cost
+// ~8 VGPRs of spills); at 2 waves (round 6, no spills) the hoisted form is back: 1.642-1.656 vs 1.654-1.661 ms/step,
+// interleaved on one box (profiles/r06/refine_ab2/i3_lrot0_*)
 #ifndef INSITE_REFINE_SCAN_LROT
-#define INSITE_REFINE_SCAN_LROT 1
+#define INSITE_REFINE_SCAN_LROT 0
 #endif
 // the per-arm constants of CF for one evaluation
 struct CfArm {
