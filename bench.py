@@ -1964,7 +1964,10 @@ def fused_run(args, dev, coh, arm_cf, coh2=None, arm_cf2=None):
     # instrumented pass: HIP timing events on the launch stream around batches of KB back-to-back launches
     # (an event record costs ~20 us of queue time on ROCm 7.2, so never one per launch), divided by KB
     hip = HipEvents()
-    KB, NBAT = max(args.steps, 10), 3
+    # batches of >= 100 launches: an event record puts ~20 us of dead queue time into the stream (ROCm 7.2,
+    # profiles/r02/c2_pipeline_trace.txt), which over round 5's 20-launch batches read as ~1 us more per launch than
+    # the timed region's own wall clock (What's weak 4)
+    KB, NBAT = max(args.steps, 100), 3
     tevs = [(hip.create(timing=True), hip.create(timing=True)) for _ in range(NBAT)]
     for e0, e1 in tevs:
         hip.record(e0, st.cuda_stream)
@@ -2046,7 +2049,9 @@ def deferred_run(args, dev, coh, arm_cf, coh2=None, arm_cf2=None):
     # instrumented pass: timing events on stream 0 around batches of KB steps; the other streams' last launches
     # are joined into stream 0 before the closing event (one ordering event per stream per batch)
     hip = HipEvents()
-    KB, NBAT = max(args.steps, 10), 3
+    # batches of >= 100 launches (>= 10 for launches over 0.5 ms): each event record is ~20 us of dead queue time
+    # (ROCm 7.2), ~1 us a launch over round 5's 20-launch batches (What's weak 4)
+    KB, NBAT = max(args.steps, 100 if args.patients * args.T <= 50_000_000 else 10), 3
     tevs = [(hip.create(timing=True), hip.create(timing=True)) for _ in range(NBAT)]
     joins = [hip.create() for _ in range(S)]
     st0 = streams[0].cuda_stream

@@ -342,3 +342,38 @@ def test_claimed_gram_tail_stale_claim_area_is_flagged(dev):
         assert np.array_equal(o[j][1].cpu().numpy(), ref[1].cpu().numpy())
     assert torch.isnan(o[2][3]).all() and torch.isnan(o[2][0]).all()
     assert (o[2][2] == -3).all()
+
+
+def test_claimed_gram_tail_is_bitwise_reproducible_and_lagged_equal(dev):
+    """The claimed gram tail's G|b do not depend on which wave took which piece (each piece's contribution has its own
+    partial slot, summed in piece order): two independent deferred streams over the same 300k x 460 cohort (claimed
+    instantiation; the claim order differs from run to run) finalise bitwise-equal G|b and models, and the lagged
+    kernel's reduction role (the N > 1 step's dyn_finalize without the STLSQ) writes the same G|b bitwise."""
+    from insite_amd import cohort, ops
+    Nn, Tn = 300_000, 460
+    coh = cohort.synthetic_pkpd(Nn, Tn, seed=4343, device=dev, equation="EQ_4_C", layout="time")
+    bits = cohort.counterfactual_arms(coh.arm, Tn, seed=4343, layout="time_bits")
+    lib = coh.lib
+    F = lib.n_terms
+    cin = torch.zeros((2, F), dtype=torch.float64, device=dev)
+    y = torch.empty((Tn, Nn), dtype=torch.float64, device=dev)
+    res = []
+    for rep in range(2):
+        ws = ops.Workspace()
+        o = _outs(dev, F)
+        for k in range(2):
+            ops.fit_rollout_deferred(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, coh.y0, coh.u, bits, cin,
+                                     coh.dt, k, k > 0, ws, T=Tn, y_out=y, out=o)
+        torch.cuda.synchronize()
+        res.append(tuple(t.clone() for t in o))
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+    wsl = ops.Workspace()
+    Gr = torch.zeros((2, F, F), dtype=torch.float64, device=dev)
+    br = torch.zeros((2, F), dtype=torch.float64, device=dev)
+    for k in range(2):
+        ops.plan_fit_rollout_lagged(coh.x, coh.u, coh.arm, coh.rows, coh.dt, lib, 0.1, 0.5, coh.y0, coh.u, bits, cin,
+                                    coh.dt, k, k > 0, wsl, (Gr, br), T=Tn, y_out=y)()
+    torch.cuda.synchronize()
+    assert torch.equal(Gr, res[0][3]) and torch.equal(br, res[0][4])
+    assert np.all(np.isfinite(Gr.cpu().numpy()))
