@@ -49,6 +49,9 @@ def parse():
                     help="untimed warmup steps (default: 5; C5 60, C4 / F4 200, C3 20 -- see WARMUP_DEFAULT)")
     ap.add_argument("--rk45-identity-order", action="store_true",
                     help="C5 ablation: lane r runs row r (no binning by n_obs)")
+    ap.add_argument("--rk45-bin", default="nobs", choices=["nobs", "attempts"],
+                    help="C5 lane binning key: n_obs (the number of observation intervals) or the per-patient attempt "
+                         "counts the previous step left (a C5 step re-rolls the same cohort; VERDICT r05 item 7)")
     ap.add_argument("--patients", type=int, default=100_000, help="patients per GPU (C2: 100k)")
     ap.add_argument("--T", type=int, default=200)
     ap.add_argument("--method", default="rk4", choices=["rk4", "euler5"])
@@ -623,13 +626,17 @@ def c5_main(args):
     coef[0, 4], coef[1, 1], coef[1, 5] = C5_COEF
     # rows padded to whole 64-B sectors (ld 64): the kernel stages each lane's outputs per sector
     y = torch.empty((N, (Tm + 7) // 8 * 8), dtype=torch.float64, device=dev)[:, :Tm]
-    steps = torch.empty((N,), dtype=torch.int32, device=dev)
+    steps = torch.zeros((N,), dtype=torch.int32, device=dev)
 
     order = not args.rk45_identity_order
+    by_attempts = order and args.rk45_bin == "attempts"
 
-    # binning by n_obs (the counting sort) runs inside every step; the plan packs the two C calls once
+    # binning (the counting sort, by n_obs or by the previous step's attempt counts) runs inside every step; the plan
+    # packs the two C calls once
     plan = ops.plan_rollout_rk45(y0, u, bits, t_dev, n_obs, coef, lib, out=y, steps=steps, layout="patient",
-                                 order=order)
+                                 order="attempts" if by_attempts else order)
+    lane_order = ((lambda: ops.rk45_order(steps, ops.RK45_ATTEMPT_BINS - 1)) if by_attempts
+                  else (lambda: ops.rk45_order(n_obs, Tm)))
 
     def run():
         plan()
@@ -657,7 +664,7 @@ def c5_main(args):
     launch_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     st = steps.to(torch.float64)
     # waves as the kernel formed them: lanes take rows in the binned order (ops.rk45_order)
-    per_wave = (st[ops.rk45_order(n_obs, Tm).long()] if order else st)[: N // 64 * 64].view(-1, 64)
+    per_wave = (st[lane_order().long()] if order else st)[: N // 64 * 64].view(-1, 64)
     intervals = (n_obs - 1).to(torch.float64)
     attempts = float(st.sum())
     flop = attempts * RK45_FLOP_PER_ATTEMPT
@@ -698,7 +705,7 @@ def c5_main(args):
     }
     if world == 1 and not args.no_parity:
         out["parity"] = c5_parity(y0, u, arm, t_obs, n_obs, coef, lib, y, steps,
-                                  ops.rk45_order(n_obs, Tm) if order else torch.arange(N, device=dev))
+                                  lane_order() if order else torch.arange(N, device=dev))
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:
@@ -2920,14 +2927,15 @@ def main():
                                 "other, the pipeline ahead on most boxes (profiles/r02/fused_sweep/)",
         }
         del fr
+    # the oracle parity of the benched cohort (every step of these modes discovers and rolls out the same cohort)
+    if rank == 0 and world == 1 and not args.no_parity:
+        out["parity"] = (c2_parity(dev, coh, arm_cf, coef, mask, y) if roll_layout == "time_bits" else
+                         {"skipped": "the parity block reads the time-major bit-arm layout"})
     # north-star probe: 1M x 500 RK4 rollout alone (the >= 40 % roofline target), rank 0, N = 1
     if rank == 0 and world == 1 and not args.no_north_star:
         del y
         torch.cuda.empty_cache()
         out["north_star_rollout"] = north_star_rollout(args, dev, coef, lib)
-    if world == 1 and not args.no_parity:
-        out["parity"] = c5_parity(y0, u, arm, t_obs, n_obs, coef, lib, y, steps,
-                                  ops.rk45_order(n_obs, Tm) if order else torch.arange(N, device=dev))
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:

@@ -834,6 +834,9 @@ def plan_fit_rollout_lagged(x, u, arm, rows, dt, lib, threshold, alpha, y0, ru, 
                                           drop_below, T, y_out, gram_blocks, slot, reduce_prev))
 
 
+RK45_ATTEMPT_BINS = 1024   # the counting sort's bin count (kRkBinMax): attempt counts above 1022 share the last bin
+
+
 def rk45_order(n_obs: torch.Tensor, T_max: int, out: torch.Tensor | None = None) -> torch.Tensor:
     """Lane order for ``rollout_rk45``: rows sorted by n_obs, descending (insite_rk45_order_i32, a
     counting sort on the device).  Scheduling only: the rollout's outputs do not depend on it."""
@@ -889,17 +892,28 @@ def _rk45_prep(y0, u, arm_bits, t_obs, n_obs, coef, lib, rtol, atol, drop_below,
         _dev("out", out, torch.float64, 2)
         if out.size(0) < shape[0] or out.size(1) < shape[1] or (pm and out.size(0) != N):
             raise ValueError(f"out must be {'[N, >=T_max]' if pm else '[T_max, >=N]'}")
+    # the binning key: n_obs (order=True), or -- order="attempts" -- the per-patient attempt counts the previous call
+    # left in ``steps`` (a re-rolled cohort takes the same counts again, so its waves group equal attempt counts: wave
+    # divergence 1.07 -> ~1.01 at C5's shape); the first call bins whatever ``steps`` holds (zeros when allocated here)
+    key, key_T = n_obs, int(Tm)
+    if isinstance(order, str):
+        if order != "attempts":
+            raise ValueError("order must be True, False/None, 'attempts' or a [N] int32 permutation")
+        if steps is None:
+            steps = torch.zeros((N,), dtype=torch.int32, device=y0.device)
+        _dev("steps", steps, torch.int32, 1)
+        key, key_T, order = steps, RK45_ATTEMPT_BINS - 1, True
     if steps is None:
         steps = torch.empty((N,), dtype=torch.int32, device=y0.device)
     order_call = None
     if order is True:
         if plan:   # the plan bins into its own buffer with its own workspace, per call
             order = torch.empty((N,), dtype=torch.int32, device=n_obs.device)
-            wsb = _lib.load().insite_rk45_order_workspace_bytes(int(Tm))
+            wsb = _lib.load().insite_rk45_order_workspace_bytes(key_T)
             ows = torch.zeros((max(1, (wsb + 7) // 8),), dtype=torch.float64, device=n_obs.device)
-            order_call = ("insite_rk45_order_i32", (_p(n_obs), N, int(Tm), _p(order), _p(ows), wsb), (order, ows))
+            order_call = ("insite_rk45_order_i32", (_p(key), N, key_T, _p(order), _p(ows), wsb), (order, ows, key))
         else:
-            order = rk45_order(n_obs, Tm)
+            order = rk45_order(key, key_T)
     elif order is False:
         order = None
     elif order is not None:
@@ -927,8 +941,9 @@ def rollout_rk45(y0: torch.Tensor, u: torch.Tensor, arm_bits: torch.Tensor, t_ob
                       time-major arms), y [T_max, N] (row k = state at t_obs[k + 1]);
     layout "patient": t_obs [N, >=T_max] f64, arm_bits [N, >=ceil((T_max-1)/32)] int32 (pack_arm_bits of
                       the patient-major arms [N, T]), y [N, T_max] -- the fast layout.
-    ``order``: True bins the rows by n_obs on the device first (``rk45_order``, part of the call), a [N]
-    int32 permutation is used as given, None/False runs lane r on row r.  Outputs do not depend on it.
+    ``order``: True bins the rows by n_obs on the device first (``rk45_order``, part of the call), "attempts" by
+    the attempt counts a previous call left in ``steps``, a [N] int32 permutation is used as given, None/False runs
+    lane r on row r.  Outputs do not depend on it.
     Returns (y, step attempts [N] int32); y elements past a patient's grid are left as they were (NaN
     when ``out`` is None)."""
     return _rk45_prep(y0, u, arm_bits, t_obs, n_obs, coef, lib, rtol, atol, drop_below, out, steps, order, layout,

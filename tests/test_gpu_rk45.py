@@ -196,3 +196,37 @@ def test_rk45_plan_equals_eager(dev, layout):
         torch.cuda.synchronize()
         assert torch.equal(torch.isnan(y_p), torch.isnan(y_e))
         assert torch.equal(torch.nan_to_num(y_p), torch.nan_to_num(y_e)) and torch.equal(s_p, s_e)
+
+
+@pytest.mark.parametrize("layout", ["time", "patient"])
+def test_rk45_plan_binned_by_attempts_equals_eager(dev, layout):
+    """order="attempts" (VERDICT r05 item 7): the plan bins its lanes by the attempt counts the previous call left in
+    ``steps`` (the first call: zeros).  Scheduling only -- three consecutive calls give outputs and attempt counts
+    bit-identical to the eager n_obs-binned rollout, and the order a call bins by is a permutation sorted by those
+    counts (descending)."""
+    from insite_amd import ops
+    from insite_amd.library import polynomial_library
+    ex, t, n, u, arm, y0, coef = _setup(3000, 37)
+    lib = polynomial_library(2, 2, True)
+    N, Tm = t.shape
+    tn = np.nan_to_num(t, nan=0.0)
+    if layout == "patient":
+        tt = torch.tensor(np.ascontiguousarray(tn), device=dev)
+        bits = ops.pack_arm_bits(torch.tensor(np.ascontiguousarray(arm[:, :Tm]), device=dev), Tm)
+    else:
+        tt = torch.tensor(np.ascontiguousarray(tn.T), device=dev)
+        bits = ops.pack_arm_bits(torch.tensor(np.ascontiguousarray(arm[:, :Tm].T), device=dev), N)
+    args = (torch.tensor(y0, device=dev), torch.tensor(u, device=dev), bits, tt, torch.tensor(n, device=dev),
+            torch.tensor(np.ascontiguousarray(coef), device=dev), lib)
+    y_e, s_e = ops.rollout_rk45(*args, layout=layout)
+    steps = torch.zeros((N,), dtype=torch.int32, device=dev)
+    plan = ops.plan_rollout_rk45(*args, layout=layout, steps=steps, order="attempts")
+    for _ in range(3):
+        y_p, s_p = plan()
+        torch.cuda.synchronize()
+        assert torch.equal(torch.isnan(y_p), torch.isnan(y_e))
+        assert torch.equal(torch.nan_to_num(y_p), torch.nan_to_num(y_e)) and torch.equal(s_p, s_e)
+    o = ops.rk45_order(steps, ops.RK45_ATTEMPT_BINS - 1).cpu().numpy()
+    assert np.array_equal(np.sort(o), np.arange(N))
+    key = np.clip(steps.cpu().numpy(), 0, ops.RK45_ATTEMPT_BINS - 1)[o]
+    assert np.all(np.diff(key) <= 0)
