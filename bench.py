@@ -49,9 +49,10 @@ def parse():
                     help="untimed warmup steps (default: 5; C5 60, C4 / F4 200, C3 20 -- see WARMUP_DEFAULT)")
     ap.add_argument("--rk45-identity-order", action="store_true",
                     help="C5 ablation: lane r runs row r (no binning by n_obs)")
-    ap.add_argument("--rk45-bin", default="nobs", choices=["nobs", "attempts"],
-                    help="C5 lane binning key: n_obs (the number of observation intervals) or the per-patient attempt "
-                         "counts the previous step left (a C5 step re-rolls the same cohort; VERDICT r05 item 7)")
+    ap.add_argument("--rk45-bin", default="attempts", choices=["nobs", "attempts"],
+                    help="C5 lane binning key: the per-patient attempt counts the previous step left (default: a C5 "
+                         "step re-rolls the same cohort, so waves group equal attempt counts; VERDICT r05 item 7: "
+                         "0.660 vs 0.707 ms/step, profiles/r06/c5_bin/) or n_obs (the number of observation intervals)")
     ap.add_argument("--patients", type=int, default=100_000, help="patients per GPU (C2: 100k)")
     ap.add_argument("--T", type=int, default=200)
     ap.add_argument("--method", default="rk4", choices=["rk4", "euler5"])
@@ -698,8 +699,10 @@ def c5_main(args):
                  #  the same figure under its explicit name: a wave's flat loop runs its slowest
                  # lane's attempt count, so sum over waves of max / sum of attempts is the issued-work inflation
                  "attempts_max_over_mean_per_wave": float((per_wave.max(dim=1).values.mean() / per_wave.mean()).item()),
-                 # what binning by the previous call's per-patient attempt count (a C5 step re-rolls the same cohort)
-                 # would give, rows sorted by attempts inside the same 4096-row chunks the n_obs binning uses
+                 "lane_binning": ("by the previous step's per-patient attempt counts (a C5 step re-rolls the same "
+                                  "cohort; the first call bins zeros)") if by_attempts else
+                                 ("by n_obs" if order else "identity"),
+                 # with n_obs binning: what attempt binning inside the same 4096-row chunks would give
                  "attempts_max_over_mean_if_binned_by_attempts": _binned_divergence(st, 4096),
                  "rhs_evals_per_s": float(st.sum() * 6 / (launch_ms * 1e-3))},
     }
