@@ -2711,10 +2711,12 @@ step_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double
 #endif
 // INSITE_DEF_DYN: the claimed gram tail (DynGram) -- 0 never, 1 always, 2 (default) by size: a launch takes the claimed
 // instantiation when its gram waves stream at least INSITE_DEF_DYN_MIN (tile, kGT-step group) units each.  Measured
-// (profiles/r06/dyn/): at the north-star 1M x 500 (488 units a wave) the claimed tail is 9 % faster; at C2's 100k x 200
-// (20 units a wave) 20-35 % slower -- the per-piece warm-ups, contractions and partial stores and the finaliser's
-// ~1 MB of piece partials (one block, latency-bound beside the streaming) cost more than the ~10 us of spread they
-// recover.  INSITE_DEF_DYN_TAIL: per mille of the tiles claimed; INSITE_DEF_DYN_PG: kGT-step groups per piece.
+// (profiles/r06/dyn_ns/, dyn_c2/): at the north-star 1M x 500 (488 units a wave; the pieces are whole tiles, the slot's
+// row budget) the claimed tail is 4-10 % faster, box to box; at C2's 100k x 200 (20 units a wave) 20-35 % slower -- the
+// per-piece warm-ups, contractions and partial stores and the finaliser's ~1 MB of piece partials (one block,
+// latency-bound beside the streaming) cost more than the ~10 us of spread they recover.  INSITE_DEF_DYN_TAIL: per mille
+// of the tiles claimed (250: 1.686-1.690 vs 1.700-1.702 ms at 150, three runs each); INSITE_DEF_DYN_PG: kGT-step
+// groups per piece (coarsened to fit the slot).
 #ifndef INSITE_DEF_DYN
 #define INSITE_DEF_DYN 2
 #endif
