@@ -59,8 +59,13 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--layout", default="time", choices=["time", "patient"],
                     help="HBM layout of the per-step arrays (DESIGN.md): time-major is the fast path")
-    ap.add_argument("--arm-format", default="bits", choices=["bits", "int8"],
-                    help="per-step arms of the time-major rollout: 1-bit mask (A <= 2) or int8")
+    ap.add_argument("--arm-format", default="bits", choices=["bits", "tiles", "int8"],
+                    help="per-step arms of the time-major rollout: 1-bit mask (A <= 2) in time-major rows, the same "
+                         "bits tile-major (ops.tile_major_bits: a tile's 32-step group in 256 contiguous bytes), or int8")
+    ap.add_argument("--ns-arms", default="tiles", choices=["bits", "tiles"],
+                    help="bit-arm layout of the north-star blocks (1M x 500): time-major rows or tile-major "
+                         "(default: at 1M patients the time-major rows' 128-B lines, 16 tiles each, leave the L2 "
+                         "between their tiles' waves -- profiles/r06/tiles/)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default=None, choices=["deferred", "lagged", "fused", "graph", "seq", "pipeline"],
                     help="deferred (default at N = 1) / fused: ONE launch per step -- the discovery of step i and "
@@ -170,6 +175,11 @@ class HipEvents:
     def __del__(self):
         for e in getattr(self, "_events", []):
             self._hip.hipEventDestroy(e)
+
+
+def bits_layout(fmt):
+    """counterfactual_arms layout of a bit-arm format name (--arm-format / --ns-arms)."""
+    return "tile_bits" if fmt == "tiles" else "time_bits"
 
 
 def rollout_bytes(N, T, U=2, w=8, arm_bits=8):
@@ -851,8 +861,12 @@ def c5_parity(y0, u, arm, t_obs, n_obs, coef, lib, y, steps, order, n_sample=409
 
 
 def _unpack_bits_rows(bits, idx, T):
-    """time-major bit words [T, W] (int32 tensor) -> [n, T] int64 arms of the rows idx (tensor on its device)."""
-    words = bits[:T].index_select(1, idx // 32)
+    """bit words -> [n, T] int64 arms of the rows idx (tensor on its device): time-major [T, W] int32, or tile-major
+    [ceil(N/64), S >= T, 2] int32 (ops.tile_major_bits)."""
+    if bits.dim() == 3:
+        words = bits[idx // 64, :T, (idx // 32) % 2].t()                        # [T, n]
+    else:
+        words = bits[:T].index_select(1, idx // 32)
     return ((words >> (idx % 32).to(torch.int32)[None, :]) & 1).t().contiguous().cpu().numpy().astype(np.int64)
 
 
@@ -1617,7 +1631,7 @@ def c4_main(args):
     lo, hi = idist.shard_bounds(N_total, rank, world)
     N = hi - lo
     coh = cohort.synthetic_pkpd(N, T, seed=args.seed * 1000 + 3 + rank, device=dev, equation="EQ_4_C", layout="time")
-    arm_cf = cohort.counterfactual_arms(coh.arm, T, seed=args.seed * 1000 + 3 + rank, layout="time_bits")
+    arm_cf = cohort.counterfactual_arms(coh.arm, T, seed=args.seed * 1000 + 3 + rank, layout=bits_layout(args.arm_format))
     lib, F = coh.lib, coh.lib.n_terms
     buf = idist.MomentBuffer(2, F, dev)
     gout = (torch.empty((2, F), dtype=torch.float64, device=dev), torch.empty((2, F), dtype=torch.int8, device=dev),
@@ -2012,7 +2026,7 @@ def deferred_run(args, dev, coh, arm_cf, coh2=None, arm_cf2=None):
     while len(pool) < need:   # more cohorts for the extra streams (distinct seeds)
         sd = args.seed * 1000 + 700 + len(pool)
         c = cohort.synthetic_pkpd(N, T, seed=sd, device=dev, equation="EQ_4_C", layout="time")
-        pool.append((c, cohort.counterfactual_arms(c.arm, T, seed=sd, layout="time_bits")))
+        pool.append((c, cohort.counterfactual_arms(c.arm, T, seed=sd, layout=bits_layout(args.arm_format))))
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     lanes = []   # per stream: (its cohorts, outs ring, ys, workspace)
     for si in range(S):
@@ -2122,8 +2136,7 @@ def c2_parity(dev, coh, arm_bits, coef, mask, y, n_sample=4096, seed=11, pooled=
     idx = np.unique(np.concatenate([rng.choice(N, min(n_sample, N), replace=False), np.arange(min(64, N)),
                                     np.arange(max(0, N - 64), N)]))
     it = torch.as_tensor(idx, device=dev)
-    words = arm_bits.index_select(1, it // 32)                                   # [T, n] int32
-    arms = ((words >> (it % 32).to(torch.int32)[None, :]) & 1).t().contiguous().cpu().numpy().astype(np.int64)
+    arms = _unpack_bits_rows(arm_bits, it, arm_bits.size(0) if arm_bits.dim() == 2 else arm_bits.size(1))
     y0s, us = coh.y0[it].cpu().numpy(), coh.u[it].cpu().numpy()
     if pooled:
         parts = [c for c in np.array_split(np.arange(idx.size), 4 * W) if c.size]
@@ -2155,7 +2168,8 @@ def c2_fused(args, dev, coh, arm_cf, cpu):
     coh2 = arm_cf2 = None
     if not args.no_rotate:
         coh2 = cohort.synthetic_pkpd(N, T, seed=args.seed * 1000 + 500, device=dev, equation="EQ_4_C", layout="time")
-        arm_cf2 = cohort.counterfactual_arms(coh2.arm, T, seed=args.seed * 1000 + 500, layout="time_bits")
+        arm_cf2 = cohort.counterfactual_arms(coh2.arm, T, seed=args.seed * 1000 + 500,
+                                             layout=bits_layout(args.arm_format))
     deferred = args.mode == "deferred"
     fr = (deferred_run if deferred else fused_run)(args, dev, coh, arm_cf, coh2, arm_cf2)
     ms_step, host_ms, step_ms, KB, NBAT = fr["ms_step"], fr["host_ms"], fr["step_ms"], fr["KB"], fr["NBAT"]
@@ -2297,7 +2311,7 @@ def c2_lagged(args, dev, world, rank, coh, arm_cf, cpu, collective):
     sched = idist.LaggedSchedule(K, delay=args.lag_delay)
     sd = args.seed * 1000 + 500 + rank
     coh2 = cohort.synthetic_pkpd(N, T, seed=sd, device=dev, equation="EQ_4_C", layout="time")
-    cohs = [(coh, arm_cf), (coh2, cohort.counterfactual_arms(coh2.arm, T, seed=sd, layout="time_bits"))]
+    cohs = [(coh, arm_cf), (coh2, cohort.counterfactual_arms(coh2.arm, T, seed=sd, layout=bits_layout(args.arm_format)))]
     buckets = [idist.MomentBucket(K, 2, F, dev) for _ in range(sched.NB)]
     ring = [(torch.zeros((2, F), dtype=f64, device=dev), torch.zeros((2, F), dtype=torch.int8, device=dev),
              torch.zeros((2,), dtype=torch.int32, device=dev)) for _ in range(3)]
@@ -2448,7 +2462,7 @@ def north_star_step(args, dev):
     N, T = ns.patients, ns.T
     sd = [args.seed * 1000 + 900, args.seed * 1000 + 901]
     cohs = [cohort.synthetic_pkpd(N, T, seed=s_, device=dev, equation="EQ_4_C", layout="time") for s_ in sd]
-    arms = [cohort.counterfactual_arms(c.arm, T, seed=s_, layout="time_bits") for c, s_ in zip(cohs, sd)]
+    arms = [cohort.counterfactual_arms(c.arm, T, seed=s_, layout=bits_layout(args.ns_arms)) for c, s_ in zip(cohs, sd)]
     torch.cuda.synchronize(dev)
     fr = deferred_run(ns, dev, cohs[0], arms[0], cohs[1], arms[1])
     rb, gb = fr["rb"], fr["gb"]
@@ -2499,9 +2513,11 @@ def north_star_rollout(args, dev, coef, lib):
     flip = torch.randint(0, Tn, (Nn, 1), generator=g, device=dev)
     armn = torch.zeros((Tn, Nn), dtype=torch.int8, device=dev)
     armn[:] = (torch.arange(Tn, device=dev)[:, None] >= flip[:, 0][None, :]).to(torch.int8)
-    nlay = "time_bits" if args.arm_format == "bits" else "time"
+    nlay = "time_bits" if args.arm_format in ("bits", "tiles") else "time"
     if nlay == "time_bits":
         armn = ops.pack_arm_bits(armn, Nn)
+        if args.ns_arms == "tiles":     # the tile-major bits (one 256-B run per tile and 32-step group)
+            armn = ops.tile_major_bits(armn, Nn)
     yn = torch.empty((Tn, Nn), dtype=torch.float64, device=dev)
     for _ in range(3):
         ops.rollout(y0n, un, armn, coef, lib, 10.0 / Tn, method="rk4", out=yn, layout=nlay)
@@ -2516,7 +2532,9 @@ def north_star_rollout(args, dev, coef, lib):
     torch.cuda.synchronize(dev)
     ms = float(np.mean([a.elapsed_time(b_) for a, b_ in evs]))
     bn = rollout_bytes(Nn, Tn, arm_bits=1 if nlay == "time_bits" else 8)
-    return {"patients": Nn, "T": Tn, "method": "rk4", "layout": nlay, "avg_launch_ms": ms,
+    return {"patients": Nn, "T": Tn, "method": "rk4",
+            "layout": nlay + (" (tile-major bits)" if nlay == "time_bits" and args.ns_arms == "tiles" else ""),
+            "avg_launch_ms": ms,
             "algorithmic_bytes": bn, "achieved_GBps": bn / (ms * 1e-3) / 1e9,
             "frac_of_8TBps": bn / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
             "patient_trajectories_per_s": Nn / (ms * 1e-3)}
@@ -2572,7 +2590,8 @@ def main():
     coh = cohort.synthetic_pkpd(N, T, seed=args.seed * 1000 + rank, device=dev, equation="EQ_4_C",
                                 layout=args.layout)
     # time-major arm sequences / trajectories: one contiguous run per step ("HBM layout")
-    roll_layout = "time_bits" if (args.layout == "time" and args.arm_format == "bits") else args.layout
+    roll_layout = (bits_layout(args.arm_format) if args.arm_format != "int8" else "time") if args.layout == "time" \
+        else args.layout
     arm_cf = cohort.counterfactual_arms(coh.arm, T, seed=args.seed * 1000 + rank, layout=roll_layout)
     lib = coh.lib
     F = lib.n_terms
@@ -2644,7 +2663,8 @@ def main():
         stlsq_plans = [ops.plan_stlsq(bufs[j].G, bufs[j].b, 0.1, 0.5, 100, True, out=(coefs[j], masks[j], iters[j]))
                        for j in range(NB)]
     roll_plans = [ops.plan_rollout(y0, coh.u, arm_cf, coefs[j], lib, coh.dt, method=args.method, T=T,
-                                   out=ys[(j // K) % RS], layout=roll_layout) for j in range(NB)]
+                                   out=ys[(j // K) % RS], layout="time_bits" if roll_layout == "tile_bits" else roll_layout)
+                  for j in range(NB)]
     # cross-stream ordering through the HIP runtime directly (torch's Event wrappers cost ~3-5 us of host
     # time each; at N > 1 the host also issues the all-reduce, and must stay ahead of a ~70 us step)
     hip = HipEvents()
@@ -2811,7 +2831,7 @@ def main():
 
     out = None
     if rank == 0:
-        arm_bits = 1 if roll_layout == "time_bits" else 8
+        arm_bits = 1 if roll_layout in ("time_bits", "tile_bits") else 8
         rb = rollout_bytes(N, T, arm_bits=arm_bits)
         achieved = rb / (roll_ms * 1e-3) / 1e9
         traffic = None
@@ -2860,6 +2880,7 @@ def main():
                                  "each batch of rollout launches on its stream, divided by the batch size "
                                  "(concurrent with the next batch's discoveries)",
                 "layout": {"time_bits": "time-major x[T,N], 1-bit arm mask [T,N/32], y[T,N]",
+                           "tile_bits": "time-major x[T,N], 1-bit arm mask tile-major [N/64,T,2], y[T,N]",
                            "time": "time-major x[T,N], int8 arm[T,N], y[T,N]",
                            "patient": "patient-major x[N,T], int8 arm[N,T], y[N,T]"}[roll_layout],
             },
@@ -2932,7 +2953,7 @@ def main():
         del fr
     # the oracle parity of the benched cohort (every step of these modes discovers and rolls out the same cohort)
     if rank == 0 and world == 1 and not args.no_parity:
-        out["parity"] = (c2_parity(dev, coh, arm_cf, coef, mask, y) if roll_layout == "time_bits" else
+        out["parity"] = (c2_parity(dev, coh, arm_cf, coef, mask, y) if roll_layout in ("time_bits", "tile_bits") else
                          {"skipped": "the parity block reads the time-major bit-arm layout"})
     # north-star probe: 1M x 500 RK4 rollout alone (the >= 40 % roofline target), rank 0, N = 1
     if rank == 0 and world == 1 and not args.no_north_star:

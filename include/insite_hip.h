@@ -75,7 +75,14 @@ extern "C" {
  *   TIME_MAJOR:    a[k * ld + r]   (ld >= n_rows; every step of a wavefront is one contiguous run)
  *   TIME_MAJOR_BITS (rollout only, n_arms <= 2): y as TIME_MAJOR; the arms are a bitmask,
  *                  arm of (r, k) = bit (r & 31) of ((const uint32_t*)arm)[k * ld_arm + (r >> 5)],
- *                  ld_arm in 32-bit words >= ceil(n_rows / 32), arm 4-byte aligned            */
+ *                  ld_arm in 32-bit words >= ceil(n_rows / 32), arm 4-byte aligned;
+ *                  or, with ld_arm < 0 (round 6, INSITE_ARM_BITS_TILE_MAJOR; insite_rollout_f64, the fused /
+ *                  deferred / lagged steps and insite_refit_rollout_moments_f64), TILE-major: with S = -ld_arm >= T
+ *                  steps per tile, arm of (r, k) = bit (r & 31) of
+ *                  ((const uint32_t*)arm)[((r >> 6) * S + k) * 2 + ((r >> 5) & 1)] -- a 64-patient tile's
+ *                  32-step arm group is 256 contiguous bytes (the time-major rows put 16 tiles on one 128-B line,
+ *                  which a 1M-patient rollout re-fetches once per tile) */
+#define INSITE_ARM_BITS_TILE_MAJOR(steps_per_tile) (-(int64_t)(steps_per_tile)) /* the ld_arm value */
 #define INSITE_LAYOUT_PATIENT_MAJOR 0
 #define INSITE_LAYOUT_TIME_MAJOR 1
 #define INSITE_LAYOUT_TIME_MAJOR_BITS 2

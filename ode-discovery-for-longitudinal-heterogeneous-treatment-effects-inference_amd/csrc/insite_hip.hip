@@ -2290,9 +2290,14 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
   }
   const int nvalid = (int)(ra.N - p0 < kWave ? ra.N - p0 : kWave);
   const unsigned yoff = act ? (unsigned)(lane * 8) : kOOB;
-  const int64_t arow = ra.lda * 4;   // bit rows: lda counts 32-bit words
-  const int64_t abase = (p0 >> 5) * 4;
-  const int arec_tail = ((nvalid + 31) >> 5) * 4;
+  // time-major bits [T, lda words] (lda > 0): a step's 2 words of this tile share a 128-B line with 15 other tiles'
+  // -- in a 1M-patient cohort those lines leave the XCD's L2 between the tiles' waves, ~16x the arm bytes re-fetched
+  // (PMC: 1.12x of the north-star step's algorithmic bytes).  Tile-major bits (lda < 0, INSITE_ARM_BITS_TILE_MAJOR:
+  // [ceil(N/64)][-lda steps][2 words]): a group's 32 steps of one tile are 256 contiguous bytes, read whole by this wave
+  const bool atile = ra.lda < 0;
+  const int64_t arow = atile ? 8 : ra.lda * 4;   // bytes per step row
+  const int64_t abase = atile ? tile * (-ra.lda) * 8 : (p0 >> 5) * 4;
+  const int arec_tail = atile ? (nvalid > 32 ? 8 : 4) : ((nvalid + 31) >> 5) * 4;
   const int kend = SR ? (g_end < ra.T ? g_end : ra.T)
                       : (g_end * kRollGS < ra.T ? g_end * kRollGS : ra.T);  // one past the last step of the range
   const int kbeg = SR ? g_begin : g_begin * kRollGS;                   // first stored step
@@ -4376,13 +4381,15 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
   if (lagged && ((G_fit == nullptr) != (b_fit == nullptr))) return INSITE_E_INVALID_ARG;
   if (ldx > ((int64_t)1 << 31) / (8 * kGT)) return INSITE_E_UNSUPPORTED;
   // ---- rollout half: insite_rollout_f64's checks for TIME_MAJOR_BITS, shared library ----
-  if (n_rows < 0 || T < 0 || substeps < 1 || !(rdt >= 0.0) || ld_arm < (n_rows + 31) / 32 || ld_y < n_rows)
+  // ld_arm > 0: time-major bits [T, ld_arm]; ld_arm < 0: tile-major bits [ceil(n_rows / 64)][-ld_arm >= T][2]
+  if (n_rows < 0 || T < 0 || substeps < 1 || !(rdt >= 0.0) || ld_y < n_rows ||
+      (ld_arm >= 0 ? ld_arm < (n_rows + 31) / 32 : -ld_arm < (int64_t)T))
     return INSITE_E_INVALID_ARG;
   if (method != INSITE_METHOD_EULER && method != INSITE_METHOD_RK4) return INSITE_E_UNSUPPORTED;
   const bool roll = n_rows > 0 && T > 0;
   if (roll && (!y0 || !arm_bits || !coef_in || !y_out || (n_statics > 0 && !ru))) return INSITE_E_INVALID_ARG;
   if (roll && (reinterpret_cast<uintptr_t>(arm_bits) & 3u) != 0) return INSITE_E_INVALID_ARG;
-  if (ld_arm * 4 > kTmMaxLd || ld_y > kTmMaxLd) return INSITE_E_UNSUPPORTED;
+  if ((ld_arm >= 0 ? ld_arm * 4 : (int64_t)8) > kTmMaxLd || ld_y > kTmMaxLd) return INSITE_E_UNSUPPORTED;
   if (gram_blocks < 0) return INSITE_E_INVALID_ARG;
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   RolloutArgs ra;
@@ -4605,7 +4612,8 @@ int32_t insite_refit_rollout_moments_f64(const double* mom, const int8_t* arm, c
                                          int64_t ld_y, double* coef_out, int8_t* mask_out, int32_t* iters_out,
                                          void* stream) {
   if (n_patients < 0 || n_arms < 1 || n_arms > 2 || n_steps < 0 || max_iter < 0 || !(threshold >= 0.0) ||
-      !(alpha >= 0.0) || T < 0 || substeps < 1 || !(dt >= 0.0) || ld_bits < (n_patients + 31) / 32 ||
+      !(alpha >= 0.0) || T < 0 || substeps < 1 || !(dt >= 0.0) ||
+      (ld_bits >= 0 ? ld_bits < (n_patients + 31) / 32 : -ld_bits < (int64_t)T) ||  // < 0: tile-major bits
       ld_y < n_patients)
     return INSITE_E_INVALID_ARG;
   if (method != INSITE_METHOD_EULER && method != INSITE_METHOD_RK4) return INSITE_E_UNSUPPORTED;
@@ -4619,7 +4627,7 @@ int32_t insite_refit_rollout_moments_f64(const double* mom, const int8_t* arm, c
   if (!mom || !arm || !rows || !global_coef || !y0 || !arm_bits || !y_out || (n_statics > 0 && !u))
     return INSITE_E_INVALID_ARG;
   if ((reinterpret_cast<uintptr_t>(arm_bits) & 3u) != 0) return INSITE_E_INVALID_ARG;
-  if (ld_bits * 4 > kTmMaxLd || ld_y > kTmMaxLd) return INSITE_E_UNSUPPORTED;
+  if ((ld_bits >= 0 ? ld_bits * 4 : (int64_t)8) > kTmMaxLd || ld_y > kTmMaxLd) return INSITE_E_UNSUPPORTED;
   RolloutArgs ra;
   ra.y0 = y0;
   ra.u = n_statics == 0 ? y0 : u;
@@ -4768,8 +4776,11 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
   if (layout != INSITE_LAYOUT_PATIENT_MAJOR && !tm) return INSITE_E_INVALID_ARG;
   const int64_t minld = tm ? n_rows : (int64_t)T;
   const int64_t minld_arm = bits ? (n_rows + 31) / 32 : minld;
+  // bits: ld_arm < 0 is the tile-major bit layout [ceil(n_rows / 64)][-ld_arm >= T][2] (rollout_bits_range)
+  const bool tiles = bits && ld_arm < 0;
   if (n_rows < 0 || T < 0 || n_arms < 1 || n_arms > INSITE_MAX_ARMS || substeps < 1 ||
-      !(dt >= 0.0) || ld_arm < minld_arm || ld_y < minld || coef_row_stride < 0 || (bits && n_arms > 2))
+      !(dt >= 0.0) || (tiles ? -ld_arm < (int64_t)T : ld_arm < minld_arm) || ld_y < minld || coef_row_stride < 0 ||
+      (bits && n_arms > 2))
     return INSITE_E_INVALID_ARG;
   if (method != INSITE_METHOD_EULER && method != INSITE_METHOD_RK4) return INSITE_E_UNSUPPORTED;
   if (n_rows == 0 || T == 0) return INSITE_OK;
@@ -4806,7 +4817,8 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
   const bool perrow = coef_row_stride != 0;
   const int na = narm_pad(n_arms);
   if (tm) {
-    if ((bits ? ld_arm * 4 : ld_arm) > kTmMaxLd || ld_y > kTmMaxLd) return INSITE_E_UNSUPPORTED;  // 32-bit offsets per step group
+    if ((tiles ? (int64_t)8 : bits ? ld_arm * 4 : ld_arm) > kTmMaxLd || ld_y > kTmMaxLd)
+      return INSITE_E_UNSUPPORTED;  // 32-bit offsets per step group
     if (n_statics == 0) ra.u = y0;
     if (bits && (reinterpret_cast<uintptr_t>(arm) & 3u) != 0) return INSITE_E_INVALID_ARG;
     const bool aw4 = bits || (ld_arm % 4 == 0 && (reinterpret_cast<uintptr_t>(arm) & 3u) == 0);
@@ -4822,6 +4834,7 @@ int32_t insite_rollout_f64(const double* y0, const double* u, const int8_t* arm,
     // 0.094 ms at PPL 1, 0.168 ms at PPL 4 (profiles/r02/ppl/); INSITE_FORCE_PPL keeps the others
 #endif
     if (ppl >= 2 && !(y16 && aw4 && n_rows % ppl == 0)) ppl = 1;
+    if (tiles) ppl = 1;  // (the tile-major bits are read by rollout_bits_range, the one-patient-per-lane form)
     const int64_t per_block = (int64_t)kBlock * ppl;
     const dim3 grid((unsigned)((n_rows + per_block - 1) / per_block));
     if (method == INSITE_METHOD_EULER) launch_rollout_tm_m<INSITE_METHOD_EULER>(na, perrow, ppl, afmt, grid, hs, ra, lib);

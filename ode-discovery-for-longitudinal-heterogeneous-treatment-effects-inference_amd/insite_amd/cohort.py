@@ -109,20 +109,24 @@ def counterfactual_arms(arm: torch.Tensor, T: int, seed: int, layout: str = "pat
 
     layout "patient": [N, round_up(T, 16)] (16-byte rows: the patient-major rollout reads 16 B per
     lane); layout "time": [T, round_up(N, 4)] (time-major; 4-byte rows let the rollout load
-    dwords); layout "time_bits": int32 [T, ceil(N/32)] bitmask (ops.pack_arm_bits)."""
+    dwords); layout "time_bits": int32 [T, ceil(N/32)] bitmask (ops.pack_arm_bits); "tile_bits": the same bits
+    tile-major, int32 [ceil(N/64), T, 2] (ops.tile_major_bits)."""
     dev = arm.device
     g = _gen(seed + 7919, dev)
     N = arm.numel()
     flip = torch.randint(0, T, (N, 1), generator=g, device=dev)
     steps = torch.arange(T, device=dev)[None, :]
     seq = torch.where(steps >= flip, 1 - arm[:, None], arm[:, None]).to(torch.int8)
-    if layout in ("time", "time_bits"):
+    if layout in ("time", "time_bits", "tile_bits"):
         ld = (N + 3) // 4 * 4
         out = torch.zeros((T, ld), dtype=torch.int8, device=dev)
         out[:, :N] = seq.t()
         if layout == "time_bits":
             from .ops import pack_arm_bits
             return pack_arm_bits(out, N)
+        if layout == "tile_bits":
+            from .ops import pack_arm_bits, tile_major_bits
+            return tile_major_bits(pack_arm_bits(out, N), N)
         return out
     lda = (T + 15) // 16 * 16
     out = torch.empty((N, lda), dtype=torch.int8, device=dev)

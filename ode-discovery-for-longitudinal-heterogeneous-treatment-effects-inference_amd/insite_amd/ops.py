@@ -37,6 +37,36 @@ def pack_arm_bits(arm: torch.Tensor, n: int | None = None) -> torch.Tensor:
     return w.to(torch.int32).contiguous()
 
 
+def tile_major_bits(bits: torch.Tensor, n: int) -> torch.Tensor:
+    """Time-major bit arms int32 [T, >= ceil(n/32)] (``pack_arm_bits``) -> the tile-major form int32
+    [ceil(n/64), T, 2] (insite_hip.h, ld_arm = INSITE_ARM_BITS_TILE_MAJOR(T)): a 64-patient tile's 32-step arm group
+    is 256 contiguous bytes, where the time-major rows put 16 tiles on one 128-B line (re-fetched once per tile by a
+    1M-patient rollout).  Data preparation, not on the hot path."""
+    _dev("bits", bits, torch.int32, 2)
+    T, W = bits.shape
+    nt = (int(n) + 63) // 64
+    if W < (int(n) + 31) // 32:
+        raise ValueError("bits must be [T, >= ceil(n/32)] int32 words")
+    w = torch.zeros((T, 2 * nt), dtype=torch.int32, device=bits.device)
+    w[:, :min(W, 2 * nt)] = bits[:, :min(W, 2 * nt)]
+    return w.view(T, nt, 2).permute(1, 0, 2).contiguous()
+
+
+def _arm_bits_ld(arm_bits: torch.Tensor, N: int, T: int) -> int:
+    """ld_arm of a bit-arm tensor: time-major [>= T, >= ceil(N/32)] int32 -> its row stride; tile-major
+    [ceil(N/64), S >= T, 2] int32 (``tile_major_bits``) -> -S (insite_hip.h: INSITE_ARM_BITS_TILE_MAJOR)."""
+    if arm_bits.dim() == 3:
+        _dev("arm_bits", arm_bits, torch.int32, 3)
+        if (arm_bits.size(0) != (N + 63) // 64 or arm_bits.size(1) < T or arm_bits.size(2) != 2
+                or not arm_bits.is_contiguous()):
+            raise ValueError("tile-major bit arms must be a contiguous [ceil(N/64), >= T, 2] int32 tensor")
+        return -arm_bits.size(1)
+    _dev("arm_bits", arm_bits, torch.int32, 2)
+    if arm_bits.size(0) < T or arm_bits.size(1) < (N + 31) // 32:
+        raise ValueError("arm_bits must be [T, >= ceil(N / 32)] int32 words (or tile-major [ceil(N/64), >= T, 2])")
+    return arm_bits.stride(0)
+
+
 def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
@@ -349,9 +379,7 @@ def _prep_refit_rollout(mom, u, arm, rows, n_steps, lib, global_coef, threshold,
         _dev("u", u, torch.float64, 2)
         if u.size(0) != N or u.size(1) != lib.n_statics or not u.is_contiguous():
             raise ValueError("u must be a contiguous [N, n_statics] tensor")
-    _dev("arm_bits", arm_bits, torch.int32, 2)
-    if arm_bits.size(0) < T or arm_bits.size(1) < (N + 31) // 32:
-        raise ValueError("arm_bits must be [T, >= ceil(N / 32)] int32 words")
+    ld_bits = _arm_bits_ld(arm_bits, N, T)
     if method not in METHODS:
         raise ValueError(f"method must be one of {sorted(METHODS)}")
     meth, sub = METHODS[method]
@@ -372,7 +400,7 @@ def _prep_refit_rollout(mom, u, arm, rows, n_steps, lib, global_coef, threshold,
     nul = ctypes.c_void_p(0)
     args = (_p(mom), _p(arm), _p(rows), N, int(n_steps), lib.n_statics, A, tab.ctypes.data_as(ctypes.c_void_p), F,
             _p(global_coef), float(threshold), float(alpha), int(max_iter), int(bool(unbias)), _p(y0),
-            _p(u) if lib.n_statics else nul, _p(arm_bits), arm_bits.stride(0), int(T), float(dt), meth, sub,
+            _p(u) if lib.n_statics else nul, _p(arm_bits), ld_bits, int(T), float(dt), meth, sub,
             float(drop_below), _p(out), out.stride(0), _p(fc), _p(fm), _p(fi))
     keep = (mom, u, arm, rows, global_coef, y0, arm_bits, out, fc, fm, fi, tab)
     return "insite_refit_rollout_moments_f64", args, dev, out, keep
@@ -621,11 +649,12 @@ def _prep_rollout(y0, u, arm, coef, lib, dt, method, substeps, drop_below, T, ou
     tm = layout != "patient"
     _dev("y0", y0, torch.float64, 1)
     N = y0.numel()
-    if layout == "time_bits":
-        _dev("arm", arm, torch.int32, 2)
-        T = arm.size(0) if T is None else int(T)
-        if arm.size(1) < (N + 31) // 32 or arm.size(0) < T:
-            raise ValueError("bit-packed arm must be [>=T, >=ceil(N/32)] int32")
+    ld_arm = None
+    if layout == "time_bits":   # time-major [>= T, >= ceil(N/32)] or tile-major [ceil(N/64), >= T, 2] int32 words
+        if not isinstance(arm, torch.Tensor) or arm.dim() not in (2, 3):
+            raise ValueError("bit-packed arm must be [>=T, >=ceil(N/32)] (or tile-major [ceil(N/64), >=T, 2]) int32")
+        T = (arm.size(0) if arm.dim() == 2 else arm.size(1)) if T is None else int(T)
+        ld_arm = _arm_bits_ld(arm, N, T)
     elif tm:
         _dev("arm", arm, torch.int8, 2)
         T = arm.size(0) if T is None else int(T)
@@ -666,7 +695,8 @@ def _prep_rollout(y0, u, arm, coef, lib, dt, method, substeps, drop_below, T, ou
         if out.size(0) != shape[0] or out.size(1) < shape[1]:
             raise ValueError(f"out must be {shape}")
     tab = lib.ctypes_table()
-    args = (_p(y0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm), arm.stride(0), _p(coef), stride,
+    args = (_p(y0), _p(u) if lib.n_statics else ctypes.c_void_p(0), _p(arm),
+            arm.stride(0) if ld_arm is None else ld_arm, _p(coef), stride,
             tab.ctypes.data_as(ctypes.c_void_p), F, N, T, lib.n_statics, A, float(dt), m, sub, float(drop_below),
             _p(out), out.stride(0), ROLLOUT_LAYOUTS[layout])
     return "insite_rollout_f64", args, y0.device, out, (y0, u, arm, coef, tab, out)
@@ -681,8 +711,9 @@ def rollout(y0: torch.Tensor, u: torch.Tensor, arm: torch.Tensor, coef: torch.Te
     layout "patient":   arm int8 [N, >=T], returns y [N,T] (the reference's [N, T] arrays).
     layout "time":      arm int8 [T, >=N], returns y [T,N] (one contiguous run per step).
     layout "time_bits": arm int32 [T, >=ceil(N/32)] bitmask (pack_arm_bits; A <= 2), y [T,N] —
-                        the fast layout on MI355X.  Row k of y is the state after
-                        observation interval k."""
+                        the fast layout on MI355X; or the same bits tile-major,
+                        int32 [ceil(N/64), >=T, 2] (tile_major_bits).  Row k of y is the state
+                        after observation interval k."""
     return _run(_prep_rollout(y0, u, arm, coef, lib, dt, method, substeps, drop_below, T, out, layout))
 
 
