@@ -1827,9 +1827,11 @@ def traffic_for(config, kernel, grid=None, args=None):
         eff_n = 1_000_000 if (big and args.patients == 100_000) else args.patients
         t_def = {"c3": 500, "c4": 60, "f4": 60, "ns": 500}.get(config, 200)
         eff_t = t_def if args.T == 200 else args.T
-        knobs = (eff_n, eff_t, args.method, args.arm_format, args.layout, args.gram_blocks, args.dstreams,
+        # the north-star step reads its arms in the --ns-arms format (default tile-major bits), the others --arm-format
+        fmt, fmt_def = (args.ns_arms, "tiles") if config == "ns" else (args.arm_format, "bits")
+        knobs = (eff_n, eff_t, args.method, fmt, args.layout, args.gram_blocks, args.dstreams,
                  int(os.environ.get("WORLD_SIZE", "1")))
-        if knobs != (1_000_000 if big else 100_000, t_def, "rk4", "bits", "time", 0, 1, 1):
+        if knobs != (1_000_000 if big else 100_000, t_def, "rk4", fmt_def, "time", 0, 1, 1):
             return None
     # this round's table first (taken on the kernels as they are now), the previous round's for configs it lacks
     hits = []
