@@ -129,6 +129,9 @@ constexpr int kGStride = kGT + 1;  // LDS row stride in doubles (odd -> lane-per
 // (32 x 23) and the scalar path's 64 x kPsStride rows
 constexpr int kGSlot = kGStride > 17 ? kGStride : 17;
 constexpr int kGPF = INSITE_PF;    // tiles in flight (register prefetch depth, 1 or 2)
+#ifndef INSITE_GRAM_SCPF
+#define INSITE_GRAM_SCPF 1
+#endif
 #ifndef INSITE_TM_DEPTH
 #define INSITE_TM_DEPTH 2
 #endif
@@ -637,6 +640,18 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
   typedef double TmTile[kGT];
   TmTile vr[TM ? kTmDepth : 1];
   bool prefetched = false;  // wave-uniform: vr holds the current item's first kTmDepth tiles already
+  // The next piece's per-patient scalars (row count, arm, statics) are requested with its first tiles and BEFORE
+  // them (INSITE_GRAM_SCPF): vmcnt is in order, so scalars loaded after the tiles at the piece start made the wave
+  // wait for every tile in flight -- one drained prefetch ring per piece
+  int sc_L = 0, sc_a = -1;
+  double sc_u[INSITE_MAX_STATICS] = {0.0, 0.0, 0.0};
+  auto sc_load = [&](int64_t pp) {
+    const int64_t pcl = pp < N ? pp : N - 1;
+    sc_L = rows[pcl];
+    sc_a = arm[pcl];
+#pragma unroll
+    for (int t = 0; t < INSITE_MAX_STATICS; ++t) sc_u[t] = u[pcl * lib.U + (t < lib.U ? t : 0)];
+  };
   // wave-uniform descriptor over steps [t0, min(t0 + kGT, lim)) based at column q0 (valid columns qv): steps
   // past lim and lanes past N (out-of-range offset) read as 0
   auto tm_load_for = [&](TmTile& v, int t0, int lim, int64_t q0, int qv, unsigned qoff) {
@@ -742,6 +757,7 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
     const int tm_valid = (int)(N - p0 < kWave ? N - p0 : kWave);
     const unsigned tm_off = p < N ? (unsigned)lane * 8u : kOOB;
     auto tm_load = [&](TmTile& v, int t0, int lim) { tm_load_for(v, t0, lim, p0, tm_valid, tm_off); };
+    if (!(TM && INSITE_GRAM_SCPF && prefetched)) sc_load(p);  // (before the first tiles)
 #ifndef INSITE_GRAM_LATE_ISSUE
     if constexpr (TM) {
       const int s1p = min(pc.sE, n_steps);
@@ -756,15 +772,11 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
     int L = 0;
     int arm_p = -1;
     double uu[INSITE_MAX_STATICS] = {0.0, 0.0, 0.0};
-    {  // per-patient scalars, issued together and unconditionally (clamped index)
-      const int64_t pc = p < N ? p : N - 1;
-      const int Lr = rows[pc];
-      const int ar = arm[pc];
+    {  // per-patient scalars, issued together and unconditionally (clamped index; sc_load)
+      const int Lr = sc_L;
+      const int ar = sc_a;
 #pragma unroll
-      for (int t = 0; t < INSITE_MAX_STATICS; ++t) {
-        const double q = u[pc * lib.U + (t < lib.U ? t : 0)];
-        uu[t] = (p < N && t < lib.U) ? q : 0.0;
-      }
+      for (int t = 0; t < INSITE_MAX_STATICS; ++t) uu[t] = (p < N && t < lib.U) ? sc_u[t] : 0.0;
       if (p < N) {
         L = Lr;
         arm_p = ar;
@@ -995,6 +1007,7 @@ __device__ __forceinline__ void gram_body(const int vblk, const int vgrid, doubl
             const int ns1p = min(np.sE, n_steps);
             const int nvalid = (int)(N - np0 < kWave ? N - np0 : kWave);
             const unsigned noff = np0 + lane < N ? (unsigned)lane * 8u : kOOB;
+            if (INSITE_GRAM_SCPF) sc_load(np0 + lane);
 #pragma unroll
             for (int d = 0; d < kTmDepth; ++d)
               if (ntb + d * kGT < ns1p) tm_load_for(vr[d], ntb + d * kGT, ns1p, np0, nvalid, noff);
@@ -2218,10 +2231,59 @@ constexpr int kRollGS = 32;  // steps per arm group
 // its rollout: no per-patient coefficient round trip through HBM, one launch less).
 // SR (step range): g_begin / g_end are STEPS [k_begin, k_end) instead of groups -- the stored steps of a range cut
 // at any step (the deferred step's step-balanced rollout ranges); earlier steps of the first group integrate only.
-template <int METHOD, int NARM, int PR, bool SR = false>
+// One 32-step group of a tile's arm bits, steps [k0, min(k0 + kRollGS, kend)) (empty past kend: returns 0).
+// time-major bits [T, lda words] (lda > 0): a step's 2 words of this tile share a 128-B line with 15 other tiles'
+// -- in a 1M-patient cohort those lines leave the XCD's L2 between the tiles' waves, ~16x the arm bytes re-fetched
+// (PMC: 1.12x of the north-star step's algorithmic bytes).  Tile-major bits (lda < 0, INSITE_ARM_BITS_TILE_MAJOR:
+// [ceil(N/64)][-lda steps][2 words]): a group's 32 steps of one tile are 256 contiguous bytes, read whole by this wave
+__device__ __forceinline__ unsigned roll_arm_group_load(const RolloutArgs& ra, const int64_t tile, const int lane,
+                                                        const int k0, const int kend) {
+  const int64_t p0 = tile * kWave;
+  const int nvalid = (int)(ra.N - p0 < kWave ? ra.N - p0 : kWave);
+  const bool atile = ra.lda < 0;
+  const int64_t arow = atile ? 8 : ra.lda * 4;  // bytes per step row
+  const int64_t abase = atile ? tile * (-ra.lda) * 8 : (p0 >> 5) * 4;
+  const int arec_tail = atile ? (nvalid > 32 ? 8 : 4) : ((nvalid + 31) >> 5) * 4;
+  const unsigned goff = (unsigned)((lane & 31) * arow + (lane >> 5) * 4);
+  const int rows = kend - k0 < kRollGS ? kend - k0 : kRollGS;
+  const int bytes = rows > 0 ? (int)((int64_t)(rows - 1) * arow + arec_tail) : 0;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(ra.arm + (int64_t)(rows > 0 ? k0 : 0) * arow + abase), (short)0, bytes, 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b32(rs, goff, 0, 0);
+}
+constexpr int kRollAG = 4;  // arm groups in flight (the rollout's arm ring)
+#ifndef INSITE_ROLL_SMASK
+#define INSITE_ROLL_SMASK 1  // 2-arm bit rollouts: the step's arm bits as the lane mask (rollout_bits_range)
+#endif
+// A rollout range's per-lane inputs, requested ahead (rollout_units: the NEXT range's before this range's stores):
+// vmcnt counts stores too and completes in order, so inputs loaded at a range's start made the wave wait for every
+// store of the previous range still in flight -- one drained store queue per tile change.
+struct RollPre {
+  double u[INSITE_MAX_STATICS];
+  double y0;
+  unsigned ar[kRollAG];
+};
+__device__ __forceinline__ void roll_pre_issue(const RolloutArgs& ra, const LibDesc& lib, const int lane,
+                                               const int64_t tile, const int g_end, RollPre& pr) {
+  const int64_t p = tile * kWave + lane;
+  const int64_t pc = p < ra.N ? p : ra.N - 1;
+#pragma unroll
+  for (int t = 0; t < INSITE_MAX_STATICS; ++t) pr.u[t] = ra.u[pc * lib.U + (t < lib.U ? t : 0)];
+  pr.y0 = ra.y0[pc];
+  const int kend = g_end * kRollGS < ra.T ? g_end * kRollGS : ra.T;
+  if (INSITE_ROLL_SMASK && (ra.lda < 0 || 2 * tile + 1 < ra.lda)) return;  // (scalar step masks: no arm groups)
+#pragma unroll
+  for (int d = 0; d < kRollAG; ++d) pr.ar[d] = roll_arm_group_load(ra, tile, lane, d * kRollGS, kend);
+}
+
+// PF (PR = 0, SR = false): the lane's statics, y0 and first arm groups come from *pre (roll_pre_issue) and the
+// global coefficient rows from *cvp (loaded once per wave) -- the same values, no loads at the range's start
+template <int METHOD, int NARM, int PR, bool SR = false, bool PF = false>
 __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const LibDesc& lib, const int lane,
                                                    const int64_t tile, const int g_begin, const int g_end,
-                                                   const RefitArgs rf = RefitArgs{}) {
+                                                   const RefitArgs rf = RefitArgs{}, const RollPre* pre = nullptr,
+                                                   const double (*cvp)[NARM][INSITE_MAX_TERMS] = nullptr) {
+  static_assert(!PF || (PR == 0 && !SR), "prefetched inputs: the global-coefficient range form");
   // rf by value: the address of the kernel's by-value argument would put a copy of it in scratch
   constexpr bool PERROW = PR == 1;
   const int64_t p0 = tile * kWave;
@@ -2233,7 +2295,7 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
     double uu[INSITE_MAX_STATICS];
 #pragma unroll
     for (int t = 0; t < INSITE_MAX_STATICS; ++t) {
-      const double v = ra.u[pc * lib.U + (t < lib.U ? t : 0)];
+      const double v = PF ? pre->u[t] : ra.u[pc * lib.U + (t < lib.U ? t : 0)];
       uu[t] = (act && t < lib.U) ? v : 0.0;
     }
     double al[NARM], be[NARM];
@@ -2271,6 +2333,8 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
       }
       if (act && rf.iters_out) rf.iters_out[p] = fit ? it : -2;
       affine_rates_regs<NARM>(lib, cv, ra.A, ra.drop, uu, al, be);
+    } else if constexpr (PF) {
+      affine_rates_regs<NARM>(lib, *cvp, ra.A, ra.drop, uu, al, be);
     } else {
       affine_rates<NARM>(lib, ra.coef + (PERROW ? pc * ra.coef_stride : 0), ra.A, ra.drop, uu, al, be);
     }
@@ -2285,19 +2349,11 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
       PB[a] = be[a];
     }
 #endif
-    const double v0 = ra.y0[pc];
+    const double v0 = PF ? pre->y0 : ra.y0[pc];
     y = act ? v0 : 0.0;
   }
   const int nvalid = (int)(ra.N - p0 < kWave ? ra.N - p0 : kWave);
   const unsigned yoff = act ? (unsigned)(lane * 8) : kOOB;
-  // time-major bits [T, lda words] (lda > 0): a step's 2 words of this tile share a 128-B line with 15 other tiles'
-  // -- in a 1M-patient cohort those lines leave the XCD's L2 between the tiles' waves, ~16x the arm bytes re-fetched
-  // (PMC: 1.12x of the north-star step's algorithmic bytes).  Tile-major bits (lda < 0, INSITE_ARM_BITS_TILE_MAJOR:
-  // [ceil(N/64)][-lda steps][2 words]): a group's 32 steps of one tile are 256 contiguous bytes, read whole by this wave
-  const bool atile = ra.lda < 0;
-  const int64_t arow = atile ? 8 : ra.lda * 4;   // bytes per step row
-  const int64_t abase = atile ? tile * (-ra.lda) * 8 : (p0 >> 5) * 4;
-  const int arec_tail = atile ? (nvalid > 32 ? 8 : 4) : ((nvalid + 31) >> 5) * 4;
   const int kend = SR ? (g_end < ra.T ? g_end : ra.T)
                       : (g_end * kRollGS < ra.T ? g_end * kRollGS : ra.T);  // one past the last step of the range
   const int kbeg = SR ? g_begin : g_begin * kRollGS;                   // first stored step
@@ -2307,20 +2363,16 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
                                              rows > 0 ? (int)(((int64_t)(rows - 1) * ra.ldy + nvalid) * 8) : 0,
                                              0x00020000);
   };
-  constexpr int kAG = 4;
-  const unsigned goff = (unsigned)((lane & 31) * arow + (lane >> 5) * 4);
-  auto grp_load = [&](int k0) -> unsigned {  // empty past the range: returns 0
-    const int rows = kend - k0 < kRollGS ? kend - k0 : kRollGS;
-    const int bytes = rows > 0 ? (int)((int64_t)(rows - 1) * arow + arec_tail) : 0;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(ra.arm + (int64_t)(rows > 0 ? k0 : 0) * arow + abase), (short)0, bytes, 0x00020000);
-    return __builtin_amdgcn_raw_buffer_load_b32(rs, goff, 0, 0);
-  };
+  constexpr int kAG = kRollAG;
+  auto grp_load = [&](int k0) -> unsigned { return roll_arm_group_load(ra, tile, lane, k0, kend); };
+#ifndef INSITE_ABL_ROLL
+#define INSITE_ABL_ROLL 0  // profiling ablations only: 1 = no arm selects (arm 0 always), 2 = no prefix re-integration
+#endif
 #ifndef INSITE_ROLLOUT_STAGEWISE
   auto step = [&](int a) {
     double A = PA[0], B = PB[0];
 #pragma unroll
-    for (int aa = 1; aa < NARM; ++aa) {
+    for (int aa = 1; aa < (INSITE_ABL_ROLL == 1 ? 1 : NARM); ++aa) {
       A = (a == aa) ? PA[aa] : A;
       B = (a == aa) ? PB[aa] : B;
     }
@@ -2348,9 +2400,72 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
     }
   };
 #endif
+#if INSITE_ROLL_SMASK && !defined(INSITE_ROLLOUT_STAGEWISE)
+  if constexpr (NARM == 2 && !SR) {
+    // A step's 64 arm bits of this tile (bit l = patient p0 + l: the two 32-patient words as they lie in either
+    // layout) ARE the wave's lane mask for the arm-1 select: one scalar load per step straight into an SGPR pair,
+    // prefetched kTG steps ahead, and v_cndmask on it (inverse ballot) -- no per-lane bit transpose, extraction or
+    // compare; per step two independent FMAs (arm 0 / arm 1, the same operands as the select-then-FMA form, so y is
+    // bitwise unchanged) and a 64-bit select.  `wide`: both words exist (not so for a last tile of <= 32 patients in a
+    // time-major [T, ceil(N/32)] array, which takes the per-lane form below).
+    const bool wide = ra.lda < 0 || 2 * tile + 1 < ra.lda;  // uniform
+    if (wide) {
+      if (kend <= 0) return;
+      typedef const __attribute__((address_space(4))) uint32_t* cu32p;  // scalar (constant) loads: arm bits are input
+      const char* ab = reinterpret_cast<const char*>(ra.arm) + (ra.lda < 0 ? tile * (-ra.lda) * 8 : (p0 >> 5) * 4);
+      const int64_t arow = ra.lda < 0 ? 8 : ra.lda * 4;
+      const int klast = kend - 1;
+      auto mload = [&](int k) -> uint64_t {  // clamped at the range's last step (the mask of steps past it is unused)
+        if (INSITE_ABL_ROLL == 3) return 0x5555555555555555ull << (k & 1);  // (ablation: no mask loads)
+        const cu32p q = (cu32p)(ab + (int64_t)(k < klast ? k : klast) * arow);
+        return (uint64_t)q[0] | ((uint64_t)q[1] << 32);
+      };
+      const double A0 = PA[0], A1 = PA[1], B0 = PB[0], B1 = PB[1];
+      auto step2 = [&](uint64_t m) {
+        const bool b = __builtin_amdgcn_inverse_ballot_w64(m);
+        const double y0 = fma(A0, y, B0), y1 = fma(A1, y, B1);
+        y = b ? y1 : y0;
+      };
+      // the next chunk's masks are requested after the chunk's first step has used its own: scalar loads return out of
+      // order, so a use of mc[] with loads outstanding waits for all of them (lgkmcnt(0)); issued behind that first use
+      // (sched_barrier) they stay in flight for the rest of the chunk.  (Two mask sets used in turn instead of the
+      // copy raised the kernel's SGPR spills into this loop.)
+      uint64_t mc[kTG], mn[kTG];
+#pragma unroll
+      for (int i = 0; i < kTG; ++i) mc[i] = mload(i);
+      for (int k0 = 0; k0 < kend; k0 += kTG) {
+        auto next_masks = [&]() {
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < kTG; ++i) mn[i] = mload(k0 + kTG + i);
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        if (k0 >= kbeg) {  // uniform: stored steps (kbeg is a multiple of kRollGS)
+          const __amdgpu_buffer_rsrc_t ys = y_rsrc(k0);
+#pragma unroll
+          for (int i = 0; i < kTG; ++i) {
+            step2(mc[i]);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y), ys, yoff + (unsigned)(i * ra.ldy * 8), 0,
+                                                  kStoreAux);
+            if (i == 0) next_masks();
+          }
+        } else {  // before the range: integrate only
+#pragma unroll
+          for (int i = 0; i < kTG; ++i) {
+            if (INSITE_ABL_ROLL != 2) step2(mc[i]);
+            if (i == 0) next_masks();
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < kTG; ++i) mc[i] = mn[i];
+      }
+      return;
+    }
+  }
+#endif
   unsigned aring[kAG];
 #pragma unroll
-  for (int d = 0; d < kAG; ++d) aring[d] = grp_load(d * kRollGS);
+  for (int d = 0; d < kAG; ++d) aring[d] = PF ? pre->ar[d] : grp_load(d * kRollGS);
   for (int k0 = 0; k0 < kend;) {
 #pragma unroll
     for (int d = 0; d < kAG; ++d) {
@@ -2369,7 +2484,7 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
               __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y), ys, so, 0, kStoreAux);
             }
           }
-        } else {  // a group before the range: integrate only
+        } else if (INSITE_ABL_ROLL != 2) {  // a group before the range: integrate only
 #pragma unroll
           for (int i = 0; i < kRollGS; ++i) step((int)((wb >> i) & 1u));
         }
@@ -2584,9 +2699,39 @@ __global__ void __launch_bounds__(kBlock) refit_rollout_kernel(RolloutArgs ra, L
 #define INSITE_STEP_DYN_STATIC 500
 #endif
 // The bit-arm rollout of the (tile, arm group) units [q, q1) (tile-major), one rollout_bits_range per tile.
+// INSITE_ROLL_PF: every range's inputs requested one range ahead (RollPre), the coefficient rows once per wave.
+#ifndef INSITE_ROLL_PF
+#define INSITE_ROLL_PF 1
+#endif
 template <int METHOD>
 __device__ __forceinline__ void rollout_units(const RolloutArgs& ra, const LibDesc& lib, const int lane, int64_t q,
                                               const int64_t q1, const int ng) {
+#if INSITE_ROLL_PF
+  if (q >= q1) return;
+  double cv[2][INSITE_MAX_TERMS];
+  load_coef_rows<2>(lib, ra.coef, ra.A, cv);
+  int64_t tile = q / ng;
+  int gb = (int)(q - tile * ng);
+  int ge = q1 - q < (int64_t)(ng - gb) ? gb + (int)(q1 - q) : ng;
+  RollPre cur;
+  roll_pre_issue(ra, lib, lane, tile, ge, cur);
+  for (;;) {
+    const int64_t qn = q + (ge - gb);
+    const bool more = qn < q1;  // uniform
+    const int64_t tn = more ? qn / ng : 0;
+    const int gbn = (int)(qn - tn * ng);
+    const int gen = q1 - qn < (int64_t)(ng - gbn) ? gbn + (int)(q1 - qn) : ng;
+    RollPre nxt;
+    if (more) roll_pre_issue(ra, lib, lane, tn, gen, nxt);  // before this range's stores
+    rollout_bits_range<METHOD, 2, 0, false, true>(ra, lib, lane, tile, gb, ge, RefitArgs{}, &cur, &cv);
+    if (!more) break;
+    cur = nxt;
+    q = qn;
+    tile = tn;
+    gb = gbn;
+    ge = gen;
+  }
+#else
   while (q < q1) {
     const int64_t tile = q / ng;
     const int gb = (int)(q - tile * ng);
@@ -2594,6 +2739,7 @@ __device__ __forceinline__ void rollout_units(const RolloutArgs& ra, const LibDe
     rollout_bits_range<METHOD, 2, false>(ra, lib, lane, tile, gb, ge);
     q += ge - gb;
   }
+#endif
 }
 // The bit-arm rollout of the (tile, step) pairs [s, s1) (tile-major, T steps a tile): one step-range
 // rollout_bits_range per tile.  Every wave of the deferred step stores the same number of steps (+-1), where the
@@ -2863,6 +3009,13 @@ __device__ __forceinline__ int64_t xcd_rank(int64_t b, int64_t lo, int64_t hi) {
 #ifndef INSITE_LAG_MERGED
 #define INSITE_LAG_MERGED 1
 #endif
+#ifndef INSITE_DEF_ROVS
+#define INSITE_DEF_ROVS 1
+#endif
+// Profiling ablation only (tools/build_variant.sh): 1 = the gram role alone, 2 = the rollout role alone, 3 = both
+#ifndef INSITE_DEF_ROLES
+#define INSITE_DEF_ROLES 3
+#endif
 template <bool SMOOTH, int METHOD, int DYN = 0>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_STEP_WPE)))
 step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, const double* __restrict__ u,
@@ -2886,6 +3039,7 @@ step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, con
       if (DYN) __hip_atomic_store(hdr_cur + kDynRecDone, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (INSITE_DEF_GPRIO) __builtin_amdgcn_s_setprio(INSITE_DEF_GPRIO);
+    if (!(INSITE_DEF_ROLES & 1)) return;
     gram_body<1, 2, SMOOTH, true, true, 0, 7, DYN>((int)blockIdx.x, gblocks, smem, x, ldx, n_steps, u, arm,
                                                               rows, N, 0, 0, w, lib, part_cur, nullptr, out, &dg);
     return;
@@ -2918,6 +3072,7 @@ step_deferred_kernel(const double* __restrict__ x, int64_t ldx, int n_steps, con
     return;
   }
   int first = gblocks + 1;
+  if (!(INSITE_DEF_ROLES & 2)) return;
   if (lagged && !INSITE_LAG_MERGED) {
     if ((int)blockIdx.x == gblocks + 1) {
       if (G_fit) fit_from_gb<7>(G_fit, b_fit, fit);
@@ -4437,6 +4592,9 @@ static int32_t run_fit_rollout(const double* x, int64_t ldx, int32_t n_steps, co
     const bool dyn = n_patients > 0 && (INSITE_DEF_DYN == 1 ||
                                         (INSITE_DEF_DYN == 2 && units_all >= (int64_t)INSITE_DEF_DYN_MIN * gb * kWavesPerBlock));
     if (dyn) split(kd1, grid, gb);
+    // INSITE_DEF_ROVS > 1: the rollout blocks oversubscribe the resident round (shorter ranges, the dispatcher hands
+    // the later ones to whichever CU frees a slot first); y does not depend on the ranges (rollout_bits_range)
+    if (INSITE_DEF_ROVS > 1) grid = gb + nfin + (grid - gb - nfin) * INSITE_DEF_ROVS;
     char* wsb = static_cast<char*>(workspace);
     char* slots = wsb + kDefAreaBytes;
     double* part_cur = reinterpret_cast<double*>(slots + (size_t)slot * ws_one + kGramWsHeader);
