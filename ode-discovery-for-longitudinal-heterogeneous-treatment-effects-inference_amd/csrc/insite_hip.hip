@@ -2271,7 +2271,7 @@ __device__ __forceinline__ void roll_pre_issue(const RolloutArgs& ra, const LibD
   for (int t = 0; t < INSITE_MAX_STATICS; ++t) pr.u[t] = ra.u[pc * lib.U + (t < lib.U ? t : 0)];
   pr.y0 = ra.y0[pc];
   const int kend = g_end * kRollGS < ra.T ? g_end * kRollGS : ra.T;
-  if (INSITE_ROLL_SMASK && (ra.lda < 0 || 2 * tile + 1 < ra.lda)) return;  // (scalar step masks: no arm groups)
+  if (INSITE_ROLL_SMASK == 1 && (ra.lda < 0 || 2 * tile + 1 < ra.lda)) return;  // (scalar step masks: no arm groups)
 #pragma unroll
   for (int d = 0; d < kRollAG; ++d) pr.ar[d] = roll_arm_group_load(ra, tile, lane, d * kRollGS, kend);
 }
@@ -2400,7 +2400,7 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
     }
   };
 #endif
-#if INSITE_ROLL_SMASK && !defined(INSITE_ROLLOUT_STAGEWISE)
+#if INSITE_ROLL_SMASK == 1 && !defined(INSITE_ROLLOUT_STAGEWISE)
   if constexpr (NARM == 2 && !SR) {
     // A step's 64 arm bits of this tile (bit l = patient p0 + l: the two 32-patient words as they lie in either
     // layout) ARE the wave's lane mask for the arm-1 select: one scalar load per step straight into an SGPR pair,
@@ -2466,6 +2466,48 @@ __device__ __forceinline__ void rollout_bits_range(const RolloutArgs& ra, const 
   unsigned aring[kAG];
 #pragma unroll
   for (int d = 0; d < kAG; ++d) aring[d] = PF ? pre->ar[d] : grp_load(d * kRollGS);
+#if INSITE_ROLL_SMASK == 2 && !defined(INSITE_ROLLOUT_STAGEWISE)
+  if constexpr (NARM == 2) {
+    // the group's raw words as loaded (lane l: step l & 31, patients 32 (l >> 5) ..): step i's lane mask is lanes i
+    // and 32 + i, read into an SGPR pair (two v_readlane) -- the words arrive kAG groups ahead through the vector path
+    const double A0 = PA[0], A1 = PA[1], B0 = PB[0], B1 = PB[1];
+    auto step2 = [&](uint64_t m) {
+      const bool b = __builtin_amdgcn_inverse_ballot_w64(m);
+      const double y0 = fma(A0, y, B0), y1 = fma(A1, y, B1);
+      y = b ? y1 : y0;
+    };
+    auto mask_of = [&](unsigned wv, int i) -> uint64_t {
+      return (uint64_t)(unsigned)__builtin_amdgcn_readlane((int)wv, i) |
+             ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)wv, 32 + i) << 32);
+    };
+    for (int k0 = 0; k0 < kend;) {
+#pragma unroll
+      for (int d = 0; d < kAG; ++d) {
+        if (k0 < kend) {  // uniform
+          const unsigned wv = aring[d];
+          aring[d] = grp_load(k0 + kAG * kRollGS);
+          if (SR ? k0 + kRollGS > kbeg : k0 >= kbeg) {  // uniform: a stored group
+#pragma unroll
+            for (int hh = 0; hh < kRollGS / kTG; ++hh) {
+              const __amdgpu_buffer_rsrc_t ys = y_rsrc(k0 + hh * kTG);
+#pragma unroll
+              for (int i = 0; i < kTG; ++i) {
+                step2(mask_of(wv, hh * kTG + i));
+                const unsigned so = (!SR || k0 + hh * kTG + i >= kbeg) ? yoff + (unsigned)(i * ra.ldy * 8) : kOOB;
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y), ys, so, 0, kStoreAux);
+              }
+            }
+          } else if (INSITE_ABL_ROLL != 2) {
+#pragma unroll
+            for (int i = 0; i < kRollGS; ++i) step2(mask_of(wv, i));
+          }
+          k0 += kRollGS;
+        }
+      }
+    }
+    return;
+  }
+#endif
   for (int k0 = 0; k0 < kend;) {
 #pragma unroll
     for (int d = 0; d < kAG; ++d) {
