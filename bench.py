@@ -121,6 +121,9 @@ def parse():
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "insite", "insite4", "f4", "ns"],
                     help="c2: BASELINE configs[1], the headline line (default); c3: configs[2], the 5-state fp32 "
                          "system (parity-test configuration, measured separately)")
+    ap.add_argument("--insite-order", default="nfev", choices=["seq_len", "nfev"],
+                    help="insite line: lanes binned by the row's window (seq_len) or by window and the previous "
+                         "step's evaluation counts (nfev)")
     ap.add_argument("--insite-only-binned", action="store_true",
                     help="--config insite: time only the product route (skip the identity-order and prepare-route "
                          "comparisons; for counter runs)")
@@ -1132,7 +1135,8 @@ def insite_main(args):
 
     # the product's binned path as a prepared plan: the seq_len sort and the refinement on the patient-major rows
     # (insite_refine_rows_f64, ABI 9: 2 C calls, no host synchronisation) inside every step
-    plan = ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5)
+    # --insite-order nfev (default): the lanes binned by window AND by the evaluation counts of the previous step
+    plan = ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, order=args.insite_order)
     plan_prep = ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, dt, 10.0, 5, rows=False)   # ABI 8 route
 
     def run(mode):   # "binned": rows binned by seq_len on the device (inside every step)
@@ -1167,7 +1171,7 @@ def insite_main(args):
     kst = torch.cuda.current_stream(dev)
     # the kernel's call index in the plan: [sort, rows kernel] in rows mode, [sort, prepare, kernel, finish] when the
     # row kernel refused the shape (prepare mode)
-    kidx_ins = {"rows": 1, "prepare": 2}[plan.mode]
+    kidx_ins = plan.kernel_call
 
     def kern():
         plan.call(kidx_ins, kst)
@@ -1187,6 +1191,8 @@ def insite_main(args):
     order = plan_nf.order.long()           # lane -> row: the waves as the kernel formed them
     torch.cuda.synchronize(dev)
     same = bool(torch.equal(s2, status) and torch.equal(i2, iters) and torch.equal(p2, preds))
+    if plan.nfev is not None:              # nfev binning: the timed plan's own waves (its order, its counts)
+        order, nf_row = plan.order.long(), plan.nfev
     nf = nf_row[order]
     K = torch.clamp(sl[order].to(torch.int64) - 5, min=0, max=T - 1)
     # SIMT divergence of the refinement: a wave runs until its slowest lane's last scan, each scan as long as its
@@ -1219,10 +1225,14 @@ def insite_main(args):
                                f"{N // 1000}k rows", "rows": N, "T": T},
         "insite": {"refined_rows": int((st >= 0).sum()), "converged": int((st == 0).sum()),
                    "zoom_failed_fallback": int((st == 3).sum()), "mean_bfgs_iterations": float(it[st >= 0].mean()),
-                   "lane_order": "rows binned by seq_len (device counting sort); the kernel gathers its lanes' "
-                                 "patient-major rows through its LDS ring and stores the predictions as row "
-                                 "segments (insite_refine_rows_f64; ops.plan_insite_refine: 2 C calls per step, "
+                   "lane_order": ("rows binned by seq_len (device counting sort)" if args.insite_order == "seq_len"
+                                  else "rows binned by seq_len (64 levels) and then by the evaluation counts the "
+                                       "previous step left (16 levels; one device counting sort over the combined "
+                                       "key)") +
+                                 "; the kernel gathers its lanes' patient-major rows through its LDS ring and stores "
+                                 "the predictions as row segments (insite_refine_rows_f64; ops.plan_insite_refine, "
                                  "no host sync)",
+                   "lane_order_key": args.insite_order,
                    "plan_equals_eager": plan_eq,
                    "identity_lane_order_ms_per_step": ms_identity,
                    "reference_wall_time_s": "88.96 s per INSITE EQ_4_A run incl. 59,000 + 11,800 refinements "

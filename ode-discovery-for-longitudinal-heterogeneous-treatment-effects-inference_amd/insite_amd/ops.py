@@ -1156,8 +1156,10 @@ class InsiteRefinePlan:
     to its inputs: refresh them in place between calls (a serving loop) or make a new plan."""
 
     def __init__(self, V, arm, u, seq_len, coef0, lib, dt, lam, tau, substeps=5, revert_on_zoom_fail=False,
-                 rows=None, nfev=None):
+                 rows=None, nfev=None, order="seq_len"):
         L = _lib.load()
+        if order not in ("seq_len", "nfev"):
+            raise ValueError("order must be 'seq_len' or 'nfev'")
         _dev("V", V, torch.float64, 2)
         _dev("arm", arm, torch.int8, 2)
         N, T = V.shape
@@ -1185,7 +1187,6 @@ class InsiteRefinePlan:
         self.order = torch.empty((N,), dtype=torch.int32, device=dev)
         self._ows = Workspace("scratch").get(L.insite_rk45_order_workspace_bytes(int(T)), dev)
         self._c0, self._mask, self._qexps, self._tab = c0, mask, qexps, lib.ctypes_table()
-        self._keep = (V, arm, u, seq_len, nfev)
         self.device = dev
         order_call = (L.insite_rk45_order_i32, (_p(seq_len), N, int(T), _p(self.order), _p(self._ows),
                                                 self._ows.numel()))
@@ -1193,6 +1194,32 @@ class InsiteRefinePlan:
             _dev("nfev", nfev, torch.int32, 1)
             if nfev.numel() != N:
                 raise ValueError("nfev must have one entry per row")
+        key_call = None
+        self.nfev = None   # (order="nfev": the evaluation counts the binning key reads, rewritten by every call)
+        if order == "nfev":
+            # lanes binned by the window (seq_len, 64 levels) and then by the evaluation counts the previous call left
+            # in ``nfev`` (16 levels): a wave runs until its longest row's last objective scan, so rows of equal window
+            # AND equal evaluation count belong together (the C5 line's attempt binning; a refined set that is refined
+            # again -- the bench step, a serving loop -- takes the same counts).  Outputs do not depend on the lane
+            # order (tested); the first call bins on zero counts, i.e. by seq_len alone.
+            if rows is False or not bits:
+                raise ValueError("order='nfev' needs the row-layout plan")
+            if nfev is None:
+                nfev = torch.zeros((N,), dtype=torch.int32, device=dev)
+            self._key = torch.empty((N,), dtype=torch.int32, device=dev)
+            key, sl_, nf_, Tq = self._key, seq_len, nfev, max(int(T), 1)
+            kws = Workspace("scratch").get(L.insite_rk45_order_workspace_bytes(RK45_ATTEMPT_BINS - 1), dev)
+            self._kws = kws
+
+            def key_fn(s):   # key = window level * 16 + min(nfev / 2, 15) in [0, 1024), on the plan's stream s
+                with torch.cuda.stream(s):
+                    q = torch.clamp(sl_, 0, Tq).mul_(63).floor_divide_(Tq).mul_(16)
+                    torch.add(q, torch.clamp(nf_ >> 1, 0, 15), out=key)
+            key_call = (key_fn, None)
+            self.nfev = nfev
+            order_call = (L.insite_rk45_order_i32, (_p(key), N, RK45_ATTEMPT_BINS - 1, _p(self.order), _p(kws),
+                                                    kws.numel()))
+        self._keep = (V, arm, u, seq_len, nfev)
         if rows is not False and bits:
             outs = (torch.empty((N, T), dtype=torch.float64, device=dev),
                     torch.empty((N,) + c0.shape, dtype=torch.float64, device=dev),
@@ -1201,7 +1228,8 @@ class InsiteRefinePlan:
                 # the row layout (ABI 9): two C calls, the counting sort and the refinement on the rows themselves
                 self.mode = "rows"
                 self.out = outs
-                self._calls = [order_call, (L.insite_refine_rows_f64, _refine_rows_call(
+                self.kernel_call = 2 if key_call else 1   # (the refinement kernel's index in _calls)
+                self._calls = ([key_call] if key_call else []) + [order_call, (L.insite_refine_rows_f64, _refine_rows_call(
                     V, arm, u, seq_len, c0, mask, qexps, A, lib, dt, lam, tau, substeps, revert_on_zoom_fail, outs,
                     nfev, self.order))]
                 return
@@ -1210,6 +1238,7 @@ class InsiteRefinePlan:
         if nfev is not None:
             raise ValueError("nfev needs the row-layout plan")
         self.mode = "prepare"
+        self.kernel_call = 2
         ldt = N + (N & 1)   # even leading dimension (the windowed kernels' 16-B ring loads)
         self.Vt = torch.empty((T, ldt), dtype=torch.float64, device=dev)[:, :N]
         self.arms = torch.empty((T, W) if bits else (T, N), dtype=torch.int32 if bits else torch.int8, device=dev)
@@ -1254,18 +1283,24 @@ class InsiteRefinePlan:
 
     def call(self, i: int, stream: torch.cuda.Stream | None = None):
         """Enqueue the plan's i-th C call alone (bench.py times the refinement kernel this way)."""
-        h = ctypes.c_void_p((stream if stream is not None else torch.cuda.current_stream(self.device)).cuda_stream)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
         fn, args = self._calls[i]
-        st = fn(*args, h)
+        if args is None:   # a torch step (the nfev binning key): its ops on the same stream
+            fn(s)
+            return
+        st = fn(*args, ctypes.c_void_p(s.cuda_stream))
         if st:
             _lib.check(getattr(fn, "__name__", "insite refine plan"), st)
 
 
 def plan_insite_refine(V, arm, u, seq_len, coef0, lib, dt, lam, tau, substeps=5, revert_on_zoom_fail=False,
-                       rows=None, nfev=None):
+                       rows=None, nfev=None, order="seq_len"):
     """``insite_refine`` (binned lane order) as a prepared plan (``InsiteRefinePlan``).  ``rows`` as in
-    ``insite_refine``; ``nfev`` (row layout only) an int32 [N] tensor receiving each row's evaluation count."""
-    return InsiteRefinePlan(V, arm, u, seq_len, coef0, lib, dt, lam, tau, substeps, revert_on_zoom_fail, rows, nfev)
+    ``insite_refine``; ``nfev`` (row layout only) an int32 [N] tensor receiving each row's evaluation count;
+    ``order`` "seq_len" (lanes binned by the row's window) or "nfev" (by the window, then by the evaluation counts
+    the previous call left in ``nfev``)."""
+    return InsiteRefinePlan(V, arm, u, seq_len, coef0, lib, dt, lam, tau, substeps, revert_on_zoom_fail, rows, nfev,
+                            order)
 
 
 def refine_prepare(V: torch.Tensor, arm: torch.Tensor, bits: bool = True, order: torch.Tensor | None = None,

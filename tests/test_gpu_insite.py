@@ -429,6 +429,18 @@ def test_refine_rows_layout_equals_prepare_route(dev, N, T, ld, m):
     torch.cuda.synchronize()
     for a, b in zip(got, p):
         assert torch.equal(a, b)
+    # lanes binned by window and the previous call's evaluation counts (the insite line's default order): the first
+    # call bins on zero counts, the next ones on the counts the previous call wrote -- every call's outputs bitwise
+    # those of the seq_len order, the counts those of the eager route
+    nplan = ops.plan_insite_refine(V, arm, coh.u, sl, c0, coh.lib, 10.0 / T, 10.0, 5, order="nfev")
+    assert nplan.mode == "rows" and nplan.kernel_call == 2
+    for _ in range(3):
+        got = nplan()
+        torch.cuda.synchronize()
+        for a, b in zip(got, p):
+            assert torch.equal(a, b)
+        assert torch.equal(nplan.nfev, nf_p)
+        assert torch.equal(torch.sort(nplan.order).values, torch.arange(N, device=dev, dtype=torch.int32))
 
 
 def test_refine_rows_unsupported_shapes_fall_back(dev):
