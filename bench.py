@@ -1411,7 +1411,7 @@ def insite4_main(args):
     st_ = torch.cuda.current_stream(dev)
     res = {}
     for name, (c0, lb) in models.items():
-        plan = ops.plan_insite_refine(V, arm, u, sl, c0, lb, dt, 10.0, 5)
+        plan = ops.plan_insite_refine(V, arm, u, sl, c0, lb, dt, 10.0, 5, order=args.insite_order)
         for _ in range(args.warmup):
             plan()
         torch.cuda.synchronize(dev)
@@ -1420,7 +1420,7 @@ def insite4_main(args):
             preds, coef, status, iters = plan()
         torch.cuda.synchronize(dev)
         ms = (time.perf_counter() - t0) / args.steps * 1e3
-        kidx = len(plan._calls) - 2              # [sort, prepare, kernel, finish]
+        kidx = plan.kernel_call                  # [(key,) sort, prepare, kernel, finish(, nfev scatter)]
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st_)
         for _ in range(args.steps):
@@ -1438,6 +1438,7 @@ def insite4_main(args):
         stn = status.cpu().numpy()
         m_act = int((np.abs(c0) > 1e-3).sum())
         res[name] = {"active_coefficients": m_act, "ms_per_step": ms, "kernel_ms": kern_ms,
+                     "lane_order_key": args.insite_order,
                      "kernel": ("insite_refine_coop_kernel<16, 4>" if 8 < m_act <= 16 and os.environ.get("INSITE_REFINE_COOP", "1") != "0"
                                 else f"insite_refine_kernel<{2 if m_act <= 2 else 3 if m_act == 3 else 4 if m_act <= 4 else 6 if m_act <= 6 else 8 if m_act <= 8 else 16 if m_act <= 16 else 36}, 4, 1>"),
                      "valu_f64_TFLOPs": flop / (kern_ms * 1e-3) / 1e12,

@@ -1202,8 +1202,6 @@ class InsiteRefinePlan:
             # AND equal evaluation count belong together (the C5 line's attempt binning; a refined set that is refined
             # again -- the bench step, a serving loop -- takes the same counts).  Outputs do not depend on the lane
             # order (tested); the first call bins on zero counts, i.e. by seq_len alone.
-            if rows is False or not bits:
-                raise ValueError("order='nfev' needs the row-layout plan")
             if nfev is None:
                 nfev = torch.zeros((N,), dtype=torch.int32, device=dev)
             self._key = torch.empty((N,), dtype=torch.int32, device=dev)
@@ -1235,10 +1233,13 @@ class InsiteRefinePlan:
                 return
             if rows:
                 raise ValueError("insite_refine_rows_f64 does not take this model / layout (INSITE_E_UNSUPPORTED)")
-        if nfev is not None:
-            raise ValueError("nfev needs the row-layout plan")
+        if nfev is not None and key_call is None:
+            raise ValueError("nfev needs the row-layout plan (or order='nfev')")
         self.mode = "prepare"
-        self.kernel_call = 2
+        self.kernel_call = 3 if key_call else 2
+        # order="nfev": the kernel counts evaluations per lane (the general entry point, the same kernels), a last
+        # torch step scatters them to row order for the next call's key
+        self.nf_lane = torch.zeros((N,), dtype=torch.int32, device=dev) if key_call else None
         ldt = N + (N & 1)   # even leading dimension (the windowed kernels' 16-B ring loads)
         self.Vt = torch.empty((T, ldt), dtype=torch.float64, device=dev)[:, :N]
         self.arms = torch.empty((T, W) if bits else (T, N), dtype=torch.int32 if bits else torch.int8, device=dev)
@@ -1251,7 +1252,7 @@ class InsiteRefinePlan:
         self.out = (torch.empty((N, T), dtype=torch.float64, device=dev), torch.empty_like(self.coef_l),
                     torch.empty_like(self.st_l), torch.empty_like(self.it_l))
         nul = ctypes.c_void_p(0)
-        self._calls = [
+        self._calls = ([key_call] if key_call else []) + [
             order_call,
             (L.insite_refine_prepare_f64, (_p(V), V.stride(0), _p(arm), arm.stride(0), N, T, _p(self.Vt), ldt,
                                            _p(self.arms) if bits else nul, W, nul if bits else _p(self.arms), N,
@@ -1261,11 +1262,12 @@ class InsiteRefinePlan:
         common = (float(dt), float(lam), int(tau), int(substeps), int(bool(revert_on_zoom_fail)), _p(self.P), N,
                   _p(self.coef_l), _p(self.st_l), _p(self.it_l))
         ustat = _p(self.u_l) if U else nul
-        if lib.n_inputs:
+        if lib.n_inputs or key_call:
             self._calls.append((L.insite_refine_general_f64, (
                 _p(self.Vt), ldt, T, _p(self.arms) if bits else nul, nul if bits else _p(self.arms), self.arms.stride(0),
                 ustat, _p(self.sl_l), N, U, c0.size, c0.ctypes.data_as(ctypes.c_void_p),
-                mask.ctypes.data_as(ctypes.c_void_p), qexps.ctypes.data_as(ctypes.c_void_p), A) + common + (nul, nul)))
+                mask.ctypes.data_as(ctypes.c_void_p), qexps.ctypes.data_as(ctypes.c_void_p), A) + common +
+                (_p(self.nf_lane) if key_call else nul, nul)))
         else:
             fn = L.insite_refine_f64 if bits else L.insite_refine_arms_f64
             self._calls.append((fn, (_p(self.Vt), ldt, T, _p(self.arms), self.arms.stride(0), ustat, _p(self.sl_l), N, U,
@@ -1275,6 +1277,13 @@ class InsiteRefinePlan:
         self._calls.append((L.insite_refine_finish_f64, (_p(self.P), N, _p(self.order), N, T, _p(P_), T,
                                                          _p(self.coef_l), int(c0.size), _p(co), _p(self.st_l), _p(so),
                                                          _p(self.it_l), _p(io))))
+        if key_call:
+            nf_row, nf_l, ordr = self.nfev, self.nf_lane, self.order
+
+            def nfev_scatter(s):   # lane counts -> row order (the next call's key)
+                with torch.cuda.stream(s):
+                    nf_row.index_copy_(0, ordr.long(), nf_l)
+            self._calls.append((nfev_scatter, None))
 
     def __call__(self, stream: torch.cuda.Stream | None = None):
         for i in range(len(self._calls)):

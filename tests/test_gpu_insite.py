@@ -561,6 +561,17 @@ def test_cooperative_dense_refine_equals_single_lane(dev, monkeypatch, N, joint,
     assert (outs["1"][2][sl <= 5] == -1).all() and (outs["1"][2][sl > 5] >= 0).all()
     for a, b in zip(outs["1"], outs["0"]):
         assert torch.equal(a, b)
+    # the 4-arm line's plan (prepare route) with its lanes binned by window and the previous call's evaluation
+    # counts: three consecutive calls, outputs and row-order counts bitwise those of the eager route
+    monkeypatch.setenv("INSITE_REFINE_COOP", "1")
+    nplan = ops.plan_insite_refine(V, arm, coh.u, sl, c0, lib, coh.dt, 10.0, 5, order="nfev")
+    assert nplan.mode == "prepare" and nplan.kernel_call == 3
+    for _ in range(3):
+        got = nplan()
+        torch.cuda.synchronize()
+        for a, b in zip(got, outs["1"][:4]):
+            assert torch.equal(a, b)
+        assert torch.equal(nplan.nfev, outs["1"][4])
 
 
 def test_refine_rows_on_bench_cohort_sampled_against_oracle(dev):
