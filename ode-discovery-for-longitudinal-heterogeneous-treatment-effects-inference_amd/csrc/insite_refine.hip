@@ -1621,11 +1621,15 @@ __device__ __forceinline__ double grp_tree_sum(double v) {
   v = v + grp_xor<4>(v);
   return 0.0 + v;
 }
-template <int MC, int NA, bool STG>
+// PM (the row layout, insite_refine_rows_f64): V [N, ldv] and arm8 [N, lda] patient-major, staged by whole rows (lane
+// = step: one coalesced row read per staged row), predictions stored into the patient-major rows; every other output
+// is indexed by the row already (p = row_order[lane-order row]), so no gather / scatter pass surrounds the kernel
+template <int MC, int NA, bool STG, bool PM = false>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(INSITE_REFINE_COOP_WPE)))
 insite_refine_coop_kernel(RefineArgs) {
   constexpr int S = MC / kCoopG;  // coordinates per lane: i = j + kCoopG s
   static_assert(MC % kCoopG == 0 && NA * 2 <= kCoopG, "one tangent per lane");
+  static_assert(!PM || STG, "the row layout stages its rows (T <= kCoopStT)");
   KArgs& ra = kernel_args();
   const int lane = threadIdx.x & (kWave - 1);
   const int j = lane & (kCoopG - 1);
@@ -1664,10 +1668,10 @@ insite_refine_coop_kernel(RefineArgs) {
     if (lane < ra.T) {
 #pragma unroll
       for (int g = 0; g < kCoopG; ++g) {
-        wV[lane * kCoopG + g] = ra.V[(int64_t)lane * ra.ldv + pg[g]];
+        wV[lane * kCoopG + g] = PM ? ra.V[pg[g] * ra.ldv + lane] : ra.V[(int64_t)lane * ra.ldv + pg[g]];
         // the arm clamped to [0, NA) (the documented contract; an out-of-range byte must not index another row's
         // or another wave's constants -- ADVICE r05)
-        const int8_t a8 = ra.arm8[(int64_t)lane * ra.lda + pg[g]];
+        const int8_t a8 = PM ? ra.arm8[pg[g] * ra.lda + lane] : ra.arm8[(int64_t)lane * ra.lda + pg[g]];
         const int8_t am = a8 < 0 ? (int8_t)0 : a8 >= NA ? (int8_t)(NA - 1) : a8;
         wA[lane * kCoopG + g] = am;
         if constexpr (kPipe) wO[lane * kCoopG + g] = (g * NA + am) * kCf5 * (int)sizeof(double);
@@ -2372,7 +2376,7 @@ insite_refine_coop_kernel(RefineArgs) {
         gk1 = gam[a][1];
       }
     for (int s = 0; s < ra.sub; ++s) y = y + h * (gk0 + gk1 * y);
-    if ((kk & (kCoopG - 1)) == j) ra.preds[(int64_t)kk * ra.ldp + p] = y;
+    if ((kk & (kCoopG - 1)) == j) ra.preds[PM ? p * ra.ldp + kk : (int64_t)kk * ra.ldp + p] = y;
   }
   if (ra.coef_out)
     for (int q = j; q < ra.n_coef; q += kCoopG) ra.coef_out[p * ra.n_coef + q] = coef_at(q);
@@ -2462,7 +2466,10 @@ void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
     else if (m <= 16) {
       const char* cv = getenv("INSITE_REFINE_COOP");
       const bool coop = cv ? cv[0] == '1' : INSITE_REFINE_COOP != 0;
-      if (NA == 4 && coop) {  // the dense 4-arm models (int8 arms): 8 lanes per row
+      if (NA == 4 && ra.pm) {  // the row layout (refine_launch admitted it: coop, T <= kCoopStT)
+        const dim3 gc((unsigned)((ra.N * kCoopG + kBlock - 1) / kBlock));
+        insite_refine_coop_kernel<16, 4, true, true><<<gc, kBlock, 0, hs>>>(ra);
+      } else if (NA == 4 && coop) {  // the dense 4-arm models (int8 arms): 8 lanes per row
         const dim3 gc((unsigned)((ra.N * kCoopG + kBlock - 1) / kBlock));
         if (ra.T <= kCoopStT) insite_refine_coop_kernel<16, 4, true><<<gc, kBlock, 0, hs>>>(ra);
         else insite_refine_coop_kernel<16, 4, false><<<gc, kBlock, 0, hs>>>(ra);
@@ -2489,7 +2496,7 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
   const bool bits = arm8 == nullptr;
   // pm: the row layout of insite_refine_rows_f64 (patient-major V / arm8 / preds, leading dimensions >= T)
   const int64_t ld_min = pm ? T : n_rows;
-  if (n_rows < 0 || T < 1 || n_arms < 1 || n_arms > (bits || pm ? 2 : 4) || substeps < 1 || !(dt > 0.0) ||
+  if (n_rows < 0 || T < 1 || n_arms < 1 || n_arms > (bits ? 2 : 4) || substeps < 1 || !(dt > 0.0) ||
       !(lam >= 0.0) || tau < 0 || ld_v < ld_min || ld_p < ld_min || n_statics < 0 ||
       n_statics > INSITE_MAX_STATICS || ld_arm < (pm ? T : (bits ? (n_rows + 31) / 32 : n_rows)) || !coef0 ||
       !mask || !exps || n_coef < 1 || (pm && bits))
@@ -2525,8 +2532,14 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
       for (int a = 0; a < n_arms; ++a)
         if ((ra.t_mask[i] >> a) & 1) ra.gmap |= 1 << (i * 8 + a * 2 + (ra.t_ex[i] & 1));
   }
-  if (pm && (D != 1 || m > 3 || T < 2 || T > 64 || (ld_v & 1) || ((uintptr_t)V & 15u) || n_rows > INT32_MAX))
+  if (pm && n_arms <= 2 &&
+      (D != 1 || m > 3 || T < 2 || T > 64 || (ld_v & 1) || ((uintptr_t)V & 15u) || n_rows > INT32_MAX))
     return INSITE_E_UNSUPPORTED;  // the windowed row kernel's shape (the reference's sequences: T <= 64, <= 3 active)
+  if (pm && n_arms > 2) {  // 3-4 arms: the cooperative kernel on the rows (the dense models, 9-16 active terms)
+    const char* cv = getenv("INSITE_REFINE_COOP");
+    const bool coop = cv ? cv[0] == '1' : INSITE_REFINE_COOP != 0;
+    if (D != 1 || m <= 8 || m > 16 || !coop || T > kCoopStT || n_rows > INT32_MAX) return INSITE_E_UNSUPPORTED;
+  }
   if (n_rows == 0) return INSITE_OK;
   if (!V || (bits && !arm_bits) || !seq_len || !preds || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;
   ra.V = V;
@@ -2558,7 +2571,7 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
   ra.st16 = ((uintptr_t)preds & 15u) == 0 && (ld_p & 1) == 0;
   const dim3 grid((unsigned)((n_rows + kBlock - 1) / kBlock));
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
-  if (bits || pm) {
+  if (bits || (pm && n_arms <= 2)) {
     if (D == 1) launch_refine<2, 1>(ra, grid, hs);
     else launch_refine<2, 4>(ra, grid, hs);
   } else {

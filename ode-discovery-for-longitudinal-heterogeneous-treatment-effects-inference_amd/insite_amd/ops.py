@@ -1050,7 +1050,7 @@ def _refine_rows_call(V, arm, u, seq_len, c0, mask, qexps, A, lib, dt, lam, tau,
 def refine_rows_supported(V, arm, u, seq_len, c0, mask, qexps, A, lib, outs) -> bool:
     """Whether insite_refine_rows_f64 takes this model and layout: the library's own answer, asked with zero rows
     (argument and shape checks only, nothing launched).  INSITE_REFINE_ROWS=0 in the environment says no."""
-    if A > 2 or os.environ.get("INSITE_REFINE_ROWS", "1") == "0":
+    if A > 4 or os.environ.get("INSITE_REFINE_ROWS", "1") == "0":
         return False
     args = _refine_rows_call(V, arm, u, seq_len, c0, mask, qexps, A, lib, 1.0, 0.0, 0, 1, False, outs, None, None,
                              n_rows=0)
@@ -1103,7 +1103,7 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
     mask, qexps, A = refine_terms(lib, c0.shape[0])
     if A > 4:
         raise ValueError("at most 4 treatment arms (joint model: 2 binary treatment inputs)")
-    if rows is not False and A <= 2:
+    if rows is not False:   # (A <= 2: the windowed kernels; 3-4 arms: the cooperative kernel of the dense models)
         if lib.n_statics and u.size(0) != N:
             raise ValueError("u must have one row per refined row")
         if seq_len.numel() != N:
@@ -1117,7 +1117,7 @@ def insite_refine(V: torch.Tensor, arm: torch.Tensor, u: torch.Tensor, seq_len: 
                 torch.empty((N,), dtype=torch.int32, device=V.device), torch.empty((N,), dtype=torch.int32, device=V.device))
         if N and V.stride(1) == 1 and arm.stride(1) == 1 and \
                 refine_rows_supported(V, arm, u, seq_len, c0, mask, qexps, A, lib, outs):
-            if int(arm.amax().item()) > 1:
+            if A <= 2 and int(arm.amax().item()) > 1:
                 raise ValueError("two-arm models need arm values 0/1")
             order = rk45_order(seq_len, T) if (binned and N > 64) else None
             args = _refine_rows_call(V, arm, u, seq_len, c0, mask, qexps, A, lib, dt, lam, tau, substeps,
@@ -1218,7 +1218,7 @@ class InsiteRefinePlan:
             order_call = (L.insite_rk45_order_i32, (_p(key), N, RK45_ATTEMPT_BINS - 1, _p(self.order), _p(kws),
                                                     kws.numel()))
         self._keep = (V, arm, u, seq_len, nfev)
-        if rows is not False and bits:
+        if rows is not False:   # (3-4 arms: the cooperative kernel's row layout where the library takes the model)
             outs = (torch.empty((N, T), dtype=torch.float64, device=dev),
                     torch.empty((N,) + c0.shape, dtype=torch.float64, device=dev),
                     torch.empty((N,), dtype=torch.int32, device=dev), torch.empty((N,), dtype=torch.int32, device=dev))

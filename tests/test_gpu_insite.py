@@ -561,11 +561,17 @@ def test_cooperative_dense_refine_equals_single_lane(dev, monkeypatch, N, joint,
     assert (outs["1"][2][sl <= 5] == -1).all() and (outs["1"][2][sl > 5] >= 0).all()
     for a, b in zip(outs["1"], outs["0"]):
         assert torch.equal(a, b)
-    # the 4-arm line's plan (prepare route) with its lanes binned by window and the previous call's evaluation
-    # counts: three consecutive calls, outputs and row-order counts bitwise those of the eager route
+    # the cooperative kernel on the reference's own rows (insite_refine_rows_f64 with 4 arms, T <= 64) against its
+    # prepare / kernel / finish route, and the 4-arm line's plan with its lanes binned by window and the previous
+    # call's evaluation counts: three consecutive calls, outputs and row-order counts bitwise those of the eager route
     monkeypatch.setenv("INSITE_REFINE_COOP", "1")
+    nf_p = torch.empty((N,), dtype=torch.int32, device=dev)
+    rp = ops.insite_refine(V, arm, coh.u, sl, c0, lib, coh.dt, 10.0, 5, nfev=nf_p, rows=False)
+    torch.cuda.synchronize()
+    for a, b in zip(rp + (nf_p,), outs["1"]):
+        assert torch.equal(a, b)
     nplan = ops.plan_insite_refine(V, arm, coh.u, sl, c0, lib, coh.dt, 10.0, 5, order="nfev")
-    assert nplan.mode == "prepare" and nplan.kernel_call == 3
+    assert (nplan.mode, nplan.kernel_call) == (("rows", 2) if T <= 64 else ("prepare", 3))
     for _ in range(3):
         got = nplan()
         torch.cuda.synchronize()

@@ -6,12 +6,14 @@ cd $GRAFT_REPO_ROOT
 O=gpurun_out/r06_insite4${TAG}
 mkdir -p $O
 if [ -z "$NOTEST" ]; then
-timeout -k 10 600 python -u -m pytest tests/test_gpu_insite.py tests/test_gpu_refine_general.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_insite.py tests/test_gpu_refine_general.py tests/test_gpu_reference_segments.py tests/test_gpu_plugin.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
 tail -2 $O/tests.txt
 fi
 for rep in $(seq 1 ${REPS:-1}); do
-  for o in seq_len nfev; do
-    timeout -k 10 600 python bench.py --config insite4 --no-cpu-baseline ${EXTRA:-} --insite-order $o > $O/insite4_${o}_$rep.jsonl 2> $O/insite4_${o}_$rep.err || { echo "insite4 $o failed"; tail -5 $O/insite4_${o}_$rep.err; exit 1; }
+  for o in ${ORDERS:-seq_len nfev}; do
+    ENVP=""; oo=$o
+    if [ "$o" = nfev_prep ]; then ENVP="INSITE_REFINE_ROWS=0"; oo=nfev; fi
+    env $ENVP timeout -k 10 600 python bench.py --config insite4 --no-cpu-baseline ${EXTRA:-} --insite-order $oo > $O/insite4_${o}_$rep.jsonl 2> $O/insite4_${o}_$rep.err || { echo "insite4 $o failed"; tail -5 $O/insite4_${o}_$rep.err; exit 1; }
     python3 -c "
 import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); m=d.get('models') or d.get('insite4') or {}
 for k,v in (m.items() if isinstance(m,dict) else []):
