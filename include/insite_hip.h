@@ -476,12 +476,15 @@ int32_t insite_refine_general_f64(const double* V, int64_t ld_v, int32_t T, cons
  * BFGS, status, outputs bitwise equal), without the prepare / finish passes: the windowed kernel gathers the rows of
  * its lanes (row_order: lane l refines row row_order[l], NULL = identity) straight from V through its LDS ring and
  * stores the predictions through the same ring as 64-B row segments.
- *   V [n_rows, ld_v] f64, ld_v even and V 16-B aligned; arm [n_rows, ld_arm] int8 with values 0 / 1 (n_arms <= 2);
+ *   V [n_rows, ld_v] f64, ld_v even and V 16-B aligned; arm [n_rows, ld_arm] int8 with values 0 / 1 (n_arms <= 2)
+ *   or in [0, n_arms) (n_arms 3-4: the dense 4-arm and joint models, 9-16 active coefficients, on the cooperative
+ *   kernel -- 8 lanes a row, the wave's 8 rows staged whole from V and arm, predictions stored into the rows; round 6);
  *   u [n_rows, n_statics], seq_len [n_rows]; preds [n_rows, ld_p], coef_out [n_rows, n_coef], status_out / iters_out
  *   / nfev_out [n_rows] -- every per-row array in ROW order.  ld_v, ld_arm, ld_p >= T.
- * Returns INSITE_E_UNSUPPORTED outside the windowed kernel's shape (T not in [2, 64], more than 3 active
- * coefficients, a state exponent >= 2 in the model, odd ld_v / unaligned V): the caller then takes the
- * prepare / insite_refine_general_f64 / finish route, which covers every model.
+ * Returns INSITE_E_UNSUPPORTED outside these kernels' shapes (n_arms <= 2: T not in [2, 64], more than 3 active
+ * coefficients, odd ld_v / unaligned V; n_arms 3-4: T > 64, not 9-16 active coefficients, INSITE_REFINE_COOP=0; either:
+ * a state exponent >= 2 in the model): the caller then takes the prepare / insite_refine_general_f64 / finish route,
+ * which covers every model.
  * Concurrency: the opt-in dynamic row assignment (INSITE_REFINE_DYN=1 in the environment; off by default) takes its
  * queue heads from 64 device words handed out round-robin per call, so at most 64 such calls may be in flight at
  * once across independent streams -- a 65th shares a head with a running call (rows skipped or refined twice).  The
