@@ -2455,7 +2455,10 @@ void launch_refine(const RefineArgs& ra, dim3 grid, hipStream_t hs) {
     else if (m <= 8) {
       const char* cv = getenv("INSITE_REFINE_COOP8");
       const bool coop = cv ? cv[0] == '1' : INSITE_REFINE_COOP8 != 0;
-      if (NA == 4 && coop) {  // the sparse 4-arm models with 5-8 active terms: 8 lanes per row, one coordinate a lane
+      if (NA == 4 && ra.pm) {  // the row layout (refine_launch admitted it: COOP8, T <= kCoopStT)
+        const dim3 gc((unsigned)((ra.N * kCoopG + kBlock - 1) / kBlock));
+        insite_refine_coop_kernel<8, 4, true, true><<<gc, kBlock, 0, hs>>>(ra);
+      } else if (NA == 4 && coop) {  // the sparse 4-arm models with 5-8 active terms: 8 lanes per row, one coordinate a lane
         const dim3 gc((unsigned)((ra.N * kCoopG + kBlock - 1) / kBlock));
         if (ra.T <= kCoopStT) insite_refine_coop_kernel<8, 4, true><<<gc, kBlock, 0, hs>>>(ra);
         else insite_refine_coop_kernel<8, 4, false><<<gc, kBlock, 0, hs>>>(ra);
@@ -2535,10 +2538,12 @@ int32_t refine_launch(const double* V, int64_t ld_v, int32_t T, const uint32_t* 
   if (pm && n_arms <= 2 &&
       (D != 1 || m > 3 || T < 2 || T > 64 || (ld_v & 1) || ((uintptr_t)V & 15u) || n_rows > INT32_MAX))
     return INSITE_E_UNSUPPORTED;  // the windowed row kernel's shape (the reference's sequences: T <= 64, <= 3 active)
-  if (pm && n_arms > 2) {  // 3-4 arms: the cooperative kernel on the rows (the dense models, 9-16 active terms)
-    const char* cv = getenv("INSITE_REFINE_COOP");
-    const bool coop = cv ? cv[0] == '1' : INSITE_REFINE_COOP != 0;
-    if (D != 1 || m <= 8 || m > 16 || !coop || T > kCoopStT || n_rows > INT32_MAX) return INSITE_E_UNSUPPORTED;
+  if (pm && n_arms > 2) {  // 3-4 arms: the cooperative kernel on the rows (the dense models, 9-16 active terms; the
+                           // sparse 5-8-term ones where the 8-coordinate cooperative kernel is selected, COOP8)
+    const char* cv = getenv(m <= 8 ? "INSITE_REFINE_COOP8" : "INSITE_REFINE_COOP");
+    const bool coop = cv ? cv[0] == '1' : (m <= 8 ? INSITE_REFINE_COOP8 : INSITE_REFINE_COOP) != 0;
+    if (D != 1 || m <= (INSITE_REFINE_M6 ? 6 : 4) || m > 16 || !coop || T > kCoopStT || n_rows > INT32_MAX)
+      return INSITE_E_UNSUPPORTED;
   }
   if (n_rows == 0) return INSITE_OK;
   if (!V || (bits && !arm_bits) || !seq_len || !preds || (n_statics > 0 && !u)) return INSITE_E_INVALID_ARG;

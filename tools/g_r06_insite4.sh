@@ -13,6 +13,7 @@ for rep in $(seq 1 ${REPS:-1}); do
   for o in ${ORDERS:-seq_len nfev}; do
     ENVP=""; oo=$o
     if [ "$o" = nfev_prep ]; then ENVP="INSITE_REFINE_ROWS=0"; oo=nfev; fi
+    if [ "$o" = nfev_coop8 ]; then ENVP="INSITE_LIB_OVERRIDE=$GRAFT_REPO_ROOT/ode-discovery-for-longitudinal-heterogeneous-treatment-effects-inference_amd/lib/ablate/libinsite_hip_coop8rows.so"; oo=nfev; fi
     env $ENVP timeout -k 10 600 python bench.py --config insite4 --no-cpu-baseline ${EXTRA:-} --insite-order $oo > $O/insite4_${o}_$rep.jsonl 2> $O/insite4_${o}_$rep.err || { echo "insite4 $o failed"; tail -5 $O/insite4_${o}_$rep.err; exit 1; }
     python3 -c "
 import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); m=d.get('models') or d.get('insite4') or {}
