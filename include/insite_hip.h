@@ -360,7 +360,9 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
 
 /* Lane order for insite_rollout_rk45_f64: rows sorted by n_obs, descending (counting sort on the
  * device; bins min(n_obs, 1023)).  No reference counterpart (scheduling only).  n_rows <= INT32_MAX.
- *   n_obs [n_rows] int32, order_out [n_rows] int32; workspace >= insite_rk45_order_workspace_bytes. */
+ *   n_obs [n_rows] int32, order_out [n_rows] int32; workspace >= insite_rk45_order_workspace_bytes (zeroed by the
+ *   call itself; a build with INSITE_RK45_ORDER_SELFRESET=1 instead needs it zero before its first use and leaves it
+ *   zero). */
 size_t insite_rk45_order_workspace_bytes(int32_t T_max);
 int32_t insite_rk45_order_i32(const int32_t* n_obs, int64_t n_rows, int32_t T_max, int32_t* order_out, void* workspace,
                               size_t workspace_bytes, void* stream);

@@ -3760,6 +3760,9 @@ rollout_rk45_flat_kernel(Rk45Args ra, LibDesc lib) {
 // (kernel), 8192 the same, 16384 slower (profiles/r05/c5_order/).  Measured and dropped (round 5): the histogram's
 // scan in the count pass's last block (a ticket after device-scope fences: the count pass 9 -> 21 us) and both
 // passes as one launch with a grid barrier on per-block epoch flags (63 us against ~26 for memset + two passes).
+#ifndef INSITE_RK45_ORDER_SELFRESET  // 1: a self-resetting workspace instead of the memset (measured slower, round 6:
+#define INSITE_RK45_ORDER_SELFRESET 0  // C5 0.672 vs 0.663 ms, INSITE 1.236 vs 1.225 -- the per-block fence + ticket)
+#endif
 constexpr int kRkBinMax = 1024;   // bins: key = min(n_obs, min(T_max, kRkBinMax - 1))
 #ifndef INSITE_RK45_BIN_CHUNK
 #define INSITE_RK45_BIN_CHUNK 4096  // rows per block of the two passes
@@ -3792,7 +3795,7 @@ __global__ void __launch_bounds__(kBlock) rk45_bin_count_kernel(const int32_t* _
 // every block scans the (small) global histogram itself: the bins' totals loaded by all threads at once, then one
 // wave's shuffle scan (lane l owns bins [l per, (l + 1) per)) -- round 4 had thread 0 walk it serially
 __global__ void __launch_bounds__(kBlock) rk45_bin_scatter_kernel(const int32_t* __restrict__ nobs, int64_t N, int nb,
-                                                                   const unsigned* __restrict__ hist,
+                                                                   unsigned* __restrict__ hist,
                                                                    unsigned* __restrict__ cursor,
                                                                    int32_t* __restrict__ order) {
   __shared__ unsigned base[kRkBinMax], cnt[kRkBinMax], tot[kRkBinMax];
@@ -3837,6 +3840,25 @@ __global__ void __launch_bounds__(kBlock) rk45_bin_scatter_kernel(const int32_t*
 #pragma unroll
   for (int q = 0; q < kPer; ++q)
     if (bin[q] >= 0) order[base[bin[q]] + rank[q]] = (int32_t)(lo + q * kBlock + threadIdx.x);
+#if INSITE_RK45_ORDER_SELFRESET
+  // (knob) the workspace resets itself instead of the memset before the count pass: every block has read the totals
+  // and taken its cursor slots before its ticket, and the last block to arrive zeroes the totals, the cursors and the
+  // ticket for the next call
+  __shared__ bool last;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(cursor + nb, 1u) == gridDim.x - 1u;
+  }
+  __syncthreads();
+  if (last) {
+    __threadfence();
+    for (int b = threadIdx.x; b < nb; b += kBlock) {
+      hist[b] = 0u;
+      cursor[b] = 0u;
+    }
+    if (threadIdx.x == 0) cursor[nb] = 0u;
+  }
+#endif
 }
 
 // =============================================================================================
@@ -5112,7 +5134,7 @@ int32_t insite_rollout_rk45_f64(const double* y0, const double* u, const uint32_
 
 size_t insite_rk45_order_workspace_bytes(int32_t T_max) {
   const int nb = (T_max < kRkBinMax - 1 ? (T_max < 1 ? 1 : T_max) : kRkBinMax - 1) + 1;
-  return (size_t)2 * nb * sizeof(unsigned);
+  return (size_t)(2 * nb + 1) * sizeof(unsigned);  // totals, cursors, the self-reset ticket
 }
 
 int32_t insite_rk45_order_i32(const int32_t* n_obs, int64_t n_rows, int32_t T_max, int32_t* order_out, void* workspace,
@@ -5124,7 +5146,8 @@ int32_t insite_rk45_order_i32(const int32_t* n_obs, int64_t n_rows, int32_t T_ma
   const int nb = (T_max < kRkBinMax - 1 ? T_max : kRkBinMax - 1) + 1;
   unsigned* hist = static_cast<unsigned*>(workspace);
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(hist, 0, (size_t)2 * nb * sizeof(unsigned), hs) != hipSuccess) return INSITE_E_HIP;
+  if (!INSITE_RK45_ORDER_SELFRESET && hipMemsetAsync(hist, 0, (size_t)2 * nb * sizeof(unsigned), hs) != hipSuccess)
+    return INSITE_E_HIP;
   const dim3 grid((unsigned)((n_rows + kRkBinChunk - 1) / kRkBinChunk));
   rk45_bin_count_kernel<<<grid, kBlock, 0, hs>>>(n_obs, n_rows, nb, hist);
   rk45_bin_scatter_kernel<<<grid, kBlock, 0, hs>>>(n_obs, n_rows, nb, hist, hist + nb, order_out);

@@ -876,7 +876,9 @@ def rk45_order(n_obs: torch.Tensor, T_max: int, out: torch.Tensor | None = None)
     if out is None:
         out = torch.empty((N,), dtype=torch.int32, device=n_obs.device)
     nb = _lib.load().insite_rk45_order_workspace_bytes(int(T_max))
-    ws = _default_ws(n_obs.device).get(nb, n_obs.device)
+    # a workspace of its own: the counting sort's totals / cursors reset themselves at the end of every call, so the
+    # buffer must be zero at its first use and hold nothing else (insite_hip.h)
+    ws = _default_ws(n_obs.device, "order").get(nb, n_obs.device)
     args = (_p(n_obs), N, int(T_max), _p(out), _p(ws), ws.numel())
     return _run(("insite_rk45_order_i32", args, n_obs.device, out))
 
