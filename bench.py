@@ -1226,9 +1226,9 @@ def insite_main(args):
         "insite": {"refined_rows": int((st >= 0).sum()), "converged": int((st == 0).sum()),
                    "zoom_failed_fallback": int((st == 3).sum()), "mean_bfgs_iterations": float(it[st >= 0].mean()),
                    "lane_order": ("rows binned by seq_len (device counting sort)" if args.insite_order == "seq_len"
-                                  else "rows binned by seq_len (64 levels) and then by the evaluation counts the "
-                                       "previous step left (16 levels; one device counting sort over the combined "
-                                       "key)") +
+                                  else "rows binned by seq_len (32 levels) and then by the evaluation counts the "
+                                       "previous step left (min(nfev, 31); one device counting sort over the "
+                                       "combined key)") +
                                  "; the kernel gathers its lanes' patient-major rows through its LDS ring and stores "
                                  "the predictions as row segments (insite_refine_rows_f64; ops.plan_insite_refine, "
                                  "no host sync)",

@@ -1199,8 +1199,8 @@ class InsiteRefinePlan:
         key_call = None
         self.nfev = None   # (order="nfev": the evaluation counts the binning key reads, rewritten by every call)
         if order == "nfev":
-            # lanes binned by the window (seq_len, 64 levels) and then by the evaluation counts the previous call left
-            # in ``nfev`` (16 levels): a wave runs until its longest row's last objective scan, so rows of equal window
+            # lanes binned by the window (seq_len, 32 levels) and then by the evaluation counts the previous call left
+            # in ``nfev`` (32 levels): a wave runs until its longest row's last objective scan, so rows of equal window
             # AND equal evaluation count belong together (the C5 line's attempt binning; a refined set that is refined
             # again -- the bench step, a serving loop -- takes the same counts).  Outputs do not depend on the lane
             # order (tested); the first call bins on zero counts, i.e. by seq_len alone.
@@ -1211,10 +1211,16 @@ class InsiteRefinePlan:
             kws = Workspace("scratch").get(L.insite_rk45_order_workspace_bytes(RK45_ATTEMPT_BINS - 1), dev)
             self._kws = kws
 
-            def key_fn(s):   # key = window level * 16 + min(nfev / 2, 15) in [0, 1024), on the plan's stream s
+            # key resolution: window levels x evaluation-count levels = 1,024 bins (INSITE_NFEV_KEY "32x32", the
+            # default: the window in 32 levels, min(nfev, 31) -- wave divergence 1.025 at the INSITE line's shape;
+            # "64x16": the window in 64 levels, min(nfev / 2, 15) -- 1.056, 1.5-2.7 % slower, profiles/r06/nfkey/)
+            wl, nl = (64, 16) if os.environ.get("INSITE_NFEV_KEY", "32x32") == "64x16" else (32, 32)
+            nsh = 0 if nl == 32 else 1
+
+            def key_fn(s):   # key = window level * nl + min(nfev >> nsh, nl - 1) in [0, 1024), on the plan's stream s
                 with torch.cuda.stream(s):
-                    q = torch.clamp(sl_, 0, Tq).mul_(63).floor_divide_(Tq).mul_(16)
-                    torch.add(q, torch.clamp(nf_ >> 1, 0, 15), out=key)
+                    q = torch.clamp(sl_, 0, Tq).mul_(wl - 1).floor_divide_(Tq).mul_(nl)
+                    torch.add(q, torch.clamp(nf_ >> nsh, 0, nl - 1), out=key)
             key_call = (key_fn, None)
             self.nfev = nfev
             order_call = (L.insite_rk45_order_i32, (_p(key), N, RK45_ATTEMPT_BINS - 1, _p(self.order), _p(kws),
